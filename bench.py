@@ -1,0 +1,131 @@
+#!/usr/bin/env python3
+"""Headline benchmark (BASELINE.json metric): DICOM slices/sec through the full pipeline on the
+T1+C cohort, one MI355X per rank.
+
+One step = the whole synthetic T1+C cohort (20 patients × 21–25 slices of 256² u16)
+per rank, end to end: read every DICOM file from disk, parse, upload, median 7×7 → 9×9 unsharp →
+SRG band → seeded region growing → dilation 3 → render 512² (original + segmentation) → JPEG q75 on
+the GPU → write both JPEG files per slice. Nothing is cached between steps.
+
+Weak scaling by default: with N ranks the global work list is N cohort replicas (distinct output
+trees) sharded contiguously, so every rank processes one full cohort per step; `--scaling strong`
+shards a single cohort instead.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+"""
+import argparse
+import json
+import os
+import shutil
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402  (must precede the native extension: shared HIP runtime)
+
+import nm03_capstone_project_amd as nm  # noqa: E402
+from nm03_capstone_project_amd.parallel import (allreduce_max, allreduce_sum, barrier,  # noqa: E402
+                                                broadcast_bytes, init_from_env, plan_cohort)
+from nm03_capstone_project_amd.parallel.cohort_runner import CohortPlan  # noqa: E402
+from nm03_capstone_project_amd.parallel.dist import shard_bounds  # noqa: E402
+
+METRIC = "DICOM slices/sec through full pipeline (T1+C cohort) at 1/2/4/8 MI355X"
+BASELINE_SLICES_PER_S = None  # the reference publishes no number
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--scaling", choices=("weak", "strong"), default="weak")
+    ap.add_argument("--batch-size", type=int, default=64)
+    ap.add_argument("--streams", type=int, default=3)
+    ap.add_argument("--threads", type=int, default=16)
+    ap.add_argument("--data-root", default=os.environ.get("NM03_BENCH_DATA", "/tmp/nm03_bench_data"))
+    ap.add_argument("--out-root", default=os.environ.get("NM03_BENCH_OUT", "/tmp/nm03_bench_out"))
+    ap.add_argument("--keep-output", action="store_true")
+    args = ap.parse_args()
+
+    ctx = init_from_env()
+    n = nm.native()
+    marker = os.path.join(args.data_root, ".complete")
+    if ctx.local_rank == 0 and not os.path.exists(marker):
+        n.synth_cohort(args.data_root, threads=16)
+        open(marker, "w").close()
+    barrier(ctx)
+    while not os.path.exists(marker):  # other nodes' local rank 0 (single node: already there)
+        time.sleep(0.1)
+
+    replicas = ctx.world if args.scaling == "weak" else 1
+    plan_bytes = b""
+    if ctx.is_root:
+        plan_bytes = plan_cohort(args.data_root, args.out_root, wipe=True, replicas=replicas).to_bytes()
+    plan = CohortPlan.from_bytes(broadcast_bytes(plan_bytes, ctx))
+    items = plan.items
+    lo, hi = shard_bounds(len(items), ctx.rank, ctx.world)
+    mine = items[lo:hi]
+
+    cfg = nm.PipelineConfig(batch_size=args.batch_size, streams=args.streams, threads=args.threads,
+                            device=ctx.local_rank)
+    engine = n.Engine(cfg.engine_config())
+    for _ in range(args.warmup):
+        st, _ = engine.run(mine)
+    bad = sum(1 for s in st if s[0] != 0) if args.warmup else 0
+    if bad:
+        raise SystemExit(f"rank {ctx.rank}: {bad} slices failed in warmup: {st[:3]}")
+
+    barrier(ctx)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ok = 0
+    stage = {"load_s": 0.0, "h2d_s": 0.0, "kernels_s": 0.0, "write_s": 0.0}
+    for _ in range(args.steps):
+        st, times = engine.run(mine)
+        ok += sum(1 for s in st if s[0] == 0)
+        for k in stage:
+            stage[k] += times[k]
+    torch.cuda.synchronize()
+    barrier(ctx)
+    dt = time.perf_counter() - t0
+    dt = allreduce_max(dt, ctx)
+    total_ok = int(allreduce_sum(ok, ctx))
+    value = total_ok / dt
+    if ctx.is_root:
+        rec = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "slices/s",
+            "n_gpus": ctx.world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(dt * 1e3 / args.steps, 3),
+            "higher_is_better": True,
+            "scaling": args.scaling,
+            "vs_baseline": (round(value / BASELINE_SLICES_PER_S, 3) if BASELINE_SLICES_PER_S else None),
+            "dtype": "fp32",
+            "data": "synthetic (20-patient T1+C-shaped DICOM cohort, 256x256 u16, generated on the box)",
+            "config": {
+                "model": "NM03 T1+C pipeline: norm/clip -> VMF 7x7 -> sharpen 9x9 -> SRG[0.74,0.91] -> "
+                         "dilate 3 -> render 512^2 x2 -> JPEG q75",
+                "global_batch": len(items),
+                "seq_len": 256,
+                "parallelism": f"dp{ctx.world}",
+                "batch_size": args.batch_size,
+                "streams": args.streams,
+                "threads": args.threads,
+                "rank0_stage_s": {k: round(v, 4) for k, v in stage.items()},
+            },
+        }
+        print(json.dumps(rec), flush=True)
+    if not args.keep_output and ctx.is_root:
+        shutil.rmtree(args.out_root, ignore_errors=True)
+    if ctx.world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,42 @@
+// nm03/app.h — cohort orchestration shared by the three reference CLIs.
+//   img_processing_sequential  ≙ SequentialImageProcessor  (main_sequential.cpp:9-363)
+//   img_processing_parallel    ≙ OptimizedParallelProcessor (main_parallel.cpp:19-411), now
+//                                 data-parallel over N MI355X ranks
+//   test_pipeline              ≙ test_pipeline.cpp:29-182 (headless)
+// All three keep the reference's stdout/stderr message catalogue, output layout
+// out-*/PGBM-XXXX/<stem>_{original,processed}.jpg and no-argument defaults.
+#pragma once
+
+#include <string>
+#include <vector>
+
+#include "nm03/engine.h"
+
+namespace nm03::app {
+
+struct AppConfig {
+  std::string data_root;  // default: cohort::default_data_root()
+  std::string out_dir;    // default per CLI: ../out-sequential, ../out-parallel, ../out-test
+  EngineConfig engine;
+  int gpus = 1;            // ranks (one process per GPU)
+  bool quiet = false;
+  bool cpu = false;        // test_pipeline: golden CPU path (BASELINE config 1)
+  bool montage = true;     // test_pipeline: 5-view montage JPEG (headless MultiViewWindow)
+  std::string json;        // metrics file
+  std::string mode = "2d"; // 2d | 3d
+  std::string input;       // test_pipeline: explicit slice path
+  int repeat = 1;
+};
+
+// Parse the shared flag set; `which` selects CLI-specific defaults. Exits on --help.
+AppConfig parse_args(int argc, char** argv, const std::string& which);
+
+int run_sequential(const AppConfig& cfg);
+int run_parallel(const AppConfig& cfg);
+int run_test_pipeline(const AppConfig& cfg);
+
+// Number of GPUs visible to this process, counted WITHOUT initialising HIP (KFD topology +
+// HIP/ROCR_VISIBLE_DEVICES), so the launcher can still fork safely afterwards.
+int visible_gpu_count();
+
+}  // namespace nm03::app

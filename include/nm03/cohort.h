@@ -1,0 +1,45 @@
+// nm03/cohort.h — dataset discovery, slice ordering and output-directory management.
+// Reference: SequentialImageProcessor / OptimizedParallelProcessor helpers
+//   extractFileNumber        main_sequential.cpp:18-30   (main_parallel.cpp:35-47)
+//   setupOutputDirectory     main_sequential.cpp:32-47   (main_parallel.cpp:49-64)
+//   findAllPatientDirectories main_sequential.cpp:93-119 (main_parallel.cpp:233-259)
+//   loadDICOMFilesForPatient main_sequential.cpp:121-168 (main_parallel.cpp:261-308)
+#pragma once
+
+#include <string>
+#include <vector>
+
+namespace nm03::cohort {
+
+// Integer between the last '-' and ".dcm" ("1-14.dcm" → 14); 1000 when absent or unparsable.
+int extract_file_number(const std::string& filename);
+
+// Data root: $NM03_DATA_ROOT, else "../data/" (the reference runs from build/).
+std::string default_data_root();
+std::string with_slash(const std::string& p);
+// <root>/Brain-Tumor-Progression/T1-Post-Combined-P001-P020/  (main_sequential.cpp:83-84)
+std::string cohort_dir(const std::string& data_root);
+// <root>/Brain-Tumor-Progression/PGBM-017/.../1-14.dcm          (test_pipeline.cpp:33-36)
+std::string test_slice_path(const std::string& data_root);
+
+// Directories under `cohort_root` whose name starts with "PGBM-", sorted lexicographically.
+std::vector<std::string> find_patient_dirs(const std::string& cohort_root);
+
+struct Series {
+  std::string series_dir;          // printed as "Using series directory: <dir>/"
+  std::vector<std::string> files;  // *.dcm, ordered by extract_file_number then name
+};
+// Series = lexicographically first sub-directory (the reference takes the first one iterated,
+// which is unspecified). Throws std::runtime_error when none exists.
+Series list_patient_series(const std::string& cohort_root, const std::string& patient_id);
+
+// mkdir -p <dir> and remove everything inside it (the reference's "mkdir -p && cd && rm -rf *"
+// via system(), done with std::filesystem — no shell).
+void setup_output_dir(const std::string& dir);
+void make_dirs(const std::string& dir);
+
+// File stem ("…/1-14.dcm" → "1-14") and file name.
+std::string stem(const std::string& path);
+std::string filename(const std::string& path);
+
+}  // namespace nm03::cohort

@@ -1,0 +1,71 @@
+// nm03/dicom.h — self-contained DICOM Part-10 reader/writer (replaces FAST's DCMTK-based
+// DICOMFileImporter with setLoadSeries(false): test_pipeline.cpp:33-42, main_sequential.cpp:175-177).
+//
+// Supported: Part-10 files (preamble + "DICM") and bare datasets; Implicit VR LE, Explicit VR LE,
+// Explicit VR BE; 8/16-bit monochrome, signed/unsigned, BitsStored masking, modality rescale,
+// PixelSpacing, undefined-length sequences. Compressed/encapsulated pixel data and deflate are
+// rejected with a SliceError (the slice is skipped like a fast::Exception in the reference).
+#pragma once
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "nm03/common.h"
+
+namespace nm03::dicom {
+
+enum class Syntax : uint8_t { kImplicitLE, kExplicitLE, kExplicitBE };
+
+struct Header {
+  int rows = 0, cols = 0, frames = 1;
+  int bits_allocated = 0, bits_stored = 0, high_bit = 0, pixel_rep = 0, samples = 1;
+  PixelType type = kU16;
+  bool has_rescale = false;
+  float slope = 1.f, intercept = 0.f;
+  float spacing_x = 1.f, spacing_y = 1.f;  // column spacing, row spacing (mm)
+  int instance_number = 0;
+  bool has_position = false;
+  double position[3] = {0, 0, 0};
+  double slice_location = 0;
+  std::string photometric, transfer_syntax, sop_instance_uid, series_uid, patient_id, modality;
+  Syntax syntax = Syntax::kExplicitLE;
+  size_t pixel_offset = 0;  // byte offset of (7FE0,0010) value in the buffer
+  size_t pixel_length = 0;  // byte length of the value field
+};
+
+// Parse a whole file image held in memory. Throws SliceError on malformed/unsupported input.
+Header parse(const uint8_t* data, size_t size);
+
+// Copy the first frame's pixels to `dst` as 16-bit words (8-bit data is widened, big-endian data
+// is byte-swapped). dst must hold rows*cols uint16.
+void copy_pixels16(const Header& h, const uint8_t* data, size_t size, uint16_t* dst);
+
+// Read a file completely (throws SliceError if it cannot be read).
+std::vector<uint8_t> read_file(const std::string& path);
+// Read into a caller-provided growable buffer (avoids reallocations in loader threads).
+size_t read_file_into(const std::string& path, std::vector<uint8_t>& buf);
+
+struct WriteSpec {
+  int rows = 256, cols = 256;
+  PixelType type = kU16;
+  int bits_stored = 16;
+  const uint16_t* pixels = nullptr;  // rows*cols 16-bit samples (8-bit type: low bytes used)
+  bool write_rescale = false;
+  float slope = 1.f, intercept = 0.f;
+  float spacing_x = 1.f, spacing_y = 1.f;
+  double slice_thickness = 1.0;
+  int instance_number = 1;
+  double position[3] = {0, 0, 0};
+  std::string patient_id = "PGBM-000";
+  std::string study_uid = "1.2.826.0.1.3680043.10.1", series_uid = "1.2.826.0.1.3680043.10.2",
+              sop_uid = "1.2.826.0.1.3680043.10.3";
+  std::string modality = "MR";
+  Syntax syntax = Syntax::kExplicitLE;
+  bool preamble = true;  // write 128-byte preamble + "DICM" + file meta group
+};
+
+std::vector<uint8_t> write(const WriteSpec& spec);
+void write_file(const std::string& path, const WriteSpec& spec);
+
+}  // namespace nm03::dicom

@@ -1,0 +1,103 @@
+// nm03/engine.h — the per-GPU batch engine (SURVEY §1.2 L3 stream scheduler).
+//
+// A run is a list of WorkItems (DICOM file → output directory). Items are cut into batches of
+// `batch_size` (DEFAULT_BATCH_SIZE = 25 in main_parallel.cpp:33) and pushed through a ring of
+// `streams` independent slots, each with its own HIP stream, pinned upload blob, device buffers
+// and host-mapped JPEG output. While slot k's kernels run, other slots' loader tasks read/parse
+// DICOMs and writer tasks write JPEGs, so disk I/O, PCIe and compute overlap (the reference runs
+// load → compute → export strictly in sequence per batch, main_parallel.cpp:330-347).
+//
+// Per batch on the GPU:  one H2D of the blob → K1a median → K1b sharpen/band → K2 SRG+morph →
+// K3 render → K4 JPEG (entropy-coded bytes land directly in host memory).
+#pragma once
+
+#include <cstdint>
+#include <functional>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "nm03/golden.h"
+#include "nm03/params.h"
+
+namespace nm03 {
+
+struct WorkItem {
+  std::string path;     // DICOM file
+  std::string out_dir;  // directory receiving <stem>_original.jpg / <stem>_processed.jpg
+};
+
+enum SliceCode : int32_t {
+  kSliceOk = 0,
+  kSliceLoadError = 1,   // unreadable / unsupported DICOM
+  kSliceTooSmall = 2,    // width<100 || height<100 (main_sequential.cpp:189-192)
+  kSliceDeviceError = 3, // HIP failure in the slice's batch
+  kSliceExportError = 4, // JPEG write failed
+  kSliceNotRun = 5,
+};
+
+struct SliceStatus {
+  int32_t code = kSliceNotRun;
+  std::string message;
+};
+
+struct StageTimes {
+  double load_s = 0;     // summed over loader tasks (CPU seconds)
+  double h2d_s = 0;      // device time of uploads
+  double kernels_s = 0;  // device time K1..K4
+  double write_s = 0;    // summed over writer tasks (CPU seconds)
+  double wall_s = 0;     // run() wall time
+  int64_t batches = 0, slices_ok = 0, slices_failed = 0;
+  int64_t bytes_in = 0, bytes_out = 0;
+  int64_t jpeg_fallbacks = 0;  // images re-encoded on the CPU after a GPU capacity overflow
+};
+
+struct EngineConfig {
+  int device = 0;
+  int batch_size = 25;  // main_parallel.cpp:33
+  int streams = 3;      // batches in flight
+  int threads = 16;     // host pool (omp_set_num_threads(16), main_parallel.cpp:401)
+  int max_dim = 512;    // buffers sized for slices up to max_dim × max_dim
+  PipelineParams pipe;
+  RenderParams render;
+  bool export_jpeg = true;
+};
+
+// Everything test_pipeline exports / tests inspect for one slice (host copies).
+struct SingleResult {
+  int w = 0, h = 0;
+  std::vector<uint16_t> median_keys;
+  std::vector<float> sharpened;
+  std::vector<uint8_t> band, region, eroded, dilated;               // 0/1 per pixel
+  std::vector<uint8_t> border_region, border_eroded, border_dilated;
+  int srg_iterations = 0;
+  // canvases and JPEG files: original, preprocessed, segmentation, erosion, dilation
+  std::vector<std::vector<uint8_t>> canvases, jpegs;
+};
+
+class Engine {
+ public:
+  explicit Engine(const EngineConfig& cfg);
+  ~Engine();
+  Engine(const Engine&) = delete;
+  Engine& operator=(const Engine&) = delete;
+
+  // Process all items (blocking). on_start(i) is called when item i starts loading (used by the
+  // sequential CLI to print "Processing: ..." at the right moment).
+  std::vector<SliceStatus> run(const std::vector<WorkItem>& items, StageTimes* times = nullptr,
+                               const std::function<void(size_t)>& on_start = {});
+
+  // One slice through every stage with all intermediate outputs copied back (test_pipeline).
+  SingleResult run_single(const golden::SliceInput& s);
+
+  const EngineConfig& config() const;
+
+ private:
+  struct Impl;
+  std::unique_ptr<Impl> impl_;
+};
+
+// Device count without initialising anything else (hipGetDeviceCount).
+int device_count();
+
+}  // namespace nm03

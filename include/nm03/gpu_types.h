@@ -1,0 +1,100 @@
+// nm03/gpu_types.h — plain-old-data descriptors shared by the host runtime and the gfx950
+// kernels. A batch is uploaded as ONE pinned blob (descriptors, tile lists, seeds, raw pixels)
+// with a single hipMemcpyAsync; every kernel then walks descriptor tables, so slices of different
+// sizes/pixel types can share one launch (SURVEY §7.1 "batched launches").
+#pragma once
+
+#include <cstdint>
+
+namespace nm03::gpu {
+
+// Median kernel output tile (64 columns × 64 rows) and sharpen/band tile (64 × 16: one mask word
+// per row, produced by a wave ballot).
+inline constexpr int kMedTileW = 64, kMedTileH = 64;
+inline constexpr int kShpTileW = 64, kShpTileH = 16;
+// Largest slice the LDS-resident region-growing kernel handles (bit-planes in LDS).
+inline constexpr int kSrgMaxDim = 512;
+
+struct SliceDesc {
+  uint32_t raw_off;    // u16 element offset of the slice in the raw/median buffers
+  uint32_t mask_off;   // u64 word offset of the slice in every bitmap buffer (h * wpr words)
+  uint16_t w, h;
+  uint16_t wpr;        // mask words per row = ceil(w/64)
+  uint8_t type;        // PixelType
+  uint8_t stored_bits;
+  float slope, intercept;
+  uint32_t seed_off;   // index into the seed table (int16 x,y pairs)
+  uint16_t seed_count;
+  uint16_t flags;
+  uint32_t f32_off;    // f32 element offset for optional sharpened output
+  uint32_t pad;
+};
+static_assert(sizeof(SliceDesc) == 40, "SliceDesc layout");
+
+struct TileDesc {
+  uint32_t slice;
+  uint16_t tx, ty;  // tile column / row
+};
+
+struct SeedXY {
+  int16_t x, y;
+};
+
+// Per-slice statistics produced on device (ordered-u32 encodings so atomicMin/Max work).
+struct SliceStats {
+  uint32_t key_min, key_max;  // raw keys (render window of the original image)
+  uint32_t s_min, s_max;      // sharpened f32 as ordered u32 (preprocessed_image window)
+};
+
+struct PipeConsts {
+  // normalise + clip (slope/intercept are per slice)
+  float nmin, nmax, nlow, nhigh, cmin, cmax;
+  float gain;
+  float band_lo, band_hi;
+  float taps[16];
+  int mask_radius;  // sharpen radius R (taps 2R+1)
+  int median_k;
+  int connectivity;  // 4 | 8
+  int dilation_size, erosion_size, border_radius;
+  uint32_t outputs;  // bit set of kOut* below
+};
+
+enum : uint32_t {
+  kOutRegion = 1u << 0,        // SRG result bitmap
+  kOutDilated = 1u << 1,       // dilation(region)
+  kOutEroded = 1u << 2,        // erosion(region) (test_pipeline only)
+  kOutBorderRegion = 1u << 3,  // renderer border of region / eroded / dilated
+  kOutBorderEroded = 1u << 4,
+  kOutBorderDilated = 1u << 5,
+  kOutSharpened = 1u << 6,     // f32 sharpened image (test_pipeline preprocessed_image)
+};
+
+// Render job: one canvas.
+enum RenderKind : uint8_t { kRenderRawGray = 0, kRenderF32Gray = 1, kRenderLabels = 2 };
+
+struct RenderDesc {
+  uint8_t kind;
+  uint8_t type, stored_bits;
+  uint8_t fill, border_value;
+  uint8_t pad0[3];
+  uint32_t slice;       // stats index
+  uint32_t src_off;     // u16 elements (raw) / f32 elements / u64 words (labels)
+  uint32_t border_off;  // u64 words (labels)
+  uint16_t src_w, src_h, wpr, pad1;
+  float ox, oy, invx, invy;
+  float slope, intercept;
+  uint32_t canvas_off;  // byte offset into the canvas buffer
+};
+
+// JPEG job: one canvas (out_w×out_h, both multiples of 16) → one entropy-coded segment.
+struct JpegDesc {
+  uint32_t canvas_off;  // bytes
+  uint32_t coef_off;    // block index of the image's first block (MCU order, 4 luma blocks/MCU)
+  uint32_t stage_off;   // u32 word offset of the bit staging area
+  uint32_t stage_words;
+  uint64_t out_off;     // byte offset in the output buffer (host-mapped)
+  uint32_t out_cap;     // capacity in bytes
+  uint32_t pad;
+};
+
+}  // namespace nm03::gpu

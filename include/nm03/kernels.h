@@ -1,0 +1,74 @@
+// nm03/kernels.h — host-callable launchers of the gfx950 kernels (src/kernels/*.hip).
+// All launchers are asynchronous on `stream` and allocation-free (graph-capturable).
+#pragma once
+
+#include <hip/hip_runtime_api.h>
+
+#include <string>
+
+#include "nm03/common.h"
+#include "nm03/gpu_types.h"
+
+namespace nm03::gpu {
+
+void check_hip(hipError_t e, const char* what);
+void check_launch(const char* what);
+
+// K1a: k×k median of raw keys → `med` (u16 keys, same layout as raw). k ∈ {3,5,7,9}.
+void launch_median(const uint16_t* raw, uint16_t* med, const SliceDesc* descs, const TileDesc* tiles, int ntiles,
+                   int k, SliceStats* stats, hipStream_t stream);
+
+// K1b: normalise+clip of the median keys, separable Gaussian unsharp mask, SRG band test →
+// `band` bitmaps (u64 words, LSB = left-most pixel). Optionally the f32 sharpened image.
+void launch_sharpen_band(const uint16_t* med, uint64_t* band, float* sharpened, const SliceDesc* descs,
+                         const TileDesc* tiles, int ntiles, const PipeConsts& pc, SliceStats* stats,
+                         hipStream_t stream);
+
+// Bitmap planes produced by K2 (each null when not requested).
+struct SrgOutputs {
+  uint64_t* region = nullptr;
+  uint64_t* dilated = nullptr;
+  uint64_t* eroded = nullptr;
+  uint64_t* border_region = nullptr;
+  uint64_t* border_eroded = nullptr;
+  uint64_t* border_dilated = nullptr;
+  int32_t* iterations = nullptr;  // per-slice fixpoint iteration count (diagnostics)
+};
+
+// K2: LDS-resident seeded region growing (bit-parallel run fills on rows and on the transposed
+// bitmap until fixpoint) + dilation/erosion + renderer borders. One workgroup per slice;
+// slices must be ≤ kSrgMaxDim in both dimensions (larger ones go through launch_srg_global).
+void launch_srg_morph(const uint64_t* band, const SliceDesc* descs, int nslices, const SeedXY* seeds,
+                      const PipeConsts& pc, const SrgOutputs& out, int max_w, int max_h, hipStream_t stream);
+
+// 3D region growing on a w×h×d bit volume (planes of h rows × ceil(w/64) words, plane ≤ 512²)
+// by LDS plane sweeps relaunched until a device flag reports no change (k5_volume.hip).
+// seeds_xyz: device int32 triples. d_flag: device word; h_flag: pinned host word. Returns sweeps.
+int srg_volume(const uint64_t* band, uint64_t* region, int w, int h, int d, const int32_t* seeds_xyz, int nseeds,
+               int connectivity, uint32_t* d_flag, uint32_t* h_flag, hipStream_t stream);
+// Cube dilation of a bit volume (size odd), separable; `tmp` same size as the volume.
+void dilate_volume(const uint64_t* src, uint64_t* dst, uint64_t* tmp, int w, int h, int d, int size,
+                   hipStream_t stream);
+
+// K3: render canvases (out_w×out_h u8 each).
+void launch_render(const uint16_t* raw, const float* f32, const uint64_t* bits, const SliceStats* stats,
+                   const RenderDesc* rd, int ncanvas, int out_w, int out_h, uint8_t* canvas, hipStream_t stream);
+
+// K4: JPEG. DCT + quantisation per 8×8 block (MCU order), then one 1024-thread workgroup per
+// image for Huffman sizing, block scan, bit emission, 0xFF stuffing and the copy to `out`
+// (host-mapped pinned memory). out_sizes[i] = bytes, or -1 when out_cap/stage was exceeded.
+struct JpegWork {
+  int16_t* coef = nullptr;     // ncanvas × blocks × 64
+  uint64_t* nzmask = nullptr;  // ncanvas × blocks
+  uint32_t* acbits = nullptr;  // ncanvas × blocks
+  int16_t* dc = nullptr;       // ncanvas × blocks
+  uint32_t* stage = nullptr;   // bit staging words
+  uint8_t* tmp = nullptr;      // stuffed bytes before the host copy
+};
+void launch_jpeg(const uint8_t* canvas, const JpegDesc* jd, int ncanvas, int out_w, int out_h, const int32_t* div_luma,
+                 const JpegWork& w, uint8_t* out, int32_t* out_sizes, hipStream_t stream);
+
+// Upload the 64 islow divisors (8·Q, natural order) for `quality` into a device buffer.
+void jpeg_divisors(int quality, int32_t* host_out64);
+
+}  // namespace nm03::gpu

@@ -1,0 +1,49 @@
+// nm03/volume.h — 3D mode (BASELINE config 5): a patient series loaded as one volume
+// (the reference forces 2D with setLoadSeries(false), test_pipeline.cpp:38-41; FAST itself
+// supports 3D SeededRegionGrowing/Dilation, which this mode provides on the GPU).
+#pragma once
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "nm03/app.h"
+#include "nm03/engine.h"
+
+namespace nm03 {
+
+struct VolumeInput {
+  int w = 0, h = 0, d = 0;
+  PixelType type = kU16;
+  int stored_bits = 16;
+  float slope = 1.f, intercept = 0.f, spacing_x = 1.f, spacing_y = 1.f;
+  std::vector<uint16_t> raw;  // d planes of h×w
+};
+
+// Load a series directory's slices (ordered like the 2D path) as a volume; all slices must share
+// dimensions and pixel format.
+VolumeInput load_volume(const std::vector<std::string>& files);
+
+struct VolumeResult {
+  int w = 0, h = 0, d = 0;
+  int sweeps = 0;
+  std::vector<uint8_t> band, region, dilated;  // 0/1 per voxel (when requested)
+  double kernels_s = 0;
+};
+
+struct VolumeParams {
+  PipelineParams pipe;        // median/sharpen/band per slice, then 3D SRG
+  int connectivity = 6;       // 6 | 26
+  int dilation_size = 7;      // cube edge (7×7×7 in config 5)
+  bool preprocess = true;     // median + sharpen per slice before the band test
+  std::vector<Seed> seeds;    // empty → reference seed pattern on the middle slice
+};
+
+// Runs the 3D pipeline on `device`; copies masks back when `want_masks`.
+VolumeResult run_volume(const VolumeInput& v, const VolumeParams& p, int device, bool want_masks);
+
+namespace app {
+int run_volume_cohort(const AppConfig& cfg);
+}
+
+}  // namespace nm03

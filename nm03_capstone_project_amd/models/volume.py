@@ -1,0 +1,28 @@
+"""3D mode (BASELINE config 5): a series as one volume, per-slice median/sharpen/band, 6- or
+26-connected seeded region growing by LDS plane sweeps, and separable cube dilation."""
+import numpy as np
+
+from .._native import native
+from .pipeline import PipelineConfig
+
+
+class VolumePipeline:
+    def __init__(self, config: PipelineConfig = None, connectivity: int = 6, dilation: int = 7):
+        self.config = config or PipelineConfig()
+        self.connectivity = connectivity
+        self.dilation = dilation
+
+    def default_seeds(self, volume):
+        d, h, w = volume.shape
+        return [(x, y, d // 2) for (x, y) in native().reference_seeds(w, h)]
+
+    def run(self, volume, seeds=None, device=None):
+        vol = np.ascontiguousarray(volume, dtype=np.uint16)
+        s = list(seeds) if seeds is not None else self.default_seeds(vol)
+        return native().run_volume(vol, self.config.pipeline_params(), self.connectivity, self.dilation, s,
+                                   self.config.device if device is None else device)
+
+    def golden(self, band, seeds):
+        n = native()
+        region = n.golden_region_grow3d(band, list(seeds), self.connectivity)
+        return region, n.golden_dilate3d(region, self.dilation)

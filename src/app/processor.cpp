@@ -1,0 +1,525 @@
+// Cohort processors behind the three CLIs. Message texts are the reference's;
+// file:line citations point at the reference statement each message reproduces.
+#include <dirent.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <iomanip>
+#include <iostream>
+#include <sstream>
+
+#include "nm03/app.h"
+#include "nm03/cohort.h"
+#include "nm03/comm.h"
+#include "nm03/dicom.h"
+#include "nm03/golden.h"
+#include "nm03/jpeg.h"
+#include "nm03/volume.h"
+
+namespace nm03::app {
+
+namespace {
+
+double now_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+void usage(const std::string& which) {
+  std::cout << "usage: " << which << " [options]\n"
+            << "  --data-root DIR        dataset root (default $NM03_DATA_ROOT or ../data/)\n"
+            << "  --out DIR              output root (default ../out-" << (which == "test_pipeline" ? "test" : which == "img_processing_sequential" ? "sequential" : "parallel") << ")\n"
+            << "  --gpus N|all           data-parallel ranks, one process per MI355X (parallel CLI)\n"
+            << "  --device N             GPU for a single-rank run\n"
+            << "  --batch-size N         slices per GPU batch (default 25)\n"
+            << "  --streams N            batches in flight per GPU (default 3)\n"
+            << "  --threads N            host I/O threads per rank (default 16)\n"
+            << "  --median-window K      3|5|7|9 (default 7)\n"
+            << "  --srg-connectivity C   4|8 (2D) / 6|26 (3D)\n"
+            << "  --dilation-size S      (default 3)    --erosion-size S (default 3)\n"
+            << "  --quality Q            JPEG quality (default 75)\n"
+            << "  --mode 2d|3d           3d: whole series as a volume (SRG 6-conn + cube dilation)\n"
+            << "  --input FILE           test_pipeline: slice to process\n"
+            << "  --cpu                  test_pipeline: golden CPU model instead of the GPU\n"
+            << "  --no-montage           test_pipeline: skip the 5-view montage JPEG\n"
+            << "  --repeat N             process the cohort N times (benchmarking)\n"
+            << "  --json FILE            write run metrics as JSON\n"
+            << "  --quiet                suppress per-slice progress lines\n";
+}
+
+void write_json(const std::string& path, const std::string& body) {
+  if (path.empty()) return;
+  std::ofstream f(path, std::ios::trunc);
+  f << body << "\n";
+}
+
+std::string fmt(double v, int p = 6) {
+  std::ostringstream o;
+  o << std::setprecision(p) << v;
+  return o.str();
+}
+
+}  // namespace
+
+int visible_gpu_count() {
+  int n = 0;
+  DIR* d = opendir("/sys/class/kfd/kfd/topology/nodes");
+  if (d) {
+    while (dirent* e = readdir(d)) {
+      if (e->d_name[0] == '.') continue;
+      std::ifstream f(std::string("/sys/class/kfd/kfd/topology/nodes/") + e->d_name + "/properties");
+      std::string k;
+      long v = 0;
+      while (f >> k >> v)
+        if (k == "simd_count" && v > 0) {
+          ++n;
+          break;
+        }
+    }
+    closedir(d);
+  }
+  for (const char* var : {"HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"}) {
+    const char* s = std::getenv(var);
+    if (s && *s) {
+      int c = 1;
+      for (const char* p = s; *p; ++p) c += *p == ',';
+      n = std::min(n > 0 ? n : c, c);
+    }
+  }
+  return n;
+}
+
+AppConfig parse_args(int argc, char** argv, const std::string& which) {
+  AppConfig c;
+  c.data_root = cohort::default_data_root();
+  c.out_dir = which == "test_pipeline" ? "../out-test" : which == "img_processing_sequential" ? "../out-sequential" : "../out-parallel";
+  if (which == "img_processing_sequential") {
+    c.engine.batch_size = 1;
+    c.engine.streams = 1;
+    c.engine.threads = 2;
+  }
+  for (int i = 1; i < argc; ++i) {
+    std::string a = argv[i];
+    auto val = [&]() -> std::string {
+      if (i + 1 >= argc) {
+        std::cerr << "missing value for " << a << std::endl;
+        std::exit(2);
+      }
+      return argv[++i];
+    };
+    if (a == "--help" || a == "-h") {
+      usage(which);
+      std::exit(0);
+    } else if (a == "--data-root") c.data_root = cohort::with_slash(val());
+    else if (a == "--out") c.out_dir = val();
+    else if (a == "--gpus") {
+      std::string v = val();
+      c.gpus = v == "all" ? std::max(1, visible_gpu_count()) : std::atoi(v.c_str());
+    } else if (a == "--device") c.engine.device = std::atoi(val().c_str());
+    else if (a == "--batch-size") c.engine.batch_size = std::atoi(val().c_str());
+    else if (a == "--streams") c.engine.streams = std::atoi(val().c_str());
+    else if (a == "--threads") c.engine.threads = std::atoi(val().c_str());
+    else if (a == "--median-window") c.engine.pipe.median_window = std::atoi(val().c_str());
+    else if (a == "--srg-connectivity") c.engine.pipe.srg_connectivity = std::atoi(val().c_str());
+    else if (a == "--dilation-size") c.engine.pipe.dilation_size = std::atoi(val().c_str());
+    else if (a == "--erosion-size") c.engine.pipe.erosion_size = std::atoi(val().c_str());
+    else if (a == "--quality") c.engine.render.jpeg_quality = std::atoi(val().c_str());
+    else if (a == "--mode") c.mode = val();
+    else if (a == "--input") c.input = val();
+    else if (a == "--cpu") c.cpu = true;
+    else if (a == "--no-montage") c.montage = false;
+    else if (a == "--repeat") c.repeat = std::max(1, std::atoi(val().c_str()));
+    else if (a == "--json") c.json = val();
+    else if (a == "--quiet") c.quiet = true;
+    else if (a == "--max-dim") c.engine.max_dim = std::atoi(val().c_str());
+    else {
+      std::cerr << "unknown option " << a << " (see --help)" << std::endl;
+      std::exit(2);
+    }
+  }
+  if (c.gpus < 1) c.gpus = 1;
+  return c;
+}
+
+// =============================================================================================
+// img_processing_sequential
+// =============================================================================================
+int run_sequential(const AppConfig& cfg) {
+  try {
+    // SequentialImageProcessor ctor: base output dir (main_sequential.cpp:81-91).
+    cohort::make_dirs(cfg.out_dir);
+    const std::string base = cohort::cohort_dir(cfg.data_root);
+    Engine engine(cfg.engine);
+    const double t0 = now_s();
+    StageTimes total;
+    int64_t slices = 0, slices_ok = 0;
+    for (int rep = 0; rep < cfg.repeat; ++rep) {
+      std::cout << "\n=== Starting Sequential Processing for All Patients ===\n" << std::endl;  // :317
+      std::vector<std::string> patients;
+      try {
+        patients = cohort::find_patient_dirs(base);
+        std::cout << "Found " << patients.size() << " patient directories." << std::endl;  // :110
+      } catch (const std::exception& e) {
+        std::cerr << "Error finding patient directories: " << e.what() << std::endl;  // :113
+        throw;
+      }
+      if (patients.empty()) {
+        std::cout << "No patient directories found. Exiting." << std::endl;  // :324
+        return 0;
+      }
+      int successful = 0;
+      for (const auto& pid : patients) {
+        try {
+          try {
+            std::cout << "\n=== Processing Patient: " << pid << " ===\n" << std::endl;  // :276
+            const std::string out = cfg.out_dir + "/" + pid;
+            try {
+              cohort::setup_output_dir(out);
+            } catch (const std::exception& e) {
+              throw std::runtime_error(std::string("Error setting up output directory: ") + e.what());
+            }
+            std::cout << "Created clean output directory: " + out << std::endl;  // :41
+            cohort::Series series;
+            try {
+              series = cohort::list_patient_series(base, pid);
+              std::cout << "Using series directory: " << series.series_dir << std::endl;  // :140
+              std::cout << "Found " << series.files.size() << " DICOM files for patient " << pid << std::endl;
+            } catch (const std::exception& e) {
+              std::cerr << "Error loading DICOM files for patient " << pid << ": " << e.what() << std::endl;  // :164
+              throw;
+            }
+            std::vector<WorkItem> items;
+            for (const auto& f : series.files) items.push_back({f, out});
+            StageTimes t;
+            // Batch 1, one stream: strictly one slice at a time, like the reference loop (:287).
+            auto st = engine.run(
+                items, &t, [&](size_t i) {
+                  if (!cfg.quiet) std::cout << "Processing: \"" << cohort::filename(items[i].path) << "\"" << std::endl;  // :172
+                });
+            int ok = 0;
+            for (size_t i = 0; i < st.size(); ++i) {
+              if (st[i].code == kSliceOk) {
+                ++ok;
+              } else {
+                std::cerr << "Error processing file " << items[i].path << ":\n"
+                          << "Detailed error: " << st[i].message << std::endl;  // :268-269
+              }
+            }
+            total.load_s += t.load_s;
+            total.h2d_s += t.h2d_s;
+            total.kernels_s += t.kernels_s;
+            total.write_s += t.write_s;
+            slices += (int64_t)st.size();
+            slices_ok += ok;
+            // Successes are counted correctly (the reference also counts swallowed failures,
+            // SURVEY §2.8 quirk 1).
+            std::cout << "\nPatient " << pid << " completed. Successfully processed " << ok << "/" << items.size()
+                      << " images." << std::endl;  // :297-299
+          } catch (const std::exception& e) {
+            std::cerr << "Error processing patient " << pid << ": " << e.what() << std::endl;  // :302
+          }
+          ++successful;
+        } catch (const std::exception& e) {
+          std::cerr << "Failed to process patient " << pid << ". Moving to next patient." << std::endl;  // :335
+        }
+      }
+      std::cout << "\n=== All Processing Completed ===\n" << std::endl;                              // :340
+      std::cout << "Successfully processed " << successful << "/" << patients.size() << " patients." << std::endl;  // :341
+    }
+    const double wall = now_s() - t0;
+    write_json(cfg.json, std::string("{\"mode\": \"sequential\", \"gpus\": 1, \"wall_s\": ") + fmt(wall) +
+                             ", \"slices\": " + std::to_string(slices) + ", \"slices_ok\": " + std::to_string(slices_ok) +
+                             ", \"slices_per_s\": " + fmt(slices_ok / std::max(wall, 1e-9)) +
+                             ", \"load_s\": " + fmt(total.load_s) + ", \"h2d_s\": " + fmt(total.h2d_s) +
+                             ", \"kernels_s\": " + fmt(total.kernels_s) + ", \"write_s\": " + fmt(total.write_s) + "}");
+  } catch (const std::exception& e) {
+    std::cerr << "Fatal error: " << e.what() << std::endl;  // :359-360
+    return 1;
+  }
+  return 0;
+}
+
+// =============================================================================================
+// img_processing_parallel — N ranks, one MI355X each, global work list sharded in contiguous
+// blocks; rank 0 plans (directories, ordering) and prints; RCCL carries plan and results.
+// =============================================================================================
+namespace {
+
+struct PatientPlan {
+  std::string id, out_dir, series_dir, error;
+  bool setup_ok = false, listed = false;
+  std::vector<std::string> files;
+};
+
+std::vector<uint8_t> encode_plan(const std::vector<PatientPlan>& pl) {
+  ByteWriter w;
+  w.u32((uint32_t)pl.size());
+  for (const auto& p : pl) {
+    w.str(p.id);
+    w.str(p.out_dir);
+    w.str(p.series_dir);
+    w.str(p.error);
+    w.u32(p.setup_ok);
+    w.u32(p.listed);
+    w.u32((uint32_t)p.files.size());
+    for (const auto& f : p.files) w.str(f);
+  }
+  return w.b;
+}
+
+std::vector<PatientPlan> decode_plan(const std::vector<uint8_t>& b) {
+  ByteReader r(b.data(), b.size());
+  std::vector<PatientPlan> pl(r.u32());
+  for (auto& p : pl) {
+    p.id = r.str();
+    p.out_dir = r.str();
+    p.series_dir = r.str();
+    p.error = r.str();
+    p.setup_ok = r.u32();
+    p.listed = r.u32();
+    p.files.resize(r.u32());
+    for (auto& f : p.files) f = r.str();
+  }
+  return pl;
+}
+
+int parallel_rank(const AppConfig& cfg, int rank, int size, Comm& comm) {
+  const std::string base = cohort::cohort_dir(cfg.data_root);
+  EngineConfig ec = cfg.engine;
+  if (size > 1) ec.device = rank;
+  Engine engine(ec);
+  const double t_start = now_s();
+  double proc_wall = 0;
+  int64_t total_ok = 0, total_slices = 0;
+  StageTimes agg;
+  for (int rep = 0; rep < cfg.repeat; ++rep) {
+    // ---- plan on rank 0 --------------------------------------------------------------------
+    std::vector<uint8_t> plan_bytes;
+    int64_t fatal = 0;
+    std::string fatal_msg;
+    if (rank == 0) {
+      std::cout << "\n=== Starting Parallel Processing for All Patients ===\n" << std::endl;  // :360
+      std::vector<PatientPlan> plan;
+      try {
+        std::vector<std::string> pids;
+        try {
+          pids = cohort::find_patient_dirs(base);
+          std::cout << "Found " << pids.size() << " patient directories." << std::endl;  // :250
+        } catch (const std::exception& e) {
+          std::cerr << "Error finding patient directories: " << e.what() << std::endl;  // :253
+          throw;
+        }
+        for (const auto& pid : pids) {
+          PatientPlan p;
+          p.id = pid;
+          p.out_dir = cfg.out_dir + "/" + pid;
+          try {
+            cohort::setup_output_dir(p.out_dir);
+            p.setup_ok = true;
+            cohort::Series s = cohort::list_patient_series(base, pid);
+            p.series_dir = s.series_dir;
+            p.files = std::move(s.files);
+            p.listed = true;
+          } catch (const std::exception& e) {
+            p.error = p.setup_ok ? e.what() : std::string("Error setting up output directory: ") + e.what();
+          }
+          plan.push_back(std::move(p));
+        }
+      } catch (const std::exception& e) {
+        fatal = 1;
+        fatal_msg = e.what();
+      }
+      plan_bytes = encode_plan(plan);
+    }
+    comm.allreduce_sum_i64(&fatal, 1);
+    if (fatal) {
+      if (rank == 0) std::cerr << "Fatal error: " << fatal_msg << std::endl;
+      return 1;
+    }
+    comm.broadcast_bytes(plan_bytes, 0);  // ncclBroadcast of the serialized work list
+    std::vector<PatientPlan> plan = decode_plan(plan_bytes);
+    std::vector<WorkItem> items;
+    std::vector<int> owner;
+    for (size_t p = 0; p < plan.size(); ++p)
+      for (const auto& f : plan[p].files) {
+        items.push_back({f, plan[p].out_dir});
+        owner.push_back((int)p);
+      }
+    // Contiguous equal blocks per rank (deterministic, ±1 slice).
+    const size_t n = items.size();
+    const size_t lo = n * rank / size, hi = n * (rank + 1) / size;
+    std::vector<WorkItem> mine(items.begin() + lo, items.begin() + hi);
+    comm.barrier();
+    const double t0 = now_s();
+    StageTimes t;
+    std::vector<SliceStatus> st = engine.run(mine, &t);
+    comm.barrier();
+    double wall = now_s() - t0;
+    comm.allreduce_max_f64(&wall, 1);
+    proc_wall += wall;
+    agg.load_s += t.load_s;
+    agg.h2d_s += t.h2d_s;
+    agg.kernels_s += t.kernels_s;
+    agg.write_s += t.write_s;
+    agg.jpeg_fallbacks += t.jpeg_fallbacks;
+    // ---- gather statuses -------------------------------------------------------------------
+    ByteWriter w;
+    w.u32((uint32_t)st.size());
+    for (const auto& s : st) {
+      w.i32(s.code);
+      w.str(s.message);
+    }
+    auto all = comm.allgather_bytes(w.b);
+    if (rank == 0) {
+      std::vector<SliceStatus> gst;
+      for (auto& b : all) {
+        ByteReader r(b.data(), b.size());
+        uint32_t k = r.u32();
+        for (uint32_t i = 0; i < k; ++i) {
+          SliceStatus s;
+          s.code = r.i32();
+          s.message = r.str();
+          gst.push_back(std::move(s));
+        }
+      }
+      // ---- print the per-patient blocks in patient order ------------------------------------
+      size_t cursor = 0;
+      int successful = 0;
+      for (size_t p = 0; p < plan.size(); ++p) {
+        const PatientPlan& pp = plan[p];
+        std::cout << "\n=== Processing Patient: " << pp.id << " using Parallel Processing ===\n" << std::endl;  // :313-315
+        if (pp.setup_ok) std::cout << "Created output directory: " + pp.out_dir << std::endl;  // :58
+        if (!pp.listed) {
+          if (pp.setup_ok) std::cerr << "Error loading DICOM files for patient " << pp.id << ": " << pp.error << std::endl;  // :304
+          std::cerr << "Error processing patient " << pp.id << ": " << pp.error << std::endl;  // :353
+          ++successful;
+          continue;
+        }
+        std::cout << "Using series directory: " << pp.series_dir << std::endl;                                 // :280
+        std::cout << "Found " << pp.files.size() << " DICOM files for patient " << pp.id << std::endl;          // :301
+        std::cout << "Found " << pp.files.size() << " images to process for patient " << pp.id << std::endl;    // :324
+        std::cout << "Using " << cfg.engine.threads << " threads\n" << std::endl;                              // :326
+        int ok = 0;
+        for (size_t i = 0; i < pp.files.size(); ++i, ++cursor) {
+          if (!cfg.quiet) std::cout << "Processing: \"" << cohort::filename(pp.files[i]) << "\"" << std::endl;  // :72-73
+          const SliceStatus& s = gst[cursor];
+          if (s.code == kSliceOk) {
+            ++ok;
+          } else if (s.code == kSliceExportError) {
+            std::cerr << s.message << std::endl;  // "Error in export stage: ..." (:214)
+          } else {
+            std::cerr << "Error processing file " << pp.files[i] << ":\n"
+                      << "Detailed error: " << s.message << std::endl;  // :165-166
+          }
+        }
+        total_ok += ok;
+        total_slices += (int64_t)pp.files.size();
+        std::cout << "\nPatient " << pp.id << " completed. Successfully processed " << ok << "/" << pp.files.size()
+                  << " images." << std::endl;  // :349-351
+        ++successful;
+      }
+      if (plan.empty()) std::cout << "No patient directories found. Exiting." << std::endl;  // :367
+      else {
+        std::cout << "\n=== All Processing Completed ===\n" << std::endl;  // :383
+        std::cout << "Successfully processed " << successful << "/" << plan.size() << " patients." << std::endl;
+      }
+    }
+  }
+  double tot = now_s() - t_start;
+  comm.allreduce_max_f64(&tot, 1);
+  if (rank == 0) {
+    write_json(cfg.json, std::string("{\"mode\": \"parallel\", \"gpus\": ") + std::to_string(size) + ", \"backend\": \"" +
+                             comm.backend() + "\", \"repeat\": " + std::to_string(cfg.repeat) + ", \"wall_s\": " + fmt(tot) +
+                             ", \"processing_wall_s\": " + fmt(proc_wall) + ", \"slices\": " + std::to_string(total_slices) +
+                             ", \"slices_ok\": " + std::to_string(total_ok) + ", \"slices_per_s\": " +
+                             fmt(total_ok / std::max(proc_wall, 1e-9)) + ", \"rank0\": {\"load_s\": " + fmt(agg.load_s) +
+                             ", \"h2d_s\": " + fmt(agg.h2d_s) + ", \"kernels_s\": " + fmt(agg.kernels_s) +
+                             ", \"write_s\": " + fmt(agg.write_s) + ", \"jpeg_fallbacks\": " +
+                             std::to_string(agg.jpeg_fallbacks) + "}}");
+  }
+  return 0;
+}
+
+}  // namespace
+
+int run_parallel(const AppConfig& cfg) {
+  try {
+    cohort::make_dirs(cfg.out_dir);  // OptimizedParallelProcessor ctor (main_parallel.cpp:219-231)
+    if (cfg.mode == "3d") return run_volume_cohort(cfg);
+    return launch_ranks(cfg.gpus, [&](int rank, int size, Comm& comm) { return parallel_rank(cfg, rank, size, comm); });
+  } catch (const std::exception& e) {
+    std::cerr << "Fatal error: " << e.what() << std::endl;  // :407-408
+    return 1;
+  }
+}
+
+// =============================================================================================
+// test_pipeline — one slice, all stages, 5 exported stage images (test_pipeline.cpp:164-179),
+// headless: the 5-view MultiViewWindow (:148-158) becomes a montage JPEG.
+// =============================================================================================
+int run_test_pipeline(const AppConfig& cfg) {
+  try {
+    const std::string path = cfg.input.empty() ? cohort::test_slice_path(cfg.data_root) : cfg.input;
+    golden::SliceInput in = golden::load_slice(path, 0);  // the test pipeline has no <100 guard
+    const PipelineParams& p = cfg.engine.pipe;
+    const RenderParams& rp = cfg.engine.render;
+    std::vector<std::vector<uint8_t>> canvases, jpegs;
+    const double t0 = now_s();
+    if (cfg.cpu) {
+      golden::SliceResult r = golden::run(in, p, true);
+      const RenderGeom g = make_render_geom(in.w, in.h, in.spacing_x, in.spacing_y, rp.out_width, rp.out_height);
+      const uint8_t fill = opacity_u8(rp.label_opacity), bv = opacity_u8(rp.border_opacity);
+      auto mm = std::minmax_element(r.sharpened.begin(), r.sharpened.end());
+      canvases.push_back(golden::render_gray(golden::rescaled(in, p), g, r.window_lo, r.window_hi));
+      canvases.push_back(golden::render_gray(r.sharpened, g, *mm.first, *mm.second));
+      canvases.push_back(golden::render_labels(r.region, golden::border(r.region, in.w, in.h, rp.border_radius), g, fill, bv));
+      canvases.push_back(golden::render_labels(r.eroded, golden::border(r.eroded, in.w, in.h, rp.border_radius), g, fill, bv));
+      canvases.push_back(golden::render_labels(r.dilated, golden::border(r.dilated, in.w, in.h, rp.border_radius), g, fill, bv));
+      for (auto& c : canvases) jpegs.push_back(jpeg::encode_gray420(c.data(), rp.out_width, rp.out_height, rp.out_width, rp.jpeg_quality));
+    } else {
+      EngineConfig ec = cfg.engine;
+      ec.batch_size = 1;
+      ec.streams = 1;
+      ec.max_dim = std::max({ec.max_dim, in.w, in.h});
+      Engine engine(ec);
+      SingleResult r = engine.run_single(in);
+      canvases = std::move(r.canvases);
+      jpegs = std::move(r.jpegs);
+    }
+    const double t1 = now_s();
+    // exportImages: wipe + create the output directory, then the 5 stage images (:7-27).
+    cohort::setup_output_dir(cfg.out_dir);
+    static const char* names[5] = {"original_image", "preprocessed_image", "segmentation", "erosion_result",
+                                   "final_dilated_result"};
+    for (int k = 0; k < 5; ++k) {
+      std::ofstream f(cfg.out_dir + "/" + names[k] + ".jpg", std::ios::binary | std::ios::trunc);
+      f.write((const char*)jpegs[k].data(), (std::streamsize)jpegs[k].size());
+    }
+    if (cfg.montage) {
+      // Headless MultiViewWindow(5, Black, ...): the five views side by side.
+      const int cw = rp.out_width, ch = rp.out_height, mw = 5 * cw;
+      std::vector<uint8_t> m((size_t)mw * ch, 0);
+      for (int k = 0; k < 5; ++k)
+        for (int y = 0; y < ch; ++y) std::memcpy(&m[(size_t)y * mw + k * cw], &canvases[k][(size_t)y * cw], cw);
+      auto j = jpeg::encode_gray420(m.data(), mw, ch, mw, rp.jpeg_quality);
+      std::ofstream f(cfg.out_dir + "/multi_view.jpg", std::ios::binary | std::ios::trunc);
+      f.write((const char*)j.data(), (std::streamsize)j.size());
+    }
+    if (!cfg.quiet)
+      std::cout << "Medical Image Processing Stages: " << (cfg.cpu ? "CPU golden model" : "MI355X") << ", "
+                << in.w << "x" << in.h << " slice, pipeline " << fmt((t1 - t0) * 1e3, 4) << " ms, exported 5 images to "
+                << cfg.out_dir << "/" << std::endl;
+    write_json(cfg.json, std::string("{\"mode\": \"test_pipeline\", \"backend\": \"") + (cfg.cpu ? "cpu" : "gpu") +
+                             "\", \"pipeline_ms\": " + fmt((t1 - t0) * 1e3) + "}");
+  } catch (const std::exception& e) {
+    std::cerr << "Fatal error: " << e.what() << std::endl;
+    return 1;
+  }
+  return 0;
+}
+
+}  // namespace nm03::app

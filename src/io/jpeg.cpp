@@ -1,0 +1,223 @@
+// Host JPEG pieces: marker writer and the golden CPU encoder. The GPU path in
+// src/kernels/k4_jpeg.hip must produce the same entropy-coded bytes as encode_scan_gray420.
+#include "nm03/jpeg.h"
+
+#include <fcntl.h>
+#include <sys/uio.h>
+#include <unistd.h>
+
+#include <cerrno>
+#include <cstring>
+#include <stdexcept>
+
+namespace nm03::jpeg {
+
+Tables make_tables(int quality) {
+  Tables t;
+  t.quality = quality;
+  quality_table(kStdLuma, quality, t.qluma);
+  quality_table(kStdChroma, quality, t.qchroma);
+  for (int i = 0; i < 64; ++i) {
+    t.div_luma[i] = (int32_t)t.qluma[i] * 8;
+    t.div_chroma[i] = (int32_t)t.qchroma[i] * 8;
+  }
+  return t;
+}
+
+namespace {
+
+void put16(std::vector<uint8_t>& b, int v) {
+  b.push_back((uint8_t)(v >> 8));
+  b.push_back((uint8_t)v);
+}
+
+void put_dqt(std::vector<uint8_t>& b, int id, const uint16_t* q) {
+  b.push_back(0xFF);
+  b.push_back(0xDB);
+  put16(b, 2 + 1 + 64);
+  b.push_back((uint8_t)id);
+  for (int k = 0; k < 64; ++k) b.push_back((uint8_t)q[kNatural[k]]);
+}
+
+void put_dht(std::vector<uint8_t>& b, int cls_id, const uint8_t* bits, const uint8_t* vals) {
+  int n = 0;
+  for (int i = 0; i < 16; ++i) n += bits[i];
+  b.push_back(0xFF);
+  b.push_back(0xC4);
+  put16(b, 2 + 1 + 16 + n);
+  b.push_back((uint8_t)cls_id);
+  for (int i = 0; i < 16; ++i) b.push_back(bits[i]);
+  for (int i = 0; i < n; ++i) b.push_back(vals[i]);
+}
+
+// MSB-first bit writer with 0xFF byte stuffing (libjpeg emit_bits / flush_bits semantics).
+struct BitWriter {
+  std::vector<uint8_t>& out;
+  uint64_t acc = 0;
+  int n = 0;
+  explicit BitWriter(std::vector<uint8_t>& o) : out(o) {}
+  void put(uint32_t code, int len) {
+    if (len == 0) return;
+    acc = (acc << len) | (code & ((1u << len) - 1u));
+    n += len;
+    while (n >= 8) {
+      uint8_t byte = (uint8_t)(acc >> (n - 8));
+      out.push_back(byte);
+      if (byte == 0xFF) out.push_back(0x00);
+      n -= 8;
+    }
+  }
+  void flush() {
+    if (n > 0) put(0x7F, 8 - n);  // pad the last byte with 1-bits (libjpeg flush_bits)
+    acc = 0;
+    n = 0;
+  }
+};
+
+void encode_block(BitWriter& w, const int16_t* zz, int& last_dc, const HuffEnc& dc, const HuffEnc& ac) {
+  int diff = zz[0] - last_dc;
+  last_dc = zz[0];
+  int nb = mag_bits(diff);
+  w.put(dc.e[nb] & 0xFFFF, (int)(dc.e[nb] >> 16));
+  if (nb) w.put((uint32_t)(diff < 0 ? diff - 1 : diff), nb);
+  int run = 0;
+  for (int k = 1; k < 64; ++k) {
+    int v = zz[k];
+    if (v == 0) {
+      ++run;
+      continue;
+    }
+    while (run > 15) {
+      w.put(ac.e[0xF0] & 0xFFFF, (int)(ac.e[0xF0] >> 16));
+      run -= 16;
+    }
+    int n = mag_bits(v);
+    uint32_t sym = ac.e[(run << 4) + n];
+    w.put(sym & 0xFFFF, (int)(sym >> 16));
+    w.put((uint32_t)(v < 0 ? v - 1 : v), n);
+    run = 0;
+  }
+  if (run > 0) w.put(ac.e[0] & 0xFFFF, (int)(ac.e[0] >> 16));
+}
+
+}  // namespace
+
+std::vector<uint8_t> make_header(int width, int height, const Tables& t) {
+  std::vector<uint8_t> b;
+  b.reserve(700);
+  b.push_back(0xFF);
+  b.push_back(0xD8);  // SOI
+  // APP0 JFIF 1.01, no units, 1:1 density, no thumbnail (libjpeg defaults).
+  const uint8_t app0[] = {0xFF, 0xE0, 0x00, 0x10, 'J', 'F', 'I', 'F', 0x00, 0x01, 0x01, 0x00, 0x00, 0x01, 0x00, 0x01, 0x00, 0x00};
+  b.insert(b.end(), app0, app0 + sizeof(app0));
+  put_dqt(b, 0, t.qluma);
+  put_dqt(b, 1, t.qchroma);
+  // SOF0
+  b.push_back(0xFF);
+  b.push_back(0xC0);
+  put16(b, 8 + 3 * 3);
+  b.push_back(8);
+  put16(b, height);
+  put16(b, width);
+  b.push_back(3);
+  const uint8_t comps[9] = {1, 0x22, 0, 2, 0x11, 1, 3, 0x11, 1};
+  b.insert(b.end(), comps, comps + 9);
+  put_dht(b, 0x00, kDcLumaBits, kDcLumaVals);
+  put_dht(b, 0x10, kAcLumaBits, kAcLumaVals);
+  put_dht(b, 0x01, kDcChromaBits, kDcChromaVals);
+  put_dht(b, 0x11, kAcChromaBits, kAcChromaVals);
+  // SOS
+  b.push_back(0xFF);
+  b.push_back(0xDA);
+  put16(b, 6 + 2 * 3);
+  b.push_back(3);
+  const uint8_t sos[6] = {1, 0x00, 2, 0x11, 3, 0x11};
+  b.insert(b.end(), sos, sos + 6);
+  b.push_back(0);
+  b.push_back(63);
+  b.push_back(0);
+  return b;
+}
+
+std::vector<uint8_t> encode_scan_gray420(const uint8_t* gray, int width, int height, int stride, const Tables& t) {
+  std::vector<uint8_t> out;
+  out.reserve((size_t)width * height / 8);
+  BitWriter w(out);
+  // libjpeg pads each component to whole blocks by edge replication and fills MCU padding with
+  // dummy blocks whose DC repeats the previous block (jccoefct.c compress_data).
+  const int bw = (width + 7) / 8, bh = (height + 7) / 8;
+  const int mcux = (width + 15) / 16, mcuy = (height + 15) / 16;
+  int last_dc_y = 0, last_dc_cb = 0, last_dc_cr = 0;
+  int32_t blk[64];
+  int16_t zz[64];
+  std::vector<int16_t> dc_row((size_t)mcux * 2, 0);
+  int16_t zero_zz[64] = {0};
+  for (int my = 0; my < mcuy; ++my) {
+    for (int mx = 0; mx < mcux; ++mx) {
+      for (int sub = 0; sub < 4; ++sub) {
+        const int by = my * 2 + (sub >> 1), bx = mx * 2 + (sub & 1);
+        if (by < bh && bx < bw) {
+          for (int r = 0; r < 8; ++r) {
+            const int y = by * 8 + r < height ? by * 8 + r : height - 1;
+            for (int c = 0; c < 8; ++c) {
+              const int x = bx * 8 + c < width ? bx * 8 + c : width - 1;
+              blk[r * 8 + c] = (int32_t)gray[(size_t)y * stride + x] - 128;
+            }
+          }
+          fdct_islow(blk);
+          for (int k = 0; k < 64; ++k) zz[k] = quantize(blk[kNatural[k]], t.div_luma[kNatural[k]]);
+        } else {
+          // Dummy block: zero AC, DC = previous block's DC in this MCU row of the component.
+          std::memset(zz, 0, sizeof(zz));
+          zz[0] = (int16_t)last_dc_y;
+        }
+        encode_block(w, zz, last_dc_y, kHuffDcLuma, kHuffAcLuma);
+      }
+      // Cb, Cr: constant 128 → all-zero blocks.
+      encode_block(w, zero_zz, last_dc_cb, kHuffDcChroma, kHuffAcChroma);
+      encode_block(w, zero_zz, last_dc_cr, kHuffDcChroma, kHuffAcChroma);
+    }
+  }
+  w.flush();
+  return out;
+}
+
+std::vector<uint8_t> encode_gray420(const uint8_t* gray, int width, int height, int stride, int quality) {
+  Tables t = make_tables(quality);
+  std::vector<uint8_t> f = make_header(width, height, t);
+  std::vector<uint8_t> s = encode_scan_gray420(gray, width, height, stride, t);
+  f.insert(f.end(), s.begin(), s.end());
+  f.push_back(0xFF);
+  f.push_back(0xD9);
+  return f;
+}
+
+void write_jpeg_file(const std::string& path, const std::vector<uint8_t>& header, const uint8_t* scan, size_t scan_len) {
+  int fd = ::open(path.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
+  if (fd < 0) throw std::runtime_error("Cannot create " + path + ": " + std::strerror(errno));
+  static const uint8_t eoi[2] = {0xFF, 0xD9};
+  struct iovec iov[3] = {{(void*)header.data(), header.size()}, {(void*)scan, scan_len}, {(void*)eoi, 2}};
+  size_t total = header.size() + scan_len + 2, done = 0;
+  int idx = 0;
+  while (done < total) {
+    ssize_t w = ::writev(fd, iov + idx, 3 - idx);
+    if (w < 0 && errno == EINTR) continue;
+    if (w < 0) {
+      ::close(fd);
+      throw std::runtime_error("Write failed: " + path);
+    }
+    done += (size_t)w;
+    size_t adv = (size_t)w;
+    while (idx < 3 && adv >= iov[idx].iov_len) {
+      adv -= iov[idx].iov_len;
+      ++idx;
+    }
+    if (idx < 3) {
+      iov[idx].iov_base = (uint8_t*)iov[idx].iov_base + adv;
+      iov[idx].iov_len -= adv;
+    }
+  }
+  ::close(fd);
+}
+
+}  // namespace nm03::jpeg

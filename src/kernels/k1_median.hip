@@ -1,0 +1,118 @@
+// K1a — k×k median (VectorMedianFilter, main_sequential.cpp:204-206) on gfx950.
+//
+// * One workgroup = 256 threads = one 64×64 output tile of one slice (tile list built on host, so
+//   slices of any size/type share a launch).
+// * The clamp-to-edge input tile (64+k-1)² is staged in LDS as packed u16 PAIRS
+//   (pixel[c], pixel[c+32]) so each v_pk_min_u16 / v_pk_max_u16 advances two medians.
+//   Row stride is odd (PW|1 words) → the lane→(row, col-group) read pattern is conflict-free for
+//   ds_read_b32 (8 rows × 4 groups per 32-lane half hit 32 distinct banks).
+// * Thread (g, r) evaluates the generated selection network (tools/gen_median_net.py) for
+//   outputs (r, 8g..8g+7) and (r, 32+8g..32+8g+7).
+// * Medians are computed on order-preserving 16-bit keys: normalise+clip is monotone, so the
+//   median of c(x) is c(median x) exactly (pixel_math.h). The same pass reduces per-slice min/max
+//   keys for the original-image render window.
+#include <hip/hip_runtime.h>
+
+#include "device_util.h"
+#include "nm03/gpu_types.h"
+#include "nm03/kernels.h"
+#include "nm03/pixel_math.h"
+
+namespace nm03::gpu {
+using nm03::gpu::vmax;
+using nm03::gpu::vmin;
+#include "nm03/median_net.inc"
+
+template <int K>
+__device__ __forceinline__ void run_net(const uint32_t* P, int stride, int r, int g, u16x2* out) {
+  auto ld = [&](int rr, int cc) -> u16x2 { return as_u16x2(P[(r + rr) * stride + 8 * g + cc]); };
+  if constexpr (K == 3) median_net_k3_w8_h1<u16x2>(ld, out);
+  else if constexpr (K == 5) median_net_k5_w8_h1<u16x2>(ld, out);
+  else if constexpr (K == 7) median_net_k7_w8_h1<u16x2>(ld, out);
+  else median_net_k9_w8_h1<u16x2>(ld, out);
+}
+
+template <int K>
+__global__ __launch_bounds__(256) void median_kernel(const uint16_t* __restrict__ raw, uint16_t* __restrict__ med,
+                                                     const SliceDesc* __restrict__ descs,
+                                                     const TileDesc* __restrict__ tiles, SliceStats* stats) {
+  constexpr int R = K / 2;
+  constexpr int PW = 32 + K - 1;  // pair columns
+  constexpr int PS = PW | 1;      // odd stride: conflict-free ds_read_b32
+  constexpr int PR = 64 + K - 1;  // rows
+  __shared__ uint32_t P[PR * PS];
+
+  const TileDesc t = tiles[blockIdx.x];
+  const SliceDesc d = descs[t.slice];
+  const int x0 = t.tx * kMedTileW, y0 = t.ty * kMedTileH;
+  const uint16_t* src = raw + d.raw_off;
+  const int W = d.w, H = d.h;
+
+  uint32_t kmin = 0xFFFFu, kmax = 0u;
+  for (int i = threadIdx.x; i < PR * PW; i += 256) {
+    const int r = i / PW, c = i - r * PW;
+    const int y = clampi(y0 - R + r, 0, H - 1);
+    const int xl = clampi(x0 - R + c, 0, W - 1), xh = clampi(x0 - R + c + 32, 0, W - 1);
+    const uint16_t* row = src + (size_t)y * W;
+    const uint32_t kl = key_from_raw(row[xl], d.type, d.stored_bits);
+    const uint32_t kh = key_from_raw(row[xh], d.type, d.stored_bits);
+    P[r * PS + c] = kl | (kh << 16);
+    kmin = min(kmin, min(kl, kh));
+    kmax = max(kmax, max(kl, kh));
+  }
+  __syncthreads();
+
+  const int g = threadIdx.x & 3, r = threadIdx.x >> 2;
+  u16x2 out[8];
+  run_net<K>(P, PS, r, g, out);
+
+  const int y = y0 + r;
+  if (y < H) {
+    uint16_t* dst = med + d.raw_off + (size_t)y * W;
+    const int xl = x0 + 8 * g;
+    if (xl + 8 <= W && xl + 40 <= W && (W & 7) == 0) {
+      // Fast path: two 16-byte stores.
+      uint4 lo, hi;
+      lo.x = out[0].x | ((uint32_t)out[1].x << 16);
+      lo.y = out[2].x | ((uint32_t)out[3].x << 16);
+      lo.z = out[4].x | ((uint32_t)out[5].x << 16);
+      lo.w = out[6].x | ((uint32_t)out[7].x << 16);
+      hi.x = out[0].y | ((uint32_t)out[1].y << 16);
+      hi.y = out[2].y | ((uint32_t)out[3].y << 16);
+      hi.z = out[4].y | ((uint32_t)out[5].y << 16);
+      hi.w = out[6].y | ((uint32_t)out[7].y << 16);
+      *reinterpret_cast<uint4*>(dst + xl) = lo;
+      *reinterpret_cast<uint4*>(dst + xl + 32) = hi;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        if (xl + j < W) dst[xl + j] = out[j].x;
+        if (xl + 32 + j < W) dst[xl + 32 + j] = out[j].y;
+      }
+    }
+  }
+
+  // Per-slice key range (render window of the original image).
+  kmin = wave_min_u32(kmin);
+  kmax = wave_max_u32(kmax);
+  if ((threadIdx.x & 63) == 0 && stats) {
+    atomicMin(&stats[t.slice].key_min, kmin);
+    atomicMax(&stats[t.slice].key_max, kmax);
+  }
+}
+
+void launch_median(const uint16_t* raw, uint16_t* med, const SliceDesc* descs, const TileDesc* tiles, int ntiles,
+                   int k, SliceStats* stats, hipStream_t stream) {
+  if (ntiles <= 0) return;
+  dim3 grid(ntiles), block(256);
+  switch (k) {
+    case 3: median_kernel<3><<<grid, block, 0, stream>>>(raw, med, descs, tiles, stats); break;
+    case 5: median_kernel<5><<<grid, block, 0, stream>>>(raw, med, descs, tiles, stats); break;
+    case 7: median_kernel<7><<<grid, block, 0, stream>>>(raw, med, descs, tiles, stats); break;
+    case 9: median_kernel<9><<<grid, block, 0, stream>>>(raw, med, descs, tiles, stats); break;
+    default: throw DeviceError("median window must be 3, 5, 7 or 9 (got " + std::to_string(k) + ")");
+  }
+  check_launch("median_kernel");
+}
+
+}  // namespace nm03::gpu

@@ -1,0 +1,101 @@
+// K2 — SeededRegionGrowing (main_sequential.cpp:232-243) + ImageCaster(UINT8) + Dilation(3) /
+// Erosion(3) (main_sequential.cpp:246-252, test_pipeline.cpp:119-125) + the SegmentationRenderer
+// border mask (radius 2), fused in one launch with ONE WORKGROUP PER SLICE and every bit-plane
+// resident in LDS (256² slice: 8 KiB per plane).
+//
+// FAST grows the region with an iterative OpenCL kernel plus host polling of a stop flag
+// (a host↔device round trip per poll, hundreds of iterations). Here the fixpoint
+// runs entirely on-chip:
+//   * horizontal step: every row's runs of in-band pixels that contain a region pixel are filled
+//     at once with the carry trick  F = (((M + S) ^ M) & M) | S  (S = R & M ⊆ M), upward, and
+//     downward on bit-reversed words; carries chain across the row's words;
+//   * vertical step: the same run fill on the TRANSPOSED planes (64×64 bit-block transposes done
+//     in registers with wave64 butterflies, device_util.h);
+//   * 8-connectivity adds a diagonal seeding step R |= M & (dil1(R↑) | dil1(R↓)).
+// The loop stops when a full iteration changes nothing (workgroup barrier + LDS flag; no host).
+// Morphology uses shifted-word ORs/ANDs; out-of-image samples are ignored (App. A.7).
+#include <hip/hip_runtime.h>
+
+#include "device_util.h"
+#include "srg_core.h"
+#include "nm03/gpu_types.h"
+#include "nm03/kernels.h"
+#include "nm03/pixel_math.h"
+
+namespace nm03::gpu {
+
+
+__global__ __launch_bounds__(256) void srg_morph_kernel(const uint64_t* __restrict__ band,
+                                                        const SliceDesc* __restrict__ descs,
+                                                        const SeedXY* __restrict__ seeds, PipeConsts pc,
+                                                        SrgOutputs out, int plane_words) {
+  extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
+  __shared__ int flag;
+  const SliceDesc d = descs[blockIdx.x];
+  const int W = d.w, H = d.h, n = d.wpr, hb = (H + 63) >> 6;
+  const int words = H * n;
+  uint64_t* M = smem;
+  uint64_t* Rg = M + plane_words;
+  uint64_t* Mt = Rg + plane_words;
+  uint64_t* Rt = Mt + plane_words;
+
+  for (int i = threadIdx.x; i < words; i += blockDim.x) {
+    M[i] = band[d.mask_off + i];
+    Rg[i] = 0ull;
+  }
+  __syncthreads();
+  for (int s = threadIdx.x; s < d.seed_count; s += blockDim.x) {
+    const SeedXY sd = seeds[d.seed_off + s];
+    if (sd.x < 0 || sd.y < 0 || sd.x >= W || sd.y >= H) continue;
+    const int wi = sd.y * n + (sd.x >> 6);
+    const uint64_t bit = 1ull << (sd.x & 63);
+    if (M[wi] & bit) atomicOr((unsigned long long*)&Rg[wi], (unsigned long long)bit);
+  }
+  transpose_plane(M, H, n, Mt, W, false, nullptr);
+  __syncthreads();
+
+  const int iters = srg_fixpoint(M, Rg, Mt, Rt, W, H, n, pc.connectivity, &flag);
+  // An iteration in which no step changed anything ⇒ Rg is the fixpoint region.
+  if (out.iterations && threadIdx.x == 0) out.iterations[blockIdx.x] = iters;
+  const size_t off = d.mask_off;
+  if (out.region) store_plane(Rg, out.region + off, words);
+  // Scratch planes now: M, Mt, Rt.
+  if (out.dilated || out.border_dilated) {
+    morph(Rg, Mt, M, W, H, n, pc.dilation_size, true);  // Mt = D
+    if (out.dilated) store_plane(Mt, out.dilated + off, words);
+    if (out.border_dilated) {
+      morph(Mt, Rt, M, W, H, n, 2 * pc.border_radius + 1, false);  // Rt = erode(D)
+      for (int i = threadIdx.x; i < words; i += blockDim.x) out.border_dilated[off + i] = Mt[i] & ~Rt[i];
+    }
+    __syncthreads();
+  }
+  if (out.border_region) {
+    morph(Rg, Rt, M, W, H, n, 2 * pc.border_radius + 1, false);
+    for (int i = threadIdx.x; i < words; i += blockDim.x) out.border_region[off + i] = Rg[i] & ~Rt[i];
+    __syncthreads();
+  }
+  if (out.eroded || out.border_eroded) {
+    morph(Rg, Mt, M, W, H, n, pc.erosion_size, false);  // Mt = E
+    if (out.eroded) store_plane(Mt, out.eroded + off, words);
+    if (out.border_eroded) {
+      morph(Mt, Rt, M, W, H, n, 2 * pc.border_radius + 1, false);
+      for (int i = threadIdx.x; i < words; i += blockDim.x) out.border_eroded[off + i] = Mt[i] & ~Rt[i];
+    }
+  }
+}
+
+void launch_srg_morph(const uint64_t* band, const SliceDesc* descs, int nslices, const SeedXY* seeds,
+                      const PipeConsts& pc, const SrgOutputs& out, int max_w, int max_h, hipStream_t stream) {
+  if (nslices <= 0) return;
+  if (max_w > kSrgMaxDim || max_h > kSrgMaxDim)
+    throw DeviceError("launch_srg_morph: slice larger than " + std::to_string(kSrgMaxDim));
+  const int n = (max_w + 63) / 64, hb = (max_h + 63) / 64;
+  int plane_words = max_h * n;
+  if (max_w * hb > plane_words) plane_words = max_w * hb;
+  plane_words = (plane_words + 1) & ~1;
+  const size_t lds = (size_t)plane_words * 4 * sizeof(uint64_t);
+  srg_morph_kernel<<<nslices, 256, lds, stream>>>(band, descs, seeds, pc, out, plane_words);
+  check_launch("srg_morph_kernel");
+}
+
+}  // namespace nm03::gpu

@@ -1,0 +1,154 @@
+// K5 — 3D mode (BASELINE config 5: 256³ volume, SeededRegionGrowing + 7×7×7 Dilation).
+//
+// Region growing on a bit volume [z][y][ceil(w/64)] by PLANE SWEEPS: one workgroup per z-plane
+// loads its band plane and region plane into LDS, seeds from the neighbouring planes
+// (R |= M & (R[z-1] | R[z+1]); 26-connectivity dilates the neighbours in-plane by one first),
+// then runs the same on-chip 2D fixpoint as K2 (srg_core.h: row run fills + transposed column run
+// fills). Planes read their neighbours while those are being rewritten — harmless, because the
+// iteration is monotone (bits are only ever added, and 64-bit words are written atomically); a
+// sweep in which no plane changed proves the fixpoint. The host relaunches sweeps until the
+// device flag stays 0; the count is ≈ the number of z-direction turns of the region, not its
+// geodesic length.
+// Cube dilation is separable: in-plane square dilation in LDS (row shifts + row ORs), then an OR
+// over z. Out-of-volume samples are ignored (App. A.7).
+#include <hip/hip_runtime.h>
+
+#include "device_util.h"
+#include "nm03/gpu_types.h"
+#include "nm03/kernels.h"
+#include "srg_core.h"
+
+namespace nm03::gpu {
+
+__global__ void srg3d_seed_kernel(const uint64_t* __restrict__ band, uint64_t* __restrict__ region, int w, int h,
+                                  int d, const int32_t* __restrict__ seeds, int nseeds) {
+  const int n = (w + 63) >> 6;
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= nseeds) return;
+  const int x = seeds[3 * s], y = seeds[3 * s + 1], z = seeds[3 * s + 2];
+  if (x < 0 || y < 0 || z < 0 || x >= w || y >= h || z >= d) return;
+  const size_t wi = ((size_t)z * h + y) * n + (x >> 6);
+  const uint64_t bit = 1ull << (x & 63);
+  if (band[wi] & bit) atomicOr((unsigned long long*)&region[wi], (unsigned long long)bit);
+}
+
+__global__ __launch_bounds__(256) void srg3d_sweep_kernel(const uint64_t* __restrict__ band, uint64_t* region, int w,
+                                                          int h, int d, int connectivity, int plane_words,
+                                                          uint32_t* changed) {
+  extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
+  __shared__ int flag;
+  const int z = blockIdx.x;
+  const int n = (w + 63) >> 6;
+  const int words = h * n;
+  uint64_t* M = smem;
+  uint64_t* Rg = M + plane_words;
+  uint64_t* Mt = Rg + plane_words;
+  uint64_t* Rt = Mt + plane_words;
+  const size_t off = (size_t)z * words;
+  int local_change = 0;
+  for (int i = threadIdx.x; i < words; i += blockDim.x) {
+    M[i] = band[off + i];
+    Rg[i] = region[off + i];
+  }
+  __syncthreads();
+  // Seeds from the neighbouring planes.
+  if (connectivity == 26) {
+    // Neighbour planes dilated in-plane by one (3×3): stage OR of both neighbours in Mt first.
+    for (int i = threadIdx.x; i < words; i += blockDim.x) {
+      uint64_t nb = 0;
+      if (z > 0) nb |= region[off - words + i];
+      if (z + 1 < d) nb |= region[off + words + i];
+      Mt[i] = nb;
+    }
+    __syncthreads();
+    morph(Mt, Mt, Rt, w, h, n, 3, true);
+  } else {
+    for (int i = threadIdx.x; i < words; i += blockDim.x) {
+      uint64_t nb = 0;
+      if (z > 0) nb |= region[off - words + i];
+      if (z + 1 < d) nb |= region[off + words + i];
+      Mt[i] = nb;
+    }
+    __syncthreads();
+  }
+  for (int i = threadIdx.x; i < words; i += blockDim.x) Rg[i] |= M[i] & Mt[i];
+  __syncthreads();
+  transpose_plane(M, h, n, Mt, w, false, nullptr);
+  __syncthreads();
+  srg_fixpoint(M, Rg, Mt, Rt, w, h, n, connectivity == 26 ? 8 : 4, &flag);
+  for (int i = threadIdx.x; i < words; i += blockDim.x) {
+    const uint64_t old = region[off + i];
+    const uint64_t nv = Rg[i] | old;
+    if (nv != old) {
+      region[off + i] = nv;
+      local_change = 1;
+    }
+  }
+  if (local_change) atomicOr(changed, 1u);
+}
+
+__global__ __launch_bounds__(256) void dilate_plane_kernel(const uint64_t* __restrict__ src, uint64_t* __restrict__ dst,
+                                                           int w, int h, int size, int plane_words) {
+  extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
+  const int n = (w + 63) >> 6, words = h * n;
+  const size_t off = (size_t)blockIdx.x * words;
+  uint64_t* A = smem;
+  uint64_t* B = A + plane_words;
+  uint64_t* T = B + plane_words;
+  for (int i = threadIdx.x; i < words; i += blockDim.x) A[i] = src[off + i];
+  __syncthreads();
+  morph(A, B, T, w, h, n, size, true);
+  for (int i = threadIdx.x; i < words; i += blockDim.x) dst[off + i] = B[i];
+}
+
+__global__ void dilate_z_kernel(const uint64_t* __restrict__ src, uint64_t* __restrict__ dst, int words, int d, int r) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (size_t)words * d) return;
+  const int z = (int)(i / words);
+  uint64_t acc = src[i];
+  for (int k = 1; k <= r; ++k) {
+    if (z - k >= 0) acc |= src[i - (size_t)k * words];
+    if (z + k < d) acc |= src[i + (size_t)k * words];
+  }
+  dst[i] = acc;
+}
+
+int srg_volume(const uint64_t* band, uint64_t* region, int w, int h, int d, const int32_t* seeds_xyz, int nseeds,
+               int connectivity, uint32_t* d_flag, uint32_t* h_flag, hipStream_t stream) {
+  if (w > kSrgMaxDim || h > kSrgMaxDim) throw DeviceError("srg_volume: plane larger than 512");
+  const int n = (w + 63) / 64, hb = (h + 63) / 64;
+  const size_t words = (size_t)h * n;
+  int plane_words = (int)words;
+  if (w * hb > plane_words) plane_words = w * hb;
+  plane_words = (plane_words + 1) & ~1;
+  check_hip(hipMemsetAsync(region, 0, words * d * sizeof(uint64_t), stream), "memset region");
+  if (nseeds > 0) {
+    srg3d_seed_kernel<<<(nseeds + 63) / 64, 64, 0, stream>>>(band, region, w, h, d, seeds_xyz, nseeds);
+    check_launch("srg3d_seed_kernel");
+  }
+  const size_t lds = (size_t)plane_words * 4 * sizeof(uint64_t);
+  int sweeps = 0;
+  for (;;) {
+    ++sweeps;
+    check_hip(hipMemsetAsync(d_flag, 0, sizeof(uint32_t), stream), "memset flag");
+    srg3d_sweep_kernel<<<d, 256, lds, stream>>>(band, region, w, h, d, connectivity, plane_words, d_flag);
+    check_launch("srg3d_sweep_kernel");
+    check_hip(hipMemcpyAsync(h_flag, d_flag, sizeof(uint32_t), hipMemcpyDeviceToHost, stream), "flag d2h");
+    check_hip(hipStreamSynchronize(stream), "sweep sync");
+    if (*h_flag == 0 || sweeps > 4 * (w + h + d)) break;
+  }
+  return sweeps;
+}
+
+void dilate_volume(const uint64_t* src, uint64_t* dst, uint64_t* tmp, int w, int h, int d, int size, hipStream_t stream) {
+  const int n = (w + 63) / 64;
+  const int words = h * n;
+  const int plane_words = (words + 1) & ~1;
+  dilate_plane_kernel<<<d, 256, (size_t)plane_words * 3 * sizeof(uint64_t), stream>>>(src, tmp, w, h, size, plane_words);
+  check_launch("dilate_plane_kernel");
+  const size_t total = (size_t)words * d;
+  dilate_z_kernel<<<(unsigned)((total + 255) / 256), 256, 0, stream>>>(tmp, dst, words, d, size / 2);
+  check_launch("dilate_z_kernel");
+}
+
+}  // namespace nm03::gpu

@@ -1,0 +1,166 @@
+// Shared LDS bit-plane region-growing core (2D slices: k2_srg_morph.hip, 3D plane sweeps:
+// k5_volume.hip). See k2_srg_morph.hip for the algorithm description.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "device_util.h"
+
+namespace nm03::gpu {
+
+__device__ __forceinline__ uint64_t brev64(uint64_t x) { return __builtin_bitreverse64(x); }
+
+__device__ __forceinline__ uint64_t fill_up(uint64_t m, uint64_t s) { return (((m + s) ^ m) & m) | s; }
+
+// Fill runs of M (n words) that intersect R, both directions. Returns true if R changed.
+__device__ __forceinline__ bool fill_row(uint64_t* R, const uint64_t* M, int n) {
+  bool changed = false;
+  uint64_t carry = 0;
+  for (int i = 0; i < n; ++i) {
+    const uint64_t m = M[i], r = R[i];
+    const uint64_t s = (r & m) | (carry & m & 1ull);
+    const uint64_t f = fill_up(m, s);
+    const uint64_t nr = r | f;
+    changed |= nr != r;
+    R[i] = nr;
+    carry = f >> 63;
+  }
+  carry = 0;
+  for (int i = n - 1; i >= 0; --i) {
+    const uint64_t m = brev64(M[i]), r = brev64(R[i]);
+    const uint64_t s = (r & m) | (carry & m & 1ull);
+    const uint64_t f = fill_up(m, s);
+    const uint64_t nr = r | f;
+    changed |= nr != r;
+    R[i] = brev64(nr);
+    carry = f >> 63;
+  }
+  return changed;
+}
+
+// Transpose a [rows][wpr] bit-plane into [cols][ceil(rows/64)]. Returns (via flag) whether any
+// destination word changed when `cmp` is set.
+__device__ inline void transpose_plane(const uint64_t* src, int rows, int wpr, uint64_t* dst, int cols, bool cmp, int* flag) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int hb = (rows + 63) >> 6;
+  const int nblocks = hb * wpr;
+  bool changed = false;
+  for (int b = wave; b < nblocks; b += nw) {
+    const int bi = b / wpr, bj = b - bi * wpr;
+    const int row = bi * 64 + lane;
+    uint64_t x = row < rows ? src[row * wpr + bj] : 0ull;
+    x = wave_transpose64(x, lane);
+    const int drow = bj * 64 + lane;
+    if (drow < cols) {
+      uint64_t* p = dst + drow * hb + bi;
+      if (cmp && *p != x) changed = true;
+      *p = x;
+    }
+  }
+  if (cmp && changed) *flag = 1;
+}
+
+__device__ __forceinline__ uint64_t last_mask(int w) {
+  const int r = w & 63;
+  return r ? ((1ull << r) - 1ull) : ~0ull;
+}
+
+// Horizontal morphology of one row: OR (dilate) or AND (erode, outside = 1) of shifts by ±1..±r.
+__device__ __forceinline__ void morph_row_h(const uint64_t* src, uint64_t* dst, int n, int w, int r, bool dil) {
+  const uint64_t lm = last_mask(w);
+  for (int i = 0; i < n; ++i) {
+    uint64_t v = src[i];
+    uint64_t prev = i > 0 ? src[i - 1] : (dil ? 0ull : ~0ull);
+    uint64_t next = i + 1 < n ? src[i + 1] : (dil ? 0ull : ~0ull);
+    if (!dil) {
+      if (i == n - 1) v |= ~lm;          // bits past the right edge count as "ignored" (=1)
+      if (i + 1 == n - 1) next |= ~lm;
+    }
+    uint64_t acc = v;
+    for (int k = 1; k <= r; ++k) {
+      const uint64_t left = (v << k) | (prev >> (64 - k));   // pixel x-k
+      const uint64_t right = (v >> k) | (next << (64 - k));  // pixel x+k
+      acc = dil ? (acc | left | right) : (acc & left & right);
+    }
+    dst[i] = (i == n - 1) ? (acc & lm) : acc;
+  }
+}
+
+// Vertical morphology: dst[y] = OP_{|dy|≤r, 0≤y+dy<H} src[y+dy].
+__device__ __forceinline__ void morph_rows_v(const uint64_t* src, uint64_t* dst, int h, int n, int r, bool dil) {
+  for (int idx = threadIdx.x; idx < h * n; idx += blockDim.x) {
+    const int y = idx / n, i = idx - y * n;
+    uint64_t acc = src[idx];
+    for (int k = 1; k <= r; ++k) {
+      if (y - k >= 0) acc = dil ? (acc | src[idx - k * n]) : (acc & src[idx - k * n]);
+      if (y + k < h) acc = dil ? (acc | src[idx + k * n]) : (acc & src[idx + k * n]);
+    }
+    dst[idx] = acc;
+  }
+}
+
+__device__ inline void morph(const uint64_t* src, uint64_t* dst, uint64_t* tmp, int w, int h, int n, int size, bool dil) {
+  const int r = size / 2;
+  for (int y = threadIdx.x; y < h; y += blockDim.x) morph_row_h(src + y * n, tmp + y * n, n, w, r, dil);
+  __syncthreads();
+  morph_rows_v(tmp, dst, h, n, r, dil);
+  __syncthreads();
+}
+
+__device__ inline void store_plane(const uint64_t* src, uint64_t* dst, int words) {
+  for (int i = threadIdx.x; i < words; i += blockDim.x) dst[i] = src[i];
+}
+
+
+// Grow Rg (seeded, ⊆ M) to the fixpoint of horizontal run fills, vertical run fills on the
+// transposed planes and (connectivity 8) diagonal seeding. Mt must hold transpose(M); Rt is
+// scratch. All planes in LDS. `flag` is an LDS int. Returns the iteration count.
+__device__ inline int srg_fixpoint(uint64_t* M, uint64_t* Rg, const uint64_t* Mt, uint64_t* Rt, int W, int H, int n,
+                            int connectivity, int* flagp) {
+  int& flag = *flagp;
+  const int hb = (H + 63) >> 6, words = H * n;
+  int iters = 0;
+  const int max_iters = W * H + 4;  // monotone growth ⇒ always terminates earlier
+  if (threadIdx.x == 0) flag = 0;
+  __syncthreads();
+  for (;;) {
+    ++iters;
+    bool ch = false;
+    for (int y = threadIdx.x; y < H; y += blockDim.x) ch |= fill_row(Rg + y * n, M + y * n, n);
+    if (ch) flag = 1;
+    __syncthreads();
+    if (connectivity == 8) {
+      // Diagonal seeding from a snapshot of the horizontally dilated rows (Rt as scratch).
+      for (int y = threadIdx.x; y < H; y += blockDim.x) morph_row_h(Rg + y * n, Rt + y * n, n, W, 1, true);
+      __syncthreads();
+      bool dch = false;
+      for (int idx = threadIdx.x; idx < words; idx += blockDim.x) {
+        const int y = idx / n;
+        uint64_t nb = 0;
+        if (y > 0) nb |= Rt[idx - n];
+        if (y + 1 < H) nb |= Rt[idx + n];
+        const uint64_t add = M[idx] & nb & ~Rg[idx];
+        if (add) {
+          Rg[idx] |= add;
+          dch = true;
+        }
+      }
+      if (dch) flag = 1;
+      __syncthreads();
+    }
+    transpose_plane(Rg, H, n, Rt, W, false, nullptr);
+    __syncthreads();
+    for (int x = threadIdx.x; x < W; x += blockDim.x) fill_row(Rt + x * hb, Mt + x * hb, hb);
+    __syncthreads();
+    transpose_plane(Rt, W, hb, Rg, H, true, &flag);
+    __syncthreads();
+    const int f = flag;
+    __syncthreads();
+    if (threadIdx.x == 0) flag = 0;
+    __syncthreads();
+    if (f == 0 || iters >= max_iters) break;
+  }
+  return iters;
+}
+
+}  // namespace nm03::gpu

@@ -1,0 +1,605 @@
+// Batch engine: host side of the MI355X pipeline (see include/nm03/engine.h).
+#include "nm03/engine.h"
+
+#include <hip/hip_runtime_api.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cstring>
+#include <mutex>
+#include <thread>
+
+#include "nm03/cohort.h"
+#include "nm03/dicom.h"
+#include "nm03/gpu_types.h"
+#include "nm03/jpeg.h"
+#include "nm03/kernels.h"
+#include "nm03/thread_pool.h"
+
+namespace nm03 {
+
+using namespace nm03::gpu;
+
+namespace {
+
+constexpr size_t kAlign = 256;
+inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+inline double now_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+enum Plane { kPBand = 0, kPRegion, kPDilated, kPEroded, kPBorderR, kPBorderE, kPBorderD, kNumPlanes };
+
+struct LoadedSlice {
+  bool ok = false;
+  int w = 0, h = 0;
+  uint8_t type = kU16, stored_bits = 16;
+  float slope = 1.f, intercept = 0.f, sx = 1.f, sy = 1.f;
+  uint32_t raw_off = 0;
+};
+
+// Per-image JPEG capacities. The entropy-coded segment of a 512² canvas is a few tens of KB;
+// anything past these caps falls back to the CPU encoder (counted in StageTimes).
+constexpr uint32_t kStageBytes = 256 * 1024;
+constexpr uint32_t kOutCap = 2 * kStageBytes + 64;
+
+struct Slot {
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
+  int cap_slices = 0, cap_canvases = 0;
+  size_t cap_pixels = 0;  // u16 elements in the raw region
+  // blob layout (byte offsets)
+  size_t off_stats = 0, off_desc = 0, off_medt = 0, off_shpt = 0, off_seeds = 0, off_render = 0, off_jpeg = 0,
+         raw_base = 0, blob_bytes = 0;
+  size_t max_medt = 0, max_shpt = 0;
+  uint8_t* h_blob = nullptr;
+  uint8_t* d_blob = nullptr;
+  uint16_t* d_med = nullptr;
+  float* d_f32 = nullptr;
+  uint64_t* d_bits = nullptr;
+  size_t plane_words = 0;
+  uint8_t* d_canvas = nullptr;
+  JpegWork jw;
+  uint8_t* h_out = nullptr;
+  uint8_t* d_out = nullptr;
+  int32_t* h_sizes = nullptr;
+  int32_t* d_sizes = nullptr;
+  std::atomic<size_t> raw_used{0};
+  std::vector<LoadedSlice> loaded;
+  // built per batch
+  std::vector<int> live;  // batch-local indices of loaded slices, in order
+  int ncanvas = 0;
+  int max_w = 0, max_h = 0;
+};
+
+void hip_free_all(Slot& s) {
+  if (s.h_blob) (void)hipHostFree(s.h_blob);
+  if (s.h_out) (void)hipHostFree(s.h_out);
+  if (s.h_sizes) (void)hipHostFree(s.h_sizes);
+  for (void* p : {(void*)s.d_blob, (void*)s.d_med, (void*)s.d_f32, (void*)s.d_bits, (void*)s.d_canvas,
+                  (void*)s.jw.coef, (void*)s.jw.nzmask, (void*)s.jw.acbits, (void*)s.jw.dc, (void*)s.jw.stage,
+                  (void*)s.jw.tmp})
+    if (p) (void)hipFree(p);
+  if (s.ev0) (void)hipEventDestroy(s.ev0);
+  if (s.ev1) (void)hipEventDestroy(s.ev1);
+  if (s.ev2) (void)hipEventDestroy(s.ev2);
+  if (s.stream) (void)hipStreamDestroy(s.stream);
+}
+
+template <class T>
+T* dmalloc(size_t count, const char* what) {
+  void* p = nullptr;
+  check_hip(hipMalloc(&p, std::max<size_t>(count, 1) * sizeof(T)), what);
+  return (T*)p;
+}
+
+}  // namespace
+
+struct Engine::Impl {
+  EngineConfig cfg;
+  std::unique_ptr<ThreadPool> pool;
+  std::vector<std::unique_ptr<Slot>> slots;
+  std::vector<uint8_t> jpeg_header;
+  int32_t divs[64];
+  PipeConsts pc{};
+
+  explicit Impl(const EngineConfig& c) : cfg(c) {
+    if (cfg.batch_size < 1) cfg.batch_size = 1;
+    if (cfg.streams < 1) cfg.streams = 1;
+    if (cfg.max_dim < 16) cfg.max_dim = 16;
+    if (cfg.max_dim > kSrgMaxDim) throw DeviceError("max_dim above " + std::to_string(kSrgMaxDim) + " not supported");
+    const auto& p = cfg.pipe;
+    if (p.median_window != 3 && p.median_window != 5 && p.median_window != 7 && p.median_window != 9)
+      throw DeviceError("median window must be 3, 5, 7 or 9");
+    if (p.sharpen_mask < 1 || p.sharpen_mask > 15 || !(p.sharpen_mask & 1))
+      throw DeviceError("sharpen mask must be odd and ≤ 15");
+    if (p.dilation_size < 1 || p.dilation_size > 63 || p.erosion_size < 1 || p.erosion_size > 63)
+      throw DeviceError("morphology sizes must be in [1, 63]");
+    pc.nmin = p.norm_min;
+    pc.nmax = p.norm_max;
+    pc.nlow = p.norm_low;
+    pc.nhigh = p.norm_high;
+    pc.cmin = p.clip_min;
+    pc.cmax = p.clip_max;
+    pc.gain = p.sharpen_gain;
+    pc.band_lo = p.srg_min;
+    pc.band_hi = p.srg_max;
+    gaussian_taps(p.sharpen_sigma, p.sharpen_mask, pc.taps);
+    pc.mask_radius = p.sharpen_mask / 2;
+    pc.median_k = p.median_window;
+    pc.connectivity = p.srg_connectivity == 8 ? 8 : 4;
+    pc.dilation_size = p.dilation_size;
+    pc.erosion_size = p.erosion_size;
+    pc.border_radius = cfg.render.border_radius;
+    jpeg::Tables t = jpeg::make_tables(cfg.render.jpeg_quality);
+    for (int i = 0; i < 64; ++i) divs[i] = t.div_luma[i];
+    jpeg_header = jpeg::make_header(cfg.render.out_width, cfg.render.out_height, t);
+    if (cfg.render.out_width % 16 || cfg.render.out_height % 16)
+      throw DeviceError("canvas size must be a multiple of 16");
+    check_hip(hipSetDevice(cfg.device), "hipSetDevice");
+    pool = std::make_unique<ThreadPool>(cfg.threads);
+    for (int i = 0; i < cfg.streams; ++i) slots.push_back(make_slot());
+  }
+
+  ~Impl() {
+    (void)hipSetDevice(cfg.device);
+    for (auto& s : slots) hip_free_all(*s);
+  }
+
+  std::unique_ptr<Slot> make_slot() {
+    auto sp = std::make_unique<Slot>();
+    Slot& s = *sp;
+    const int B = cfg.batch_size;
+    const int md = cfg.max_dim;
+    s.cap_slices = B;
+    s.cap_canvases = std::max(2 * B, 5);
+    s.cap_pixels = (size_t)B * align_up((size_t)md * md, 8);
+    const size_t tx_med = (md + kMedTileW - 1) / kMedTileW, ty_med = (md + kMedTileH - 1) / kMedTileH;
+    const size_t tx_shp = (md + kShpTileW - 1) / kShpTileW, ty_shp = (md + kShpTileH - 1) / kShpTileH;
+    s.max_medt = (size_t)B * tx_med * ty_med;
+    s.max_shpt = (size_t)B * tx_shp * ty_shp;
+    size_t o = 0;
+    s.off_stats = o;
+    o = align_up(o + (size_t)B * sizeof(SliceStats), kAlign);
+    s.off_desc = o;
+    o = align_up(o + (size_t)B * sizeof(SliceDesc), kAlign);
+    s.off_medt = o;
+    o = align_up(o + s.max_medt * sizeof(TileDesc), kAlign);
+    s.off_shpt = o;
+    o = align_up(o + s.max_shpt * sizeof(TileDesc), kAlign);
+    s.off_seeds = o;
+    o = align_up(o + (size_t)B * kMaxSeeds * sizeof(SeedXY), kAlign);
+    s.off_render = o;
+    o = align_up(o + (size_t)s.cap_canvases * sizeof(RenderDesc), kAlign);
+    s.off_jpeg = o;
+    o = align_up(o + (size_t)s.cap_canvases * sizeof(JpegDesc), kAlign);
+    s.raw_base = o;
+    s.blob_bytes = o + s.cap_pixels * sizeof(uint16_t);
+    try {
+      check_hip(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking), "hipStreamCreate");
+      check_hip(hipEventCreate(&s.ev0), "hipEventCreate");
+      check_hip(hipEventCreate(&s.ev1), "hipEventCreate");
+      check_hip(hipEventCreate(&s.ev2), "hipEventCreate");
+      check_hip(hipHostMalloc((void**)&s.h_blob, s.blob_bytes, hipHostMallocDefault), "hipHostMalloc blob");
+      s.d_blob = dmalloc<uint8_t>(s.blob_bytes, "hipMalloc blob");
+      s.d_med = dmalloc<uint16_t>(s.cap_pixels, "hipMalloc median");
+      s.d_f32 = dmalloc<float>(s.cap_pixels, "hipMalloc f32");
+      s.plane_words = (size_t)B * md * ((md + 63) / 64);
+      s.d_bits = dmalloc<uint64_t>(s.plane_words * kNumPlanes, "hipMalloc bits");
+      const int cw = cfg.render.out_width, ch = cfg.render.out_height;
+      const size_t canvas_bytes = (size_t)cw * ch;
+      const size_t blocks = canvas_bytes / 64;
+      s.d_canvas = dmalloc<uint8_t>(canvas_bytes * s.cap_canvases, "hipMalloc canvas");
+      s.jw.coef = dmalloc<int16_t>(blocks * 64 * s.cap_canvases, "hipMalloc coef");
+      s.jw.nzmask = dmalloc<uint64_t>(blocks * s.cap_canvases, "hipMalloc nz");
+      s.jw.acbits = dmalloc<uint32_t>(blocks * s.cap_canvases, "hipMalloc acbits");
+      s.jw.dc = dmalloc<int16_t>(blocks * s.cap_canvases, "hipMalloc dc");
+      s.jw.stage = dmalloc<uint32_t>((size_t)kStageBytes / 4 * s.cap_canvases, "hipMalloc stage");
+      s.jw.tmp = dmalloc<uint8_t>((size_t)kOutCap * s.cap_canvases, "hipMalloc jpeg tmp");
+      check_hip(hipHostMalloc((void**)&s.h_out, (size_t)kOutCap * s.cap_canvases, hipHostMallocMapped),
+                "hipHostMalloc out");
+      check_hip(hipHostGetDevicePointer((void**)&s.d_out, s.h_out, 0), "hipHostGetDevicePointer out");
+      check_hip(hipHostMalloc((void**)&s.h_sizes, sizeof(int32_t) * s.cap_canvases, hipHostMallocMapped),
+                "hipHostMalloc sizes");
+      check_hip(hipHostGetDevicePointer((void**)&s.d_sizes, s.h_sizes, 0), "hipHostGetDevicePointer sizes");
+    } catch (...) {
+      hip_free_all(s);
+      throw;
+    }
+    return sp;
+  }
+
+  // ---- loading -------------------------------------------------------------------------------
+  void load_into(Slot& s, int i, const std::string& path, SliceStatus& st, std::atomic<int64_t>& load_ns,
+                 std::atomic<int64_t>& bytes_in) {
+    thread_local std::vector<uint8_t> buf;
+    const double t0 = now_s();
+    try {
+      const size_t n = dicom::read_file_into(path, buf);
+      dicom::Header h = dicom::parse(buf.data(), n);
+      const int md = cfg.pipe.min_dim;
+      if (md > 0 && (h.cols < md || h.rows < md)) {
+        st.code = kSliceTooSmall;
+        st.message = "Image dimensions too small: " + std::to_string(h.cols) + "x" + std::to_string(h.rows);
+      } else if (h.cols > cfg.max_dim || h.rows > cfg.max_dim) {
+        st.code = kSliceLoadError;
+        st.message = "Image dimensions " + std::to_string(h.cols) + "x" + std::to_string(h.rows) +
+                     " exceed the engine limit " + std::to_string(cfg.max_dim);
+      } else {
+        const size_t npix = (size_t)h.rows * h.cols;
+        const size_t alloc = align_up(npix, 8);
+        const size_t off = s.raw_used.fetch_add(alloc);
+        if (off + alloc > s.cap_pixels) throw SliceError("batch pixel capacity exceeded");
+        uint16_t* dst = reinterpret_cast<uint16_t*>(s.h_blob + s.raw_base) + off;
+        dicom::copy_pixels16(h, buf.data(), n, dst);
+        LoadedSlice& L = s.loaded[i];
+        L.w = h.cols;
+        L.h = h.rows;
+        L.type = h.type == kU8 ? kU16 : h.type;
+        L.stored_bits = (uint8_t)(h.type == kU8 ? 8 : h.bits_stored);
+        L.slope = cfg.pipe.apply_rescale ? h.slope : 1.f;
+        L.intercept = cfg.pipe.apply_rescale ? h.intercept : 0.f;
+        L.sx = h.spacing_x;
+        L.sy = h.spacing_y;
+        L.raw_off = (uint32_t)off;
+        L.ok = true;
+        st.code = kSliceOk;
+        bytes_in += (int64_t)n;
+      }
+    } catch (const std::exception& e) {
+      st.code = kSliceLoadError;
+      st.message = e.what();
+    }
+    load_ns += (int64_t)((now_s() - t0) * 1e9);
+  }
+
+  // ---- descriptor build + GPU enqueue --------------------------------------------------------
+  // mode 0: export pair (original, processed); mode 1: test_pipeline (5 canvases, all planes).
+  void build_and_run(Slot& s, int mode, StageTimes* acc) {
+    const int nl = (int)s.live.size();
+    uint8_t* hb = s.h_blob;
+    auto* stats = reinterpret_cast<SliceStats*>(hb + s.off_stats);
+    auto* desc = reinterpret_cast<SliceDesc*>(hb + s.off_desc);
+    auto* medt = reinterpret_cast<TileDesc*>(hb + s.off_medt);
+    auto* shpt = reinterpret_cast<TileDesc*>(hb + s.off_shpt);
+    auto* seeds = reinterpret_cast<SeedXY*>(hb + s.off_seeds);
+    auto* rd = reinterpret_cast<RenderDesc*>(hb + s.off_render);
+    auto* jd = reinterpret_cast<JpegDesc*>(hb + s.off_jpeg);
+    int nmed = 0, nshp = 0, nseed = 0, ncanv = 0;
+    uint32_t mask_off = 0;
+    s.max_w = s.max_h = 0;
+    const int cw = cfg.render.out_width, ch = cfg.render.out_height;
+    const uint32_t canvas_bytes = (uint32_t)(cw * ch);
+    const uint32_t blocks = canvas_bytes / 64;
+    const uint8_t fill = opacity_u8(cfg.render.label_opacity), bval = opacity_u8(cfg.render.border_opacity);
+    for (int c = 0; c < nl; ++c) {
+      const LoadedSlice& L = s.loaded[s.live[c]];
+      stats[c] = SliceStats{0xFFFFFFFFu, 0u, 0xFFFFFFFFu, 0u};
+      SliceDesc& d = desc[c];
+      std::memset(&d, 0, sizeof(d));
+      d.raw_off = L.raw_off;
+      d.w = (uint16_t)L.w;
+      d.h = (uint16_t)L.h;
+      d.wpr = (uint16_t)((L.w + 63) / 64);
+      d.mask_off = mask_off;
+      mask_off += (uint32_t)(d.h * d.wpr);
+      d.type = L.type;
+      d.stored_bits = L.stored_bits;
+      d.slope = L.slope;
+      d.intercept = L.intercept;
+      d.f32_off = L.raw_off;
+      auto sv = reference_seeds(L.w, L.h);
+      d.seed_off = (uint32_t)nseed;
+      d.seed_count = (uint16_t)std::min<size_t>(sv.size(), kMaxSeeds);
+      for (int k = 0; k < d.seed_count; ++k) seeds[nseed++] = SeedXY{(int16_t)sv[k].x, (int16_t)sv[k].y};
+      for (int ty = 0; ty < (L.h + kMedTileH - 1) / kMedTileH; ++ty)
+        for (int tx = 0; tx < (L.w + kMedTileW - 1) / kMedTileW; ++tx) medt[nmed++] = TileDesc{(uint32_t)c, (uint16_t)tx, (uint16_t)ty};
+      for (int ty = 0; ty < (L.h + kShpTileH - 1) / kShpTileH; ++ty)
+        for (int tx = 0; tx < d.wpr; ++tx) shpt[nshp++] = TileDesc{(uint32_t)c, (uint16_t)tx, (uint16_t)ty};
+      s.max_w = std::max(s.max_w, L.w);
+      s.max_h = std::max(s.max_h, L.h);
+      const RenderGeom g = make_render_geom(L.w, L.h, L.sx, L.sy, cw, ch);
+      auto base_rd = [&](RenderKind kind) {
+        RenderDesc r;
+        std::memset(&r, 0, sizeof(r));
+        r.kind = kind;
+        r.type = L.type;
+        r.stored_bits = L.stored_bits;
+        r.fill = fill;
+        r.border_value = bval;
+        r.slice = (uint32_t)c;
+        r.src_w = (uint16_t)L.w;
+        r.src_h = (uint16_t)L.h;
+        r.wpr = d.wpr;
+        r.ox = g.ox;
+        r.oy = g.oy;
+        r.invx = g.invx;
+        r.invy = g.invy;
+        r.slope = L.slope;
+        r.intercept = L.intercept;
+        return r;
+      };
+      auto labels = [&](Plane lab, Plane brd) {
+        RenderDesc r = base_rd(kRenderLabels);
+        r.src_off = (uint32_t)(lab * s.plane_words + d.mask_off);
+        r.border_off = (uint32_t)(brd * s.plane_words + d.mask_off);
+        return r;
+      };
+      RenderDesc orig = base_rd(kRenderRawGray);
+      orig.src_off = L.raw_off;
+      if (mode == 0) {
+        rd[ncanv++] = orig;
+        rd[ncanv++] = labels(kPDilated, kPBorderD);
+      } else {
+        rd[ncanv++] = orig;
+        RenderDesc pre = base_rd(kRenderF32Gray);
+        pre.src_off = d.f32_off;
+        rd[ncanv++] = pre;
+        rd[ncanv++] = labels(kPRegion, kPBorderR);
+        rd[ncanv++] = labels(kPEroded, kPBorderE);
+        rd[ncanv++] = labels(kPDilated, kPBorderD);
+      }
+    }
+    for (int k = 0; k < ncanv; ++k) {
+      rd[k].canvas_off = (uint32_t)k * canvas_bytes;
+      JpegDesc& j = jd[k];
+      std::memset(&j, 0, sizeof(j));
+      j.canvas_off = (uint32_t)k * canvas_bytes;
+      j.coef_off = (uint32_t)k * blocks;
+      j.stage_off = (uint32_t)k * (kStageBytes / 4);
+      j.stage_words = kStageBytes / 4;
+      j.out_off = (uint64_t)k * kOutCap;
+      j.out_cap = kOutCap;
+    }
+    s.ncanvas = ncanv;
+    if (nl == 0) return;
+
+    const size_t bytes = s.raw_base + s.raw_used.load() * sizeof(uint16_t);
+    uint8_t* db = s.d_blob;
+    const auto* d_stats_c = reinterpret_cast<SliceStats*>(db + s.off_stats);
+    auto* d_stats = reinterpret_cast<SliceStats*>(db + s.off_stats);
+    auto* d_desc = reinterpret_cast<SliceDesc*>(db + s.off_desc);
+    auto* d_medt = reinterpret_cast<TileDesc*>(db + s.off_medt);
+    auto* d_shpt = reinterpret_cast<TileDesc*>(db + s.off_shpt);
+    auto* d_seeds = reinterpret_cast<SeedXY*>(db + s.off_seeds);
+    auto* d_rd = reinterpret_cast<RenderDesc*>(db + s.off_render);
+    auto* d_jd = reinterpret_cast<JpegDesc*>(db + s.off_jpeg);
+    auto* d_raw = reinterpret_cast<uint16_t*>(db + s.raw_base);
+    auto plane = [&](Plane p) { return s.d_bits + p * s.plane_words; };
+
+    check_hip(hipEventRecord(s.ev0, s.stream), "event");
+    check_hip(hipMemcpyAsync(s.d_blob, s.h_blob, bytes, hipMemcpyHostToDevice, s.stream), "H2D blob");
+    check_hip(hipEventRecord(s.ev1, s.stream), "event");
+    launch_median(d_raw, s.d_med, d_desc, d_medt, nmed, pc.median_k, d_stats, s.stream);
+    launch_sharpen_band(s.d_med, plane(kPBand), mode == 1 ? s.d_f32 : nullptr, d_desc, d_shpt, nshp, pc, d_stats,
+                        s.stream);
+    SrgOutputs o;
+    o.dilated = plane(kPDilated);
+    o.border_dilated = plane(kPBorderD);
+    if (mode == 1) {
+      o.region = plane(kPRegion);
+      o.eroded = plane(kPEroded);
+      o.border_region = plane(kPBorderR);
+      o.border_eroded = plane(kPBorderE);
+    }
+    launch_srg_morph(plane(kPBand), d_desc, nl, d_seeds, pc, o, s.max_w, s.max_h, s.stream);
+    (void)d_stats_c;
+    launch_render(d_raw, s.d_f32, s.d_bits, d_stats, d_rd, ncanv, cw, ch, s.d_canvas, s.stream);
+    launch_jpeg(s.d_canvas, d_jd, ncanv, cw, ch, divs, s.jw, s.d_out, s.d_sizes, s.stream);
+    check_hip(hipEventRecord(s.ev2, s.stream), "event");
+    check_hip(hipEventSynchronize(s.ev2), "batch sync");
+    if (acc) {
+      float a = 0, b = 0;
+      (void)hipEventElapsedTime(&a, s.ev0, s.ev1);
+      (void)hipEventElapsedTime(&b, s.ev1, s.ev2);
+      acc->h2d_s += a * 1e-3;
+      acc->kernels_s += b * 1e-3;
+    }
+  }
+
+  // Bytes of canvas k's JPEG (header + segment + EOI); falls back to the CPU encoder when the
+  // GPU reported a capacity overflow (-1).
+  bool jpeg_segment(Slot& s, int k, std::vector<uint8_t>& fallback, int64_t* fallbacks) {
+    if (s.h_sizes[k] >= 0) return true;
+    const int cw = cfg.render.out_width, ch = cfg.render.out_height;
+    std::vector<uint8_t> canvas((size_t)cw * ch);
+    check_hip(hipMemcpy(canvas.data(), s.d_canvas + (size_t)k * cw * ch, canvas.size(), hipMemcpyDeviceToHost),
+              "canvas D2H");
+    jpeg::Tables t = jpeg::make_tables(cfg.render.jpeg_quality);
+    fallback = jpeg::encode_scan_gray420(canvas.data(), cw, ch, cw, t);
+    if (fallbacks) ++*fallbacks;
+    return false;
+  }
+
+  void process_batch(Slot& s, const std::vector<WorkItem>& items, size_t first, size_t count,
+                     std::vector<SliceStatus>& status, StageTimes& acc, std::mutex& acc_m,
+                     const std::function<void(size_t)>& on_start) {
+    s.raw_used = 0;
+    s.loaded.assign(count, LoadedSlice{});
+    std::atomic<int64_t> load_ns{0}, bytes_in{0}, write_ns{0}, bytes_out{0};
+    {
+      TaskGroup tg(*pool);
+      for (size_t i = 0; i < count; ++i) {
+        tg.run([&, i] {
+          if (on_start) on_start(first + i);
+          load_into(s, (int)i, items[first + i].path, status[first + i], load_ns, bytes_in);
+        });
+      }
+      tg.wait();
+    }
+    s.live.clear();
+    for (size_t i = 0; i < count; ++i)
+      if (s.loaded[i].ok) s.live.push_back((int)i);
+    StageTimes local;
+    int64_t fallbacks = 0;
+    if (!s.live.empty()) {
+      try {
+        build_and_run(s, 0, &local);
+      } catch (const std::exception& e) {
+        for (int i : s.live) status[first + i] = SliceStatus{kSliceDeviceError, e.what()};
+        s.live.clear();
+      }
+    }
+    if (cfg.export_jpeg && !s.live.empty()) {
+      // CPU fallbacks (rare) are resolved here, on the slot thread that owns the device context.
+      std::vector<std::vector<uint8_t>> fb(s.ncanvas);
+      std::vector<char> use_fb(s.ncanvas, 0);
+      for (int k = 0; k < s.ncanvas; ++k) {
+        try {
+          use_fb[k] = !jpeg_segment(s, k, fb[k], &fallbacks);
+        } catch (const std::exception& e) {
+          const size_t item = first + s.live[k / 2];
+          status[item] = SliceStatus{kSliceExportError, e.what()};
+        }
+      }
+      TaskGroup tg(*pool);
+      for (int c = 0; c < (int)s.live.size(); ++c) {
+        const size_t item = first + s.live[c];
+        if (status[item].code != kSliceOk) continue;
+        tg.run([&, c, item] {
+          const double t0 = now_s();
+          try {
+            const std::string base = cohort::with_slash(items[item].out_dir) + cohort::stem(items[item].path);
+            for (int k = 0; k < 2; ++k) {
+              const int cv = 2 * c + k;
+              const std::string path = base + (k == 0 ? "_original.jpg" : "_processed.jpg");
+              const uint8_t* seg = use_fb[cv] ? fb[cv].data() : s.h_out + (size_t)cv * kOutCap;
+              const size_t len = use_fb[cv] ? fb[cv].size() : (size_t)s.h_sizes[cv];
+              jpeg::write_jpeg_file(path, jpeg_header, seg, len);
+              bytes_out += (int64_t)(jpeg_header.size() + len + 2);
+            }
+          } catch (const std::exception& e) {
+            status[item] = SliceStatus{kSliceExportError, std::string("Error in export stage: ") + e.what()};
+          }
+          write_ns += (int64_t)((now_s() - t0) * 1e9);
+        });
+      }
+      tg.wait();
+    }
+    std::lock_guard<std::mutex> g(acc_m);
+    acc.load_s += load_ns.load() * 1e-9;
+    acc.write_s += write_ns.load() * 1e-9;
+    acc.h2d_s += local.h2d_s;
+    acc.kernels_s += local.kernels_s;
+    acc.bytes_in += bytes_in.load();
+    acc.bytes_out += bytes_out.load();
+    acc.jpeg_fallbacks += fallbacks;
+    acc.batches += 1;
+  }
+
+  std::vector<SliceStatus> run(const std::vector<WorkItem>& items, StageTimes* times,
+                               const std::function<void(size_t)>& on_start) {
+    const double t0 = now_s();
+    std::vector<SliceStatus> status(items.size());
+    StageTimes acc;
+    std::mutex acc_m;
+    const size_t B = (size_t)cfg.batch_size;
+    const size_t nb = (items.size() + B - 1) / B;
+    std::atomic<size_t> next{0};
+    std::vector<std::thread> th;
+    std::exception_ptr err;
+    std::mutex err_m;
+    for (auto& sp : slots) {
+      Slot* s = sp.get();
+      th.emplace_back([&, s] {
+        try {
+          check_hip(hipSetDevice(cfg.device), "hipSetDevice");
+          for (size_t b; (b = next.fetch_add(1)) < nb;) {
+            const size_t first = b * B, count = std::min(B, items.size() - first);
+            process_batch(*s, items, first, count, status, acc, acc_m, on_start);
+          }
+        } catch (...) {
+          std::lock_guard<std::mutex> g(err_m);
+          if (!err) err = std::current_exception();
+        }
+      });
+    }
+    for (auto& t : th) t.join();
+    if (err) std::rethrow_exception(err);
+    for (const auto& st : status) (st.code == kSliceOk ? acc.slices_ok : acc.slices_failed) += 1;
+    acc.wall_s = now_s() - t0;
+    if (times) *times = acc;
+    return status;
+  }
+
+  SingleResult run_single(const golden::SliceInput& in) {
+    check_hip(hipSetDevice(cfg.device), "hipSetDevice");
+    Slot& s = *slots[0];
+    if (in.w > cfg.max_dim || in.h > cfg.max_dim) throw DeviceError("slice exceeds engine max_dim");
+    s.raw_used = align_up((size_t)in.w * in.h, 8);
+    s.loaded.assign(1, LoadedSlice{});
+    LoadedSlice& L = s.loaded[0];
+    L.ok = true;
+    L.w = in.w;
+    L.h = in.h;
+    L.type = in.type;
+    L.stored_bits = (uint8_t)in.stored_bits;
+    L.slope = cfg.pipe.apply_rescale ? in.slope : 1.f;
+    L.intercept = cfg.pipe.apply_rescale ? in.intercept : 0.f;
+    L.sx = in.spacing_x;
+    L.sy = in.spacing_y;
+    L.raw_off = 0;
+    std::memcpy(s.h_blob + s.raw_base, in.raw.data(), in.raw.size() * sizeof(uint16_t));
+    s.live.assign(1, 0);
+    build_and_run(s, 1, nullptr);
+    SingleResult r;
+    r.w = in.w;
+    r.h = in.h;
+    const size_t npix = (size_t)in.w * in.h;
+    r.median_keys.resize(npix);
+    r.sharpened.resize(npix);
+    check_hip(hipMemcpy(r.median_keys.data(), s.d_med, npix * 2, hipMemcpyDeviceToHost), "D2H median");
+    check_hip(hipMemcpy(r.sharpened.data(), s.d_f32, npix * 4, hipMemcpyDeviceToHost), "D2H sharpened");
+    const int wpr = (in.w + 63) / 64;
+    std::vector<uint64_t> words((size_t)in.h * wpr);
+    auto unpack = [&](Plane p, std::vector<uint8_t>& dst) {
+      check_hip(hipMemcpy(words.data(), s.d_bits + p * s.plane_words, words.size() * 8, hipMemcpyDeviceToHost),
+                "D2H plane");
+      dst.assign(npix, 0);
+      for (int y = 0; y < in.h; ++y)
+        for (int x = 0; x < in.w; ++x) dst[(size_t)y * in.w + x] = (words[(size_t)y * wpr + x / 64] >> (x % 64)) & 1;
+    };
+    unpack(kPBand, r.band);
+    unpack(kPRegion, r.region);
+    unpack(kPEroded, r.eroded);
+    unpack(kPDilated, r.dilated);
+    unpack(kPBorderR, r.border_region);
+    unpack(kPBorderE, r.border_eroded);
+    unpack(kPBorderD, r.border_dilated);
+    const int cw = cfg.render.out_width, ch = cfg.render.out_height;
+    for (int k = 0; k < s.ncanvas; ++k) {
+      std::vector<uint8_t> cv((size_t)cw * ch);
+      check_hip(hipMemcpy(cv.data(), s.d_canvas + (size_t)k * cw * ch, cv.size(), hipMemcpyDeviceToHost), "D2H canvas");
+      r.canvases.push_back(std::move(cv));
+      std::vector<uint8_t> fb;
+      const bool gpu_ok = jpeg_segment(s, k, fb, nullptr);
+      std::vector<uint8_t> f = jpeg_header;
+      if (gpu_ok)
+        f.insert(f.end(), s.h_out + (size_t)k * kOutCap, s.h_out + (size_t)k * kOutCap + s.h_sizes[k]);
+      else
+        f.insert(f.end(), fb.begin(), fb.end());
+      f.push_back(0xFF);
+      f.push_back(0xD9);
+      r.jpegs.push_back(std::move(f));
+    }
+    return r;
+  }
+};
+
+Engine::Engine(const EngineConfig& cfg) : impl_(std::make_unique<Impl>(cfg)) {}
+Engine::~Engine() = default;
+std::vector<SliceStatus> Engine::run(const std::vector<WorkItem>& items, StageTimes* times,
+                                     const std::function<void(size_t)>& on_start) {
+  return impl_->run(items, times, on_start);
+}
+SingleResult Engine::run_single(const golden::SliceInput& s) { return impl_->run_single(s); }
+const EngineConfig& Engine::config() const { return impl_->cfg; }
+
+int device_count() {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+}  // namespace nm03

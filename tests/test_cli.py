@@ -1,0 +1,47 @@
+"""CLIs on CPU: test_pipeline --cpu (BASELINE config 1, golden plumbing) and argument handling."""
+import io
+import os
+
+import numpy as np
+import pytest
+
+from conftest import run_bin
+
+
+def test_test_pipeline_cpu(native, cohort_root, tmp_path):
+    out = tmp_path / "out-test"
+    (out).mkdir()
+    (out / "stale.jpg").write_bytes(b"x")
+    r = run_bin("test_pipeline", "--cpu", "--data-root", cohort_root, "--out", str(out))
+    assert r.returncode == 0, r.stderr
+    names = sorted(p.name for p in out.iterdir())
+    assert names == sorted(["original_image.jpg", "preprocessed_image.jpg", "segmentation.jpg", "erosion_result.jpg",
+                            "final_dilated_result.jpg", "multi_view.jpg"])
+    # golden_run gives the same original/dilated exports
+    raw, meta = native.read_slice(native.test_slice_path(cohort_root))
+    g = native.golden_run(raw, meta["type"], meta["stored_bits"], meta["slope"], meta["intercept"],
+                          native.PipelineParams(), native.RenderParams(), meta["spacing_x"], meta["spacing_y"])
+    assert (out / "original_image.jpg").read_bytes() == g["jpeg_original"]
+    assert (out / "final_dilated_result.jpg").read_bytes() == g["jpeg_processed"]
+    PIL = pytest.importorskip("PIL.Image")
+    im = PIL.open(io.BytesIO((out / "multi_view.jpg").read_bytes()))
+    assert im.size == (2560, 512)
+
+
+def test_cli_help_and_bad_flag():
+    for tool in ("test_pipeline", "img_processing_sequential", "img_processing_parallel"):
+        r = run_bin(tool, "--help")
+        assert r.returncode == 0 and "--data-root" in r.stdout
+        r = run_bin(tool, "--bogus")
+        assert r.returncode == 2
+
+
+def test_synth_tool(tmp_path):
+    r = run_bin("nm03_synth", "--data-root", str(tmp_path), "--patients", "2", "--min-slices", "2", "--max-slices", "3")
+    assert r.returncode == 0, r.stderr
+    assert "Wrote" in r.stdout
+
+
+def test_missing_data_root_is_fatal(tmp_path):
+    r = run_bin("test_pipeline", "--cpu", "--data-root", str(tmp_path / "nope"), "--out", str(tmp_path / "o"))
+    assert r.returncode == 1 and "Fatal error" in r.stderr

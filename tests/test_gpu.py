@@ -1,0 +1,313 @@
+"""GPU tests (MI355X): every HIP kernel vs the plain-PyTorch fp32 reference and the C++ golden
+model, engine end-to-end byte identity, CLIs, fault handling, 3D mode."""
+import io
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import nm03_capstone_project_amd as nm
+from nm03_capstone_project_amd import ops
+from nm03_capstone_project_amd.ops import reference as R
+
+from conftest import run_bin
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _require_gpu():
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    # The native extension must be the one actually running (no silent fallback).
+    assert nm.native().device_count() >= 1
+
+
+def _phantom(native, h=256, w=256, p=3, s=12, seed=7):
+    return native.phantom_slice(h, w, p, s, 25, seed)
+
+
+# ---------------------------------------------------------------------------------------------
+# K1a median
+# ---------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("k", [3, 5, 7, 9])
+@pytest.mark.parametrize("shape", [(256, 256), (130, 100), (512, 512), (64, 200)])
+def test_median_kernel_vs_torch_and_golden(native, k, shape):
+    h, w = shape
+    raw = _phantom(native, h, w)
+    t = torch.from_numpy(raw.view(np.int16)).cuda()
+    med = ops.median2d(t, k).cpu().numpy().view(np.uint16)
+    assert np.array_equal(med, native.golden_median_u16(raw, k))
+    ref = R.median(torch.from_numpy(raw.astype(np.float32)).cuda(), k).cpu().numpy()
+    assert np.array_equal(med.astype(np.float32), ref)
+
+
+def test_median_kernel_batched_random_full_range(native):
+    rng = np.random.default_rng(1)
+    raw = rng.integers(0, 65536, size=(5, 128, 192), dtype=np.uint16)
+    t = torch.from_numpy(raw.view(np.int16)).cuda()
+    med = ops.median2d(t, 7).cpu().numpy().view(np.uint16)
+    for i in range(5):
+        assert np.array_equal(med[i], native.golden_median_u16(raw[i], 7))
+
+
+def test_median_signed_and_stored_bits(native):
+    rng = np.random.default_rng(2)
+    vals = rng.integers(-2048, 2048, size=(100, 120)).astype(np.int16)
+    raw = vals.view(np.uint16) & np.uint16(0x0FFF)  # 12-bit two's complement in a 16-bit container
+    t = torch.from_numpy(raw.view(np.int16)).cuda()
+    med = ops.median2d(t, 5, pixel_type="i16", stored_bits=12).cpu().numpy().view(np.uint16)
+    keys = ((vals.astype(np.int32) & 0xFFFF) ^ 0x8000).astype(np.uint16)  # order-preserving keys
+    assert np.array_equal(med, native.golden_median_u16(keys, 5))
+
+
+# ---------------------------------------------------------------------------------------------
+# K1b sharpen + band
+# ---------------------------------------------------------------------------------------------
+def test_sharpen_band_vs_golden_and_torch(native):
+    raw = _phantom(native)
+    mk = native.golden_median_u16(raw, 7)
+    t = torch.from_numpy(mk.view(np.int16)).cuda()
+    s, band = ops.sharpen_band(t)
+    s = s.cpu().numpy()
+    p = native.PipelineParams()
+    c = native.golden_norm_clip(mk, "u16", 16, 1.0, 0.0, p)
+    gs = native.golden_sharpen(c, 2.0, 0.5, 9, False)
+    assert np.array_equal(s, gs)  # bit-exact: same separable order, no FMA contraction
+    ref = R.sharpen(torch.from_numpy(c)).numpy()
+    assert np.abs(s - ref).max() < 2e-6
+    assert np.array_equal(band.cpu().numpy(), (gs >= np.float32(0.74)) & (gs <= np.float32(0.91)))
+
+
+def test_sharpen_band_odd_size_rescale(native):
+    raw = _phantom(native, 150, 203)
+    mk = native.golden_median_u16(raw, 7)
+    t = torch.from_numpy(mk.view(np.int16)).cuda()
+    s, band = ops.sharpen_band(t, slope=1.25, intercept=-40.0)
+    p = native.PipelineParams()
+    c = native.golden_norm_clip(mk, "u16", 16, 1.25, -40.0, p)
+    gs = native.golden_sharpen(c, 2.0, 0.5, 9, False)
+    assert np.array_equal(s.cpu().numpy(), gs)
+
+
+# ---------------------------------------------------------------------------------------------
+# K2 SRG + morphology
+# ---------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("conn", [4, 8])
+@pytest.mark.parametrize("shape,density", [((256, 256), 0.55), ((512, 512), 0.6), ((131, 77), 0.5), ((256, 256), 0.7)])
+def test_region_grow_kernel_vs_golden(native, conn, shape, density):
+    h, w = shape
+    rng = np.random.default_rng(h * w + conn)
+    band = rng.random(shape) < density
+    seeds = [(x, y, 0) for (x, y) in native.reference_seeds(w, h)]
+    cfg = nm.PipelineConfig(srg_connectivity=conn)
+    out = ops.region_grow(torch.from_numpy(band).cuda(), seeds, cfg)
+    g = native.golden_region_grow(band.astype(np.uint8), seeds, conn)
+    assert np.array_equal(out["region"].cpu().numpy(), g.astype(bool))
+    assert np.array_equal(out["dilated"].cpu().numpy(), native.golden_morph(g, 3, True).astype(bool))
+    assert np.array_equal(out["eroded"].cpu().numpy(), native.golden_morph(g, 3, False).astype(bool))
+    assert np.array_equal(out["border_region"].cpu().numpy(), native.golden_border(g, 2).astype(bool))
+    ref = R.region_grow(torch.from_numpy(band).cuda(), seeds, conn).cpu().numpy()
+    assert np.array_equal(out["region"].cpu().numpy(), ref)
+
+
+def test_region_grow_spiral_needs_many_turns(native):
+    """A 1-pixel spiral corridor forces many alternations of horizontal/vertical run fills."""
+    h = w = 128
+    band = np.zeros((h, w), bool)
+    lo, hi = 2, w - 3
+    y = x = 2
+    while lo < hi:
+        band[lo, lo:hi + 1] = True
+        band[lo:hi + 1, hi] = True
+        band[hi, lo:hi + 1] = True
+        band[lo + 2:hi + 1, lo] = True
+        band[lo + 2, lo:lo + 3] = True
+        lo += 4
+        hi -= 4
+    seeds = [(2, 2, 0)]
+    out = ops.region_grow(torch.from_numpy(band).cuda(), seeds)
+    g = native.golden_region_grow(band.astype(np.uint8), seeds, 4)
+    assert np.array_equal(out["region"].cpu().numpy(), g.astype(bool))
+
+
+# ---------------------------------------------------------------------------------------------
+# K4 JPEG
+# ---------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("kind", ["noise", "phantom", "labels", "black"])
+def test_jpeg_kernel_vs_golden_and_libjpeg(native, kind):
+    rng = np.random.default_rng(3)
+    if kind == "noise":
+        c = rng.integers(0, 256, size=(3, 512, 512), dtype=np.uint8)
+    elif kind == "black":
+        c = np.zeros((2, 512, 512), np.uint8)
+    else:
+        raw = _phantom(native).astype(np.float32)
+        g = native.golden_render_gray(raw, float(raw.min()), float(raw.max()), 1.0, 1.0, 512, 512)
+        if kind == "labels":
+            g = np.where(g > 140, 153, 0).astype(np.uint8)
+            g[::37] = 255
+        c = np.stack([g, g[::-1].copy()])
+    outs = ops.jpeg_encode(torch.from_numpy(c).cuda(), 75)
+    for i in range(c.shape[0]):
+        assert outs[i] is not None
+        assert outs[i] == native.jpeg_encode_gray420(c[i], 75)
+    PIL = pytest.importorskip("PIL.Image")
+    bio = io.BytesIO()
+    PIL.fromarray(c[0]).convert("RGB").save(bio, format="JPEG", quality=75)
+    assert outs[0] == bio.getvalue()
+
+
+def test_jpeg_capacity_overflow_reports(native):
+    # 1024×1024 noise exceeds the per-image staging cap → None (callers fall back to the CPU)
+    c = np.random.default_rng(0).integers(0, 256, size=(1, 1024, 1024), dtype=np.uint8)
+    outs = ops.jpeg_encode(torch.from_numpy(c).cuda(), 100)
+    assert outs[0] is None or outs[0] == native.jpeg_encode_gray420(c[0], 100)
+
+
+# ---------------------------------------------------------------------------------------------
+# Engine: every stage of one slice vs the golden model
+# ---------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("shape,spacing", [((256, 256), (1.0, 1.0)), ((200, 160), (0.9, 1.2)), ((512, 512), (0.5, 0.5))])
+def test_engine_single_all_stages_bit_exact(native, shape, spacing):
+    h, w = shape
+    raw = _phantom(native, h, w)
+    meta = {"type": "u16", "stored_bits": 16, "slope": 1.0, "intercept": 0.0, "spacing_x": spacing[0],
+            "spacing_y": spacing[1]}
+    pipe = nm.SlicePipeline(nm.PipelineConfig(batch_size=1, streams=1, threads=2))
+    gpu = pipe.run_array(raw, meta)
+    ref = pipe.golden(raw, meta)
+    assert np.array_equal(gpu["sharpened"], ref["sharpened"])
+    for k in ("band", "region", "dilated", "eroded"):
+        assert np.array_equal(gpu[k], ref[k].astype(bool)), k
+    assert gpu["jpegs"][0] == ref["jpeg_original"]
+    assert gpu["jpegs"][4] == ref["jpeg_processed"]
+    for j in gpu["jpegs"]:
+        assert j[:2] == b"\xff\xd8" and j[-2:] == b"\xff\xd9"
+
+
+def test_engine_signed_rescaled(native):
+    raw = (_phantom(native).astype(np.int32) - 300).astype(np.int16).view(np.uint16)
+    meta = {"type": "i16", "stored_bits": 16, "slope": 1.5, "intercept": 100.0}
+    pipe = nm.SlicePipeline(nm.PipelineConfig(batch_size=1, streams=1, threads=2))
+    gpu, ref = pipe.run_array(raw, meta), pipe.golden(raw, meta)
+    for k in ("band", "region", "dilated"):
+        assert np.array_equal(gpu[k], ref[k].astype(bool)), k
+    assert gpu["jpegs"][0] == ref["jpeg_original"] and gpu["jpegs"][4] == ref["jpeg_processed"]
+
+
+# ---------------------------------------------------------------------------------------------
+# Engine: cohort runs, configurations agree byte-for-byte with each other and the golden model
+# ---------------------------------------------------------------------------------------------
+def _items(native, root, out):
+    base = native.cohort_dir(root)
+    items = []
+    for pid in native.find_patient_dirs(base):
+        _, files = native.list_patient_series(base, pid)
+        od = os.path.join(out, pid)
+        os.makedirs(od, exist_ok=True)
+        items += [(f, od) for f in files]
+    return items
+
+
+def _tree(d):
+    res = {}
+    for dp, _, fs in os.walk(d):
+        for f in fs:
+            p = os.path.join(dp, f)
+            res[os.path.relpath(p, d)] = open(p, "rb").read()
+    return res
+
+
+def test_engine_cohort_configs_identical(native, cohort_root, tmp_path):
+    trees = []
+    for i, (b, s, t) in enumerate([(1, 1, 1), (25, 3, 8), (7, 2, 4), (64, 4, 16)]):
+        out = str(tmp_path / f"o{i}")
+        items = _items(native, cohort_root, out)
+        cfg = nm.PipelineConfig(batch_size=b, streams=s, threads=t)
+        st, times = native.Engine(cfg.engine_config()).run(items)
+        assert all(code == 0 for code, _ in st), st
+        assert times["slices_ok"] == len(items) and times["jpeg_fallbacks"] == 0
+        trees.append(_tree(out))
+    assert len(trees[0]) == 2 * len(items)
+    for t in trees[1:]:
+        assert t == trees[0]
+    # spot-check against the golden model
+    f, _ = items[len(items) // 2]
+    raw, meta = native.read_slice(f)
+    g = native.golden_run(raw, meta["type"], meta["stored_bits"], meta["slope"], meta["intercept"],
+                          native.PipelineParams(), native.RenderParams(), meta["spacing_x"], meta["spacing_y"])
+    stem = os.path.splitext(os.path.basename(f))[0]
+    pid = os.path.basename(os.path.dirname(os.path.dirname(f)))
+    assert trees[0][f"{pid}/{stem}_original.jpg"] == g["jpeg_original"]
+    assert trees[0][f"{pid}/{stem}_processed.jpg"] == g["jpeg_processed"]
+
+
+def test_engine_fault_isolation(native, tmp_path):
+    d = tmp_path / "series"
+    d.mkdir()
+    good = native.phantom_slice(256, 256, 1, 5, 25, 1)
+    (d / "1-1.dcm").write_bytes(native.dicom_bytes(good))
+    (d / "1-2.dcm").write_bytes(b"DICM-but-not-really" * 10)
+    (d / "1-3.dcm").write_bytes(native.dicom_bytes(np.zeros((64, 64), np.uint16)))  # < 100 guard
+    (d / "1-4.dcm").write_bytes(native.dicom_bytes(good[::-1].copy()))
+    out = tmp_path / "out"
+    out.mkdir()
+    items = [(str(d / f"1-{i}.dcm"), str(out)) for i in range(1, 5)]
+    st, times = native.Engine(nm.PipelineConfig(batch_size=4, streams=1, threads=2).engine_config()).run(items)
+    codes = [c for c, _ in st]
+    assert codes == [0, 1, 2, 0]
+    assert "too small" in st[2][1]
+    assert sorted(p.name for p in out.iterdir()) == ["1-1_original.jpg", "1-1_processed.jpg", "1-4_original.jpg",
+                                                     "1-4_processed.jpg"]
+
+
+# ---------------------------------------------------------------------------------------------
+# CLIs on the GPU: sequential ≡ parallel byte-for-byte, reference message catalogue
+# ---------------------------------------------------------------------------------------------
+def test_cli_sequential_equals_parallel(native, cohort_root, tmp_path):
+    seq, par = tmp_path / "out-sequential", tmp_path / "out-parallel"
+    r1 = run_bin("img_processing_sequential", "--data-root", cohort_root, "--out", str(seq))
+    assert r1.returncode == 0, r1.stderr
+    r2 = run_bin("img_processing_parallel", "--data-root", cohort_root, "--out", str(par))
+    assert r2.returncode == 0, r2.stderr
+    t1, t2 = _tree(str(seq)), _tree(str(par))
+    assert t1 == t2 and len(t1) > 0
+    for line in ("=== Starting Sequential Processing for All Patients ===", "Found 4 patient directories.",
+                 "=== Processing Patient: PGBM-001 ===", "Created clean output directory: ", "Using series directory: ",
+                 'Processing: "1-01.dcm"', "completed. Successfully processed", "=== All Processing Completed ===",
+                 "Successfully processed 4/4 patients."):
+        assert line in r1.stdout, line
+    for line in ("=== Starting Parallel Processing for All Patients ===",
+                 "=== Processing Patient: PGBM-001 using Parallel Processing ===", "Created output directory: ",
+                 "images to process for patient PGBM-001", "Using 16 threads", "Successfully processed 4/4 patients."):
+        assert line in r2.stdout, line
+
+
+def test_cli_test_pipeline_gpu_equals_cpu(native, cohort_root, tmp_path):
+    a, b = tmp_path / "gpu", tmp_path / "cpu"
+    r = run_bin("test_pipeline", "--data-root", cohort_root, "--out", str(a))
+    assert r.returncode == 0, r.stderr
+    r = run_bin("test_pipeline", "--cpu", "--data-root", cohort_root, "--out", str(b))
+    assert r.returncode == 0, r.stderr
+    assert _tree(str(a)) == _tree(str(b))
+
+
+# ---------------------------------------------------------------------------------------------
+# 3D mode
+# ---------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("conn", [6, 26])
+def test_volume_vs_golden(native, conn):
+    d, h, w = 24, 96, 128
+    vol = np.stack([native.phantom_slice(h, w, 2, z, d, 5) for z in range(d)])
+    vp = nm.VolumePipeline(connectivity=conn, dilation=5)
+    seeds = vp.default_seeds(vol)
+    res = vp.run(vol, seeds)
+    # band per slice == 2D golden band
+    for z in (0, d // 2, d - 1):
+        g = native.golden_run(vol[z])
+        assert np.array_equal(res["band"][z], g["band"]), z
+    region, dil = vp.golden(res["band"], seeds)
+    assert np.array_equal(res["region"], region)
+    assert np.array_equal(res["dilated"], dil)
+    assert res["sweeps"] >= 1
