@@ -2,6 +2,10 @@
 // message catalogue. Prints one JSON line.
 //   --config cohort  (2/3)   full synthetic T1+C cohort, end-to-end (read → GPU → JPEG files)
 //   --config volume  (5)     one patient series as a volume, 3D SRG + cube dilation
+//   --config cpu-reference   BASELINE.md protocol: the golden CPU model in the reference's
+//                            structure — per patient, batches of ≤25 slices over 16 threads
+//                            (#pragma omp parallel for, main_parallel.cpp:336), then a SERIAL
+//                            export of the batch (render + JPEG + write, main_parallel.cpp:346)
 #include <chrono>
 #include <cstdlib>
 #include <iostream>
@@ -9,6 +13,9 @@
 
 #include "nm03/cohort.h"
 #include "nm03/engine.h"
+#include "nm03/golden.h"
+#include "nm03/jpeg.h"
+#include "nm03/thread_pool.h"
 #include "nm03/volume.h"
 
 static double now_s() {
@@ -68,6 +75,57 @@ int main(int argc, char** argv) {
                 << ", \"ms_per_step\": " << dt * 1e3 / steps << ", \"slices_per_s\": " << acc.slices_ok / dt
                 << ", \"load_s\": " << acc.load_s << ", \"h2d_s\": " << acc.h2d_s << ", \"kernels_s\": " << acc.kernels_s
                 << ", \"write_s\": " << acc.write_s << "}" << std::endl;
+    } else if (config == "cpu-reference") {
+      nm03::ThreadPool pool(ec.threads);
+      std::vector<std::pair<std::string, std::vector<std::string>>> pats;
+      for (const auto& p : pids) {
+        auto s = nm03::cohort::list_patient_series(base, p);
+        const std::string od = out + "/" + p;
+        nm03::cohort::make_dirs(od);
+        pats.push_back({od, s.files});
+      }
+      auto one_pass = [&]() -> size_t {
+        size_t ok = 0;
+        for (auto& pp : pats) {
+          const auto& files = pp.second;
+          for (size_t b0 = 0; b0 < files.size(); b0 += (size_t)ec.batch_size) {
+            const size_t nb = std::min((size_t)ec.batch_size, files.size() - b0);
+            std::vector<nm03::golden::SliceInput> in(nb);
+            std::vector<nm03::golden::SliceResult> res(nb);
+            std::vector<char> good(nb, 0);
+            {
+              nm03::TaskGroup tg(pool);
+              for (size_t i = 0; i < nb; ++i)
+                tg.run([&, i] {
+                  try {
+                    in[i] = nm03::golden::load_slice(files[b0 + i], ec.pipe.min_dim);
+                    res[i] = nm03::golden::run(in[i], ec.pipe, false);
+                    good[i] = 1;
+                  } catch (...) {
+                  }
+                });
+              tg.wait();
+            }
+            for (size_t i = 0; i < nb; ++i) {  // serial export, like exportBatch
+              if (!good[i]) continue;
+              auto j = nm03::golden::export_jpegs(in[i], res[i], ec.pipe, ec.render);
+              const std::string stem = pp.first + "/" + nm03::cohort::stem(files[b0 + i]);
+              nm03::jpeg::write_jpeg_file(stem + "_original.jpg", {}, j.original.data(), j.original.size() - 2);
+              nm03::jpeg::write_jpeg_file(stem + "_processed.jpg", {}, j.processed.data(), j.processed.size() - 2);
+              ++ok;
+            }
+          }
+        }
+        return ok;
+      };
+      for (int w = 0; w < warmup; ++w) one_pass();
+      size_t ok = 0;
+      const double t0 = now_s();
+      for (int k = 0; k < steps; ++k) ok += one_pass();
+      const double dt = now_s() - t0;
+      std::cout << "{\"config\": \"cpu-reference\", \"threads\": " << ec.threads << ", \"batch\": " << ec.batch_size
+                << ", \"steps\": " << steps << ", \"ms_per_step\": " << dt * 1e3 / steps
+                << ", \"slices_per_s\": " << ok / dt << "}" << std::endl;
     } else if (config == "volume") {
       if (pids.empty()) throw std::runtime_error("no patients");
       auto s = nm03::cohort::list_patient_series(base, pids[0]);
