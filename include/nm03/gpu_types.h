@@ -88,13 +88,16 @@ struct RenderDesc {
 
 // JPEG job: one canvas (out_w×out_h, both multiples of 16) → one entropy-coded segment.
 struct JpegDesc {
-  uint32_t canvas_off;  // bytes
+  uint32_t canvas_off;  // bytes (generic path: rendered canvas)
   uint32_t coef_off;    // block index of the image's first block (MCU order, 4 luma blocks/MCU)
   uint32_t stage_off;   // u32 word offset of the bit staging area
   uint32_t stage_words;
   uint64_t out_off;     // byte offset in the output buffer (host-mapped)
   uint32_t out_cap;     // capacity in bytes
-  uint32_t pad;
+  int32_t render;       // ≥0: fused 2× render from RenderDesc[render] (no canvas); -1: read canvas
 };
+
+// Byte-stuffing chunk (bytes of entropy-coded data per workgroup in the stuffing kernels).
+inline constexpr int kStuffChunk = 4096;
 
 }  // namespace nm03::gpu

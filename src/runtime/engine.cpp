@@ -70,6 +70,7 @@ struct Slot {
   // built per batch
   std::vector<int> live;  // batch-local indices of loaded slices, in order
   int ncanvas = 0;
+  bool any_canvas = false;  // some image of the batch needs the generic render → canvas path
   int max_w = 0, max_h = 0;
 };
 
@@ -79,7 +80,7 @@ void hip_free_all(Slot& s) {
   if (s.h_sizes) (void)hipHostFree(s.h_sizes);
   for (void* p : {(void*)s.d_blob, (void*)s.d_med, (void*)s.d_f32, (void*)s.d_bits, (void*)s.d_canvas,
                   (void*)s.jw.coef, (void*)s.jw.nzmask, (void*)s.jw.acbits, (void*)s.jw.dc, (void*)s.jw.stage,
-                  (void*)s.jw.tmp})
+                  (void*)s.jw.boff, (void*)s.jw.total, (void*)s.jw.chunk_ff})
     if (p) (void)hipFree(p);
   if (s.ev0) (void)hipEventDestroy(s.ev0);
   if (s.ev1) (void)hipEventDestroy(s.ev1);
@@ -196,7 +197,10 @@ struct Engine::Impl {
       s.jw.acbits = dmalloc<uint32_t>(blocks * s.cap_canvases, "hipMalloc acbits");
       s.jw.dc = dmalloc<int16_t>(blocks * s.cap_canvases, "hipMalloc dc");
       s.jw.stage = dmalloc<uint32_t>((size_t)kStageBytes / 4 * s.cap_canvases, "hipMalloc stage");
-      s.jw.tmp = dmalloc<uint8_t>((size_t)kOutCap * s.cap_canvases, "hipMalloc jpeg tmp");
+      s.jw.boff = dmalloc<uint32_t>(blocks * s.cap_canvases, "hipMalloc boff");
+      s.jw.total = dmalloc<uint32_t>(s.cap_canvases, "hipMalloc total");
+      s.jw.max_chunks = (int)(kStageBytes / kStuffChunk);
+      s.jw.chunk_ff = dmalloc<uint32_t>((size_t)s.jw.max_chunks * s.cap_canvases, "hipMalloc chunk_ff");
       check_hip(hipHostMalloc((void**)&s.h_out, (size_t)kOutCap * s.cap_canvases, hipHostMallocMapped),
                 "hipHostMalloc out");
       check_hip(hipHostGetDevicePointer((void**)&s.d_out, s.h_out, 0), "hipHostGetDevicePointer out");
@@ -267,6 +271,7 @@ struct Engine::Impl {
     auto* rd = reinterpret_cast<RenderDesc*>(hb + s.off_render);
     auto* jd = reinterpret_cast<JpegDesc*>(hb + s.off_jpeg);
     int nmed = 0, nshp = 0, nseed = 0, ncanv = 0;
+    s.any_canvas = false;
     uint32_t mask_off = 0;
     s.max_w = s.max_h = 0;
     const int cw = cfg.render.out_width, ch = cfg.render.out_height;
@@ -351,6 +356,10 @@ struct Engine::Impl {
       j.stage_words = kStageBytes / 4;
       j.out_off = (uint64_t)k * kOutCap;
       j.out_cap = kOutCap;
+      // Export runs render straight into the JPEG block kernel when the fit is an exact 2× (the
+      // canvas is never materialised); test runs keep canvases for inspection.
+      j.render = (mode == 0 && render_is_exact_2x(rd[k], cw, ch)) ? k : -1;
+      if (j.render < 0) s.any_canvas = true;
     }
     s.ncanvas = ncanv;
     if (nl == 0) return;
@@ -385,8 +394,14 @@ struct Engine::Impl {
     }
     launch_srg_morph(plane(kPBand), d_desc, nl, d_seeds, pc, o, s.max_w, s.max_h, s.stream);
     (void)d_stats_c;
-    launch_render(d_raw, s.d_f32, s.d_bits, d_stats, d_rd, ncanv, cw, ch, s.d_canvas, s.stream);
-    launch_jpeg(s.d_canvas, d_jd, ncanv, cw, ch, divs, s.jw, s.d_out, s.d_sizes, s.stream);
+    if (s.any_canvas) launch_render(d_raw, s.d_f32, s.d_bits, d_stats, d_rd, ncanv, cw, ch, s.d_canvas, s.stream);
+    JpegRenderSrc rsrc;
+    rsrc.raw = d_raw;
+    rsrc.f32 = s.d_f32;
+    rsrc.bits = s.d_bits;
+    rsrc.stats = d_stats;
+    rsrc.rd = d_rd;
+    launch_jpeg(s.d_canvas, d_jd, ncanv, cw, ch, divs, s.jw, s.d_out, s.d_sizes, s.stream, &rsrc);
     check_hip(hipEventRecord(s.ev2, s.stream), "event");
     check_hip(hipEventSynchronize(s.ev2), "batch sync");
     if (acc) {
@@ -403,6 +418,15 @@ struct Engine::Impl {
   bool jpeg_segment(Slot& s, int k, std::vector<uint8_t>& fallback, int64_t* fallbacks) {
     if (s.h_sizes[k] >= 0) return true;
     const int cw = cfg.render.out_width, ch = cfg.render.out_height;
+    if (!s.any_canvas) {
+      // Fused batches never materialised canvases: render them now (rare overflow path).
+      uint8_t* db = s.d_blob;
+      launch_render(reinterpret_cast<uint16_t*>(db + s.raw_base), s.d_f32, s.d_bits,
+                    reinterpret_cast<SliceStats*>(db + s.off_stats), reinterpret_cast<RenderDesc*>(db + s.off_render),
+                    s.ncanvas, cw, ch, s.d_canvas, s.stream);
+      check_hip(hipStreamSynchronize(s.stream), "fallback render");
+      s.any_canvas = true;
+    }
     std::vector<uint8_t> canvas((size_t)cw * ch);
     check_hip(hipMemcpy(canvas.data(), s.d_canvas + (size_t)k * cw * ch, canvas.size(), hipMemcpyDeviceToHost),
               "canvas D2H");
