@@ -43,7 +43,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--scaling", choices=("weak", "strong"), default="weak")
     ap.add_argument("--batch-size", type=int, default=64)
-    ap.add_argument("--streams", type=int, default=3)
+    ap.add_argument("--streams", type=int, default=6)
     ap.add_argument("--threads", type=int, default=16)
     ap.add_argument("--data-root", default=os.environ.get("NM03_BENCH_DATA", "/tmp/nm03_bench_data"))
     ap.add_argument("--out-root", default=os.environ.get("NM03_BENCH_OUT", "/tmp/nm03_bench_out"))

@@ -61,6 +61,7 @@ struct EngineConfig {
   PipelineParams pipe;
   RenderParams render;
   bool export_jpeg = true;
+  bool resume = false;  // skip items whose two JPEGs already exist (SURVEY §5.4 --resume)
 };
 
 // Everything test_pipeline exports / tests inspect for one slice (host copies).

@@ -48,6 +48,7 @@ class PipelineConfig:
     max_dim: int = 512
     device: int = 0
     export_jpeg: bool = True
+    resume: bool = False
 
     _PIPE = ("norm_low", "norm_high", "norm_min", "norm_max", "clip_min", "clip_max", "median_window",
              "sharpen_gain", "sharpen_sigma", "sharpen_mask", "srg_min", "srg_max", "srg_connectivity",
@@ -76,6 +77,7 @@ class PipelineConfig:
         c.pipe = self.pipeline_params()
         c.render = self.render_params()
         c.export_jpeg = self.export_jpeg
+        c.resume = self.resume
         return c
 
     def replace(self, **kw):

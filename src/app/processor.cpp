@@ -48,7 +48,10 @@ void usage(const std::string& which) {
             << "  --no-montage           test_pipeline: skip the 5-view montage JPEG\n"
             << "  --repeat N             process the cohort N times (benchmarking)\n"
             << "  --json FILE            write run metrics as JSON\n"
-            << "  --quiet                suppress per-slice progress lines\n";
+            << "  --resume               keep existing outputs; skip slices whose two JPEGs exist\n"
+            << "  --quiet                suppress per-slice progress lines\n"
+            << "env: NM03_DATA_ROOT, NM03_LOG=info|warn|error|none, NM03_ROCTX=1,\n"
+            << "     NM03_FAULT=corrupt_dicom:<i>,fail_batch:<k>,fail_write:<j>\n";
 }
 
 void write_json(const std::string& path, const std::string& body) {
@@ -136,6 +139,7 @@ AppConfig parse_args(int argc, char** argv, const std::string& which) {
     else if (a == "--json") c.json = val();
     else if (a == "--quiet") c.quiet = true;
     else if (a == "--max-dim") c.engine.max_dim = std::atoi(val().c_str());
+    else if (a == "--resume") c.engine.resume = true;
     else {
       std::cerr << "unknown option " << a << " (see --help)" << std::endl;
       std::exit(2);
@@ -178,7 +182,10 @@ int run_sequential(const AppConfig& cfg) {
             std::cout << "\n=== Processing Patient: " << pid << " ===\n" << std::endl;  // :276
             const std::string out = cfg.out_dir + "/" + pid;
             try {
-              cohort::setup_output_dir(out);
+              if (cfg.engine.resume)
+                cohort::make_dirs(out);
+              else
+                cohort::setup_output_dir(out);
             } catch (const std::exception& e) {
               throw std::runtime_error(std::string("Error setting up output directory: ") + e.what());
             }
@@ -318,7 +325,10 @@ int parallel_rank(const AppConfig& cfg, int rank, int size, Comm& comm) {
           p.id = pid;
           p.out_dir = cfg.out_dir + "/" + pid;
           try {
-            cohort::setup_output_dir(p.out_dir);
+            if (cfg.engine.resume)
+              cohort::make_dirs(p.out_dir);
+            else
+              cohort::setup_output_dir(p.out_dir);
             p.setup_ok = true;
             cohort::Series s = cohort::list_patient_series(base, pid);
             p.series_dir = s.series_dir;

@@ -234,7 +234,8 @@ PYBIND11_MODULE(_nm03, m) {
       .def_readwrite("max_dim", &EngineConfig::max_dim)
       .def_readwrite("pipe", &EngineConfig::pipe)
       .def_readwrite("render", &EngineConfig::render)
-      .def_readwrite("export_jpeg", &EngineConfig::export_jpeg);
+      .def_readwrite("export_jpeg", &EngineConfig::export_jpeg)
+      .def_readwrite("resume", &EngineConfig::resume);
 
   m.def("reference_seeds", [](int w, int h) {
     std::vector<std::pair<int, int>> v;

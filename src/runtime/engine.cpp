@@ -2,6 +2,7 @@
 #include "nm03/engine.h"
 
 #include <hip/hip_runtime_api.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <atomic>
@@ -15,6 +16,7 @@
 #include "nm03/gpu_types.h"
 #include "nm03/jpeg.h"
 #include "nm03/kernels.h"
+#include "nm03/log.h"
 #include "nm03/thread_pool.h"
 
 namespace nm03 {
@@ -141,6 +143,9 @@ struct Engine::Impl {
     check_hip(hipSetDevice(cfg.device), "hipSetDevice");
     pool = std::make_unique<ThreadPool>(cfg.threads);
     for (int i = 0; i < cfg.streams; ++i) slots.push_back(make_slot());
+    log_info("engine on device " + std::to_string(cfg.device) + ": batch " + std::to_string(cfg.batch_size) + ", " +
+             std::to_string(cfg.streams) + " streams, " + std::to_string(cfg.threads) + " host threads, max_dim " +
+             std::to_string(cfg.max_dim));
   }
 
   ~Impl() {
@@ -215,11 +220,13 @@ struct Engine::Impl {
   }
 
   // ---- loading -------------------------------------------------------------------------------
-  void load_into(Slot& s, int i, const std::string& path, SliceStatus& st, std::atomic<int64_t>& load_ns,
-                 std::atomic<int64_t>& bytes_in) {
+  void load_into(Slot& s, int i, size_t item, const std::string& path, SliceStatus& st,
+                 std::atomic<int64_t>& load_ns, std::atomic<int64_t>& bytes_in) {
     thread_local std::vector<uint8_t> buf;
+    TraceRange tr("nm03.load");
     const double t0 = now_s();
     try {
+      if (fault_plan().corrupt_dicom == (int64_t)item) throw SliceError("injected fault: corrupt DICOM data");
       const size_t n = dicom::read_file_into(path, buf);
       dicom::Header h = dicom::parse(buf.data(), n);
       const int md = cfg.pipe.min_dim;
@@ -256,6 +263,11 @@ struct Engine::Impl {
       st.message = e.what();
     }
     load_ns += (int64_t)((now_s() - t0) * 1e9);
+  }
+
+  static bool outputs_exist(const WorkItem& w) {
+    const std::string base = cohort::with_slash(w.out_dir) + cohort::stem(w.path);
+    return access((base + "_original.jpg").c_str(), F_OK) == 0 && access((base + "_processed.jpg").c_str(), F_OK) == 0;
   }
 
   // ---- descriptor build + GPU enqueue --------------------------------------------------------
@@ -447,7 +459,11 @@ struct Engine::Impl {
       for (size_t i = 0; i < count; ++i) {
         tg.run([&, i] {
           if (on_start) on_start(first + i);
-          load_into(s, (int)i, items[first + i].path, status[first + i], load_ns, bytes_in);
+          if (cfg.resume && outputs_exist(items[first + i])) {
+            status[first + i] = SliceStatus{kSliceOk, "resumed: outputs already present"};
+            return;
+          }
+          load_into(s, (int)i, first + i, items[first + i].path, status[first + i], load_ns, bytes_in);
         });
       }
       tg.wait();
@@ -459,6 +475,9 @@ struct Engine::Impl {
     int64_t fallbacks = 0;
     if (!s.live.empty()) {
       try {
+        TraceRange tr("nm03.gpu_batch");
+        if (fault_plan().fail_batch == (int64_t)(first / (size_t)cfg.batch_size))
+          throw DeviceError("injected fault: device batch failure");
         build_and_run(s, 0, &local);
       } catch (const std::exception& e) {
         for (int i : s.live) status[first + i] = SliceStatus{kSliceDeviceError, e.what()};
@@ -483,7 +502,9 @@ struct Engine::Impl {
         if (status[item].code != kSliceOk) continue;
         tg.run([&, c, item] {
           const double t0 = now_s();
+          TraceRange tr("nm03.export");
           try {
+            if (fault_plan().fail_write == (int64_t)item) throw std::runtime_error("injected fault: export failure");
             const std::string base = cohort::with_slash(items[item].out_dir) + cohort::stem(items[item].path);
             for (int k = 0; k < 2; ++k) {
               const int cv = 2 * c + k;
@@ -543,6 +564,9 @@ struct Engine::Impl {
     if (err) std::rethrow_exception(err);
     for (const auto& st : status) (st.code == kSliceOk ? acc.slices_ok : acc.slices_failed) += 1;
     acc.wall_s = now_s() - t0;
+    if (acc.jpeg_fallbacks) log_warn(std::to_string(acc.jpeg_fallbacks) + " JPEG(s) exceeded GPU capacity; CPU-encoded");
+    log_info("run: " + std::to_string(items.size()) + " slices in " + std::to_string(acc.batches) + " batches, " +
+             std::to_string(acc.wall_s * 1e3) + " ms, " + std::to_string(acc.slices_failed) + " failed");
     if (times) *times = acc;
     return status;
   }

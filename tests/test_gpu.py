@@ -311,3 +311,43 @@ def test_volume_vs_golden(native, conn):
     assert np.array_equal(res["region"], region)
     assert np.array_equal(res["dilated"], dil)
     assert res["sweeps"] >= 1
+
+
+# ---------------------------------------------------------------------------------------------
+# Fault injection / resume / log levels
+# ---------------------------------------------------------------------------------------------
+def test_fault_injection_isolated(native, cohort_root, tmp_path):
+    import re
+    base = native.cohort_dir(cohort_root)
+    n_items = sum(len(native.list_patient_series(base, p)[1]) for p in native.find_patient_dirs(base))
+    r = run_bin("img_processing_parallel", "--data-root", cohort_root, "--out", str(tmp_path / "o"), "--batch-size", "4",
+                env={"NM03_FAULT": "corrupt_dicom:1,fail_batch:2,fail_write:0"})
+    assert r.returncode == 0, r.stderr
+    assert "injected fault: corrupt DICOM data" in r.stderr
+    assert "injected fault: device batch failure" in r.stderr
+    assert "Error in export stage: injected fault: export failure" in r.stderr
+    ok = sum(int(m) for m in re.findall(r"Successfully processed (\d+)/\d+ images", r.stdout))
+    assert ok == n_items - 6  # item 0 (export), item 1 (load), batch 2 = items 8..11
+    assert "Successfully processed 4/4 patients." in r.stdout
+
+
+def test_resume_keeps_existing(native, cohort_root, tmp_path):
+    out = tmp_path / "o"
+    assert run_bin("img_processing_parallel", "--data-root", cohort_root, "--out", str(out)).returncode == 0
+    files = sorted(out.rglob("*.jpg"))
+    victim = files[3]
+    victim.unlink()
+    key = (victim.parent, victim.name.rsplit("_", 1)[0])  # the slice whose pair gets re-exported
+    keep = {f: f.stat().st_mtime_ns for f in files if (f.parent, f.name.rsplit("_", 1)[0]) != key}
+    r = run_bin("img_processing_parallel", "--data-root", cohort_root, "--out", str(out), "--resume")
+    assert r.returncode == 0, r.stderr
+    assert victim.exists()
+    assert all(f.stat().st_mtime_ns == t for f, t in keep.items())
+
+
+def test_log_levels(native, cohort_root, tmp_path):
+    r = run_bin("img_processing_parallel", "--data-root", cohort_root, "--out", str(tmp_path / "a"), "--quiet",
+                env={"NM03_LOG": "info"})
+    assert r.returncode == 0 and "[nm03 INFO] engine on device 0" in r.stdout
+    r = run_bin("img_processing_parallel", "--data-root", cohort_root, "--out", str(tmp_path / "b"), "--quiet")
+    assert r.returncode == 0 and "[nm03 INFO]" not in r.stdout

@@ -1,0 +1,67 @@
+#!/usr/bin/env python3
+"""Engine configuration sweep on one GPU (one process, one torch import): batch size × streams ×
+host threads on the synthetic T1+C cohort, plus a pinned-H2D bandwidth probe. One JSON per line.
+
+    python tools/sweep_engine.py [--steps 8] [--grid "32,64,128:2,3,4,6:16,24"]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+import nm03_capstone_project_amd as nm  # noqa: E402
+from nm03_capstone_project_amd.parallel import plan_cohort  # noqa: E402
+
+
+def h2d_probe(mb=64, reps=10):
+    x = torch.empty(mb << 20, dtype=torch.uint8).pin_memory()
+    y = torch.empty_like(x, device="cuda")
+    y.copy_(x, non_blocking=True)
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    for _ in range(reps):
+        y.copy_(x, non_blocking=True)
+    torch.cuda.synchronize()
+    return mb * reps / 1024 / (time.perf_counter() - t)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=8)
+    ap.add_argument("--grid", default="32,64,128:2,3,4,6:16,24")
+    ap.add_argument("--data-root", default="/tmp/nm03_bench_data")
+    ap.add_argument("--out-root", default="/tmp/nm03_sweep_out")
+    a = ap.parse_args()
+    n = nm.native()
+    if not os.path.exists(os.path.join(a.data_root, ".complete")):
+        n.synth_cohort(a.data_root, threads=16)
+        open(os.path.join(a.data_root, ".complete"), "w").close()
+    print(json.dumps({"h2d_pinned_GBps": round(h2d_probe(), 2)}), flush=True)
+    items = plan_cohort(a.data_root, a.out_root).items
+    bs, ss, ts = (list(map(int, g.split(","))) for g in a.grid.split(":"))
+    for b in bs:
+        for s in ss:
+            for t in ts:
+                cfg = nm.PipelineConfig(batch_size=b, streams=s, threads=t)
+                eng = n.Engine(cfg.engine_config())
+                for _ in range(2):
+                    eng.run(items)
+                t0 = time.perf_counter()
+                agg = {"load_s": 0.0, "h2d_s": 0.0, "kernels_s": 0.0, "write_s": 0.0}
+                for _ in range(a.steps):
+                    st, tm = eng.run(items)
+                    for k in agg:
+                        agg[k] += tm[k]
+                dt = (time.perf_counter() - t0) / a.steps
+                print(json.dumps({"batch": b, "streams": s, "threads": t, "ms_per_step": round(dt * 1e3, 3),
+                                  "slices_per_s": round(len(items) / dt, 1),
+                                  **{k: round(v / a.steps * 1e3, 3) for k, v in agg.items()}}), flush=True)
+                del eng
+
+
+if __name__ == "__main__":
+    main()
