@@ -129,13 +129,17 @@ NM03_HD float render_src_coord(int u, float o, float inv) {
   return t * inv;
 }
 
-NM03_HD uint8_t gray_u8(float v, float lo, float hi) {
-  float r = hi - lo;
-  float g = 0.0f;
-  if (r > 0.0f) {
-    g = v - lo;
-    g = g / r;
-  }
+// Window mapping of the gray renderers: g = (v - lo) * inv, inv = 1/(hi - lo) computed once per
+// image (window_inv). FAST's GLSL shader divides per fragment, which GLSL does not round correctly
+// anyway; a per-image reciprocal is the contract here (golden, kernels and torch reference agree).
+NM03_HD float window_inv(float lo, float hi) {
+  const float r = hi - lo;
+  return r > 0.0f ? 1.0f / r : 0.0f;
+}
+
+NM03_HD uint8_t gray_u8(float v, float lo, float inv) {
+  float g = v - lo;
+  g = g * inv;
   g = g < 0.0f ? 0.0f : g;
   g = g > 1.0f ? 1.0f : g;
   float t = g * 255.0f;

@@ -101,7 +101,8 @@ def render_gray(values, lo, hi, out_w=512, out_h=512):
     top = (1 - wx) * a + wx * b
     bot = (1 - wx) * c + wx * d
     val = (1 - wy)[:, None] * top + wy[:, None] * bot
-    g = ((val - lo) / (hi - lo)).clamp(0, 1) if hi > lo else torch.zeros_like(val)
+    inv = torch.tensor(1.0, dtype=torch.float32) / torch.tensor(hi - lo, dtype=torch.float32) if hi > lo else torch.tensor(0.0)
+    g = ((val - lo) * inv.to(val.device)).clamp(0, 1)
     out = torch.floor(g * 255 + 0.5).to(torch.uint8)
     inside = ((sx >= 0) & (sx < w))[None, :] & ((sy >= 0) & (sy < h))[:, None]
     return torch.where(inside, out, torch.zeros_like(out))

@@ -295,6 +295,7 @@ std::vector<uint8_t> dilate3d(const std::vector<uint8_t>& m, int w, int h, int d
 
 std::vector<uint8_t> render_gray(const std::vector<float>& v, const RenderGeom& g, float lo, float hi) {
   std::vector<uint8_t> out((size_t)g.out_w * g.out_h, 0);
+  const float inv = window_inv(lo, hi);
   for (int u = 0; u < g.out_h; ++u) {
     const float sy = render_src_coord(u, g.oy, g.invy);
     if (!(sy >= 0.0f && sy < (float)g.src_h)) continue;
@@ -311,7 +312,7 @@ std::vector<uint8_t> render_gray(const std::vector<float>& v, const RenderGeom& 
       const int x0 = clampi((int)x0f, 0, g.src_w - 1), x1 = clampi((int)x0f + 1, 0, g.src_w - 1);
       const float val = bilerp(v[(size_t)y0 * g.src_w + x0], v[(size_t)y0 * g.src_w + x1], v[(size_t)y1 * g.src_w + x0],
                                v[(size_t)y1 * g.src_w + x1], wx, wy);
-      out[(size_t)u * g.out_w + t] = gray_u8(val, lo, hi);
+      out[(size_t)u * g.out_w + t] = gray_u8(val, lo, inv);
     }
   }
   return out;

@@ -43,6 +43,10 @@ __device__ __forceinline__ uint32_t hlen(uint32_t e) { return e >> 16; }
 __global__ __launch_bounds__(256) void jpeg_block_kernel(const uint8_t* __restrict__ canvas,
                                                          const JpegDesc* __restrict__ jd, int ncanvas, int out_w,
                                                          int out_h, QuantRecip q, JpegWork w, JpegRenderSrc rs) {
+  // AC code lengths in LDS: 63 per-lane lookups per block become ds_read_u8 instead of gathers.
+  __shared__ uint8_t aclen[256];
+  aclen[threadIdx.x] = (uint8_t)hlen(kHuffAcLuma.e[threadIdx.x]);
+  __syncthreads();
   const int bpi = (out_w >> 3) * (out_h >> 3);
   const int gid = blockIdx.x * blockDim.x + threadIdx.x;
   if (gid >= bpi * ncanvas) return;
@@ -90,13 +94,13 @@ __global__ __launch_bounds__(256) void jpeg_block_kernel(const uint8_t* __restri
       ++run;
     } else {
       nz |= 1ull << k;
-      bits += (uint32_t)(run >> 4) * hlen(kHuffAcLuma.e[0xF0]);
+      bits += (uint32_t)(run >> 4) * aclen[0xF0];
       const int n = mag_bits_fast(v);
-      bits += hlen(kHuffAcLuma.e[((run & 15) << 4) + n]) + (uint32_t)n;
+      bits += aclen[((run & 15) << 4) + n] + (uint32_t)n;
       run = 0;
     }
   }
-  if (run) bits += hlen(kHuffAcLuma.e[0x00]);
+  if (run) bits += aclen[0x00];
   const size_t bi = (size_t)d.coef_off + b;
   uint4* dst = reinterpret_cast<uint4*>(w.coef + bi * 64);
 #pragma unroll
@@ -189,6 +193,11 @@ struct GBitWriter {
 
 __global__ __launch_bounds__(256) void jpeg_emit_kernel(const JpegDesc* __restrict__ jd, int ncanvas, int bpi,
                                                         JpegWork w) {
+  __shared__ uint32_t actab[256];
+  __shared__ uint32_t dctab[16];
+  actab[threadIdx.x] = kHuffAcLuma.e[threadIdx.x];
+  if (threadIdx.x < 16) dctab[threadIdx.x] = kHuffDcLuma.e[threadIdx.x];
+  __syncthreads();
   const int gid = blockIdx.x * blockDim.x + threadIdx.x;
   if (gid >= bpi * ncanvas) return;
   const int img = gid / bpi, b = gid - img * bpi;
@@ -199,7 +208,7 @@ __global__ __launch_bounds__(256) void jpeg_emit_kernel(const JpegDesc* __restri
   GBitWriter bw(w.stage + d.stage_off, w.boff[bi]);
   const int diff = (int)dc[b] - (b ? (int)dc[b - 1] : 0);
   const int n = mag_bits_fast(diff);
-  bw.put_sym(kHuffDcLuma.e[n]);
+  bw.put_sym(dctab[n]);
   if (n) bw.put((uint32_t)(diff < 0 ? diff - 1 : diff), n);
   uint64_t nz = w.nzmask[bi] & ~1ull;
   const int16_t* cf = w.coef + bi * 64;
@@ -209,16 +218,16 @@ __global__ __launch_bounds__(256) void jpeg_emit_kernel(const JpegDesc* __restri
     nz &= nz - 1;
     int run = k - last - 1;
     while (run > 15) {
-      bw.put_sym(kHuffAcLuma.e[0xF0]);
+      bw.put_sym(actab[0xF0]);
       run -= 16;
     }
     const int v = cf[k];
     const int nb = mag_bits_fast(v);
-    bw.put_sym(kHuffAcLuma.e[(run << 4) + nb]);
+    bw.put_sym(actab[(run << 4) + nb]);
     bw.put((uint32_t)(v < 0 ? v - 1 : v), nb);
     last = k;
   }
-  if (last < 63) bw.put_sym(kHuffAcLuma.e[0x00]);
+  if (last < 63) bw.put_sym(actab[0x00]);
   bw.flush();
 }
 

@@ -12,7 +12,7 @@
 namespace nm03::gpu {
 
 struct RWindow {
-  float lo, hi;
+  float lo, inv;  // window start and 1/(hi-lo) (pixel_math.h window_inv)
 };
 
 __device__ __forceinline__ RWindow render_window(const RenderDesc& d, const SliceStats* stats) {
@@ -20,9 +20,11 @@ __device__ __forceinline__ RWindow render_window(const RenderDesc& d, const Slic
   if (d.kind == kRenderRawGray) {
     const float a = rescaled_value((uint16_t)st.key_min, d.type, d.slope, d.intercept);
     const float b = rescaled_value((uint16_t)st.key_max, d.type, d.slope, d.intercept);
-    return {fminf(a, b), fmaxf(a, b)};
+    const float lo = fminf(a, b), hi = fmaxf(a, b);
+    return {lo, window_inv(lo, hi)};
   }
-  return {ordered_to_float(st.s_min), ordered_to_float(st.s_max)};
+  const float lo = ordered_to_float(st.s_min), hi = ordered_to_float(st.s_max);
+  return {lo, window_inv(lo, hi)};
 }
 
 // Source value for gray renders at clamped (x, y).
@@ -60,7 +62,7 @@ __device__ __forceinline__ uint32_t render_pixel(const RenderDesc& d, const uint
   const int x0 = clampi((int)x0f, 0, W - 1), x1 = clampi((int)x0f + 1, 0, W - 1);
   const float a = render_src_value(d, raw, f32, x0, y0), b = render_src_value(d, raw, f32, x1, y0);
   const float c = render_src_value(d, raw, f32, x0, y1), e = render_src_value(d, raw, f32, x1, y1);
-  return gray_u8(bilerp(a, b, c, e, wx, wy), win.lo, win.hi);
+  return gray_u8(bilerp(a, b, c, e, wx, wy), win.lo, win.inv);
 }
 
 // Fused 2× render of the 8×8 canvas block (bx, by) into px[64] (row-major), for a RenderDesc
@@ -94,24 +96,26 @@ __device__ __forceinline__ void render_block_2x(const RenderDesc& d, const uint1
 #pragma unroll
     for (int i = 0; i < 6; ++i) patch[j][i] = render_src_value(d, raw, f32, clampi(sx0 + i, 0, W - 1), y);
   }
+  // Per-column and per-row interpolation weights (same expressions as render_pixel, hoisted).
+  float wxs[8], wys[8];
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    const float fx = render_src_coord(bx * 8 + c, d.ox, d.invx) - 0.5f;
+    wxs[c] = fx - floorf(fx);
+    const float fy = render_src_coord(by * 8 + c, d.oy, d.invy) - 0.5f;
+    wys[c] = fy - floorf(fy);
+  }
+  // For an exact 2× fit floor(f) - (4b-1) == (k+1)/2; the compile-time index keeps the patch in
+  // registers (a float-derived index would force it to scratch). The weights stay float-derived.
 #pragma unroll
   for (int r = 0; r < 8; ++r) {
-    const float sy = render_src_coord(by * 8 + r, d.oy, d.invy);
-    const float fy = sy - 0.5f;
-    const float y0f = floorf(fy);
-    const float wy = fy - y0f;
-    // For an exact 2× fit floor(fy) - sy0 == (r+1)/2; using the compile-time form keeps the patch
-    // in registers (a float-derived index would force it to scratch). Weights stay float-derived.
     const int j0 = (r + 1) >> 1;
 #pragma unroll
     for (int c = 0; c < 8; ++c) {
-      const float sx = render_src_coord(bx * 8 + c, d.ox, d.invx);
-      const float fx = sx - 0.5f;
-      const float x0f = floorf(fx);
-      const float wx = fx - x0f;
       const int i0 = (c + 1) >> 1;
-      const float val = bilerp(patch[j0][i0], patch[j0][i0 + 1], patch[j0 + 1][i0], patch[j0 + 1][i0 + 1], wx, wy);
-      px[r * 8 + c] = (int32_t)gray_u8(val, win.lo, win.hi);
+      const float val =
+          bilerp(patch[j0][i0], patch[j0][i0 + 1], patch[j0 + 1][i0], patch[j0 + 1][i0 + 1], wxs[c], wys[r]);
+      px[r * 8 + c] = (int32_t)gray_u8(val, win.lo, win.inv);
     }
   }
 }

@@ -14,3 +14,6 @@ timeout -k 10 300 python bench.py --steps 10 --warmup 2 > gpurun_out/bench.log 2
 echo "bench ok $(date)" >> $P
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_iter -o bench -- python3 bench.py --steps 3 --warmup 1 > gpurun_out/prof_iter.log 2>&1 || exit 32
 echo "done $(date)" >> $P
+build/bin/nm03_synth --data-root /tmp/vol/ --patients 1 --min-slices 256 --max-slices 256 --threads 16 > /dev/null || exit 33
+timeout -k 10 300 build/bin/nm03_bench --config volume --data-root /tmp/vol/ --steps 3 --warmup 1 > gpurun_out/volume.log 2>&1 || exit 34
+echo "volume ok $(date)" >> $P
