@@ -36,6 +36,30 @@ METRIC = "DICOM slices/sec through full pipeline (T1+C cohort) at 1/2/4/8 MI355X
 BASELINE_SLICES_PER_S = None  # the reference publishes no number
 
 
+class _roctx_range:
+    """roctx range for rocprofv3 --marker-trace timelines (tools/timeline.py); no-op unless NM03_ROCTX=1."""
+    _lib = None
+
+    def __init__(self, name):
+        self.name = name.encode()
+        if _roctx_range._lib is None:
+            _roctx_range._lib = False
+            if os.environ.get("NM03_ROCTX", "0") not in ("", "0"):
+                import ctypes
+                try:
+                    _roctx_range._lib = ctypes.CDLL("librocprofiler-sdk-roctx.so.1")
+                except OSError:
+                    pass
+
+    def __enter__(self):
+        if self._lib:
+            self._lib.roctxRangePushA(self.name)
+
+    def __exit__(self, *exc):
+        if self._lib:
+            self._lib.roctxRangePop()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -48,6 +72,7 @@ def main():
     ap.add_argument("--data-root", default=os.environ.get("NM03_BENCH_DATA", "/tmp/nm03_bench_data"))
     ap.add_argument("--out-root", default=os.environ.get("NM03_BENCH_OUT", "/tmp/nm03_bench_out"))
     ap.add_argument("--keep-output", action="store_true")
+    ap.add_argument("--graphs", action="store_true", help="hipGraph replay of the per-batch kernel chain")
     args = ap.parse_args()
 
     ctx = init_from_env()
@@ -70,7 +95,7 @@ def main():
     mine = items[lo:hi]
 
     cfg = nm.PipelineConfig(batch_size=args.batch_size, streams=args.streams, threads=args.threads,
-                            device=ctx.local_rank)
+                            device=ctx.local_rank, graphs=args.graphs)
     engine = n.Engine(cfg.engine_config())
     for _ in range(args.warmup):
         st, _ = engine.run(mine)
@@ -84,7 +109,8 @@ def main():
     ok = 0
     stage = {"load_s": 0.0, "h2d_s": 0.0, "kernels_s": 0.0, "write_s": 0.0}
     for _ in range(args.steps):
-        st, times = engine.run(mine)
+        with _roctx_range("bench.step"):
+            st, times = engine.run(mine)
         ok += sum(1 for s in st if s[0] == 0)
         for k in stage:
             stage[k] += times[k]

@@ -62,6 +62,12 @@ struct EngineConfig {
   RenderParams render;
   bool export_jpeg = true;
   bool resume = false;  // skip items whose two JPEGs already exist (SURVEY §5.4 --resume)
+  // Replay each slot's per-batch kernel chain from a captured hipGraph (one graph per launch
+  // signature). Ignored (eager launches) when NM03_SYNC_LAUNCHES debugging is on. Off by default:
+  // measured on MI355X/ROCm 7.2 with 6 slots, replay ran at 85k slices/s vs 110k eager
+  // (profiles/graphs_ab.txt) — the chain is only 8 launches per 64 slices, so there is no launch
+  // overhead to win and graph launches lose cross-stream overlap.
+  bool graphs = false;
 };
 
 // Everything test_pipeline exports / tests inspect for one slice (host copies).

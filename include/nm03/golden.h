@@ -86,4 +86,11 @@ struct SliceJpegs {
 };
 SliceJpegs export_jpegs(const SliceInput& s, const SliceResult& r, const PipelineParams& p, const RenderParams& rp);
 
+// test_pipeline's five stage images (test_pipeline.cpp:164-179): original, preprocessed,
+// segmentation, erosion, dilation — canvases and their JPEG files.
+struct StageImages {
+  std::vector<std::vector<uint8_t>> canvases, jpegs;
+};
+StageImages test_pipeline_images(const SliceInput& s, const PipelineParams& p, const RenderParams& rp);
+
 }  // namespace nm03::golden

@@ -13,6 +13,8 @@ namespace nm03::gpu {
 
 void check_hip(hipError_t e, const char* what);
 void check_launch(const char* what);
+// NM03_SYNC_LAUNCHES=1: synchronise after every launch (debugging; disables graph capture).
+bool sync_launches();
 
 // K1a: k×k median of raw keys → `med` (u16 keys, same layout as raw). k ∈ {3,5,7,9}.
 void launch_median(const uint16_t* raw, uint16_t* med, const SliceDesc* descs, const TileDesc* tiles, int ntiles,

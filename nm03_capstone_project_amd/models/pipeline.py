@@ -49,6 +49,7 @@ class PipelineConfig:
     device: int = 0
     export_jpeg: bool = True
     resume: bool = False
+    graphs: bool = False  # replay per-batch kernel chains from captured hipGraphs (slower, see engine.h)
 
     _PIPE = ("norm_low", "norm_high", "norm_min", "norm_max", "clip_min", "clip_max", "median_window",
              "sharpen_gain", "sharpen_sigma", "sharpen_mask", "srg_min", "srg_max", "srg_connectivity",
@@ -78,6 +79,7 @@ class PipelineConfig:
         c.render = self.render_params()
         c.export_jpeg = self.export_jpeg
         c.resume = self.resume
+        c.graphs = self.graphs
         return c
 
     def replace(self, **kw):

@@ -480,16 +480,9 @@ int run_test_pipeline(const AppConfig& cfg) {
     std::vector<std::vector<uint8_t>> canvases, jpegs;
     const double t0 = now_s();
     if (cfg.cpu) {
-      golden::SliceResult r = golden::run(in, p, true);
-      const RenderGeom g = make_render_geom(in.w, in.h, in.spacing_x, in.spacing_y, rp.out_width, rp.out_height);
-      const uint8_t fill = opacity_u8(rp.label_opacity), bv = opacity_u8(rp.border_opacity);
-      auto mm = std::minmax_element(r.sharpened.begin(), r.sharpened.end());
-      canvases.push_back(golden::render_gray(golden::rescaled(in, p), g, r.window_lo, r.window_hi));
-      canvases.push_back(golden::render_gray(r.sharpened, g, *mm.first, *mm.second));
-      canvases.push_back(golden::render_labels(r.region, golden::border(r.region, in.w, in.h, rp.border_radius), g, fill, bv));
-      canvases.push_back(golden::render_labels(r.eroded, golden::border(r.eroded, in.w, in.h, rp.border_radius), g, fill, bv));
-      canvases.push_back(golden::render_labels(r.dilated, golden::border(r.dilated, in.w, in.h, rp.border_radius), g, fill, bv));
-      for (auto& c : canvases) jpegs.push_back(jpeg::encode_gray420(c.data(), rp.out_width, rp.out_height, rp.out_width, rp.jpeg_quality));
+      golden::StageImages r = golden::test_pipeline_images(in, p, rp);
+      canvases = std::move(r.canvases);
+      jpegs = std::move(r.jpegs);
     } else {
       EngineConfig ec = cfg.engine;
       ec.batch_size = 1;

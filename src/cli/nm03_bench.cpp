@@ -6,9 +6,15 @@
 //                            structure — per patient, batches of ≤25 slices over 16 threads
 //                            (#pragma omp parallel for, main_parallel.cpp:336), then a SERIAL
 //                            export of the batch (render + JPEG + write, main_parallel.cpp:346)
+//   --config volume-cpu      config 5 on the golden CPU model (per-slice preprocessing on the
+//                            thread pool, then 3D SRG + cube dilation)
+//   --config single          config 1: test_pipeline's single slice (all stages + 5 renders +
+//                            5 JPEGs, test_pipeline.cpp:29-182) on the GPU, latency per slice
+//   --config single-cpu      config 1 on the golden CPU model
 #include <chrono>
 #include <cstdlib>
 #include <iostream>
+#include <memory>
 #include <string>
 
 #include "nm03/cohort.h"
@@ -146,6 +152,78 @@ int main(int argc, char** argv) {
       std::cout << "{\"config\": \"volume\", \"dims\": [" << v.w << ", " << v.h << ", " << v.d << "], \"steps\": " << steps
                 << ", \"ms_per_volume\": " << dt * 1e3 / steps << ", \"gpu_ms_per_volume\": " << ks * 1e3 / steps
                 << ", \"sweeps\": " << sweeps << "}" << std::endl;
+    } else if (config == "volume-cpu") {
+      if (pids.empty()) throw std::runtime_error("no patients");
+      auto s = nm03::cohort::list_patient_series(base, pids[0]);
+      nm03::ThreadPool pool(ec.threads);
+      auto one = [&]() -> size_t {
+        nm03::VolumeInput v = nm03::load_volume(s.files);
+        const size_t plane = (size_t)v.w * v.h;
+        std::vector<uint8_t> band(plane * v.d);
+        {
+          nm03::TaskGroup tg(pool);
+          for (int z = 0; z < v.d; ++z)
+            tg.run([&, z] {
+              nm03::golden::SliceInput si;
+              si.w = v.w;
+              si.h = v.h;
+              si.type = v.type;
+              si.stored_bits = v.stored_bits;
+              si.slope = v.slope;
+              si.intercept = v.intercept;
+              si.raw.assign(v.raw.begin() + z * plane, v.raw.begin() + (z + 1) * plane);
+              auto c = nm03::golden::norm_clip(si, ec.pipe);
+              auto m = nm03::golden::median(c, v.w, v.h, ec.pipe.median_window);
+              auto sh = nm03::golden::sharpen(m, v.w, v.h, ec.pipe.sharpen_gain, ec.pipe.sharpen_sigma,
+                                              ec.pipe.sharpen_mask);
+              auto b = nm03::golden::band(sh, ec.pipe.srg_min, ec.pipe.srg_max);
+              std::copy(b.begin(), b.end(), band.begin() + z * plane);
+            });
+          tg.wait();
+        }
+        auto seeds = nm03::reference_seeds(v.w, v.h);
+        for (auto& sd : seeds) sd.z = v.d / 2;
+        auto region = nm03::golden::region_grow3d(band, v.w, v.h, v.d, seeds, 6);
+        auto dil = nm03::golden::dilate3d(region, v.w, v.h, v.d, dil3d);
+        size_t n = 0;
+        for (uint8_t x : dil) n += x;
+        return n;
+      };
+      for (int w = 0; w < warmup; ++w) one();
+      const double t0 = now_s();
+      size_t vox = 0;
+      for (int k = 0; k < steps; ++k) vox = one();
+      const double dt = now_s() - t0;
+      std::cout << "{\"config\": \"volume-cpu\", \"threads\": " << ec.threads << ", \"slices\": " << s.files.size()
+                << ", \"steps\": " << steps << ", \"ms_per_volume\": " << dt * 1e3 / steps
+                << ", \"dilated_voxels\": " << vox << "}" << std::endl;
+    } else if (config == "single" || config == "single-cpu") {
+      const bool cpu = config == "single-cpu";
+      const std::string f = nm03::cohort::test_slice_path(root);
+      std::unique_ptr<nm03::Engine> eng;
+      if (!cpu) {
+        ec.streams = 1;
+        eng = std::make_unique<nm03::Engine>(ec);
+      }
+      auto one = [&] {
+        nm03::golden::SliceInput si = nm03::golden::load_slice(f, 0);
+        size_t n = 0;
+        if (cpu) {
+          auto r = nm03::golden::test_pipeline_images(si, ec.pipe, ec.render);
+          for (auto& j : r.jpegs) n += j.size();
+          return n;
+        }
+        auto r = eng->run_single(si);
+        for (auto& j : r.jpegs) n += j.size();
+        return n;
+      };
+      for (int w = 0; w < warmup; ++w) one();
+      const double t0 = now_s();
+      size_t bytes = 0;
+      for (int k = 0; k < steps; ++k) bytes = one();
+      const double dt = now_s() - t0;
+      std::cout << "{\"config\": \"" << config << "\", \"steps\": " << steps
+                << ", \"ms_per_slice\": " << dt * 1e3 / steps << ", \"jpeg_bytes\": " << bytes << "}" << std::endl;
     } else {
       throw std::runtime_error("unknown config " + config);
     }

@@ -364,4 +364,21 @@ SliceJpegs export_jpegs(const SliceInput& s, const SliceResult& r, const Pipelin
   return j;
 }
 
+StageImages test_pipeline_images(const SliceInput& in, const PipelineParams& p, const RenderParams& rp) {
+  StageImages out;
+  SliceResult r = run(in, p, true);
+  const RenderGeom g = make_render_geom(in.w, in.h, in.spacing_x, in.spacing_y, rp.out_width, rp.out_height);
+  const uint8_t fill = opacity_u8(rp.label_opacity), bv = opacity_u8(rp.border_opacity);
+  auto mm = std::minmax_element(r.sharpened.begin(), r.sharpened.end());
+  auto& c = out.canvases;
+  c.push_back(render_gray(rescaled(in, p), g, r.window_lo, r.window_hi));
+  c.push_back(render_gray(r.sharpened, g, *mm.first, *mm.second));
+  c.push_back(render_labels(r.region, border(r.region, in.w, in.h, rp.border_radius), g, fill, bv));
+  c.push_back(render_labels(r.eroded, border(r.eroded, in.w, in.h, rp.border_radius), g, fill, bv));
+  c.push_back(render_labels(r.dilated, border(r.dilated, in.w, in.h, rp.border_radius), g, fill, bv));
+  for (auto& cv : c) out.jpegs.push_back(jpeg::encode_gray420(cv.data(), rp.out_width, rp.out_height, rp.out_width,
+                                                               rp.jpeg_quality));
+  return out;
+}
+
 }  // namespace nm03::golden

@@ -6,8 +6,10 @@
 
 #include <algorithm>
 #include <atomic>
+#include <array>
 #include <chrono>
 #include <cstring>
+#include <map>
 #include <mutex>
 #include <thread>
 
@@ -74,6 +76,9 @@ struct Slot {
   int ncanvas = 0;
   bool any_canvas = false;  // some image of the batch needs the generic render → canvas path
   int max_w = 0, max_h = 0;
+  // Captured kernel chains keyed by launch signature (see GraphKey in build_and_run). Every
+  // pointer in the chain is fixed per slot, so a signature fully determines the launches.
+  std::map<std::array<int, 10>, hipGraphExec_t> graphs;
 };
 
 void hip_free_all(Slot& s) {
@@ -84,6 +89,8 @@ void hip_free_all(Slot& s) {
                   (void*)s.jw.coef, (void*)s.jw.nzmask, (void*)s.jw.acbits, (void*)s.jw.dc, (void*)s.jw.stage,
                   (void*)s.jw.boff, (void*)s.jw.total, (void*)s.jw.chunk_ff})
     if (p) (void)hipFree(p);
+  for (auto& kv : s.graphs) (void)hipGraphExecDestroy(kv.second);
+  s.graphs.clear();
   if (s.ev0) (void)hipEventDestroy(s.ev0);
   if (s.ev1) (void)hipEventDestroy(s.ev1);
   if (s.ev2) (void)hipEventDestroy(s.ev2);
@@ -392,28 +399,58 @@ struct Engine::Impl {
     check_hip(hipEventRecord(s.ev0, s.stream), "event");
     check_hip(hipMemcpyAsync(s.d_blob, s.h_blob, bytes, hipMemcpyHostToDevice, s.stream), "H2D blob");
     check_hip(hipEventRecord(s.ev1, s.stream), "event");
-    launch_median(d_raw, s.d_med, d_desc, d_medt, nmed, pc.median_k, d_stats, s.stream);
-    launch_sharpen_band(s.d_med, plane(kPBand), mode == 1 ? s.d_f32 : nullptr, d_desc, d_shpt, nshp, pc, d_stats,
-                        s.stream);
-    SrgOutputs o;
-    o.dilated = plane(kPDilated);
-    o.border_dilated = plane(kPBorderD);
-    if (mode == 1) {
-      o.region = plane(kPRegion);
-      o.eroded = plane(kPEroded);
-      o.border_region = plane(kPBorderR);
-      o.border_eroded = plane(kPBorderE);
+    auto chain = [&] {
+      launch_median(d_raw, s.d_med, d_desc, d_medt, nmed, pc.median_k, d_stats, s.stream);
+      launch_sharpen_band(s.d_med, plane(kPBand), mode == 1 ? s.d_f32 : nullptr, d_desc, d_shpt, nshp, pc, d_stats,
+                          s.stream);
+      SrgOutputs o;
+      o.dilated = plane(kPDilated);
+      o.border_dilated = plane(kPBorderD);
+      if (mode == 1) {
+        o.region = plane(kPRegion);
+        o.eroded = plane(kPEroded);
+        o.border_region = plane(kPBorderR);
+        o.border_eroded = plane(kPBorderE);
+      }
+      launch_srg_morph(plane(kPBand), d_desc, nl, d_seeds, pc, o, s.max_w, s.max_h, s.stream);
+      (void)d_stats_c;
+      if (s.any_canvas) launch_render(d_raw, s.d_f32, s.d_bits, d_stats, d_rd, ncanv, cw, ch, s.d_canvas, s.stream);
+      JpegRenderSrc rsrc;
+      rsrc.raw = d_raw;
+      rsrc.f32 = s.d_f32;
+      rsrc.bits = s.d_bits;
+      rsrc.stats = d_stats;
+      rsrc.rd = d_rd;
+      launch_jpeg(s.d_canvas, d_jd, ncanv, cw, ch, divs, s.jw, s.d_out, s.d_sizes, s.stream, &rsrc);
+    };
+    if (!cfg.graphs || sync_launches()) {
+      chain();
+    } else {
+      const std::array<int, 10> key{nmed, nshp, nl, ncanv, s.max_w, s.max_h, (int)s.any_canvas, mode, cw, ch};
+      auto it = s.graphs.find(key);
+      if (it == s.graphs.end()) {
+        hipGraph_t g = nullptr;
+        hipGraphExec_t ge = nullptr;
+        check_hip(hipStreamBeginCapture(s.stream, hipStreamCaptureModeThreadLocal), "begin capture");
+        try {
+          chain();
+        } catch (...) {
+          (void)hipStreamEndCapture(s.stream, &g);
+          if (g) (void)hipGraphDestroy(g);
+          throw;
+        }
+        check_hip(hipStreamEndCapture(s.stream, &g), "end capture");
+        const hipError_t e = hipGraphInstantiate(&ge, g, nullptr, nullptr, 0);
+        (void)hipGraphDestroy(g);
+        check_hip(e, "graph instantiate");
+        if (s.graphs.size() >= 16) {  // bounded cache: signatures vary only with batch fill
+          (void)hipGraphExecDestroy(s.graphs.begin()->second);
+          s.graphs.erase(s.graphs.begin());
+        }
+        it = s.graphs.emplace(key, ge).first;
+      }
+      check_hip(hipGraphLaunch(it->second, s.stream), "graph launch");
     }
-    launch_srg_morph(plane(kPBand), d_desc, nl, d_seeds, pc, o, s.max_w, s.max_h, s.stream);
-    (void)d_stats_c;
-    if (s.any_canvas) launch_render(d_raw, s.d_f32, s.d_bits, d_stats, d_rd, ncanv, cw, ch, s.d_canvas, s.stream);
-    JpegRenderSrc rsrc;
-    rsrc.raw = d_raw;
-    rsrc.f32 = s.d_f32;
-    rsrc.bits = s.d_bits;
-    rsrc.stats = d_stats;
-    rsrc.rd = d_rd;
-    launch_jpeg(s.d_canvas, d_jd, ncanv, cw, ch, divs, s.jw, s.d_out, s.d_sizes, s.stream, &rsrc);
     check_hip(hipEventRecord(s.ev2, s.stream), "event");
     check_hip(hipEventSynchronize(s.ev2), "batch sync");
     if (acc) {

@@ -13,14 +13,18 @@ void check_hip(hipError_t e, const char* what) {
   if (e != hipSuccess) throw DeviceError(std::string(what) + ": " + hipGetErrorString(e));
 }
 
-void check_launch(const char* what) {
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) throw DeviceError(std::string("launch of ") + what + " failed: " + hipGetErrorString(e));
-  static const bool sync_debug = [] {
+bool sync_launches() {
+  static const bool on = [] {
     const char* s = std::getenv("NM03_SYNC_LAUNCHES");
     return s && *s && *s != '0';
   }();
-  if (sync_debug) {
+  return on;
+}
+
+void check_launch(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) throw DeviceError(std::string("launch of ") + what + " failed: " + hipGetErrorString(e));
+  if (sync_launches()) {
     e = hipDeviceSynchronize();
     if (e != hipSuccess) throw DeviceError(std::string(what) + " failed: " + hipGetErrorString(e));
   }

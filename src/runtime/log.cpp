@@ -39,7 +39,9 @@ struct Roctx {
   Roctx() {
     const char* e = std::getenv("NM03_ROCTX");
     if (!e || !*e || *e == '0') return;
-    void* h = dlopen("libroctx64.so.4", RTLD_NOW | RTLD_GLOBAL);
+    // rocprofv3 --marker-trace intercepts the rocprofiler-sdk flavour; the legacy one is a fallback.
+    void* h = dlopen("librocprofiler-sdk-roctx.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) h = dlopen("libroctx64.so.4", RTLD_NOW | RTLD_GLOBAL);
     if (!h) h = dlopen("libroctx64.so", RTLD_NOW | RTLD_GLOBAL);
     if (!h) return;
     push = (int (*)(const char*))dlsym(h, "roctxRangePushA");

@@ -221,13 +221,19 @@ def _tree(d):
 
 def test_engine_cohort_configs_identical(native, cohort_root, tmp_path):
     trees = []
-    for i, (b, s, t) in enumerate([(1, 1, 1), (25, 3, 8), (7, 2, 4), (64, 4, 16)]):
+    # (batch, streams, threads, hipGraph replay); graph runs go twice through one engine so the
+    # second pass replays cached graphs.
+    for i, (b, s, t, g) in enumerate([(1, 1, 1, False), (25, 3, 8, True), (7, 2, 4, False), (64, 4, 16, True),
+                                      (64, 4, 16, False)]):
         out = str(tmp_path / f"o{i}")
         items = _items(native, cohort_root, out)
-        cfg = nm.PipelineConfig(batch_size=b, streams=s, threads=t)
-        st, times = native.Engine(cfg.engine_config()).run(items)
-        assert all(code == 0 for code, _ in st), st
-        assert times["slices_ok"] == len(items) and times["jpeg_fallbacks"] == 0
+        ec = nm.PipelineConfig(batch_size=b, streams=s, threads=t).engine_config()
+        ec.graphs = g
+        eng = native.Engine(ec)
+        for _ in range(2 if g else 1):
+            st, times = eng.run(items)
+            assert all(code == 0 for code, _ in st), st
+            assert times["slices_ok"] == len(items) and times["jpeg_fallbacks"] == 0
         trees.append(_tree(out))
     assert len(trees[0]) == 2 * len(items)
     for t in trees[1:]:

@@ -11,6 +11,8 @@ rc=$?
 echo "pytest rc=$rc $(date)" >> $P
 [ $rc -le 1 ] || exit $rc
 timeout -k 10 300 python bench.py --steps 10 --warmup 2 > gpurun_out/bench.log 2>&1 || exit 31
+timeout -k 10 300 python bench.py --steps 10 --warmup 2 --graphs > gpurun_out/bench_graphs.log 2>&1 || exit 35
+timeout -k 10 300 python bench.py --steps 10 --warmup 2 > gpurun_out/bench2.log 2>&1 || exit 36
 echo "bench ok $(date)" >> $P
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_iter -o bench -- python3 bench.py --steps 3 --warmup 1 > gpurun_out/prof_iter.log 2>&1 || exit 32
 echo "done $(date)" >> $P
