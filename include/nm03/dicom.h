@@ -37,6 +37,10 @@ struct Header {
 // Parse a whole file image held in memory. Throws SliceError on malformed/unsupported input.
 Header parse(const uint8_t* data, size_t size);
 
+// Parse from a prefix `avail` bytes long of a `size`-byte file: succeeds when every element up to
+// the pixel data lies in the prefix (throws SliceError "Truncated" otherwise).
+Header parse_prefix(const uint8_t* data, size_t avail, size_t size);
+
 // Copy the first frame's pixels to `dst` as 16-bit words (8-bit data is widened, big-endian data
 // is byte-swapped). dst must hold rows*cols uint16.
 void copy_pixels16(const Header& h, const uint8_t* data, size_t size, uint16_t* dst);
@@ -45,6 +49,33 @@ void copy_pixels16(const Header& h, const uint8_t* data, size_t size, uint16_t* 
 std::vector<uint8_t> read_file(const std::string& path);
 // Read into a caller-provided growable buffer (avoids reallocations in loader threads).
 size_t read_file_into(const std::string& path, std::vector<uint8_t>& buf);
+
+// A slice file opened for loading: the header is parsed from a 16 KiB prefix and, for
+// little-endian 16-bit data, the pixels are read with one pread straight into the destination
+// (the engine's pinned upload blob) — no intermediate whole-file buffer and no extra copy.
+class SliceFile {
+ public:
+  explicit SliceFile(const std::string& path);
+  ~SliceFile();
+  SliceFile(const SliceFile&) = delete;
+  SliceFile& operator=(const SliceFile&) = delete;
+  size_t size() const { return size_; }
+  // Parses the header (`buf` is scratch space owned by the caller and must outlive pixels16).
+  const Header& header(std::vector<uint8_t>& buf);
+  // First frame as 16-bit words into dst (rows*cols elements).
+  void pixels16(uint16_t* dst);
+  // True when pixels16 reads straight from the file (prefix parse, LE 16-bit data).
+  bool direct() const { return !whole_; }
+
+ private:
+  void pread_all(void* dst, size_t n, size_t off);
+  std::string path_;
+  int fd_ = -1;
+  size_t size_ = 0;
+  Header h_;
+  bool whole_ = true;
+  std::vector<uint8_t>* buf_ = nullptr;
+};
 
 struct WriteSpec {
   int rows = 256, cols = 256;

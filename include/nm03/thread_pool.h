@@ -4,10 +4,12 @@
 // so patient and batch boundaries never idle the workers.
 #pragma once
 
+#include <algorithm>
 #include <atomic>
 #include <condition_variable>
 #include <cstddef>
-#include <deque>
+#include <cstdint>
+#include <memory>
 #include <functional>
 #include <mutex>
 #include <thread>
@@ -15,6 +17,10 @@
 
 namespace nm03 {
 
+// Tasks carry a priority (lower runs first; FIFO among equals). The engine uses the batch index,
+// so the loads and exports of earlier batches overtake later ones: the first batch reaches the GPU
+// after ~batch/threads loads instead of after every in-flight slot's loads (pipeline fill), and the
+// last batches' exports are not queued behind anything (drain).
 class ThreadPool {
  public:
   explicit ThreadPool(int n) {
@@ -32,16 +38,36 @@ class ThreadPool {
   ThreadPool(const ThreadPool&) = delete;
   ThreadPool& operator=(const ThreadPool&) = delete;
 
-  void submit(std::function<void()> f) {
+  void submit(std::function<void()> f, uint64_t prio = 0) {
     {
       std::lock_guard<std::mutex> g(m_);
-      q_.push_back(std::move(f));
+      push(std::move(f), prio);
     }
     cv_.notify_one();
+  }
+  // `n` copies of `f` under one lock (bulk fan-out of a parallel-for).
+  void submit_n(int n, const std::function<void()>& f, uint64_t prio = 0) {
+    {
+      std::lock_guard<std::mutex> g(m_);
+      for (int i = 0; i < n; ++i) push(f, prio);
+    }
+    if (n == 1)
+      cv_.notify_one();
+    else
+      cv_.notify_all();
   }
   int size() const { return (int)workers_.size(); }
 
  private:
+  struct Task {
+    uint64_t prio, seq;
+    std::function<void()> f;
+  };
+  static bool later(const Task& a, const Task& b) { return a.prio != b.prio ? a.prio > b.prio : a.seq > b.seq; }
+  void push(std::function<void()> f, uint64_t prio) {
+    q_.push_back(Task{prio, seq_++, std::move(f)});
+    std::push_heap(q_.begin(), q_.end(), later);
+  }
   void loop() {
     for (;;) {
       std::function<void()> f;
@@ -49,14 +75,16 @@ class ThreadPool {
         std::unique_lock<std::mutex> g(m_);
         cv_.wait(g, [this] { return stop_ || !q_.empty(); });
         if (stop_ && q_.empty()) return;
-        f = std::move(q_.front());
-        q_.pop_front();
+        std::pop_heap(q_.begin(), q_.end(), later);
+        f = std::move(q_.back().f);
+        q_.pop_back();
       }
       f();
     }
   }
   std::vector<std::thread> workers_;
-  std::deque<std::function<void()>> q_;
+  std::vector<Task> q_;  // binary heap on (prio, seq)
+  uint64_t seq_ = 0;
   std::mutex m_;
   std::condition_variable cv_;
   bool stop_ = false;
@@ -66,16 +94,36 @@ class ThreadPool {
 class TaskGroup {
  public:
   explicit TaskGroup(ThreadPool& p) : pool_(p) {}
-  void run(std::function<void()> f) {
+  void run(std::function<void()> f, uint64_t prio = 0) {
     {
       std::lock_guard<std::mutex> g(m_);
       ++pending_;
     }
-    pool_.submit([this, f = std::move(f)] {
-      f();
+    pool_.submit(
+        [this, f = std::move(f)] {
+          f();
+          done(1);
+        },
+        prio);
+  }
+  // fn(i) for i in [0, n): min(n, pool size) runners pull indices from a shared counter.
+  void for_each(size_t n, std::function<void(size_t)> fn, uint64_t prio = 0) {
+    if (n == 0) return;
+    const int runners = (int)std::min<size_t>(n, (size_t)pool_.size());
+    auto st = std::make_shared<ForEach>();
+    st->n = n;
+    st->fn = std::move(fn);
+    {
       std::lock_guard<std::mutex> g(m_);
-      if (--pending_ == 0) cv_.notify_all();
-    });
+      pending_ += (size_t)runners;
+    }
+    pool_.submit_n(
+        runners,
+        [this, st] {
+          for (size_t i; (i = st->next.fetch_add(1)) < st->n;) st->fn(i);
+          done(1);
+        },
+        prio);
   }
   void wait() {
     std::unique_lock<std::mutex> g(m_);
@@ -84,6 +132,16 @@ class TaskGroup {
   ~TaskGroup() { wait(); }
 
  private:
+  struct ForEach {
+    std::atomic<size_t> next{0};
+    size_t n = 0;
+    std::function<void(size_t)> fn;
+  };
+  void done(size_t k) {
+    std::lock_guard<std::mutex> g(m_);
+    pending_ -= k;
+    if (pending_ == 0) cv_.notify_all();
+  }
   ThreadPool& pool_;
   std::mutex m_;
   std::condition_variable cv_;

@@ -8,6 +8,7 @@
 #include <sys/stat.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <cerrno>
 #include <cstdio>
 #include <cstdlib>
@@ -153,8 +154,12 @@ uint16_t us_value(const Cursor& c, const Elem& e) {
 
 }  // namespace
 
-Header parse(const uint8_t* data, size_t size) {
+Header parse(const uint8_t* data, size_t size) { return parse_prefix(data, size, size); }
+
+Header parse_prefix(const uint8_t* data, size_t avail, size_t size) {
   Header h;
+  const size_t full = size;
+  size = avail;
   Cursor c{data, size, 0, false};
   bool explicit_vr = true;
   if (size >= 132 && std::memcmp(data + 128, "DICM", 4) == 0) {
@@ -280,7 +285,7 @@ Header parse(const uint8_t* data, size_t size) {
   }
   if (h.bits_stored <= 0 || h.bits_stored > h.bits_allocated) h.bits_stored = h.bits_allocated;
   const size_t need = (size_t)h.rows * h.cols * (h.bits_allocated / 8);
-  if (h.pixel_length < need || h.pixel_offset + need > size)
+  if (h.pixel_length < need || h.pixel_offset + need > full)
     throw SliceError("DICOM pixel data shorter than Rows*Columns");
   if (!(h.slope == h.slope) || h.slope == 0.f) h.slope = 1.f;
   return h;
@@ -321,6 +326,66 @@ size_t read_file_into(const std::string& path, std::vector<uint8_t>& buf) {
   }
   ::close(fd);
   return n;
+}
+
+// ------------------------------------------------------------------------------------------------
+// SliceFile: header from a 16 KiB prefix, pixels read straight into the caller's buffer.
+// ------------------------------------------------------------------------------------------------
+SliceFile::SliceFile(const std::string& path) : path_(path) {
+  fd_ = ::open(path.c_str(), O_RDONLY | O_CLOEXEC);
+  if (fd_ < 0) throw SliceError("Cannot open file: " + path + " (" + std::strerror(errno) + ")");
+  struct stat st;
+  if (fstat(fd_, &st) != 0) {
+    ::close(fd_);
+    fd_ = -1;
+    throw SliceError("Cannot stat file: " + path);
+  }
+  size_ = (size_t)st.st_size;
+}
+
+SliceFile::~SliceFile() {
+  if (fd_ >= 0) ::close(fd_);
+}
+
+void SliceFile::pread_all(void* dst, size_t n, size_t off) {
+  size_t got = 0;
+  while (got < n) {
+    ssize_t r = ::pread(fd_, (uint8_t*)dst + got, n - got, (off_t)(off + got));
+    if (r < 0 && errno == EINTR) continue;
+    if (r <= 0) throw SliceError("Read error on file: " + path_);
+    got += (size_t)r;
+  }
+}
+
+const Header& SliceFile::header(std::vector<uint8_t>& buf) {
+  constexpr size_t kPrefix = 16384;
+  const size_t pre = std::min(size_, kPrefix);
+  if (buf.size() < pre) buf.resize(pre);
+  pread_all(buf.data(), pre, 0);
+  buf_ = &buf;
+  if (pre < size_) {
+    try {
+      h_ = parse_prefix(buf.data(), pre, size_);
+      whole_ = false;
+      // Direct reads only for raw little-endian 16-bit samples; everything else is converted.
+      if (h_.bits_allocated == 16 && h_.syntax != Syntax::kExplicitBE) return h_;
+    } catch (const SliceError&) {
+      // header longer than the prefix (or malformed): parse the whole file below
+    }
+  }
+  if (buf.size() < size_) buf.resize(size_);
+  if (pre < size_) pread_all(buf.data() + pre, size_ - pre, pre);
+  h_ = parse(buf.data(), size_);
+  whole_ = true;
+  return h_;
+}
+
+void SliceFile::pixels16(uint16_t* dst) {
+  if (whole_) {
+    copy_pixels16(h_, buf_->data(), size_, dst);
+  } else {
+    pread_all(dst, (size_t)h_.rows * h_.cols * 2, h_.pixel_offset);
+  }
 }
 
 std::vector<uint8_t> read_file(const std::string& path) {

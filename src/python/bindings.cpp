@@ -291,6 +291,14 @@ PYBIND11_MODULE(_nm03, m) {
       py::arg("slope") = 1.f, py::arg("intercept") = 0.f, py::arg("spacing_x") = 1.f, py::arg("spacing_y") = 1.f,
       py::arg("instance") = 1, py::arg("patient_id") = "PGBM-000", py::arg("syntax") = "explicit",
       py::arg("preamble") = true);
+  m.def("read_pixels_direct", [](const std::string& path) {
+    dicom::SliceFile f(path);
+    std::vector<uint8_t> scratch;
+    const dicom::Header& h = f.header(scratch);
+    std::vector<uint16_t> px((size_t)h.rows * h.cols);
+    f.pixels16(px.data());
+    return py::make_tuple(to_np<uint16_t>(px, {h.rows, h.cols}), f.direct());
+  });
   m.def(
       "read_slice",
       [](const std::string& path, int min_dim) {

@@ -8,6 +8,8 @@
 #include <atomic>
 #include <array>
 #include <chrono>
+#include <condition_variable>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -150,12 +152,14 @@ struct Engine::Impl {
     check_hip(hipSetDevice(cfg.device), "hipSetDevice");
     pool = std::make_unique<ThreadPool>(cfg.threads);
     for (int i = 0; i < cfg.streams; ++i) slots.push_back(make_slot());
+    start_workers();
     log_info("engine on device " + std::to_string(cfg.device) + ": batch " + std::to_string(cfg.batch_size) + ", " +
              std::to_string(cfg.streams) + " streams, " + std::to_string(cfg.threads) + " host threads, max_dim " +
              std::to_string(cfg.max_dim));
   }
 
   ~Impl() {
+    stop_workers();
     (void)hipSetDevice(cfg.device);
     for (auto& s : slots) hip_free_all(*s);
   }
@@ -193,7 +197,13 @@ struct Engine::Impl {
       check_hip(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking), "hipStreamCreate");
       check_hip(hipEventCreate(&s.ev0), "hipEventCreate");
       check_hip(hipEventCreate(&s.ev1), "hipEventCreate");
-      check_hip(hipEventCreate(&s.ev2), "hipEventCreate");
+      // Batch completion is waited on by the slot thread: a blocking-sync event sleeps instead of
+      // spinning a core the loader/writer pool needs (NM03_EVENT_SPIN=1 restores spinning).
+      static const bool spin = [] {
+        const char* e = std::getenv("NM03_EVENT_SPIN");
+        return e && *e && *e != '0';
+      }();
+      check_hip(hipEventCreateWithFlags(&s.ev2, spin ? hipEventDefault : hipEventBlockingSync), "hipEventCreate");
       check_hip(hipHostMalloc((void**)&s.h_blob, s.blob_bytes, hipHostMallocDefault), "hipHostMalloc blob");
       s.d_blob = dmalloc<uint8_t>(s.blob_bytes, "hipMalloc blob");
       s.d_med = dmalloc<uint16_t>(s.cap_pixels, "hipMalloc median");
@@ -234,8 +244,9 @@ struct Engine::Impl {
     const double t0 = now_s();
     try {
       if (fault_plan().corrupt_dicom == (int64_t)item) throw SliceError("injected fault: corrupt DICOM data");
-      const size_t n = dicom::read_file_into(path, buf);
-      dicom::Header h = dicom::parse(buf.data(), n);
+      dicom::SliceFile file(path);
+      const size_t n = file.size();
+      const dicom::Header& h = file.header(buf);
       const int md = cfg.pipe.min_dim;
       if (md > 0 && (h.cols < md || h.rows < md)) {
         st.code = kSliceTooSmall;
@@ -250,7 +261,7 @@ struct Engine::Impl {
         const size_t off = s.raw_used.fetch_add(alloc);
         if (off + alloc > s.cap_pixels) throw SliceError("batch pixel capacity exceeded");
         uint16_t* dst = reinterpret_cast<uint16_t*>(s.h_blob + s.raw_base) + off;
-        dicom::copy_pixels16(h, buf.data(), n, dst);
+        file.pixels16(dst);
         LoadedSlice& L = s.loaded[i];
         L.w = h.cols;
         L.h = h.rows;
@@ -488,21 +499,23 @@ struct Engine::Impl {
   void process_batch(Slot& s, const std::vector<WorkItem>& items, size_t first, size_t count,
                      std::vector<SliceStatus>& status, StageTimes& acc, std::mutex& acc_m,
                      const std::function<void(size_t)>& on_start) {
+    const uint64_t batch = first / (size_t)cfg.batch_size;  // pool priority: earlier batches first
     s.raw_used = 0;
     s.loaded.assign(count, LoadedSlice{});
     std::atomic<int64_t> load_ns{0}, bytes_in{0}, write_ns{0}, bytes_out{0};
     {
       TaskGroup tg(*pool);
-      for (size_t i = 0; i < count; ++i) {
-        tg.run([&, i] {
-          if (on_start) on_start(first + i);
-          if (cfg.resume && outputs_exist(items[first + i])) {
-            status[first + i] = SliceStatus{kSliceOk, "resumed: outputs already present"};
-            return;
-          }
-          load_into(s, (int)i, first + i, items[first + i].path, status[first + i], load_ns, bytes_in);
-        });
-      }
+      tg.for_each(
+          count,
+          [&](size_t i) {
+            if (on_start) on_start(first + i);
+            if (cfg.resume && outputs_exist(items[first + i])) {
+              status[first + i] = SliceStatus{kSliceOk, "resumed: outputs already present"};
+              return;
+            }
+            load_into(s, (int)i, first + i, items[first + i].path, status[first + i], load_ns, bytes_in);
+          },
+          2 * batch);
       tg.wait();
     }
     s.live.clear();
@@ -534,29 +547,30 @@ struct Engine::Impl {
         }
       }
       TaskGroup tg(*pool);
-      for (int c = 0; c < (int)s.live.size(); ++c) {
-        const size_t item = first + s.live[c];
-        if (status[item].code != kSliceOk) continue;
-        tg.run([&, c, item] {
-          const double t0 = now_s();
-          TraceRange tr("nm03.export");
-          try {
-            if (fault_plan().fail_write == (int64_t)item) throw std::runtime_error("injected fault: export failure");
-            const std::string base = cohort::with_slash(items[item].out_dir) + cohort::stem(items[item].path);
-            for (int k = 0; k < 2; ++k) {
-              const int cv = 2 * c + k;
-              const std::string path = base + (k == 0 ? "_original.jpg" : "_processed.jpg");
-              const uint8_t* seg = use_fb[cv] ? fb[cv].data() : s.h_out + (size_t)cv * kOutCap;
-              const size_t len = use_fb[cv] ? fb[cv].size() : (size_t)s.h_sizes[cv];
-              jpeg::write_jpeg_file(path, jpeg_header, seg, len);
-              bytes_out += (int64_t)(jpeg_header.size() + len + 2);
+      tg.for_each(
+          s.live.size(),
+          [&](size_t c) {
+            const size_t item = first + s.live[c];
+            if (status[item].code != kSliceOk) return;
+            const double t0 = now_s();
+            TraceRange tr("nm03.export");
+            try {
+              if (fault_plan().fail_write == (int64_t)item) throw std::runtime_error("injected fault: export failure");
+              const std::string base = cohort::with_slash(items[item].out_dir) + cohort::stem(items[item].path);
+              for (int k = 0; k < 2; ++k) {
+                const int cv = 2 * (int)c + k;
+                const std::string path = base + (k == 0 ? "_original.jpg" : "_processed.jpg");
+                const uint8_t* seg = use_fb[cv] ? fb[cv].data() : s.h_out + (size_t)cv * kOutCap;
+                const size_t len = use_fb[cv] ? fb[cv].size() : (size_t)s.h_sizes[cv];
+                jpeg::write_jpeg_file(path, jpeg_header, seg, len);
+                bytes_out += (int64_t)(jpeg_header.size() + len + 2);
+              }
+            } catch (const std::exception& e) {
+              status[item] = SliceStatus{kSliceExportError, std::string("Error in export stage: ") + e.what()};
             }
-          } catch (const std::exception& e) {
-            status[item] = SliceStatus{kSliceExportError, std::string("Error in export stage: ") + e.what()};
-          }
-          write_ns += (int64_t)((now_s() - t0) * 1e9);
-        });
-      }
+            write_ns += (int64_t)((now_s() - t0) * 1e9);
+          },
+          2 * batch + 1);
       tg.wait();
     }
     std::lock_guard<std::mutex> g(acc_m);
@@ -570,35 +584,90 @@ struct Engine::Impl {
     acc.batches += 1;
   }
 
+  // ---- persistent slot workers: one host thread per slot, parked between runs --------------
+  struct Job {
+    const std::vector<WorkItem>* items = nullptr;
+    std::vector<SliceStatus>* status = nullptr;
+    StageTimes* acc = nullptr;
+    std::mutex* acc_m = nullptr;
+    const std::function<void(size_t)>* on_start = nullptr;
+    size_t nb = 0;
+    std::atomic<size_t> next{0};
+    std::exception_ptr err;
+    std::mutex err_m;
+  };
+  std::vector<std::thread> workers;
+  std::mutex job_m, run_m;
+  std::condition_variable job_cv, done_cv;
+  Job* job = nullptr;
+  uint64_t job_gen = 0;
+  int busy = 0;
+  bool quit = false;
+
+  void start_workers() {
+    for (auto& sp : slots) workers.emplace_back([this, s = sp.get()] { worker(s); });
+  }
+  void stop_workers() {
+    {
+      std::lock_guard<std::mutex> g(job_m);
+      quit = true;
+    }
+    job_cv.notify_all();
+    for (auto& t : workers) t.join();
+    workers.clear();
+  }
+
+  void worker(Slot* s) {
+    (void)hipSetDevice(cfg.device);
+    uint64_t seen = 0;
+    for (;;) {
+      Job* j;
+      {
+        std::unique_lock<std::mutex> g(job_m);
+        job_cv.wait(g, [&] { return quit || job_gen != seen; });
+        if (quit) return;
+        seen = job_gen;
+        j = job;
+      }
+      try {
+        const size_t B = (size_t)cfg.batch_size, n = j->items->size();
+        for (size_t b; (b = j->next.fetch_add(1)) < j->nb;) {
+          const size_t first = b * B, count = std::min(B, n - first);
+          process_batch(*s, *j->items, first, count, *j->status, *j->acc, *j->acc_m, *j->on_start);
+        }
+      } catch (...) {
+        std::lock_guard<std::mutex> g(j->err_m);
+        if (!j->err) j->err = std::current_exception();
+      }
+      std::lock_guard<std::mutex> g(job_m);
+      if (--busy == 0) done_cv.notify_all();
+    }
+  }
+
   std::vector<SliceStatus> run(const std::vector<WorkItem>& items, StageTimes* times,
                                const std::function<void(size_t)>& on_start) {
+    std::lock_guard<std::mutex> serial(run_m);
     const double t0 = now_s();
     std::vector<SliceStatus> status(items.size());
     StageTimes acc;
     std::mutex acc_m;
-    const size_t B = (size_t)cfg.batch_size;
-    const size_t nb = (items.size() + B - 1) / B;
-    std::atomic<size_t> next{0};
-    std::vector<std::thread> th;
-    std::exception_ptr err;
-    std::mutex err_m;
-    for (auto& sp : slots) {
-      Slot* s = sp.get();
-      th.emplace_back([&, s] {
-        try {
-          check_hip(hipSetDevice(cfg.device), "hipSetDevice");
-          for (size_t b; (b = next.fetch_add(1)) < nb;) {
-            const size_t first = b * B, count = std::min(B, items.size() - first);
-            process_batch(*s, items, first, count, status, acc, acc_m, on_start);
-          }
-        } catch (...) {
-          std::lock_guard<std::mutex> g(err_m);
-          if (!err) err = std::current_exception();
-        }
-      });
+    Job j;
+    j.items = &items;
+    j.status = &status;
+    j.acc = &acc;
+    j.acc_m = &acc_m;
+    j.on_start = &on_start;
+    j.nb = (items.size() + (size_t)cfg.batch_size - 1) / (size_t)cfg.batch_size;
+    {
+      std::unique_lock<std::mutex> g(job_m);
+      job = &j;
+      busy = (int)workers.size();
+      ++job_gen;
+      job_cv.notify_all();
+      done_cv.wait(g, [&] { return busy == 0; });
+      job = nullptr;
     }
-    for (auto& t : th) t.join();
-    if (err) std::rethrow_exception(err);
+    if (j.err) std::rethrow_exception(j.err);
     for (const auto& st : status) (st.code == kSliceOk ? acc.slices_ok : acc.slices_failed) += 1;
     acc.wall_s = now_s() - t0;
     if (acc.jpeg_fallbacks) log_warn(std::to_string(acc.jpeg_fallbacks) + " JPEG(s) exceeded GPU capacity; CPU-encoded");
@@ -609,6 +678,7 @@ struct Engine::Impl {
   }
 
   SingleResult run_single(const golden::SliceInput& in) {
+    std::lock_guard<std::mutex> serial(run_m);
     check_hip(hipSetDevice(cfg.device), "hipSetDevice");
     Slot& s = *slots[0];
     if (in.w > cfg.max_dim || in.h > cfg.max_dim) throw DeviceError("slice exceeds engine max_dim");

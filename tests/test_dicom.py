@@ -50,6 +50,29 @@ def test_sequence_skipping(native):
     assert np.array_equal(native.dicom_pixels(bytes(b)), px)
 
 
+@pytest.mark.parametrize("kind", ["explicit", "implicit", "big", "u8", "long_header", "tiny"])
+def test_slice_file_direct_read(native, tmp_path, kind):
+    """SliceFile (engine loader): prefix-parsed header + pread of the pixels must equal the
+    whole-file parse for every layout, and fall back to the whole-file path where needed."""
+    rng = np.random.default_rng(1)
+    shape = (8, 8) if kind == "tiny" else (300, 257)
+    px = rng.integers(0, 250 if kind == "u8" else 65535, size=shape).astype(np.uint16)
+    syntax = kind if kind in ("implicit", "big") else "explicit"
+    b = bytearray(native.dicom_bytes(px, type="u8" if kind == "u8" else "u16",
+                                     bits_stored=8 if kind == "u8" else 16, syntax=syntax))
+    if kind == "long_header":  # a 40 KiB private OB element pushes the pixels past the prefix
+        tag = (0x0009).to_bytes(2, "little") + (0x0010).to_bytes(2, "little")
+        blob = tag + b"OB\x00\x00" + (40000).to_bytes(4, "little") + bytes(40000)
+        pos = b.index((0x0010).to_bytes(2, "little") + (0x0020).to_bytes(2, "little"))  # PatientID
+        b[pos:pos] = blob
+    p = tmp_path / "x.dcm"
+    p.write_bytes(bytes(b))
+    got, direct = native.read_pixels_direct(str(p))
+    assert np.array_equal(got, native.dicom_pixels(bytes(b)))
+    assert np.array_equal(got, px)
+    assert direct == (kind in ("explicit", "implicit"))
+
+
 def test_rejects_compressed_and_garbage(native):
     with pytest.raises(Exception):
         native.dicom_parse(b"\x00" * 50)
