@@ -89,7 +89,6 @@ struct RenderDesc {
 // JPEG job: one canvas (out_w×out_h, both multiples of 16) → one entropy-coded segment.
 struct JpegDesc {
   uint32_t canvas_off;  // bytes (generic path: rendered canvas)
-  uint32_t coef_off;    // block index of the image's first block (MCU order, 4 luma blocks/MCU)
   uint32_t stage_off;   // u32 word offset of the bit staging area
   uint32_t stage_words;
   uint64_t out_off;     // byte offset in the output buffer (host-mapped)

@@ -112,6 +112,17 @@ NM03_HD int mag_bits(int v) {
   return n;
 }
 
+// Products inside the FDCT: every operand fits in 24 signed bits (pass-1 inputs are |x| ≤ 128 sums,
+// pass-2 inputs ≤ 2^15) and every product in 31 bits, so the device uses the full-rate
+// v_mul_i32_i24 instead of the quarter-rate v_mul_lo_u32 — the results are identical.
+NM03_HD int32_t fdct_mul(int32_t a, int32_t b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __mul24(a, b);
+#else
+  return a * b;
+#endif
+}
+
 // LL&M integer forward DCT, libjpeg jfdctint "islow" arithmetic.  `d` holds 64 level-shifted
 // samples (x-128) in natural order; on return it holds coefficients scaled up by 8.
 NM03_HD void fdct_islow(int32_t* d) {
@@ -130,20 +141,20 @@ NM03_HD void fdct_islow(int32_t* d) {
     int32_t t10 = t0 + t3, t13 = t0 - t3, t11 = t1 + t2, t12 = t1 - t2;
     p[0] = (t10 + t11) * (1 << P1);
     p[4] = (t10 - t11) * (1 << P1);
-    int32_t z1 = (t12 + t13) * F0_541;
-    p[2] = NM03_DESCALE(z1 + t13 * F0_765, CB - P1);
-    p[6] = NM03_DESCALE(z1 + t12 * (-F1_847), CB - P1);
+    int32_t z1 = fdct_mul(t12 + t13, F0_541);
+    p[2] = NM03_DESCALE(z1 + fdct_mul(t13, F0_765), CB - P1);
+    p[6] = NM03_DESCALE(z1 + fdct_mul(t12, -F1_847), CB - P1);
     z1 = t4 + t7;
     int32_t z2 = t5 + t6, z3 = t4 + t6, z4 = t5 + t7;
-    int32_t z5 = (z3 + z4) * F1_175;
-    t4 = t4 * F0_298;
-    t5 = t5 * F2_053;
-    t6 = t6 * F3_072;
-    t7 = t7 * F1_501;
-    z1 = z1 * (-F0_899);
-    z2 = z2 * (-F2_562);
-    z3 = z3 * (-F1_961);
-    z4 = z4 * (-F0_390);
+    int32_t z5 = fdct_mul(z3 + z4, F1_175);
+    t4 = fdct_mul(t4, F0_298);
+    t5 = fdct_mul(t5, F2_053);
+    t6 = fdct_mul(t6, F3_072);
+    t7 = fdct_mul(t7, F1_501);
+    z1 = fdct_mul(z1, -F0_899);
+    z2 = fdct_mul(z2, -F2_562);
+    z3 = fdct_mul(z3, -F1_961);
+    z4 = fdct_mul(z4, -F0_390);
     z3 += z5;
     z4 += z5;
     p[7] = NM03_DESCALE(t4 + z1 + z3, CB - P1);
@@ -161,20 +172,20 @@ NM03_HD void fdct_islow(int32_t* d) {
     int32_t t10 = t0 + t3, t13 = t0 - t3, t11 = t1 + t2, t12 = t1 - t2;
     p[0] = NM03_DESCALE(t10 + t11, P1);
     p[32] = NM03_DESCALE(t10 - t11, P1);
-    int32_t z1 = (t12 + t13) * F0_541;
-    p[16] = NM03_DESCALE(z1 + t13 * F0_765, CB + P1);
-    p[48] = NM03_DESCALE(z1 + t12 * (-F1_847), CB + P1);
+    int32_t z1 = fdct_mul(t12 + t13, F0_541);
+    p[16] = NM03_DESCALE(z1 + fdct_mul(t13, F0_765), CB + P1);
+    p[48] = NM03_DESCALE(z1 + fdct_mul(t12, -F1_847), CB + P1);
     z1 = t4 + t7;
     int32_t z2 = t5 + t6, z3 = t4 + t6, z4 = t5 + t7;
-    int32_t z5 = (z3 + z4) * F1_175;
-    t4 = t4 * F0_298;
-    t5 = t5 * F2_053;
-    t6 = t6 * F3_072;
-    t7 = t7 * F1_501;
-    z1 = z1 * (-F0_899);
-    z2 = z2 * (-F2_562);
-    z3 = z3 * (-F1_961);
-    z4 = z4 * (-F0_390);
+    int32_t z5 = fdct_mul(z3 + z4, F1_175);
+    t4 = fdct_mul(t4, F0_298);
+    t5 = fdct_mul(t5, F2_053);
+    t6 = fdct_mul(t6, F3_072);
+    t7 = fdct_mul(t7, F1_501);
+    z1 = fdct_mul(z1, -F0_899);
+    z2 = fdct_mul(z2, -F2_562);
+    z3 = fdct_mul(z3, -F1_961);
+    z4 = fdct_mul(z4, -F0_390);
     z3 += z5;
     z4 += z5;
     p[56] = NM03_DESCALE(t4 + z1 + z3, CB + P1);

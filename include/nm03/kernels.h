@@ -56,22 +56,22 @@ void dilate_volume(const uint64_t* src, uint64_t* dst, uint64_t* tmp, int w, int
 void launch_render(const uint16_t* raw, const float* f32, const uint64_t* bits, const SliceStats* stats,
                    const RenderDesc* rd, int ncanvas, int out_w, int out_h, uint8_t* canvas, hipStream_t stream);
 
-// K4: JPEG. (1) per 8×8 block: [fused 2× render or canvas read] → islow FDCT → reciprocal
-// quantisation → zig-zag + AC Huffman cost; (2) per image: DC costs, block scan, zero staging;
-// (3) per block: Huffman bit emission into staging; (4) per 4 KiB chunk: 0xFF counting, then
-// stuffed copy straight into `out` (host-mapped pinned memory). out_sizes[i] = bytes, or -1 when
-// the image exceeded its staging/out capacity (caller re-encodes on the CPU).
+// K4: JPEG. (1) single pass, workgroup per 256 luma blocks of an image: [fused 2× render or
+// canvas read] → islow FDCT → reciprocal quantisation → Huffman cost → workgroup scan →
+// decoupled look-back across the image → bit emission into the staging words; (2) per 4 KiB
+// chunk: 0xFF counting, then the stuffed copy straight into `out` (host-mapped pinned memory).
+// out_sizes[i] = bytes, or -1 when the image exceeded its staging/out capacity (caller
+// re-encodes on the CPU).
 struct JpegWork {
-  int16_t* coef = nullptr;     // ncanvas × blocks × 64
-  uint64_t* nzmask = nullptr;  // ncanvas × blocks
-  uint32_t* acbits = nullptr;  // ncanvas × blocks
-  int16_t* dc = nullptr;       // ncanvas × blocks
-  uint32_t* boff = nullptr;    // ncanvas × blocks: bit offset of each luma block
-  uint32_t* total = nullptr;   // ncanvas: total bits (0xFFFFFFFF = overflow)
+  uint32_t* stage = nullptr;     // ncanvas × stage_words bit staging; all-zero between launches
+                                 // (zeroed once at allocation, then kept clear by the stuffing kernel)
+  uint64_t* look = nullptr;      // look_cap look-back status words (zeroed once; cleared after use)
+  size_t look_cap = 0;           // ≥ ncanvas × ceil(blocks / 256)
+  size_t look_used = 0;          // set by launch_jpeg
+  uint32_t* ticket = nullptr;    // ordered workgroup ticket counter (zeroed once; self-resetting)
+  uint32_t* total = nullptr;     // ncanvas: total bits (0xFFFFFFFF = overflow)
   uint32_t* chunk_ff = nullptr;  // ncanvas × max_chunks: 0xFF bytes per stuffing chunk
-  uint32_t* stage = nullptr;   // bit staging words
-  uint8_t* tmp = nullptr;      // unused (kept for ABI of older callers)
-  int max_chunks = 0;          // stage bytes / kStuffChunk
+  int max_chunks = 0;            // stage bytes / kStuffChunk
 };
 // Fused-render inputs (needed when any JpegDesc.render ≥ 0).
 struct JpegRenderSrc {
@@ -82,7 +82,7 @@ struct JpegRenderSrc {
   const RenderDesc* rd = nullptr;
 };
 void launch_jpeg(const uint8_t* canvas, const JpegDesc* jd, int ncanvas, int out_w, int out_h, const int32_t* div_luma,
-                 const JpegWork& w, uint8_t* out, int32_t* out_sizes, hipStream_t stream,
+                 JpegWork& w, uint8_t* out, int32_t* out_sizes, hipStream_t stream,
                  const JpegRenderSrc* fused = nullptr);
 // True when RenderDesc r is an exact 2× fit onto the canvas (the fused fast path applies).
 bool render_is_exact_2x(const RenderDesc& r, int out_w, int out_h);

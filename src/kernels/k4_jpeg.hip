@@ -40,129 +40,16 @@ __device__ __forceinline__ int mag_bits_fast(int v) {
 }
 __device__ __forceinline__ uint32_t hlen(uint32_t e) { return e >> 16; }
 
-__global__ __launch_bounds__(256) void jpeg_block_kernel(const uint8_t* __restrict__ canvas,
-                                                         const JpegDesc* __restrict__ jd, int ncanvas, int out_w,
-                                                         int out_h, QuantRecip q, JpegWork w, JpegRenderSrc rs) {
-  // AC code lengths in LDS: 63 per-lane lookups per block become ds_read_u8 instead of gathers.
-  __shared__ uint8_t aclen[256];
-  aclen[threadIdx.x] = (uint8_t)hlen(kHuffAcLuma.e[threadIdx.x]);
-  __syncthreads();
-  const int bpi = (out_w >> 3) * (out_h >> 3);
-  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
-  if (gid >= bpi * ncanvas) return;
-  const int img = gid / bpi, b = gid - img * bpi;
-  const JpegDesc d = jd[img];
-  const int mcux = out_w >> 4;
-  const int mcu = b >> 2, sub = b & 3;
-  const int bx = 2 * (mcu % mcux) + (sub & 1), by = 2 * (mcu / mcux) + (sub >> 1);
-  int32_t blk[64];
-  if (d.render >= 0) {
-    const RenderDesc rd = rs.rd[d.render];
-    const RWindow win = rd.kind == kRenderLabels ? RWindow{0.f, 0.f} : render_window(rd, rs.stats);
-    render_block_2x(rd, rs.raw, rs.f32, rs.bits, win, bx, by, blk);
-#pragma unroll
-    for (int i = 0; i < 64; ++i) blk[i] -= 128;
-  } else {
-    const uint8_t* src = canvas + d.canvas_off + (size_t)(by * 8) * out_w + bx * 8;
-#pragma unroll
-    for (int r = 0; r < 8; ++r) {
-      const uint2 v = *reinterpret_cast<const uint2*>(src + (size_t)r * out_w);
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        blk[r * 8 + c] = (int32_t)((v.x >> (8 * c)) & 0xFF) - 128;
-        blk[r * 8 + 4 + c] = (int32_t)((v.y >> (8 * c)) & 0xFF) - 128;
-      }
-    }
-  }
-  fdct_islow(blk);
-  int16_t zz[64];
-#pragma unroll
-  for (int k = 0; k < 64; ++k) {
-    const int n = kNatural[k];
-    const int32_t x = blk[n];
-    const uint32_t a = (uint32_t)(x < 0 ? -x : x) + q.half[n];
-    const int32_t qv = (int32_t)__umulhi(a, q.m[n]);
-    zz[k] = (int16_t)(x < 0 ? -qv : qv);
-  }
-  uint64_t nz = 0;
-  uint32_t bits = 0;
-  int run = 0;
-#pragma unroll
-  for (int k = 1; k < 64; ++k) {
-    const int v = zz[k];
-    if (v == 0) {
-      ++run;
-    } else {
-      nz |= 1ull << k;
-      bits += (uint32_t)(run >> 4) * aclen[0xF0];
-      const int n = mag_bits_fast(v);
-      bits += aclen[((run & 15) << 4) + n] + (uint32_t)n;
-      run = 0;
-    }
-  }
-  if (run) bits += aclen[0x00];
-  const size_t bi = (size_t)d.coef_off + b;
-  uint4* dst = reinterpret_cast<uint4*>(w.coef + bi * 64);
-#pragma unroll
-  for (int qd = 0; qd < 8; ++qd) {
-    uint4 v;
-    v.x = (uint16_t)zz[qd * 8 + 0] | ((uint32_t)(uint16_t)zz[qd * 8 + 1] << 16);
-    v.y = (uint16_t)zz[qd * 8 + 2] | ((uint32_t)(uint16_t)zz[qd * 8 + 3] << 16);
-    v.z = (uint16_t)zz[qd * 8 + 4] | ((uint32_t)(uint16_t)zz[qd * 8 + 5] << 16);
-    v.w = (uint16_t)zz[qd * 8 + 6] | ((uint32_t)(uint16_t)zz[qd * 8 + 7] << 16);
-    dst[qd] = v;
-  }
-  w.nzmask[bi] = nz;
-  w.acbits[bi] = bits;
-  w.dc[bi] = zz[0];
+__device__ __forceinline__ int16_t quant_recip(int32_t x, const QuantRecip& q, int n) {
+  const uint32_t a = (uint32_t)(x < 0 ? -x : x) + q.half[n];
+  const int32_t v = (int32_t)__umulhi(a, q.m[n]);
+  return (int16_t)(x < 0 ? -v : v);
 }
 
-__global__ __launch_bounds__(1024) void jpeg_scan_kernel(const JpegDesc* __restrict__ jd, int mcus, JpegWork w,
-                                                         int32_t* __restrict__ out_sizes) {
-  __shared__ uint32_t sh[17];
-  const JpegDesc d = jd[blockIdx.x];
-  const int tid = threadIdx.x;
-  const int per = (mcus + (int)blockDim.x - 1) / (int)blockDim.x;
-  const int m0 = min(tid * per, mcus), m1 = min(m0 + per, mcus);
-  const int16_t* dc = w.dc + d.coef_off;
-  const uint32_t* acb = w.acbits + d.coef_off;
-  const uint32_t chroma_bits = 2u * (hlen(kHuffDcChroma.e[0]) + hlen(kHuffAcChroma.e[0]));
-  uint32_t bits = 0;
-  for (int m = m0; m < m1; ++m) {
+__device__ __forceinline__ int wave_sum_i32(int v) {
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const int b = 4 * m + s;
-      const int diff = (int)dc[b] - (b ? (int)dc[b - 1] : 0);
-      const int n = mag_bits_fast(diff);
-      bits += hlen(kHuffDcLuma.e[n]) + (uint32_t)n + acb[b];
-    }
-    bits += chroma_bits;
-  }
-  uint32_t total = 0;
-  uint32_t pos = block_exclusive_scan(bits, sh, &total);
-  const uint32_t nbytes = (total + 7) >> 3;
-  const bool overflow = nbytes > d.stage_words * 4u || 2u * nbytes + 16u > d.out_cap ||
-                        (nbytes + kStuffChunk - 1) / kStuffChunk > (uint32_t)w.max_chunks;
-  if (tid == 0) {
-    w.total[blockIdx.x] = overflow ? 0xFFFFFFFFu : total;
-    if (overflow) out_sizes[blockIdx.x] = -1;
-  }
-  if (overflow) return;
-  uint32_t* boff = w.boff + d.coef_off;
-  for (int m = m0; m < m1; ++m) {
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const int b = 4 * m + s;
-      boff[b] = pos;
-      const int diff = (int)dc[b] - (b ? (int)dc[b - 1] : 0);
-      const int n = mag_bits_fast(diff);
-      pos += hlen(kHuffDcLuma.e[n]) + (uint32_t)n + acb[b];
-    }
-    pos += chroma_bits;
-  }
-  uint32_t* stage = w.stage + d.stage_off;
-  const uint32_t nwords = (total + 31) >> 5;
-  for (uint32_t i = tid; i < nwords; i += blockDim.x) stage[i] = 0u;
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
 }
 
 struct GBitWriter {
@@ -191,44 +78,202 @@ struct GBitWriter {
   }
 };
 
-__global__ __launch_bounds__(256) void jpeg_emit_kernel(const JpegDesc* __restrict__ jd, int ncanvas, int bpi,
-                                                        JpegWork w) {
+// Look-back status word: hi = state (0 = not yet, 1 = aggregate, 2 = inclusive prefix), lo = bits.
+// The stuffing-count kernel (next in the stream) clears the words again for the next launch.
+// Relaxed agent-scope atomics: the word itself carries the value, nothing else is published
+// through it (the stage bits are consumed by later kernels), and acquire/release would add an L2
+// writeback (buffer_wbl2) per store and an L2 invalidate (buffer_inv) per poll on gfx950.
+__device__ __forceinline__ uint64_t look_load(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void look_store(uint64_t* p, uint32_t state, uint32_t v) {
+  __hip_atomic_store(p, ((uint64_t)state << 32) | v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t sat_add(uint32_t a, uint32_t b) {
+  const uint32_t s = a + b;
+  return s < a ? 0xFFFFFFFFu : s;
+}
+
+constexpr int kJpegWG = 256;     // luma blocks (threads) per workgroup = 64 MCUs
+constexpr int kCoefStride = 33;  // u32 words per thread in LDS (32 zig-zag pairs + 1 pad)
+
+// Single-pass encoder: workgroup L (ordered ticket) encodes blocks [256p, 256p+256) of image i.
+//  1. render (fused 2×) or read the 8×8 block, islow FDCT, reciprocal quantisation;
+//  2. Huffman cost of the block (DC needs the previous block's DC: LDS neighbour, and for the
+//     first block of the workgroup a wave-0 recomputation of the preceding block's DC = Σ(x-128));
+//  3. workgroup exclusive scan of the costs, then a decoupled look-back over the image's earlier
+//     workgroups (tickets are taken in dispatch order, so every predecessor is already resident);
+//  4. each thread writes its block's codes at its bit offset (atomicOr into the zeroed stage).
+// The last workgroup of an image publishes the total (or the overflow marker).
+__global__ __launch_bounds__(kJpegWG) void jpeg_fused_kernel(const uint8_t* __restrict__ canvas,
+                                                             const JpegDesc* __restrict__ jd, int ncanvas, int out_w,
+                                                             int out_h, QuantRecip q, JpegWork w, JpegRenderSrc rs,
+                                                             int32_t* __restrict__ out_sizes) {
   __shared__ uint32_t actab[256];
+  __shared__ uint8_t aclen[256];
   __shared__ uint32_t dctab[16];
-  actab[threadIdx.x] = kHuffAcLuma.e[threadIdx.x];
-  if (threadIdx.x < 16) dctab[threadIdx.x] = kHuffDcLuma.e[threadIdx.x];
-  __syncthreads();
-  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
-  if (gid >= bpi * ncanvas) return;
-  const int img = gid / bpi, b = gid - img * bpi;
-  if (w.total[img] == 0xFFFFFFFFu) return;
-  const JpegDesc d = jd[img];
-  const size_t bi = (size_t)d.coef_off + b;
-  const int16_t* dc = w.dc + d.coef_off;
-  GBitWriter bw(w.stage + d.stage_off, w.boff[bi]);
-  const int diff = (int)dc[b] - (b ? (int)dc[b - 1] : 0);
-  const int n = mag_bits_fast(diff);
-  bw.put_sym(dctab[n]);
-  if (n) bw.put((uint32_t)(diff < 0 ? diff - 1 : diff), n);
-  uint64_t nz = w.nzmask[bi] & ~1ull;
-  const int16_t* cf = w.coef + bi * 64;
-  int last = 0;
-  while (nz) {
-    const int k = __builtin_ctzll(nz);
-    nz &= nz - 1;
-    int run = k - last - 1;
-    while (run > 15) {
-      bw.put_sym(actab[0xF0]);
-      run -= 16;
-    }
-    const int v = cf[k];
-    const int nb = mag_bits_fast(v);
-    bw.put_sym(actab[(run << 4) + nb]);
-    bw.put((uint32_t)(v < 0 ? v - 1 : v), nb);
-    last = k;
+  __shared__ int32_t sdc[kJpegWG];
+  __shared__ uint32_t scoef[kJpegWG * kCoefStride];  // per-thread zig-zag pairs (odd stride: no conflicts)
+  __shared__ uint32_t sh[17];
+  __shared__ uint32_t s_ticket, s_prefix;
+  __shared__ int32_t s_prevdc;
+  const int tid = threadIdx.x;
+  const uint32_t e = kHuffAcLuma.e[tid];
+  actab[tid] = e;
+  aclen[tid] = (uint8_t)hlen(e);
+  if (tid < 16) dctab[tid] = tid < 12 ? kHuffDcLuma.e[tid] : 0u;
+  const int bpi = (out_w >> 3) * (out_h >> 3);
+  const int parts = (bpi + kJpegWG - 1) / kJpegWG;
+  const uint32_t nwg = (uint32_t)(parts * ncanvas);
+  if (tid == 0) {
+    const uint32_t t = atomicAdd(w.ticket, 1u);
+    if (t == nwg - 1) atomicExch(w.ticket, 0u);  // every ticket of this launch is taken
+    s_ticket = t;
   }
-  if (last < 63) bw.put_sym(actab[0x00]);
-  bw.flush();
+  __syncthreads();
+  const int img = (int)(s_ticket / (uint32_t)parts), part = (int)(s_ticket % (uint32_t)parts);
+  const JpegDesc d = jd[img];
+  const int mcux = out_w >> 4;
+  const int b = part * kJpegWG + tid;
+  const bool valid = b < bpi;
+  RenderDesc rd;
+  RWindow win{0.f, 0.f};
+  if (d.render >= 0) {
+    rd = rs.rd[d.render];
+    if (rd.kind != kRenderLabels) win = render_window(rd, rs.stats);
+  }
+  // ---- 1. block → quantised zig-zag coefficients (kept in LDS; nz = non-zero AC mask) -------
+  uint32_t* mycoef = scoef + tid * kCoefStride;
+  uint64_t nz = 0;
+  int dc0 = 0;
+  if (valid) {
+    const int mcu = b >> 2, sub = b & 3;
+    const int bx = 2 * (mcu % mcux) + (sub & 1), by = 2 * (mcu / mcux) + (sub >> 1);
+    int32_t blk[64];
+    if (d.render >= 0) {
+      render_block_2x(rd, rs.raw, rs.f32, rs.bits, win, bx, by, blk);
+#pragma unroll
+      for (int i = 0; i < 64; ++i) blk[i] -= 128;
+    } else {
+      const uint8_t* src = canvas + d.canvas_off + (size_t)(by * 8) * out_w + bx * 8;
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        const uint2 v = *reinterpret_cast<const uint2*>(src + (size_t)r * out_w);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          blk[r * 8 + c] = (int32_t)((v.x >> (8 * c)) & 0xFF) - 128;
+          blk[r * 8 + 4 + c] = (int32_t)((v.y >> (8 * c)) & 0xFF) - 128;
+        }
+      }
+    }
+    fdct_islow(blk);
+#pragma unroll
+    for (int k = 0; k < 64; k += 2) {
+      const int16_t a = quant_recip(blk[kNatural[k]], q, kNatural[k]);
+      const int16_t c = quant_recip(blk[kNatural[k + 1]], q, kNatural[k + 1]);
+      if (k == 0) dc0 = a;
+      nz |= (k > 0 && a != 0 ? 1ull << k : 0ull) | (c != 0 ? 1ull << (k + 1) : 0ull);
+      mycoef[k >> 1] = (uint32_t)(uint16_t)a | ((uint32_t)(uint16_t)c << 16);
+    }
+  }
+  sdc[tid] = dc0;
+  // DC of the block preceding this workgroup's first block (0 at the start of the image).
+  if (tid < 64) {
+    int dcp = 0;
+    if (part > 0) {
+      const int pb = part * kJpegWG - 1;
+      const int mcu = pb >> 2, sub = pb & 3;
+      const int u = 8 * (2 * (mcu % mcux) + (sub & 1)) + (tid & 7);
+      const int v = 8 * (2 * (mcu / mcux) + (sub >> 1)) + (tid >> 3);
+      const int px = d.render >= 0 ? (int)render_pixel(rd, rs.raw, rs.f32, rs.bits, win, u, v)
+                                   : (int)canvas[d.canvas_off + (size_t)v * out_w + u];
+      dcp = quant_recip(wave_sum_i32(px - 128), q, 0);
+    }
+    if (tid == 0) s_prevdc = dcp;
+  }
+  __syncthreads();
+  // ---- 2. Huffman cost ----------------------------------------------------------------------
+  const int diff = dc0 - (tid ? sdc[tid - 1] : s_prevdc);
+  const int dn = mag_bits_fast(diff);
+  uint32_t bits = 0;
+  if (valid) {
+    bits = hlen(dctab[dn]) + (uint32_t)dn;
+    int last = 0;
+    for (uint64_t m = nz; m; m &= m - 1) {
+      const int k = __builtin_ctzll(m);
+      const int v = (int16_t)(mycoef[k >> 1] >> (16 * (k & 1)));
+      const int run = k - last - 1;
+      const int n = mag_bits_fast(v);
+      bits += (uint32_t)(run >> 4) * aclen[0xF0] + aclen[((run & 15) << 4) + n] + (uint32_t)n;
+      last = k;
+    }
+    if (last < 63) bits += aclen[0x00];
+    if ((b & 3) == 3) bits += 2u * (hlen(kHuffDcChroma.e[0]) + hlen(kHuffAcChroma.e[0]));  // Cb, Cr: DC 0 + EOB
+  }
+  // ---- 3. workgroup scan + look-back --------------------------------------------------------
+  uint32_t agg = 0;
+  const uint32_t excl = block_exclusive_scan(bits, sh, &agg);
+  uint64_t* look = w.look + (size_t)img * parts;
+  if (tid == 0) {
+    uint32_t prefix = 0;
+    if (part == 0) {
+      look_store(&look[0], 2u, agg);
+    } else {
+      look_store(&look[part], 1u, agg);
+      int p = part - 1;
+      uint32_t spins = 0;
+      while (p >= 0) {
+        const uint64_t st = look_load(&look[p]);
+        const uint32_t hi = (uint32_t)(st >> 32);
+        if (hi == 0u) {
+          if (++spins > (1u << 26)) {  // cannot happen with ordered tickets; never hang the GPU
+            prefix = 0xFFFFFFFFu;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+          continue;
+        }
+        prefix = sat_add(prefix, (uint32_t)st);
+        if (hi == 2u) break;
+        --p;
+      }
+      look_store(&look[part], 2u, sat_add(prefix, agg));
+    }
+    s_prefix = prefix;
+  }
+  __syncthreads();
+  const uint32_t prefix = s_prefix;
+  const uint32_t end = sat_add(prefix, agg);
+  const uint32_t cap_bits = d.stage_words * 32u;
+  // ---- 4. emission ---------------------------------------------------------------------------
+  if (valid && end <= cap_bits) {
+    GBitWriter bw(w.stage + d.stage_off, prefix + excl);
+    bw.put_sym(dctab[dn]);
+    if (dn) bw.put((uint32_t)(diff < 0 ? diff - 1 : diff), dn);
+    int last = 0;
+    for (uint64_t m = nz; m; m &= m - 1) {
+      const int k = __builtin_ctzll(m);
+      const int v = (int16_t)(mycoef[k >> 1] >> (16 * (k & 1)));
+      int run = k - last - 1;
+      while (run > 15) {
+        bw.put_sym(actab[0xF0]);
+        run -= 16;
+      }
+      const int nb = mag_bits_fast(v);
+      bw.put_sym(actab[(run << 4) + nb]);
+      bw.put((uint32_t)(v < 0 ? v - 1 : v), nb);
+      last = k;
+    }
+    if (last < 63) bw.put_sym(actab[0x00]);
+    bw.flush();
+  }
+  if (part == parts - 1 && tid == 0) {
+    const uint32_t nbytes = (end + 7) >> 3;
+    const bool overflow = end == 0xFFFFFFFFu || end > cap_bits || 2u * nbytes + 16u > d.out_cap ||
+                          (nbytes + kStuffChunk - 1) / kStuffChunk > (uint32_t)w.max_chunks;
+    w.total[img] = overflow ? 0xFFFFFFFFu : end;
+    if (overflow) out_sizes[img] = -1;
+  }
 }
 
 // Byte i of the entropy-coded segment (MSB-first words), final byte padded with 1-bits.
@@ -240,69 +285,113 @@ __device__ __forceinline__ uint32_t seg_byte(const uint32_t* stage, uint32_t i, 
 
 constexpr int kStuffThreads = 256;
 constexpr int kBytesPerThread = kStuffChunk / kStuffThreads;  // 16
+constexpr int kStuffGrid = 512;                               // persistent-style: 2 workgroups per CU
 
-__global__ __launch_bounds__(kStuffThreads) void jpeg_stuff_count_kernel(const JpegDesc* __restrict__ jd, JpegWork w) {
-  __shared__ uint32_t cnt;
-  const int img = blockIdx.y, chunk = blockIdx.x;
-  const uint32_t total = w.total[img];
-  if (total == 0xFFFFFFFFu) return;
-  const uint32_t nbytes = (total + 7) >> 3;
-  const uint32_t c0 = (uint32_t)chunk * kStuffChunk;
-  if (c0 >= nbytes) return;
-  const JpegDesc d = jd[img];
-  const uint32_t* stage = w.stage + d.stage_off;
-  if (threadIdx.x == 0) cnt = 0;
-  __syncthreads();
-  uint32_t ff = 0;
-  const uint32_t b0 = c0 + threadIdx.x * kBytesPerThread;
-  for (int k = 0; k < kBytesPerThread; ++k) {
-    const uint32_t i = b0 + k;
-    if (i < nbytes) ff += seg_byte(stage, i, nbytes, total & 7u) == 0xFFu;
+// Bytes of the largest image of the launch (an overflowed image forces the full sweep: its
+// partially written stage must be cleared). Every workgroup reduces the ≤ few hundred totals.
+__device__ __forceinline__ uint32_t launch_max_bytes(const JpegWork& w, int ncanvas, uint32_t* sh) {
+  uint32_t m = 0;
+  for (int i = threadIdx.x; i < ncanvas; i += blockDim.x) {
+    const uint32_t t = w.total[i];
+    m = max(m, t == 0xFFFFFFFFu ? 0x7FFFFFFFu : (t + 7) >> 3);
   }
-  if (ff) atomicAdd(&cnt, ff);
+  m = wave_max_u32(m);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = m;
   __syncthreads();
-  if (threadIdx.x == 0) w.chunk_ff[(size_t)img * w.max_chunks + chunk] = cnt;
+  uint32_t r = 0;
+  for (int i = 0; i < (int)(blockDim.x >> 6); ++i) r = max(r, sh[i]);
+  __syncthreads();
+  return r;
 }
 
-__global__ __launch_bounds__(kStuffThreads) void jpeg_stuff_write_kernel(const JpegDesc* __restrict__ jd, JpegWork w,
-                                                                         uint8_t* __restrict__ out,
+// Work items are (chunk, image) in chunk-major order, so the valid chunks of every image come first
+// and the grid-stride loop stops at the largest image instead of sweeping max_chunks × images.
+__global__ __launch_bounds__(kStuffThreads) void jpeg_stuff_count_kernel(const JpegDesc* __restrict__ jd, int ncanvas,
+                                                                         JpegWork w) {
+  __shared__ uint32_t cnt;
+  __shared__ uint32_t shm[16];
+  // The encoder's look-back words are done with: clear them for the next launch.
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < w.look_used; i += (size_t)gridDim.x * blockDim.x)
+    w.look[i] = 0ull;
+  const uint32_t maxb = launch_max_bytes(w, ncanvas, shm);
+  const int n = ncanvas * w.max_chunks;
+  for (int it = blockIdx.x; it < n; it += gridDim.x) {
+    const int chunk = it / ncanvas, img = it - chunk * ncanvas;
+    const uint32_t c0 = (uint32_t)chunk * kStuffChunk;
+    if (c0 >= maxb) break;
+    const uint32_t total = w.total[img];
+    if (total == 0xFFFFFFFFu) continue;
+    const uint32_t nbytes = (total + 7) >> 3;
+    if (c0 >= nbytes) continue;
+    const uint32_t* stage = w.stage + jd[img].stage_off;
+    if (threadIdx.x == 0) cnt = 0;
+    __syncthreads();
+    uint32_t ff = 0;
+    const uint32_t b0 = c0 + threadIdx.x * kBytesPerThread;
+#pragma unroll
+    for (int k = 0; k < kBytesPerThread; ++k) {
+      const uint32_t i = b0 + k;
+      if (i < nbytes) ff += seg_byte(stage, i, nbytes, total & 7u) == 0xFFu;
+    }
+    if (ff) atomicAdd(&cnt, ff);
+    __syncthreads();
+    if (threadIdx.x == 0) w.chunk_ff[(size_t)img * w.max_chunks + chunk] = cnt;
+  }
+}
+
+// Writes the stuffed chunk into host-mapped memory and clears the stage words it consumed, so the
+// stage is all-zero again for the next launch (the encoder ORs bits into it).
+__global__ __launch_bounds__(kStuffThreads) void jpeg_stuff_write_kernel(const JpegDesc* __restrict__ jd, int ncanvas,
+                                                                         JpegWork w, uint8_t* __restrict__ out,
                                                                          int32_t* __restrict__ out_sizes) {
   __shared__ uint32_t sh[17];
   __shared__ uint8_t buf[2 * kStuffChunk];
-  const int img = blockIdx.y, chunk = blockIdx.x;
-  const uint32_t total = w.total[img];
-  if (total == 0xFFFFFFFFu) return;
-  const uint32_t nbytes = (total + 7) >> 3;
-  const uint32_t c0 = (uint32_t)chunk * kStuffChunk;
-  if (c0 >= nbytes) return;
-  const JpegDesc d = jd[img];
-  const uint32_t* stage = w.stage + d.stage_off;
-  const uint32_t* ffc = w.chunk_ff + (size_t)img * w.max_chunks;
-  // Output offset of this chunk = bytes before it + 0xFF stuffing inserted before it.
-  uint32_t before = 0;
-  for (int c = 0; c < chunk; ++c) before += ffc[c];
-  const uint32_t obase = c0 + before;
-  const uint32_t b0 = c0 + threadIdx.x * kBytesPerThread;
-  uint32_t v[kBytesPerThread];
-  uint32_t mine = 0;
+  const uint32_t maxb = launch_max_bytes(w, ncanvas, sh);
+  const int n = ncanvas * w.max_chunks;
+  for (int it = blockIdx.x; it < n; it += gridDim.x) {
+    const int chunk = it / ncanvas, img = it - chunk * ncanvas;
+    const uint32_t c0 = (uint32_t)chunk * kStuffChunk;
+    if (c0 >= maxb) break;
+    const JpegDesc d = jd[img];
+    uint32_t* stage = w.stage + d.stage_off;
+    const uint32_t total = w.total[img];
+    if (total == 0xFFFFFFFFu) {  // overflowed image (rare): clear whatever the encoder wrote
+      for (uint32_t i = c0 / 4 + threadIdx.x; i < (c0 + kStuffChunk) / 4 && i < d.stage_words; i += blockDim.x)
+        stage[i] = 0u;
+      continue;
+    }
+    const uint32_t nbytes = (total + 7) >> 3;
+    if (c0 >= nbytes) continue;
+    const uint32_t* ffc = w.chunk_ff + (size_t)img * w.max_chunks;
+    // Output offset of this chunk = bytes before it + 0xFF stuffing inserted before it.
+    uint32_t before = 0;
+    for (int c = 0; c < chunk; ++c) before += ffc[c];
+    const uint32_t obase = c0 + before;
+    const uint32_t b0 = c0 + threadIdx.x * kBytesPerThread;
+    uint32_t v[kBytesPerThread];
+    uint32_t mine = 0;
 #pragma unroll
-  for (int k = 0; k < kBytesPerThread; ++k) {
-    const uint32_t i = b0 + k;
-    v[k] = i < nbytes ? seg_byte(stage, i, nbytes, total & 7u) : 0x100u;  // 0x100 = past the end
-    mine += v[k] < 0x100u ? (v[k] == 0xFFu ? 2u : 1u) : 0u;
-  }
-  uint32_t chunk_len = 0;
-  uint32_t o = block_exclusive_scan(mine, sh, &chunk_len);
+    for (int k = 0; k < kBytesPerThread; ++k) {
+      const uint32_t i = b0 + k;
+      v[k] = i < nbytes ? seg_byte(stage, i, nbytes, total & 7u) : 0x100u;  // 0x100 = past the end
+      mine += v[k] < 0x100u ? (v[k] == 0xFFu ? 2u : 1u) : 0u;
+    }
+    uint32_t chunk_len = 0;
+    uint32_t o = block_exclusive_scan(mine, sh, &chunk_len);  // ends with a barrier: stage reads done
 #pragma unroll
-  for (int k = 0; k < kBytesPerThread; ++k) {
-    if (v[k] >= 0x100u) continue;
-    buf[o++] = (uint8_t)v[k];
-    if (v[k] == 0xFFu) buf[o++] = 0;
+    for (int k = 0; k < kBytesPerThread; ++k) {
+      if (v[k] >= 0x100u) continue;
+      buf[o++] = (uint8_t)v[k];
+      if (v[k] == 0xFFu) buf[o++] = 0;
+    }
+    const uint32_t w0 = c0 / 4, w1 = min((nbytes + 3) / 4, (c0 + kStuffChunk) / 4);
+    for (uint32_t i = w0 + threadIdx.x; i < w1; i += blockDim.x) stage[i] = 0u;
+    __syncthreads();
+    uint8_t* dst = out + d.out_off + obase;
+    for (uint32_t i = threadIdx.x; i < chunk_len; i += blockDim.x) dst[i] = buf[i];
+    if (c0 + kStuffChunk >= nbytes && threadIdx.x == 0) out_sizes[img] = (int32_t)(obase + chunk_len);
+    __syncthreads();  // buf is reused by the next iteration
   }
-  __syncthreads();
-  uint8_t* dst = out + d.out_off + obase;
-  for (uint32_t i = threadIdx.x; i < chunk_len; i += blockDim.x) dst[i] = buf[i];
-  if (c0 + kStuffChunk >= nbytes && threadIdx.x == 0) out_sizes[img] = (int32_t)(obase + chunk_len);
 }
 
 bool render_is_exact_2x(const RenderDesc& r, int out_w, int out_h) {
@@ -311,10 +400,11 @@ bool render_is_exact_2x(const RenderDesc& r, int out_w, int out_h) {
 }
 
 void launch_jpeg(const uint8_t* canvas, const JpegDesc* jd, int ncanvas, int out_w, int out_h, const int32_t* div_luma,
-                 const JpegWork& w, uint8_t* out, int32_t* out_sizes, hipStream_t stream, const JpegRenderSrc* fused) {
+                 JpegWork& w, uint8_t* out, int32_t* out_sizes, hipStream_t stream, const JpegRenderSrc* fused) {
   if (ncanvas <= 0) return;
   if (out_w % 16 || out_h % 16) throw DeviceError("GPU JPEG encoder needs canvas dims that are multiples of 16");
-  if (w.max_chunks <= 0 || !w.boff || !w.total || !w.chunk_ff) throw DeviceError("launch_jpeg: JpegWork incomplete");
+  if (w.max_chunks <= 0 || !w.total || !w.chunk_ff || !w.stage || !w.look || !w.ticket)
+    throw DeviceError("launch_jpeg: JpegWork incomplete");
   QuantRecip q;
   for (int i = 0; i < 64; ++i) {
     const uint32_t dv = (uint32_t)div_luma[i];
@@ -324,17 +414,14 @@ void launch_jpeg(const uint8_t* canvas, const JpegDesc* jd, int ncanvas, int out
   JpegRenderSrc rs;
   if (fused) rs = *fused;
   const int bpi = (out_w / 8) * (out_h / 8);
-  const int nblk = bpi * ncanvas;
-  jpeg_block_kernel<<<(nblk + 255) / 256, 256, 0, stream>>>(canvas, jd, ncanvas, out_w, out_h, q, w, rs);
-  check_launch("jpeg_block_kernel");
-  jpeg_scan_kernel<<<ncanvas, 1024, 0, stream>>>(jd, (out_w / 16) * (out_h / 16), w, out_sizes);
-  check_launch("jpeg_scan_kernel");
-  jpeg_emit_kernel<<<(nblk + 255) / 256, 256, 0, stream>>>(jd, ncanvas, bpi, w);
-  check_launch("jpeg_emit_kernel");
-  dim3 sg(w.max_chunks, ncanvas);
-  jpeg_stuff_count_kernel<<<sg, kStuffThreads, 0, stream>>>(jd, w);
+  const int parts = (bpi + kJpegWG - 1) / kJpegWG;
+  if ((size_t)parts * ncanvas > w.look_cap) throw DeviceError("launch_jpeg: look-back capacity exceeded");
+  w.look_used = (size_t)parts * ncanvas;
+  jpeg_fused_kernel<<<parts * ncanvas, kJpegWG, 0, stream>>>(canvas, jd, ncanvas, out_w, out_h, q, w, rs, out_sizes);
+  check_launch("jpeg_fused_kernel");
+  jpeg_stuff_count_kernel<<<kStuffGrid, kStuffThreads, 0, stream>>>(jd, ncanvas, w);
   check_launch("jpeg_stuff_count_kernel");
-  jpeg_stuff_write_kernel<<<sg, kStuffThreads, 0, stream>>>(jd, w, out, out_sizes);
+  jpeg_stuff_write_kernel<<<kStuffGrid, kStuffThreads, 0, stream>>>(jd, ncanvas, w, out, out_sizes);
   check_launch("jpeg_stuff_write_kernel");
 }
 

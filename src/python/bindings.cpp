@@ -588,14 +588,12 @@ PYBIND11_MODULE(_nm03, m) {
     for (int i = 0; i < n; ++i) {
       std::memset(&jd[i], 0, sizeof(jd[i]));
       jd[i].canvas_off = (uint32_t)((size_t)i * w * h);
-      jd[i].coef_off = (uint32_t)(i * blocks);
       jd[i].stage_off = (uint32_t)(i * (stage_bytes / 4));
       jd[i].stage_words = stage_bytes / 4;
       jd[i].out_off = (uint64_t)i * out_cap;
       jd[i].out_cap = out_cap;
       jd[i].render = -1;
     }
-    const size_t nb = (size_t)n * blocks;
     size_t off = 0;
     auto take = [&](size_t bytes) {
       size_t o = off;
@@ -603,19 +601,19 @@ PYBIND11_MODULE(_nm03, m) {
       return o;
     };
     const int max_chunks = (int)(stage_bytes / gpu::kStuffChunk);
-    const size_t o_jd = take(sizeof(gpu::JpegDesc) * n), o_coef = take(nb * 128), o_nz = take(nb * 8), o_ac = take(nb * 4),
-                 o_dc = take(nb * 2), o_stage = take((size_t)n * stage_bytes), o_boff = take(nb * 4),
+    const size_t look_cap = (size_t)n * ((blocks + 255) / 256);
+    const size_t o_jd = take(sizeof(gpu::JpegDesc) * n), o_stage = take((size_t)n * stage_bytes),
+                 o_look = take(look_cap * 8), o_ticket = take(8), o_zero_end = off,
                  o_tot = take((size_t)n * 4), o_cff = take((size_t)n * max_chunks * 4),
                  o_out = take((size_t)n * out_cap), o_sz = take((size_t)n * 4);
     uint8_t* dev = (uint8_t*)scratch().get(off);
     gpu::check_hip(hipMemcpyAsync(dev + o_jd, jd.data(), sizeof(gpu::JpegDesc) * n, hipMemcpyHostToDevice, st), "H2D");
+    gpu::check_hip(hipMemsetAsync(dev + o_stage, 0, o_zero_end - o_stage, st), "memset jpeg work");
     gpu::JpegWork wk;
-    wk.coef = (int16_t*)(dev + o_coef);
-    wk.nzmask = (uint64_t*)(dev + o_nz);
-    wk.acbits = (uint32_t*)(dev + o_ac);
-    wk.dc = (int16_t*)(dev + o_dc);
     wk.stage = (uint32_t*)(dev + o_stage);
-    wk.boff = (uint32_t*)(dev + o_boff);
+    wk.look = (uint64_t*)(dev + o_look);
+    wk.look_cap = look_cap;
+    wk.ticket = (uint32_t*)(dev + o_ticket);
     wk.total = (uint32_t*)(dev + o_tot);
     wk.chunk_ff = (uint32_t*)(dev + o_cff);
     wk.max_chunks = max_chunks;

@@ -88,8 +88,8 @@ void hip_free_all(Slot& s) {
   if (s.h_out) (void)hipHostFree(s.h_out);
   if (s.h_sizes) (void)hipHostFree(s.h_sizes);
   for (void* p : {(void*)s.d_blob, (void*)s.d_med, (void*)s.d_f32, (void*)s.d_bits, (void*)s.d_canvas,
-                  (void*)s.jw.coef, (void*)s.jw.nzmask, (void*)s.jw.acbits, (void*)s.jw.dc, (void*)s.jw.stage,
-                  (void*)s.jw.boff, (void*)s.jw.total, (void*)s.jw.chunk_ff})
+                  (void*)s.jw.stage, (void*)s.jw.look, (void*)s.jw.ticket,
+                  (void*)s.jw.total, (void*)s.jw.chunk_ff})
     if (p) (void)hipFree(p);
   for (auto& kv : s.graphs) (void)hipGraphExecDestroy(kv.second);
   s.graphs.clear();
@@ -214,15 +214,17 @@ struct Engine::Impl {
       const size_t canvas_bytes = (size_t)cw * ch;
       const size_t blocks = canvas_bytes / 64;
       s.d_canvas = dmalloc<uint8_t>(canvas_bytes * s.cap_canvases, "hipMalloc canvas");
-      s.jw.coef = dmalloc<int16_t>(blocks * 64 * s.cap_canvases, "hipMalloc coef");
-      s.jw.nzmask = dmalloc<uint64_t>(blocks * s.cap_canvases, "hipMalloc nz");
-      s.jw.acbits = dmalloc<uint32_t>(blocks * s.cap_canvases, "hipMalloc acbits");
-      s.jw.dc = dmalloc<int16_t>(blocks * s.cap_canvases, "hipMalloc dc");
       s.jw.stage = dmalloc<uint32_t>((size_t)kStageBytes / 4 * s.cap_canvases, "hipMalloc stage");
-      s.jw.boff = dmalloc<uint32_t>(blocks * s.cap_canvases, "hipMalloc boff");
+      s.jw.look_cap = (size_t)s.cap_canvases * ((blocks + 255) / 256);
+      s.jw.look = dmalloc<uint64_t>(s.jw.look_cap, "hipMalloc look-back");
+      s.jw.ticket = dmalloc<uint32_t>(1, "hipMalloc ticket");
       s.jw.total = dmalloc<uint32_t>(s.cap_canvases, "hipMalloc total");
       s.jw.max_chunks = (int)(kStageBytes / kStuffChunk);
       s.jw.chunk_ff = dmalloc<uint32_t>((size_t)s.jw.max_chunks * s.cap_canvases, "hipMalloc chunk_ff");
+      // The encoder ORs bits into the stage and polls look-back states: both start clear.
+      check_hip(hipMemset(s.jw.stage, 0, (size_t)kStageBytes * s.cap_canvases), "memset stage");
+      check_hip(hipMemset(s.jw.look, 0, s.jw.look_cap * sizeof(uint64_t)), "memset look-back");
+      check_hip(hipMemset(s.jw.ticket, 0, sizeof(uint32_t)), "memset ticket");
       check_hip(hipHostMalloc((void**)&s.h_out, (size_t)kOutCap * s.cap_canvases, hipHostMallocMapped),
                 "hipHostMalloc out");
       check_hip(hipHostGetDevicePointer((void**)&s.d_out, s.h_out, 0), "hipHostGetDevicePointer out");
@@ -306,7 +308,6 @@ struct Engine::Impl {
     s.max_w = s.max_h = 0;
     const int cw = cfg.render.out_width, ch = cfg.render.out_height;
     const uint32_t canvas_bytes = (uint32_t)(cw * ch);
-    const uint32_t blocks = canvas_bytes / 64;
     const uint8_t fill = opacity_u8(cfg.render.label_opacity), bval = opacity_u8(cfg.render.border_opacity);
     for (int c = 0; c < nl; ++c) {
       const LoadedSlice& L = s.loaded[s.live[c]];
@@ -381,7 +382,6 @@ struct Engine::Impl {
       JpegDesc& j = jd[k];
       std::memset(&j, 0, sizeof(j));
       j.canvas_off = (uint32_t)k * canvas_bytes;
-      j.coef_off = (uint32_t)k * blocks;
       j.stage_off = (uint32_t)k * (kStageBytes / 4);
       j.stage_words = kStageBytes / 4;
       j.out_off = (uint64_t)k * kOutCap;
