@@ -97,11 +97,11 @@ def main():
     cfg = nm.PipelineConfig(batch_size=args.batch_size, streams=args.streams, threads=args.threads,
                             device=ctx.local_rank, graphs=args.graphs)
     engine = n.Engine(cfg.engine_config())
+    work = n.WorkList(mine)  # the shard's work list in native form (built once, like the plan)
     for _ in range(args.warmup):
-        st, _ = engine.run(mine)
-    bad = sum(1 for s in st if s[0] != 0) if args.warmup else 0
-    if bad:
-        raise SystemExit(f"rank {ctx.rank}: {bad} slices failed in warmup: {st[:3]}")
+        codes, msgs, _ = engine.run_list(work)
+        if msgs:
+            raise SystemExit(f"rank {ctx.rank}: {len(msgs)} slices failed in warmup: {list(msgs.items())[:3]}")
 
     barrier(ctx)
     torch.cuda.synchronize()
@@ -110,8 +110,8 @@ def main():
     stage = {"load_s": 0.0, "h2d_s": 0.0, "kernels_s": 0.0, "write_s": 0.0}
     for _ in range(args.steps):
         with _roctx_range("bench.step"):
-            st, times = engine.run(mine)
-        ok += sum(1 for s in st if s[0] == 0)
+            codes, msgs, times = engine.run_list(work)
+        ok += len(codes) - len(msgs)
         for k in stage:
             stage[k] += times[k]
     torch.cuda.synchronize()

@@ -460,11 +460,38 @@ PYBIND11_MODULE(_nm03, m) {
   });
 
   // ---- engine --------------------------------------------------------------------------------------
+  // A work list converted once to its native form (the cohort plan), reusable across runs.
+  struct WorkList {
+    std::vector<WorkItem> items;
+  };
+  py::class_<WorkList>(m, "WorkList")
+      .def(py::init([](const std::vector<std::pair<std::string, std::string>>& items) {
+        WorkList w;
+        w.items.reserve(items.size());
+        for (auto& p : items) w.items.push_back({p.first, p.second});
+        return w;
+      }))
+      .def("__len__", [](const WorkList& w) { return w.items.size(); });
+  auto times_dict = [](const StageTimes& t) {
+    py::dict td;
+    td["load_s"] = t.load_s;
+    td["h2d_s"] = t.h2d_s;
+    td["kernels_s"] = t.kernels_s;
+    td["write_s"] = t.write_s;
+    td["wall_s"] = t.wall_s;
+    td["batches"] = t.batches;
+    td["slices_ok"] = t.slices_ok;
+    td["slices_failed"] = t.slices_failed;
+    td["bytes_in"] = t.bytes_in;
+    td["bytes_out"] = t.bytes_out;
+    td["jpeg_fallbacks"] = t.jpeg_fallbacks;
+    return td;
+  };
   py::class_<Engine>(m, "Engine")
       .def(py::init<const EngineConfig&>())
       .def(
           "run",
-          [](Engine& e, const std::vector<std::pair<std::string, std::string>>& items) {
+          [times_dict](Engine& e, const std::vector<std::pair<std::string, std::string>>& items) {
             std::vector<WorkItem> wi;
             for (auto& p : items) wi.push_back({p.first, p.second});
             StageTimes t;
@@ -475,19 +502,26 @@ PYBIND11_MODULE(_nm03, m) {
             }
             std::vector<std::pair<int, std::string>> out;
             for (auto& s : st) out.push_back({s.code, s.message});
-            py::dict td;
-            td["load_s"] = t.load_s;
-            td["h2d_s"] = t.h2d_s;
-            td["kernels_s"] = t.kernels_s;
-            td["write_s"] = t.write_s;
-            td["wall_s"] = t.wall_s;
-            td["batches"] = t.batches;
-            td["slices_ok"] = t.slices_ok;
-            td["slices_failed"] = t.slices_failed;
-            td["bytes_in"] = t.bytes_in;
-            td["bytes_out"] = t.bytes_out;
-            td["jpeg_fallbacks"] = t.jpeg_fallbacks;
-            return py::make_tuple(out, td);
+            return py::make_tuple(out, times_dict(t));
+          })
+      .def(
+          "run_list",
+          // Compact form for hot loops: (codes int32[n], {index: message} for non-OK slices, times).
+          [times_dict](Engine& e, const WorkList& wl) {
+            StageTimes t;
+            std::vector<SliceStatus> st;
+            {
+              py::gil_scoped_release nogil;
+              st = e.run(wl.items, &t);
+            }
+            py::array_t<int32_t> codes((py::ssize_t)st.size());
+            auto c = codes.mutable_unchecked<1>();
+            py::dict msgs;
+            for (size_t i = 0; i < st.size(); ++i) {
+              c((py::ssize_t)i) = st[i].code;
+              if (st[i].code != kSliceOk) msgs[py::int_(i)] = st[i].message;
+            }
+            return py::make_tuple(codes, msgs, times_dict(t));
           })
       .def("run_single",
            [](Engine& e, py::array_t<uint16_t, py::array::c_style | py::array::forcecast> raw, const std::string& type,

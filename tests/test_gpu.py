@@ -266,6 +266,11 @@ def test_engine_fault_isolation(native, tmp_path):
     assert "too small" in st[2][1]
     assert sorted(p.name for p in out.iterdir()) == ["1-1_original.jpg", "1-1_processed.jpg", "1-4_original.jpg",
                                                      "1-4_processed.jpg"]
+    # compact hot-loop form: same codes, messages only for the failures
+    eng = native.Engine(nm.PipelineConfig(batch_size=2, streams=2, threads=2).engine_config())
+    codes, msgs, t2 = eng.run_list(native.WorkList(items))
+    assert codes.tolist() == [0, 1, 2, 0] and sorted(msgs) == [1, 2] and "too small" in msgs[2]
+    assert t2["slices_ok"] == 2 and t2["slices_failed"] == 2
 
 
 # ---------------------------------------------------------------------------------------------

@@ -40,8 +40,10 @@ def main():
     if not os.path.exists(os.path.join(a.data_root, ".complete")):
         n.synth_cohort(a.data_root, threads=16)
         open(os.path.join(a.data_root, ".complete"), "w").close()
-    print(json.dumps({"h2d_pinned_GBps": round(h2d_probe(), 2)}), flush=True)
-    items = plan_cohort(a.data_root, a.out_root).items
+    cpu_max = open("/sys/fs/cgroup/cpu.max").read().strip() if os.path.exists("/sys/fs/cgroup/cpu.max") else "n/a"
+    print(json.dumps({"h2d_pinned_GBps": round(h2d_probe(), 2), "cgroup_cpu_max": cpu_max,
+                      "affinity_cpus": len(os.sched_getaffinity(0))}), flush=True)
+    items = n.WorkList(plan_cohort(a.data_root, a.out_root).items)
     bs, ss, ts = (list(map(int, g.split(","))) for g in a.grid.split(":"))
     for b in bs:
         for s in ss:
@@ -49,11 +51,11 @@ def main():
                 cfg = nm.PipelineConfig(batch_size=b, streams=s, threads=t)
                 eng = n.Engine(cfg.engine_config())
                 for _ in range(2):
-                    eng.run(items)
+                    eng.run_list(items)
                 t0 = time.perf_counter()
                 agg = {"load_s": 0.0, "h2d_s": 0.0, "kernels_s": 0.0, "write_s": 0.0}
                 for _ in range(a.steps):
-                    st, tm = eng.run(items)
+                    _, _, tm = eng.run_list(items)
                     for k in agg:
                         agg[k] += tm[k]
                 dt = (time.perf_counter() - t0) / a.steps
