@@ -95,7 +95,7 @@ def main():
     mine = items[lo:hi]
 
     cfg = nm.PipelineConfig(batch_size=args.batch_size, streams=args.streams, threads=args.threads,
-                            device=ctx.local_rank, graphs=args.graphs)
+                            device=ctx.device_index, graphs=args.graphs)
     engine = n.Engine(cfg.engine_config())
     work = n.WorkList(mine)  # the shard's work list in native form (built once, like the plan)
     for _ in range(args.warmup):

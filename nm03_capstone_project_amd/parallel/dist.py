@@ -20,18 +20,28 @@ class DistContext:
     def is_root(self):
         return self.rank == 0
 
+    @property
+    def device_index(self):
+        """HIP device of this rank (the local rank unless NM03_DEVICE_OVERRIDE is set)."""
+        return self.device.index if (self.device is not None and self.device.type == "cuda") else 0
+
 
 def init_from_env(backend=None, use_gpu=None):
-    """Initialise the default process group when WORLD_SIZE > 1; always returns a DistContext."""
+    """Initialise the default process group when WORLD_SIZE > 1; always returns a DistContext.
+
+    Rehearsal overrides (several ranks on a one-GPU box): NM03_DIST_BACKEND=gloo selects the
+    collective backend, NM03_DEVICE_OVERRIDE=<i> pins every rank to device i (RCCL refuses two
+    ranks on one device, gloo does not)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
     if use_gpu is None:
         use_gpu = torch.cuda.is_available()
-    dev = torch.device("cuda", local) if use_gpu else torch.device("cpu")
+    dev_index = int(os.environ.get("NM03_DEVICE_OVERRIDE", local))
+    dev = torch.device("cuda", dev_index) if use_gpu else torch.device("cpu")
     if use_gpu:
-        torch.cuda.set_device(local)
-    be = backend or ("nccl" if use_gpu else "gloo")
+        torch.cuda.set_device(dev_index)
+    be = backend or os.environ.get("NM03_DIST_BACKEND") or ("nccl" if use_gpu else "gloo")
     if world > 1 and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         kw = {"device_id": dev} if (be == "nccl" and use_gpu) else {}
