@@ -33,7 +33,10 @@ from nm03_capstone_project_amd.parallel.cohort_runner import CohortPlan  # noqa:
 from nm03_capstone_project_amd.parallel.dist import shard_bounds  # noqa: E402
 
 METRIC = "DICOM slices/sec through full pipeline (T1+C cohort) at 1/2/4/8 MI355X"
-BASELINE_SLICES_PER_S = None  # the reference publishes no number
+# The reference publishes no number; BASELINE.md defines the comparison point as the measured
+# reference-equivalent CPU run of the same cohort (golden model, 16 threads, batch 25, serial
+# export: profiles/baselines/c3_cpu.json).
+BASELINE_SLICES_PER_S = 171.43
 
 
 class _roctx_range:

@@ -29,12 +29,24 @@ def h2d_probe(mb=64, reps=10):
     return mb * reps / 1024 / (time.perf_counter() - t)
 
 
+def throttled():
+    """cgroup v2 CPU throttling so far (µs); 0 when unavailable."""
+    try:
+        for line in open("/sys/fs/cgroup/cpu.stat"):
+            if line.startswith("throttled_usec"):
+                return int(line.split()[1])
+    except OSError:
+        pass
+    return 0
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=8)
     ap.add_argument("--grid", default="32,64,128:2,3,4,6:16,24")
     ap.add_argument("--data-root", default="/tmp/nm03_bench_data")
     ap.add_argument("--out-root", default="/tmp/nm03_sweep_out")
+    ap.add_argument("--repeat", type=int, default=1, help="measurements per configuration")
     a = ap.parse_args()
     n = nm.native()
     if not os.path.exists(os.path.join(a.data_root, ".complete")):
@@ -52,16 +64,20 @@ def main():
                 eng = n.Engine(cfg.engine_config())
                 for _ in range(2):
                     eng.run_list(items)
-                t0 = time.perf_counter()
-                agg = {"load_s": 0.0, "h2d_s": 0.0, "kernels_s": 0.0, "write_s": 0.0}
-                for _ in range(a.steps):
-                    _, _, tm = eng.run_list(items)
-                    for k in agg:
-                        agg[k] += tm[k]
-                dt = (time.perf_counter() - t0) / a.steps
-                print(json.dumps({"batch": b, "streams": s, "threads": t, "ms_per_step": round(dt * 1e3, 3),
-                                  "slices_per_s": round(len(items) / dt, 1),
-                                  **{k: round(v / a.steps * 1e3, 3) for k, v in agg.items()}}), flush=True)
+                for _ in range(a.repeat):
+                    thr0 = throttled()
+                    t0 = time.perf_counter()
+                    agg = {"load_s": 0.0, "h2d_s": 0.0, "kernels_s": 0.0, "write_s": 0.0}
+                    for _ in range(a.steps):
+                        _, _, tm = eng.run_list(items)
+                        for k in agg:
+                            agg[k] += tm[k]
+                    dt = (time.perf_counter() - t0) / a.steps
+                    thr1 = throttled()
+                    print(json.dumps({"batch": b, "streams": s, "threads": t, "ms_per_step": round(dt * 1e3, 3),
+                                      "slices_per_s": round(len(items) / dt, 1),
+                                      "throttled_ms": round((thr1 - thr0) / 1e3, 2),
+                                      **{k: round(v / a.steps * 1e3, 3) for k, v in agg.items()}}), flush=True)
                 del eng
 
 
