@@ -144,7 +144,7 @@ NM03_HD uint8_t gray_u8(float v, float lo, float inv) {
   g = g > 1.0f ? 1.0f : g;
   float t = g * 255.0f;
   t = t + 0.5f;
-  return (uint8_t)(int)floorf(t);
+  return (uint8_t)(int)t;  // t ∈ [0.5, 255.5]: truncation == floor
 }
 
 // Bilinear lerp in the order: rows first, then between rows.

@@ -19,6 +19,8 @@
 //                        64-byte-coalesced stores straight into host-mapped pinned memory.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "device_util.h"
 #include "nm03/gpu_types.h"
 #include "nm03/jpeg_common.h"
@@ -95,7 +97,11 @@ __device__ __forceinline__ uint32_t sat_add(uint32_t a, uint32_t b) {
 }
 
 constexpr int kJpegWG = 256;     // luma blocks (threads) per workgroup = 64 MCUs
-constexpr int kCoefStride = 33;  // u32 words per thread in LDS (32 zig-zag pairs + 1 pad)
+constexpr int kCoefStride = 32;  // u32 words per thread in LDS: 32 zig-zag pairs, XOR-swizzled
+// Pair p of thread t lives at word t*32 + (p ^ (t & 31)): the unrolled stores (same p in every
+// lane) spread over the banks without the padding word, keeping the workgroup at 34 KiB of LDS
+// (4 workgroups per CU).
+__device__ __forceinline__ int coef_slot(int p, int t) { return p ^ (t & 31); }
 
 // Single-pass encoder: workgroup L (ordered ticket) encodes blocks [256p, 256p+256) of image i.
 //  1. render (fused 2×) or read the 8×8 block, islow FDCT, reciprocal quantisation;
@@ -105,19 +111,23 @@ constexpr int kCoefStride = 33;  // u32 words per thread in LDS (32 zig-zag pair
 //     workgroups (tickets are taken in dispatch order, so every predecessor is already resident);
 //  4. each thread writes its block's codes at its bit offset (atomicOr into the zeroed stage).
 // The last workgroup of an image publishes the total (or the overflow marker).
-__global__ __launch_bounds__(kJpegWG) void jpeg_fused_kernel(const uint8_t* __restrict__ canvas,
+__global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(4))) void jpeg_fused_kernel(const uint8_t* __restrict__ canvas,
                                                              const JpegDesc* __restrict__ jd, int ncanvas, int out_w,
                                                              int out_h, QuantRecip q, JpegWork w, JpegRenderSrc rs,
-                                                             int32_t* __restrict__ out_sizes) {
+                                                             int32_t* __restrict__ out_sizes, int dbg) {
   __shared__ uint32_t actab[256];
   __shared__ uint8_t aclen[256];
   __shared__ uint32_t dctab[16];
   __shared__ int32_t sdc[kJpegWG];
-  __shared__ uint32_t scoef[kJpegWG * kCoefStride];  // per-thread zig-zag pairs (odd stride: no conflicts)
+  __shared__ uint32_t scoef[kJpegWG * kCoefStride];  // per-thread zig-zag pairs
   __shared__ uint32_t sh[17];
   __shared__ uint32_t s_ticket, s_prefix;
   __shared__ int32_t s_prevdc;
   const int tid = threadIdx.x;
+  if (dbg == 8) {  // profiling variant: empty workgroup
+    if (tid == 999) w.total[0] = 1u;
+    return;
+  }
   const uint32_t e = kHuffAcLuma.e[tid];
   actab[tid] = e;
   aclen[tid] = (uint8_t)hlen(e);
@@ -126,12 +136,21 @@ __global__ __launch_bounds__(kJpegWG) void jpeg_fused_kernel(const uint8_t* __re
   const int parts = (bpi + kJpegWG - 1) / kJpegWG;
   const uint32_t nwg = (uint32_t)(parts * ncanvas);
   if (tid == 0) {
-    const uint32_t t = atomicAdd(w.ticket, 1u);
-    if (t == nwg - 1) atomicExch(w.ticket, 0u);  // every ticket of this launch is taken
+    uint32_t t = blockIdx.x;
+    if (dbg == 9) {  // ordered tickets instead of the dispatch index (A/B)
+      t = atomicAdd(w.ticket, 1u);
+      if (t == nwg - 1) atomicExch(w.ticket, 0u);  // every ticket of this launch is taken
+    }
     s_ticket = t;
   }
   __syncthreads();
-  const int img = (int)(s_ticket / (uint32_t)parts), part = (int)(s_ticket % (uint32_t)parts);
+  // Workgroup-uniform in SGPRs, so the descriptor loads below are scalar (constant cache).
+  const uint32_t ticket = __builtin_amdgcn_readfirstlane(s_ticket);
+  const int img = (int)(ticket / (uint32_t)parts), part = (int)(ticket % (uint32_t)parts);
+  if (dbg == 7) {  // profiling variant: tables + ticket only
+    if (ticket == 0xFFFFFFF1u) w.total[0] = 1u;
+    return;
+  }
   const JpegDesc d = jd[img];
   const int mcux = out_w >> 4;
   const int b = part * kJpegWG + tid;
@@ -150,7 +169,10 @@ __global__ __launch_bounds__(kJpegWG) void jpeg_fused_kernel(const uint8_t* __re
     const int mcu = b >> 2, sub = b & 3;
     const int bx = 2 * (mcu % mcux) + (sub & 1), by = 2 * (mcu / mcux) + (sub >> 1);
     int32_t blk[64];
-    if (d.render >= 0) {
+    if (dbg == 6) {  // profiling variant: no render
+#pragma unroll
+      for (int i = 0; i < 64; ++i) blk[i] = (i * 7 + bx + by) & 255;
+    } else if (d.render >= 0) {
       render_block_2x(rd, rs.raw, rs.f32, rs.bits, win, bx, by, blk);
 #pragma unroll
       for (int i = 0; i < 64; ++i) blk[i] -= 128;
@@ -166,6 +188,13 @@ __global__ __launch_bounds__(kJpegWG) void jpeg_fused_kernel(const uint8_t* __re
         }
       }
     }
+    if (dbg == 1 || dbg == 6) {  // profiling variants: stop before the FDCT
+      int acc = 0;
+#pragma unroll
+      for (int i = 0; i < 64; ++i) acc += blk[i] * (i + 1);
+      if (acc == 0x7FFFFFF1) w.total[0] = 1u;
+      return;
+    }
     fdct_islow(blk);
 #pragma unroll
     for (int k = 0; k < 64; k += 2) {
@@ -173,7 +202,7 @@ __global__ __launch_bounds__(kJpegWG) void jpeg_fused_kernel(const uint8_t* __re
       const int16_t c = quant_recip(blk[kNatural[k + 1]], q, kNatural[k + 1]);
       if (k == 0) dc0 = a;
       nz |= (k > 0 && a != 0 ? 1ull << k : 0ull) | (c != 0 ? 1ull << (k + 1) : 0ull);
-      mycoef[k >> 1] = (uint32_t)(uint16_t)a | ((uint32_t)(uint16_t)c << 16);
+      mycoef[coef_slot(k >> 1, tid)] = (uint32_t)(uint16_t)a | ((uint32_t)(uint16_t)c << 16);
     }
   }
   sdc[tid] = dc0;
@@ -201,7 +230,7 @@ __global__ __launch_bounds__(kJpegWG) void jpeg_fused_kernel(const uint8_t* __re
     int last = 0;
     for (uint64_t m = nz; m; m &= m - 1) {
       const int k = __builtin_ctzll(m);
-      const int v = (int16_t)(mycoef[k >> 1] >> (16 * (k & 1)));
+      const int v = (int16_t)(mycoef[coef_slot(k >> 1, tid)] >> (16 * (k & 1)));
       const int run = k - last - 1;
       const int n = mag_bits_fast(v);
       bits += (uint32_t)(run >> 4) * aclen[0xF0] + aclen[((run & 15) << 4) + n] + (uint32_t)n;
@@ -253,7 +282,7 @@ __global__ __launch_bounds__(kJpegWG) void jpeg_fused_kernel(const uint8_t* __re
     int last = 0;
     for (uint64_t m = nz; m; m &= m - 1) {
       const int k = __builtin_ctzll(m);
-      const int v = (int16_t)(mycoef[k >> 1] >> (16 * (k & 1)));
+      const int v = (int16_t)(mycoef[coef_slot(k >> 1, tid)] >> (16 * (k & 1)));
       int run = k - last - 1;
       while (run > 15) {
         bw.put_sym(actab[0xF0]);
@@ -417,7 +446,13 @@ void launch_jpeg(const uint8_t* canvas, const JpegDesc* jd, int ncanvas, int out
   const int parts = (bpi + kJpegWG - 1) / kJpegWG;
   if ((size_t)parts * ncanvas > w.look_cap) throw DeviceError("launch_jpeg: look-back capacity exceeded");
   w.look_used = (size_t)parts * ncanvas;
-  jpeg_fused_kernel<<<parts * ncanvas, kJpegWG, 0, stream>>>(canvas, jd, ncanvas, out_w, out_h, q, w, rs, out_sizes);
+  // NM03_JPEG_DBG selects truncated profiling variants (output invalid; tools/gpu_jpeg_split.sh).
+  static const int dbg = [] {
+    const char* e = std::getenv("NM03_JPEG_DBG");
+    return e ? std::atoi(e) : 0;
+  }();
+  jpeg_fused_kernel<<<parts * ncanvas, kJpegWG, 0, stream>>>(canvas, jd, ncanvas, out_w, out_h, q, w, rs, out_sizes,
+                                                              dbg);
   check_launch("jpeg_fused_kernel");
   jpeg_stuff_count_kernel<<<kStuffGrid, kStuffThreads, 0, stream>>>(jd, ncanvas, w);
   check_launch("jpeg_stuff_count_kernel");

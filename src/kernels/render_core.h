@@ -65,6 +65,11 @@ __device__ __forceinline__ uint32_t render_pixel(const RenderDesc& d, const uint
   return gray_u8(bilerp(a, b, c, e, wx, wy), win.lo, win.inv);
 }
 
+#ifndef NM03_VEC_PATCH
+#define NM03_VEC_PATCH 0
+#endif
+constexpr bool kVecPatch = NM03_VEC_PATCH;  // 8-byte row loads measured slower (97 vs 93 us / batch)
+
 // Fused 2× render of the 8×8 canvas block (bx, by) into px[64] (row-major), for a RenderDesc
 // with render_is_exact_2x(): the block's source footprint is a 6×6 patch (gray) or 4×4 (labels).
 __device__ __forceinline__ void render_block_2x(const RenderDesc& d, const uint16_t* raw, const float* f32,
@@ -90,31 +95,43 @@ __device__ __forceinline__ void render_block_2x(const RenderDesc& d, const uint1
   }
   const int sx0 = 4 * bx - 1, sy0 = 4 * by - 1;
   float patch[6][6];
+  if (kVecPatch && d.kind == kRenderRawGray && sx0 >= 1 && sx0 + 6 <= W && !(W & 1)) {
+    // Interior columns: the patch row plus one sample either side is 8 contiguous 4-byte-aligned
+    // u16 (source column 4bx-2 is even, rows are even-sized) → two 8-byte loads per row.
 #pragma unroll
-  for (int j = 0; j < 6; ++j) {
-    const int y = clampi(sy0 + j, 0, H - 1);
+    for (int j = 0; j < 6; ++j) {
+      const int y = clampi(sy0 + j, 0, H - 1);
+      const uint2* p = reinterpret_cast<const uint2*>(raw + d.src_off + (size_t)y * W + (sx0 - 1));
+      const uint2 lo = p[0], hi = p[1];
+      const uint32_t wv[4] = {lo.x, lo.y, hi.x, hi.y};
 #pragma unroll
-    for (int i = 0; i < 6; ++i) patch[j][i] = render_src_value(d, raw, f32, clampi(sx0 + i, 0, W - 1), y);
+      for (int i = 0; i < 6; ++i) {
+        const uint32_t word = wv[(i + 1) >> 1];
+        const uint16_t r = (uint16_t)((i + 1) & 1 ? (word >> 16) : (word & 0xFFFFu));
+        patch[j][i] = rescaled_value(key_from_raw(r, d.type, d.stored_bits), d.type, d.slope, d.intercept);
+      }
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+      const int y = clampi(sy0 + j, 0, H - 1);
+#pragma unroll
+      for (int i = 0; i < 6; ++i) patch[j][i] = render_src_value(d, raw, f32, clampi(sx0 + i, 0, W - 1), y);
+    }
   }
-  // Per-column and per-row interpolation weights (same expressions as render_pixel, hoisted).
-  float wxs[8], wys[8];
-#pragma unroll
-  for (int c = 0; c < 8; ++c) {
-    const float fx = render_src_coord(bx * 8 + c, d.ox, d.invx) - 0.5f;
-    wxs[c] = fx - floorf(fx);
-    const float fy = render_src_coord(by * 8 + c, d.oy, d.invy) - 0.5f;
-    wys[c] = fy - floorf(fy);
-  }
-  // For an exact 2× fit floor(f) - (4b-1) == (k+1)/2; the compile-time index keeps the patch in
-  // registers (a float-derived index would force it to scratch). The weights stay float-derived.
+  // Exact 2× fit: the source coordinate of canvas pixel k is 2b + k/2 - 0.25 (exact in f32), so
+  // the interpolation weight is 0.75 for even and 0.25 for odd k — the very values render_pixel
+  // computes — and floor(f) - (4b-1) == (k+1)/2 is a compile-time patch index.
 #pragma unroll
   for (int r = 0; r < 8; ++r) {
     const int j0 = (r + 1) >> 1;
+    const float wy = (r & 1) ? 0.25f : 0.75f;
 #pragma unroll
     for (int c = 0; c < 8; ++c) {
       const int i0 = (c + 1) >> 1;
+      const float wx = (c & 1) ? 0.25f : 0.75f;
       const float val =
-          bilerp(patch[j0][i0], patch[j0][i0 + 1], patch[j0 + 1][i0], patch[j0 + 1][i0 + 1], wxs[c], wys[r]);
+          bilerp(patch[j0][i0], patch[j0][i0 + 1], patch[j0 + 1][i0], patch[j0 + 1][i0 + 1], wx, wy);
       px[r * 8 + c] = (int32_t)gray_u8(val, win.lo, win.inv);
     }
   }
