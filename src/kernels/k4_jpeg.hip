@@ -2,21 +2,18 @@
 // main_sequential.cpp:61-73). Output is byte-identical to libjpeg(-turbo) baseline q75 4:2:0
 // (nm03/jpeg_common.h; golden encoder src/io/jpeg.cpp; tests/test_jpeg.py vs Pillow).
 //
-// Every stage is massively parallel (a batch of 64 slices = 128 canvases = 524k luma blocks):
-//  1 jpeg_block_kernel   thread per 8×8 luma block (MCU order). Pixels come from the canvas, or
-//                        — for an exact 2× fit, the common case — are rendered on the fly from the
-//                        6×6 source patch (render_core.h), so the 256 KiB canvas never exists.
-//                        islow FDCT, quantisation by exact reciprocal multiply (umulhi by
-//                        ceil(2^32/d): exact for |x| < 2^16, d < 2^16), zig-zag, non-zero mask and
-//                        the predictor-independent Huffman cost (AC codes, ZRLs, EOB).
-//  2 jpeg_scan_kernel    workgroup per image: DC-difference costs, MCU bit counts (chroma of a
-//                        gray canvas is 8 zero bits per MCU), workgroup exclusive scan → bit
-//                        offset of every block; zero the image's staging words.
-//  3 jpeg_emit_kernel    thread per luma block: writes its codes at its bit offset (atomicOr only
-//                        touches words shared with neighbouring blocks' ranges).
-//  4 jpeg_stuff_*        workgroup per 4 KiB chunk: count 0xFF bytes; then prefix over previous
-//                        chunks, in-chunk scan, stuffed bytes staged in LDS and copied with
-//                        64-byte-coalesced stores straight into host-mapped pinned memory.
+// Two launches per batch (a batch of 64 slices = 128 canvases = 524k luma blocks):
+//  1 jpeg_fused_kernel   workgroup per 256 luma blocks (64 MCUs) of an image, thread per block.
+//                        Pixels come from the canvas or — for an exact 2× fit, the common case —
+//                        are rendered on the fly from the 6×6 source patch (render_core.h), so the
+//                        256 KiB canvas never exists. islow FDCT (24-bit multiplies), quantisation
+//                        by exact reciprocal (umulhi by ceil(2^32/d): exact for |x|, d < 2^16),
+//                        Huffman cost, workgroup scan, decoupled look-back over the image's
+//                        earlier workgroups, then the codes are ORed into the zeroed stage words.
+//  2 jpeg_stuff_*        grid-stride over (chunk, image) 4 KiB chunks, chunk-major: count 0xFF
+//                        bytes; then prefix over previous chunks, in-chunk scan, stuffed bytes
+//                        staged in LDS and copied straight into host-mapped pinned memory; the
+//                        consumed stage words are cleared for the next launch.
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
@@ -103,12 +100,15 @@ constexpr int kCoefStride = 32;  // u32 words per thread in LDS: 32 zig-zag pair
 // (4 workgroups per CU).
 __device__ __forceinline__ int coef_slot(int p, int t) { return p ^ (t & 31); }
 
-// Single-pass encoder: workgroup L (ordered ticket) encodes blocks [256p, 256p+256) of image i.
+// Single-pass encoder: workgroup L = blockIdx encodes blocks [256p, 256p+256) of image i.
 //  1. render (fused 2×) or read the 8×8 block, islow FDCT, reciprocal quantisation;
 //  2. Huffman cost of the block (DC needs the previous block's DC: LDS neighbour, and for the
 //     first block of the workgroup a wave-0 recomputation of the preceding block's DC = Σ(x-128));
 //  3. workgroup exclusive scan of the costs, then a decoupled look-back over the image's earlier
-//     workgroups (tickets are taken in dispatch order, so every predecessor is already resident);
+//     workgroups. Workgroups are dispatched in index order (per XCD), so the lowest unfinished
+//     workgroup is always resident and never waits: the chain always progresses. The spin is
+//     bounded anyway (an image whose look-back times out is re-encoded on the CPU), and
+//     NM03_JPEG_DBG=9 swaps in ordered tickets (atomic counter) for A/B runs;
 //  4. each thread writes its block's codes at its bit offset (atomicOr into the zeroed stage).
 // The last workgroup of an image publishes the total (or the overflow marker).
 __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(4))) void jpeg_fused_kernel(const uint8_t* __restrict__ canvas,
@@ -255,7 +255,7 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(4))) vo
         const uint64_t st = look_load(&look[p]);
         const uint32_t hi = (uint32_t)(st >> 32);
         if (hi == 0u) {
-          if (++spins > (1u << 26)) {  // cannot happen with ordered tickets; never hang the GPU
+          if (++spins > (1u << 26)) {  // cannot happen with in-order dispatch; never hang the GPU
             prefix = 0xFFFFFFFFu;
             break;
           }
