@@ -49,16 +49,54 @@ __global__ __launch_bounds__(256) void median_kernel(const uint16_t* __restrict_
   const int W = d.w, H = d.h;
 
   uint32_t kmin = 0xFFFFu, kmax = 0u;
-  for (int i = threadIdx.x; i < PR * PW; i += 256) {
-    const int r = i / PW, c = i - r * PW;
-    const int y = clampi(y0 - R + r, 0, H - 1);
-    const int xl = clampi(x0 - R + c, 0, W - 1), xh = clampi(x0 - R + c + 32, 0, W - 1);
-    const uint16_t* row = src + (size_t)y * W;
-    const uint32_t kl = key_from_raw(row[xl], d.type, d.stored_bits);
-    const uint32_t kh = key_from_raw(row[xh], d.type, d.stored_bits);
-    P[r * PS + c] = kl | (kh << 16);
-    kmin = min(kmin, min(kl, kh));
-    kmax = max(kmax, max(kl, kh));
+  if ((W & 3) == 0 && (d.raw_off & 3) == 0) {
+    // Vector path: window pixels p = 0..71 are image columns x0-4+p (8-byte aligned groups of
+    // 4). Pair column c holds window pixels c+4-R (low half) and c+36-R (high half), so a task
+    // (row, group gi < 10) loads groups gi and gi+8 — one 8-byte load each, per-pixel clamped
+    // loads only where a group leaves the image — and writes up to 4 pair words.
+    for (int i = threadIdx.x; i < PR * 10; i += 256) {
+      const int r = i / 10, gi = i - r * 10;
+      const int y = clampi(y0 - R + r, 0, H - 1);
+      const uint16_t* row = src + (size_t)y * W;
+      auto group = [&](int g4, uint16_t* px) {
+        const int xs = x0 - 4 + 4 * g4;
+        if (xs >= 0 && xs + 4 <= W) {
+          const uint2 v = *reinterpret_cast<const uint2*>(row + xs);
+          px[0] = (uint16_t)v.x;
+          px[1] = (uint16_t)(v.x >> 16);
+          px[2] = (uint16_t)v.y;
+          px[3] = (uint16_t)(v.y >> 16);
+        } else {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) px[q] = row[clampi(xs + q, 0, W - 1)];
+        }
+      };
+      uint16_t lo[4], hi[4];
+      group(gi, lo);
+      group(gi + 8, hi);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int c = 4 * gi + q - (4 - R);
+        if (c < 0 || c >= PW) continue;
+        const uint32_t kl = key_from_raw(lo[q], d.type, d.stored_bits);
+        const uint32_t kh = key_from_raw(hi[q], d.type, d.stored_bits);
+        P[r * PS + c] = kl | (kh << 16);
+        kmin = min(kmin, min(kl, kh));
+        kmax = max(kmax, max(kl, kh));
+      }
+    }
+  } else {
+    for (int i = threadIdx.x; i < PR * PW; i += 256) {
+      const int r = i / PW, c = i - r * PW;
+      const int y = clampi(y0 - R + r, 0, H - 1);
+      const int xl = clampi(x0 - R + c, 0, W - 1), xh = clampi(x0 - R + c + 32, 0, W - 1);
+      const uint16_t* row = src + (size_t)y * W;
+      const uint32_t kl = key_from_raw(row[xl], d.type, d.stored_bits);
+      const uint32_t kh = key_from_raw(row[xh], d.type, d.stored_bits);
+      P[r * PS + c] = kl | (kh << 16);
+      kmin = min(kmin, min(kl, kh));
+      kmax = max(kmax, max(kl, kh));
+    }
   }
   __syncthreads();
 
