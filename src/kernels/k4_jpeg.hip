@@ -51,31 +51,6 @@ __device__ __forceinline__ int wave_sum_i32(int v) {
   return v;
 }
 
-struct GBitWriter {
-  uint32_t* words;
-  uint32_t widx;
-  uint64_t acc;
-  int nacc;
-  __device__ GBitWriter(uint32_t* w, uint32_t pos) : words(w), widx(pos >> 5), acc(0), nacc((int)(pos & 31)) {}
-  __device__ __forceinline__ void put(uint32_t code, int len) {
-    acc = (acc << len) | (uint64_t)(code & ((1u << len) - 1u));
-    nacc += len;
-    if (nacc >= 32) {
-      const uint32_t wv = (uint32_t)(acc >> (nacc - 32));
-      if (wv) atomicOr(&words[widx], wv);
-      ++widx;
-      nacc -= 32;
-      acc &= (1ull << nacc) - 1ull;
-    }
-  }
-  __device__ __forceinline__ void put_sym(uint32_t e) { put(e & 0xFFFFu, (int)(e >> 16)); }
-  __device__ __forceinline__ void flush() {
-    if (nacc > 0) {
-      const uint32_t wv = (uint32_t)(acc << (32 - nacc));
-      if (wv) atomicOr(&words[widx], wv);
-    }
-  }
-};
 
 // Look-back status word: hi = state (0 = not yet, 1 = aggregate, 2 = inclusive prefix), lo = bits.
 // The stuffing-count kernel (next in the stream) clears the words again for the next launch.
@@ -100,6 +75,43 @@ constexpr int kCoefStride = 32;  // u32 words per thread in LDS: 32 zig-zag pair
 // (4 workgroups per CU).
 __device__ __forceinline__ int coef_slot(int p, int t) { return p ^ (t & 31); }
 
+constexpr int kPrivWords = 5;    // per-block Huffman bits kept in LDS (160 bits, odd stride) ...
+constexpr int kSpillWords = 56;  // ... the rest in the block's global spill slot (a block needs ≤ 1700)
+
+// MSB-first bit writer for one block: words [0, kPrivWords) go to LDS, later words (noisy,
+// high-detail blocks only) to global memory. Counts every bit.
+struct LBitWriter {
+  uint32_t* buf;
+  uint32_t* spill;
+  uint32_t bits = 0;
+  uint64_t acc = 0;
+  int nacc = 0;
+  __device__ LBitWriter(uint32_t* b, uint32_t* s) : buf(b), spill(s) {}
+  __device__ __forceinline__ void store(uint32_t wi, uint32_t v) {
+    if (wi < (uint32_t)kPrivWords)
+      buf[wi] = v;
+    else
+      spill[wi - kPrivWords] = v;
+  }
+  __device__ __forceinline__ void put(uint32_t code, int len) {
+    acc = (acc << len) | (uint64_t)(code & ((1u << len) - 1u));
+    nacc += len;
+    bits += (uint32_t)len;
+    if (nacc >= 32) {
+      store((bits - (uint32_t)nacc) >> 5, (uint32_t)(acc >> (nacc - 32)));
+      nacc -= 32;
+      acc &= (1ull << nacc) - 1ull;
+    }
+  }
+  __device__ __forceinline__ void put_sym(uint32_t e) { put(e & 0xFFFFu, (int)(e >> 16)); }
+  __device__ __forceinline__ void finish() {
+    if (nacc > 0) store(bits >> 5, (uint32_t)(acc << (32 - nacc)));
+  }
+};
+__device__ __forceinline__ uint32_t priv_word(const uint32_t* pb, const uint32_t* spill, uint32_t i) {
+  return i < (uint32_t)kPrivWords ? pb[i] : spill[i - kPrivWords];
+}
+
 // Single-pass encoder: workgroup L = blockIdx encodes blocks [256p, 256p+256) of image i.
 //  1. render (fused 2×) or read the 8×8 block, islow FDCT, reciprocal quantisation;
 //  2. Huffman cost of the block (DC needs the previous block's DC: LDS neighbour, and for the
@@ -119,7 +131,8 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(4))) vo
   __shared__ uint8_t aclen[256];
   __shared__ uint32_t dctab[16];
   __shared__ int32_t sdc[kJpegWG];
-  __shared__ uint32_t scoef[kJpegWG * kCoefStride];  // per-thread zig-zag pairs
+  __shared__ uint32_t scoef[kJpegWG * kCoefStride];  // per-thread zig-zag pairs; later the WG bit range
+  __shared__ uint32_t spriv[kJpegWG * kPrivWords];   // per-block Huffman bits
   __shared__ uint32_t sh[17];
   __shared__ uint32_t s_ticket, s_prefix;
   __shared__ int32_t s_prevdc;
@@ -221,32 +234,48 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(4))) vo
     if (tid == 0) s_prevdc = dcp;
   }
   __syncthreads();
-  // ---- 2. Huffman cost ----------------------------------------------------------------------
+  // ---- 2. Huffman coding of the block into its private bit buffer (bits = its cost) ----------
   const int diff = dc0 - (tid ? sdc[tid - 1] : s_prevdc);
   const int dn = mag_bits_fast(diff);
+  uint32_t* const pbuf = spriv + tid * kPrivWords;
+  uint32_t* const pspill = w.spill + ((size_t)blockIdx.x * kJpegWG + tid) * kSpillWords;
   uint32_t bits = 0;
   if (valid) {
-    bits = hlen(dctab[dn]) + (uint32_t)dn;
+    LBitWriter lw(pbuf, pspill);
+    lw.put_sym(dctab[dn]);
+    if (dn) lw.put((uint32_t)(diff < 0 ? diff - 1 : diff), dn);
     int last = 0;
     for (uint64_t m = nz; m; m &= m - 1) {
       const int k = __builtin_ctzll(m);
       const int v = (int16_t)(mycoef[coef_slot(k >> 1, tid)] >> (16 * (k & 1)));
-      const int run = k - last - 1;
-      const int n = mag_bits_fast(v);
-      bits += (uint32_t)(run >> 4) * aclen[0xF0] + aclen[((run & 15) << 4) + n] + (uint32_t)n;
+      int run = k - last - 1;
+      while (run > 15) {
+        lw.put_sym(actab[0xF0]);
+        run -= 16;
+      }
+      const int nb = mag_bits_fast(v);
+      lw.put_sym(actab[(run << 4) + nb]);
+      lw.put((uint32_t)(v < 0 ? v - 1 : v), nb);
       last = k;
     }
-    if (last < 63) bits += aclen[0x00];
-    if ((b & 3) == 3) bits += 2u * (hlen(kHuffDcChroma.e[0]) + hlen(kHuffAcChroma.e[0]));  // Cb, Cr: DC 0 + EOB
+    if (last < 63) lw.put_sym(actab[0x00]);
+    if ((b & 3) == 3) {  // the MCU's Cb and Cr blocks of a gray image: DC diff 0 + EOB each
+      lw.put_sym(kHuffDcChroma.e[0]);
+      lw.put_sym(kHuffAcChroma.e[0]);
+      lw.put_sym(kHuffDcChroma.e[0]);
+      lw.put_sym(kHuffAcChroma.e[0]);
+    }
+    lw.finish();
+    bits = lw.bits;
   }
   // ---- 3. workgroup scan + look-back --------------------------------------------------------
   uint32_t agg = 0;
-  const uint32_t excl = block_exclusive_scan(bits, sh, &agg);
+  const uint32_t excl = block_exclusive_scan(bits, sh, &agg);  // ends with a barrier
   uint64_t* look = w.look + (size_t)img * parts;
   if (tid == 0) {
     uint32_t prefix = 0;
-    if (part == 0) {
-      look_store(&look[0], 2u, agg);
+    if (part == 0 || dbg == 4) {  // dbg 4: profiling variant without the look-back wait
+      look_store(&look[part], 2u, agg);
     } else {
       look_store(&look[part], 1u, agg);
       int p = part - 1;
@@ -270,31 +299,48 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(4))) vo
     }
     s_prefix = prefix;
   }
+  // Meanwhile: assemble the workgroup's contiguous bit range in LDS (the coefficient area is free).
+  uint32_t* swg = scoef;
+  const uint32_t nlocal = (agg + 31) >> 5;
+  const bool in_lds = nlocal < (uint32_t)(kJpegWG * kCoefStride);  // workgroup-uniform
+  const uint32_t nwp = (bits + 31) >> 5;
+  if (in_lds) {
+    for (uint32_t i = tid; i <= nlocal; i += kJpegWG) swg[i] = 0u;
+    __syncthreads();
+    for (uint32_t i = 0; i < nwp; ++i) {
+      const uint32_t v = priv_word(pbuf, pspill, i), dst = excl + 32u * i, wi = dst >> 5, shf = dst & 31u;
+      atomicOr(&swg[wi], v >> shf);
+      if (shf) atomicOr(&swg[wi + 1], v << (32u - shf));
+    }
+  }
   __syncthreads();
   const uint32_t prefix = s_prefix;
   const uint32_t end = sat_add(prefix, agg);
   const uint32_t cap_bits = d.stage_words * 32u;
-  // ---- 4. emission ---------------------------------------------------------------------------
-  if (valid && end <= cap_bits) {
-    GBitWriter bw(w.stage + d.stage_off, prefix + excl);
-    bw.put_sym(dctab[dn]);
-    if (dn) bw.put((uint32_t)(diff < 0 ? diff - 1 : diff), dn);
-    int last = 0;
-    for (uint64_t m = nz; m; m &= m - 1) {
-      const int k = __builtin_ctzll(m);
-      const int v = (int16_t)(mycoef[coef_slot(k >> 1, tid)] >> (16 * (k & 1)));
-      int run = k - last - 1;
-      while (run > 15) {
-        bw.put_sym(actab[0xF0]);
-        run -= 16;
+  uint32_t* stage = w.stage + d.stage_off;
+  // ---- 4. emission: coalesced word stores (only the two edge words, shared with the
+  //         neighbouring workgroups, are atomic) --------------------------------------------------
+  if (end <= cap_bits && agg) {
+    if (in_lds) {
+      const uint32_t s = prefix & 31u, base = prefix >> 5;
+      const uint32_t nw = ((prefix + agg + 31u) >> 5) - base;
+      for (uint32_t j = tid; j < nw; j += kJpegWG) {
+        uint32_t v = j < nlocal ? swg[j] >> s : 0u;
+        if (s && j > 0) v |= swg[j - 1] << (32u - s);
+        if (j == 0 || j == nw - 1)
+          atomicOr(&stage[base + j], v);
+        else
+          stage[base + j] = v;
       }
-      const int nb = mag_bits_fast(v);
-      bw.put_sym(actab[(run << 4) + nb]);
-      bw.put((uint32_t)(v < 0 ? v - 1 : v), nb);
-      last = k;
+    } else {
+      // Extremely detailed workgroup (> 256 Kbit): each block ORs its words into the stage.
+      for (uint32_t i = 0; i < nwp; ++i) {
+        const uint32_t v = priv_word(pbuf, pspill, i), dst = prefix + excl + 32u * i, wi = dst >> 5,
+                       shf = dst & 31u;
+        atomicOr(&stage[wi], v >> shf);
+        if (shf) atomicOr(&stage[wi + 1], v << (32u - shf));
+      }
     }
-    if (last < 63) bw.put_sym(actab[0x00]);
-    bw.flush();
   }
   if (part == parts - 1 && tid == 0) {
     const uint32_t nbytes = (end + 7) >> 3;
@@ -432,7 +478,7 @@ void launch_jpeg(const uint8_t* canvas, const JpegDesc* jd, int ncanvas, int out
                  JpegWork& w, uint8_t* out, int32_t* out_sizes, hipStream_t stream, const JpegRenderSrc* fused) {
   if (ncanvas <= 0) return;
   if (out_w % 16 || out_h % 16) throw DeviceError("GPU JPEG encoder needs canvas dims that are multiples of 16");
-  if (w.max_chunks <= 0 || !w.total || !w.chunk_ff || !w.stage || !w.look || !w.ticket)
+  if (w.max_chunks <= 0 || !w.total || !w.chunk_ff || !w.stage || !w.look || !w.ticket || !w.spill)
     throw DeviceError("launch_jpeg: JpegWork incomplete");
   QuantRecip q;
   for (int i = 0; i < 64; ++i) {

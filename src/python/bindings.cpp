@@ -638,6 +638,7 @@ PYBIND11_MODULE(_nm03, m) {
     const size_t look_cap = (size_t)n * ((blocks + 255) / 256);
     const size_t o_jd = take(sizeof(gpu::JpegDesc) * n), o_stage = take((size_t)n * stage_bytes),
                  o_look = take(look_cap * 8), o_ticket = take(8), o_zero_end = off,
+                 o_spill = take(look_cap * 256 * 56 * 4),
                  o_tot = take((size_t)n * 4), o_cff = take((size_t)n * max_chunks * 4),
                  o_out = take((size_t)n * out_cap), o_sz = take((size_t)n * 4);
     uint8_t* dev = (uint8_t*)scratch().get(off);
@@ -648,6 +649,7 @@ PYBIND11_MODULE(_nm03, m) {
     wk.look = (uint64_t*)(dev + o_look);
     wk.look_cap = look_cap;
     wk.ticket = (uint32_t*)(dev + o_ticket);
+    wk.spill = (uint32_t*)(dev + o_spill);
     wk.total = (uint32_t*)(dev + o_tot);
     wk.chunk_ff = (uint32_t*)(dev + o_cff);
     wk.max_chunks = max_chunks;

@@ -88,7 +88,7 @@ void hip_free_all(Slot& s) {
   if (s.h_out) (void)hipHostFree(s.h_out);
   if (s.h_sizes) (void)hipHostFree(s.h_sizes);
   for (void* p : {(void*)s.d_blob, (void*)s.d_med, (void*)s.d_f32, (void*)s.d_bits, (void*)s.d_canvas,
-                  (void*)s.jw.stage, (void*)s.jw.look, (void*)s.jw.ticket,
+                  (void*)s.jw.stage, (void*)s.jw.look, (void*)s.jw.ticket, (void*)s.jw.spill,
                   (void*)s.jw.total, (void*)s.jw.chunk_ff})
     if (p) (void)hipFree(p);
   for (auto& kv : s.graphs) (void)hipGraphExecDestroy(kv.second);
@@ -218,6 +218,7 @@ struct Engine::Impl {
       s.jw.look_cap = (size_t)s.cap_canvases * ((blocks + 255) / 256);
       s.jw.look = dmalloc<uint64_t>(s.jw.look_cap, "hipMalloc look-back");
       s.jw.ticket = dmalloc<uint32_t>(1, "hipMalloc ticket");
+      s.jw.spill = dmalloc<uint32_t>(s.jw.look_cap * 256 * 56, "hipMalloc jpeg spill");
       s.jw.total = dmalloc<uint32_t>(s.cap_canvases, "hipMalloc total");
       s.jw.max_chunks = (int)(kStageBytes / kStuffChunk);
       s.jw.chunk_ff = dmalloc<uint32_t>((size_t)s.jw.max_chunks * s.cap_canvases, "hipMalloc chunk_ff");
