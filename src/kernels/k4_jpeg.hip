@@ -497,8 +497,14 @@ void launch_jpeg(const uint8_t* canvas, const JpegDesc* jd, int ncanvas, int out
     const char* e = std::getenv("NM03_JPEG_DBG");
     return e ? std::atoi(e) : 0;
   }();
-  jpeg_fused_kernel<<<parts * ncanvas, kJpegWG, 0, stream>>>(canvas, jd, ncanvas, out_w, out_h, q, w, rs, out_sizes,
-                                                              dbg);
+  // NM03_JPEG_LDS_PAD: extra dynamic LDS per workgroup (caps the encoder's residency per CU so
+  // other streams' kernels keep LDS to run alongside it).
+  static const int pad = [] {
+    const char* e = std::getenv("NM03_JPEG_LDS_PAD");
+    return e ? std::atoi(e) : 0;
+  }();
+  jpeg_fused_kernel<<<parts * ncanvas, kJpegWG, pad, stream>>>(canvas, jd, ncanvas, out_w, out_h, q, w, rs,
+                                                                out_sizes, dbg);
   check_launch("jpeg_fused_kernel");
   jpeg_stuff_count_kernel<<<kStuffGrid, kStuffThreads, 0, stream>>>(jd, ncanvas, w);
   check_launch("jpeg_stuff_count_kernel");
