@@ -23,9 +23,14 @@ namespace nm03 {
 // last batches' exports are not queued behind anything (drain).
 class ThreadPool {
  public:
-  explicit ThreadPool(int n) {
+  // `on_start` runs first on every worker thread (e.g. NUMA pinning).
+  explicit ThreadPool(int n, std::function<void()> on_start = {}) {
     if (n < 1) n = 1;
-    for (int i = 0; i < n; ++i) workers_.emplace_back([this] { loop(); });
+    for (int i = 0; i < n; ++i)
+      workers_.emplace_back([this, on_start] {
+        if (on_start) on_start();
+        loop();
+      });
   }
   ~ThreadPool() {
     {

@@ -14,6 +14,7 @@
 #include "nm03/comm.h"
 #include "nm03/dicom.h"
 #include "nm03/engine.h"
+#include "nm03/numa.h"
 #include "nm03/golden.h"
 #include "nm03/jpeg.h"
 #include "nm03/kernels.h"
@@ -291,6 +292,8 @@ PYBIND11_MODULE(_nm03, m) {
       py::arg("slope") = 1.f, py::arg("intercept") = 0.f, py::arg("spacing_x") = 1.f, py::arg("spacing_y") = 1.f,
       py::arg("instance") = 1, py::arg("patient_id") = "PGBM-000", py::arg("syntax") = "explicit",
       py::arg("preamble") = true);
+  m.def("numa_parse_cpulist", &numa::parse_cpulist);
+  m.def("numa_node_cpus", &numa::node_cpus);
   m.def("read_pixels_direct", [](const std::string& path) {
     dicom::SliceFile f(path);
     std::vector<uint8_t> scratch;

@@ -21,6 +21,7 @@
 #include "nm03/jpeg.h"
 #include "nm03/kernels.h"
 #include "nm03/log.h"
+#include "nm03/numa.h"
 #include "nm03/thread_pool.h"
 
 namespace nm03 {
@@ -110,13 +111,14 @@ T* dmalloc(size_t count, const char* what) {
 
 struct Engine::Impl {
   EngineConfig cfg;
+  numa::Placement place;
   std::unique_ptr<ThreadPool> pool;
   std::vector<std::unique_ptr<Slot>> slots;
   std::vector<uint8_t> jpeg_header;
   int32_t divs[64];
   PipeConsts pc{};
 
-  explicit Impl(const EngineConfig& c) : cfg(c) {
+  explicit Impl(const EngineConfig& c) : cfg(c), place(c.device) {
     if (cfg.batch_size < 1) cfg.batch_size = 1;
     if (cfg.streams < 1) cfg.streams = 1;
     if (cfg.max_dim < 16) cfg.max_dim = 16;
@@ -150,12 +152,15 @@ struct Engine::Impl {
     if (cfg.render.out_width % 16 || cfg.render.out_height % 16)
       throw DeviceError("canvas size must be a multiple of 16");
     check_hip(hipSetDevice(cfg.device), "hipSetDevice");
-    pool = std::make_unique<ThreadPool>(cfg.threads);
-    for (int i = 0; i < cfg.streams; ++i) slots.push_back(make_slot());
+    // Host threads and pinned buffers on the GPU's socket (numa.h).
+    pool = std::make_unique<ThreadPool>(cfg.threads, [this] { place.bind_this_thread(); });
+    place.run_bound([&] {
+      for (int i = 0; i < cfg.streams; ++i) slots.push_back(make_slot());
+    });
     start_workers();
     log_info("engine on device " + std::to_string(cfg.device) + ": batch " + std::to_string(cfg.batch_size) + ", " +
              std::to_string(cfg.streams) + " streams, " + std::to_string(cfg.threads) + " host threads, max_dim " +
-             std::to_string(cfg.max_dim));
+             std::to_string(cfg.max_dim) + ", " + place.describe());
   }
 
   ~Impl() {
@@ -619,6 +624,7 @@ struct Engine::Impl {
   }
 
   void worker(Slot* s) {
+    place.bind_this_thread();
     (void)hipSetDevice(cfg.device);
     uint64_t seen = 0;
     for (;;) {

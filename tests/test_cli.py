@@ -45,3 +45,11 @@ def test_synth_tool(tmp_path):
 def test_missing_data_root_is_fatal(tmp_path):
     r = run_bin("test_pipeline", "--cpu", "--data-root", str(tmp_path / "nope"), "--out", str(tmp_path / "o"))
     assert r.returncode == 1 and "Fatal error" in r.stderr
+
+
+def test_numa_cpulist_parsing(native):
+    """Host NUMA placement (numa.h): sysfs cpulists such as node0 of an MI355X node."""
+    assert native.numa_parse_cpulist("0-3,8,10-11") == [0, 1, 2, 3, 8, 10, 11]
+    assert native.numa_parse_cpulist("0-63,128-191")[-1] == 191
+    assert native.numa_parse_cpulist("") == []
+    assert native.numa_node_cpus(-1) == []
