@@ -68,6 +68,10 @@ struct EngineConfig {
   // (profiles/graphs_ab.txt) — the chain is only 8 launches per 64 slices, so there is no launch
   // overhead to win and graph launches lose cross-stream overlap.
   bool graphs = false;
+  // Tapered batch schedule (small first and last batches; engine.cpp plan_batches). Off by default:
+  // measured 209k vs 220k slices/s (4 interleaved runs each) — the extra batches cost more than the
+  // shorter fill/drain gains. NM03_BATCH_TAPER=1 turns it on.
+  bool taper = false;
 };
 
 // Everything test_pipeline exports / tests inspect for one slice (host copies).

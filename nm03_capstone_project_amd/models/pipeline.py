@@ -50,6 +50,7 @@ class PipelineConfig:
     export_jpeg: bool = True
     resume: bool = False
     graphs: bool = False  # replay per-batch kernel chains from captured hipGraphs (slower, see engine.h)
+    taper: bool = False  # small first/last batches (measured slower, see engine.h)
 
     _PIPE = ("norm_low", "norm_high", "norm_min", "norm_max", "clip_min", "clip_max", "median_window",
              "sharpen_gain", "sharpen_sigma", "sharpen_mask", "srg_min", "srg_max", "srg_connectivity",
@@ -80,6 +81,7 @@ class PipelineConfig:
         c.export_jpeg = self.export_jpeg
         c.resume = self.resume
         c.graphs = self.graphs
+        c.taper = self.taper
         return c
 
     def replace(self, **kw):

@@ -237,7 +237,8 @@ PYBIND11_MODULE(_nm03, m) {
       .def_readwrite("render", &EngineConfig::render)
       .def_readwrite("export_jpeg", &EngineConfig::export_jpeg)
       .def_readwrite("resume", &EngineConfig::resume)
-      .def_readwrite("graphs", &EngineConfig::graphs);
+      .def_readwrite("graphs", &EngineConfig::graphs)
+      .def_readwrite("taper", &EngineConfig::taper);
 
   m.def("reference_seeds", [](int w, int h) {
     std::vector<std::pair<int, int>> v;

@@ -119,6 +119,7 @@ struct Engine::Impl {
   PipeConsts pc{};
 
   explicit Impl(const EngineConfig& c) : cfg(c), place(c.device) {
+    if (const char* e = std::getenv("NM03_BATCH_TAPER"); e && *e) cfg.taper = *e != '0';
     if (cfg.batch_size < 1) cfg.batch_size = 1;
     if (cfg.streams < 1) cfg.streams = 1;
     if (cfg.max_dim < 16) cfg.max_dim = 16;
@@ -502,10 +503,10 @@ struct Engine::Impl {
     return false;
   }
 
-  void process_batch(Slot& s, const std::vector<WorkItem>& items, size_t first, size_t count,
+  void process_batch(Slot& s, const std::vector<WorkItem>& items, size_t batch, size_t first, size_t count,
                      std::vector<SliceStatus>& status, StageTimes& acc, std::mutex& acc_m,
                      const std::function<void(size_t)>& on_start) {
-    const uint64_t batch = first / (size_t)cfg.batch_size;  // pool priority: earlier batches first
+    // `batch` doubles as the host-pool priority: earlier batches first.
     s.raw_used = 0;
     s.loaded.assign(count, LoadedSlice{});
     std::atomic<int64_t> load_ns{0}, bytes_in{0}, write_ns{0}, bytes_out{0};
@@ -532,7 +533,7 @@ struct Engine::Impl {
     if (!s.live.empty()) {
       try {
         TraceRange tr("nm03.gpu_batch");
-        if (fault_plan().fail_batch == (int64_t)(first / (size_t)cfg.batch_size))
+        if (fault_plan().fail_batch == (int64_t)batch)
           throw DeviceError("injected fault: device batch failure");
         build_and_run(s, 0, &local);
       } catch (const std::exception& e) {
@@ -590,6 +591,35 @@ struct Engine::Impl {
     acc.batches += 1;
   }
 
+  // Batch schedule. Tapered (batch ≥ 16): a quarter- and a half-size batch first, so the upload
+  // engine starts after a few loads instead of a full batch (pipeline fill), full batches in the
+  // middle, and a remainder split into shrinking batches so the last kernels and exports after
+  // the final upload are short (drain). Uniform otherwise.
+  static std::vector<std::pair<size_t, size_t>> plan_batches(size_t n, size_t B, bool taper) {
+    std::vector<std::pair<size_t, size_t>> out;
+    size_t first = 0;
+    auto take = [&](size_t c) {
+      c = std::min(c, n - first);
+      if (c) out.push_back({first, c});
+      first += c;
+    };
+    if (!taper || B < 16 || n <= 2 * B) {
+      while (first < n) take(B);
+      return out;
+    }
+    take(B / 4);
+    take(B / 2);
+    while (n - first > B + B / 2) take(B);
+    const size_t left = n - first;
+    if (left > B / 2) {
+      take((left + 1) / 2);
+      const size_t rest = n - first;
+      take((rest + 1) / 2);
+    }
+    take(n - first);
+    return out;
+  }
+
   // ---- persistent slot workers: one host thread per slot, parked between runs --------------
   struct Job {
     const std::vector<WorkItem>* items = nullptr;
@@ -597,7 +627,7 @@ struct Engine::Impl {
     StageTimes* acc = nullptr;
     std::mutex* acc_m = nullptr;
     const std::function<void(size_t)>* on_start = nullptr;
-    size_t nb = 0;
+    std::vector<std::pair<size_t, size_t>> batches;  // (first, count)
     std::atomic<size_t> next{0};
     std::exception_ptr err;
     std::mutex err_m;
@@ -637,10 +667,9 @@ struct Engine::Impl {
         j = job;
       }
       try {
-        const size_t B = (size_t)cfg.batch_size, n = j->items->size();
-        for (size_t b; (b = j->next.fetch_add(1)) < j->nb;) {
-          const size_t first = b * B, count = std::min(B, n - first);
-          process_batch(*s, *j->items, first, count, *j->status, *j->acc, *j->acc_m, *j->on_start);
+        for (size_t b; (b = j->next.fetch_add(1)) < j->batches.size();) {
+          const auto [first, count] = j->batches[b];
+          process_batch(*s, *j->items, b, first, count, *j->status, *j->acc, *j->acc_m, *j->on_start);
         }
       } catch (...) {
         std::lock_guard<std::mutex> g(j->err_m);
@@ -664,7 +693,7 @@ struct Engine::Impl {
     j.acc = &acc;
     j.acc_m = &acc_m;
     j.on_start = &on_start;
-    j.nb = (items.size() + (size_t)cfg.batch_size - 1) / (size_t)cfg.batch_size;
+    j.batches = plan_batches(items.size(), (size_t)cfg.batch_size, cfg.taper);
     {
       std::unique_lock<std::mutex> g(job_m);
       job = &j;
