@@ -27,8 +27,8 @@ sys.path.insert(0, ROOT)
 import torch  # noqa: E402  (must precede the native extension: shared HIP runtime)
 
 import nm03_capstone_project_amd as nm  # noqa: E402
-from nm03_capstone_project_amd.parallel import (allreduce_max, allreduce_sum, barrier,  # noqa: E402
-                                                broadcast_bytes, init_from_env, plan_cohort)
+from nm03_capstone_project_amd.parallel import (allreduce_max, allreduce_sum, auto_threads,  # noqa: E402
+                                                barrier, broadcast_bytes, init_from_env, plan_cohort)
 from nm03_capstone_project_amd.parallel.cohort_runner import CohortPlan  # noqa: E402
 from nm03_capstone_project_amd.parallel.dist import shard_bounds  # noqa: E402
 
@@ -71,7 +71,7 @@ def main():
     ap.add_argument("--scaling", choices=("weak", "strong"), default="weak")
     ap.add_argument("--batch-size", type=int, default=64)
     ap.add_argument("--streams", type=int, default=6)
-    ap.add_argument("--threads", type=int, default=16)
+    ap.add_argument("--threads", type=int, default=0, help="host I/O threads per rank (0 = CPU budget / ranks, ≤16)")
     ap.add_argument("--data-root", default=os.environ.get("NM03_BENCH_DATA", "/tmp/nm03_bench_data"))
     ap.add_argument("--out-root", default=os.environ.get("NM03_BENCH_OUT", "/tmp/nm03_bench_out"))
     ap.add_argument("--keep-output", action="store_true")
@@ -79,6 +79,8 @@ def main():
     args = ap.parse_args()
 
     ctx = init_from_env()
+    if args.threads <= 0:
+        args.threads = auto_threads()
     n = nm.native()
     marker = os.path.join(args.data_root, ".complete")
     if ctx.local_rank == 0 and not os.path.exists(marker):

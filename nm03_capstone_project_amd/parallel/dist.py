@@ -60,6 +60,27 @@ def _dev(ctx):
     return ctx.device if (ctx is not None and ctx.backend == "nccl") else torch.device("cpu")
 
 
+def cpu_budget():
+    """CPUs this process may use: the affinity mask capped by the cgroup v2 CPU quota (cpu.max)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+def auto_threads(local_world=None, cap=16):
+    """Host I/O threads per rank: the CPU budget shared by the node's ranks (LOCAL_WORLD_SIZE),
+    at most `cap` (16 = the reference's omp_set_num_threads(16), main_parallel.cpp:401). Running
+    more busy threads than the cgroup quota allows gets the whole process throttled."""
+    if local_world is None:
+        local_world = int(os.environ.get("LOCAL_WORLD_SIZE", os.environ.get("WORLD_SIZE", "1")))
+    return max(2, min(cap, cpu_budget() // max(1, local_world)))
+
+
 def shard_bounds(n, rank, world):
     """Contiguous equal blocks (±1 item), deterministic: [n*r/W, n*(r+1)/W)."""
     return n * rank // world, n * (rank + 1) // world

@@ -100,3 +100,13 @@ def test_distributed_plan_broadcast(cohort_root, tmp_path):
     n = res[0][1]
     assert all(r[1] == n for r in res) and n > 0
     assert res[0][2] == 0 and res[-1][3] == n and res[0][3] == res[1][2]
+
+
+def test_auto_threads_respects_budget(monkeypatch):
+    from nm03_capstone_project_amd.parallel import dist
+    monkeypatch.setattr(dist, "cpu_budget", lambda: 16)
+    assert dist.auto_threads(1) == 16
+    assert dist.auto_threads(8) == 2
+    monkeypatch.setattr(dist, "cpu_budget", lambda: 256)
+    assert dist.auto_threads(8) == 16
+    assert dist.cpu_budget.__name__  # patched
