@@ -25,6 +25,7 @@ struct AppConfig {
   std::string json;        // metrics file
   std::string mode = "2d"; // 2d | 3d
   std::string input;       // test_pipeline: explicit slice path
+  std::string dump_mhd;    // test_pipeline: directory for MetaImage stage dumps (empty = off)
   int repeat = 1;
 };
 

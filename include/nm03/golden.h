@@ -52,6 +52,8 @@ std::vector<float> sharpen(const std::vector<float>& img, int w, int h, float ga
 std::vector<float> sharpen_direct(const std::vector<float>& img, int w, int h, float gain, float sigma, int mask);
 
 std::vector<uint8_t> band(const std::vector<float>& s, float lo, float hi);
+// BinaryThresholding (lo ≤ x ≤ hi → 1): the band test as a standalone op (k6_threshold.hip).
+inline std::vector<uint8_t> binary_threshold(const std::vector<float>& s, float lo, float hi) { return band(s, lo, hi); }
 
 // Seeded region growing: pixels connected (4 or 8) to an in-band seed through in-band pixels.
 std::vector<uint8_t> region_grow(const std::vector<uint8_t>& band, int w, int h, const std::vector<Seed>& seeds,
@@ -91,6 +93,8 @@ SliceJpegs export_jpegs(const SliceInput& s, const SliceResult& r, const Pipelin
 struct StageImages {
   std::vector<std::vector<uint8_t>> canvases, jpegs;
 };
-StageImages test_pipeline_images(const SliceInput& s, const PipelineParams& p, const RenderParams& rp);
+// `stages` (optional) receives the intermediate arrays (for --dump-mhd).
+StageImages test_pipeline_images(const SliceInput& s, const PipelineParams& p, const RenderParams& rp,
+                                 SliceResult* stages = nullptr);
 
 }  // namespace nm03::golden

@@ -36,6 +36,15 @@ def median2d(raw, k=7, pixel_type="u16", stored_bits=16):
     return out if raw.dim() == 3 else out[0]
 
 
+def threshold(x, lo, hi):
+    """BinaryThresholding: lo ≤ x ≤ hi → 1 (uint8), on an f32 CUDA tensor of any shape (K6)."""
+    _check(x, (torch.float32,), "x")
+    xc = x.contiguous()
+    out = torch.empty(xc.shape, dtype=torch.uint8, device=xc.device)
+    native().k_threshold(xc.data_ptr(), out.data_ptr(), xc.numel(), float(lo), float(hi), _stream())
+    return out
+
+
 def unpack_bits(words, width):
     """[N, H, wpr] int64 bit-planes → [N, H, width] bool (LSB = left-most pixel)."""
     sh = torch.arange(64, device=words.device, dtype=torch.int64)

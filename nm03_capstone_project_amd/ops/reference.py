@@ -41,6 +41,11 @@ def band(s, lo=0.74, hi=0.91):
     return (s >= lo) & (s <= hi)
 
 
+def threshold(x, lo, hi):
+    """BinaryThresholding reference: lo ≤ x ≤ hi → 1 (uint8)."""
+    return ((x >= lo) & (x <= hi)).to(torch.uint8)
+
+
 def dilate(mask, size=3):
     r = size // 2
     x = mask.float()[None, None]

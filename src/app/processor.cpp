@@ -19,6 +19,7 @@
 #include "nm03/dicom.h"
 #include "nm03/golden.h"
 #include "nm03/jpeg.h"
+#include "nm03/metaimage.h"
 #include "nm03/volume.h"
 
 namespace nm03::app {
@@ -46,6 +47,7 @@ void usage(const std::string& which) {
             << "  --input FILE           test_pipeline: slice to process\n"
             << "  --cpu                  test_pipeline: golden CPU model instead of the GPU\n"
             << "  --no-montage           test_pipeline: skip the 5-view montage JPEG\n"
+            << "  --dump-mhd DIR         test_pipeline: write stage arrays as MetaImage (.mhd/.raw)\n"
             << "  --repeat N             process the cohort N times (benchmarking)\n"
             << "  --json FILE            write run metrics as JSON\n"
             << "  --resume               keep existing outputs; skip slices whose two JPEGs exist\n"
@@ -135,6 +137,7 @@ AppConfig parse_args(int argc, char** argv, const std::string& which) {
     else if (a == "--input") c.input = val();
     else if (a == "--cpu") c.cpu = true;
     else if (a == "--no-montage") c.montage = false;
+    else if (a == "--dump-mhd") c.dump_mhd = val();
     else if (a == "--repeat") c.repeat = std::max(1, std::atoi(val().c_str()));
     else if (a == "--json") c.json = val();
     else if (a == "--quiet") c.quiet = true;
@@ -478,11 +481,17 @@ int run_test_pipeline(const AppConfig& cfg) {
     const PipelineParams& p = cfg.engine.pipe;
     const RenderParams& rp = cfg.engine.render;
     std::vector<std::vector<uint8_t>> canvases, jpegs;
+    // Stage arrays for --dump-mhd: sharpened f32 and the four masks (band, SRG, erosion, dilation).
+    std::vector<float> d_sharp;
+    std::vector<std::vector<uint8_t>> d_masks;
     const double t0 = now_s();
     if (cfg.cpu) {
-      golden::StageImages r = golden::test_pipeline_images(in, p, rp);
+      golden::SliceResult st;
+      golden::StageImages r = golden::test_pipeline_images(in, p, rp, cfg.dump_mhd.empty() ? nullptr : &st);
       canvases = std::move(r.canvases);
       jpegs = std::move(r.jpegs);
+      d_sharp = std::move(st.sharpened);
+      d_masks = {std::move(st.band), std::move(st.region), std::move(st.eroded), std::move(st.dilated)};
     } else {
       EngineConfig ec = cfg.engine;
       ec.batch_size = 1;
@@ -492,6 +501,18 @@ int run_test_pipeline(const AppConfig& cfg) {
       SingleResult r = engine.run_single(in);
       canvases = std::move(r.canvases);
       jpegs = std::move(r.jpegs);
+      d_sharp = std::move(r.sharpened);
+      d_masks = {std::move(r.band), std::move(r.region), std::move(r.eroded), std::move(r.dilated)};
+    }
+    if (!cfg.dump_mhd.empty()) {
+      cohort::make_dirs(cfg.dump_mhd);
+      const std::string b = cohort::with_slash(cfg.dump_mhd);
+      mhd::write(b + "input", in.raw.data(), in.w, in.h, 1, in.type == kI16 ? mhd::MetType::kShort : mhd::MetType::kUShort,
+                 in.spacing_x, in.spacing_y);
+      mhd::write(b + "sharpened", d_sharp.data(), in.w, in.h, 1, mhd::MetType::kFloat, in.spacing_x, in.spacing_y);
+      static const char* mnames[4] = {"band", "segmentation", "erosion", "dilation"};
+      for (int k = 0; k < 4; ++k)
+        mhd::write(b + mnames[k], d_masks[k].data(), in.w, in.h, 1, mhd::MetType::kUChar, in.spacing_x, in.spacing_y);
     }
     const double t1 = now_s();
     // exportImages: wipe + create the output directory, then the 5 stage images (:7-27).

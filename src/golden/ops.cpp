@@ -364,7 +364,8 @@ SliceJpegs export_jpegs(const SliceInput& s, const SliceResult& r, const Pipelin
   return j;
 }
 
-StageImages test_pipeline_images(const SliceInput& in, const PipelineParams& p, const RenderParams& rp) {
+StageImages test_pipeline_images(const SliceInput& in, const PipelineParams& p, const RenderParams& rp,
+                                 SliceResult* stages) {
   StageImages out;
   SliceResult r = run(in, p, true);
   const RenderGeom g = make_render_geom(in.w, in.h, in.spacing_x, in.spacing_y, rp.out_width, rp.out_height);
@@ -378,6 +379,7 @@ StageImages test_pipeline_images(const SliceInput& in, const PipelineParams& p, 
   c.push_back(render_labels(r.dilated, border(r.dilated, in.w, in.h, rp.border_radius), g, fill, bv));
   for (auto& cv : c) out.jpegs.push_back(jpeg::encode_gray420(cv.data(), rp.out_width, rp.out_height, rp.out_width,
                                                                rp.jpeg_quality));
+  if (stages) *stages = std::move(r);
   return out;
 }
 

@@ -14,6 +14,7 @@
 #include "nm03/comm.h"
 #include "nm03/dicom.h"
 #include "nm03/engine.h"
+#include "nm03/metaimage.h"
 #include "nm03/numa.h"
 #include "nm03/golden.h"
 #include "nm03/jpeg.h"
@@ -294,6 +295,39 @@ PYBIND11_MODULE(_nm03, m) {
       py::arg("instance") = 1, py::arg("patient_id") = "PGBM-000", py::arg("syntax") = "explicit",
       py::arg("preamble") = true);
   m.def("numa_parse_cpulist", &numa::parse_cpulist);
+  m.def(
+      "mhd_write",
+      [](const std::string& base, py::array arr, float sx, float sy, float sz) {
+        py::buffer_info bi = arr.request();
+        if (!(py::array::c_style & arr.flags())) throw std::invalid_argument("array must be C-contiguous");
+        mhd::MetType t;
+        const std::string f = bi.format;
+        if (bi.itemsize == 1) t = mhd::MetType::kUChar;
+        else if (bi.itemsize == 2 && (f == "H")) t = mhd::MetType::kUShort;
+        else if (bi.itemsize == 2 && (f == "h")) t = mhd::MetType::kShort;
+        else if (bi.itemsize == 4 && f == "f") t = mhd::MetType::kFloat;
+        else throw std::invalid_argument("mhd_write: uint8, uint16, int16 or float32 arrays only");
+        int w = 1, h = 1, d = 1;
+        if (bi.ndim == 2) { h = (int)bi.shape[0]; w = (int)bi.shape[1]; }
+        else if (bi.ndim == 3) { d = (int)bi.shape[0]; h = (int)bi.shape[1]; w = (int)bi.shape[2]; }
+        else throw std::invalid_argument("mhd_write: 2D or 3D arrays only");
+        mhd::write(base, bi.ptr, w, h, d, t, sx, sy, sz);
+      },
+      py::arg("base"), py::arg("array"), py::arg("sx") = 1.f, py::arg("sy") = 1.f, py::arg("sz") = 1.f);
+  m.def("mhd_read", [](const std::string& path) {
+    mhd::Image im = mhd::read(path);
+    std::vector<py::ssize_t> shape = im.d > 1 ? std::vector<py::ssize_t>{im.d, im.h, im.w}
+                                               : std::vector<py::ssize_t>{im.h, im.w};
+    py::array a;
+    switch (im.type) {
+      case mhd::MetType::kUChar: a = py::array_t<uint8_t>(shape); break;
+      case mhd::MetType::kUShort: a = py::array_t<uint16_t>(shape); break;
+      case mhd::MetType::kShort: a = py::array_t<int16_t>(shape); break;
+      case mhd::MetType::kFloat: a = py::array_t<float>(shape); break;
+    }
+    std::memcpy(a.mutable_data(), im.bytes.data(), im.bytes.size());
+    return py::make_tuple(a, py::make_tuple(im.spacing[0], im.spacing[1], im.spacing[2]));
+  });
   m.def("numa_node_cpus", &numa::node_cpus);
   m.def("read_pixels_direct", [](const std::string& path) {
     dicom::SliceFile f(path);
@@ -590,6 +624,11 @@ PYBIND11_MODULE(_nm03, m) {
       py::arg("seeds") = std::vector<std::tuple<int, int, int>>{}, py::arg("device") = 0);
 
   // ---- raw-pointer kernel entry points (torch interop; all synchronous on `stream`) ----------------
+  m.def("k_threshold", [](uintptr_t in, uintptr_t out, size_t n, float lo, float hi, uintptr_t stream) {
+    hipStream_t st = as_stream(stream);
+    gpu::launch_threshold((const float*)in, (uint8_t*)out, n, lo, hi, st);
+    gpu::check_hip(hipStreamSynchronize(st), "k_threshold");
+  });
   m.def("k_median", [](uintptr_t raw, uintptr_t out, int n, int h, int w, int k, const std::string& type, int stored_bits,
                        uintptr_t stream) {
     hipStream_t st = as_stream(stream);

@@ -53,3 +53,32 @@ def test_numa_cpulist_parsing(native):
     assert native.numa_parse_cpulist("0-63,128-191")[-1] == 191
     assert native.numa_parse_cpulist("") == []
     assert native.numa_node_cpus(-1) == []
+
+
+@pytest.mark.parametrize("dtype", [np.uint8, np.uint16, np.int16, np.float32])
+def test_metaimage_roundtrip(native, tmp_path, dtype):
+    a = (np.arange(3 * 5 * 7) % 200).astype(dtype).reshape(3, 5, 7)
+    native.mhd_write(str(tmp_path / "vol"), a, 0.5, 0.75, 2.0)
+    b, sp = native.mhd_read(str(tmp_path / "vol.mhd"))
+    assert b.dtype == a.dtype and np.array_equal(a, b) and sp == (0.5, 0.75, 2.0)
+    native.mhd_write(str(tmp_path / "img"), a[1].copy())
+    c, _ = native.mhd_read(str(tmp_path / "img.mhd"))
+    assert np.array_equal(c, a[1])
+    assert "NDims = 2" in (tmp_path / "img.mhd").read_text()
+
+
+def test_test_pipeline_dump_mhd_cpu(native, cohort_root, tmp_path):
+    """--dump-mhd writes the stage arrays; they equal the golden model of the same slice."""
+    dump = tmp_path / "mhd"
+    r = run_bin("test_pipeline", "--cpu", "--data-root", cohort_root, "--out", str(tmp_path / "o"),
+                "--dump-mhd", str(dump))
+    assert r.returncode == 0, r.stderr
+    raw, meta = native.read_slice(native.test_slice_path(cohort_root))
+    g = native.golden_run(raw, meta["type"], meta["stored_bits"], meta["slope"], meta["intercept"])
+    inp, _ = native.mhd_read(str(dump / "input.mhd"))
+    assert np.array_equal(inp.view(np.uint16), raw)
+    sh, _ = native.mhd_read(str(dump / "sharpened.mhd"))
+    assert np.array_equal(sh, g["sharpened"])
+    for name, key in (("band", "band"), ("segmentation", "region"), ("dilation", "dilated")):
+        m, _ = native.mhd_read(str(dump / f"{name}.mhd"))
+        assert np.array_equal(m.astype(bool), np.asarray(g[key]).astype(bool)), name

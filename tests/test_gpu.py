@@ -362,3 +362,24 @@ def test_log_levels(native, cohort_root, tmp_path):
     assert r.returncode == 0 and "[nm03 INFO] engine on device 0" in r.stdout
     r = run_bin("img_processing_parallel", "--data-root", cohort_root, "--out", str(tmp_path / "b"), "--quiet")
     assert r.returncode == 0 and "[nm03 INFO]" not in r.stdout
+
+
+def test_threshold_kernel_vs_torch(native):
+    from nm03_capstone_project_amd.ops import reference, threshold
+    x = torch.rand(3, 97, 131, device="cuda") * 2.0  # odd total size exercises the tail path
+    got = threshold(x, 0.74, 0.91)
+    assert got.dtype == torch.uint8 and torch.equal(got, reference.threshold(x, 0.74, 0.91))
+    y = torch.tensor([0.74, 0.91, 0.7399999, 0.9100001], device="cuda")
+    assert threshold(y, 0.74, 0.91).tolist() == [1, 1, 0, 0]
+
+
+def test_test_pipeline_dump_mhd_gpu_equals_cpu(native, cohort_root, tmp_path):
+    for backend in ("gpu", "cpu"):
+        args = ["--data-root", cohort_root, "--out", str(tmp_path / f"o_{backend}"),
+                "--dump-mhd", str(tmp_path / f"m_{backend}")]
+        r = run_bin("test_pipeline", *(["--cpu"] if backend == "cpu" else []), *args)
+        assert r.returncode == 0, r.stderr
+    for name in ("input", "sharpened", "band", "segmentation", "erosion", "dilation"):
+        a, _ = native.mhd_read(str(tmp_path / "m_gpu" / f"{name}.mhd"))
+        b, _ = native.mhd_read(str(tmp_path / "m_cpu" / f"{name}.mhd"))
+        assert np.array_equal(a.astype(np.float64), b.astype(np.float64)), name
