@@ -17,7 +17,7 @@ for r in $(seq $rounds); do
     for e in "${envs[@]}"; do [ "${e%%=*}" = "AB_ROOT" ] && script="${e#*=}/bench.py"; done
     args=()
     for e in "${envs[@]}"; do [ "${e%%=*}" = "AB_ARGS" ] && read -ra args <<< "${e#*=}"; done
-    line=$(env "${envs[@]}" timeout -k 10 200 python $script --steps ${STEPS:-20} --warmup 3 "${args[@]}" 2>/dev/null | grep metric) || exit 7
+    line=$(env "${envs[@]}" timeout -k 10 200 python $script --steps ${STEPS:-100} --warmup 5 "${args[@]}" 2>/dev/null | grep metric) || exit 7
     echo "{\"variant\": \"$v\", \"round\": $r, \"bench\": $line}" >> gpurun_out/ab.jsonl
   done
 done
