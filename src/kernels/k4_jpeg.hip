@@ -93,8 +93,9 @@ struct LBitWriter {
     else
       spill[wi - kPrivWords] = v;
   }
+  // `code` must fit in `len` bits (Huffman codes do; magnitudes are masked by the caller).
   __device__ __forceinline__ void put(uint32_t code, int len) {
-    acc = (acc << len) | (uint64_t)(code & ((1u << len) - 1u));
+    acc = (acc << len) | (uint64_t)code;
     nacc += len;
     bits += (uint32_t)len;
     if (nacc >= 32) {
@@ -218,6 +219,10 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(4))) vo
       mycoef[coef_slot(k >> 1, tid)] = (uint32_t)(uint16_t)a | ((uint32_t)(uint16_t)c << 16);
     }
   }
+  if (dbg == 2) {  // profiling variant: stop after FDCT + quantisation
+    if (dc0 == 0x7FFFFFF1 || nz == 0x123456789ull) w.total[0] = 1u;
+    return;
+  }
   sdc[tid] = dc0;
   // DC of the block preceding this workgroup's first block (0 at the start of the image).
   if (tid < 64) {
@@ -242,8 +247,11 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(4))) vo
   uint32_t bits = 0;
   if (valid) {
     LBitWriter lw(pbuf, pspill);
-    lw.put_sym(dctab[dn]);
-    if (dn) lw.put((uint32_t)(diff < 0 ? diff - 1 : diff), dn);
+    {
+      const uint32_t e = dctab[dn];
+      const uint32_t mag = (uint32_t)(diff < 0 ? diff - 1 : diff) & ((1u << dn) - 1u);
+      lw.put(((e & 0xFFFFu) << dn) | mag, (int)(e >> 16) + dn);
+    }
     int last = 0;
     for (uint64_t m = nz; m; m &= m - 1) {
       const int k = __builtin_ctzll(m);
@@ -254,8 +262,10 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(4))) vo
         run -= 16;
       }
       const int nb = mag_bits_fast(v);
-      lw.put_sym(actab[(run << 4) + nb]);
-      lw.put((uint32_t)(v < 0 ? v - 1 : v), nb);
+      // symbol and magnitude bits in one put: ≤ 16 + 11 bits
+      const uint32_t e = actab[(run << 4) + nb];
+      const uint32_t mag = (uint32_t)(v < 0 ? v - 1 : v) & ((1u << nb) - 1u);
+      lw.put(((e & 0xFFFFu) << nb) | mag, (int)(e >> 16) + nb);
       last = k;
     }
     if (last < 63) lw.put_sym(actab[0x00]);
@@ -267,6 +277,10 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(4))) vo
     }
     lw.finish();
     bits = lw.bits;
+  }
+  if (dbg == 3) {  // profiling variant: stop after Huffman coding
+    if (bits == 0x7FFFFFF1u) w.total[0] = 1u;
+    return;
   }
   // ---- 3. workgroup scan + look-back --------------------------------------------------------
   uint32_t agg = 0;

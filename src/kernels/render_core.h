@@ -122,17 +122,39 @@ __device__ __forceinline__ void render_block_2x(const RenderDesc& d, const uint1
   // Exact 2× fit: the source coordinate of canvas pixel k is 2b + k/2 - 0.25 (exact in f32), so
   // the interpolation weight is 0.75 for even and 0.25 for odd k — the very values render_pixel
   // computes — and floor(f) - (4b-1) == (k+1)/2 is a compile-time patch index.
+  // Columns are processed in pairs (2m, 2m+1) as float2 so the f32 multiplies and adds map to
+  // v_pk_mul_f32 / v_pk_add_f32; every element goes through exactly bilerp()'s and gray_u8()'s
+  // operation sequence (no contraction), so results are bit-identical to the scalar contract.
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  const f2 wx2 = {0.75f, 0.25f}, ix2 = {1.0f - 0.75f, 1.0f - 0.25f};
+  f2 hl[6][4];  // horizontal lerps: row j of the patch at canvas columns (2m, 2m+1)
+#pragma unroll
+  for (int j = 0; j < 6; ++j)
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const f2 a = {patch[j][m], patch[j][m + 1]}, bb = {patch[j][m + 1], patch[j][m + 2]};
+      const f2 t0 = ix2 * a;
+      const f2 t1 = wx2 * bb;
+      hl[j][m] = t0 + t1;
+    }
+  const f2 lo2 = {win.lo, win.lo}, inv2 = {win.inv, win.inv};
 #pragma unroll
   for (int r = 0; r < 8; ++r) {
     const int j0 = (r + 1) >> 1;
-    const float wy = (r & 1) ? 0.25f : 0.75f;
+    const float wy = (r & 1) ? 0.25f : 0.75f, iy = 1.0f - wy;
 #pragma unroll
-    for (int c = 0; c < 8; ++c) {
-      const int i0 = (c + 1) >> 1;
-      const float wx = (c & 1) ? 0.25f : 0.75f;
-      const float val =
-          bilerp(patch[j0][i0], patch[j0][i0 + 1], patch[j0 + 1][i0], patch[j0 + 1][i0 + 1], wx, wy);
-      px[r * 8 + c] = (int32_t)gray_u8(val, win.lo, win.inv);
+    for (int m = 0; m < 4; ++m) {
+      const f2 u0 = iy * hl[j0][m];
+      const f2 u1 = wy * hl[j0 + 1][m];
+      const f2 val = u0 + u1;
+      f2 g = val - lo2;
+      g = g * inv2;
+      g.x = g.x < 0.0f ? 0.0f : (g.x > 1.0f ? 1.0f : g.x);
+      g.y = g.y < 0.0f ? 0.0f : (g.y > 1.0f ? 1.0f : g.y);
+      f2 t = g * 255.0f;
+      t = t + 0.5f;
+      px[r * 8 + 2 * m] = (int32_t)(uint8_t)(int)t.x;
+      px[r * 8 + 2 * m + 1] = (int32_t)(uint8_t)(int)t.y;
     }
   }
 }
