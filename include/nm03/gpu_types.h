@@ -27,7 +27,7 @@ struct SliceDesc {
   uint16_t seed_count;
   uint16_t flags;
   uint32_t f32_off;    // f32 element offset for optional sharpened output
-  uint32_t pad;
+  uint32_t med_tile0;  // index of the slice's first median tile in the batch tile list
 };
 static_assert(sizeof(SliceDesc) == 40, "SliceDesc layout");
 

@@ -17,14 +17,16 @@ void check_launch(const char* what);
 bool sync_launches();
 
 // K1a: k×k median of raw keys → `med` (u16 keys, same layout as raw). k ∈ {3,5,7,9}.
+// Per-slice key range: with `tile_mm` (2 u32 per tile) each tile stores its (min, max) and
+// launch_sharpen_band reduces them into stats (no atomics); without it, atomics on stats.
 void launch_median(const uint16_t* raw, uint16_t* med, const SliceDesc* descs, const TileDesc* tiles, int ntiles,
-                   int k, SliceStats* stats, hipStream_t stream);
+                   int k, SliceStats* stats, hipStream_t stream, uint32_t* tile_mm = nullptr);
 
 // K1b: normalise+clip of the median keys, separable Gaussian unsharp mask, SRG band test →
 // `band` bitmaps (u64 words, LSB = left-most pixel). Optionally the f32 sharpened image.
 void launch_sharpen_band(const uint16_t* med, uint64_t* band, float* sharpened, const SliceDesc* descs,
                          const TileDesc* tiles, int ntiles, const PipeConsts& pc, SliceStats* stats,
-                         hipStream_t stream);
+                         hipStream_t stream, const uint32_t* tile_mm = nullptr);
 
 // Bitmap planes produced by K2 (each null when not requested).
 struct SrgOutputs {

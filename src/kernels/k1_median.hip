@@ -13,6 +13,8 @@
 //   keys for the original-image render window.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "device_util.h"
 #include "nm03/gpu_types.h"
 #include "nm03/kernels.h"
@@ -35,7 +37,8 @@ __device__ __forceinline__ void run_net(const uint32_t* P, int stride, int r, in
 template <int K>
 __global__ __launch_bounds__(256) void median_kernel(const uint16_t* __restrict__ raw, uint16_t* __restrict__ med,
                                                      const SliceDesc* __restrict__ descs,
-                                                     const TileDesc* __restrict__ tiles, SliceStats* stats) {
+                                                     const TileDesc* __restrict__ tiles, SliceStats* stats,
+                                                     uint32_t* __restrict__ tile_mm, int dbg) {
   constexpr int R = K / 2;
   constexpr int PW = 32 + K - 1;  // pair columns
   constexpr int PS = PW | 1;      // odd stride: conflict-free ds_read_b32
@@ -102,7 +105,12 @@ __global__ __launch_bounds__(256) void median_kernel(const uint16_t* __restrict_
 
   const int g = threadIdx.x & 3, r = threadIdx.x >> 2;
   u16x2 out[8];
-  run_net<K>(P, PS, r, g, out);
+  if (dbg == 1) {  // profiling variant: tile load + store only
+#pragma unroll
+    for (int j = 0; j < 8; ++j) out[j] = as_u16x2(P[(r + R) * PS + 8 * g + j + R]);
+  } else {
+    run_net<K>(P, PS, r, g, out);
+  }
 
   const int y = y0 + r;
   if (y < H) {
@@ -130,24 +138,47 @@ __global__ __launch_bounds__(256) void median_kernel(const uint16_t* __restrict_
     }
   }
 
-  // Per-slice key range (render window of the original image).
+  // Per-slice key range (render window of the original image). Same-address device atomics from
+  // every wave of a slice serialise (≈12 us per 64-slice batch): instead each tile stores its
+  // range and the sharpen kernel reduces the slice's tiles.
   kmin = wave_min_u32(kmin);
   kmax = wave_max_u32(kmax);
-  if ((threadIdx.x & 63) == 0 && stats) {
+  if (tile_mm) {
+    __shared__ uint32_t smm[8];
+    const int wv = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+      smm[2 * wv] = kmin;
+      smm[2 * wv + 1] = kmax;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      uint32_t a = smm[0], b = smm[1];
+      for (int i = 1; i < 4; ++i) {
+        a = min(a, smm[2 * i]);
+        b = max(b, smm[2 * i + 1]);
+      }
+      tile_mm[2 * blockIdx.x] = a;
+      tile_mm[2 * blockIdx.x + 1] = b;
+    }
+  } else if ((threadIdx.x & 63) == 0 && stats) {
     atomicMin(&stats[t.slice].key_min, kmin);
     atomicMax(&stats[t.slice].key_max, kmax);
   }
 }
 
 void launch_median(const uint16_t* raw, uint16_t* med, const SliceDesc* descs, const TileDesc* tiles, int ntiles,
-                   int k, SliceStats* stats, hipStream_t stream) {
+                   int k, SliceStats* stats, hipStream_t stream, uint32_t* tile_mm) {
   if (ntiles <= 0) return;
   dim3 grid(ntiles), block(256);
+  static const int dbg = [] {  // NM03_MEDIAN_DBG=1: profiling variant (output invalid)
+    const char* e = std::getenv("NM03_MEDIAN_DBG");
+    return e ? std::atoi(e) : 0;
+  }();
   switch (k) {
-    case 3: median_kernel<3><<<grid, block, 0, stream>>>(raw, med, descs, tiles, stats); break;
-    case 5: median_kernel<5><<<grid, block, 0, stream>>>(raw, med, descs, tiles, stats); break;
-    case 7: median_kernel<7><<<grid, block, 0, stream>>>(raw, med, descs, tiles, stats); break;
-    case 9: median_kernel<9><<<grid, block, 0, stream>>>(raw, med, descs, tiles, stats); break;
+    case 3: median_kernel<3><<<grid, block, 0, stream>>>(raw, med, descs, tiles, stats, tile_mm, dbg); break;
+    case 5: median_kernel<5><<<grid, block, 0, stream>>>(raw, med, descs, tiles, stats, tile_mm, dbg); break;
+    case 7: median_kernel<7><<<grid, block, 0, stream>>>(raw, med, descs, tiles, stats, tile_mm, dbg); break;
+    case 9: median_kernel<9><<<grid, block, 0, stream>>>(raw, med, descs, tiles, stats, tile_mm, dbg); break;
     default: throw DeviceError("median window must be 3, 5, 7 or 9 (got " + std::to_string(k) + ")");
   }
   check_launch("median_kernel");

@@ -24,7 +24,7 @@ __global__ __launch_bounds__(256) void sharpen_band_kernel(const uint16_t* __res
                                                            float* __restrict__ sharpened,
                                                            const SliceDesc* __restrict__ descs,
                                                            const TileDesc* __restrict__ tiles, PipeConsts pc,
-                                                           SliceStats* stats) {
+                                                           SliceStats* stats, const uint32_t* __restrict__ tile_mm) {
   __shared__ float C[(kShpTileH + 2 * kMaxR) * kCS];
   __shared__ float T[kShpTileH * kCS];
   const TileDesc t = tiles[blockIdx.x];
@@ -44,6 +44,21 @@ __global__ __launch_bounds__(256) void sharpen_band_kernel(const uint16_t* __res
   nc.cmin = pc.cmin;
   nc.cmax = pc.cmax;
 
+  // The slice's first tile folds the median tiles' key ranges into stats (render window).
+  if (tile_mm && stats && t.tx == 0 && t.ty == 0 && threadIdx.x < 64) {
+    const int ntl = ((W + kMedTileW - 1) / kMedTileW) * ((H + kMedTileH - 1) / kMedTileH);
+    uint32_t a = 0xFFFFFFFFu, b = 0u;
+    for (int i = threadIdx.x; i < ntl; i += 64) {
+      a = min(a, tile_mm[2 * (d.med_tile0 + i)]);
+      b = max(b, tile_mm[2 * (d.med_tile0 + i) + 1]);
+    }
+    a = wave_min_u32(a);
+    b = wave_max_u32(b);
+    if (threadIdx.x == 0) {
+      stats[t.slice].key_min = a;
+      stats[t.slice].key_max = b;
+    }
+  }
   for (int i = threadIdx.x; i < ch * cw; i += 256) {
     const int r = i / cw, c = i - r * cw;
     const int y = clampi(y0 - R + r, 0, H - 1), x = clampi(x0 - R + c, 0, W - 1);
@@ -94,10 +109,10 @@ __global__ __launch_bounds__(256) void sharpen_band_kernel(const uint16_t* __res
 
 void launch_sharpen_band(const uint16_t* med, uint64_t* band, float* sharpened, const SliceDesc* descs,
                          const TileDesc* tiles, int ntiles, const PipeConsts& pc, SliceStats* stats,
-                         hipStream_t stream) {
+                         hipStream_t stream, const uint32_t* tile_mm) {
   if (ntiles <= 0) return;
   if (pc.mask_radius < 0 || pc.mask_radius > kMaxR) throw DeviceError("sharpen mask must be ≤ 15");
-  sharpen_band_kernel<<<ntiles, 256, 0, stream>>>(med, band, sharpened, descs, tiles, pc, stats);
+  sharpen_band_kernel<<<ntiles, 256, 0, stream>>>(med, band, sharpened, descs, tiles, pc, stats, tile_mm);
   check_launch("sharpen_band_kernel");
 }
 

@@ -63,6 +63,7 @@ struct Slot {
   uint8_t* h_blob = nullptr;
   uint8_t* d_blob = nullptr;
   uint16_t* d_med = nullptr;
+  uint32_t* d_tile_mm = nullptr;  // per median tile (min, max) key
   float* d_f32 = nullptr;
   uint64_t* d_bits = nullptr;
   size_t plane_words = 0;
@@ -88,7 +89,7 @@ void hip_free_all(Slot& s) {
   if (s.h_blob) (void)hipHostFree(s.h_blob);
   if (s.h_out) (void)hipHostFree(s.h_out);
   if (s.h_sizes) (void)hipHostFree(s.h_sizes);
-  for (void* p : {(void*)s.d_blob, (void*)s.d_med, (void*)s.d_f32, (void*)s.d_bits, (void*)s.d_canvas,
+  for (void* p : {(void*)s.d_blob, (void*)s.d_med, (void*)s.d_tile_mm, (void*)s.d_f32, (void*)s.d_bits, (void*)s.d_canvas,
                   (void*)s.jw.stage, (void*)s.jw.look, (void*)s.jw.ticket, (void*)s.jw.spill,
                   (void*)s.jw.total, (void*)s.jw.chunk_ff})
     if (p) (void)hipFree(p);
@@ -213,6 +214,7 @@ struct Engine::Impl {
       check_hip(hipHostMalloc((void**)&s.h_blob, s.blob_bytes, hipHostMallocDefault), "hipHostMalloc blob");
       s.d_blob = dmalloc<uint8_t>(s.blob_bytes, "hipMalloc blob");
       s.d_med = dmalloc<uint16_t>(s.cap_pixels, "hipMalloc median");
+      s.d_tile_mm = dmalloc<uint32_t>(2 * s.max_medt, "hipMalloc tile ranges");
       s.d_f32 = dmalloc<float>(s.cap_pixels, "hipMalloc f32");
       s.plane_words = (size_t)B * md * ((md + 63) / 64);
       s.d_bits = dmalloc<uint64_t>(s.plane_words * kNumPlanes, "hipMalloc bits");
@@ -336,6 +338,7 @@ struct Engine::Impl {
       d.seed_off = (uint32_t)nseed;
       d.seed_count = (uint16_t)std::min<size_t>(sv.size(), kMaxSeeds);
       for (int k = 0; k < d.seed_count; ++k) seeds[nseed++] = SeedXY{(int16_t)sv[k].x, (int16_t)sv[k].y};
+      d.med_tile0 = (uint32_t)nmed;
       for (int ty = 0; ty < (L.h + kMedTileH - 1) / kMedTileH; ++ty)
         for (int tx = 0; tx < (L.w + kMedTileW - 1) / kMedTileW; ++tx) medt[nmed++] = TileDesc{(uint32_t)c, (uint16_t)tx, (uint16_t)ty};
       for (int ty = 0; ty < (L.h + kShpTileH - 1) / kShpTileH; ++ty)
@@ -418,9 +421,9 @@ struct Engine::Impl {
     check_hip(hipMemcpyAsync(s.d_blob, s.h_blob, bytes, hipMemcpyHostToDevice, s.stream), "H2D blob");
     check_hip(hipEventRecord(s.ev1, s.stream), "event");
     auto chain = [&] {
-      launch_median(d_raw, s.d_med, d_desc, d_medt, nmed, pc.median_k, d_stats, s.stream);
+      launch_median(d_raw, s.d_med, d_desc, d_medt, nmed, pc.median_k, d_stats, s.stream, s.d_tile_mm);
       launch_sharpen_band(s.d_med, plane(kPBand), mode == 1 ? s.d_f32 : nullptr, d_desc, d_shpt, nshp, pc, d_stats,
-                          s.stream);
+                          s.stream, s.d_tile_mm);
       SrgOutputs o;
       o.dilated = plane(kPDilated);
       o.border_dilated = plane(kPBorderD);
