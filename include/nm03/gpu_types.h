@@ -11,7 +11,7 @@ namespace nm03::gpu {
 // Median kernel output tile (64 columns × 64 rows) and sharpen/band tile (64 × 16: one mask word
 // per row, produced by a wave ballot).
 inline constexpr int kMedTileW = 64, kMedTileH = 64;
-inline constexpr int kShpTileW = 64, kShpTileH = 16;
+inline constexpr int kShpTileW = 64, kShpTileH = 64;
 // Largest slice the LDS-resident region-growing kernel handles (bit-planes in LDS).
 inline constexpr int kSrgMaxDim = 512;
 

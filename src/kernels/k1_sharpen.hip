@@ -2,11 +2,18 @@
 // both are monotone), ImageSharpening (9×9 Gaussian unsharp mask, main_sequential.cpp:208-210)
 // and the SeededRegionGrowing band test [0.74, 0.91] (main_sequential.cpp:232-233).
 //
-// One workgroup = 256 threads = a 64×16 output tile. Lane = column, so the band test of a row
-// is one __ballot → one 64-bit mask word (no bit packing pass). The clamp-to-edge input tile
-// (16+2R)×(64+2R) f32 and the vertical-pass tile live in LDS; the Gaussian is applied
-// separably in the contract order of golden::sharpen (vertical, then horizontal, taps ascending,
-// no FMA contraction), so the result is bit-identical to the CPU golden model.
+// One workgroup = 256 threads = a 64×64 output tile; the mask radius R is a template parameter
+// (compile-time tile geometry: no runtime divisions in the index math).
+//  1. the clamp-to-edge (64+2R)² input tile is loaded in 8-byte groups of 4 median keys
+//     (per-key clamped loads only where a group leaves the image), normalised+clipped once per
+//     key and kept in LDS as f32;
+//  2. vertical pass: a thread owns a column × 16 rows and slides a (16+2R)-value window held in
+//     registers (each LDS value read once instead of 2R+1 times);
+//  3. horizontal pass + combine + band: a thread owns 16 columns of a row (register window
+//     again); the band bits of the four 16-column segments form the row's 64-bit mask word.
+// The Gaussian is applied separably in the contract order of golden::sharpen (vertical, then
+// horizontal, taps ascending, no FMA contraction), so the result is bit-identical to the CPU
+// golden model.
 #include <hip/hip_runtime.h>
 
 #include "device_util.h"
@@ -17,21 +24,25 @@
 namespace nm03::gpu {
 
 constexpr int kMaxR = 7;
-constexpr int kCW = kShpTileW + 2 * kMaxR;  // 78
-constexpr int kCS = kCW + 1;                // LDS row stride (odd)
+static_assert(kShpTileW == 64 && kShpTileH == 64, "sharpen tile is 64x64");
 
+template <int R>
 __global__ __launch_bounds__(256) void sharpen_band_kernel(const uint16_t* __restrict__ med, uint64_t* __restrict__ band,
                                                            float* __restrict__ sharpened,
                                                            const SliceDesc* __restrict__ descs,
                                                            const TileDesc* __restrict__ tiles, PipeConsts pc,
                                                            SliceStats* stats, const uint32_t* __restrict__ tile_mm) {
-  __shared__ float C[(kShpTileH + 2 * kMaxR) * kCS];
-  __shared__ float T[kShpTileH * kCS];
+  constexpr int TW = kShpTileW, TH = kShpTileH;
+  constexpr int CW = TW + 2 * R, CH = TH + 2 * R;
+  constexpr int CS = CW | 1;          // odd LDS row stride
+  constexpr int RA = (R + 3) / 4;     // 4-key groups of halo on each side
+  constexpr int G = TW / 4 + 2 * RA;  // groups per input row
+  constexpr int RB = 16;              // rows per vertical-pass task
+  __shared__ float C[CH * CS];
+  __shared__ float T[TH * CS];
   const TileDesc t = tiles[blockIdx.x];
   const SliceDesc d = descs[t.slice];
-  const int R = pc.mask_radius;
-  const int cw = kShpTileW + 2 * R, ch = kShpTileH + 2 * R;
-  const int x0 = t.tx * kShpTileW, y0 = t.ty * kShpTileH;
+  const int x0 = t.tx * TW, y0 = t.ty * TH;
   const int W = d.w, H = d.h;
   const uint16_t* src = med + d.raw_off;
   NormClip nc;
@@ -59,48 +70,104 @@ __global__ __launch_bounds__(256) void sharpen_band_kernel(const uint16_t* __res
       stats[t.slice].key_max = b;
     }
   }
-  for (int i = threadIdx.x; i < ch * cw; i += 256) {
-    const int r = i / cw, c = i - r * cw;
-    const int y = clampi(y0 - R + r, 0, H - 1), x = clampi(x0 - R + c, 0, W - 1);
-    C[r * kCS + c] = norm_clip_key(src[(size_t)y * W + x], d.type, nc);
-  }
-  __syncthreads();
-  // Vertical pass for the 16 output rows over all cw columns.
-  for (int i = threadIdx.x; i < kShpTileH * cw; i += 256) {
-    const int r = i / cw, c = i - r * cw;
-    float acc = 0.0f;
-    for (int k = 0; k <= 2 * R; ++k) {
-      const float p = pc.taps[k] * C[(r + k) * kCS + c];
-      acc = acc + p;
+
+  // ---- 1. input tile → normalised+clipped f32 in LDS ------------------------------------------
+  if ((W & 3) == 0 && (d.raw_off & 3) == 0) {
+    // Window columns x0 - 4·RA + 4g + q; tile column c = 4g + q - (4·RA - R).
+    for (int i = threadIdx.x; i < CH * G; i += 256) {
+      const int r = i / G, g = i - r * G;
+      const int y = clampi(y0 - R + r, 0, H - 1);
+      const uint16_t* row = src + (size_t)y * W;
+      const int xs = x0 - 4 * RA + 4 * g;
+      uint16_t px[4];
+      if (xs >= 0 && xs + 4 <= W) {
+        const uint2 v = *reinterpret_cast<const uint2*>(row + xs);
+        px[0] = (uint16_t)v.x;
+        px[1] = (uint16_t)(v.x >> 16);
+        px[2] = (uint16_t)v.y;
+        px[3] = (uint16_t)(v.y >> 16);
+      } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) px[q] = row[clampi(xs + q, 0, W - 1)];
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int c = 4 * g + q - (4 * RA - R);
+        if (c >= 0 && c < CW) C[r * CS + c] = norm_clip_key(px[q], d.type, nc);
+      }
     }
-    T[r * kCS + c] = acc;
+  } else {
+    for (int i = threadIdx.x; i < CH * CW; i += 256) {
+      const int r = i / CW, c = i - r * CW;
+      const int y = clampi(y0 - R + r, 0, H - 1), x = clampi(x0 - R + c, 0, W - 1);
+      C[r * CS + c] = norm_clip_key(src[(size_t)y * W + x], d.type, nc);
+    }
   }
   __syncthreads();
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+
+  // ---- 2. vertical pass: column c, rows [RB·rb, RB·rb + RB) from a register window -----------
+  for (int task = threadIdx.x; task < CW * (TH / RB); task += 256) {
+    const int rb = task / CW, c = task - rb * CW;
+    float win[RB + 2 * R];
+#pragma unroll
+    for (int k = 0; k < RB + 2 * R; ++k) win[k] = C[(rb * RB + k) * CS + c];
+#pragma unroll
+    for (int rr = 0; rr < RB; ++rr) {
+      float acc = 0.0f;
+#pragma unroll
+      for (int k = 0; k <= 2 * R; ++k) {
+        const float p = pc.taps[k] * win[rr + k];
+        acc = acc + p;
+      }
+      T[(rb * RB + rr) * CS + c] = acc;
+    }
+  }
+  __syncthreads();
+
+  // ---- 3. horizontal pass + combine + band: a thread owns row r, columns [16·seg, 16·seg + 16)
+  //         and slides a (16+2R)-value register window; band bits go through LDS to form the
+  //         64-bit row words.
+  __shared__ uint16_t bm[TH * 4];
+  const int r = threadIdx.x >> 2, seg = threadIdx.x & 3;
+  const int y = y0 + r;
   float smin = INFINITY, smax = -INFINITY;
-  for (int rr = wave * 4; rr < wave * 4 + 4; ++rr) {
-    float acc = 0.0f;
-    for (int k = 0; k <= 2 * R; ++k) {
-      const float p = pc.taps[k] * T[rr * kCS + lane + k];
-      acc = acc + p;
+  {
+    float win[16 + 2 * R];
+#pragma unroll
+    for (int k = 0; k < 16 + 2 * R; ++k) win[k] = T[r * CS + 16 * seg + k];
+    uint32_t bits = 0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      float acc = 0.0f;
+#pragma unroll
+      for (int k = 0; k <= 2 * R; ++k) {
+        const float p = pc.taps[k] * win[j + k];
+        acc = acc + p;
+      }
+      const int xj = x0 + 16 * seg + j;
+      const float cv = C[(r + R) * CS + 16 * seg + j + R];
+      const float sv = sharpen_combine(cv, acc, pc.gain);
+      const bool inside = xj < W && y < H;
+      bits |= (inside && in_band(sv, pc.band_lo, pc.band_hi)) ? (1u << j) : 0u;
+      if (sharpened && inside) {
+        sharpened[d.f32_off + (size_t)y * W + xj] = sv;
+        smin = fminf(smin, sv);
+        smax = fmaxf(smax, sv);
+      }
     }
-    const float c = C[(rr + R) * kCS + lane + R];
-    const float s = sharpen_combine(c, acc, pc.gain);
-    const int x = x0 + lane, y = y0 + rr;
-    const bool inside = x < W && y < H;
-    const unsigned long long word = __ballot(inside && in_band(s, pc.band_lo, pc.band_hi));
-    if (y < H && lane == 0) band[d.mask_off + (size_t)y * d.wpr + t.tx] = word;
-    if (sharpened && inside) {
-      sharpened[d.f32_off + (size_t)y * W + x] = s;
-      smin = fminf(smin, s);
-      smax = fmaxf(smax, s);
-    }
+    bm[r * 4 + seg] = (uint16_t)bits;
+  }
+  __syncthreads();
+  if (threadIdx.x < TH && y0 + (int)threadIdx.x < H) {
+    const uint16_t* q = bm + threadIdx.x * 4;
+    const uint64_t word = (uint64_t)q[0] | ((uint64_t)q[1] << 16) | ((uint64_t)q[2] << 32) | ((uint64_t)q[3] << 48);
+    band[d.mask_off + (size_t)(y0 + threadIdx.x) * d.wpr + t.tx] = word;
   }
   if (sharpened && stats) {
     uint32_t a = float_to_ordered(smin), b = float_to_ordered(smax);
     a = wave_min_u32(a);
     b = wave_max_u32(b);
-    if (lane == 0) {
+    if ((threadIdx.x & 63) == 0) {
       atomicMin(&stats[t.slice].s_min, a);
       atomicMax(&stats[t.slice].s_max, b);
     }
@@ -111,8 +178,22 @@ void launch_sharpen_band(const uint16_t* med, uint64_t* band, float* sharpened, 
                          const TileDesc* tiles, int ntiles, const PipeConsts& pc, SliceStats* stats,
                          hipStream_t stream, const uint32_t* tile_mm) {
   if (ntiles <= 0) return;
-  if (pc.mask_radius < 0 || pc.mask_radius > kMaxR) throw DeviceError("sharpen mask must be ≤ 15");
-  sharpen_band_kernel<<<ntiles, 256, 0, stream>>>(med, band, sharpened, descs, tiles, pc, stats, tile_mm);
+#define NM03_SHARPEN_CASE(RR)                                                                              \
+  case RR:                                                                                               \
+    sharpen_band_kernel<RR><<<ntiles, 256, 0, stream>>>(med, band, sharpened, descs, tiles, pc, stats, tile_mm); \
+    break;
+  switch (pc.mask_radius) {
+    NM03_SHARPEN_CASE(0)
+    NM03_SHARPEN_CASE(1)
+    NM03_SHARPEN_CASE(2)
+    NM03_SHARPEN_CASE(3)
+    NM03_SHARPEN_CASE(4)
+    NM03_SHARPEN_CASE(5)
+    NM03_SHARPEN_CASE(6)
+    NM03_SHARPEN_CASE(7)
+    default: throw DeviceError("sharpen mask must be ≤ 15");
+  }
+#undef NM03_SHARPEN_CASE
   check_launch("sharpen_band_kernel");
 }
 

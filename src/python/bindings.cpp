@@ -152,7 +152,7 @@ BatchTables upload_tables(int n, int h, int w, PixelType type, int stored_bits, 
     for (auto& q : seeds) sd.push_back({(int16_t)q.x, (int16_t)q.y});
     for (int ty = 0; ty < (h + 63) / 64; ++ty)
       for (int tx = 0; tx < (w + 63) / 64; ++tx) mt.push_back({(uint32_t)i, (uint16_t)tx, (uint16_t)ty});
-    for (int ty = 0; ty < (h + 15) / 16; ++ty)
+    for (int ty = 0; ty < (h + gpu::kShpTileH - 1) / gpu::kShpTileH; ++ty)
       for (int tx = 0; tx < wpr; ++tx) sh.push_back({(uint32_t)i, (uint16_t)tx, (uint16_t)ty});
   }
   if (sd.empty()) sd.push_back({0, 0});

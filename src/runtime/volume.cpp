@@ -95,7 +95,7 @@ struct VolumeDevice {
         raw(ps * v.d * 2), med(ps * v.d * 2), band(words * v.d * 8), region(words * v.d * 8), dil(words * v.d * 8),
         tmp(words * v.d * 8), desc(sizeof(SliceDesc) * v.d),
         medt(sizeof(TileDesc) * v.d * ((v.w + 63) / 64) * ((v.h + 63) / 64)),
-        shpt(sizeof(TileDesc) * v.d * ((v.w + 63) / 64) * ((v.h + 15) / 16)), stats(sizeof(SliceStats) * v.d),
+        shpt(sizeof(TileDesc) * v.d * ((v.w + 63) / 64) * ((v.h + kShpTileH - 1) / kShpTileH)), stats(sizeof(SliceStats) * v.d),
         seeds(sizeof(int32_t) * 3 * kMaxSeeds), flag(16) {
     check_hip(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking), "stream");
     check_hip(hipHostMalloc((void**)&h_flag, 16, hipHostMallocDefault), "hipHostMalloc flag");
@@ -124,7 +124,7 @@ static void volume_preprocess(VolumeDevice& V, const VolumeInput& v, const Pipel
     s.intercept = p.apply_rescale ? v.intercept : 0.f;
     for (int ty = 0; ty < (v.h + 63) / 64; ++ty)
       for (int tx = 0; tx < (v.w + 63) / 64; ++tx) mt.push_back({(uint32_t)z, (uint16_t)tx, (uint16_t)ty});
-    for (int ty = 0; ty < (v.h + 15) / 16; ++ty)
+    for (int ty = 0; ty < (v.h + kShpTileH - 1) / kShpTileH; ++ty)
       for (int tx = 0; tx < V.wpr; ++tx) st.push_back({(uint32_t)z, (uint16_t)tx, (uint16_t)ty});
   }
   std::vector<SliceStats> stats(v.d, SliceStats{0xFFFFFFFFu, 0u, 0xFFFFFFFFu, 0u});
