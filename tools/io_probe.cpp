@@ -5,6 +5,7 @@
 #include <unistd.h>
 
 #include <atomic>
+#include <cstdlib>
 #include <chrono>
 #include <cstdio>
 #include <string>
@@ -28,9 +29,11 @@ int main(int argc, char** argv) {
     for (auto& f : nm03::cohort::list_patient_series(base, p).files) files.push_back(f);
   nm03::cohort::make_dirs(out);
   std::vector<uint8_t> hdr(623, 0x11), seg(15000, 0x22);
-  for (int nt : {1, threads}) {
-    for (int rep = 0; rep < 3; ++rep) {
+  for (int d = 0; d < 20; ++d) nm03::cohort::make_dirs(out + "/d" + std::to_string(d));
+  for (int nt : {1, 4, 8, threads}) {
+    for (int rep = 0; rep < 2; ++rep) {
       std::atomic<size_t> next{0};
+      const int odfd = open(out.c_str(), O_RDONLY | O_DIRECTORY | O_CLOEXEC);
       auto work = [&](int phase) {
         std::vector<uint8_t> scratch;
         std::vector<uint16_t> px(512 * 512);
@@ -39,15 +42,24 @@ int main(int argc, char** argv) {
             nm03::dicom::SliceFile sf(files[i]);
             sf.header(scratch);
             sf.pixels16(px.data());
-          } else {
-            const std::string b = out + "/" + std::to_string(i);
+          } else if (phase == 1) {  // like the engine: 20 patient directories
+            const std::string b = out + "/d" + std::to_string(i % 20) + "/" + std::to_string(i);
             nm03::jpeg::write_jpeg_file(b + "_a.jpg", hdr, seg.data(), seg.size());
             nm03::jpeg::write_jpeg_file(b + "_b.jpg", hdr, seg.data(), seg.size());
+          } else {  // phase 2: same writes relative to a directory fd (openat)
+            for (const char* sfx : {"_a.jpg", "_b.jpg"}) {
+              const std::string nm = std::to_string(i) + sfx;
+              const int fd = openat(odfd, nm.c_str(), O_WRONLY | O_CREAT | O_CLOEXEC, 0644);
+              if (pwrite(fd, seg.data(), seg.size(), 0) < 0) std::abort();
+              struct stat st;
+              fstat(fd, &st);
+              close(fd);
+            }
           }
         }
       };
-      double t[2];
-      for (int phase = 0; phase < 2; ++phase) {
+      double t[3];
+      for (int phase = 0; phase < 3; ++phase) {
         next = 0;
         const double t0 = now();
         std::vector<std::thread> th;
@@ -55,10 +67,11 @@ int main(int argc, char** argv) {
         for (auto& x : th) x.join();
         t[phase] = now() - t0;
       }
+      close(odfd);
       std::printf("{\"threads\": %d, \"load_us_per_slice\": %.2f, \"write_us_per_slice_pair\": %.2f, "
-                  "\"load_slices_per_s\": %.0f, \"write_pairs_per_s\": %.0f}\n",
-                  nt, t[0] * 1e6 * nt / files.size(), t[1] * 1e6 * nt / files.size(), files.size() / t[0],
-                  files.size() / t[1]);
+                  "\"write_openat_us_per_pair\": %.2f, \"load_slices_per_s\": %.0f, \"write_pairs_per_s\": %.0f}\n",
+                  nt, t[0] * 1e6 * nt / files.size(), t[1] * 1e6 * nt / files.size(), t[2] * 1e6 * nt / files.size(),
+                  files.size() / t[0], files.size() / t[1]);
     }
   }
 }
