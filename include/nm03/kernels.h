@@ -70,7 +70,7 @@ struct JpegWork {
   uint64_t* look = nullptr;      // look_cap look-back status words (zeroed once; cleared after use)
   size_t look_cap = 0;           // ≥ ncanvas × ceil(blocks / 256)
   size_t look_used = 0;          // set by launch_jpeg
-  uint32_t* ticket = nullptr;    // ordered workgroup ticket counter (zeroed once; self-resetting)
+  uint32_t* ticket = nullptr;    // per-image part ticket counters (≥ ncanvas; zeroed once; self-resetting)
   uint32_t* spill = nullptr;     // look_cap × 256 × 56 words: Huffman bits of very detailed blocks
   uint32_t* total = nullptr;     // ncanvas: total bits (0xFFFFFFFF = overflow)
   uint32_t* chunk_ff = nullptr;  // ncanvas × max_chunks: 0xFF bytes per stuffing chunk

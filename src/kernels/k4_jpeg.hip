@@ -113,15 +113,14 @@ __device__ __forceinline__ uint32_t priv_word(const uint32_t* pb, const uint32_t
   return i < (uint32_t)kPrivWords ? pb[i] : spill[i - kPrivWords];
 }
 
-// Single-pass encoder: workgroup L = blockIdx encodes blocks [256p, 256p+256) of image i.
+// Single-pass encoder: workgroup with ticket L encodes blocks [256p, 256p+256) of image i.
 //  1. render (fused 2×) or read the 8×8 block, islow FDCT, reciprocal quantisation;
 //  2. Huffman cost of the block (DC needs the previous block's DC: LDS neighbour, and for the
 //     first block of the workgroup a wave-0 recomputation of the preceding block's DC = Σ(x-128));
 //  3. workgroup exclusive scan of the costs, then a decoupled look-back over the image's earlier
-//     workgroups. Workgroups are dispatched in index order (per XCD), so the lowest unfinished
-//     workgroup is always resident and never waits: the chain always progresses. The spin is
-//     bounded anyway (an image whose look-back times out is re-encoded on the CPU), and
-//     NM03_JPEG_DBG=9 swaps in ordered tickets (atomic counter) for A/B runs;
+//     workgroups in ticket order (tickets are taken when a workgroup starts, so every workgroup
+//     waited on is already resident). The spin is bounded anyway (an image whose look-back
+//     times out is re-encoded on the CPU);
 //  4. each thread writes its block's codes at its bit offset (atomicOr into the zeroed stage).
 // The last workgroup of an image publishes the total (or the overflow marker).
 __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(4))) void jpeg_fused_kernel(const uint8_t* __restrict__ canvas,
@@ -148,33 +147,41 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(4))) vo
   if (tid < 16) dctab[tid] = tid < 12 ? kHuffDcLuma.e[tid] : 0u;
   const int bpi = (out_w >> 3) * (out_h >> 3);
   const int parts = (bpi + kJpegWG - 1) / kJpegWG;
-  const uint32_t nwg = (uint32_t)(parts * ncanvas);
-  if (tid == 0) {
-    uint32_t t = blockIdx.x;
-    if (dbg == 9) {  // ordered tickets instead of the dispatch index (A/B)
-      t = atomicAdd(w.ticket, 1u);
-      if (t == nwg - 1) atomicExch(w.ticket, 0u);  // every ticket of this launch is taken
-    }
-    s_ticket = t;
-  }
-  __syncthreads();
-  // Workgroup-uniform in SGPRs, so the descriptor loads below are scalar (constant cache).
-  const uint32_t ticket = __builtin_amdgcn_readfirstlane(s_ticket);
-  const int img = (int)(ticket / (uint32_t)parts), part = (int)(ticket % (uint32_t)parts);
-  if (dbg == 7) {  // profiling variant: tables + ticket only
-    if (ticket == 0xFFFFFFF1u) w.total[0] = 1u;
-    return;
-  }
+  // The image is fixed by the dispatch index; only the part comes from the ticket, so the
+  // descriptor loads below overlap the ticket's round trip.
+  const int img = (int)(blockIdx.x / (uint32_t)parts);
   const JpegDesc d = jd[img];
-  const int mcux = out_w >> 4;
-  const int b = part * kJpegWG + tid;
-  const bool valid = b < bpi;
   RenderDesc rd;
   RWindow win{0.f, 0.f};
   if (d.render >= 0) {
     rd = rs.rd[d.render];
     if (rd.kind != kRenderLabels) win = render_window(rd, rs.stats);
   }
+  if (tid == 0) {
+    // Ordered tickets per image: workgroup b encodes image b / parts and takes the next part of
+    // that image from the image's counter, so it only ever waits on parts whose workgroups have
+    // already started — progress is guaranteed even when other kernels (other streams, other
+    // processes on the same GPU) share the CUs or the queue is preempted. (Using the dispatch
+    // index as the part is ~5% faster, NM03_JPEG_DBG=9, but two encoders interleaving on the same
+    // XCDs can starve each other's predecessors: measured 2.3 s/step stalls with two ranks per
+    // GPU.) One counter per image keeps the serialised atomics per address at `parts`.
+    uint32_t p = blockIdx.x - (uint32_t)img * (uint32_t)parts;
+    if (dbg != 9) {
+      p = atomicAdd(&w.ticket[img], 1u);
+      if (p == (uint32_t)parts - 1) atomicExch(&w.ticket[img], 0u);  // the image's last ticket
+    }
+    s_ticket = p;
+  }
+  __syncthreads();
+  // The part is workgroup-uniform: keep it in an SGPR.
+  const int part = (int)__builtin_amdgcn_readfirstlane(s_ticket);
+  if (dbg == 7) {  // profiling variant: tables + ticket only
+    if (part == 0x7FFFFFF1) w.total[0] = 1u;
+    return;
+  }
+  const int mcux = out_w >> 4;
+  const int b = part * kJpegWG + tid;
+  const bool valid = b < bpi;
   // ---- 1. block → quantised zig-zag coefficients (kept in LDS; nz = non-zero AC mask) -------
   uint32_t* mycoef = scoef + tid * kCoefStride;
   uint64_t nz = 0;
@@ -298,7 +305,7 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(4))) vo
         const uint64_t st = look_load(&look[p]);
         const uint32_t hi = (uint32_t)(st >> 32);
         if (hi == 0u) {
-          if (++spins > (1u << 26)) {  // cannot happen with in-order dispatch; never hang the GPU
+          if (++spins > (1u << 26)) {  // cannot happen with ordered tickets; never hang the GPU
             prefix = 0xFFFFFFFFu;
             break;
           }

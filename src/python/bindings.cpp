@@ -680,7 +680,7 @@ PYBIND11_MODULE(_nm03, m) {
     const int max_chunks = (int)(stage_bytes / gpu::kStuffChunk);
     const size_t look_cap = (size_t)n * ((blocks + 255) / 256);
     const size_t o_jd = take(sizeof(gpu::JpegDesc) * n), o_stage = take((size_t)n * stage_bytes),
-                 o_look = take(look_cap * 8), o_ticket = take(8), o_zero_end = off,
+                 o_look = take(look_cap * 8), o_ticket = take(4 * (size_t)n), o_zero_end = off,
                  o_spill = take(look_cap * 256 * 56 * 4),
                  o_tot = take((size_t)n * 4), o_cff = take((size_t)n * max_chunks * 4),
                  o_out = take((size_t)n * out_cap), o_sz = take((size_t)n * 4);

@@ -225,7 +225,7 @@ struct Engine::Impl {
       s.jw.stage = dmalloc<uint32_t>((size_t)kStageBytes / 4 * s.cap_canvases, "hipMalloc stage");
       s.jw.look_cap = (size_t)s.cap_canvases * ((blocks + 255) / 256);
       s.jw.look = dmalloc<uint64_t>(s.jw.look_cap, "hipMalloc look-back");
-      s.jw.ticket = dmalloc<uint32_t>(1, "hipMalloc ticket");
+      s.jw.ticket = dmalloc<uint32_t>(s.cap_canvases, "hipMalloc tickets");
       s.jw.spill = dmalloc<uint32_t>(s.jw.look_cap * 256 * 56, "hipMalloc jpeg spill");
       s.jw.total = dmalloc<uint32_t>(s.cap_canvases, "hipMalloc total");
       s.jw.max_chunks = (int)(kStageBytes / kStuffChunk);
@@ -233,7 +233,7 @@ struct Engine::Impl {
       // The encoder ORs bits into the stage and polls look-back states: both start clear.
       check_hip(hipMemset(s.jw.stage, 0, (size_t)kStageBytes * s.cap_canvases), "memset stage");
       check_hip(hipMemset(s.jw.look, 0, s.jw.look_cap * sizeof(uint64_t)), "memset look-back");
-      check_hip(hipMemset(s.jw.ticket, 0, sizeof(uint32_t)), "memset ticket");
+      check_hip(hipMemset(s.jw.ticket, 0, sizeof(uint32_t) * s.cap_canvases), "memset tickets");
       check_hip(hipHostMalloc((void**)&s.h_out, (size_t)kOutCap * s.cap_canvases, hipHostMallocMapped),
                 "hipHostMalloc out");
       check_hip(hipHostGetDevicePointer((void**)&s.d_out, s.h_out, 0), "hipHostGetDevicePointer out");
