@@ -4,6 +4,7 @@
 #pragma once
 
 #include <cstdint>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -39,7 +40,21 @@ struct VolumeParams {
   std::vector<Seed> seeds;    // empty → reference seed pattern on the middle slice
 };
 
-// Runs the 3D pipeline on `device`; copies masks back when `want_masks`.
+// Runs the 3D pipeline on `device`; copies masks back when `want_masks`. A VolumeRunner keeps
+// its device buffers, stream and events between runs (rebuilt when the volume shape changes);
+// run_volume() is the one-shot form.
+class VolumeRunner {
+ public:
+  explicit VolumeRunner(int device);
+  ~VolumeRunner();
+  VolumeRunner(const VolumeRunner&) = delete;
+  VolumeRunner& operator=(const VolumeRunner&) = delete;
+  VolumeResult run(const VolumeInput& v, const VolumeParams& p, bool want_masks);
+
+ private:
+  struct Impl;
+  std::unique_ptr<Impl> impl_;
+};
 VolumeResult run_volume(const VolumeInput& v, const VolumeParams& p, int device, bool want_masks);
 
 namespace app {

@@ -139,12 +139,13 @@ int main(int argc, char** argv) {
       nm03::VolumeParams vp;
       vp.pipe = ec.pipe;
       vp.dilation_size = dil3d;
-      for (int w = 0; w < warmup; ++w) nm03::run_volume(v, vp, ec.device, false);
+      nm03::VolumeRunner runner(ec.device);
+      for (int w = 0; w < warmup; ++w) runner.run(v, vp, false);
       double ks = 0;
       int sweeps = 0;
       const double t0 = now_s();
       for (int k = 0; k < steps; ++k) {
-        auto r = nm03::run_volume(v, vp, ec.device, false);
+        auto r = runner.run(v, vp, false);
         ks += r.kernels_s;
         sweeps = r.sweeps;
       }

@@ -7,6 +7,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cstring>
+#include <memory>
 #include <iostream>
 
 #include "nm03/cohort.h"
@@ -88,7 +89,8 @@ struct VolumeDevice {
   hipStream_t stream = nullptr;
   DevBuf raw, med, band, region, dil, tmp, desc, medt, shpt, stats, seeds, flag;
   uint32_t* h_flag = nullptr;
-  std::vector<SliceDesc> hdesc;
+  uint8_t* h_tables = nullptr;  // pinned staging: descriptors, tile lists, stats (reused per run)
+  size_t n_medt, n_shpt;
   VolumeDevice(const VolumeInput& v)
       : w(v.w), h(v.h), d(v.d), wpr((v.w + 63) / 64), words((size_t)v.h * ((v.w + 63) / 64)),
         ps(((size_t)v.w * v.h + 7) / 8 * 8),
@@ -96,11 +98,18 @@ struct VolumeDevice {
         tmp(words * v.d * 8), desc(sizeof(SliceDesc) * v.d),
         medt(sizeof(TileDesc) * v.d * ((v.w + 63) / 64) * ((v.h + 63) / 64)),
         shpt(sizeof(TileDesc) * v.d * ((v.w + 63) / 64) * ((v.h + kShpTileH - 1) / kShpTileH)), stats(sizeof(SliceStats) * v.d),
-        seeds(sizeof(int32_t) * 3 * kMaxSeeds), flag(16) {
+        seeds(sizeof(int32_t) * 3 * kMaxSeeds), flag(16),
+        n_medt((size_t)v.d * ((v.w + 63) / 64) * ((v.h + 63) / 64)),
+        n_shpt((size_t)v.d * ((v.w + 63) / 64) * ((v.h + kShpTileH - 1) / kShpTileH)) {
     check_hip(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking), "stream");
     check_hip(hipHostMalloc((void**)&h_flag, 16, hipHostMallocDefault), "hipHostMalloc flag");
+    check_hip(hipHostMalloc((void**)&h_tables, table_bytes(), hipHostMallocDefault), "hipHostMalloc tables");
+  }
+  size_t table_bytes() const {
+    return sizeof(SliceDesc) * d + sizeof(TileDesc) * (n_medt + n_shpt) + sizeof(SliceStats) * d;
   }
   ~VolumeDevice() {
+    if (h_tables) (void)hipHostFree(h_tables);
     if (h_flag) (void)hipHostFree(h_flag);
     if (stream) (void)hipStreamDestroy(stream);
   }
@@ -109,10 +118,16 @@ struct VolumeDevice {
 }  // namespace
 
 static void volume_preprocess(VolumeDevice& V, const VolumeInput& v, const PipelineParams& p, const PipeConsts& pc) {
-  std::vector<TileDesc> mt, st;
-  V.hdesc.assign(v.d, SliceDesc{});
+  // Tables are written into pinned staging (valid until the next run, which starts after this
+  // run's final sync), so the uploads stay asynchronous.
+  auto* hdesc = reinterpret_cast<SliceDesc*>(V.h_tables);
+  auto* mt = reinterpret_cast<TileDesc*>(hdesc + v.d);
+  auto* st = mt + V.n_medt;
+  auto* stats = reinterpret_cast<SliceStats*>(st + V.n_shpt);
+  size_t nm = 0, ns = 0;
   for (int z = 0; z < v.d; ++z) {
-    SliceDesc& s = V.hdesc[z];
+    SliceDesc& s = hdesc[z];
+    std::memset(&s, 0, sizeof(s));
     s.raw_off = (uint32_t)(z * V.ps);
     s.mask_off = (uint32_t)(z * V.words);
     s.w = (uint16_t)v.w;
@@ -123,24 +138,28 @@ static void volume_preprocess(VolumeDevice& V, const VolumeInput& v, const Pipel
     s.slope = p.apply_rescale ? v.slope : 1.f;
     s.intercept = p.apply_rescale ? v.intercept : 0.f;
     for (int ty = 0; ty < (v.h + 63) / 64; ++ty)
-      for (int tx = 0; tx < (v.w + 63) / 64; ++tx) mt.push_back({(uint32_t)z, (uint16_t)tx, (uint16_t)ty});
+      for (int tx = 0; tx < (v.w + 63) / 64; ++tx) mt[nm++] = {(uint32_t)z, (uint16_t)tx, (uint16_t)ty};
     for (int ty = 0; ty < (v.h + kShpTileH - 1) / kShpTileH; ++ty)
-      for (int tx = 0; tx < V.wpr; ++tx) st.push_back({(uint32_t)z, (uint16_t)tx, (uint16_t)ty});
+      for (int tx = 0; tx < V.wpr; ++tx) st[ns++] = {(uint32_t)z, (uint16_t)tx, (uint16_t)ty};
+    stats[z] = SliceStats{0xFFFFFFFFu, 0u, 0xFFFFFFFFu, 0u};
   }
-  std::vector<SliceStats> stats(v.d, SliceStats{0xFFFFFFFFu, 0u, 0xFFFFFFFFu, 0u});
-  for (int z = 0; z < v.d; ++z)
-    check_hip(hipMemcpyAsync(V.raw.as<uint16_t>() + z * V.ps, v.raw.data() + (size_t)z * v.w * v.h,
-                             (size_t)v.w * v.h * 2, hipMemcpyHostToDevice, V.stream),
-              "H2D volume");
-  check_hip(hipMemcpyAsync(V.desc.p, V.hdesc.data(), sizeof(SliceDesc) * v.d, hipMemcpyHostToDevice, V.stream), "H2D");
-  check_hip(hipMemcpyAsync(V.medt.p, mt.data(), sizeof(TileDesc) * mt.size(), hipMemcpyHostToDevice, V.stream), "H2D");
-  check_hip(hipMemcpyAsync(V.shpt.p, st.data(), sizeof(TileDesc) * st.size(), hipMemcpyHostToDevice, V.stream), "H2D");
-  check_hip(hipMemcpyAsync(V.stats.p, stats.data(), sizeof(SliceStats) * v.d, hipMemcpyHostToDevice, V.stream), "H2D");
-  check_hip(hipStreamSynchronize(V.stream), "sync");  // host vectors go out of scope
-  launch_median(V.raw.as<uint16_t>(), V.med.as<uint16_t>(), V.desc.as<SliceDesc>(), V.medt.as<TileDesc>(),
-                (int)mt.size(), pc.median_k, V.stats.as<SliceStats>(), V.stream);
+  const size_t plane = (size_t)v.w * v.h;
+  if (V.ps == plane) {  // planes are contiguous on both sides: one copy
+    check_hip(hipMemcpyAsync(V.raw.p, v.raw.data(), plane * v.d * 2, hipMemcpyHostToDevice, V.stream), "H2D volume");
+  } else {
+    for (int z = 0; z < v.d; ++z)
+      check_hip(hipMemcpyAsync(V.raw.as<uint16_t>() + z * V.ps, v.raw.data() + z * plane, plane * 2,
+                               hipMemcpyHostToDevice, V.stream),
+                "H2D volume");
+  }
+  check_hip(hipMemcpyAsync(V.desc.p, hdesc, sizeof(SliceDesc) * v.d, hipMemcpyHostToDevice, V.stream), "H2D");
+  check_hip(hipMemcpyAsync(V.medt.p, mt, sizeof(TileDesc) * nm, hipMemcpyHostToDevice, V.stream), "H2D");
+  check_hip(hipMemcpyAsync(V.shpt.p, st, sizeof(TileDesc) * ns, hipMemcpyHostToDevice, V.stream), "H2D");
+  check_hip(hipMemcpyAsync(V.stats.p, stats, sizeof(SliceStats) * v.d, hipMemcpyHostToDevice, V.stream), "H2D");
+  launch_median(V.raw.as<uint16_t>(), V.med.as<uint16_t>(), V.desc.as<SliceDesc>(), V.medt.as<TileDesc>(), (int)nm,
+                pc.median_k, V.stats.as<SliceStats>(), V.stream);
   launch_sharpen_band(V.med.as<uint16_t>(), V.band.as<uint64_t>(), nullptr, V.desc.as<SliceDesc>(),
-                      V.shpt.as<TileDesc>(), (int)st.size(), pc, V.stats.as<SliceStats>(), V.stream);
+                      V.shpt.as<TileDesc>(), (int)ns, pc, V.stats.as<SliceStats>(), V.stream);
 }
 
 static void volume_segment(VolumeDevice& V, const VolumeInput& v, const VolumeParams& p, int* sweeps) {
@@ -172,34 +191,61 @@ static void unpack_volume(const DevBuf& b, const VolumeDevice& V, std::vector<ui
         out[((size_t)z * V.h + y) * V.w + x] = (words[(size_t)z * V.words + (size_t)y * V.wpr + x / 64] >> (x % 64)) & 1;
 }
 
-VolumeResult run_volume(const VolumeInput& v, const VolumeParams& p, int device, bool want_masks) {
+// Device buffers, stream and events are cached across runs (allocation and stream creation cost
+// more than the kernels for a 256³ volume); they are rebuilt only when the volume shape changes.
+struct VolumeRunner::Impl {
+  int device;
+  std::unique_ptr<VolumeDevice> V;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  explicit Impl(int dev) : device(dev) {
+    check_hip(hipSetDevice(device), "hipSetDevice");
+    check_hip(hipEventCreate(&e0), "event");
+    check_hip(hipEventCreate(&e1), "event");
+  }
+  ~Impl() {
+    (void)hipSetDevice(device);
+    V.reset();
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+  }
+};
+
+VolumeRunner::VolumeRunner(int device) : impl_(std::make_unique<Impl>(device)) {}
+VolumeRunner::~VolumeRunner() = default;
+
+VolumeResult VolumeRunner::run(const VolumeInput& v, const VolumeParams& p, bool want_masks) {
   if (v.d < 1 || v.w < 1 || v.h < 1) throw SliceError("empty volume");
-  check_hip(hipSetDevice(device), "hipSetDevice");
-  VolumeDevice V(v);
+  Impl& I = *impl_;
+  check_hip(hipSetDevice(I.device), "hipSetDevice");
+  if (!I.V || I.V->w != v.w || I.V->h != v.h || I.V->d != v.d) {
+    I.V.reset();
+    I.V = std::make_unique<VolumeDevice>(v);
+  }
+  VolumeDevice& V = *I.V;
   const PipeConsts pc = make_consts(p.pipe, 2);
-  hipEvent_t e0, e1;
-  check_hip(hipEventCreate(&e0), "event");
-  check_hip(hipEventCreate(&e1), "event");
-  check_hip(hipEventRecord(e0, V.stream), "event");
+  check_hip(hipEventRecord(I.e0, V.stream), "event");
   VolumeResult r;
   r.w = v.w;
   r.h = v.h;
   r.d = v.d;
   volume_preprocess(V, v, p.pipe, pc);
   volume_segment(V, v, p, &r.sweeps);
-  check_hip(hipEventRecord(e1, V.stream), "event");
-  check_hip(hipEventSynchronize(e1), "sync");
+  check_hip(hipEventRecord(I.e1, V.stream), "event");
+  check_hip(hipEventSynchronize(I.e1), "sync");
   float ms = 0;
-  (void)hipEventElapsedTime(&ms, e0, e1);
+  (void)hipEventElapsedTime(&ms, I.e0, I.e1);
   r.kernels_s = ms * 1e-3;
-  (void)hipEventDestroy(e0);
-  (void)hipEventDestroy(e1);
   if (want_masks) {
     unpack_volume(V.band, V, r.band);
     unpack_volume(V.region, V, r.region);
     unpack_volume(V.dil, V, r.dilated);
   }
   return r;
+}
+
+VolumeResult run_volume(const VolumeInput& v, const VolumeParams& p, int device, bool want_masks) {
+  VolumeRunner runner(device);
+  return runner.run(v, p, want_masks);
 }
 
 namespace app {
@@ -218,6 +264,7 @@ int run_volume_cohort(const AppConfig& cfg) {
   const RenderParams& rp = cfg.engine.render;
   jpeg::Tables t = jpeg::make_tables(rp.jpeg_quality);
   int successful = 0;
+  VolumeRunner runner(cfg.engine.device);
   for (const auto& pid : pids) {
     try {
       std::cout << "\n=== Processing Patient: " << pid << " as a 3D volume ===\n" << std::endl;
@@ -232,7 +279,7 @@ int run_volume_cohort(const AppConfig& cfg) {
       vp.pipe = cfg.engine.pipe;
       vp.connectivity = cfg.engine.pipe.srg_connectivity == 26 ? 26 : 6;
       vp.dilation_size = cfg.engine.pipe.dilation_size;
-      VolumeResult r = run_volume(v, vp, cfg.engine.device, true);
+      VolumeResult r = runner.run(v, vp, true);
       // Export per slice (golden renderer + encoder on the host; the 3D path is not the headline).
       PipelineParams pp = cfg.engine.pipe;
       for (int z = 0; z < v.d; ++z) {
