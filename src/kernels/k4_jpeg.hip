@@ -69,11 +69,7 @@ __device__ __forceinline__ uint32_t sat_add(uint32_t a, uint32_t b) {
 }
 
 constexpr int kJpegWG = 256;     // luma blocks (threads) per workgroup = 64 MCUs
-constexpr int kCoefStride = 32;  // u32 words per thread in LDS: 32 zig-zag pairs, XOR-swizzled
-// Pair p of thread t lives at word t*32 + (p ^ (t & 31)): the unrolled stores (same p in every
-// lane) spread over the banks without the padding word, keeping the workgroup at 34 KiB of LDS
-// (4 workgroups per CU).
-__device__ __forceinline__ int coef_slot(int p, int t) { return p ^ (t & 31); }
+constexpr int kAsmWords = 2048;  // LDS assembly buffer for the workgroup's bit range (64 Kbit)
 
 constexpr int kPrivWords = 5;    // per-block Huffman bits kept in LDS (160 bits, odd stride) ...
 constexpr int kSpillWords = 56;  // ... the rest in the block's global spill slot (a block needs ≤ 1700)
@@ -128,11 +124,10 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(4))) vo
                                                              int out_h, QuantRecip q, JpegWork w, JpegRenderSrc rs,
                                                              int32_t* __restrict__ out_sizes, int dbg) {
   __shared__ uint32_t actab[256];
-  __shared__ uint8_t aclen[256];
   __shared__ uint32_t dctab[16];
   __shared__ int32_t sdc[kJpegWG];
-  __shared__ uint32_t scoef[kJpegWG * kCoefStride];  // per-thread zig-zag pairs; later the WG bit range
-  __shared__ uint32_t spriv[kJpegWG * kPrivWords];   // per-block Huffman bits
+  __shared__ uint32_t spriv[kJpegWG * kPrivWords];  // per-block AC Huffman bits
+  __shared__ uint32_t swg[kAsmWords + 2];           // the workgroup's bit range
   __shared__ uint32_t sh[17];
   __shared__ uint32_t s_ticket, s_prefix;
   __shared__ int32_t s_prevdc;
@@ -141,9 +136,7 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(4))) vo
     if (tid == 999) w.total[0] = 1u;
     return;
   }
-  const uint32_t e = kHuffAcLuma.e[tid];
-  actab[tid] = e;
-  aclen[tid] = (uint8_t)hlen(e);
+  actab[tid] = kHuffAcLuma.e[tid];
   if (tid < 16) dctab[tid] = tid < 12 ? kHuffDcLuma.e[tid] : 0u;
   const int bpi = (out_w >> 3) * (out_h >> 3);
   const int parts = (bpi + kJpegWG - 1) / kJpegWG;
@@ -182,10 +175,15 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(4))) vo
   const int mcux = out_w >> 4;
   const int b = part * kJpegWG + tid;
   const bool valid = b < bpi;
-  // ---- 1. block → quantised zig-zag coefficients (kept in LDS; nz = non-zero AC mask) -------
-  uint32_t* mycoef = scoef + tid * kCoefStride;
-  uint64_t nz = 0;
+  // ---- 1+2. block → DCT → quantisation fused with the AC Huffman coding ------------------------
+  // The coefficients never leave registers: the zig-zag walk is unrolled, each coefficient is
+  // quantised and — if non-zero in some lane of the wave (else the position is skipped) — coded
+  // straight into the block's private bit buffer. The DC code depends on the previous block's DC,
+  // so the AC stream is coded first and the DC code is prepended at assembly time.
+  uint32_t* const pbuf = spriv + tid * kPrivWords;
+  uint32_t* const pspill = w.spill + ((size_t)blockIdx.x * kJpegWG + tid) * kSpillWords;
   int dc0 = 0;
+  uint32_t acbits = 0;
   if (valid) {
     const int mcu = b >> 2, sub = b & 3;
     const int bx = 2 * (mcu % mcux) + (sub & 1), by = 2 * (mcu / mcux) + (sub >> 1);
@@ -217,17 +215,55 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(4))) vo
       return;
     }
     fdct_islow(blk);
+    // Quantise into packed int16 pairs first (frees the 64 int32 DCT registers), then walk the
+    // zig-zag order from those registers.
+    uint32_t zp[32];
 #pragma unroll
     for (int k = 0; k < 64; k += 2) {
       const int16_t a = quant_recip(blk[kNatural[k]], q, kNatural[k]);
       const int16_t c = quant_recip(blk[kNatural[k + 1]], q, kNatural[k + 1]);
-      if (k == 0) dc0 = a;
-      nz |= (k > 0 && a != 0 ? 1ull << k : 0ull) | (c != 0 ? 1ull << (k + 1) : 0ull);
-      mycoef[coef_slot(k >> 1, tid)] = (uint32_t)(uint16_t)a | ((uint32_t)(uint16_t)c << 16);
+      zp[k >> 1] = (uint32_t)(uint16_t)a | ((uint32_t)(uint16_t)c << 16);
     }
+    dc0 = (int16_t)(zp[0] & 0xFFFFu);
+    LBitWriter lw(pbuf, pspill);
+    int last = 0;
+    // Outer loop not unrolled: zp[j] is indexed by a wave-uniform counter (register indexing, no
+    // scratch), keeping the code compact.
+#pragma unroll 1
+    for (int j = 0; j < 32; ++j) {
+      const uint32_t word = zp[j];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int k = 2 * j + h;
+        const int v = (int16_t)(word >> (16 * h));
+        if (k > 0 && __ballot(v != 0)) {
+          if (v != 0) {
+            int run = k - last - 1;
+            while (run > 15) {
+              lw.put_sym(actab[0xF0]);
+              run -= 16;
+            }
+            const int nb = mag_bits_fast(v);
+            const uint32_t e = actab[(run << 4) + nb];  // symbol and magnitude in one put (≤ 27 bits)
+            const uint32_t mag = (uint32_t)(v < 0 ? v - 1 : v) & ((1u << nb) - 1u);
+            lw.put(((e & 0xFFFFu) << nb) | mag, (int)(e >> 16) + nb);
+            last = k;
+          }
+        }
+      }
+    }
+    if (last < 63) lw.put_sym(actab[0x00]);
+    if ((b & 3) == 3) {  // the MCU's Cb and Cr blocks of a gray image: DC diff 0 + EOB each
+      lw.put_sym(kHuffDcChroma.e[0]);
+      lw.put_sym(kHuffAcChroma.e[0]);
+      lw.put_sym(kHuffDcChroma.e[0]);
+      lw.put_sym(kHuffAcChroma.e[0]);
+    }
+    lw.finish();
+    acbits = lw.bits;
   }
-  if (dbg == 2) {  // profiling variant: stop after FDCT + quantisation
-    if (dc0 == 0x7FFFFFF1 || nz == 0x123456789ull) w.total[0] = 1u;
+  if (dbg == 2) {  // profiling variant: stop after FDCT + quantisation + AC coding
+    if (dc0 == 0x7FFFFFF1 || acbits == 0x7FFFFFF1u) w.total[0] = 1u;
     return;
   }
   sdc[tid] = dc0;
@@ -246,49 +282,13 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(4))) vo
     if (tid == 0) s_prevdc = dcp;
   }
   __syncthreads();
-  // ---- 2. Huffman coding of the block into its private bit buffer (bits = its cost) ----------
+  // DC code (Huffman symbol + magnitude bits, ≤ 20 bits, right-aligned).
   const int diff = dc0 - (tid ? sdc[tid - 1] : s_prevdc);
   const int dn = mag_bits_fast(diff);
-  uint32_t* const pbuf = spriv + tid * kPrivWords;
-  uint32_t* const pspill = w.spill + ((size_t)blockIdx.x * kJpegWG + tid) * kSpillWords;
-  uint32_t bits = 0;
-  if (valid) {
-    LBitWriter lw(pbuf, pspill);
-    {
-      const uint32_t e = dctab[dn];
-      const uint32_t mag = (uint32_t)(diff < 0 ? diff - 1 : diff) & ((1u << dn) - 1u);
-      lw.put(((e & 0xFFFFu) << dn) | mag, (int)(e >> 16) + dn);
-    }
-    int last = 0;
-    for (uint64_t m = nz; m; m &= m - 1) {
-      const int k = __builtin_ctzll(m);
-      const int v = (int16_t)(mycoef[coef_slot(k >> 1, tid)] >> (16 * (k & 1)));
-      int run = k - last - 1;
-      while (run > 15) {
-        lw.put_sym(actab[0xF0]);
-        run -= 16;
-      }
-      const int nb = mag_bits_fast(v);
-      // symbol and magnitude bits in one put: ≤ 16 + 11 bits
-      const uint32_t e = actab[(run << 4) + nb];
-      const uint32_t mag = (uint32_t)(v < 0 ? v - 1 : v) & ((1u << nb) - 1u);
-      lw.put(((e & 0xFFFFu) << nb) | mag, (int)(e >> 16) + nb);
-      last = k;
-    }
-    if (last < 63) lw.put_sym(actab[0x00]);
-    if ((b & 3) == 3) {  // the MCU's Cb and Cr blocks of a gray image: DC diff 0 + EOB each
-      lw.put_sym(kHuffDcChroma.e[0]);
-      lw.put_sym(kHuffAcChroma.e[0]);
-      lw.put_sym(kHuffDcChroma.e[0]);
-      lw.put_sym(kHuffAcChroma.e[0]);
-    }
-    lw.finish();
-    bits = lw.bits;
-  }
-  if (dbg == 3) {  // profiling variant: stop after Huffman coding
-    if (bits == 0x7FFFFFF1u) w.total[0] = 1u;
-    return;
-  }
+  const uint32_t dce = dctab[dn];
+  const int dclen = valid ? (int)(dce >> 16) + dn : 0;
+  const uint32_t dccode = ((dce & 0xFFFFu) << dn) | ((uint32_t)(diff < 0 ? diff - 1 : diff) & ((1u << dn) - 1u));
+  const uint32_t bits = valid ? (uint32_t)dclen + acbits : 0u;
   // ---- 3. workgroup scan + look-back --------------------------------------------------------
   uint32_t agg = 0;
   const uint32_t excl = block_exclusive_scan(bits, sh, &agg);  // ends with a barrier
@@ -320,18 +320,25 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(4))) vo
     }
     s_prefix = prefix;
   }
-  // Meanwhile: assemble the workgroup's contiguous bit range in LDS (the coefficient area is free).
-  uint32_t* swg = scoef;
+  // Meanwhile: assemble the workgroup's contiguous bit range in LDS: each block's DC code, then
+  // its AC words shifted behind it.
   const uint32_t nlocal = (agg + 31) >> 5;
-  const bool in_lds = nlocal < (uint32_t)(kJpegWG * kCoefStride);  // workgroup-uniform
-  const uint32_t nwp = (bits + 31) >> 5;
+  const bool in_lds = nlocal < (uint32_t)kAsmWords;  // workgroup-uniform
+  const uint32_t nwp = (acbits + 31) >> 5;
+  const uint32_t acpos = excl + (uint32_t)dclen;
   if (in_lds) {
     for (uint32_t i = tid; i <= nlocal; i += kJpegWG) swg[i] = 0u;
     __syncthreads();
-    for (uint32_t i = 0; i < nwp; ++i) {
-      const uint32_t v = priv_word(pbuf, pspill, i), dst = excl + 32u * i, wi = dst >> 5, shf = dst & 31u;
-      atomicOr(&swg[wi], v >> shf);
-      if (shf) atomicOr(&swg[wi + 1], v << (32u - shf));
+    if (valid) {
+      const uint32_t dv = dclen ? dccode << (32 - dclen) : 0u, sh0 = excl & 31u, w0 = excl >> 5;
+      atomicOr(&swg[w0], dv >> sh0);
+      if (sh0) atomicOr(&swg[w0 + 1], dv << (32u - sh0));
+      const uint32_t shf = acpos & 31u, wa = acpos >> 5;
+      for (uint32_t i = 0; i < nwp; ++i) {
+        const uint32_t v = priv_word(pbuf, pspill, i);
+        atomicOr(&swg[wa + i], v >> shf);
+        if (shf) atomicOr(&swg[wa + i + 1], v << (32u - shf));
+      }
     }
   }
   __syncthreads();
@@ -343,21 +350,25 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(4))) vo
   //         neighbouring workgroups, are atomic) --------------------------------------------------
   if (end <= cap_bits && agg) {
     if (in_lds) {
-      const uint32_t s = prefix & 31u, base = prefix >> 5;
+      const uint32_t sft = prefix & 31u, base = prefix >> 5;
       const uint32_t nw = ((prefix + agg + 31u) >> 5) - base;
       for (uint32_t j = tid; j < nw; j += kJpegWG) {
-        uint32_t v = j < nlocal ? swg[j] >> s : 0u;
-        if (s && j > 0) v |= swg[j - 1] << (32u - s);
+        uint32_t v = j < nlocal ? swg[j] >> sft : 0u;
+        if (sft && j > 0) v |= swg[j - 1] << (32u - sft);
         if (j == 0 || j == nw - 1)
           atomicOr(&stage[base + j], v);
         else
           stage[base + j] = v;
       }
-    } else {
-      // Extremely detailed workgroup (> 256 Kbit): each block ORs its words into the stage.
+    } else if (valid) {
+      // Very detailed workgroup (> 64 Kbit): each block ORs its bits straight into the stage.
+      const uint32_t p0 = prefix + excl;
+      const uint32_t dv = dclen ? dccode << (32 - dclen) : 0u;
+      atomicOr(&stage[p0 >> 5], dv >> (p0 & 31u));
+      if (p0 & 31u) atomicOr(&stage[(p0 >> 5) + 1], dv << (32u - (p0 & 31u)));
+      const uint32_t pa = prefix + acpos;
       for (uint32_t i = 0; i < nwp; ++i) {
-        const uint32_t v = priv_word(pbuf, pspill, i), dst = prefix + excl + 32u * i, wi = dst >> 5,
-                       shf = dst & 31u;
+        const uint32_t v = priv_word(pbuf, pspill, i), dst = pa + 32u * i, wi = dst >> 5, shf = dst & 31u;
         atomicOr(&stage[wi], v >> shf);
         if (shf) atomicOr(&stage[wi + 1], v << (32u - shf));
       }
