@@ -11,6 +11,7 @@ class VolumePipeline:
         self.config = config or PipelineConfig()
         self.connectivity = connectivity
         self.dilation = dilation
+        self._runners = {}  # device -> native VolumeRunner (buffers/stream reused across volumes)
 
     def default_seeds(self, volume):
         d, h, w = volume.shape
@@ -19,8 +20,11 @@ class VolumePipeline:
     def run(self, volume, seeds=None, device=None):
         vol = np.ascontiguousarray(volume, dtype=np.uint16)
         s = list(seeds) if seeds is not None else self.default_seeds(vol)
-        return native().run_volume(vol, self.config.pipeline_params(), self.connectivity, self.dilation, s,
-                                   self.config.device if device is None else device)
+        dev = self.config.device if device is None else device
+        runner = self._runners.get(dev)
+        if runner is None:
+            runner = self._runners[dev] = native().VolumeRunner(dev)
+        return runner.run(vol, self.config.pipeline_params(), self.connectivity, self.dilation, s)
 
     def golden(self, band, seeds):
         n = native()

@@ -324,6 +324,20 @@ def test_volume_vs_golden(native, conn):
     assert res["sweeps"] >= 1
 
 
+def test_volume_runner_reuse_across_shapes(native):
+    """One persistent VolumePipeline runner over volumes of changing shape and content: every
+    result equals the golden of that volume (no stale buffers/tables from the previous run)."""
+    vp = nm.VolumePipeline(connectivity=6, dilation=3)
+    for (d, h, w, seed) in ((8, 64, 64, 1), (12, 80, 96, 2), (8, 64, 64, 3), (8, 64, 64, 3)):
+        vol = np.stack([native.phantom_slice(h, w, 2, z, d, seed) for z in range(d)])
+        seeds = vp.default_seeds(vol)
+        res = vp.run(vol, seeds)
+        region, dil = vp.golden(res["band"], seeds)
+        assert np.array_equal(res["region"], region), (d, h, w, seed)
+        assert np.array_equal(res["dilated"], dil), (d, h, w, seed)
+    assert len(vp._runners) == 1
+
+
 # ---------------------------------------------------------------------------------------------
 # Fault injection / resume / log levels (SURVEY §5.3-§5.5)
 # ---------------------------------------------------------------------------------------------
