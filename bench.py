@@ -28,7 +28,8 @@ import torch  # noqa: E402  (must precede the native extension: shared HIP runti
 
 import nm03_capstone_project_amd as nm  # noqa: E402
 from nm03_capstone_project_amd.parallel import (allreduce_max, allreduce_sum, auto_threads,  # noqa: E402
-                                                barrier, broadcast_bytes, init_from_env, plan_cohort)
+                                                barrier, broadcast_bytes, cgroup_cpu_stat, init_from_env,
+                                                plan_cohort)
 from nm03_capstone_project_amd.parallel.cohort_runner import CohortPlan  # noqa: E402
 from nm03_capstone_project_amd.parallel.dist import shard_bounds  # noqa: E402
 
@@ -125,7 +126,8 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     ok = 0
-    stage = {"load_s": 0.0, "h2d_s": 0.0, "kernels_s": 0.0, "write_s": 0.0}
+    stage = {"load_s": 0.0, "load_cpu_s": 0.0, "h2d_s": 0.0, "kernels_s": 0.0, "write_s": 0.0, "write_cpu_s": 0.0}
+    cg0 = cgroup_cpu_stat()
     for _ in range(args.steps):
         with _roctx_range("bench.step"):
             codes, msgs, times = engine.run_list(work)
@@ -135,6 +137,7 @@ def main():
     torch.cuda.synchronize()
     barrier(ctx)
     dt = time.perf_counter() - t0
+    cg1 = cgroup_cpu_stat()
     dt = allreduce_max(dt, ctx)
     total_ok = int(allreduce_sum(ok, ctx))
     value = total_ok / dt
@@ -162,6 +165,9 @@ def main():
                 "streams": args.streams,
                 "threads": args.threads,
                 "rank0_stage_s": {k: round(v, 4) for k, v in stage.items()},
+                # host CPU of the whole cgroup over the timed region (all ranks of this container)
+                "cgroup_cpu_ms_per_step": {k[:-5]: round((cg1[k] - cg0.get(k, 0)) / 1e3 / args.steps, 3)
+                                           for k in ("usage_usec", "throttled_usec") if k in cg1},
                 "storage": {"data": args.data_root, "out": args.out_root},
             },
         }

@@ -53,9 +53,17 @@ size_t read_file_into(const std::string& path, std::vector<uint8_t>& buf);
 // A slice file opened for loading: the header is parsed from a 16 KiB prefix and, for
 // little-endian 16-bit data, the pixels are read with one pread straight into the destination
 // (the engine's pinned upload blob) — no intermediate whole-file buffer and no extra copy.
+// How SliceFile moves a slice from the page cache into the caller's (pinned) buffer:
+//   kDirect — parse a `prefix`-byte header read, then pread the pixels straight into dst (pixel
+//             bytes already in the prefix are copied from it);
+//   kStaged — one pread of the whole file into the caller's scratch buffer (cache-resident), then
+//             non-temporal stores into dst: no read-for-ownership of the destination lines, which
+//             the copy engine reads next anyway.
+enum class ReadMode { kDirect, kStaged };
+
 class SliceFile {
  public:
-  explicit SliceFile(const std::string& path);
+  explicit SliceFile(const std::string& path, ReadMode mode = ReadMode::kDirect, size_t prefix = 16384);
   ~SliceFile();
   SliceFile(const SliceFile&) = delete;
   SliceFile& operator=(const SliceFile&) = delete;
@@ -72,10 +80,16 @@ class SliceFile {
   std::string path_;
   int fd_ = -1;
   size_t size_ = 0;
+  ReadMode mode_ = ReadMode::kDirect;
+  size_t prefix_ = 16384;
+  size_t have_ = 0;  // bytes of the file at the start of *buf_
   Header h_;
   bool whole_ = true;
   std::vector<uint8_t>* buf_ = nullptr;
 };
+
+// memcpy with non-temporal (streaming) stores for the 16-byte-aligned body of dst.
+void stream_copy(void* dst, const void* src, size_t n);
 
 struct WriteSpec {
   int rows = 256, cols = 256;

@@ -42,10 +42,12 @@ struct SliceStatus {
 };
 
 struct StageTimes {
-  double load_s = 0;     // summed over loader tasks (CPU seconds)
-  double h2d_s = 0;      // device time of uploads
-  double kernels_s = 0;  // device time K1..K4
-  double write_s = 0;    // summed over writer tasks (CPU seconds)
+  double load_s = 0;       // wall time summed over loader tasks
+  double h2d_s = 0;        // device time of uploads
+  double kernels_s = 0;    // device time K1..K4
+  double write_s = 0;      // wall time summed over writer tasks
+  double load_cpu_s = 0;   // thread CPU time of the loader tasks
+  double write_cpu_s = 0;  // thread CPU time of the writer tasks
   double wall_s = 0;     // run() wall time
   int64_t batches = 0, slices_ok = 0, slices_failed = 0;
   int64_t bytes_in = 0, bytes_out = 0;

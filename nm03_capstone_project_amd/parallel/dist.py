@@ -72,6 +72,19 @@ def cpu_budget():
     return n
 
 
+def cgroup_cpu_stat():
+    """cgroup v2 cpu.stat counters (usage_usec, throttled_usec, nr_throttled, ...); {} when unavailable.
+    Deltas over a timed region show whether the host side ran into the CPU quota."""
+    out = {}
+    try:
+        for line in open("/sys/fs/cgroup/cpu.stat"):
+            k, v = line.split()[:2]
+            out[k] = int(v)
+    except (OSError, ValueError):
+        pass
+    return out
+
+
 def auto_threads(local_world=None, cap=16):
     """Host I/O threads per rank: the CPU budget shared by the node's ranks (LOCAL_WORLD_SIZE),
     at most `cap` (16 = the reference's omp_set_num_threads(16), main_parallel.cpp:401). Running

@@ -5,6 +5,7 @@
 #include "nm03/dicom.h"
 
 #include <fcntl.h>
+#include <immintrin.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
@@ -331,7 +332,8 @@ size_t read_file_into(const std::string& path, std::vector<uint8_t>& buf) {
 // ------------------------------------------------------------------------------------------------
 // SliceFile: header from a 16 KiB prefix, pixels read straight into the caller's buffer.
 // ------------------------------------------------------------------------------------------------
-SliceFile::SliceFile(const std::string& path) : path_(path) {
+SliceFile::SliceFile(const std::string& path, ReadMode mode, size_t prefix)
+    : path_(path), mode_(mode), prefix_(prefix < 1024 ? 1024 : prefix) {
   fd_ = ::open(path.c_str(), O_RDONLY | O_CLOEXEC);
   if (fd_ < 0) throw SliceError("Cannot open file: " + path + " (" + std::strerror(errno) + ")");
   struct stat st;
@@ -358,11 +360,11 @@ void SliceFile::pread_all(void* dst, size_t n, size_t off) {
 }
 
 const Header& SliceFile::header(std::vector<uint8_t>& buf) {
-  constexpr size_t kPrefix = 16384;
-  const size_t pre = std::min(size_, kPrefix);
+  const size_t pre = mode_ == ReadMode::kStaged ? size_ : std::min(size_, prefix_);
   if (buf.size() < pre) buf.resize(pre);
   pread_all(buf.data(), pre, 0);
   buf_ = &buf;
+  have_ = pre;
   if (pre < size_) {
     try {
       h_ = parse_prefix(buf.data(), pre, size_);
@@ -375,6 +377,7 @@ const Header& SliceFile::header(std::vector<uint8_t>& buf) {
   }
   if (buf.size() < size_) buf.resize(size_);
   if (pre < size_) pread_all(buf.data() + pre, size_ - pre, pre);
+  have_ = size_;
   h_ = parse(buf.data(), size_);
   whole_ = true;
   return h_;
@@ -382,10 +385,44 @@ const Header& SliceFile::header(std::vector<uint8_t>& buf) {
 
 void SliceFile::pixels16(uint16_t* dst) {
   if (whole_) {
-    copy_pixels16(h_, buf_->data(), size_, dst);
-  } else {
-    pread_all(dst, (size_t)h_.rows * h_.cols * 2, h_.pixel_offset);
+    const bool raw16 = h_.bits_allocated == 16 && h_.syntax != Syntax::kExplicitBE;
+    const size_t n = (size_t)h_.rows * h_.cols * 2;
+    if (raw16 && mode_ == ReadMode::kStaged) {
+      if (h_.pixel_offset + n > size_) throw SliceError("Truncated pixel data");
+      stream_copy(dst, buf_->data() + h_.pixel_offset, n);
+    } else {
+      copy_pixels16(h_, buf_->data(), size_, dst);
+    }
+    return;
   }
+  // Pixel bytes that came with the header read are taken from it; the rest is read into dst.
+  const size_t n = (size_t)h_.rows * h_.cols * 2;
+  size_t k = h_.pixel_offset < have_ ? std::min(n, have_ - h_.pixel_offset) : 0;
+  if (k) std::memcpy(dst, buf_->data() + h_.pixel_offset, k);
+  if (k < n) pread_all(reinterpret_cast<uint8_t*>(dst) + k, n - k, h_.pixel_offset + k);
+}
+
+void stream_copy(void* dst, const void* src, size_t n) {
+  auto* d = static_cast<uint8_t*>(dst);
+  const auto* s = static_cast<const uint8_t*>(src);
+  size_t head = (16 - ((uintptr_t)d & 15)) & 15;
+  if (head > n) head = n;
+  std::memcpy(d, s, head);
+  d += head;
+  s += head;
+  n -= head;
+  for (; n >= 64; n -= 64, d += 64, s += 64) {
+    const __m128i a = _mm_loadu_si128(reinterpret_cast<const __m128i*>(s));
+    const __m128i b = _mm_loadu_si128(reinterpret_cast<const __m128i*>(s + 16));
+    const __m128i c = _mm_loadu_si128(reinterpret_cast<const __m128i*>(s + 32));
+    const __m128i e = _mm_loadu_si128(reinterpret_cast<const __m128i*>(s + 48));
+    _mm_stream_si128(reinterpret_cast<__m128i*>(d), a);
+    _mm_stream_si128(reinterpret_cast<__m128i*>(d + 16), b);
+    _mm_stream_si128(reinterpret_cast<__m128i*>(d + 32), c);
+    _mm_stream_si128(reinterpret_cast<__m128i*>(d + 48), e);
+  }
+  std::memcpy(d, s, n);
+  _mm_sfence();  // streaming stores are weakly ordered: complete them before the upload is queued
 }
 
 std::vector<uint8_t> read_file(const std::string& path) {

@@ -357,14 +357,20 @@ PYBIND11_MODULE(_nm03, m) {
     return py::make_tuple(a, py::make_tuple(im.spacing[0], im.spacing[1], im.spacing[2]));
   });
   m.def("numa_node_cpus", &numa::node_cpus);
-  m.def("read_pixels_direct", [](const std::string& path) {
-    dicom::SliceFile f(path);
-    std::vector<uint8_t> scratch;
-    const dicom::Header& h = f.header(scratch);
-    std::vector<uint16_t> px((size_t)h.rows * h.cols);
-    f.pixels16(px.data());
-    return py::make_tuple(to_np<uint16_t>(px, {h.rows, h.cols}), f.direct());
-  });
+  m.def("numa_device_node", &numa::device_node, py::arg("device"));
+  m.def(
+      "read_pixels_direct",
+      [](const std::string& path, const std::string& mode, size_t prefix) {
+        dicom::SliceFile f(path, mode == "staged" ? dicom::ReadMode::kStaged : dicom::ReadMode::kDirect, prefix);
+        std::vector<uint8_t> scratch;
+        const dicom::Header& h = f.header(scratch);
+        std::vector<uint16_t> px((size_t)h.rows * h.cols + 1);  // +1: misaligned destination below
+        uint16_t* dst = px.data() + 1;
+        f.pixels16(dst);
+        std::vector<uint16_t> out(dst, dst + (size_t)h.rows * h.cols);
+        return py::make_tuple(to_np<uint16_t>(out, {h.rows, h.cols}), f.direct());
+      },
+      py::arg("path"), py::arg("mode") = "direct", py::arg("prefix") = 16384);
   m.def(
       "read_slice",
       [](const std::string& path, int min_dim) {
@@ -544,6 +550,8 @@ PYBIND11_MODULE(_nm03, m) {
     td["h2d_s"] = t.h2d_s;
     td["kernels_s"] = t.kernels_s;
     td["write_s"] = t.write_s;
+    td["load_cpu_s"] = t.load_cpu_s;
+    td["write_cpu_s"] = t.write_cpu_s;
     td["wall_s"] = t.wall_s;
     td["batches"] = t.batches;
     td["slices_ok"] = t.slices_ok;

@@ -5,6 +5,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <ctime>
 #include <atomic>
 #include <array>
 #include <chrono>
@@ -32,6 +33,14 @@ namespace {
 
 constexpr size_t kAlign = 256;
 inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+// CPU time of the calling thread (ns): loader/writer tasks report it next to their wall time, so a
+// CPU-quota stall or preemption (wall ≫ cpu) can be told apart from work (wall ≈ cpu).
+inline int64_t thread_cpu_ns() {
+  timespec ts;
+  clock_gettime(CLOCK_THREAD_CPUTIME_ID, &ts);
+  return (int64_t)ts.tv_sec * 1000000000 + ts.tv_nsec;
+}
+
 inline double now_s() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
@@ -118,9 +127,18 @@ struct Engine::Impl {
   std::vector<uint8_t> jpeg_header;
   int32_t divs[64];
   PipeConsts pc{};
+  // Loader read path (dicom::ReadMode); NM03_LOAD_MODE=direct|staged, NM03_LOAD_PREFIX=<bytes>.
+  // Staged is the default: 231k/232k/224k vs 221k/205k/223k slices/s for direct (interleaved,
+  // tools/gpu_load_ab.sh); a 4 KiB direct prefix misaligns the pixel pread's destination and is
+  // slower still (198k/187k/200k).
+  dicom::ReadMode read_mode_ = dicom::ReadMode::kStaged;
+  size_t read_prefix_ = 16384;
 
   explicit Impl(const EngineConfig& c) : cfg(c), place(c.device) {
     if (const char* e = std::getenv("NM03_BATCH_TAPER"); e && *e) cfg.taper = *e != '0';
+    if (const char* e = std::getenv("NM03_LOAD_MODE"); e && *e)
+      read_mode_ = std::string(e) == "staged" ? dicom::ReadMode::kStaged : dicom::ReadMode::kDirect;
+    if (const char* e = std::getenv("NM03_LOAD_PREFIX"); e && *e) read_prefix_ = (size_t)std::atol(e);
     if (cfg.batch_size < 1) cfg.batch_size = 1;
     if (cfg.streams < 1) cfg.streams = 1;
     if (cfg.max_dim < 16) cfg.max_dim = 16;
@@ -249,13 +267,14 @@ struct Engine::Impl {
 
   // ---- loading -------------------------------------------------------------------------------
   void load_into(Slot& s, int i, size_t item, const std::string& path, SliceStatus& st,
-                 std::atomic<int64_t>& load_ns, std::atomic<int64_t>& bytes_in) {
+                 std::atomic<int64_t>& load_ns, std::atomic<int64_t>& load_cpu_ns, std::atomic<int64_t>& bytes_in) {
     thread_local std::vector<uint8_t> buf;
     TraceRange tr("nm03.load");
     const double t0 = now_s();
+    const int64_t c0 = thread_cpu_ns();
     try {
       if (fault_plan().corrupt_dicom == (int64_t)item) throw SliceError("injected fault: corrupt DICOM data");
-      dicom::SliceFile file(path);
+      dicom::SliceFile file(path, read_mode_, read_prefix_);
       const size_t n = file.size();
       const dicom::Header& h = file.header(buf);
       const int md = cfg.pipe.min_dim;
@@ -292,6 +311,7 @@ struct Engine::Impl {
       st.message = e.what();
     }
     load_ns += (int64_t)((now_s() - t0) * 1e9);
+    load_cpu_ns += thread_cpu_ns() - c0;
   }
 
   static bool outputs_exist(const WorkItem& w) {
@@ -512,7 +532,7 @@ struct Engine::Impl {
     // `batch` doubles as the host-pool priority: earlier batches first.
     s.raw_used = 0;
     s.loaded.assign(count, LoadedSlice{});
-    std::atomic<int64_t> load_ns{0}, bytes_in{0}, write_ns{0}, bytes_out{0};
+    std::atomic<int64_t> load_ns{0}, bytes_in{0}, write_ns{0}, bytes_out{0}, load_cpu_ns{0}, write_cpu_ns{0};
     {
       TaskGroup tg(*pool);
       tg.for_each(
@@ -523,7 +543,7 @@ struct Engine::Impl {
               status[first + i] = SliceStatus{kSliceOk, "resumed: outputs already present"};
               return;
             }
-            load_into(s, (int)i, first + i, items[first + i].path, status[first + i], load_ns, bytes_in);
+            load_into(s, (int)i, first + i, items[first + i].path, status[first + i], load_ns, load_cpu_ns, bytes_in);
           },
           2 * batch);
       tg.wait();
@@ -563,6 +583,7 @@ struct Engine::Impl {
             const size_t item = first + s.live[c];
             if (status[item].code != kSliceOk) return;
             const double t0 = now_s();
+            const int64_t c0 = thread_cpu_ns();
             TraceRange tr("nm03.export");
             try {
               if (fault_plan().fail_write == (int64_t)item) throw std::runtime_error("injected fault: export failure");
@@ -579,6 +600,7 @@ struct Engine::Impl {
               status[item] = SliceStatus{kSliceExportError, std::string("Error in export stage: ") + e.what()};
             }
             write_ns += (int64_t)((now_s() - t0) * 1e9);
+            write_cpu_ns += thread_cpu_ns() - c0;
           },
           2 * batch + 1);
       tg.wait();
@@ -586,6 +608,8 @@ struct Engine::Impl {
     std::lock_guard<std::mutex> g(acc_m);
     acc.load_s += load_ns.load() * 1e-9;
     acc.write_s += write_ns.load() * 1e-9;
+    acc.load_cpu_s += load_cpu_ns.load() * 1e-9;
+    acc.write_cpu_s += write_cpu_ns.load() * 1e-9;
     acc.h2d_s += local.h2d_s;
     acc.kernels_s += local.kernels_s;
     acc.bytes_in += bytes_in.load();

@@ -50,10 +50,12 @@ def test_sequence_skipping(native):
     assert np.array_equal(native.dicom_pixels(bytes(b)), px)
 
 
+@pytest.mark.parametrize("mode,prefix", [("direct", 16384), ("direct", 1024), ("staged", 0)])
 @pytest.mark.parametrize("kind", ["explicit", "implicit", "big", "u8", "long_header", "tiny"])
-def test_slice_file_direct_read(native, tmp_path, kind):
-    """SliceFile (engine loader): prefix-parsed header + pread of the pixels must equal the
-    whole-file parse for every layout, and fall back to the whole-file path where needed."""
+def test_slice_file_direct_read(native, tmp_path, kind, mode, prefix):
+    """SliceFile (engine loader): prefix-parsed header + pread of the pixels (direct; pixel bytes
+    inside the prefix come from it) or one whole-file read + streaming stores (staged) must equal
+    the whole-file parse for every layout, and fall back to the whole-file path where needed."""
     rng = np.random.default_rng(1)
     shape = (8, 8) if kind == "tiny" else (300, 257)
     px = rng.integers(0, 250 if kind == "u8" else 65535, size=shape).astype(np.uint16)
@@ -67,10 +69,10 @@ def test_slice_file_direct_read(native, tmp_path, kind):
         b[pos:pos] = blob
     p = tmp_path / "x.dcm"
     p.write_bytes(bytes(b))
-    got, direct = native.read_pixels_direct(str(p))
+    got, direct = native.read_pixels_direct(str(p), mode, prefix)
     assert np.array_equal(got, native.dicom_pixels(bytes(b)))
     assert np.array_equal(got, px)
-    assert direct == (kind in ("explicit", "implicit"))
+    assert direct == (mode == "direct" and kind in ("explicit", "implicit"))
 
 
 def test_rejects_compressed_and_garbage(native):
