@@ -17,6 +17,7 @@ shards a single cohort instead.
 import argparse
 import json
 import os
+import resource
 import shutil
 import sys
 import time
@@ -126,8 +127,10 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     ok = 0
-    stage = {"load_s": 0.0, "load_cpu_s": 0.0, "h2d_s": 0.0, "kernels_s": 0.0, "write_s": 0.0, "write_cpu_s": 0.0}
+    stage = {"load_s": 0.0, "load_cpu_s": 0.0, "h2d_s": 0.0, "kernels_s": 0.0, "write_s": 0.0, "write_cpu_s": 0.0,
+             "slot_cpu_s": 0.0}
     cg0 = cgroup_cpu_stat()
+    ru0 = resource.getrusage(resource.RUSAGE_SELF)
     for _ in range(args.steps):
         with _roctx_range("bench.step"):
             codes, msgs, times = engine.run_list(work)
@@ -138,6 +141,7 @@ def main():
     barrier(ctx)
     dt = time.perf_counter() - t0
     cg1 = cgroup_cpu_stat()
+    ru1 = resource.getrusage(resource.RUSAGE_SELF)
     dt = allreduce_max(dt, ctx)
     total_ok = int(allreduce_sum(ok, ctx))
     value = total_ok / dt
@@ -168,6 +172,8 @@ def main():
                 # host CPU of the whole cgroup over the timed region (all ranks of this container)
                 "cgroup_cpu_ms_per_step": {k[:-5]: round((cg1[k] - cg0.get(k, 0)) / 1e3 / args.steps, 3)
                                            for k in ("usage_usec", "throttled_usec") if k in cg1},
+                "rank0_process_cpu_ms_per_step": round((ru1.ru_utime + ru1.ru_stime - ru0.ru_utime - ru0.ru_stime)
+                                                       * 1e3 / args.steps, 3),
                 "storage": {"data": args.data_root, "out": args.out_root},
             },
         }

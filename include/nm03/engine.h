@@ -48,6 +48,7 @@ struct StageTimes {
   double write_s = 0;      // wall time summed over writer tasks
   double load_cpu_s = 0;   // thread CPU time of the loader tasks
   double write_cpu_s = 0;  // thread CPU time of the writer tasks
+  double slot_cpu_s = 0;   // thread CPU time of the slot threads (descriptors, launches, waits)
   double wall_s = 0;     // run() wall time
   int64_t batches = 0, slices_ok = 0, slices_failed = 0;
   int64_t bytes_in = 0, bytes_out = 0;

@@ -552,6 +552,7 @@ PYBIND11_MODULE(_nm03, m) {
     td["write_s"] = t.write_s;
     td["load_cpu_s"] = t.load_cpu_s;
     td["write_cpu_s"] = t.write_cpu_s;
+    td["slot_cpu_s"] = t.slot_cpu_s;
     td["wall_s"] = t.wall_s;
     td["batches"] = t.batches;
     td["slices_ok"] = t.slices_ok;

@@ -2,6 +2,7 @@
 #include "nm03/engine.h"
 
 #include <hip/hip_runtime_api.h>
+#include <sys/prctl.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -84,6 +85,20 @@ struct Slot {
   int32_t* d_sizes = nullptr;
   std::atomic<size_t> raw_used{0};
   std::vector<LoadedSlice> loaded;
+  // Progressive upload: raw-region allocations in offset order with a done flag each; the slot
+  // thread uploads the longest finished prefix while later loads are still running.
+  struct Alloc {
+    size_t off = 0, len = 0;  // u16 elements
+    std::atomic<bool> done{false};
+  };
+  std::unique_ptr<Alloc[]> allocs;
+  size_t n_allocs = 0;
+  std::mutex alloc_m;
+  std::mutex prog_m;
+  std::condition_variable prog_cv;
+  size_t loads_finished = 0;  // guarded by prog_m
+  size_t uploaded = 0;        // u16 elements of the raw region already queued for upload
+  bool upload_started = false;
   // built per batch
   std::vector<int> live;  // batch-local indices of loaded slices, in order
   int ncanvas = 0;
@@ -139,6 +154,7 @@ struct Engine::Impl {
     if (const char* e = std::getenv("NM03_LOAD_MODE"); e && *e)
       read_mode_ = std::string(e) == "staged" ? dicom::ReadMode::kStaged : dicom::ReadMode::kDirect;
     if (const char* e = std::getenv("NM03_LOAD_PREFIX"); e && *e) read_prefix_ = (size_t)std::atol(e);
+    if (const char* e = std::getenv("NM03_UPLOAD_CHUNK_KB"); e && *e) upload_chunk_ = (size_t)std::atol(e) << 10;
     if (cfg.batch_size < 1) cfg.batch_size = 1;
     if (cfg.streams < 1) cfg.streams = 1;
     if (cfg.max_dim < 16) cfg.max_dim = 16;
@@ -222,12 +238,8 @@ struct Engine::Impl {
       check_hip(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking), "hipStreamCreate");
       check_hip(hipEventCreate(&s.ev0), "hipEventCreate");
       check_hip(hipEventCreate(&s.ev1), "hipEventCreate");
-      // Batch completion is waited on by the slot thread: a blocking-sync event sleeps instead of
-      // spinning a core the loader/writer pool needs (NM03_EVENT_SPIN=1 restores spinning).
-      static const bool spin = [] {
-        const char* e = std::getenv("NM03_EVENT_SPIN");
-        return e && *e && *e != '0';
-      }();
+      // Batch completion is waited on by the slot thread (wait_batch).
+      const bool spin = wait_mode() == WaitMode::kSpin;
       check_hip(hipEventCreateWithFlags(&s.ev2, spin ? hipEventDefault : hipEventBlockingSync), "hipEventCreate");
       check_hip(hipHostMalloc((void**)&s.h_blob, s.blob_bytes, hipHostMallocDefault), "hipHostMalloc blob");
       s.d_blob = dmalloc<uint8_t>(s.blob_bytes, "hipMalloc blob");
@@ -265,6 +277,86 @@ struct Engine::Impl {
     return sp;
   }
 
+  // ---- progressive upload --------------------------------------------------------------------
+  // While a batch loads, queue the H2D copy of every finished, contiguous prefix of the raw region
+  // once it has grown by `upload_chunk_` bytes: the copy engine starts after a few loads instead
+  // of after the whole batch (pipeline fill at the start of a run, load/upload overlap inside
+  // every batch). NM03_UPLOAD_CHUNK_KB (0 = one upload per batch after all loads).
+  size_t upload_chunk_ = 2u << 20;
+
+  void upload_progress(Slot& s, size_t count) {
+    size_t next = 0, seen = 0;
+    for (;;) {
+      bool all;
+      {
+        std::unique_lock<std::mutex> g(s.prog_m);
+        s.prog_cv.wait(g, [&] { return s.loads_finished != seen; });
+        seen = s.loads_finished;
+        all = seen == count;
+      }
+      size_t n;
+      {
+        std::lock_guard<std::mutex> g(s.alloc_m);
+        n = s.n_allocs;
+      }
+      size_t end = s.uploaded;
+      while (next < n && s.allocs[next].done.load(std::memory_order_acquire)) {
+        end = s.allocs[next].off + s.allocs[next].len;
+        ++next;
+      }
+      if (all) return;  // the remainder goes with the tables in build_and_run
+      if ((end - s.uploaded) * 2 >= upload_chunk_) {
+        if (!s.upload_started) {
+          check_hip(hipEventRecord(s.ev0, s.stream), "event");
+          s.upload_started = true;
+        }
+        check_hip(hipMemcpyAsync(s.d_blob + s.raw_base + s.uploaded * 2, s.h_blob + s.raw_base + s.uploaded * 2,
+                                 (end - s.uploaded) * 2, hipMemcpyHostToDevice, s.stream),
+                  "H2D pixels");
+        s.uploaded = end;
+      }
+    }
+  }
+
+  // ---- batch completion ----------------------------------------------------------------------
+  // The slot thread waits for its batch here. A blocking-sync hipEventSynchronize still spins in
+  // the runtime before it sleeps, which cost ≈0.7 ms of slot-thread CPU per batch — CPU the
+  // loader/writer pool needs. `poll` sleeps in short steps (timer slack lowered to 1 µs on slot
+  // threads) and queries the event: a few µs of CPU per batch, ≤ poll interval of added latency,
+  // hidden by the other slots in flight. NM03_EVENT_WAIT=poll|block|spin, NM03_EVENT_POLL_US.
+  enum class WaitMode { kPoll, kBlock, kSpin };
+  static WaitMode wait_mode() {
+    static const WaitMode m = [] {
+      const char* e = std::getenv("NM03_EVENT_WAIT");
+      const std::string v = e ? e : "";
+      if (v == "block") return WaitMode::kBlock;
+      if (v == "spin") return WaitMode::kSpin;
+      if (const char* sp = std::getenv("NM03_EVENT_SPIN"); sp && *sp && *sp != '0') return WaitMode::kSpin;
+      return WaitMode::kPoll;
+    }();
+    return m;
+  }
+  static int poll_us() {
+    static const int us = [] {
+      const char* e = std::getenv("NM03_EVENT_POLL_US");
+      const int v = e && *e ? std::atoi(e) : 20;
+      return v < 1 ? 1 : v;
+    }();
+    return us;
+  }
+  void wait_batch(hipEvent_t ev) {
+    if (wait_mode() != WaitMode::kPoll) {
+      check_hip(hipEventSynchronize(ev), "batch sync");
+      return;
+    }
+    for (;;) {
+      const hipError_t e = hipEventQuery(ev);
+      if (e == hipSuccess) return;
+      if (e != hipErrorNotReady) check_hip(e, "batch sync");
+      std::this_thread::sleep_for(std::chrono::microseconds(poll_us()));
+    }
+  }
+
   // ---- loading -------------------------------------------------------------------------------
   void load_into(Slot& s, int i, size_t item, const std::string& path, SliceStatus& st,
                  std::atomic<int64_t>& load_ns, std::atomic<int64_t>& load_cpu_ns, std::atomic<int64_t>& bytes_in) {
@@ -288,10 +380,25 @@ struct Engine::Impl {
       } else {
         const size_t npix = (size_t)h.rows * h.cols;
         const size_t alloc = align_up(npix, 8);
-        const size_t off = s.raw_used.fetch_add(alloc);
-        if (off + alloc > s.cap_pixels) throw SliceError("batch pixel capacity exceeded");
+        size_t off, idx;
+        {
+          std::lock_guard<std::mutex> g(s.alloc_m);
+          off = s.raw_used.load(std::memory_order_relaxed);
+          if (off + alloc > s.cap_pixels) throw SliceError("batch pixel capacity exceeded");
+          s.raw_used.store(off + alloc, std::memory_order_relaxed);
+          idx = s.n_allocs++;
+          s.allocs[idx].off = off;
+          s.allocs[idx].len = alloc;
+          s.allocs[idx].done.store(false, std::memory_order_relaxed);
+        }
         uint16_t* dst = reinterpret_cast<uint16_t*>(s.h_blob + s.raw_base) + off;
-        file.pixels16(dst);
+        try {
+          file.pixels16(dst);
+        } catch (...) {
+          s.allocs[idx].done.store(true, std::memory_order_release);  // space stays unused
+          throw;
+        }
+        s.allocs[idx].done.store(true, std::memory_order_release);
         LoadedSlice& L = s.loaded[i];
         L.w = h.cols;
         L.h = h.rows;
@@ -424,7 +531,6 @@ struct Engine::Impl {
     s.ncanvas = ncanv;
     if (nl == 0) return;
 
-    const size_t bytes = s.raw_base + s.raw_used.load() * sizeof(uint16_t);
     uint8_t* db = s.d_blob;
     const auto* d_stats_c = reinterpret_cast<SliceStats*>(db + s.off_stats);
     auto* d_stats = reinterpret_cast<SliceStats*>(db + s.off_stats);
@@ -437,8 +543,15 @@ struct Engine::Impl {
     auto* d_raw = reinterpret_cast<uint16_t*>(db + s.raw_base);
     auto plane = [&](Plane p) { return s.d_bits + p * s.plane_words; };
 
-    check_hip(hipEventRecord(s.ev0, s.stream), "event");
-    check_hip(hipMemcpyAsync(s.d_blob, s.h_blob, bytes, hipMemcpyHostToDevice, s.stream), "H2D blob");
+    if (!s.upload_started) check_hip(hipEventRecord(s.ev0, s.stream), "event");
+    // Tables, then the raw pixels not already queued by upload_progress (all of them without it).
+    check_hip(hipMemcpyAsync(s.d_blob, s.h_blob, s.raw_base, hipMemcpyHostToDevice, s.stream), "H2D tables");
+    const size_t raw_end = s.raw_used.load();
+    if (raw_end > s.uploaded)
+      check_hip(hipMemcpyAsync(s.d_blob + s.raw_base + s.uploaded * 2, s.h_blob + s.raw_base + s.uploaded * 2,
+                               (raw_end - s.uploaded) * 2, hipMemcpyHostToDevice, s.stream),
+                "H2D pixels");
+    s.uploaded = raw_end;
     check_hip(hipEventRecord(s.ev1, s.stream), "event");
     auto chain = [&] {
       launch_median(d_raw, s.d_med, d_desc, d_medt, nmed, pc.median_k, d_stats, s.stream, s.d_tile_mm);
@@ -493,7 +606,7 @@ struct Engine::Impl {
       check_hip(hipGraphLaunch(it->second, s.stream), "graph launch");
     }
     check_hip(hipEventRecord(s.ev2, s.stream), "event");
-    check_hip(hipEventSynchronize(s.ev2), "batch sync");
+    wait_batch(s.ev2);
     if (acc) {
       float a = 0, b = 0;
       (void)hipEventElapsedTime(&a, s.ev0, s.ev1);
@@ -532,6 +645,14 @@ struct Engine::Impl {
     // `batch` doubles as the host-pool priority: earlier batches first.
     s.raw_used = 0;
     s.loaded.assign(count, LoadedSlice{});
+    if (!s.allocs) s.allocs.reset(new Slot::Alloc[s.cap_slices]);
+    s.n_allocs = 0;
+    s.uploaded = 0;
+    s.upload_started = false;
+    {
+      std::lock_guard<std::mutex> g(s.prog_m);
+      s.loads_finished = 0;
+    }
     std::atomic<int64_t> load_ns{0}, bytes_in{0}, write_ns{0}, bytes_out{0}, load_cpu_ns{0}, write_cpu_ns{0};
     {
       TaskGroup tg(*pool);
@@ -541,16 +662,26 @@ struct Engine::Impl {
             if (on_start) on_start(first + i);
             if (cfg.resume && outputs_exist(items[first + i])) {
               status[first + i] = SliceStatus{kSliceOk, "resumed: outputs already present"};
-              return;
+            } else {
+              load_into(s, (int)i, first + i, items[first + i].path, status[first + i], load_ns, load_cpu_ns, bytes_in);
             }
-            load_into(s, (int)i, first + i, items[first + i].path, status[first + i], load_ns, load_cpu_ns, bytes_in);
+            if (upload_chunk_) {
+              {
+                std::lock_guard<std::mutex> g(s.prog_m);
+                ++s.loads_finished;
+              }
+              s.prog_cv.notify_one();
+            }
           },
           2 * batch);
+      if (upload_chunk_) upload_progress(s, count);
       tg.wait();
     }
     s.live.clear();
     for (size_t i = 0; i < count; ++i)
       if (s.loaded[i].ok) s.live.push_back((int)i);
+    // Nothing to run, but early chunks may be in flight: the next batch reuses the pinned blob.
+    if (s.live.empty() && s.upload_started) check_hip(hipStreamSynchronize(s.stream), "upload drain");
     StageTimes local;
     int64_t fallbacks = 0;
     if (!s.live.empty()) {
@@ -562,6 +693,7 @@ struct Engine::Impl {
       } catch (const std::exception& e) {
         for (int i : s.live) status[first + i] = SliceStatus{kSliceDeviceError, e.what()};
         s.live.clear();
+        if (s.upload_started) (void)hipStreamSynchronize(s.stream);  // blob is reused next batch
       }
     }
     if (cfg.export_jpeg && !s.live.empty()) {
@@ -682,6 +814,7 @@ struct Engine::Impl {
 
   void worker(Slot* s) {
     place.bind_this_thread();
+    (void)prctl(PR_SET_TIMERSLACK, 1000UL, 0, 0, 0);  // 1 µs: short poll sleeps stay short
     (void)hipSetDevice(cfg.device);
     uint64_t seen = 0;
     for (;;) {
@@ -693,6 +826,7 @@ struct Engine::Impl {
         seen = job_gen;
         j = job;
       }
+      const int64_t c0 = thread_cpu_ns();
       try {
         for (size_t b; (b = j->next.fetch_add(1)) < j->batches.size();) {
           const auto [first, count] = j->batches[b];
@@ -701,6 +835,10 @@ struct Engine::Impl {
       } catch (...) {
         std::lock_guard<std::mutex> g(j->err_m);
         if (!j->err) j->err = std::current_exception();
+      }
+      {
+        std::lock_guard<std::mutex> g(*j->acc_m);
+        j->acc->slot_cpu_s += (thread_cpu_ns() - c0) * 1e-9;
       }
       std::lock_guard<std::mutex> g(job_m);
       if (--busy == 0) done_cv.notify_all();
@@ -746,6 +884,8 @@ struct Engine::Impl {
     Slot& s = *slots[0];
     if (in.w > cfg.max_dim || in.h > cfg.max_dim) throw DeviceError("slice exceeds engine max_dim");
     s.raw_used = align_up((size_t)in.w * in.h, 8);
+    s.uploaded = 0;
+    s.upload_started = false;
     s.loaded.assign(1, LoadedSlice{});
     LoadedSlice& L = s.loaded[0];
     L.ok = true;
