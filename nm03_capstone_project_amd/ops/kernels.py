@@ -104,6 +104,32 @@ def region_grow(band, seeds=None, config: PipelineConfig = None):
     return res
 
 
+def region_grow3d(band, seeds=(), connectivity=6, region=None):
+    """3D seeded region growing (K5 plane sweeps) on a bool band [D, H, W] (CUDA, H, W ≤ 512).
+    `seeds` are (x, y, z) voxels; `region` (bool [D, H, W], ⊆ band) is grown further instead of
+    starting from nothing — the z-slab decomposition re-grows a slab after its neighbours added
+    boundary voxels. Returns (region bool [D, H, W], sweeps)."""
+    if band.dim() != 3 or not band.is_cuda:
+        raise ValueError("band must be a CUDA tensor [D, H, W]")
+    d, h, w = band.shape
+    bw = pack_bits(band.bool()).contiguous()
+    rw = pack_bits(region.bool() & band.bool()).contiguous() if region is not None else torch.zeros_like(bw)
+    sweeps = native().k_srg3d(bw.data_ptr(), rw.data_ptr(), w, h, d, [tuple(map(int, s)) for s in seeds],
+                              int(connectivity), region is None, _stream())
+    return unpack_bits(rw, w), sweeps
+
+
+def dilate3d(mask, size=7):
+    """Cube dilation (size×size×size, out-of-volume samples ignored) of a bool [D, H, W] CUDA mask."""
+    if mask.dim() != 3 or not mask.is_cuda:
+        raise ValueError("mask must be a CUDA tensor [D, H, W]")
+    d, h, w = mask.shape
+    src = pack_bits(mask.bool()).contiguous()
+    dst, tmp = torch.empty_like(src), torch.empty_like(src)
+    native().k_dilate3d(src.data_ptr(), dst.data_ptr(), tmp.data_ptr(), w, h, d, int(size), _stream())
+    return unpack_bits(dst, w)
+
+
 def jpeg_encode(canvas, quality=75, header=True):
     """GPU JPEG of uint8 gray canvases [N,H,W] (H, W multiples of 16) → list of bytes (complete
     JFIF files when header=True, else the entropy-coded segments)."""

@@ -111,7 +111,7 @@ __global__ void dilate_z_kernel(const uint64_t* __restrict__ src, uint64_t* __re
 }
 
 int srg_volume(const uint64_t* band, uint64_t* region, int w, int h, int d, const int32_t* seeds_xyz, int nseeds,
-               int connectivity, uint32_t* d_flag, uint32_t* h_flag, hipStream_t stream) {
+               int connectivity, uint32_t* d_flag, uint32_t* h_flag, hipStream_t stream, bool reset) {
   if (w > kSrgMaxDim || h > kSrgMaxDim || d > kSrgMaxDim) throw DeviceError("srg_volume: dimension larger than 512");
   const int n = (w + 63) / 64, wb = (w + 63) / 64;
   const size_t words = (size_t)h * n;
@@ -121,7 +121,7 @@ int srg_volume(const uint64_t* band, uint64_t* region, int w, int h, int d, cons
   if (w * ((maxrows + 63) / 64) > plane_words) plane_words = w * ((maxrows + 63) / 64);
   plane_words = (plane_words + 1) & ~1;
   (void)wb;
-  check_hip(hipMemsetAsync(region, 0, words * d * sizeof(uint64_t), stream), "memset region");
+  if (reset) check_hip(hipMemsetAsync(region, 0, words * d * sizeof(uint64_t), stream), "memset region");
   if (nseeds > 0) {
     srg3d_seed_kernel<<<(nseeds + 63) / 64, 64, 0, stream>>>(band, region, w, h, d, seeds_xyz, nseeds);
     check_launch("srg3d_seed_kernel");

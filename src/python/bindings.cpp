@@ -689,6 +689,52 @@ PYBIND11_MODULE(_nm03, m) {
     gpu::launch_srg_morph((const uint64_t*)band, t.desc, n, t.seeds, consts_from(p, border_radius), o, w, h, st);
     gpu::check_hip(hipStreamSynchronize(st), "k_srg_morph");
   });
+  // 3D region growing on bit volumes [d][h][ceil(w/64)] (int64 words), continuing from the region
+  // already present when reset is false; returns the sweep count. Synchronous on `stream`.
+  m.def("k_srg3d", [](uintptr_t band, uintptr_t region, int w, int h, int d,
+                      const std::vector<std::tuple<int, int, int>>& seeds, int connectivity, bool reset,
+                      uintptr_t stream) {
+    hipStream_t st = as_stream(stream);
+    if (connectivity != 6 && connectivity != 26) throw std::invalid_argument("connectivity must be 6 or 26");
+    std::vector<int32_t> sx;
+    for (const auto& [x, y, z] : seeds) {
+      sx.push_back(x);
+      sx.push_back(y);
+      sx.push_back(z);
+    }
+    int32_t* d_seeds = nullptr;
+    uint32_t* d_flag = nullptr;
+    uint32_t* h_flag = nullptr;
+    auto release = [&] {
+      if (d_seeds) (void)hipFree(d_seeds);
+      if (d_flag) (void)hipFree(d_flag);
+      if (h_flag) (void)hipHostFree(h_flag);
+    };
+    try {
+      gpu::check_hip(hipMalloc((void**)&d_flag, 2 * sizeof(uint32_t)), "hipMalloc flag");
+      gpu::check_hip(hipHostMalloc((void**)&h_flag, 2 * sizeof(uint32_t), hipHostMallocDefault), "hipHostMalloc flag");
+      if (!sx.empty()) {
+        gpu::check_hip(hipMalloc((void**)&d_seeds, sx.size() * sizeof(int32_t)), "hipMalloc seeds");
+        gpu::check_hip(hipMemcpyAsync(d_seeds, sx.data(), sx.size() * sizeof(int32_t), hipMemcpyHostToDevice, st),
+                       "H2D seeds");
+      }
+      const int sweeps = gpu::srg_volume((const uint64_t*)band, (uint64_t*)region, w, h, d, d_seeds,
+                                         (int)(sx.size() / 3), connectivity, d_flag, h_flag, st, reset);
+      gpu::check_hip(hipStreamSynchronize(st), "k_srg3d");
+      release();
+      return sweeps;
+    } catch (...) {
+      (void)hipStreamSynchronize(st);
+      release();
+      throw;
+    }
+  });
+  m.def("k_dilate3d", [](uintptr_t src, uintptr_t dst, uintptr_t tmp, int w, int h, int d, int size, uintptr_t stream) {
+    hipStream_t st = as_stream(stream);
+    if (size < 1 || !(size & 1)) throw std::invalid_argument("dilation size must be odd and >= 1");
+    gpu::dilate_volume((const uint64_t*)src, (uint64_t*)dst, (uint64_t*)tmp, w, h, d, size, st);
+    gpu::check_hip(hipStreamSynchronize(st), "k_dilate3d");
+  });
   m.def("k_jpeg", [](uintptr_t canvas, int n, int h, int w, int quality, uintptr_t stream) {
     hipStream_t st = as_stream(stream);
     const int blocks = (w / 8) * (h / 8);

@@ -273,6 +273,35 @@ def test_engine_fault_isolation(native, tmp_path):
     assert t2["slices_ok"] == 2 and t2["slices_failed"] == 2
 
 
+def test_engine_progressive_upload_identical(native, cohort_root, tmp_path, monkeypatch):
+    """Progressive H2D (finished prefixes of a batch's raw region queued while loads run) with
+    1 KiB / 64 KiB chunks vs one upload per batch: same statuses, byte-identical JPEGs, on a work
+    list mixing slice sizes with unreadable and too-small files (failed loads leave holes in the
+    allocation order)."""
+    d = tmp_path / "extra"
+    d.mkdir()
+    (d / "1-1.dcm").write_bytes(native.dicom_bytes(native.phantom_slice(160, 200, 2, 7, 25, 3)))
+    (d / "1-2.dcm").write_bytes(b"DICM-but-not-really" * 10)
+    (d / "1-3.dcm").write_bytes(native.dicom_bytes(np.zeros((64, 64), np.uint16)))
+    (d / "1-4.dcm").write_bytes(native.dicom_bytes(native.phantom_slice(512, 384, 3, 9, 25, 4)))
+    runs = []
+    for i, kb in enumerate(["0", "1", "64"]):
+        out = str(tmp_path / f"o{i}")
+        items = _items(native, cohort_root, out)[:40]
+        os.makedirs(os.path.join(out, "extra"), exist_ok=True)
+        extra = [(str(d / f"1-{k}.dcm"), os.path.join(out, "extra")) for k in range(1, 5)]
+        items = items[:9] + extra[:2] + items[9:30] + extra[2:] + items[30:]
+        monkeypatch.setenv("NM03_UPLOAD_CHUNK_KB", kb)
+        eng = native.Engine(nm.PipelineConfig(batch_size=16, streams=3, threads=4).engine_config())
+        st, _ = eng.run(items)
+        del eng
+        runs.append(([c for c, _ in st], _tree(out)))
+    assert runs[0][0].count(0) == len(runs[0][0]) - 2
+    for codes, tree in runs[1:]:
+        assert codes == runs[0][0]
+        assert tree == runs[0][1]
+
+
 # ---------------------------------------------------------------------------------------------
 # CLIs on the GPU: sequential ≡ parallel byte-for-byte, reference message catalogue
 # ---------------------------------------------------------------------------------------------
@@ -397,3 +426,85 @@ def test_test_pipeline_dump_mhd_gpu_equals_cpu(native, cohort_root, tmp_path):
         a, _ = native.mhd_read(str(tmp_path / "m_gpu" / f"{name}.mhd"))
         b, _ = native.mhd_read(str(tmp_path / "m_cpu" / f"{name}.mhd"))
         assert np.array_equal(a.astype(np.float64), b.astype(np.float64)), name
+
+
+# ---------------------------------------------------------------------------------------------
+# 3D torch ops and the z-slab decomposition (parallel/volume_slabs.py) on the GPU
+# ---------------------------------------------------------------------------------------------
+def test_region_grow3d_and_dilate3d_ops_vs_golden(native):
+    from nm03_capstone_project_amd import ops
+    rng = np.random.default_rng(11)
+    band = (rng.random((20, 70, 130)) < 0.4).astype(np.uint8)
+    seeds = [(int(x), int(y), int(z)) for z, y, x in zip(*np.nonzero(band))][:40:8]
+    bt = torch.from_numpy(band.astype(bool)).cuda()
+    for conn in (6, 26):
+        ref = native.golden_region_grow3d(band, seeds, conn)
+        reg, sweeps = ops.region_grow3d(bt, seeds, conn)
+        assert sweeps >= 2 and np.array_equal(reg.cpu().numpy().astype(np.uint8), ref)
+        # continuing from a partial region (seed voxels only) reaches the same fixpoint
+        part = np.zeros_like(band)
+        for x, y, z in seeds:
+            part[z, y, x] = band[z, y, x]
+        reg2, _ = ops.region_grow3d(bt, [], conn, region=torch.from_numpy(part.astype(bool)).cuda())
+        assert np.array_equal(reg2.cpu().numpy().astype(np.uint8), ref)
+        for size in (3, 7):
+            dil = ops.dilate3d(reg, size)
+            assert np.array_equal(dil.cpu().numpy().astype(np.uint8), native.golden_dilate3d(ref, size))
+
+
+def test_volume_slabs_single_rank_equals_volume_pipeline(native):
+    from nm03_capstone_project_amd.parallel.volume_slabs import run_volume_slabs
+    d, h, w = 24, 96, 128
+    vol = np.stack([native.phantom_slice(h, w, 2, z, d, 5) for z in range(d)])
+    vp = nm.VolumePipeline(connectivity=6, dilation=7)
+    ref = vp.run(vol)
+    ctx = nm.parallel.DistContext(0, 1, 0, "none", torch.device("cuda", 0))
+    r = run_volume_slabs(volume=vol, ctx=ctx, connectivity=6, dilation=7, backend="gpu")
+    assert ref["region"].sum() > 0
+    assert np.array_equal(r["band"].cpu().numpy().astype(np.uint8), ref["band"])
+    assert np.array_equal(r["region"].cpu().numpy().astype(np.uint8), ref["region"])
+    assert np.array_equal(r["dilated"].cpu().numpy().astype(np.uint8), ref["dilated"])
+
+
+def _slab_gpu_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), NM03_DEVICE_OVERRIDE="0")
+    import nm03_capstone_project_amd as nmx
+    from nm03_capstone_project_amd.parallel.volume_slabs import run_volume_slabs
+    ctx = nmx.parallel.init_from_env(backend="gloo")
+    try:
+        n = nmx.native()
+        d, h, w = 24, 96, 128
+        vol = np.stack([n.phantom_slice(h, w, 2, z, d, 5) for z in range(d)])
+        r = run_volume_slabs(volume=vol, ctx=ctx, connectivity=26, dilation=7, backend="gpu", gather=True)
+        q.put((rank, r["region"].cpu().numpy().astype(np.uint8), r["dilated"].cpu().numpy().astype(np.uint8),
+               r["rounds"]))
+    finally:
+        torch.distributed.destroy_process_group()
+
+
+def test_volume_slabs_two_ranks_on_one_gpu(native):
+    """Two ranks (spawned, gloo collectives, both on device 0) decompose one volume into z-slabs:
+    the gathered masks equal the single-GPU VolumePipeline result."""
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    d, h, w = 24, 96, 128
+    vol = np.stack([native.phantom_slice(h, w, 2, z, d, 5) for z in range(d)])
+    ref = nm.VolumePipeline(connectivity=26, dilation=7).run(vol)
+    mctx = mp.get_context("spawn")
+    q = mctx.Queue()
+    ps = [mctx.Process(target=_slab_gpu_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=100) for _ in range(2)]
+    for p in ps:
+        p.join(30)
+        assert p.exitcode == 0
+    for rank, region, dil, rounds in res:
+        assert np.array_equal(region, ref["region"]), rank
+        assert np.array_equal(dil, ref["dilated"]), rank
+        assert rounds >= 2  # the lesion spans the slab boundary: at least one exchange added voxels

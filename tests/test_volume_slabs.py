@@ -1,0 +1,91 @@
+"""Z-slab decomposition of one 3D volume over ranks (parallel/volume_slabs.py) on the
+CPU: gloo process groups of 2 and 3 ranks, golden backend. The reassembled region and dilation must
+equal the single-volume golden 3D region growing + cube dilation exactly, including a serpentine
+band that crosses every slab boundary many times (many exchange rounds)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _serpentine(d, h, w):
+    """A one-voxel-thick tube that runs up and down the full z range along x: every slab boundary
+    is crossed ~w/2 times, so growth must hop between slabs round after round."""
+    b = np.zeros((d, h, w), np.uint8)
+    y = h // 2
+    for x in range(0, w, 2):
+        b[:, y, x] = 1
+        if x + 1 < w:
+            z = d - 1 if (x // 2) % 2 == 0 else 0
+            b[z, y, x + 1] = 1
+    return b
+
+
+def _volumes():
+    rng = np.random.default_rng(5)
+    rand = (rng.random((13, 37, 70)) < 0.33).astype(np.uint8)
+    seeds_rand = [(int(x), int(y), int(z)) for z, y, x in zip(*np.nonzero(rand))][:6:2] + [(1, 1, 6)]
+    snake = _serpentine(11, 5, 23)
+    return {"random": (rand, seeds_rand), "snake": (snake, [(0, 2, 0)])}
+
+
+def _worker(rank, world, port, conn, dilation, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    from nm03_capstone_project_amd.parallel import dist as D
+    from nm03_capstone_project_amd.parallel.volume_slabs import run_volume_slabs
+    ctx = D.init_from_env(backend="gloo", use_gpu=False)
+    try:
+        out = {}
+        for name, (band, seeds) in _volumes().items():
+            r = run_volume_slabs(band=band, ctx=ctx, connectivity=conn, dilation=dilation, seeds=seeds,
+                                 backend="cpu", gather=True)
+            out[name] = (r["region"].numpy().astype(np.uint8), r["dilated"].numpy().astype(np.uint8), r["rounds"])
+        q.put((rank, out))
+    finally:
+        torch.distributed.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,conn,dilation", [(2, 6, 7), (3, 26, 3), (3, 6, 5)])
+def test_slabs_equal_single_volume(native, world, conn, dilation):
+    port = _free_port()
+    mctx = mp.get_context("spawn")
+    q = mctx.Queue()
+    ps = [mctx.Process(target=_worker, args=(r, world, port, conn, dilation, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = sorted((q.get(timeout=180) for _ in range(world)), key=lambda t: t[0])
+    for p in ps:
+        p.join(60)
+        assert p.exitcode == 0
+    for name, (band, seeds) in _volumes().items():
+        ref_r = native.golden_region_grow3d(band, seeds, conn)
+        ref_d = native.golden_dilate3d(ref_r, dilation)
+        assert ref_r.sum() > 0
+        for rank, out in res:
+            region, dil, rounds = out[name]
+            assert np.array_equal(region, ref_r), (name, rank)
+            assert np.array_equal(dil, ref_d), (name, rank)
+        if name == "snake" and conn == 6:
+            assert res[0][1][name][2] > 4  # growth hopped across slab boundaries several times
+
+
+def test_single_rank_matches_golden(native):
+    from nm03_capstone_project_amd.parallel.volume_slabs import run_volume_slabs
+    band, seeds = _volumes()["random"]
+    r = run_volume_slabs(band=band, connectivity=6, dilation=7, seeds=seeds, backend="cpu")
+    ref = native.golden_region_grow3d(band, seeds, 6)
+    assert np.array_equal(r["region"].numpy().astype(np.uint8), ref)
+    assert np.array_equal(r["dilated"].numpy().astype(np.uint8), native.golden_dilate3d(ref, 7))
+    assert r["rounds"] == 1 and r["z0"] == 0
