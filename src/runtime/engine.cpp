@@ -281,11 +281,14 @@ struct Engine::Impl {
   // While a batch loads, queue the H2D copy of every finished, contiguous prefix of the raw region
   // once it has grown by `upload_chunk_` bytes: the copy engine starts after a few loads instead
   // of after the whole batch (pipeline fill at the start of a run, load/upload overlap inside
-  // every batch). NM03_UPLOAD_CHUNK_KB (0 = one upload per batch after all loads).
+  // every batch). NM03_UPLOAD_CHUNK_KB (0 = one upload per batch after all loads) sets the minimum;
+  // batches of large slices use a quarter of the batch (512² × 64: 8 MiB — many concurrent small
+  // copies cost 10% of the upload rate there, profiles/iter5/c4_sweep.txt).
   size_t upload_chunk_ = 2u << 20;
 
   void upload_progress(Slot& s, size_t count) {
     size_t next = 0, seen = 0;
+    size_t chunk = 0;  // bytes; at least upload_chunk_, and a quarter of the batch (large slices)
     for (;;) {
       bool all;
       {
@@ -305,7 +308,8 @@ struct Engine::Impl {
         ++next;
       }
       if (all) return;  // the remainder goes with the tables in build_and_run
-      if ((end - s.uploaded) * 2 >= upload_chunk_) {
+      if (!chunk && next > 0) chunk = std::max(upload_chunk_, count * s.allocs[0].len * 2 / 4);
+      if (chunk && (end - s.uploaded) * 2 >= chunk) {
         if (!s.upload_started) {
           check_hip(hipEventRecord(s.ev0, s.stream), "event");
           s.upload_started = true;

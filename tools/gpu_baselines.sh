@@ -28,7 +28,7 @@ timeout -k 10 120 $B/nm03_bench --config cohort --data-root $T/cohort/ --out /tm
 timeout -k 10 300 $B/nm03_bench --config cpu-reference --data-root $T/cohort/ --out /tmp/bl_o3c --steps 2 --warmup 1 --batch-size 25 --threads 16 > $O/c3_cpu.json || exit 133
 echo "c3 done $(date)" >> $O/progress.txt
 # config 4: 512² × 10k, 5×5 median (CPU reference on a 400-slice subset of the same shape)
-timeout -k 10 300 $B/nm03_bench --config cohort --data-root $T/stress/ --out /tmp/bl_o4 --steps 3 --warmup 1 --batch-size 64 --streams 6 --median-window 5 --max-dim 512 > $O/c4_gpu.json || exit 141
+timeout -k 10 300 $B/nm03_bench --config cohort --data-root $T/stress/ --out /tmp/bl_o4 --steps 3 --warmup 1 --batch-size 64 --streams 3 --median-window 5 --max-dim 512 > $O/c4_gpu.json || exit 141
 timeout -k 10 300 $B/nm03_bench --config cpu-reference --data-root $T/stress_cpu/ --out /tmp/bl_o4c --steps 1 --warmup 0 --batch-size 25 --threads 16 --median-window 5 > $O/c4_cpu.json || exit 142
 echo "c4 done $(date)" >> $O/progress.txt
 # config 5: 256³ volume
