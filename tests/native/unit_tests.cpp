@@ -1,0 +1,417 @@
+// Native unit tests of the host runtime (SURVEY §4.2 tier T0/T1, registered with CTest and run by
+// tests/test_native_unit.py): cohort naming rules, DICOM round trips through every loader path,
+// streaming copies, the JPEG container, golden operators against brute-force definitions, the
+// host thread pool, loopback collectives and the wire format, NUMA cpulists and the CLI defaults.
+// Host code only — no GPU is touched, so this runs in CPU-only CI.
+//
+//   build/bin/nm03_unit_tests [filter]      (exit status = number of failed checks)
+#include <unistd.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <functional>
+#include <queue>
+#include <random>
+#include <set>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "nm03/app.h"
+#include "nm03/cohort.h"
+#include "nm03/comm.h"
+#include "nm03/dicom.h"
+#include "nm03/golden.h"
+#include "nm03/jpeg.h"
+#include "nm03/numa.h"
+#include "nm03/params.h"
+#include "nm03/thread_pool.h"
+
+namespace {
+
+int g_failed = 0, g_checks = 0;
+const char* g_test = "";
+
+#define CHECK(cond)                                                                         \
+  do {                                                                                      \
+    ++g_checks;                                                                             \
+    if (!(cond)) {                                                                          \
+      ++g_failed;                                                                           \
+      std::fprintf(stderr, "FAIL [%s] %s:%d: %s\n", g_test, __FILE__, __LINE__, #cond);     \
+    }                                                                                       \
+  } while (0)
+
+struct Test {
+  const char* name;
+  std::function<void()> fn;
+};
+std::vector<Test>& registry() {
+  static std::vector<Test> r;
+  return r;
+}
+struct Reg {
+  Reg(const char* n, std::function<void()> f) { registry().push_back({n, std::move(f)}); }
+};
+#define TEST(name)                      \
+  static void name();                   \
+  static Reg reg_##name(#name, name);   \
+  static void name()
+
+std::string tmpdir() {
+  static std::string d = [] {
+    char t[] = "/tmp/nm03_unit_XXXXXX";
+    const char* p = mkdtemp(t);
+    return std::string(p ? p : "/tmp");
+  }();
+  return d;
+}
+
+// ---- cohort naming (main_sequential.cpp:18-30, 93-168) ------------------------------------------
+TEST(extract_file_number_rules) {
+  using nm03::cohort::extract_file_number;
+  CHECK(extract_file_number("1-14.dcm") == 14);
+  CHECK(extract_file_number("1-01.dcm") == 1);
+  CHECK(extract_file_number("a-b-7.dcm") == 7);
+  CHECK(extract_file_number("junk.dcm") == 1000);  // no '-': parse failure → 1000
+  CHECK(extract_file_number("1-.dcm") == 1000);
+  CHECK(extract_file_number("1-x2.dcm") == 1000);
+}
+
+TEST(path_helpers) {
+  using namespace nm03::cohort;
+  CHECK(with_slash("a/b") == "a/b/");
+  CHECK(with_slash("a/b/") == "a/b/");
+  CHECK(stem("/x/y/1-14.dcm") == "1-14");
+  CHECK(filename("/x/y/1-14.dcm") == "1-14.dcm");
+  CHECK(cohort_dir("/d/").find("Brain-Tumor-Progression/T1-Post-Combined-P001-P020") != std::string::npos);
+}
+
+TEST(patient_discovery_sorted_and_filtered) {
+  using namespace nm03::cohort;
+  const std::string root = tmpdir() + "/cohort/";
+  for (const char* p : {"PGBM-010", "PGBM-002", "OTHER-1", "PGBM-001"}) make_dirs(root + p + "/series-b");
+  make_dirs(root + "PGBM-001/series-a");
+  for (int k : {10, 2, 1}) {
+    nm03::dicom::WriteSpec ws;
+    std::vector<uint16_t> px(16, 7);
+    ws.rows = ws.cols = 4;
+    ws.pixels = px.data();
+    nm03::dicom::write_file(root + "PGBM-001/series-a/1-" + std::to_string(k) + ".dcm", ws);
+  }
+  const auto ids = find_patient_dirs(root);
+  CHECK(ids.size() == 3);
+  CHECK(ids.size() == 3 && ids[0] == "PGBM-001" && ids[1] == "PGBM-002" && ids[2] == "PGBM-010");
+  const Series s = list_patient_series(root, "PGBM-001");  // sorted series dirs: "series-a" first
+  CHECK(s.series_dir.find("series-a") != std::string::npos);
+  CHECK(s.files.size() == 3);
+  CHECK(s.files.size() == 3 && stem(s.files[0]) == "1-1" && stem(s.files[1]) == "1-2" && stem(s.files[2]) == "1-10");
+}
+
+// ---- DICOM ---------------------------------------------------------------------------------------
+std::vector<uint16_t> ramp(int n, uint32_t mul) {
+  std::vector<uint16_t> v(n);
+  for (int i = 0; i < n; ++i) v[i] = (uint16_t)(i * mul + 13);
+  return v;
+}
+
+TEST(dicom_round_trip_all_syntaxes) {
+  using namespace nm03::dicom;
+  for (Syntax sx : {Syntax::kExplicitLE, Syntax::kImplicitLE, Syntax::kExplicitBE}) {
+    const int rows = 33, cols = 47;
+    auto px = ramp(rows * cols, 977);
+    WriteSpec ws;
+    ws.rows = rows;
+    ws.cols = cols;
+    ws.pixels = px.data();
+    ws.syntax = sx;
+    ws.write_rescale = true;
+    ws.slope = 2.f;
+    ws.intercept = -5.f;
+    ws.spacing_x = 0.75f;
+    const auto bytes = write(ws);
+    const Header h = parse(bytes.data(), bytes.size());
+    CHECK(h.rows == rows && h.cols == cols && h.syntax == sx);
+    CHECK(h.slope == 2.f && h.intercept == -5.f && h.spacing_x == 0.75f);
+    std::vector<uint16_t> got(rows * cols);
+    copy_pixels16(h, bytes.data(), bytes.size(), got.data());
+    CHECK(got == px);
+  }
+}
+
+TEST(slice_file_modes_agree) {
+  using namespace nm03::dicom;
+  const int rows = 128, cols = 160;  // 40 KiB of pixels: larger than the 16 KiB prefix
+  auto px = ramp(rows * cols, 31337);
+  WriteSpec ws;
+  ws.rows = rows;
+  ws.cols = cols;
+  ws.pixels = px.data();
+  const std::string path = tmpdir() + "/slice.dcm";
+  write_file(path, ws);
+  struct Mode {
+    ReadMode m;
+    size_t prefix;
+  };
+  for (Mode md : {Mode{ReadMode::kDirect, 16384}, Mode{ReadMode::kDirect, 1024}, Mode{ReadMode::kStaged, 0}}) {
+    SliceFile f(path, md.m, md.prefix);
+    std::vector<uint8_t> scratch;
+    const Header& h = f.header(scratch);
+    CHECK(h.rows == rows && h.cols == cols);
+    std::vector<uint16_t> buf(rows * cols + 3, 0xABCD);
+    f.pixels16(buf.data() + 3);  // misaligned destination
+    CHECK(std::equal(px.begin(), px.end(), buf.begin() + 3));
+    CHECK(buf[0] == 0xABCD && buf[2] == 0xABCD);
+    CHECK(f.direct() == (md.m == ReadMode::kDirect));
+  }
+}
+
+TEST(stream_copy_edges) {
+  std::vector<uint8_t> src(5000), dst(5100);
+  for (size_t i = 0; i < src.size(); ++i) src[i] = (uint8_t)(i * 7 + 1);
+  for (size_t off : {0u, 1u, 7u, 15u, 16u, 33u})
+    for (size_t n : {0u, 1u, 15u, 63u, 64u, 65u, 1000u, 4999u}) {
+      std::fill(dst.begin(), dst.end(), 0);
+      nm03::dicom::stream_copy(dst.data() + off, src.data() + 1, n);
+      CHECK(std::equal(src.begin() + 1, src.begin() + 1 + n, dst.begin() + off));
+      CHECK(dst[off + n] == 0 && (off == 0 || dst[off - 1] == 0));
+    }
+}
+
+TEST(dicom_rejects_garbage) {
+  const std::string junk = "DICM-but-not-really";
+  bool threw = false;
+  try {
+    (void)nm03::dicom::parse(reinterpret_cast<const uint8_t*>(junk.data()), junk.size());
+  } catch (const std::exception&) {
+    threw = true;
+  }
+  CHECK(threw);
+}
+
+// ---- JPEG container ------------------------------------------------------------------------------
+TEST(jpeg_container) {
+  std::vector<uint8_t> img(64 * 48);
+  for (size_t i = 0; i < img.size(); ++i) img[i] = (uint8_t)(i % 251);
+  const auto j = nm03::jpeg::encode_gray420(img.data(), 64, 48, 64, 75);
+  CHECK(j.size() > 200 && j[0] == 0xFF && j[1] == 0xD8);                    // SOI
+  CHECK(j[j.size() - 2] == 0xFF && j[j.size() - 1] == 0xD9);                  // EOI
+  const auto t = nm03::jpeg::make_tables(75);
+  const auto hdr = nm03::jpeg::make_header(64, 48, t);
+  CHECK(hdr.size() < j.size() && std::equal(hdr.begin(), hdr.end(), j.begin()));
+  // the scan never contains an unstuffed 0xFF followed by a non-zero, non-RST byte
+  bool ok = true;
+  for (size_t i = hdr.size(); i + 2 < j.size(); ++i)
+    if (j[i] == 0xFF && j[i + 1] != 0x00) ok = false;
+  CHECK(ok);
+}
+
+// ---- golden operators vs brute-force definitions --------------------------------------------------
+TEST(golden_median_brute_force) {
+  const int w = 23, h = 17;
+  std::mt19937 rng(3);
+  std::vector<float> img(w * h);
+  for (auto& v : img) v = (float)(rng() % 1000);
+  for (int k : {3, 5, 7}) {
+    const auto m = nm03::golden::median(img, w, h, k);
+    bool ok = true;
+    for (int y = 0; y < h; ++y)
+      for (int x = 0; x < w; ++x) {
+        std::vector<float> win;
+        for (int dy = -k / 2; dy <= k / 2; ++dy)
+          for (int dx = -k / 2; dx <= k / 2; ++dx)
+            win.push_back(img[std::clamp(y + dy, 0, h - 1) * w + std::clamp(x + dx, 0, w - 1)]);
+        std::nth_element(win.begin(), win.begin() + win.size() / 2, win.end());
+        ok &= m[y * w + x] == win[win.size() / 2];
+      }
+    CHECK(ok);
+  }
+}
+
+std::vector<uint8_t> bfs_grow(const std::vector<uint8_t>& band, int w, int h, const std::vector<nm03::Seed>& seeds,
+                              int conn) {
+  std::vector<uint8_t> r(w * h, 0);
+  std::queue<std::pair<int, int>> q;
+  for (const auto& s : seeds)
+    if (s.x >= 0 && s.y >= 0 && s.x < w && s.y < h && band[s.y * w + s.x] && !r[s.y * w + s.x]) {
+      r[s.y * w + s.x] = 1;
+      q.push({s.x, s.y});
+    }
+  while (!q.empty()) {
+    auto [x, y] = q.front();
+    q.pop();
+    for (int dy = -1; dy <= 1; ++dy)
+      for (int dx = -1; dx <= 1; ++dx) {
+        if ((dx == 0 && dy == 0) || (conn == 4 && dx != 0 && dy != 0)) continue;
+        const int nx = x + dx, ny = y + dy;
+        if (nx < 0 || ny < 0 || nx >= w || ny >= h || !band[ny * w + nx] || r[ny * w + nx]) continue;
+        r[ny * w + nx] = 1;
+        q.push({nx, ny});
+      }
+  }
+  return r;
+}
+
+TEST(golden_region_grow_vs_bfs) {
+  const int w = 61, h = 45;
+  std::mt19937 rng(9);
+  std::vector<uint8_t> band(w * h);
+  for (auto& b : band) b = (rng() % 100) < 58;
+  const auto seeds = nm03::reference_seeds(w, h);
+  for (int conn : {4, 8}) CHECK(nm03::golden::region_grow(band, w, h, seeds, conn) == bfs_grow(band, w, h, seeds, conn));
+}
+
+TEST(golden_morphology_brute_force) {
+  const int w = 29, h = 21;
+  std::mt19937 rng(4);
+  std::vector<uint8_t> m(w * h);
+  for (auto& b : m) b = (rng() % 100) < 30;
+  for (int size : {3, 5}) {
+    const auto d = nm03::golden::dilate(m, w, h, size), e = nm03::golden::erode(m, w, h, size);
+    bool ok = true;
+    const int r = size / 2;
+    for (int y = 0; y < h; ++y)
+      for (int x = 0; x < w; ++x) {
+        int any = 0, all = 1;
+        for (int dy = -r; dy <= r; ++dy)
+          for (int dx = -r; dx <= r; ++dx) {
+            const int nx = x + dx, ny = y + dy;
+            if (nx < 0 || ny < 0 || nx >= w || ny >= h) continue;  // out-of-image samples ignored
+            any |= m[ny * w + nx];
+            all &= m[ny * w + nx];
+          }
+        ok &= d[y * w + x] == any && e[y * w + x] == all;
+      }
+    CHECK(ok);
+  }
+}
+
+TEST(reference_seed_pattern) {
+  // centre ± (W/8, H/8) + grid x, y ∈ [W/4, 3W/4) step W/10 (main_sequential.cpp:214-241)
+  const auto s = nm03::reference_seeds(256, 256);
+  CHECK(s.size() == 41);
+  std::set<std::pair<int, int>> uniq;
+  for (const auto& p : s) {
+    CHECK(p.x >= 0 && p.x < 256 && p.y >= 0 && p.y < 256);
+    uniq.insert({p.x, p.y});
+  }
+  CHECK(uniq.count({128, 128}) == 1);
+  CHECK(!nm03::reference_seeds(8, 8).empty());  // step clamped ≥ 1: no infinite loop below 10 px
+}
+
+// ---- host runtime ----------------------------------------------------------------------------------
+TEST(thread_pool_for_each_exactly_once) {
+  nm03::ThreadPool pool(4);
+  for (size_t n : {0u, 1u, 3u, 100u, 1000u}) {
+    std::vector<std::atomic<int>> hits(n);
+    nm03::TaskGroup tg(pool);
+    tg.for_each(n, [&](size_t i) { hits[i].fetch_add(1); }, 5);
+    tg.wait();
+    bool ok = true;
+    for (auto& h : hits) ok &= h.load() == 1;
+    CHECK(ok);
+  }
+}
+
+TEST(thread_pool_priorities_order_a_single_worker) {
+  nm03::ThreadPool pool(1);
+  std::vector<int> order;
+  std::mutex m;
+  std::atomic<bool> go{false};
+  nm03::TaskGroup tg(pool);
+  tg.run([&] { while (!go.load()) std::this_thread::yield(); }, 0);  // hold the worker
+  for (int p : {5, 1, 3, 1, 0}) tg.run([&, p] { std::lock_guard<std::mutex> g(m); order.push_back(p); }, (uint64_t)p);
+  go = true;
+  tg.wait();
+  CHECK((order == std::vector<int>{0, 1, 1, 3, 5}));
+}
+
+TEST(loopback_collectives) {
+  for (int n : {1, 2, 4}) {
+    auto group = nm03::make_loopback_group(n);
+    std::vector<std::thread> th;
+    std::atomic<int> bad{0};
+    for (int r = 0; r < n; ++r)
+      th.emplace_back([&, r] {
+        nm03::Comm& c = *group[r];
+        std::vector<uint8_t> b = r == 0 ? std::vector<uint8_t>{1, 2, 3} : std::vector<uint8_t>{};
+        c.broadcast_bytes(b, 0);
+        if (b != std::vector<uint8_t>{1, 2, 3}) ++bad;
+        const auto all = c.allgather_bytes(std::vector<uint8_t>(r + 1, (uint8_t)r));
+        for (int k = 0; k < n; ++k)
+          if (all[k] != std::vector<uint8_t>(k + 1, (uint8_t)k)) ++bad;
+        int64_t s = r + 1;
+        c.allreduce_sum_i64(&s, 1);
+        if (s != (int64_t)n * (n + 1) / 2) ++bad;
+        double mx = r * 1.5;
+        c.allreduce_max_f64(&mx, 1);
+        if (mx != (n - 1) * 1.5) ++bad;
+        c.barrier();
+      });
+    for (auto& t : th) t.join();
+    CHECK(bad.load() == 0);
+  }
+}
+
+TEST(wire_format_round_trip) {
+  nm03::ByteWriter w;
+  w.u32(0xDEADBEEF);
+  w.i32(-7);
+  w.u64(0x0123456789ABCDEFull);
+  w.f64(-2.5);
+  w.str("PGBM-017/1-14.dcm");
+  w.str("");
+  nm03::ByteReader r(w.b.data(), w.b.size());
+  CHECK(r.u32() == 0xDEADBEEF);
+  CHECK(r.i32() == -7);
+  CHECK(r.u64() == 0x0123456789ABCDEFull);
+  CHECK(r.f64() == -2.5);
+  CHECK(r.str() == "PGBM-017/1-14.dcm");
+  CHECK(r.str().empty());
+  CHECK(r.pos == w.b.size());
+}
+
+TEST(numa_cpulist) {
+  using nm03::numa::parse_cpulist;
+  CHECK((parse_cpulist("0-3,8,10-11") == std::vector<int>{0, 1, 2, 3, 8, 10, 11}));
+  CHECK(parse_cpulist("").empty());
+  CHECK((parse_cpulist("5") == std::vector<int>{5}));
+}
+
+TEST(cli_defaults_are_reference_literals) {
+  char prog[] = "img_processing_parallel";
+  char* argv[] = {prog, nullptr};
+  const nm03::app::AppConfig c = nm03::app::parse_args(1, argv, "parallel");
+  const nm03::PipelineParams& p = c.engine.pipe;
+  CHECK(c.engine.batch_size == 25 && c.engine.threads == 16);                       // main_parallel.cpp:33,401
+  CHECK(p.median_window == 7 && p.sharpen_mask == 9 && p.sharpen_gain == 2.0f);     // :204-210
+  CHECK(p.srg_min == 0.74f && p.srg_max == 0.91f && p.dilation_size == 3);          // :232-252
+  CHECK(p.norm_low == 0.5f && p.norm_high == 2.5f && p.clip_min == 0.68f && p.clip_max == 4000.0f);
+  CHECK(c.out_dir.find("out-parallel") != std::string::npos);
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  const std::string filter = argc > 1 ? argv[1] : "";
+  int run = 0;
+  for (const Test& t : registry()) {
+    if (!filter.empty() && std::string(t.name).find(filter) == std::string::npos) continue;
+    g_test = t.name;
+    const int before = g_failed;
+    try {
+      t.fn();
+    } catch (const std::exception& e) {
+      ++g_failed;
+      std::fprintf(stderr, "FAIL [%s] exception: %s\n", t.name, e.what());
+    }
+    std::printf("%s %s\n", g_failed == before ? "ok  " : "FAIL", t.name);
+    ++run;
+  }
+  std::printf("%d tests, %d checks, %d failed\n", run, g_checks, g_failed);
+  std::string cleanup = "rm -rf " + tmpdir();
+  if (tmpdir().rfind("/tmp/nm03_unit_", 0) == 0) (void)std::system(cleanup.c_str());
+  return g_failed ? 1 : 0;
+}

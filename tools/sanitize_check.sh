@@ -1,7 +1,8 @@
 #!/bin/bash
 # Host sanitizer sweep (CPU): ASan+leaks, UBSan and TSan builds of the native code
 # (device code unaffected: -Xarch_host), each running the CPU paths — DICOM/JPEG codecs, golden
-# model, thread pool (cpu-reference = 8 threads), synthetic writer, MetaImage dumps.
+# model, thread pool (cpu-reference = 8 threads), synthetic writer, MetaImage dumps, and the native
+# unit tests (thread pool priorities, loopback collectives across threads, loader read paths).
 set -o pipefail
 cd "$(dirname "$0")/.."
 D=/tmp/nm03_sanitize_data
@@ -10,7 +11,8 @@ export ASAN_OPTIONS=detect_leaks=1 UBSAN_OPTIONS=print_stacktrace=1:halt_on_erro
 for s in address undefined thread; do
   python build.py --sanitize $s > /tmp/nm03_build_$s.log 2>&1 || { echo "$s: build failed"; exit 2; }
   B=build-$s/bin
-  timeout 600 $B/test_pipeline --cpu --data-root $D/ --out /tmp/nm03_san_$s/t --dump-mhd /tmp/nm03_san_$s/m > /tmp/nm03_san_$s.log 2>&1 &&
+  timeout 600 $B/nm03_unit_tests > /tmp/nm03_san_$s.log 2>&1 &&
+  timeout 600 $B/test_pipeline --cpu --data-root $D/ --out /tmp/nm03_san_$s/t --dump-mhd /tmp/nm03_san_$s/m >> /tmp/nm03_san_$s.log 2>&1 &&
   timeout 600 $B/nm03_bench --config cpu-reference --data-root $D/ --out /tmp/nm03_san_$s/c --steps 1 --warmup 0 --threads 8 >> /tmp/nm03_san_$s.log 2>&1 &&
   timeout 600 $B/nm03_synth --data-root /tmp/nm03_san_$s/synth/ --patients 2 --threads 4 >> /tmp/nm03_san_$s.log 2>&1
   rc=$?
