@@ -6,7 +6,9 @@
 //  1 jpeg_fused_kernel   workgroup per 256 luma blocks (64 MCUs) of an image, thread per block.
 //                        Pixels come from the canvas or — for an exact 2× fit, the common case —
 //                        are rendered on the fly from the 6×6 source patch (render_core.h), so the
-//                        256 KiB canvas never exists. islow FDCT (24-bit multiplies), quantisation
+//                        256 KiB canvas never exists. The workgroup first stages its source rows
+//                        in LDS (gray: rescaled f32, 18 × 258 for a 256² slice; labels: the label
+//                        and border bit rows) with coalesced loads: 76 → 67 µs per 64-slice batch. islow FDCT (24-bit multiplies), quantisation
 //                        by exact reciprocal (umulhi by ceil(2^32/d): exact for |x|, d < 2^16),
 //                        Huffman cost, workgroup scan, decoupled look-back over the image's
 //                        earlier workgroups, then the codes are ORed into the zeroed stage words.
@@ -71,6 +73,12 @@ __device__ __forceinline__ uint32_t sat_add(uint32_t a, uint32_t b) {
 constexpr int kJpegWG = 256;     // luma blocks (threads) per workgroup = 64 MCUs
 constexpr int kAsmWords = 2048;  // LDS assembly buffer for the workgroup's bit range (64 Kbit)
 
+// Gray source staging: the raw rows a workgroup's 64 MCUs read (8 per MCU row + a 1-row halo each
+// side, full width + 1-column halos, edge-clamped) are loaded once, coalesced, into LDS; the 6×6
+// patches of the exact-2× render then come from LDS instead of 36 scattered global loads per
+// block. Pixels are converted to f32 (rescale) once while staging, not once per patch use (2.25×).
+constexpr int kPatchLds = 4864;  // f32 elements (19 KiB; 256²: 18 × 258 = 4644); larger footprints use global loads
+
 constexpr int kPrivWords = 5;    // per-block Huffman bits kept in LDS (160 bits, odd stride) ...
 constexpr int kSpillWords = 56;  // ... the rest in the block's global spill slot (a block needs ≤ 1700)
 
@@ -131,6 +139,7 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(4))) vo
   __shared__ uint32_t sh[17];
   __shared__ uint32_t s_ticket, s_prefix;
   __shared__ int32_t s_prevdc;
+  __shared__ __attribute__((aligned(16))) float spatch[kPatchLds];
   const int tid = threadIdx.x;
   if (dbg == 8) {  // profiling variant: empty workgroup
     if (tid == 999) w.total[0] = 1u;
@@ -175,6 +184,78 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(4))) vo
   const int mcux = out_w >> 4;
   const int b = part * kJpegWG + tid;
   const bool valid = b < bpi;
+  // ---- 0. stage the source rows of this workgroup in LDS (workgroup-uniform decision) ----------
+  int ys0 = 0, pcols = 0;
+  bool staged = false, lstaged = false;
+  uint64_t* const slab = reinterpret_cast<uint64_t*>(spatch);  // label images reuse the area
+  if (d.render >= 0 && rd.kind == kRenderLabels && dbg != 12) {
+    // Label render rows: 4by .. 4by+3 for the workgroup's block rows → 8 per MCU row.
+    const int m0 = part * (kJpegWG / 4), m1 = min(m0 + kJpegWG / 4, bpi >> 2) - 1;
+    const int r0 = m0 / mcux, r1 = m1 / mcux;
+    const int nrows = 8 * (r1 - r0) + 8, wpr = rd.wpr, nw = nrows * wpr;
+    if (2 * nw * 2 <= kPatchLds) {  // two u64 planes in the f32 area
+      lstaged = true;
+      ys0 = 8 * r0;
+      pcols = nw;  // offset of the border plane
+      for (int i = tid; i < nw; i += kJpegWG) {
+        const int j = i / wpr, k = i - j * wpr;
+        const size_t wi = (size_t)clampi(ys0 + j, 0, rd.src_h - 1) * wpr + k;
+        slab[i] = rs.bits[rd.src_off + wi];
+        slab[nw + i] = rs.bits[rd.border_off + wi];
+      }
+      __syncthreads();
+    }
+  }
+  if (d.render >= 0 && rd.kind == kRenderRawGray && dbg != 12) {  // dbg 12: A/B with global loads
+    const int m0 = part * (kJpegWG / 4), m1 = min(m0 + kJpegWG / 4, bpi >> 2) - 1;
+    const int r0 = m0 / mcux, r1 = m1 / mcux;
+    const int nrows = 8 * (r1 - r0) + 10;
+    pcols = rd.src_w + 2;
+    if (nrows * pcols <= kPatchLds && !(rd.src_off & 1)) {
+      staged = true;
+      ys0 = 8 * r0 - 1;
+      const int W = rd.src_w, H = rd.src_h, hw = W >> 1;  // W is a multiple of 8 (exact 2× fit)
+      const uint16_t* src = rs.raw + rd.src_off;
+      // Interior: 4-byte loads of pixel pairs, all issued before the LDS stores (one latency).
+      const int nw = nrows * hw;
+      constexpr int kU = 12;  // ≥ 18 rows × 128 pairs / 256 threads for a 256² source: one round of loads
+      uint32_t v[kU];
+#pragma unroll
+      for (int t = 0; t < kU; ++t) {
+        const int i = tid + t * kJpegWG;
+        v[t] = 0u;
+        if (i < nw) {
+          const int j = i / hw, k = i - j * hw;
+          v[t] = *reinterpret_cast<const uint32_t*>(src + (size_t)clampi(ys0 + j, 0, H - 1) * W + 2 * k);
+        }
+      }
+      auto value = [&](uint16_t r) {
+        return rescaled_value(key_from_raw(r, rd.type, rd.stored_bits), rd.type, rd.slope, rd.intercept);
+      };
+#pragma unroll
+      for (int t = 0; t < kU; ++t) {
+        const int i = tid + t * kJpegWG;
+        if (i < nw) {
+          const int j = i / hw, k = i - j * hw;
+          spatch[j * pcols + 2 * k + 1] = value((uint16_t)(v[t] & 0xFFFFu));
+          spatch[j * pcols + 2 * k + 2] = value((uint16_t)(v[t] >> 16));
+        }
+      }
+      for (int i = tid + kU * kJpegWG; i < nw; i += kJpegWG) {  // larger footprints
+        const int j = i / hw, k = i - j * hw;
+        const uint32_t u = *reinterpret_cast<const uint32_t*>(src + (size_t)clampi(ys0 + j, 0, H - 1) * W + 2 * k);
+        spatch[j * pcols + 2 * k + 1] = value((uint16_t)(u & 0xFFFFu));
+        spatch[j * pcols + 2 * k + 2] = value((uint16_t)(u >> 16));
+      }
+      // Clamped halo columns 0 and W+1.
+      for (int i = tid; i < 2 * nrows; i += kJpegWG) {
+        const int j = i >> 1, right = i & 1;
+        spatch[j * pcols + (right ? W + 1 : 0)] =
+            value(src[(size_t)clampi(ys0 + j, 0, H - 1) * W + (right ? W - 1 : 0)]);
+      }
+      __syncthreads();
+    }
+  }
   // ---- 1+2. block → DCT → quantisation fused with the AC Huffman coding ------------------------
   // The coefficients never leave registers: the zig-zag walk is unrolled, each coefficient is
   // quantised and — if non-zero in some lane of the wave (else the position is skipped) — coded
@@ -191,8 +272,23 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(4))) vo
     if (dbg == 6) {  // profiling variant: no render
 #pragma unroll
       for (int i = 0; i < 64; ++i) blk[i] = (i * 7 + bx + by) & 255;
+    } else if (lstaged) {
+      const int wpr = rd.wpr;
+      render_labels_2x(rd, [&](int y, int k, uint64_t& lab, uint64_t& brd) {
+        const int i = (y - ys0) * wpr + k;
+        lab = slab[i];
+        brd = slab[pcols + i];
+      }, bx, by, blk);
+#pragma unroll
+      for (int i = 0; i < 64; ++i) blk[i] -= 128;
+    } else if (staged) {
+      // Patch element (j, i) = source (4by-1+j, 4bx-1+i) = LDS (4by-1+j-ys0, 4bx+i).
+      const float* pp = spatch + (4 * by - 1 - ys0) * pcols + 4 * bx;
+      render_patch_2x([&](int j, int i) { return pp[j * pcols + i]; }, win, blk);
+#pragma unroll
+      for (int i = 0; i < 64; ++i) blk[i] -= 128;
     } else if (d.render >= 0) {
-      render_block_2x(rd, rs.raw, rs.f32, rs.bits, win, bx, by, blk);
+      render_block_2x(rd, rs.raw, rs.f32, rs.bits, win, bx, by, blk, dbg == 11);
 #pragma unroll
       for (int i = 0; i < 64; ++i) blk[i] -= 128;
     } else {

@@ -70,27 +70,97 @@ __device__ __forceinline__ uint32_t render_pixel(const RenderDesc& d, const uint
 #endif
 constexpr bool kVecPatch = NM03_VEC_PATCH;  // 8-byte row loads measured slower (97 vs 93 us / batch)
 
+// Exact-2× bilinear interpolation + window of one 8×8 canvas block from its 6×6 source patch
+// (source rows 4by-1..4by+4, columns 4bx-1..4bx+4, edge-clamped; fetch(j, i) → f32 value) into
+// px[64]. The patch is a local array filled here so it stays in registers.
+template <class Fetch>
+__device__ __forceinline__ void render_patch_2x(Fetch&& fetch, RWindow win, int32_t* px) {
+  // Exact 2× fit: the source coordinate of canvas pixel k is 2b + k/2 - 0.25 (exact in f32), so
+  // the interpolation weight is 0.75 for even and 0.25 for odd k — the very values render_pixel
+  // computes — and floor(f) - (4b-1) == (k+1)/2 is a compile-time patch index.
+  // Columns are processed in pairs (2m, 2m+1) as float2 so the f32 multiplies and adds map to
+  // v_pk_mul_f32 / v_pk_add_f32; every element goes through exactly bilerp()'s and gray_u8()'s
+  // operation sequence (no contraction), so results are bit-identical to the scalar contract.
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  const f2 wx2 = {0.75f, 0.25f}, ix2 = {1.0f - 0.75f, 1.0f - 0.25f};
+  // Horizontal lerps of patch row j at canvas columns (2m, 2m+1). Output row r blends rows
+  // j0 = (r+1)/2 and j0+1, so a sliding window of two lerp rows suffices (low register pressure;
+  // the rows are produced in the same order and with the same operations as a full table).
+  auto hrow = [&](int j, f2 (&h)[4]) {
+    float row[6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) row[i] = fetch(j, i);
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const f2 a = {row[m], row[m + 1]}, bb = {row[m + 1], row[m + 2]};
+      const f2 t0 = ix2 * a;
+      const f2 t1 = wx2 * bb;
+      h[m] = t0 + t1;
+    }
+  };
+  f2 h0[4], h1[4];
+  hrow(0, h0);
+  hrow(1, h1);
+  const f2 lo2 = {win.lo, win.lo}, inv2 = {win.inv, win.inv};
+#pragma unroll
+  for (int r = 0; r < 8; ++r) {
+    if (r & 1) {  // j0 = (r+1)/2 advances on odd rows
+#pragma unroll
+      for (int m = 0; m < 4; ++m) h0[m] = h1[m];
+      hrow(((r + 1) >> 1) + 1, h1);
+    }
+    const float wy = (r & 1) ? 0.25f : 0.75f, iy = 1.0f - wy;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const f2 u0 = iy * h0[m];
+      const f2 u1 = wy * h1[m];
+      const f2 val = u0 + u1;
+      f2 g = val - lo2;
+      g = g * inv2;
+      g.x = g.x < 0.0f ? 0.0f : (g.x > 1.0f ? 1.0f : g.x);
+      g.y = g.y < 0.0f ? 0.0f : (g.y > 1.0f ? 1.0f : g.y);
+      f2 t = g * 255.0f;
+      t = t + 0.5f;
+      px[r * 8 + 2 * m] = (int32_t)(uint8_t)(int)t.x;
+      px[r * 8 + 2 * m + 1] = (int32_t)(uint8_t)(int)t.y;
+    }
+  }
+}
+
+// Exact-2× label render of the 8×8 canvas block (bx, by): canvas columns 8bx..8bx+7 map to source
+// columns 4bx..4bx+3, always inside one 64-bit word k = 4bx/64 of the label and border rows;
+// words(y, k, lab, brd) returns word k of source row y (edge-clamped row index).
+template <class Words>
+__device__ __forceinline__ void render_labels_2x(const RenderDesc& d, Words&& words, int bx, int by, int32_t* px) {
+  const int W = d.src_w, H = d.src_h;
+#pragma unroll
+  for (int r = 0; r < 8; ++r) {
+    const float sy = render_src_coord(by * 8 + r, d.oy, d.invy);
+    const int y = clampi((int)floorf(sy), 0, H - 1);
+    uint64_t lab, brd;
+    words(y, (4 * bx) >> 6, lab, brd);
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const float sx = render_src_coord(bx * 8 + c, d.ox, d.invx);
+      const int x = clampi((int)floorf(sx), 0, W - 1);
+      const uint64_t bit = 1ull << (x & 63);
+      px[r * 8 + c] = (brd & bit) ? (int32_t)d.border_value : ((lab & bit) ? (int32_t)d.fill : 0);
+    }
+  }
+}
+
 // Fused 2× render of the 8×8 canvas block (bx, by) into px[64] (row-major), for a RenderDesc
 // with render_is_exact_2x(): the block's source footprint is a 6×6 patch (gray) or 4×4 (labels).
 __device__ __forceinline__ void render_block_2x(const RenderDesc& d, const uint16_t* raw, const float* f32,
-                                                const uint64_t* bits, RWindow win, int bx, int by, int32_t* px) {
+                                                const uint64_t* bits, RWindow win, int bx, int by, int32_t* px,
+                                                bool synth_src = false) {
   const int W = d.src_w, H = d.src_h;
   if (d.kind == kRenderLabels) {
-    // Canvas columns 8bx..8bx+7 map to source columns 4bx..4bx+3: always inside one 64-bit word.
-#pragma unroll
-    for (int r = 0; r < 8; ++r) {
-      const float sy = render_src_coord(by * 8 + r, d.oy, d.invy);
-      const int y = clampi((int)floorf(sy), 0, H - 1);
-      const size_t wi = (size_t)y * d.wpr + ((4 * bx) >> 6);
-      const uint64_t lab = bits[d.src_off + wi], brd = bits[d.border_off + wi];
-#pragma unroll
-      for (int c = 0; c < 8; ++c) {
-        const float sx = render_src_coord(bx * 8 + c, d.ox, d.invx);
-        const int x = clampi((int)floorf(sx), 0, W - 1);
-        const uint64_t bit = 1ull << (x & 63);
-        px[r * 8 + c] = (brd & bit) ? (int32_t)d.border_value : ((lab & bit) ? (int32_t)d.fill : 0);
-      }
-    }
+    render_labels_2x(d, [&](int y, int k, uint64_t& lab, uint64_t& brd) {
+      const size_t wi = (size_t)y * d.wpr + k;
+      lab = bits[d.src_off + wi];
+      brd = bits[d.border_off + wi];
+    }, bx, by, px);
     return;
   }
   const int sx0 = 4 * bx - 1, sy0 = 4 * by - 1;
@@ -111,6 +181,11 @@ __device__ __forceinline__ void render_block_2x(const RenderDesc& d, const uint1
         patch[j][i] = rescaled_value(key_from_raw(r, d.type, d.stored_bits), d.type, d.slope, d.intercept);
       }
     }
+  } else if (synth_src) {  // profiling variant (NM03_JPEG_DBG=11): same math, no source loads
+#pragma unroll
+    for (int j = 0; j < 6; ++j)
+#pragma unroll
+      for (int i = 0; i < 6; ++i) patch[j][i] = (float)((sx0 + i) * 3 + (sy0 + j) * 5) * win.inv;
   } else {
 #pragma unroll
     for (int j = 0; j < 6; ++j) {
@@ -119,44 +194,7 @@ __device__ __forceinline__ void render_block_2x(const RenderDesc& d, const uint1
       for (int i = 0; i < 6; ++i) patch[j][i] = render_src_value(d, raw, f32, clampi(sx0 + i, 0, W - 1), y);
     }
   }
-  // Exact 2× fit: the source coordinate of canvas pixel k is 2b + k/2 - 0.25 (exact in f32), so
-  // the interpolation weight is 0.75 for even and 0.25 for odd k — the very values render_pixel
-  // computes — and floor(f) - (4b-1) == (k+1)/2 is a compile-time patch index.
-  // Columns are processed in pairs (2m, 2m+1) as float2 so the f32 multiplies and adds map to
-  // v_pk_mul_f32 / v_pk_add_f32; every element goes through exactly bilerp()'s and gray_u8()'s
-  // operation sequence (no contraction), so results are bit-identical to the scalar contract.
-  typedef float f2 __attribute__((ext_vector_type(2)));
-  const f2 wx2 = {0.75f, 0.25f}, ix2 = {1.0f - 0.75f, 1.0f - 0.25f};
-  f2 hl[6][4];  // horizontal lerps: row j of the patch at canvas columns (2m, 2m+1)
-#pragma unroll
-  for (int j = 0; j < 6; ++j)
-#pragma unroll
-    for (int m = 0; m < 4; ++m) {
-      const f2 a = {patch[j][m], patch[j][m + 1]}, bb = {patch[j][m + 1], patch[j][m + 2]};
-      const f2 t0 = ix2 * a;
-      const f2 t1 = wx2 * bb;
-      hl[j][m] = t0 + t1;
-    }
-  const f2 lo2 = {win.lo, win.lo}, inv2 = {win.inv, win.inv};
-#pragma unroll
-  for (int r = 0; r < 8; ++r) {
-    const int j0 = (r + 1) >> 1;
-    const float wy = (r & 1) ? 0.25f : 0.75f, iy = 1.0f - wy;
-#pragma unroll
-    for (int m = 0; m < 4; ++m) {
-      const f2 u0 = iy * hl[j0][m];
-      const f2 u1 = wy * hl[j0 + 1][m];
-      const f2 val = u0 + u1;
-      f2 g = val - lo2;
-      g = g * inv2;
-      g.x = g.x < 0.0f ? 0.0f : (g.x > 1.0f ? 1.0f : g.x);
-      g.y = g.y < 0.0f ? 0.0f : (g.y > 1.0f ? 1.0f : g.y);
-      f2 t = g * 255.0f;
-      t = t + 0.5f;
-      px[r * 8 + 2 * m] = (int32_t)(uint8_t)(int)t.x;
-      px[r * 8 + 2 * m + 1] = (int32_t)(uint8_t)(int)t.y;
-    }
-  }
+  render_patch_2x([&](int j, int i) { return patch[j][i]; }, win, px);
 }
 
 }  // namespace nm03::gpu
