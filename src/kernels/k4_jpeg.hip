@@ -8,8 +8,9 @@
 //                        are rendered on the fly from the 6×6 source patch (render_core.h), so the
 //                        256 KiB canvas never exists. The workgroup first stages its source rows
 //                        in LDS (gray: rescaled f32, 18 × 258 for a 256² slice; labels: the label
-//                        and border bit rows) with coalesced loads: 76 → 67 µs per 64-slice batch. islow FDCT (24-bit multiplies), quantisation
-//                        by exact reciprocal (umulhi by ceil(2^32/d): exact for |x|, d < 2^16),
+//                        and border bit rows) with coalesced loads: 76 → 67 µs per 64-slice batch.
+//                        islow FDCT (24-bit multiplies), quantisation by exact reciprocal (umulhi
+//                        by ceil(2^32/d): exact for |x|, d < 2^16),
 //                        Huffman cost, workgroup scan, decoupled look-back over the image's
 //                        earlier workgroups, then the codes are ORed into the zeroed stage words.
 //  2 jpeg_stuff_*        grid-stride over (chunk, image) 4 KiB chunks, chunk-major: count 0xFF
