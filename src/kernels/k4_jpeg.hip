@@ -390,18 +390,27 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(4))) vo
   uint32_t agg = 0;
   const uint32_t excl = block_exclusive_scan(bits, sh, &agg);  // ends with a barrier
   uint64_t* look = w.look + (size_t)img * parts;
-  if (tid == 0) {
+  if (tid < 64) {
+    // Wave 0 looks back through a window of 64 predecessors per round trip: lane l reads the
+    // status of part (hi - l); the nearest inclusive prefix ends the window and the aggregates up
+    // to it are summed across the wave. (A serial walk costs one device-scope load latency per
+    // predecessor — the critical path of images whose parts all run concurrently.)
+    const int lane = tid;
     uint32_t prefix = 0;
     if (part == 0 || dbg == 4) {  // dbg 4: profiling variant without the look-back wait
-      look_store(&look[part], 2u, agg);
+      if (lane == 0) look_store(&look[part], 2u, agg);
     } else {
-      look_store(&look[part], 1u, agg);
-      int p = part - 1;
+      if (lane == 0) look_store(&look[part], 1u, agg);
+      int hi = part - 1;
       uint32_t spins = 0;
-      while (p >= 0) {
-        const uint64_t st = look_load(&look[p]);
-        const uint32_t hi = (uint32_t)(st >> 32);
-        if (hi == 0u) {
+      for (;;) {
+        const int p = hi - lane;
+        const uint64_t st = p >= 0 ? look_load(&look[p]) : (2ull << 32);  // before part 0: inclusive 0
+        const uint32_t state = (uint32_t)(st >> 32);
+        const uint64_t incl = __ballot(state == 2u);
+        const int stop = incl ? __builtin_ctzll(incl) : 64;  // nearest inclusive prefix
+        const uint64_t need = stop >= 63 ? ~0ull : ((2ull << stop) - 1ull);
+        if (__ballot(state == 0u) & need) {  // a needed predecessor has not published yet
           if (++spins > (1u << 26)) {  // cannot happen with ordered tickets; never hang the GPU
             prefix = 0xFFFFFFFFu;
             break;
@@ -409,13 +418,21 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(4))) vo
           __builtin_amdgcn_s_sleep(1);
           continue;
         }
-        prefix = sat_add(prefix, (uint32_t)st);
-        if (hi == 2u) break;
-        --p;
+        uint32_t lo32 = lane <= stop ? (uint32_t)st : 0u, hi32 = 0u;  // 64-bit wave sum
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+          const uint32_t l2 = __shfl_xor(lo32, o, 64), h2 = __shfl_xor(hi32, o, 64);
+          const uint32_t s = lo32 + l2;
+          hi32 += h2 + (s < lo32 ? 1u : 0u);
+          lo32 = s;
+        }
+        prefix = sat_add(prefix, hi32 ? 0xFFFFFFFFu : lo32);
+        if (stop < 64) break;
+        hi -= 64;
       }
-      look_store(&look[part], 2u, sat_add(prefix, agg));
+      if (lane == 0) look_store(&look[part], 2u, sat_add(prefix, agg));
     }
-    s_prefix = prefix;
+    if (lane == 0) s_prefix = prefix;
   }
   // Meanwhile: assemble the workgroup's contiguous bit range in LDS: each block's DC code, then
   // its AC words shifted behind it.
