@@ -658,6 +658,7 @@ struct Engine::Impl {
       s.loads_finished = 0;
     }
     std::atomic<int64_t> load_ns{0}, bytes_in{0}, write_ns{0}, bytes_out{0}, load_cpu_ns{0}, write_cpu_ns{0};
+    std::string upload_error;
     {
       TaskGroup tg(*pool);
       tg.for_each(
@@ -678,7 +679,15 @@ struct Engine::Impl {
             }
           },
           2 * batch);
-      if (upload_chunk_) upload_progress(s, count);
+      if (upload_chunk_) {
+        // A failed early upload fails the batch like any device error (below), not the run; the
+        // loads still finish (tg.wait) before the blob is touched again.
+        try {
+          upload_progress(s, count);
+        } catch (const std::exception& e) {
+          upload_error = e.what();
+        }
+      }
       tg.wait();
     }
     s.live.clear();
@@ -691,6 +700,7 @@ struct Engine::Impl {
     if (!s.live.empty()) {
       try {
         TraceRange tr("nm03.gpu_batch");
+        if (!upload_error.empty()) throw DeviceError(upload_error);
         if (fault_plan().fail_batch == (int64_t)batch)
           throw DeviceError("injected fault: device batch failure");
         build_and_run(s, 0, &local);
