@@ -301,8 +301,10 @@ int parallel_rank(const AppConfig& cfg, int rank, int size, Comm& comm) {
   const std::string base = cohort::cohort_dir(cfg.data_root);
   EngineConfig ec = cfg.engine;
   if (size > 1) ec.device = rank;
+  const double t_setup = now_s();
   Engine engine(ec);
   const double t_start = now_s();
+  const double setup_s = t_start - t_setup;
   double proc_wall = 0;
   int64_t total_ok = 0, total_slices = 0;
   StageTimes agg;
@@ -446,7 +448,8 @@ int parallel_rank(const AppConfig& cfg, int rank, int size, Comm& comm) {
   comm.allreduce_max_f64(&tot, 1);
   if (rank == 0) {
     write_json(cfg.json, std::string("{\"mode\": \"parallel\", \"gpus\": ") + std::to_string(size) + ", \"backend\": \"" +
-                             comm.backend() + "\", \"repeat\": " + std::to_string(cfg.repeat) + ", \"wall_s\": " + fmt(tot) +
+                             comm.backend() + "\", \"repeat\": " + std::to_string(cfg.repeat) + ", \"engine_setup_s\": " +
+                             fmt(setup_s) + ", \"wall_s\": " + fmt(tot) +
                              ", \"processing_wall_s\": " + fmt(proc_wall) + ", \"slices\": " + std::to_string(total_slices) +
                              ", \"slices_ok\": " + std::to_string(total_ok) + ", \"slices_per_s\": " +
                              fmt(total_ok / std::max(proc_wall, 1e-9)) + ", \"rank0\": {\"load_s\": " + fmt(agg.load_s) +

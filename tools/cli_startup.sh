@@ -1,0 +1,36 @@
+#!/bin/bash
+# (gpurun) where the CLI wall clock goes: bare HIP runtime init, then img_processing_parallel on the
+# full cohort (wall vs engine set-up vs processing from --json), 4 runs each.
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+O=gpurun_out/cli_startup.txt
+: > $O
+D=/dev/shm/nm03_cli_data
+build/bin/nm03_synth --data-root $D/ --threads 16 > /dev/null || exit 1
+for r in 1 2 3 4; do
+  python3 - >> $O <<'PY' || exit 2
+import ctypes, time
+t0 = time.perf_counter()
+lib = ctypes.CDLL("libamdhip64.so")
+t1 = time.perf_counter()
+n = ctypes.c_int()
+lib.hipGetDeviceCount(ctypes.byref(n))
+lib.hipSetDevice(0)
+p = ctypes.c_void_p()
+lib.hipMalloc(ctypes.byref(p), 1 << 20)
+lib.hipDeviceSynchronize()
+t2 = time.perf_counter()
+print(f"hip: dlopen {1e3*(t1-t0):.1f} ms, init+first malloc {1e3*(t2-t1):.1f} ms")
+PY
+done
+for r in 1 2 3; do
+  for extra in "" "--max-dim 256" "--max-dim 256 --streams 1"; do
+    s=$(date +%s.%N)
+    (cd /tmp && timeout -k 10 60 $GRAFT_REPO_ROOT/build/bin/img_processing_parallel --data-root $D/ --out /dev/shm/nm03_cli_out --json /tmp/cli.json --quiet $extra > /dev/null 2>&1) || exit 3
+    e=$(date +%s.%N)
+    echo "[$extra] cli wall $(python3 -c "print(round(($e-$s)*1e3,1))") ms; $(cut -c1-190 /tmp/cli.json)" >> $O
+  done
+done
+rm -rf $D /dev/shm/nm03_cli_out
