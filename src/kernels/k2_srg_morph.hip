@@ -24,8 +24,17 @@
 
 namespace nm03::gpu {
 
+// Threads per slice workgroup. Row/column fills use one thread per row (≤ 512), the 64×64 bit
+// transposes and morphology passes spread over every wave. A batch has only one workgroup per
+// slice, so per-workgroup latency is the cost: 256 → 512 → 1024 threads measured 32.4 → 24.9 →
+// 23.1 µs per 64-slice batch (isolated, tools/gpu_kprof.sh).
+#ifndef NM03_SRG_THREADS
+#define NM03_SRG_THREADS 1024
+#endif
+constexpr int kSrgThreads = NM03_SRG_THREADS;
 
-__global__ __launch_bounds__(256) void srg_morph_kernel(const uint64_t* __restrict__ band,
+
+__global__ __launch_bounds__(kSrgThreads) void srg_morph_kernel(const uint64_t* __restrict__ band,
                                                         const SliceDesc* __restrict__ descs,
                                                         const SeedXY* __restrict__ seeds, PipeConsts pc,
                                                         SrgOutputs out, int plane_words) {
@@ -94,7 +103,7 @@ void launch_srg_morph(const uint64_t* band, const SliceDesc* descs, int nslices,
   if (max_w * hb > plane_words) plane_words = max_w * hb;
   plane_words = (plane_words + 1) & ~1;
   const size_t lds = (size_t)plane_words * 4 * sizeof(uint64_t);
-  srg_morph_kernel<<<nslices, 256, lds, stream>>>(band, descs, seeds, pc, out, plane_words);
+  srg_morph_kernel<<<nslices, kSrgThreads, lds, stream>>>(band, descs, seeds, pc, out, plane_words);
   check_launch("srg_morph_kernel");
 }
 
