@@ -26,6 +26,14 @@ class VolumePipeline:
             runner = self._runners[dev] = native().VolumeRunner(dev)
         return runner.run(vol, self.config.pipeline_params(), self.connectivity, self.dilation, s)
 
+    def run_slabs(self, volume=None, ctx=None, seeds=None, band=None, backend="auto", gather=True):
+        """The same pipeline on a volume split into z-slabs over the ranks of `ctx` (one process per
+        GPU, torch.distributed; parallel/volume_slabs.py). Returns the masks of the whole volume on
+        every rank with gather=True, else this rank's slab."""
+        from ..parallel.volume_slabs import run_volume_slabs
+        return run_volume_slabs(volume=volume, ctx=ctx, config=self.config, connectivity=self.connectivity,
+                                dilation=self.dilation, seeds=seeds, band=band, backend=backend, gather=gather)
+
     def golden(self, band, seeds):
         n = native()
         region = n.golden_region_grow3d(band, list(seeds), self.connectivity)

@@ -89,3 +89,14 @@ def test_single_rank_matches_golden(native):
     assert np.array_equal(r["region"].numpy().astype(np.uint8), ref)
     assert np.array_equal(r["dilated"].numpy().astype(np.uint8), native.golden_dilate3d(ref, 7))
     assert r["rounds"] == 1 and r["z0"] == 0
+
+
+def test_volume_pipeline_run_slabs_cpu(native):
+    """VolumePipeline.run_slabs (single process, golden backend) == golden 3D region growing + dilation."""
+    import nm03_capstone_project_amd as nm
+    band, seeds = _volumes()["random"]
+    vp = nm.VolumePipeline(connectivity=26, dilation=5)
+    r = vp.run_slabs(band=band, seeds=seeds, backend="cpu")
+    ref = native.golden_region_grow3d(band, seeds, 26)
+    assert np.array_equal(r["region"].numpy().astype(np.uint8), ref)
+    assert np.array_equal(r["dilated"].numpy().astype(np.uint8), native.golden_dilate3d(ref, 5))
