@@ -74,6 +74,9 @@ class SliceFile {
   void pixels16(uint16_t* dst);
   // True when pixels16 reads straight from the file (prefix parse, LE 16-bit data).
   bool direct() const { return !whole_; }
+  // Staged reads of little-endian 16-bit data: the first frame's samples inside the caller's
+  // scratch buffer (valid until it is reused), else nullptr.
+  const uint16_t* staged_samples() const;
 
  private:
   void pread_all(void* dst, size_t n, size_t off);

@@ -28,8 +28,11 @@ struct SliceDesc {
   uint16_t flags;
   uint32_t f32_off;    // f32 element offset for optional sharpened output
   uint32_t med_tile0;  // index of the slice's first median tile in the batch tile list
+  uint32_t blob_off;   // u16 element offset of the slice as uploaded (engine batches: K0 expands it to raw_off)
 };
-static_assert(sizeof(SliceDesc) == 40, "SliceDesc layout");
+static_assert(sizeof(SliceDesc) == 44, "SliceDesc layout");
+// SliceDesc::flags
+inline constexpr uint16_t kSliceFlagPacked12 = 1;  // uploaded as 12-bit pairs (nm03/pack12.h)
 
 struct TileDesc {
   uint32_t slice;

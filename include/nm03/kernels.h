@@ -92,6 +92,11 @@ void launch_jpeg(const uint8_t* canvas, const JpegDesc* jd, int ncanvas, int out
                  const JpegRenderSrc* fused = nullptr);
 // K6: binary threshold lo ≤ x ≤ hi → u8 0/1 (in 16-byte aligned, out 4-byte aligned).
 void launch_threshold(const float* in, uint8_t* out, size_t n, float lo, float hi, hipStream_t stream);
+
+// K0: expand a batch's uploaded raw region (12-bit packed or plain 16-bit slices, SliceDesc::blob_off
+// and flags) into the 16-bit sample buffer at SliceDesc::raw_off.
+void launch_unpack(const uint16_t* blob_raw, uint16_t* raw, const SliceDesc* descs, int nslices, int max_pixels,
+                   hipStream_t stream);
 // True when RenderDesc r is an exact 2× fit onto the canvas (the fused fast path applies).
 bool render_is_exact_2x(const RenderDesc& r, int out_w, int out_h);
 

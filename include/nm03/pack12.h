@@ -1,0 +1,30 @@
+// nm03/pack12.h — 12-bit transfer packing of 16-bit samples for the host→device upload.
+//
+// MR series store 12-bit samples in 16-bit words (BitsStored = 12 on typical T1 acquisitions); the
+// raw pixels are the one large PCIe transfer of the pipeline (128 KiB per 256² slice), and the
+// upload engine is the step's bottleneck (ARCHITECTURE.md §6). When every sample of a slice fits in
+// 12 bits, the loader ships it as 12-bit pairs — 3 bytes per 2 samples, 25% fewer bytes on PCIe
+// and in host memory — and the GPU expands it back to the identical 16-bit words before the first
+// kernel (k0_unpack.hip). Slices with any sample ≥ 4096 are shipped unchanged. Lossless by
+// construction: the pipeline sees bit-identical input either way.
+//
+// Layout: pair k = samples (2k, 2k+1) → 24-bit little-endian value s[2k] | s[2k+1] << 12 at byte 3k.
+#pragma once
+
+#include <cstddef>
+#include <cstdint>
+
+namespace nm03::pack12 {
+
+// True when the CPU has the vector unit the packer uses (AVX2); otherwise pack() always declines.
+bool available();
+
+// Packs n samples (n % 16 == 0) into dst (capacity ≥ n * 3 / 2 + 32: the vector stores write up to
+// 32 bytes past the packed end) when all fit in 12 bits; returns the packed byte count n * 3 / 2, or
+// 0 (dst untouched beyond scratch use) when some sample needs more bits or n % 16 != 0.
+size_t pack(const uint16_t* src, size_t n, uint8_t* dst);
+
+// Scalar reference of the inverse (tests; the device expands with k0_unpack.hip).
+void unpack(const uint8_t* src, size_t n, uint16_t* dst);
+
+}  // namespace nm03::pack12

@@ -402,6 +402,14 @@ void SliceFile::pixels16(uint16_t* dst) {
   if (k < n) pread_all(reinterpret_cast<uint8_t*>(dst) + k, n - k, h_.pixel_offset + k);
 }
 
+const uint16_t* SliceFile::staged_samples() const {
+  if (!whole_ || mode_ != ReadMode::kStaged || !buf_) return nullptr;
+  if (h_.bits_allocated != 16 || h_.syntax == Syntax::kExplicitBE) return nullptr;
+  const size_t n = (size_t)h_.rows * h_.cols * 2;
+  if (h_.pixel_offset + n > size_ || (h_.pixel_offset & 1)) return nullptr;
+  return reinterpret_cast<const uint16_t*>(buf_->data() + h_.pixel_offset);
+}
+
 void stream_copy(void* dst, const void* src, size_t n) {
   auto* d = static_cast<uint8_t*>(dst);
   const auto* s = static_cast<const uint8_t*>(src);

@@ -24,6 +24,7 @@
 #include "nm03/kernels.h"
 #include "nm03/log.h"
 #include "nm03/numa.h"
+#include "nm03/pack12.h"
 #include "nm03/thread_pool.h"
 
 namespace nm03 {
@@ -53,7 +54,8 @@ struct LoadedSlice {
   int w = 0, h = 0;
   uint8_t type = kU16, stored_bits = 16;
   float slope = 1.f, intercept = 0.f, sx = 1.f, sy = 1.f;
-  uint32_t raw_off = 0;
+  uint32_t blob_off = 0;  // u16 offset of the uploaded samples in the blob's raw region
+  bool packed = false;    // uploaded as 12-bit pairs (nm03/pack12.h)
 };
 
 // Per-image JPEG capacities. The entropy-coded segment of a 512² canvas is a few tens of KB;
@@ -72,6 +74,7 @@ struct Slot {
   size_t max_medt = 0, max_shpt = 0;
   uint8_t* h_blob = nullptr;
   uint8_t* d_blob = nullptr;
+  uint16_t* d_raw_x = nullptr;  // expanded 16-bit samples of the batch (K0 output, every kernel's input)
   uint16_t* d_med = nullptr;
   uint32_t* d_tile_mm = nullptr;  // per median tile (min, max) key
   float* d_f32 = nullptr;
@@ -113,7 +116,7 @@ void hip_free_all(Slot& s) {
   if (s.h_blob) (void)hipHostFree(s.h_blob);
   if (s.h_out) (void)hipHostFree(s.h_out);
   if (s.h_sizes) (void)hipHostFree(s.h_sizes);
-  for (void* p : {(void*)s.d_blob, (void*)s.d_med, (void*)s.d_tile_mm, (void*)s.d_f32, (void*)s.d_bits, (void*)s.d_canvas,
+  for (void* p : {(void*)s.d_blob, (void*)s.d_raw_x, (void*)s.d_med, (void*)s.d_tile_mm, (void*)s.d_f32, (void*)s.d_bits, (void*)s.d_canvas,
                   (void*)s.jw.stage, (void*)s.jw.look, (void*)s.jw.ticket, (void*)s.jw.spill,
                   (void*)s.jw.total, (void*)s.jw.chunk_ff})
     if (p) (void)hipFree(p);
@@ -148,12 +151,15 @@ struct Engine::Impl {
   // slower still (198k/187k/200k).
   dicom::ReadMode read_mode_ = dicom::ReadMode::kStaged;
   size_t read_prefix_ = 16384;
+  // 12-bit transfer packing of slices whose samples fit (nm03/pack12.h); NM03_PACK12=0 disables.
+  bool pack12_ = pack12::available();
 
   explicit Impl(const EngineConfig& c) : cfg(c), place(c.device) {
     if (const char* e = std::getenv("NM03_BATCH_TAPER"); e && *e) cfg.taper = *e != '0';
     if (const char* e = std::getenv("NM03_LOAD_MODE"); e && *e)
       read_mode_ = std::string(e) == "staged" ? dicom::ReadMode::kStaged : dicom::ReadMode::kDirect;
     if (const char* e = std::getenv("NM03_LOAD_PREFIX"); e && *e) read_prefix_ = (size_t)std::atol(e);
+    if (const char* e = std::getenv("NM03_PACK12"); e && *e && *e == '0') pack12_ = false;
     if (const char* e = std::getenv("NM03_UPLOAD_CHUNK_KB"); e && *e) upload_chunk_ = (size_t)std::atol(e) << 10;
     if (cfg.batch_size < 1) cfg.batch_size = 1;
     if (cfg.streams < 1) cfg.streams = 1;
@@ -243,6 +249,7 @@ struct Engine::Impl {
       check_hip(hipEventCreateWithFlags(&s.ev2, spin ? hipEventDefault : hipEventBlockingSync), "hipEventCreate");
       check_hip(hipHostMalloc((void**)&s.h_blob, s.blob_bytes, hipHostMallocDefault), "hipHostMalloc blob");
       s.d_blob = dmalloc<uint8_t>(s.blob_bytes, "hipMalloc blob");
+      s.d_raw_x = dmalloc<uint16_t>(s.cap_pixels, "hipMalloc raw");
       s.d_med = dmalloc<uint16_t>(s.cap_pixels, "hipMalloc median");
       s.d_tile_mm = dmalloc<uint32_t>(2 * s.max_medt, "hipMalloc tile ranges");
       s.d_f32 = dmalloc<float>(s.cap_pixels, "hipMalloc f32");
@@ -383,7 +390,15 @@ struct Engine::Impl {
                      " exceed the engine limit " + std::to_string(cfg.max_dim);
       } else {
         const size_t npix = (size_t)h.rows * h.cols;
-        const size_t alloc = align_up(npix, 8);
+        // 12-bit transfer packing when every sample fits (staged reads of raw 16-bit data).
+        thread_local std::vector<uint8_t> pk;
+        const uint16_t* samples = pack12_ ? file.staged_samples() : nullptr;
+        size_t pbytes = 0;
+        if (samples && (npix & 15) == 0) {
+          if (pk.size() < npix / 2 * 3 + 64) pk.resize(npix / 2 * 3 + 64);
+          pbytes = pack12::pack(samples, npix, pk.data());
+        }
+        const size_t alloc = pbytes ? align_up(pbytes / 2, 8) : align_up(npix, 8);
         size_t off, idx;
         {
           std::lock_guard<std::mutex> g(s.alloc_m);
@@ -397,7 +412,10 @@ struct Engine::Impl {
         }
         uint16_t* dst = reinterpret_cast<uint16_t*>(s.h_blob + s.raw_base) + off;
         try {
-          file.pixels16(dst);
+          if (pbytes)
+            dicom::stream_copy(dst, pk.data(), pbytes);
+          else
+            file.pixels16(dst);
         } catch (...) {
           s.allocs[idx].done.store(true, std::memory_order_release);  // space stays unused
           throw;
@@ -412,7 +430,8 @@ struct Engine::Impl {
         L.intercept = cfg.pipe.apply_rescale ? h.intercept : 0.f;
         L.sx = h.spacing_x;
         L.sy = h.spacing_y;
-        L.raw_off = (uint32_t)off;
+        L.blob_off = (uint32_t)off;
+        L.packed = pbytes != 0;
         L.ok = true;
         st.code = kSliceOk;
         bytes_in += (int64_t)n;
@@ -449,12 +468,17 @@ struct Engine::Impl {
     const int cw = cfg.render.out_width, ch = cfg.render.out_height;
     const uint32_t canvas_bytes = (uint32_t)(cw * ch);
     const uint8_t fill = opacity_u8(cfg.render.label_opacity), bval = opacity_u8(cfg.render.border_opacity);
+    uint32_t xoff = 0;  // expanded-sample offsets (K0 output) in batch order
     for (int c = 0; c < nl; ++c) {
       const LoadedSlice& L = s.loaded[s.live[c]];
       stats[c] = SliceStats{0xFFFFFFFFu, 0u, 0xFFFFFFFFu, 0u};
       SliceDesc& d = desc[c];
       std::memset(&d, 0, sizeof(d));
-      d.raw_off = L.raw_off;
+      const uint32_t raw_off = xoff;
+      xoff += (uint32_t)align_up((size_t)L.w * L.h, 8);
+      d.raw_off = raw_off;
+      d.blob_off = L.blob_off;
+      d.flags = L.packed ? kSliceFlagPacked12 : 0;
       d.w = (uint16_t)L.w;
       d.h = (uint16_t)L.h;
       d.wpr = (uint16_t)((L.w + 63) / 64);
@@ -464,7 +488,7 @@ struct Engine::Impl {
       d.stored_bits = L.stored_bits;
       d.slope = L.slope;
       d.intercept = L.intercept;
-      d.f32_off = L.raw_off;
+      d.f32_off = raw_off;
       auto sv = reference_seeds(L.w, L.h);
       d.seed_off = (uint32_t)nseed;
       d.seed_count = (uint16_t)std::min<size_t>(sv.size(), kMaxSeeds);
@@ -504,7 +528,7 @@ struct Engine::Impl {
         return r;
       };
       RenderDesc orig = base_rd(kRenderRawGray);
-      orig.src_off = L.raw_off;
+      orig.src_off = raw_off;
       if (mode == 0) {
         rd[ncanv++] = orig;
         rd[ncanv++] = labels(kPDilated, kPBorderD);
@@ -544,7 +568,7 @@ struct Engine::Impl {
     auto* d_seeds = reinterpret_cast<SeedXY*>(db + s.off_seeds);
     auto* d_rd = reinterpret_cast<RenderDesc*>(db + s.off_render);
     auto* d_jd = reinterpret_cast<JpegDesc*>(db + s.off_jpeg);
-    auto* d_raw = reinterpret_cast<uint16_t*>(db + s.raw_base);
+    auto* d_raw = s.d_raw_x;
     auto plane = [&](Plane p) { return s.d_bits + p * s.plane_words; };
 
     if (!s.upload_started) check_hip(hipEventRecord(s.ev0, s.stream), "event");
@@ -558,6 +582,7 @@ struct Engine::Impl {
     s.uploaded = raw_end;
     check_hip(hipEventRecord(s.ev1, s.stream), "event");
     auto chain = [&] {
+      launch_unpack(reinterpret_cast<const uint16_t*>(db + s.raw_base), d_raw, d_desc, nl, s.max_w * s.max_h, s.stream);
       launch_median(d_raw, s.d_med, d_desc, d_medt, nmed, pc.median_k, d_stats, s.stream, s.d_tile_mm);
       launch_sharpen_band(s.d_med, plane(kPBand), mode == 1 ? s.d_f32 : nullptr, d_desc, d_shpt, nshp, pc, d_stats,
                           s.stream, s.d_tile_mm);
@@ -628,7 +653,7 @@ struct Engine::Impl {
     if (!s.any_canvas) {
       // Fused batches never materialised canvases: render them now (rare overflow path).
       uint8_t* db = s.d_blob;
-      launch_render(reinterpret_cast<uint16_t*>(db + s.raw_base), s.d_f32, s.d_bits,
+      launch_render(s.d_raw_x, s.d_f32, s.d_bits,
                     reinterpret_cast<SliceStats*>(db + s.off_stats), reinterpret_cast<RenderDesc*>(db + s.off_render),
                     s.ncanvas, cw, ch, s.d_canvas, s.stream);
       check_hip(hipStreamSynchronize(s.stream), "fallback render");
@@ -911,7 +936,8 @@ struct Engine::Impl {
     L.intercept = cfg.pipe.apply_rescale ? in.intercept : 0.f;
     L.sx = in.spacing_x;
     L.sy = in.spacing_y;
-    L.raw_off = 0;
+    L.blob_off = 0;
+    L.packed = false;
     std::memcpy(s.h_blob + s.raw_base, in.raw.data(), in.raw.size() * sizeof(uint16_t));
     s.live.assign(1, 0);
     build_and_run(s, 1, nullptr);

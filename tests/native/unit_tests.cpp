@@ -27,6 +27,7 @@
 #include "nm03/golden.h"
 #include "nm03/jpeg.h"
 #include "nm03/numa.h"
+#include "nm03/pack12.h"
 #include "nm03/params.h"
 #include "nm03/thread_pool.h"
 
@@ -189,6 +190,30 @@ TEST(dicom_rejects_garbage) {
     threw = true;
   }
   CHECK(threw);
+}
+
+TEST(pack12_round_trip_and_declines) {
+  using namespace nm03::pack12;
+  if (!available()) return;  // no AVX2: the engine ships 16-bit samples
+  std::mt19937 rng(12);
+  for (size_t n : {16u, 48u, 65536u}) {
+    std::vector<uint16_t> px(n);
+    for (auto& v : px) v = (uint16_t)(rng() & 0xFFF);
+    px[0] = 0xFFF;
+    std::vector<uint8_t> packed(n / 2 * 3 + 32, 0xEE);
+    CHECK(pack(px.data(), n, packed.data()) == n / 2 * 3);
+    std::vector<uint16_t> back(n);
+    unpack(packed.data(), n, back.data());
+    CHECK(back == px);
+    // byte layout: pair k = s[2k] | s[2k+1] << 12, little endian at byte 3k
+    const uint32_t v0 = packed[0] | (packed[1] << 8) | (packed[2] << 16);
+    CHECK(v0 == ((uint32_t)px[0] | ((uint32_t)px[1] << 12)));
+    px[n - 1] = 0x1000;  // one 13-bit sample: shipped unpacked
+    CHECK(pack(px.data(), n, packed.data()) == 0);
+  }
+  std::vector<uint16_t> odd(24, 5);
+  std::vector<uint8_t> out(64);
+  CHECK(pack(odd.data(), odd.size(), out.data()) == 0);  // n % 16 != 0
 }
 
 // ---- JPEG container ------------------------------------------------------------------------------
