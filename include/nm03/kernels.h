@@ -19,8 +19,12 @@ bool sync_launches();
 // K1a: k×k median of raw keys → `med` (u16 keys, same layout as raw). k ∈ {3,5,7,9}.
 // Per-slice key range: with `tile_mm` (2 u32 per tile) each tile stores its (min, max) and
 // launch_sharpen_band reduces them into stats (no atomics); without it, atomics on stats.
+// With `blob` (engine batches) the samples are read from the uploaded blob at SliceDesc::blob_off
+// (12-bit packed slices decoded on the fly) instead of `raw`, and the expanded 16-bit samples are
+// written to `raw_out` at raw_off (what launch_unpack would produce).
 void launch_median(const uint16_t* raw, uint16_t* med, const SliceDesc* descs, const TileDesc* tiles, int ntiles,
-                   int k, SliceStats* stats, hipStream_t stream, uint32_t* tile_mm = nullptr);
+                   int k, SliceStats* stats, hipStream_t stream, uint32_t* tile_mm = nullptr,
+                   const uint16_t* blob = nullptr, uint16_t* raw_out = nullptr);
 
 // K1b: normalise+clip of the median keys, separable Gaussian unsharp mask, SRG band test →
 // `band` bitmaps (u64 words, LSB = left-most pixel). Optionally the f32 sharpened image.

@@ -11,6 +11,10 @@
 // * Medians are computed on order-preserving 16-bit keys: normalise+clip is monotone, so the
 //   median of c(x) is c(median x) exactly (pixel_math.h). The same pass reduces per-slice min/max
 //   keys for the original-image render window.
+// * Engine batches (`blob` set): the tile is read straight from the uploaded blob — 12-bit packed
+//   pairs (nm03/pack12.h) are decoded in the load — and each workgroup writes its 64×64 interior
+//   as expanded 16-bit samples to `raw` for the render/JPEG stages. This replaces the separate
+//   K0 expansion pass (one launch and one full read + write of the batch's samples less).
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
@@ -38,7 +42,8 @@ template <int K>
 __global__ __launch_bounds__(256) void median_kernel(const uint16_t* __restrict__ raw, uint16_t* __restrict__ med,
                                                      const SliceDesc* __restrict__ descs,
                                                      const TileDesc* __restrict__ tiles, SliceStats* stats,
-                                                     uint32_t* __restrict__ tile_mm, int dbg) {
+                                                     uint32_t* __restrict__ tile_mm, int dbg,
+                                                     const uint16_t* __restrict__ blob, uint16_t* __restrict__ raw_out) {
   constexpr int R = K / 2;
   constexpr int PW = 32 + K - 1;  // pair columns
   constexpr int PS = PW | 1;      // odd stride: conflict-free ds_read_b32
@@ -48,35 +53,72 @@ __global__ __launch_bounds__(256) void median_kernel(const uint16_t* __restrict_
   const TileDesc t = tiles[blockIdx.x];
   const SliceDesc d = descs[t.slice];
   const int x0 = t.tx * kMedTileW, y0 = t.ty * kMedTileH;
-  const uint16_t* src = raw + d.raw_off;
   const int W = d.w, H = d.h;
+  // Source: the expanded raw buffer, or (blob set) the slice as uploaded — plain 16-bit samples or
+  // a 12-bit little-endian stream (sample p at bits [12p, 12p + 12) from the slice's first byte).
+  const bool from_blob = blob != nullptr;
+  const bool packed = from_blob && (d.flags & kSliceFlagPacked12);
+  const uint16_t* src = from_blob ? blob + d.blob_off : raw + d.raw_off;
+  const uint8_t* pb = reinterpret_cast<const uint8_t*>(src);
+  auto sample = [&](int y, int x) -> uint16_t {
+    const uint32_t p = (uint32_t)y * W + x;
+    if (!packed) return src[p];
+    const uint32_t o = (3u * p) >> 1;
+    const uint32_t v = (uint32_t)pb[o] | ((uint32_t)pb[o + 1] << 8);
+    return (uint16_t)((p & 1u) ? (v >> 4) : (v & 0xFFFu));
+  };
+  // Expanded-sample side output (blob mode): the tile interior, each pixel written by one task.
+  uint16_t* rdst = from_blob ? raw_out + d.raw_off : nullptr;
+  const int yin_hi = min(y0 + kMedTileH, H), xin_hi = min(x0 + kMedTileW, W);
 
   uint32_t kmin = 0xFFFFu, kmax = 0u;
-  if ((W & 3) == 0 && (d.raw_off & 3) == 0) {
+  if ((W & 3) == 0 && (d.raw_off & 3) == 0 && (!from_blob || packed || (d.blob_off & 3) == 0)) {
     // Vector path: window pixels p = 0..71 are image columns x0-4+p (8-byte aligned groups of
     // 4). Pair column c holds window pixels c+4-R (low half) and c+36-R (high half), so a task
     // (row, group gi < 10) loads groups gi and gi+8 — one 8-byte load each, per-pixel clamped
     // loads only where a group leaves the image — and writes up to 4 pair words.
     for (int i = threadIdx.x; i < PR * 10; i += 256) {
       const int r = i / 10, gi = i - r * 10;
-      const int y = clampi(y0 - R + r, 0, H - 1);
+      const int yy = y0 - R + r;
+      const int y = clampi(yy, 0, H - 1);
       const uint16_t* row = src + (size_t)y * W;
-      auto group = [&](int g4, uint16_t* px) {
+      const bool row_in = rdst && yy >= y0 && yy < yin_hi;
+      auto group = [&](int g4, uint16_t* px, bool store) {
         const int xs = x0 - 4 + 4 * g4;
         if (xs >= 0 && xs + 4 <= W) {
-          const uint2 v = *reinterpret_cast<const uint2*>(row + xs);
+          uint2 v;
+          if (packed) {
+            // 4 samples = 48 bits at byte o = 1.5·p (p = y·W + xs ≡ 0 mod 4, so o is even): two
+            // aligned dword loads from o & ~3 cover them (the device blob has tail slack for the
+            // 2 bytes this can read past a slice that ends the blob).
+            const size_t o = ((size_t)y * W + xs) * 3 >> 1;
+            const uint32_t* q = reinterpret_cast<const uint32_t*>(pb + (o & ~(size_t)3));
+            const uint64_t b = ((uint64_t)q[0] | ((uint64_t)q[1] << 32)) >> ((o & 2) * 8);
+            v.x = ((uint32_t)b & 0xFFFu) | (((uint32_t)(b >> 12) & 0xFFFu) << 16);
+            v.y = ((uint32_t)(b >> 24) & 0xFFFu) | (((uint32_t)(b >> 36) & 0xFFFu) << 16);
+          } else {
+            v = *reinterpret_cast<const uint2*>(row + xs);
+          }
           px[0] = (uint16_t)v.x;
           px[1] = (uint16_t)(v.x >> 16);
           px[2] = (uint16_t)v.y;
           px[3] = (uint16_t)(v.y >> 16);
+          if (store && row_in && xs >= x0 && xs < xin_hi)
+            *reinterpret_cast<uint2*>(rdst + (size_t)yy * W + xs) = v;
         } else {
 #pragma unroll
-          for (int q = 0; q < 4; ++q) px[q] = row[clampi(xs + q, 0, W - 1)];
+          for (int q = 0; q < 4; ++q) px[q] = sample(y, clampi(xs + q, 0, W - 1));
+          if (store && row_in) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+              if (xs + q >= x0 && xs + q < xin_hi) rdst[(size_t)yy * W + xs + q] = px[q];
+          }
         }
       };
       uint16_t lo[4], hi[4];
-      group(gi, lo);
-      group(gi + 8, hi);
+      // Groups 8 and 9 are loaded twice (as lo and as hi): only the lo load stores them.
+      group(gi, lo, gi >= 1);
+      group(gi + 8, hi, gi + 8 >= 10 && gi + 8 <= 16);
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int c = 4 * gi + q - (4 - R);
@@ -91,11 +133,16 @@ __global__ __launch_bounds__(256) void median_kernel(const uint16_t* __restrict_
   } else {
     for (int i = threadIdx.x; i < PR * PW; i += 256) {
       const int r = i / PW, c = i - r * PW;
-      const int y = clampi(y0 - R + r, 0, H - 1);
-      const int xl = clampi(x0 - R + c, 0, W - 1), xh = clampi(x0 - R + c + 32, 0, W - 1);
-      const uint16_t* row = src + (size_t)y * W;
-      const uint32_t kl = key_from_raw(row[xl], d.type, d.stored_bits);
-      const uint32_t kh = key_from_raw(row[xh], d.type, d.stored_bits);
+      const int yy = y0 - R + r;
+      const int y = clampi(yy, 0, H - 1);
+      const int ul = x0 - R + c, uh = ul + 32;
+      const uint16_t sl = sample(y, clampi(ul, 0, W - 1)), sh = sample(y, clampi(uh, 0, W - 1));
+      if (rdst && yy >= y0 && yy < yin_hi) {
+        if (ul >= x0 && ul < min(x0 + 32, xin_hi)) rdst[(size_t)yy * W + ul] = sl;
+        if (uh >= x0 + 32 && uh < xin_hi) rdst[(size_t)yy * W + uh] = sh;
+      }
+      const uint32_t kl = key_from_raw(sl, d.type, d.stored_bits);
+      const uint32_t kh = key_from_raw(sh, d.type, d.stored_bits);
       P[r * PS + c] = kl | (kh << 16);
       kmin = min(kmin, min(kl, kh));
       kmax = max(kmax, max(kl, kh));
@@ -167,7 +214,9 @@ __global__ __launch_bounds__(256) void median_kernel(const uint16_t* __restrict_
 }
 
 void launch_median(const uint16_t* raw, uint16_t* med, const SliceDesc* descs, const TileDesc* tiles, int ntiles,
-                   int k, SliceStats* stats, hipStream_t stream, uint32_t* tile_mm) {
+                   int k, SliceStats* stats, hipStream_t stream, uint32_t* tile_mm, const uint16_t* blob,
+                   uint16_t* raw_out) {
+  if (blob && !raw_out) throw DeviceError("launch_median: blob input needs a raw_out buffer");
   if (ntiles <= 0) return;
   dim3 grid(ntiles), block(256);
   static const int dbg = [] {  // NM03_MEDIAN_DBG=1: profiling variant (output invalid)
@@ -175,10 +224,10 @@ void launch_median(const uint16_t* raw, uint16_t* med, const SliceDesc* descs, c
     return e ? std::atoi(e) : 0;
   }();
   switch (k) {
-    case 3: median_kernel<3><<<grid, block, 0, stream>>>(raw, med, descs, tiles, stats, tile_mm, dbg); break;
-    case 5: median_kernel<5><<<grid, block, 0, stream>>>(raw, med, descs, tiles, stats, tile_mm, dbg); break;
-    case 7: median_kernel<7><<<grid, block, 0, stream>>>(raw, med, descs, tiles, stats, tile_mm, dbg); break;
-    case 9: median_kernel<9><<<grid, block, 0, stream>>>(raw, med, descs, tiles, stats, tile_mm, dbg); break;
+    case 3: median_kernel<3><<<grid, block, 0, stream>>>(raw, med, descs, tiles, stats, tile_mm, dbg, blob, raw_out); break;
+    case 5: median_kernel<5><<<grid, block, 0, stream>>>(raw, med, descs, tiles, stats, tile_mm, dbg, blob, raw_out); break;
+    case 7: median_kernel<7><<<grid, block, 0, stream>>>(raw, med, descs, tiles, stats, tile_mm, dbg, blob, raw_out); break;
+    case 9: median_kernel<9><<<grid, block, 0, stream>>>(raw, med, descs, tiles, stats, tile_mm, dbg, blob, raw_out); break;
     default: throw DeviceError("median window must be 3, 5, 7 or 9 (got " + std::to_string(k) + ")");
   }
   check_launch("median_kernel");

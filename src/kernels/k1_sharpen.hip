@@ -126,9 +126,11 @@ __global__ __launch_bounds__(256) void sharpen_band_kernel(const uint16_t* __res
 
   // ---- 3. horizontal pass + combine + band: a thread owns row r, columns [16·seg, 16·seg + 16)
   //         and slides a (16+2R)-value register window; band bits go through LDS to form the
-  //         64-bit row words.
-  __shared__ uint16_t bm[TH * 4];
-  const int r = threadIdx.x >> 2, seg = threadIdx.x & 3;
+  //         64-bit row words. Wave = segment, lane = row: a half-wave reads 32 rows at the odd
+  //         stride CS, i.e. 32 distinct banks (row-major lanes put segments 0/2 and 1/3 of a row
+  //         on one bank: 2-way conflicts on every read).
+  __shared__ uint16_t bm[4 * TH];
+  const int r = threadIdx.x & (TH - 1), seg = threadIdx.x / TH;
   const int y = y0 + r;
   float smin = INFINITY, smax = -INFINITY;
   {
@@ -155,12 +157,13 @@ __global__ __launch_bounds__(256) void sharpen_band_kernel(const uint16_t* __res
         smax = fmaxf(smax, sv);
       }
     }
-    bm[r * 4 + seg] = (uint16_t)bits;
+    bm[seg * TH + r] = (uint16_t)bits;
   }
   __syncthreads();
   if (threadIdx.x < TH && y0 + (int)threadIdx.x < H) {
-    const uint16_t* q = bm + threadIdx.x * 4;
-    const uint64_t word = (uint64_t)q[0] | ((uint64_t)q[1] << 16) | ((uint64_t)q[2] << 32) | ((uint64_t)q[3] << 48);
+    const uint16_t* q = bm + threadIdx.x;
+    const uint64_t word = (uint64_t)q[0] | ((uint64_t)q[TH] << 16) | ((uint64_t)q[2 * TH] << 32) |
+                          ((uint64_t)q[3 * TH] << 48);
     band[d.mask_off + (size_t)(y0 + threadIdx.x) * d.wpr + t.tx] = word;
   }
   if (sharpened && stats) {

@@ -35,6 +35,12 @@ namespace {
 
 constexpr size_t kAlign = 256;
 inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+// NM03_SEPARATE_UNPACK=1: expand the upload with the standalone K0 pass instead of inside the
+// median's tile load (A/B switch; both produce identical buffers).
+bool separate_unpack() {
+  const char* e = std::getenv("NM03_SEPARATE_UNPACK");  // read per batch: tests flip it in-process
+  return e && e[0] && e[0] != '0';
+}
 // CPU time of the calling thread (ns): loader/writer tasks report it next to their wall time, so a
 // CPU-quota stall or preemption (wall ≫ cpu) can be told apart from work (wall ≈ cpu).
 inline int64_t thread_cpu_ns() {
@@ -248,7 +254,8 @@ struct Engine::Impl {
       const bool spin = wait_mode() == WaitMode::kSpin;
       check_hip(hipEventCreateWithFlags(&s.ev2, spin ? hipEventDefault : hipEventBlockingSync), "hipEventCreate");
       check_hip(hipHostMalloc((void**)&s.h_blob, s.blob_bytes, hipHostMallocDefault), "hipHostMalloc blob");
-      s.d_blob = dmalloc<uint8_t>(s.blob_bytes, "hipMalloc blob");
+      // +64 B tail slack: the median's packed-group loads read whole dwords (k1_median.hip).
+      s.d_blob = dmalloc<uint8_t>(s.blob_bytes + 64, "hipMalloc blob");
       s.d_raw_x = dmalloc<uint16_t>(s.cap_pixels, "hipMalloc raw");
       s.d_med = dmalloc<uint16_t>(s.cap_pixels, "hipMalloc median");
       s.d_tile_mm = dmalloc<uint32_t>(2 * s.max_medt, "hipMalloc tile ranges");
@@ -582,8 +589,14 @@ struct Engine::Impl {
     s.uploaded = raw_end;
     check_hip(hipEventRecord(s.ev1, s.stream), "event");
     auto chain = [&] {
-      launch_unpack(reinterpret_cast<const uint16_t*>(db + s.raw_base), d_raw, d_desc, nl, s.max_w * s.max_h, s.stream);
-      launch_median(d_raw, s.d_med, d_desc, d_medt, nmed, pc.median_k, d_stats, s.stream, s.d_tile_mm);
+      const auto* blob_raw = reinterpret_cast<const uint16_t*>(db + s.raw_base);
+      if (separate_unpack()) {  // A/B: the standalone K0 expansion pass before the median
+        launch_unpack(blob_raw, d_raw, d_desc, nl, s.max_w * s.max_h, s.stream);
+        launch_median(d_raw, s.d_med, d_desc, d_medt, nmed, pc.median_k, d_stats, s.stream, s.d_tile_mm);
+      } else {  // the median reads the upload directly and writes the expanded samples
+        launch_median(nullptr, s.d_med, d_desc, d_medt, nmed, pc.median_k, d_stats, s.stream, s.d_tile_mm, blob_raw,
+                      d_raw);
+      }
       launch_sharpen_band(s.d_med, plane(kPBand), mode == 1 ? s.d_f32 : nullptr, d_desc, d_shpt, nshp, pc, d_stats,
                           s.stream, s.d_tile_mm);
       SrgOutputs o;

@@ -299,6 +299,34 @@ def test_engine_pack12_identical(native, cohort_root, tmp_path, monkeypatch):
     assert runs[0][1] == runs[1][1]
 
 
+def test_engine_fused_unpack_identical(native, cohort_root, tmp_path, monkeypatch):
+    """Upload expansion inside the median's tile load (default) vs the standalone K0 pass
+    (NM03_SEPARATE_UNPACK=1), with 12-bit packing on: byte-identical JPEGs on batches mixing packed
+    slices, a 13-bit slice (plain 16-bit blob, vector loads) and an odd-sized slice (plain blob,
+    W % 4 != 0: per-pixel loads) and a packed 200×112 slice (partial edge tiles in x and y)."""
+    d = tmp_path / "mixed"
+    d.mkdir()
+    hi = native.phantom_slice(256, 256, 4, 11, 25, 9).astype(np.uint32) + 3000
+    (d / "1-1.dcm").write_bytes(native.dicom_bytes(np.minimum(hi, 65535).astype(np.uint16)))
+    (d / "1-2.dcm").write_bytes(native.dicom_bytes(native.phantom_slice(150, 203, 2, 7, 25, 3)))
+    (d / "1-3.dcm").write_bytes(native.dicom_bytes(native.phantom_slice(112, 200, 2, 9, 25, 5)))
+    monkeypatch.setenv("NM03_PACK12", "1")
+    runs = []
+    for i, flag in enumerate(["1", "0"]):
+        out = str(tmp_path / f"o{i}")
+        items = _items(native, cohort_root, out)[:20]
+        os.makedirs(os.path.join(out, "mixed"), exist_ok=True)
+        extra = [(str(d / f"1-{k}.dcm"), os.path.join(out, "mixed")) for k in range(1, 4)]
+        items = items[:5] + extra + items[5:]
+        monkeypatch.setenv("NM03_SEPARATE_UNPACK", flag)
+        eng = native.Engine(nm.PipelineConfig(batch_size=8, streams=2, threads=4).engine_config())
+        st, _ = eng.run(items)
+        del eng
+        runs.append(([c for c, _ in st], _tree(out)))
+    assert runs[0][0] == runs[1][0] and runs[0][0].count(0) == len(runs[0][0])
+    assert runs[0][1] == runs[1][1]
+
+
 def test_engine_progressive_upload_identical(native, cohort_root, tmp_path, monkeypatch):
     """Progressive H2D (finished prefixes of a batch's raw region queued while loads run) with
     1 KiB / 64 KiB chunks vs one upload per batch: same statuses, byte-identical JPEGs, on a work
