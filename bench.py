@@ -33,6 +33,8 @@ from nm03_capstone_project_amd.parallel import (allreduce_max, allreduce_sum, au
                                                 plan_cohort)
 from nm03_capstone_project_amd.parallel.cohort_runner import CohortPlan  # noqa: E402
 from nm03_capstone_project_amd.parallel.dist import shard_bounds  # noqa: E402
+from nm03_capstone_project_amd.parallel.numa_data import (ensure_node_replicas, localize_items,  # noqa: E402
+                                                          numa_nodes, replica_root)
 
 METRIC = "DICOM slices/sec through full pipeline (T1+C cohort) at 1/2/4/8 MI355X"
 # The reference publishes no number; BASELINE.md defines the comparison point as the measured
@@ -91,28 +93,34 @@ def main():
     ap.add_argument("--keep-data", action="store_true", help="keep a generated dataset in tmpfs after the run")
     ap.add_argument("--keep-output", action="store_true")
     ap.add_argument("--graphs", action="store_true", help="hipGraph replay of the per-batch kernel chain")
+    ap.add_argument("--numa-data", choices=("auto", "off"), default=os.environ.get("NM03_BENCH_NUMA_DATA", "auto"),
+                    help="auto: one input copy per NUMA node, each rank reads the copy on its GPU's node")
     args = ap.parse_args()
 
     ctx = init_from_env()
     if args.threads <= 0:
         args.threads = auto_threads()
     n = nm.native()
-    marker = os.path.join(args.data_root, ".complete")
-    if ctx.local_rank == 0 and not os.path.exists(marker):
-        n.synth_cohort(args.data_root, threads=16)
-        open(marker, "w").close()
+    # Input cohort in tmpfs: one copy per NUMA node on multi-socket hosts (numa_data.py), so every
+    # rank reads the copy on its own GPU's node.
+    nodes = numa_nodes(n.numa_node_cpus) if args.numa_data == "auto" else []
+    roots = [replica_root(args.data_root, k) for k in nodes] or [args.data_root]
+    if ctx.local_rank == 0:
+        ensure_node_replicas(args.data_root, nodes, lambda root: n.synth_cohort(root, threads=16), n.numa_node_cpus)
     barrier(ctx)
-    while not os.path.exists(marker):  # other nodes' local rank 0 (single node: already there)
+    while not all(os.path.exists(os.path.join(r, ".complete")) for r in roots):  # other hosts' local rank 0
         time.sleep(0.1)
+    dev_node = n.numa_device_node(ctx.device_index) if nodes else -1
+    local_root = replica_root(args.data_root, dev_node) if dev_node in nodes else roots[0]
 
     replicas = ctx.world if args.scaling == "weak" else 1
     plan_bytes = b""
     if ctx.is_root:
-        plan_bytes = plan_cohort(args.data_root, args.out_root, wipe=True, replicas=replicas).to_bytes()
+        plan_bytes = plan_cohort(roots[0], args.out_root, wipe=True, replicas=replicas).to_bytes()
     plan = CohortPlan.from_bytes(broadcast_bytes(plan_bytes, ctx))
     items = plan.items
     lo, hi = shard_bounds(len(items), ctx.rank, ctx.world)
-    mine = items[lo:hi]
+    mine = localize_items(items[lo:hi], roots[0], local_root)
 
     cfg = nm.PipelineConfig(batch_size=args.batch_size, streams=args.streams, threads=args.threads,
                             device=ctx.device_index, graphs=args.graphs)
@@ -174,7 +182,7 @@ def main():
                                            for k in ("usage_usec", "throttled_usec") if k in cg1},
                 "rank0_process_cpu_ms_per_step": round((ru1.ru_utime + ru1.ru_stime - ru0.ru_utime - ru0.ru_stime)
                                                        * 1e3 / args.steps, 3),
-                "storage": {"data": args.data_root, "out": args.out_root},
+                "storage": {"data": local_root, "input_copies": len(roots), "out": args.out_root},
             },
         }
         print(json.dumps(rec), flush=True)
@@ -183,7 +191,8 @@ def main():
     # tmpfs holds data in RAM: drop a generated dataset unless asked to keep it (local rank 0,
     # after the final barrier every rank has passed).
     if ctx.local_rank == 0 and not args.keep_data and args.data_root.startswith("/dev/shm/"):
-        shutil.rmtree(args.data_root, ignore_errors=True)
+        for r in roots:
+            shutil.rmtree(r, ignore_errors=True)
     if ctx.world > 1:
         torch.distributed.destroy_process_group()
 
