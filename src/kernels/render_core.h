@@ -117,8 +117,11 @@ __device__ __forceinline__ void render_patch_2x(Fetch&& fetch, RWindow win, int3
       const f2 val = u0 + u1;
       f2 g = val - lo2;
       g = g * inv2;
-      g.x = g.x < 0.0f ? 0.0f : (g.x > 1.0f ? 1.0f : g.x);
-      g.y = g.y < 0.0f ? 0.0f : (g.y > 1.0f ? 1.0f : g.y);
+      // gray_u8's clamp to [0, 1] as one clamped v_max_f32 (g is never NaN: finite samples and
+      // window). The u8 cast below is a no-op on [0.5, 255.5] but keeps the allocation at 127
+      // VGPRs (without it the encoder spills to scratch).
+      g.x = __builtin_amdgcn_fmed3f(g.x, 0.0f, 1.0f);
+      g.y = __builtin_amdgcn_fmed3f(g.y, 0.0f, 1.0f);
       f2 t = g * 255.0f;
       t = t + 0.5f;
       px[r * 8 + 2 * m] = (int32_t)(uint8_t)(int)t.x;
