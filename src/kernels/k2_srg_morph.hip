@@ -43,52 +43,57 @@ __global__ __launch_bounds__(kSrgThreads) void srg_morph_kernel(const uint64_t* 
   const SliceDesc d = descs[blockIdx.x];
   const int W = d.w, H = d.h, n = d.wpr, hb = (H + 63) >> 6;
   const int words = H * n;
+  // LDS row strides: odd word counts, so the thread-per-row sweeps and the 64-row transposes (lane
+  // = row) hit 32 distinct 8-byte bank pairs per half-wave instead of 4-way conflicts at stride 4.
+  const int sn = n | 1, st = hb | 1;
+  auto at = [&](int q) { const int y = q / n; return y * sn + (q - y * n); };  // dense → LDS index
   uint64_t* M = smem;
   uint64_t* Rg = M + plane_words;
   uint64_t* Mt = Rg + plane_words;
   uint64_t* Rt = Mt + plane_words;
 
   for (int i = threadIdx.x; i < words; i += blockDim.x) {
-    M[i] = band[d.mask_off + i];
-    Rg[i] = 0ull;
+    const int j = at(i);
+    M[j] = band[d.mask_off + i];
+    Rg[j] = 0ull;
   }
   __syncthreads();
   for (int s = threadIdx.x; s < d.seed_count; s += blockDim.x) {
     const SeedXY sd = seeds[d.seed_off + s];
     if (sd.x < 0 || sd.y < 0 || sd.x >= W || sd.y >= H) continue;
-    const int wi = sd.y * n + (sd.x >> 6);
+    const int wi = sd.y * sn + (sd.x >> 6);
     const uint64_t bit = 1ull << (sd.x & 63);
     if (M[wi] & bit) atomicOr((unsigned long long*)&Rg[wi], (unsigned long long)bit);
   }
-  transpose_plane(M, H, n, Mt, W, false, nullptr);
+  transpose_plane(M, H, n, Mt, W, false, nullptr, sn, st);
   __syncthreads();
 
-  const int iters = srg_fixpoint(M, Rg, Mt, Rt, W, H, n, pc.connectivity, &flag);
+  const int iters = srg_fixpoint(M, Rg, Mt, Rt, W, H, n, pc.connectivity, &flag, sn, st);
   // An iteration in which no step changed anything ⇒ Rg is the fixpoint region.
   if (out.iterations && threadIdx.x == 0) out.iterations[blockIdx.x] = iters;
   const size_t off = d.mask_off;
-  if (out.region) store_plane(Rg, out.region + off, words);
-  // Scratch planes now: M, Mt, Rt.
+  if (out.region) store_plane(Rg, out.region + off, H, n, sn);
+  // Scratch planes now: M, Mt, Rt (all used in row layout, stride sn, from here on).
   if (out.dilated || out.border_dilated) {
-    morph(Rg, Mt, M, W, H, n, pc.dilation_size, true);  // Mt = D
-    if (out.dilated) store_plane(Mt, out.dilated + off, words);
+    morph(Rg, Mt, M, W, H, n, pc.dilation_size, true, sn);  // Mt = D
+    if (out.dilated) store_plane(Mt, out.dilated + off, H, n, sn);
     if (out.border_dilated) {
-      morph(Mt, Rt, M, W, H, n, 2 * pc.border_radius + 1, false);  // Rt = erode(D)
-      for (int i = threadIdx.x; i < words; i += blockDim.x) out.border_dilated[off + i] = Mt[i] & ~Rt[i];
+      morph(Mt, Rt, M, W, H, n, 2 * pc.border_radius + 1, false, sn);  // Rt = erode(D)
+      for (int i = threadIdx.x; i < words; i += blockDim.x) out.border_dilated[off + i] = Mt[at(i)] & ~Rt[at(i)];
     }
     __syncthreads();
   }
   if (out.border_region) {
-    morph(Rg, Rt, M, W, H, n, 2 * pc.border_radius + 1, false);
-    for (int i = threadIdx.x; i < words; i += blockDim.x) out.border_region[off + i] = Rg[i] & ~Rt[i];
+    morph(Rg, Rt, M, W, H, n, 2 * pc.border_radius + 1, false, sn);
+    for (int i = threadIdx.x; i < words; i += blockDim.x) out.border_region[off + i] = Rg[at(i)] & ~Rt[at(i)];
     __syncthreads();
   }
   if (out.eroded || out.border_eroded) {
-    morph(Rg, Mt, M, W, H, n, pc.erosion_size, false);  // Mt = E
-    if (out.eroded) store_plane(Mt, out.eroded + off, words);
+    morph(Rg, Mt, M, W, H, n, pc.erosion_size, false, sn);  // Mt = E
+    if (out.eroded) store_plane(Mt, out.eroded + off, H, n, sn);
     if (out.border_eroded) {
-      morph(Mt, Rt, M, W, H, n, 2 * pc.border_radius + 1, false);
-      for (int i = threadIdx.x; i < words; i += blockDim.x) out.border_eroded[off + i] = Mt[i] & ~Rt[i];
+      morph(Mt, Rt, M, W, H, n, 2 * pc.border_radius + 1, false, sn);
+      for (int i = threadIdx.x; i < words; i += blockDim.x) out.border_eroded[off + i] = Mt[at(i)] & ~Rt[at(i)];
     }
   }
 }
@@ -98,9 +103,10 @@ void launch_srg_morph(const uint64_t* band, const SliceDesc* descs, int nslices,
   if (nslices <= 0) return;
   if (max_w > kSrgMaxDim || max_h > kSrgMaxDim)
     throw DeviceError("launch_srg_morph: slice larger than " + std::to_string(kSrgMaxDim));
+  // Planes hold rows at the kernel's odd strides (n | 1 and hb | 1 words); a slice's n ≤ this n.
   const int n = (max_w + 63) / 64, hb = (max_h + 63) / 64;
-  int plane_words = max_h * n;
-  if (max_w * hb > plane_words) plane_words = max_w * hb;
+  int plane_words = max_h * (n | 1);
+  if (max_w * (hb | 1) > plane_words) plane_words = max_w * (hb | 1);
   plane_words = (plane_words + 1) & ~1;
   const size_t lds = (size_t)plane_words * 4 * sizeof(uint64_t);
   srg_morph_kernel<<<nslices, kSrgThreads, lds, stream>>>(band, descs, seeds, pc, out, plane_words);

@@ -38,21 +38,24 @@ __device__ __forceinline__ bool fill_row(uint64_t* R, const uint64_t* M, int n) 
   return changed;
 }
 
-// Transpose a [rows][wpr] bit-plane into [cols][ceil(rows/64)]. Returns (via flag) whether any
-// destination word changed when `cmp` is set.
-__device__ inline void transpose_plane(const uint64_t* src, int rows, int wpr, uint64_t* dst, int cols, bool cmp, int* flag) {
+// Transpose a [rows][wpr] bit-plane (row stride ss words) into [cols][ceil(rows/64)] (row stride
+// ds words; 0 = dense). Returns (via flag) whether any destination word changed when `cmp` is set.
+__device__ inline void transpose_plane(const uint64_t* src, int rows, int wpr, uint64_t* dst, int cols, bool cmp, int* flag,
+                                       int ss = 0, int ds = 0) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
   const int hb = (rows + 63) >> 6;
+  if (ss == 0) ss = wpr;
+  if (ds == 0) ds = hb;
   const int nblocks = hb * wpr;
   bool changed = false;
   for (int b = wave; b < nblocks; b += nw) {
     const int bi = b / wpr, bj = b - bi * wpr;
     const int row = bi * 64 + lane;
-    uint64_t x = row < rows ? src[row * wpr + bj] : 0ull;
+    uint64_t x = row < rows ? src[row * ss + bj] : 0ull;
     x = wave_transpose64(x, lane);
     const int drow = bj * 64 + lane;
     if (drow < cols) {
-      uint64_t* p = dst + drow * hb + bi;
+      uint64_t* p = dst + drow * ds + bi;
       if (cmp && *p != x) changed = true;
       *p = x;
     }
@@ -86,39 +89,51 @@ __device__ __forceinline__ void morph_row_h(const uint64_t* src, uint64_t* dst, 
   }
 }
 
-// Vertical morphology: dst[y] = OP_{|dy|≤r, 0≤y+dy<H} src[y+dy].
-__device__ __forceinline__ void morph_rows_v(const uint64_t* src, uint64_t* dst, int h, int n, int r, bool dil) {
-  for (int idx = threadIdx.x; idx < h * n; idx += blockDim.x) {
-    const int y = idx / n, i = idx - y * n;
+// Vertical morphology: dst[y] = OP_{|dy|≤r, 0≤y+dy<H} src[y+dy] (row stride s words, 0 = n).
+__device__ __forceinline__ void morph_rows_v(const uint64_t* src, uint64_t* dst, int h, int n, int r, bool dil,
+                                             int s = 0) {
+  if (s == 0) s = n;
+  for (int q = threadIdx.x; q < h * n; q += blockDim.x) {
+    const int y = q / n, idx = y * s + (q - y * n);
     uint64_t acc = src[idx];
     for (int k = 1; k <= r; ++k) {
-      if (y - k >= 0) acc = dil ? (acc | src[idx - k * n]) : (acc & src[idx - k * n]);
-      if (y + k < h) acc = dil ? (acc | src[idx + k * n]) : (acc & src[idx + k * n]);
+      if (y - k >= 0) acc = dil ? (acc | src[idx - k * s]) : (acc & src[idx - k * s]);
+      if (y + k < h) acc = dil ? (acc | src[idx + k * s]) : (acc & src[idx + k * s]);
     }
     dst[idx] = acc;
   }
 }
 
-__device__ inline void morph(const uint64_t* src, uint64_t* dst, uint64_t* tmp, int w, int h, int n, int size, bool dil) {
+__device__ inline void morph(const uint64_t* src, uint64_t* dst, uint64_t* tmp, int w, int h, int n, int size, bool dil,
+                             int s = 0) {
+  if (s == 0) s = n;
   const int r = size / 2;
-  for (int y = threadIdx.x; y < h; y += blockDim.x) morph_row_h(src + y * n, tmp + y * n, n, w, r, dil);
+  for (int y = threadIdx.x; y < h; y += blockDim.x) morph_row_h(src + y * s, tmp + y * s, n, w, r, dil);
   __syncthreads();
-  morph_rows_v(tmp, dst, h, n, r, dil);
+  morph_rows_v(tmp, dst, h, n, r, dil, s);
   __syncthreads();
 }
 
-__device__ inline void store_plane(const uint64_t* src, uint64_t* dst, int words) {
-  for (int i = threadIdx.x; i < words; i += blockDim.x) dst[i] = src[i];
+// Copy an LDS plane with row stride s (n words per row) to a dense global plane.
+__device__ inline void store_plane(const uint64_t* src, uint64_t* dst, int h, int n, int s) {
+  for (int q = threadIdx.x; q < h * n; q += blockDim.x) {
+    const int y = q / n;
+    dst[q] = src[y * s + (q - y * n)];
+  }
 }
 
 
 // Grow Rg (seeded, ⊆ M) to the fixpoint of horizontal run fills, vertical run fills on the
 // transposed planes and (connectivity 8) diagonal seeding. Mt must hold transpose(M); Rt is
-// scratch. All planes in LDS. `flag` is an LDS int. Returns the iteration count.
+// scratch. All planes in LDS; M/Rg rows are sn words apart, Mt/Rt rows st words apart (0 = dense;
+// odd strides keep the thread-per-row sweeps and transposes free of LDS bank conflicts). `flag` is
+// an LDS int. Returns the iteration count.
 __device__ inline int srg_fixpoint(uint64_t* M, uint64_t* Rg, const uint64_t* Mt, uint64_t* Rt, int W, int H, int n,
-                            int connectivity, int* flagp) {
+                            int connectivity, int* flagp, int sn = 0, int st = 0) {
   int& flag = *flagp;
   const int hb = (H + 63) >> 6, words = H * n;
+  if (sn == 0) sn = n;
+  if (st == 0) st = hb;
   int iters = 0;
   const int max_iters = W * H + 4;  // monotone growth ⇒ always terminates earlier
   if (threadIdx.x == 0) flag = 0;
@@ -126,19 +141,19 @@ __device__ inline int srg_fixpoint(uint64_t* M, uint64_t* Rg, const uint64_t* Mt
   for (;;) {
     ++iters;
     bool ch = false;
-    for (int y = threadIdx.x; y < H; y += blockDim.x) ch |= fill_row(Rg + y * n, M + y * n, n);
+    for (int y = threadIdx.x; y < H; y += blockDim.x) ch |= fill_row(Rg + y * sn, M + y * sn, n);
     if (ch) flag = 1;
     __syncthreads();
     if (connectivity == 8) {
       // Diagonal seeding from a snapshot of the horizontally dilated rows (Rt as scratch).
-      for (int y = threadIdx.x; y < H; y += blockDim.x) morph_row_h(Rg + y * n, Rt + y * n, n, W, 1, true);
+      for (int y = threadIdx.x; y < H; y += blockDim.x) morph_row_h(Rg + y * sn, Rt + y * sn, n, W, 1, true);
       __syncthreads();
       bool dch = false;
-      for (int idx = threadIdx.x; idx < words; idx += blockDim.x) {
-        const int y = idx / n;
+      for (int q = threadIdx.x; q < words; q += blockDim.x) {
+        const int y = q / n, idx = y * sn + (q - y * n);
         uint64_t nb = 0;
-        if (y > 0) nb |= Rt[idx - n];
-        if (y + 1 < H) nb |= Rt[idx + n];
+        if (y > 0) nb |= Rt[idx - sn];
+        if (y + 1 < H) nb |= Rt[idx + sn];
         const uint64_t add = M[idx] & nb & ~Rg[idx];
         if (add) {
           Rg[idx] |= add;
@@ -148,11 +163,11 @@ __device__ inline int srg_fixpoint(uint64_t* M, uint64_t* Rg, const uint64_t* Mt
       if (dch) flag = 1;
       __syncthreads();
     }
-    transpose_plane(Rg, H, n, Rt, W, false, nullptr);
+    transpose_plane(Rg, H, n, Rt, W, false, nullptr, sn, st);
     __syncthreads();
-    for (int x = threadIdx.x; x < W; x += blockDim.x) fill_row(Rt + x * hb, Mt + x * hb, hb);
+    for (int x = threadIdx.x; x < W; x += blockDim.x) fill_row(Rt + x * st, Mt + x * st, hb);
     __syncthreads();
-    transpose_plane(Rt, W, hb, Rg, H, true, &flag);
+    transpose_plane(Rt, W, hb, Rg, H, true, &flag, st, sn);
     __syncthreads();
     const int f = flag;
     __syncthreads();
