@@ -59,7 +59,10 @@ size_t read_file_into(const std::string& path, std::vector<uint8_t>& buf);
 //   kStaged — one pread of the whole file into the caller's scratch buffer (cache-resident), then
 //             non-temporal stores into dst: no read-for-ownership of the destination lines, which
 //             the copy engine reads next anyway.
-enum class ReadMode { kDirect, kStaged };
+//   kMapped — the file is mapped (MAP_POPULATE) and parsed / packed / copied straight from the
+//             page-cache pages: no copy into a scratch buffer, at the price of a mapping and an
+//             unmap (TLB shootdown) per file. Otherwise behaves like kStaged.
+enum class ReadMode { kDirect, kStaged, kMapped };
 
 class SliceFile {
  public:
@@ -80,7 +83,9 @@ class SliceFile {
 
  private:
   void pread_all(void* dst, size_t n, size_t off);
+  const uint8_t* data() const { return map_ ? map_ : buf_->data(); }
   std::string path_;
+  const uint8_t* map_ = nullptr;  // kMapped: the whole file
   int fd_ = -1;
   size_t size_ = 0;
   ReadMode mode_ = ReadMode::kDirect;

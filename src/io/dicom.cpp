@@ -6,6 +6,7 @@
 
 #include <fcntl.h>
 #include <immintrin.h>
+#include <sys/mman.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
@@ -346,6 +347,7 @@ SliceFile::SliceFile(const std::string& path, ReadMode mode, size_t prefix)
 }
 
 SliceFile::~SliceFile() {
+  if (map_) ::munmap(const_cast<uint8_t*>(map_), size_);
   if (fd_ >= 0) ::close(fd_);
 }
 
@@ -360,6 +362,16 @@ void SliceFile::pread_all(void* dst, size_t n, size_t off) {
 }
 
 const Header& SliceFile::header(std::vector<uint8_t>& buf) {
+  buf_ = &buf;
+  if (mode_ == ReadMode::kMapped && size_ > 0) {
+    void* m = ::mmap(nullptr, size_, PROT_READ, MAP_PRIVATE | MAP_POPULATE, fd_, 0);
+    if (m == MAP_FAILED) throw SliceError("Cannot map file: " + path_);
+    map_ = static_cast<const uint8_t*>(m);
+    have_ = size_;
+    h_ = parse(map_, size_);
+    whole_ = true;
+    return h_;
+  }
   const size_t pre = mode_ == ReadMode::kStaged ? size_ : std::min(size_, prefix_);
   if (buf.size() < pre) buf.resize(pre);
   pread_all(buf.data(), pre, 0);
@@ -387,11 +399,11 @@ void SliceFile::pixels16(uint16_t* dst) {
   if (whole_) {
     const bool raw16 = h_.bits_allocated == 16 && h_.syntax != Syntax::kExplicitBE;
     const size_t n = (size_t)h_.rows * h_.cols * 2;
-    if (raw16 && mode_ == ReadMode::kStaged) {
+    if (raw16 && mode_ != ReadMode::kDirect) {
       if (h_.pixel_offset + n > size_) throw SliceError("Truncated pixel data");
-      stream_copy(dst, buf_->data() + h_.pixel_offset, n);
+      stream_copy(dst, data() + h_.pixel_offset, n);
     } else {
-      copy_pixels16(h_, buf_->data(), size_, dst);
+      copy_pixels16(h_, data(), size_, dst);
     }
     return;
   }
@@ -403,11 +415,11 @@ void SliceFile::pixels16(uint16_t* dst) {
 }
 
 const uint16_t* SliceFile::staged_samples() const {
-  if (!whole_ || mode_ != ReadMode::kStaged || !buf_) return nullptr;
+  if (!whole_ || mode_ == ReadMode::kDirect || !buf_) return nullptr;
   if (h_.bits_allocated != 16 || h_.syntax == Syntax::kExplicitBE) return nullptr;
   const size_t n = (size_t)h_.rows * h_.cols * 2;
   if (h_.pixel_offset + n > size_ || (h_.pixel_offset & 1)) return nullptr;
-  return reinterpret_cast<const uint16_t*>(buf_->data() + h_.pixel_offset);
+  return reinterpret_cast<const uint16_t*>(data() + h_.pixel_offset);
 }
 
 void stream_copy(void* dst, const void* src, size_t n) {

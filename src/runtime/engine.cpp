@@ -151,7 +151,7 @@ struct Engine::Impl {
   std::vector<uint8_t> jpeg_header;
   int32_t divs[64];
   PipeConsts pc{};
-  // Loader read path (dicom::ReadMode); NM03_LOAD_MODE=direct|staged, NM03_LOAD_PREFIX=<bytes>.
+  // Loader read path (dicom::ReadMode); NM03_LOAD_MODE=direct|staged|mapped, NM03_LOAD_PREFIX=<bytes>.
   // Staged is the default: 231k/232k/224k vs 221k/205k/223k slices/s for direct (interleaved,
   // tools/gpu_load_ab.sh); a 4 KiB direct prefix misaligns the pixel pread's destination and is
   // slower still (198k/187k/200k).
@@ -163,7 +163,9 @@ struct Engine::Impl {
   explicit Impl(const EngineConfig& c) : cfg(c), place(c.device) {
     if (const char* e = std::getenv("NM03_BATCH_TAPER"); e && *e) cfg.taper = *e != '0';
     if (const char* e = std::getenv("NM03_LOAD_MODE"); e && *e)
-      read_mode_ = std::string(e) == "staged" ? dicom::ReadMode::kStaged : dicom::ReadMode::kDirect;
+      read_mode_ = std::string(e) == "staged" ? dicom::ReadMode::kStaged
+                   : std::string(e) == "mapped" ? dicom::ReadMode::kMapped
+                                                : dicom::ReadMode::kDirect;
     if (const char* e = std::getenv("NM03_LOAD_PREFIX"); e && *e) read_prefix_ = (size_t)std::atol(e);
     if (const char* e = std::getenv("NM03_PACK12"); e && *e && *e == '0') pack12_ = false;
     if (const char* e = std::getenv("NM03_UPLOAD_CHUNK_KB"); e && *e) upload_chunk_ = (size_t)std::atol(e) << 10;

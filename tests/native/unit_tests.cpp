@@ -156,7 +156,8 @@ TEST(slice_file_modes_agree) {
     ReadMode m;
     size_t prefix;
   };
-  for (Mode md : {Mode{ReadMode::kDirect, 16384}, Mode{ReadMode::kDirect, 1024}, Mode{ReadMode::kStaged, 0}}) {
+  for (Mode md : {Mode{ReadMode::kDirect, 16384}, Mode{ReadMode::kDirect, 1024}, Mode{ReadMode::kStaged, 0},
+                  Mode{ReadMode::kMapped, 0}}) {
     SliceFile f(path, md.m, md.prefix);
     std::vector<uint8_t> scratch;
     const Header& h = f.header(scratch);
@@ -166,6 +167,10 @@ TEST(slice_file_modes_agree) {
     CHECK(std::equal(px.begin(), px.end(), buf.begin() + 3));
     CHECK(buf[0] == 0xABCD && buf[2] == 0xABCD);
     CHECK(f.direct() == (md.m == ReadMode::kDirect));
+    if (md.m != ReadMode::kDirect) {  // staged / mapped expose the samples in place
+      const uint16_t* sm = f.staged_samples();
+      CHECK(sm != nullptr && std::equal(px.begin(), px.end(), sm));
+    }
   }
 }
 
