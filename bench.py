@@ -93,6 +93,9 @@ def main():
     ap.add_argument("--keep-data", action="store_true", help="keep a generated dataset in tmpfs after the run")
     ap.add_argument("--keep-output", action="store_true")
     ap.add_argument("--graphs", action="store_true", help="hipGraph replay of the per-batch kernel chain")
+    ap.add_argument("--stream-steps", action="store_true",
+                    help="submit the K timed cohort passes as one work stream (the engine pipelines across pass "
+                         "boundaries as it does across patients) instead of one engine call per pass")
     ap.add_argument("--numa-data", choices=("auto", "off"), default=os.environ.get("NM03_BENCH_NUMA_DATA", "auto"),
                     help="auto: one input copy per NUMA node, each rank reads the copy on its GPU's node")
     args = ap.parse_args()
@@ -139,12 +142,20 @@ def main():
              "slot_cpu_s": 0.0}
     cg0 = cgroup_cpu_stat()
     ru0 = resource.getrusage(resource.RUSAGE_SELF)
-    for _ in range(args.steps):
-        with _roctx_range("bench.step"):
-            codes, msgs, times = engine.run_list(work)
+    if args.stream_steps:
+        stream = n.WorkList(mine * args.steps)
+        with _roctx_range("bench.steps"):
+            codes, msgs, times = engine.run_list(stream)
         ok += len(codes) - len(msgs)
         for k in stage:
             stage[k] += times[k]
+    else:
+        for _ in range(args.steps):
+            with _roctx_range("bench.step"):
+                codes, msgs, times = engine.run_list(work)
+            ok += len(codes) - len(msgs)
+            for k in stage:
+                stage[k] += times[k]
     torch.cuda.synchronize()
     barrier(ctx)
     dt = time.perf_counter() - t0
@@ -176,6 +187,7 @@ def main():
                 "batch_size": args.batch_size,
                 "streams": args.streams,
                 "threads": args.threads,
+                "stream_steps": bool(args.stream_steps),
                 "rank0_stage_s": {k: round(v, 4) for k, v in stage.items()},
                 # host CPU of the whole cgroup over the timed region (all ranks of this container)
                 "cgroup_cpu_ms_per_step": {k[:-5]: round((cg1[k] - cg0.get(k, 0)) / 1e3 / args.steps, 3)
