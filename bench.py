@@ -8,33 +8,32 @@ SRG band → seeded region growing → dilation 3 → render 512² (original + s
 the GPU → write both JPEG files per slice. Nothing is cached between steps.
 
 Weak scaling by default: with N ranks the global work list is N cohort replicas (distinct output
-trees) sharded contiguously, so every rank processes one full cohort per step; `--scaling strong`
-shards a single cohort instead.
+trees) sharded contiguously, so every rank processes one full cohort per step. The strong-scaling
+figure (BASELINE config 3: ONE 465-slice cohort sharded over the N ranks) is measured right after
+and reported under config.strong (`--scaling strong` makes it the headline value instead).
+
+Ranks: `python bench.py --gpus N` starts N rank processes itself (before anything touches a GPU)
+and supervises them; under torchrun (WORLD_SIZE set) each process is one rank. Either way the
+ranks talk through the native communicator the CLI uses (src/dist: RCCL over xGMI, or the
+shared-memory host comm when ranks share a GPU), bootstrapped via the torch rendezvous store.
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+    NM03_DEVICE_OVERRIDE=0 python bench.py --gpus 4      # 4 ranks sharing GPU 0 (rehearsal)
 """
 import argparse
 import json
 import os
 import resource
 import shutil
+import signal
+import socket
+import subprocess
 import sys
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
-
-import torch  # noqa: E402  (must precede the native extension: shared HIP runtime)
-
-import nm03_capstone_project_amd as nm  # noqa: E402
-from nm03_capstone_project_amd.parallel import (allreduce_max, allreduce_sum, auto_threads,  # noqa: E402
-                                                barrier, broadcast_bytes, cgroup_cpu_stat, init_from_env,
-                                                plan_cohort)
-from nm03_capstone_project_amd.parallel.cohort_runner import CohortPlan  # noqa: E402
-from nm03_capstone_project_amd.parallel.dist import shard_bounds  # noqa: E402
-from nm03_capstone_project_amd.parallel.numa_data import (ensure_node_replicas, localize_items,  # noqa: E402
-                                                          numa_nodes, replica_root)
 
 METRIC = "DICOM slices/sec through full pipeline (T1+C cohort) at 1/2/4/8 MI355X"
 # The reference publishes no number; BASELINE.md defines the comparison point as the measured
@@ -79,15 +78,18 @@ def _scratch():
     return shm if os.path.isdir(shm) and os.access(shm, os.W_OK) else "/tmp"
 
 
-def main():
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--scaling", choices=("weak", "strong"), default="weak")
+    ap.add_argument("--scaling", choices=("weak", "strong"), default="weak",
+                    help="which figure is the headline value; the other is reported next to it")
+    ap.add_argument("--no-secondary", action="store_true", help="skip the other scaling mode's measurement")
     ap.add_argument("--batch-size", type=int, default=64)
     ap.add_argument("--streams", type=int, default=6)
     ap.add_argument("--threads", type=int, default=0, help="host I/O threads per rank (0 = CPU budget / ranks, ≤16)")
+    ap.add_argument("--comm", choices=("auto", "rccl", "host"), default=os.environ.get("NM03_COMM", "auto"))
     ap.add_argument("--data-root", default=os.environ.get("NM03_BENCH_DATA", os.path.join(_scratch(), "nm03_bench_data")))
     ap.add_argument("--out-root", default=os.environ.get("NM03_BENCH_OUT", os.path.join(_scratch(), "nm03_bench_out")))
     ap.add_argument("--keep-data", action="store_true", help="keep a generated dataset in tmpfs after the run")
@@ -95,84 +97,212 @@ def main():
     ap.add_argument("--graphs", action="store_true", help="hipGraph replay of the per-batch kernel chain")
     ap.add_argument("--stream-steps", action="store_true",
                     help="submit the K timed cohort passes as one work stream (the engine pipelines across pass "
-                         "boundaries as it does across patients) instead of one engine call per pass")
+                         "boundaries as it does across patients) instead of one engine call per pass; every pass "
+                         "writes its own output tree")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="CPU rehearsal of the launcher, rendezvous, comm, sharding and aggregation: every step "
+                         "of a real run except the engine (no GPU); the JSON value is meaningless")
     ap.add_argument("--numa-data", choices=("auto", "off"), default=os.environ.get("NM03_BENCH_NUMA_DATA", "auto"),
                     help="auto: one input copy per NUMA node, each rank reads the copy on its GPU's node")
-    args = ap.parse_args()
+    return ap.parse_args(argv)
 
-    ctx = init_from_env()
+
+# ------------------------------------------------------------------------------------------------
+# Launcher: `--gpus N` without WORLD_SIZE. Runs before anything touches a GPU (no torch.cuda, no
+# HIP call in this process): it only spawns the N rank processes and watches them.
+# ------------------------------------------------------------------------------------------------
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch(args, argv, grace_s=5.0):
+    n = args.gpus
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env))
+    rc, failed_at = 0, None
+    while any(p.poll() is None for p in procs):
+        for r, p in enumerate(procs):
+            code = p.poll()
+            if code not in (None, 0) and rc == 0:
+                rc = code if code > 0 else 128 - code
+                failed_at = time.monotonic()
+                print(f"bench: rank {r} exited with status {code}", file=sys.stderr, flush=True)
+        if failed_at is not None:
+            waited = time.monotonic() - failed_at
+            for p in procs:
+                if p.poll() is None:
+                    if waited > 2 * grace_s:
+                        p.kill()
+                    elif waited > grace_s:
+                        p.send_signal(signal.SIGTERM)
+        time.sleep(0.01)
+    for r, p in enumerate(procs):
+        if p.returncode not in (0, None) and rc == 0:
+            rc = p.returncode if p.returncode > 0 else 128 - p.returncode
+            print(f"bench: rank {r} exited with status {p.returncode}", file=sys.stderr, flush=True)
+    return rc
+
+
+# ------------------------------------------------------------------------------------------------
+# One rank
+# ------------------------------------------------------------------------------------------------
+def _pass_items(items, out_root, k):
+    """The work list of stream-steps pass k: same inputs, output tree out_root/pass-k/..."""
+    out = []
+    made = set()
+    for f, od in items:
+        d = os.path.join(out_root, f"pass-{k:03d}", os.path.relpath(od, out_root))
+        if d not in made:
+            os.makedirs(d, exist_ok=True)
+            made.add(d)
+        out.append((f, d))
+    return out
+
+
+class _DryEngine:
+    """--dry-run stand-in for the native Engine: every slice 'succeeds' instantly."""
+
+    def run_list(self, work):
+        import numpy as np
+        zero = {k: 0.0 for k in ("load_s", "load_cpu_s", "h2d_s", "kernels_s", "write_s", "write_cpu_s",
+                                 "slot_cpu_s")}
+        return np.zeros(len(work), dtype=np.int32), {}, zero
+
+
+def run_rank(args):
+    import torch  # the native extension shares torch's HIP runtime: import torch first
+
+    import nm03_capstone_project_amd as nm
+    from nm03_capstone_project_amd.parallel.cohort_runner import CohortPlan, plan_cohort
+    from nm03_capstone_project_amd.parallel.dist import auto_threads, cgroup_cpu_stat, shard_bounds
+    from nm03_capstone_project_amd.parallel.native_comm import make_native_comm, rank_device, rank_env
+    from nm03_capstone_project_amd.parallel.numa_data import (ensure_node_replicas, localize_items, numa_nodes,
+                                                              replica_root)
+
+    rank, world, local_rank, local_world = rank_env()
+    device = rank_device(local_rank)
     if args.threads <= 0:
-        args.threads = auto_threads()
+        args.threads = auto_threads(local_world)
     n = nm.native()
+    if torch.cuda.is_available():
+        torch.cuda.set_device(device)
+    comm, comm_info = make_native_comm(rank, world, device, args.comm)
+    is_root = rank == 0
+
     # Input cohort in tmpfs: one copy per NUMA node on multi-socket hosts (numa_data.py), so every
     # rank reads the copy on its own GPU's node.
     nodes = numa_nodes(n.numa_node_cpus) if args.numa_data == "auto" else []
     roots = [replica_root(args.data_root, k) for k in nodes] or [args.data_root]
-    if ctx.local_rank == 0:
+    if local_rank == 0:
         ensure_node_replicas(args.data_root, nodes, lambda root: n.synth_cohort(root, threads=16), n.numa_node_cpus)
-    barrier(ctx)
-    while not all(os.path.exists(os.path.join(r, ".complete")) for r in roots):  # other hosts' local rank 0
-        time.sleep(0.1)
-    dev_node = n.numa_device_node(ctx.device_index) if nodes else -1
+    comm.barrier()
+    dev_node = n.numa_device_node(device) if nodes else -1
     local_root = replica_root(args.data_root, dev_node) if dev_node in nodes else roots[0]
 
-    replicas = ctx.world if args.scaling == "weak" else 1
-    plan_bytes = b""
-    if ctx.is_root:
-        plan_bytes = plan_cohort(roots[0], args.out_root, wipe=True, replicas=replicas).to_bytes()
-    plan = CohortPlan.from_bytes(broadcast_bytes(plan_bytes, ctx))
-    items = plan.items
-    lo, hi = shard_bounds(len(items), ctx.rank, ctx.world)
-    mine = localize_items(items[lo:hi], roots[0], local_root)
-
+    fail_rank = os.environ.get("NM03_BENCH_FAIL_RANK", "")  # fault injection (tests): this rank dies here
+    if fail_rank != "" and int(fail_rank) == rank:
+        print(f"bench: rank {rank}: injected failure", file=sys.stderr, flush=True)
+        os._exit(5)
     cfg = nm.PipelineConfig(batch_size=args.batch_size, streams=args.streams, threads=args.threads,
-                            device=ctx.device_index, graphs=args.graphs)
-    engine = n.Engine(cfg.engine_config())
-    work = n.WorkList(mine)  # the shard's work list in native form (built once, like the plan)
-    for _ in range(args.warmup):
-        codes, msgs, _ = engine.run_list(work)
-        if msgs:
-            raise SystemExit(f"rank {ctx.rank}: {len(msgs)} slices failed in warmup: {list(msgs.items())[:3]}")
+                            device=device, graphs=args.graphs)
+    engine = _DryEngine() if args.dry_run else n.Engine(cfg.engine_config())
 
-    barrier(ctx)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    ok = 0
-    stage = {"load_s": 0.0, "load_cpu_s": 0.0, "h2d_s": 0.0, "kernels_s": 0.0, "write_s": 0.0, "write_cpu_s": 0.0,
-             "slot_cpu_s": 0.0}
-    cg0 = cgroup_cpu_stat()
-    ru0 = resource.getrusage(resource.RUSAGE_SELF)
-    if args.stream_steps:
-        stream = n.WorkList(mine * args.steps)
-        with _roctx_range("bench.steps"):
-            codes, msgs, times = engine.run_list(stream)
-        ok += len(codes) - len(msgs)
-        for k in stage:
-            stage[k] += times[k]
-    else:
-        for _ in range(args.steps):
-            with _roctx_range("bench.step"):
-                codes, msgs, times = engine.run_list(work)
+    def shard(scaling, out_root):
+        """This rank's work list: weak = its own cohort replica, strong = its block of one cohort."""
+        replicas = world if scaling == "weak" else 1
+        plan_bytes = plan_cohort(roots[0], out_root, wipe=True, replicas=replicas).to_bytes() if is_root else b""
+        plan = CohortPlan.from_bytes(comm.broadcast_bytes(plan_bytes, 0))
+        items = plan.items
+        lo, hi = shard_bounds(len(items), rank, world)
+        return localize_items(items[lo:hi], roots[0], local_root), len(items)
+
+    def measure(scaling, out_root, steps, warmup):
+        mine, global_items = shard(scaling, out_root)
+        work = n.WorkList(mine)  # the shard's work list in native form (built once, like the plan)
+        for _ in range(warmup):
+            codes, msgs, _ = engine.run_list(work)
+            if msgs:
+                raise SystemExit(f"rank {rank}: {len(msgs)} slices failed in warmup: {list(msgs.items())[:3]}")
+        stream = None
+        if args.stream_steps:
+            stream = n.WorkList([it for k in range(steps) for it in _pass_items(mine, out_root, k)])
+        stage = {"load_s": 0.0, "load_cpu_s": 0.0, "h2d_s": 0.0, "kernels_s": 0.0, "write_s": 0.0,
+                 "write_cpu_s": 0.0, "slot_cpu_s": 0.0}
+        ok = 0
+        comm.barrier()
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+        cg0 = cgroup_cpu_stat()
+        ru0 = resource.getrusage(resource.RUSAGE_SELF)
+        t0 = time.perf_counter()
+        if stream is not None:
+            with _roctx_range("bench.steps"):
+                codes, msgs, times = engine.run_list(stream)
             ok += len(codes) - len(msgs)
             for k in stage:
                 stage[k] += times[k]
-    torch.cuda.synchronize()
-    barrier(ctx)
-    dt = time.perf_counter() - t0
-    cg1 = cgroup_cpu_stat()
-    ru1 = resource.getrusage(resource.RUSAGE_SELF)
-    dt = allreduce_max(dt, ctx)
-    total_ok = int(allreduce_sum(ok, ctx))
-    value = total_ok / dt
-    if ctx.is_root:
+        else:
+            for _ in range(steps):
+                with _roctx_range("bench.step"):
+                    codes, msgs, times = engine.run_list(work)
+                ok += len(codes) - len(msgs)
+                for k in stage:
+                    stage[k] += times[k]
+        t_own = time.perf_counter() - t0  # this rank's own time, before waiting for the others
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+        comm.barrier()
+        dt = time.perf_counter() - t0
+        cg1 = cgroup_cpu_stat()
+        ru1 = resource.getrusage(resource.RUSAGE_SELF)
+        cpu_ms = (ru1.ru_utime + ru1.ru_stime - ru0.ru_utime - ru0.ru_stime) * 1e3 / steps
+        dt = comm.allreduce_max([dt])[0]
+        total_ok = comm.allreduce_sum([ok])[0]
+        fields = ["slices", "slices_ok", "own_s", "process_cpu_ms_per_step"] + list(stage)
+        row = [float(len(mine) * steps), float(ok), t_own, cpu_ms] + [stage[k] for k in stage]
+        allrows = comm.allgather_f64(row)
+        per_rank = {f: [round(allrows[r * len(fields) + i], 6) for r in range(world)] for i, f in enumerate(fields)}
+        per_rank["slices_per_s"] = [round(s / max(t, 1e-12), 1) for s, t in zip(per_rank["slices_ok"], per_rank["own_s"])]
+        own = per_rank["own_s"]
+        return {
+            "value": total_ok / dt,
+            "ms_per_step": dt * 1e3 / steps,
+            "global_batch": global_items,
+            "slices_ok": int(total_ok),
+            "per_rank": per_rank,
+            "own_time_imbalance": round(max(own) / max(min(own), 1e-12), 4),
+            "rank0_stage_s": {k: round(v, 4) for k, v in stage.items()},
+            "rank0_process_cpu_ms_per_step": round(cpu_ms, 3),
+            # host CPU of the whole cgroup over the timed region (all ranks of this container)
+            "cgroup_cpu_ms_per_step": {k[:-5]: round((cg1[k] - cg0.get(k, 0)) / 1e3 / steps, 3)
+                                       for k in ("usage_usec", "throttled_usec") if k in cg1},
+        }
+
+    primary = measure(args.scaling, args.out_root, args.steps, args.warmup)
+    secondary = None
+    other = "strong" if args.scaling == "weak" else "weak"
+    if not args.no_secondary and world > 1:
+        secondary = measure(other, os.path.join(args.out_root, other), args.steps, 1)
+    elif not args.no_secondary:
+        secondary = {"value": primary["value"], "ms_per_step": primary["ms_per_step"],
+                     "global_batch": primary["global_batch"], "note": "1 rank: weak and strong coincide"}
+
+    if is_root:
+        value = primary["value"]
         rec = {
             "metric": METRIC,
             "value": round(value, 2),
             "unit": "slices/s",
-            "n_gpus": ctx.world,
+            "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": round(dt * 1e3 / args.steps, 3),
+            "ms_per_step": round(primary["ms_per_step"], 3),
             "higher_is_better": True,
             "scaling": args.scaling,
             "vs_baseline": (round(value / BASELINE_SLICES_PER_S, 3) if BASELINE_SLICES_PER_S else None),
@@ -181,33 +311,50 @@ def main():
             "config": {
                 "model": "NM03 T1+C pipeline: norm/clip -> VMF 7x7 -> sharpen 9x9 -> SRG[0.74,0.91] -> "
                          "dilate 3 -> render 512^2 x2 -> JPEG q75",
-                "global_batch": len(items),
+                "global_batch": primary["global_batch"],
                 "seq_len": 256,
-                "parallelism": f"dp{ctx.world}",
+                "parallelism": f"dp{world}",
                 "batch_size": args.batch_size,
                 "streams": args.streams,
                 "threads": args.threads,
                 "stream_steps": bool(args.stream_steps),
-                "rank0_stage_s": {k: round(v, 4) for k, v in stage.items()},
-                # host CPU of the whole cgroup over the timed region (all ranks of this container)
-                "cgroup_cpu_ms_per_step": {k[:-5]: round((cg1[k] - cg0.get(k, 0)) / 1e3 / args.steps, 3)
-                                           for k in ("usage_usec", "throttled_usec") if k in cg1},
-                "rank0_process_cpu_ms_per_step": round((ru1.ru_utime + ru1.ru_stime - ru0.ru_utime - ru0.ru_stime)
-                                                       * 1e3 / args.steps, 3),
+                "comm": comm_info,
+                "rank0_stage_s": primary["rank0_stage_s"],
+                "cgroup_cpu_ms_per_step": primary["cgroup_cpu_ms_per_step"],
+                "rank0_process_cpu_ms_per_step": primary["rank0_process_cpu_ms_per_step"],
+                "per_rank": primary["per_rank"],
+                "own_time_imbalance": primary["own_time_imbalance"],
                 "storage": {"data": local_root, "input_copies": len(roots), "out": args.out_root},
             },
         }
+        if secondary is not None:
+            rec["config"][other] = {k: (round(v, 3) if isinstance(v, float) else v) for k, v in secondary.items()
+                                    if k in ("value", "ms_per_step", "global_batch", "per_rank", "note",
+                                             "own_time_imbalance")}
         print(json.dumps(rec), flush=True)
-    if not args.keep_output and ctx.is_root:
+    comm.barrier()
+    del engine
+    if not args.keep_output and is_root:
         shutil.rmtree(args.out_root, ignore_errors=True)
     # tmpfs holds data in RAM: drop a generated dataset unless asked to keep it (local rank 0,
     # after the final barrier every rank has passed).
-    if ctx.local_rank == 0 and not args.keep_data and args.data_root.startswith("/dev/shm/"):
+    if local_rank == 0 and not args.keep_data and args.data_root.startswith("/dev/shm/"):
         for r in roots:
             shutil.rmtree(r, ignore_errors=True)
-    if ctx.world > 1:
-        torch.distributed.destroy_process_group()
+    return 0
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse_args(argv)
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is None:
+        if args.gpus > 1:
+            return launch(args, argv)
+    elif int(world_env) != args.gpus:
+        raise SystemExit(f"bench: WORLD_SIZE={world_env} but --gpus {args.gpus}: launch with matching values")
+    return run_rank(args)
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

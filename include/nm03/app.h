@@ -10,6 +10,7 @@
 #include <string>
 #include <vector>
 
+#include "nm03/comm.h"
 #include "nm03/engine.h"
 
 namespace nm03::app {
@@ -18,7 +19,10 @@ struct AppConfig {
   std::string data_root;  // default: cohort::default_data_root()
   std::string out_dir;    // default per CLI: ../out-sequential, ../out-parallel, ../out-test
   EngineConfig engine;
-  int gpus = 1;            // ranks (one process per GPU)
+  // Ranks, one process per GPU. 0 = every visible GPU: the no-argument img_processing_parallel
+  // uses the whole node, as the reference's omp_set_num_threads(16) uses the whole laptop
+  // (main_parallel.cpp:401).
+  int gpus = 0;
   bool quiet = false;
   bool cpu = false;        // test_pipeline: golden CPU path (BASELINE config 1)
   bool montage = true;     // test_pipeline: 5-view montage JPEG (headless MultiViewWindow)
@@ -39,5 +43,9 @@ int run_test_pipeline(const AppConfig& cfg);
 // Number of GPUs visible to this process, counted WITHOUT initialising HIP (KFD topology +
 // HIP/ROCR_VISIBLE_DEVICES), so the launcher can still fork safely afterwards.
 int visible_gpu_count();
+
+// Ranks for img_processing_parallel: --gpus N, or every visible GPU when unset. Throws when N
+// exceeds the visible GPUs and no NM03_DEVICE_OVERRIDE shares one device between ranks.
+int resolve_gpus(const AppConfig& cfg, const LaunchOptions& lo);
 
 }  // namespace nm03::app

@@ -7,19 +7,36 @@
 // timed region. No pixel data crosses GPUs: each rank reads its own DICOMs and writes its own JPEGs.
 //
 //   RcclComm      — RCCL (ncclBroadcast / ncclAllGather / ncclAllReduce) on device staging
-//                   buffers, i.e. over xGMI inside an 8×MI355X node.
+//                   buffers, i.e. over xGMI inside an 8×MI355X node. Non-blocking init and
+//                   deadline-bounded waits: a dead or stuck peer ends in ncclCommAbort + CommError.
+//   HostComm      — ranks of one node over a process-shared memory segment (futex barrier, one
+//                   slot per rank). Used when ranks share a GPU (RCCL refuses two ranks per
+//                   device: rehearsals on a one-GPU box) or when NM03_COMM=host.
 //   LoopbackComm  — N in-process ranks (threads) sharing memory; the test double used by the CPU
 //                   test-suite (no GPU needed).
+//
+// Failure model (the reference turns every failure into a message + continue or
+// exit 1, main_parallel.cpp:352-356, 377-380, 406-409): every blocking collective has a deadline
+// (NM03_COMM_TIMEOUT_S, default 120 s). The shared segment carries a job-wide abort flag; the
+// launcher raises it the moment a rank exits non-zero, so peers blocked in a collective fail
+// within milliseconds instead of hanging, and the job exits with "Rank k exited with status s".
 #pragma once
 
 #include <cstddef>
 #include <cstdint>
 #include <functional>
 #include <memory>
+#include <stdexcept>
 #include <string>
 #include <vector>
 
 namespace nm03 {
+
+// A collective could not complete: timeout, a peer failed (abort flag), or an RCCL error.
+class CommError : public std::runtime_error {
+ public:
+  explicit CommError(const std::string& m) : std::runtime_error(m) {}
+};
 
 class Comm {
  public:
@@ -39,22 +56,94 @@ class Comm {
   std::vector<std::vector<uint8_t>> allgather_bytes(const std::vector<uint8_t>& mine);  // variable sizes
 };
 
+// Deadline of one blocking collective wait: NM03_COMM_TIMEOUT_S (default 120 s).
+double comm_timeout_s();
+
+// ---- process-shared control segment -------------------------------------------------------------
+// Host collectives, the RCCL unique-id hand-off and the job abort flag live here.
+class ShmSegment {
+ public:
+  ~ShmSegment();
+  int size() const;
+  size_t slot_bytes() const;
+  // Anonymous MAP_SHARED mapping: create BEFORE fork, every child inherits it.
+  static std::shared_ptr<ShmSegment> create_anonymous(int n, size_t slot_bytes = 1 << 20);
+  // Named segment for independently launched ranks (torchrun): rank 0 creates it under a fresh
+  // random name and publishes the name out of band (e.g. the torch TCPStore); the others attach.
+  // Rank 0's object unlinks the name once every rank has attached (the mapping stays valid).
+  static std::shared_ptr<ShmSegment> create_named(int n, std::string* name, size_t slot_bytes = 1 << 20);
+  static std::shared_ptr<ShmSegment> attach_named(const std::string& name, int n, double timeout_s);
+  // Rank 0 (named creator): wait until all n ranks attached, then unlink the name.
+  void wait_attached_and_unlink(double timeout_s);
+
+  // Abort flag: the first caller records `rank` as the failed one; waiters wake and throw.
+  void raise_abort(int rank);
+  bool aborted() const;
+  int abort_rank() const;  // -1 when not aborted
+  // Throws CommError if the job was aborted.
+  void check_abort(int self) const;
+
+  // RCCL unique id (128 bytes) published by rank 0, awaited by the others (deadline + abort).
+  void publish_uid(const std::vector<uint8_t>& uid);
+  std::vector<uint8_t> wait_uid(int self, double timeout_s) const;
+
+  // Generation barrier across all ranks of the segment; deadline + abort aware.
+  void barrier(int self, double timeout_s);
+  uint8_t* slot(int r) const;
+
+  struct Header;
+
+ private:
+  ShmSegment() = default;
+  Header* h_ = nullptr;
+  size_t map_bytes_ = 0;
+  std::string unlink_name_;
+};
+
 // In-process loopback group of n ranks; comms[i]->rank() == i. Each must be used by its own thread.
 std::vector<std::unique_ptr<Comm>> make_loopback_group(int n);
 
+// Host collectives over a shared segment (one comm per rank process).
+// timeout_s ≤ 0: comm_timeout_s().
+std::unique_ptr<Comm> make_host_comm(std::shared_ptr<ShmSegment> seg, int rank, double timeout_s = -1);
+
 // RCCL communicator for `rank` of `size`, bound to HIP device `device`. `unique_id` is the
-// 128-byte ncclUniqueId produced by rank 0 (rccl_unique_id()).
-std::unique_ptr<Comm> make_rccl_comm(int rank, int size, const std::vector<uint8_t>& unique_id, int device);
+// 128-byte ncclUniqueId produced by rank 0 (rccl_unique_id()). `seg` (optional) supplies the job
+// abort flag that bounded waits also watch.
+std::unique_ptr<Comm> make_rccl_comm(int rank, int size, const std::vector<uint8_t>& unique_id, int device,
+                                     std::shared_ptr<ShmSegment> seg = nullptr, double timeout_s = -1);
 std::vector<uint8_t> rccl_unique_id();
 
 // Single-rank communicator (no-ops).
 std::unique_ptr<Comm> make_self_comm();
 
-// Fork `n-1` child processes BEFORE any HIP call (fork after HIP init is unsafe), hand every rank
-// the RCCL unique id through pipes, and run body(rank, n, comm) in each. Returns rank 0's exit
-// code or the first non-zero child status (a dead rank makes the job fail).
-// `use_rccl=false` gives every rank a self/loopback-free comm (testing the launcher only).
-int launch_ranks(int n, const std::function<int(int rank, int size, Comm& comm)>& body, bool use_rccl = true);
+// ---- launcher ----------------------------------------------------------------------------------
+struct LaunchOptions {
+  // "rccl" | "host" | "auto" (default; NM03_COMM overrides): RCCL when every rank has its own
+  // GPU, the host comm when ranks share one (device_override ≥ 0).
+  std::string comm = "auto";
+  // ≥ 0: every rank uses this HIP device (NM03_DEVICE_OVERRIDE), e.g. N ranks on a one-GPU box.
+  int device_override = -1;
+  // After the first failed rank, peers get this long to fail on the abort flag by themselves
+  // before they are sent SIGTERM (and SIGKILL after the same again).
+  double grace_s = 5.0;
+  // Collective deadline for the ranks' comms; ≤ 0: comm_timeout_s().
+  double timeout_s = -1;
+  int device_of(int rank) const { return device_override >= 0 ? device_override : rank; }
+  // The backend actually used for n ranks.
+  std::string resolve(int n) const;
+  // Defaults from the environment (NM03_COMM, NM03_DEVICE_OVERRIDE).
+  static LaunchOptions from_env();
+};
+
+// n == 1: body runs in this process with a self comm. n > 1: fork n rank processes BEFORE any HIP
+// call (fork after HIP init is unsafe); this process becomes a supervisor that never touches the
+// GPU: it reaps ranks as they exit, raises the abort flag on the first non-zero exit, prints
+// "Rank k exited with status s", terminates stragglers after the grace period, and returns the
+// first non-zero status (0 when every rank succeeded). Children die with the supervisor
+// (PR_SET_PDEATHSIG). Rank r runs body(r, n, comm) on device opts.device_of(r).
+int launch_ranks(int n, const std::function<int(int rank, int size, Comm& comm)>& body,
+                 const LaunchOptions& opts = LaunchOptions::from_env());
 
 // Simple binary (de)serialisation helpers for messages.
 struct ByteWriter {

@@ -40,6 +40,7 @@ struct FaultPlan {
   int64_t corrupt_dicom = -1;  // work-item index whose DICOM is treated as corrupt
   int64_t fail_batch = -1;     // batch index whose device work fails
   int64_t fail_write = -1;     // work-item index whose JPEG export fails
+  int64_t rank_exit = -1;      // rank (img_processing_parallel) that dies after the plan broadcast
 };
 const FaultPlan& fault_plan();  // parsed once from NM03_FAULT
 

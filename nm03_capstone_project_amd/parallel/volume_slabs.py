@@ -107,6 +107,10 @@ def grow_slabs(band, z0, seeds, ctx=None, connectivity=6, backend="cpu", device=
     dl = band.shape[0]
     rank = dist.get_rank() if _active() else 0
     world = dist.get_world_size() if _active() else 1
+    # Every slab needs a plane (edge planes are exchanged): agreed collectively, so all ranks raise
+    # together instead of one rank failing while its peers wait in the all-gather.
+    if world > 1 and -allreduce_max(-float(dl), ctx) < 1:
+        raise ValueError("grow_slabs: every rank needs at least one plane (depth < world size)")
     mine = [(int(x), int(y), int(z) - z0) for (x, y, z) in seeds if z0 <= int(z) < z0 + dl]
     region, sweeps = be.grow(band, None, mine, connectivity)
     rounds = 1
@@ -189,6 +193,8 @@ def run_volume_slabs(volume=None, ctx=None, config=None, connectivity=6, dilatio
     rank = dist.get_rank() if _active() else 0
     world = dist.get_world_size() if _active() else 1
     depth, h, w = (volume if volume is not None else band).shape
+    if depth < world:  # same shape on every rank: all raise together, before any collective
+        raise ValueError(f"run_volume_slabs: depth {depth} < {world} ranks leaves empty slabs")
     z0, z1 = shard_bounds(depth, rank, world)
     device = ctx.device if (ctx is not None and ctx.device is not None) else None
     be = _backend(backend, device)

@@ -19,6 +19,7 @@
 #include "nm03/dicom.h"
 #include "nm03/golden.h"
 #include "nm03/jpeg.h"
+#include "nm03/log.h"
 #include "nm03/metaimage.h"
 #include "nm03/volume.h"
 
@@ -53,7 +54,8 @@ void usage(const std::string& which) {
             << "  --resume               keep existing outputs; skip slices whose two JPEGs exist\n"
             << "  --quiet                suppress per-slice progress lines\n"
             << "env: NM03_DATA_ROOT, NM03_LOG=info|warn|error|none, NM03_ROCTX=1,\n"
-            << "     NM03_FAULT=corrupt_dicom:<i>,fail_batch:<k>,fail_write:<j>\n";
+            << "     NM03_FAULT=corrupt_dicom:<i>,fail_batch:<k>,fail_write:<j>,rank_exit:<r>\n"
+            << "     NM03_COMM=auto|rccl|host, NM03_DEVICE_OVERRIDE=<device>, NM03_COMM_TIMEOUT_S=<s>\n";
 }
 
 void write_json(const std::string& path, const std::string& body) {
@@ -123,7 +125,7 @@ AppConfig parse_args(int argc, char** argv, const std::string& which) {
     else if (a == "--out") c.out_dir = val();
     else if (a == "--gpus") {
       std::string v = val();
-      c.gpus = v == "all" ? std::max(1, visible_gpu_count()) : std::atoi(v.c_str());
+      c.gpus = v == "all" ? 0 : std::max(1, std::atoi(v.c_str()));
     } else if (a == "--device") c.engine.device = std::atoi(val().c_str());
     else if (a == "--batch-size") c.engine.batch_size = std::atoi(val().c_str());
     else if (a == "--streams") c.engine.streams = std::atoi(val().c_str());
@@ -148,7 +150,6 @@ AppConfig parse_args(int argc, char** argv, const std::string& which) {
       std::exit(2);
     }
   }
-  if (c.gpus < 1) c.gpus = 1;
   return c;
 }
 
@@ -214,9 +215,22 @@ int run_sequential(const AppConfig& cfg) {
             for (size_t i = 0; i < st.size(); ++i) {
               if (st[i].code == kSliceOk) {
                 ++ok;
+              } else if (st[i].code == kSliceDeviceError) {
+                // Not a pipeline (fast::Exception-class) error: the reference's outer per-image
+                // catch reports these (main_sequential.cpp:291-293).
+                std::cerr << "Failed to process image " << (i + 1) << " for patient " << pid
+                          << ". Moving to next image." << std::endl;
               } else {
+                std::string e = st[i].message;
+                if (st[i].code == kSliceExportError) {
+                  // exportProcessedImage logs and rethrows (main_sequential.cpp:74-76), then
+                  // processSingleImage logs the same error again (:267-269).
+                  static const std::string kPrefix = "Error in export stage: ";
+                  if (e.compare(0, kPrefix.size(), kPrefix) == 0) e = e.substr(kPrefix.size());
+                  std::cerr << kPrefix << e << std::endl;
+                }
                 std::cerr << "Error processing file " << items[i].path << ":\n"
-                          << "Detailed error: " << st[i].message << std::endl;  // :268-269
+                          << "Detailed error: " << e << std::endl;  // :268-269
               }
             }
             total.load_s += t.load_s;
@@ -297,16 +311,56 @@ std::vector<PatientPlan> decode_plan(const std::vector<uint8_t>& b) {
   return pl;
 }
 
-int parallel_rank(const AppConfig& cfg, int rank, int size, Comm& comm) {
+// Per-rank figures all-gathered to rank 0 for the --json report.
+constexpr const char* kRankFields[] = {"slices",      "slices_ok", "wall_s",  "engine_setup_s", "load_s",
+                                       "load_cpu_s",  "h2d_s",     "kernels_s", "write_s",      "write_cpu_s",
+                                       "slot_cpu_s",  "jpeg_fallbacks"};
+constexpr size_t kNumRankFields = sizeof(kRankFields) / sizeof(kRankFields[0]);
+
+std::string per_rank_json(const std::vector<std::vector<double>>& rows) {
+  std::ostringstream o;
+  o << "{";
+  for (size_t f = 0; f < kNumRankFields; ++f) {
+    o << (f ? ", " : "") << "\"" << kRankFields[f] << "\": [";
+    for (size_t r = 0; r < rows.size(); ++r) o << (r ? ", " : "") << fmt(rows[r][f], 9);
+    o << "]";
+  }
+  // Imbalance of the processing wall time across ranks (max / min), the first thing to look at
+  // when a scaling curve bends.
+  double mx = 0, mn = 1e300;
+  for (const auto& r : rows) {
+    mx = std::max(mx, r[2]);
+    mn = std::min(mn, r[2]);
+  }
+  o << ", \"wall_imbalance\": " << fmt(mn > 0 ? mx / mn : 1.0, 6) << "}";
+  return o.str();
+}
+
+int parallel_rank(const AppConfig& cfg, int rank, int size, Comm& comm, int device) {
   const std::string base = cohort::cohort_dir(cfg.data_root);
   EngineConfig ec = cfg.engine;
-  if (size > 1) ec.device = rank;
+  ec.device = device;
   const double t_setup = now_s();
-  Engine engine(ec);
+  // An engine that fails to come up on one rank must not leave the others blocked in the first
+  // collective: agree on it before going on.
+  std::unique_ptr<Engine> engine_p;
+  std::string setup_error;
+  try {
+    engine_p = std::make_unique<Engine>(ec);
+  } catch (const std::exception& e) {
+    setup_error = e.what();
+  }
+  int64_t setup_failed = setup_error.empty() ? 0 : 1;
+  comm.allreduce_sum_i64(&setup_failed, 1);
+  if (setup_failed) {
+    if (!setup_error.empty()) std::cerr << "Fatal error: rank " << rank << " (device " << device << "): " << setup_error << std::endl;
+    return 1;
+  }
+  Engine& engine = *engine_p;
   const double t_start = now_s();
   const double setup_s = t_start - t_setup;
-  double proc_wall = 0;
-  int64_t total_ok = 0, total_slices = 0;
+  double proc_wall = 0, my_wall = 0;
+  int64_t total_ok = 0, total_slices = 0, my_slices = 0, my_ok = 0;
   StageTimes agg;
   for (int rep = 0; rep < cfg.repeat; ++rep) {
     // ---- plan on rank 0 --------------------------------------------------------------------
@@ -356,6 +410,10 @@ int parallel_rank(const AppConfig& cfg, int rank, int size, Comm& comm) {
       return 1;
     }
     comm.broadcast_bytes(plan_bytes, 0);  // ncclBroadcast of the serialized work list
+    if (fault_plan().rank_exit == rank && size > 1) {  // NM03_FAULT=rank_exit:<r>: a rank dies mid-job
+      std::cerr << "injected fault: rank " << rank << " exits" << std::endl;
+      _exit(9);
+    }
     std::vector<PatientPlan> plan = decode_plan(plan_bytes);
     std::vector<WorkItem> items;
     std::vector<int> owner;
@@ -372,15 +430,21 @@ int parallel_rank(const AppConfig& cfg, int rank, int size, Comm& comm) {
     const double t0 = now_s();
     StageTimes t;
     std::vector<SliceStatus> st = engine.run(mine, &t);
+    my_wall += now_s() - t0;  // this rank's own processing time (before waiting for the others)
     comm.barrier();
     double wall = now_s() - t0;
     comm.allreduce_max_f64(&wall, 1);
     proc_wall += wall;
     agg.load_s += t.load_s;
+    agg.load_cpu_s += t.load_cpu_s;
     agg.h2d_s += t.h2d_s;
     agg.kernels_s += t.kernels_s;
     agg.write_s += t.write_s;
+    agg.write_cpu_s += t.write_cpu_s;
+    agg.slot_cpu_s += t.slot_cpu_s;
     agg.jpeg_fallbacks += t.jpeg_fallbacks;
+    my_slices += (int64_t)mine.size();
+    for (const auto& s : st) my_ok += s.code == kSliceOk;
     // ---- gather statuses -------------------------------------------------------------------
     ByteWriter w;
     w.u32((uint32_t)st.size());
@@ -446,7 +510,16 @@ int parallel_rank(const AppConfig& cfg, int rank, int size, Comm& comm) {
   }
   double tot = now_s() - t_start;
   comm.allreduce_max_f64(&tot, 1);
+  // Per-rank stage figures, all-gathered (fields: kRankFields).
+  const double mine_row[kNumRankFields] = {(double)my_slices, (double)my_ok,     my_wall,          setup_s,
+                                           agg.load_s,        agg.load_cpu_s,    agg.h2d_s,        agg.kernels_s,
+                                           agg.write_s,       agg.write_cpu_s,   agg.slot_cpu_s,   (double)agg.jpeg_fallbacks};
+  std::vector<double> all_rows(kNumRankFields * (size_t)size);
+  comm.allgather(mine_row, sizeof(mine_row), all_rows.data());
   if (rank == 0) {
+    std::vector<std::vector<double>> rows((size_t)size);
+    for (int r = 0; r < size; ++r)
+      rows[r].assign(all_rows.begin() + (size_t)r * kNumRankFields, all_rows.begin() + (size_t)(r + 1) * kNumRankFields);
     write_json(cfg.json, std::string("{\"mode\": \"parallel\", \"gpus\": ") + std::to_string(size) + ", \"backend\": \"" +
                              comm.backend() + "\", \"repeat\": " + std::to_string(cfg.repeat) + ", \"engine_setup_s\": " +
                              fmt(setup_s) + ", \"wall_s\": " + fmt(tot) +
@@ -455,18 +528,32 @@ int parallel_rank(const AppConfig& cfg, int rank, int size, Comm& comm) {
                              fmt(total_ok / std::max(proc_wall, 1e-9)) + ", \"rank0\": {\"load_s\": " + fmt(agg.load_s) +
                              ", \"h2d_s\": " + fmt(agg.h2d_s) + ", \"kernels_s\": " + fmt(agg.kernels_s) +
                              ", \"write_s\": " + fmt(agg.write_s) + ", \"jpeg_fallbacks\": " +
-                             std::to_string(agg.jpeg_fallbacks) + "}}");
+                             std::to_string(agg.jpeg_fallbacks) + "}, \"per_rank\": " + per_rank_json(rows) + "}");
   }
   return 0;
 }
 
 }  // namespace
 
+int resolve_gpus(const AppConfig& cfg, const LaunchOptions& lo) {
+  const int visible = visible_gpu_count();
+  const int n = cfg.gpus > 0 ? cfg.gpus : std::max(1, visible);  // default: every visible GPU
+  if (n > 1 && lo.device_override < 0 && visible > 0 && n > visible)
+    throw std::runtime_error("--gpus " + std::to_string(n) + " exceeds the " + std::to_string(visible) +
+                             " visible GPU(s); set NM03_DEVICE_OVERRIDE=<device> to run several ranks on one GPU");
+  return n;
+}
+
 int run_parallel(const AppConfig& cfg) {
   try {
     cohort::make_dirs(cfg.out_dir);  // OptimizedParallelProcessor ctor (main_parallel.cpp:219-231)
     if (cfg.mode == "3d") return run_volume_cohort(cfg);
-    return launch_ranks(cfg.gpus, [&](int rank, int size, Comm& comm) { return parallel_rank(cfg, rank, size, comm); });
+    LaunchOptions lo = LaunchOptions::from_env();
+    const int n = resolve_gpus(cfg, lo);
+    return launch_ranks(n, [&](int rank, int size, Comm& comm) {
+      const int dev = size > 1 ? lo.device_of(rank) : lo.device_override >= 0 ? lo.device_override : cfg.engine.device;
+      return parallel_rank(cfg, rank, size, comm, dev);
+    }, lo);
   } catch (const std::exception& e) {
     std::cerr << "Fatal error: " << e.what() << std::endl;  // :407-408
     return 1;

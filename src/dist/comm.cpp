@@ -1,18 +1,21 @@
-// Comm implementations: loopback (threads), self, RCCL over xGMI, and the fork-based launcher.
+// Comm implementations: loopback (threads), self, host (shared segment across processes), and the
+// fork-based launcher with its supervisor. RCCL lives in rccl_comm.cpp, the segment in shm.cpp.
 #include "nm03/comm.h"
 
-#include <hip/hip_runtime_api.h>
-#include <rccl/rccl.h>
+#include <signal.h>
+#include <sys/prctl.h>
 #include <sys/wait.h>
 #include <unistd.h>
 
 #include <algorithm>
+#include <cerrno>
+#include <chrono>
 #include <condition_variable>
+#include <cstdio>
 #include <cstring>
 #include <mutex>
 #include <stdexcept>
-
-#include "nm03/common.h"
+#include <thread>
 
 namespace nm03 {
 
@@ -84,11 +87,23 @@ std::vector<std::vector<uint8_t>> Comm::allgather_bytes(const std::vector<uint8_
   return out;
 }
 
+namespace {
+
+// Reductions shared by the host-memory comms: all-gather, then fold in rank order.
+template <class T, class Op>
+void fold_allgather(Comm& c, T* v, size_t n, Op op) {
+  std::vector<T> all(n * (size_t)c.size());
+  c.allgather(v, n * sizeof(T), all.data());
+  for (size_t i = 0; i < n; ++i) {
+    T s = all[i];
+    for (int r = 1; r < c.size(); ++r) s = op(s, all[(size_t)r * n + i]);
+    v[i] = s;
+  }
+}
+
 // ---------------------------------------------------------------------------------------------
 // Loopback: shared hub, every collective = deposit + barrier + read + barrier.
 // ---------------------------------------------------------------------------------------------
-namespace {
-
 struct Hub {
   int n;
   std::mutex m;
@@ -104,8 +119,8 @@ struct Hub {
       arrived = 0;
       ++generation;
       cv.notify_all();
-    } else {
-      cv.wait(g, [&] { return generation != gen; });
+    } else if (!cv.wait_for(g, std::chrono::duration<double>(comm_timeout_s()), [&] { return generation != gen; })) {
+      throw CommError("loopback collective timed out");
     }
   }
 };
@@ -129,22 +144,10 @@ class LoopbackComm final : public Comm {
     hub_->sync();
   }
   void allreduce_sum_i64(int64_t* v, size_t n) override {
-    std::vector<int64_t> all(n * hub_->n);
-    allgather(v, n * sizeof(int64_t), all.data());
-    for (size_t i = 0; i < n; ++i) {
-      int64_t s = 0;
-      for (int r = 0; r < hub_->n; ++r) s += all[(size_t)r * n + i];
-      v[i] = s;
-    }
+    fold_allgather(*this, v, n, [](int64_t a, int64_t b) { return a + b; });
   }
   void allreduce_max_f64(double* v, size_t n) override {
-    std::vector<double> all(n * hub_->n);
-    allgather(v, n * sizeof(double), all.data());
-    for (size_t i = 0; i < n; ++i) {
-      double s = all[i];
-      for (int r = 1; r < hub_->n; ++r) s = std::max(s, all[(size_t)r * n + i]);
-      v[i] = s;
-    }
+    fold_allgather(*this, v, n, [](double a, double b) { return std::max(a, b); });
   }
   void barrier() override { hub_->sync(); }
 
@@ -166,114 +169,109 @@ class SelfComm final : public Comm {
 };
 
 // ---------------------------------------------------------------------------------------------
-// RCCL: collectives on a device staging buffer on a private stream.
+// Host comm: ranks in separate processes over a ShmSegment. Payloads larger than a slot move in
+// slot-sized chunks; every chunk is deposit + barrier + read + barrier.
 // ---------------------------------------------------------------------------------------------
-void nccl_check(ncclResult_t r, const char* what) {
-  if (r != ncclSuccess) throw DeviceError(std::string(what) + ": " + ncclGetErrorString(r));
-}
-void hip_ck(hipError_t e, const char* what) {
-  if (e != hipSuccess) throw DeviceError(std::string(what) + ": " + hipGetErrorString(e));
-}
-
-class RcclComm final : public Comm {
+class HostComm final : public Comm {
  public:
-  RcclComm(int rank, int size, const std::vector<uint8_t>& uid, int device) : rank_(rank), size_(size), dev_(device) {
-    if (uid.size() != sizeof(ncclUniqueId)) throw DeviceError("bad ncclUniqueId size");
-    ncclUniqueId id;
-    std::memcpy(&id, uid.data(), sizeof(id));
-    hip_ck(hipSetDevice(dev_), "hipSetDevice");
-    hip_ck(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "hipStreamCreate");
-    nccl_check(ncclCommInitRank(&comm_, size_, id, rank_), "ncclCommInitRank");
-  }
-  ~RcclComm() override {
-    if (comm_) ncclCommDestroy(comm_);
-    if (buf_) (void)hipFree(buf_);
-    if (stream_) (void)hipStreamDestroy(stream_);
+  HostComm(std::shared_ptr<ShmSegment> seg, int rank, double timeout_s)
+      : seg_(std::move(seg)), rank_(rank), timeout_(timeout_s > 0 ? timeout_s : comm_timeout_s()) {
+    if (rank_ < 0 || rank_ >= seg_->size()) throw CommError("host comm rank out of range");
   }
   int rank() const override { return rank_; }
-  int size() const override { return size_; }
-  const char* backend() const override { return "rccl"; }
-
+  int size() const override { return seg_->size(); }
+  const char* backend() const override { return "host"; }
   void broadcast(void* buf, size_t bytes, int root) override {
-    if (!bytes) return;
-    uint8_t* d = stage(bytes);
-    if (rank_ == root) hip_ck(hipMemcpyAsync(d, buf, bytes, hipMemcpyHostToDevice, stream_), "H2D");
-    nccl_check(ncclBroadcast(d, d, bytes, ncclUint8, root, comm_, stream_), "ncclBroadcast");
-    hip_ck(hipMemcpyAsync(buf, d, bytes, hipMemcpyDeviceToHost, stream_), "D2H");
-    wait();
+    const size_t cap = seg_->slot_bytes();
+    for (size_t off = 0; off < bytes; off += cap) {
+      const size_t len = std::min(cap, bytes - off);
+      if (rank_ == root) std::memcpy(seg_->slot(root), (uint8_t*)buf + off, len);
+      seg_->barrier(rank_, timeout_);
+      if (rank_ != root) std::memcpy((uint8_t*)buf + off, seg_->slot(root), len);
+      seg_->barrier(rank_, timeout_);
+    }
   }
   void allgather(const void* send, size_t bytes, void* recv) override {
-    if (!bytes) return;
-    uint8_t* d = stage(bytes * (size_t)(size_ + 1));
-    uint8_t* dsend = d + bytes * (size_t)size_;
-    hip_ck(hipMemcpyAsync(dsend, send, bytes, hipMemcpyHostToDevice, stream_), "H2D");
-    nccl_check(ncclAllGather(dsend, d, bytes, ncclUint8, comm_, stream_), "ncclAllGather");
-    hip_ck(hipMemcpyAsync(recv, d, bytes * size_, hipMemcpyDeviceToHost, stream_), "D2H");
-    wait();
+    const size_t cap = seg_->slot_bytes();
+    const int n = size();
+    for (size_t off = 0; off < bytes; off += cap) {
+      const size_t len = std::min(cap, bytes - off);
+      std::memcpy(seg_->slot(rank_), (const uint8_t*)send + off, len);
+      seg_->barrier(rank_, timeout_);
+      for (int r = 0; r < n; ++r) std::memcpy((uint8_t*)recv + (size_t)r * bytes + off, seg_->slot(r), len);
+      seg_->barrier(rank_, timeout_);
+    }
   }
-  void allreduce_sum_i64(int64_t* v, size_t n) override { reduce(v, n, ncclInt64, ncclSum); }
-  void allreduce_max_f64(double* v, size_t n) override { reduce(v, n, ncclFloat64, ncclMax); }
-  void barrier() override {
-    int64_t one = 1;
-    allreduce_sum_i64(&one, 1);
+  void allreduce_sum_i64(int64_t* v, size_t n) override {
+    fold_allgather(*this, v, n, [](int64_t a, int64_t b) { return a + b; });
   }
+  void allreduce_max_f64(double* v, size_t n) override {
+    fold_allgather(*this, v, n, [](double a, double b) { return std::max(a, b); });
+  }
+  void barrier() override { seg_->barrier(rank_, timeout_); }
 
  private:
-  void reduce(void* v, size_t n, ncclDataType_t t, ncclRedOp_t op) {
-    if (!n) return;
-    const size_t bytes = n * 8;
-    uint8_t* d = stage(bytes);
-    hip_ck(hipMemcpyAsync(d, v, bytes, hipMemcpyHostToDevice, stream_), "H2D");
-    nccl_check(ncclAllReduce(d, d, n, t, op, comm_, stream_), "ncclAllReduce");
-    hip_ck(hipMemcpyAsync(v, d, bytes, hipMemcpyDeviceToHost, stream_), "D2H");
-    wait();
-  }
-  uint8_t* stage(size_t bytes) {
-    if (bytes > cap_) {
-      if (buf_) hip_ck(hipFree(buf_), "hipFree");
-      cap_ = std::max<size_t>(bytes, 1 << 20);
-      hip_ck(hipMalloc(&buf_, cap_), "hipMalloc comm");
-    }
-    return (uint8_t*)buf_;
-  }
-  void wait() {
-    // Poll with an async-error check so a dead peer surfaces as an error instead of a hang.
-    for (;;) {
-      hipError_t q = hipStreamQuery(stream_);
-      if (q == hipSuccess) return;
-      if (q != hipErrorNotReady) hip_ck(q, "comm stream");
-      ncclResult_t ar = ncclSuccess;
-      nccl_check(ncclCommGetAsyncError(comm_, &ar), "ncclCommGetAsyncError");
-      nccl_check(ar, "RCCL async error");
-      usleep(50);
-    }
-  }
-  int rank_, size_, dev_;
-  hipStream_t stream_ = nullptr;
-  ncclComm_t comm_ = nullptr;
-  void* buf_ = nullptr;
-  size_t cap_ = 0;
+  std::shared_ptr<ShmSegment> seg_;
+  int rank_;
+  double timeout_;
 };
 
-bool read_full(int fd, void* p, size_t n) {
-  uint8_t* q = (uint8_t*)p;
-  while (n) {
-    ssize_t r = ::read(fd, q, n);
-    if (r <= 0) return false;
-    q += r;
-    n -= (size_t)r;
-  }
-  return true;
+double mono_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
-bool write_full(int fd, const void* p, size_t n) {
-  const uint8_t* q = (const uint8_t*)p;
-  while (n) {
-    ssize_t r = ::write(fd, q, n);
-    if (r <= 0) return false;
-    q += r;
-    n -= (size_t)r;
+
+int exit_code(int st) { return WIFEXITED(st) ? WEXITSTATUS(st) : 128 + (WIFSIGNALED(st) ? WTERMSIG(st) : 0); }
+
+// Supervisor: reap every rank; the first non-zero exit raises the abort flag, stragglers get
+// `grace` seconds to notice, then SIGTERM, then SIGKILL.
+int supervise(std::vector<pid_t>& kids, ShmSegment& seg, double grace) {
+  const int n = (int)kids.size();
+  int alive = n, rc = 0;
+  double fail_t = -1;
+  int signals_sent = 0;
+  while (alive > 0) {
+    // Only our own rank processes are reaped (the caller may have other children, e.g. Python).
+    bool reaped = false;
+    for (int r = 0; r < n; ++r) {
+      if (kids[r] <= 0) continue;
+      int st = 0;
+      const pid_t p = waitpid(kids[r], &st, WNOHANG);
+      if (p == 0 || (p < 0 && errno == EINTR)) continue;
+      kids[r] = -1;
+      --alive;
+      reaped = true;
+      const int code = p < 0 ? 1 : exit_code(st);
+      if (code != 0) {
+        fprintf(stderr, "Rank %d exited with status %d\n", r, code);
+        fflush(stderr);
+        if (!rc) {
+          rc = code;
+          fail_t = mono_s();
+          seg.raise_abort(r);
+        }
+      }
+    }
+    if (reaped || alive == 0) continue;
+    if (!rc) {
+      std::this_thread::sleep_for(std::chrono::milliseconds(2));
+      continue;
+    }
+    // A rank failed and nobody else exited yet: escalate on stragglers once the grace periods pass.
+    const double waited = mono_s() - fail_t;
+    if (signals_sent < 2 && waited > grace * (signals_sent + 1)) {
+      const int sig = signals_sent == 0 ? SIGTERM : SIGKILL;
+      for (int r = 0; r < n; ++r)
+        if (kids[r] > 0) {
+          fprintf(stderr, "Rank %d still running %.1f s after the failure: sending %s\n", r, waited,
+                  sig == SIGTERM ? "SIGTERM" : "SIGKILL");
+          kill(kids[r], sig);
+        }
+      fflush(stderr);
+      ++signals_sent;
+    }
+    std::this_thread::sleep_for(std::chrono::milliseconds(5));
   }
-  return true;
+  return rc;
 }
 
 }  // namespace
@@ -287,83 +285,78 @@ std::vector<std::unique_ptr<Comm>> make_loopback_group(int n) {
 
 std::unique_ptr<Comm> make_self_comm() { return std::make_unique<SelfComm>(); }
 
-std::unique_ptr<Comm> make_rccl_comm(int rank, int size, const std::vector<uint8_t>& uid, int device) {
-  return std::make_unique<RcclComm>(rank, size, uid, device);
+std::unique_ptr<Comm> make_host_comm(std::shared_ptr<ShmSegment> seg, int rank, double timeout_s) {
+  return std::make_unique<HostComm>(std::move(seg), rank, timeout_s);
 }
 
-std::vector<uint8_t> rccl_unique_id() {
-  ncclUniqueId id;
-  nccl_check(ncclGetUniqueId(&id), "ncclGetUniqueId");
-  std::vector<uint8_t> v(sizeof(id));
-  std::memcpy(v.data(), &id, sizeof(id));
-  return v;
+std::string LaunchOptions::resolve(int n) const {
+  if (comm == "rccl" || comm == "host") return comm;
+  if (comm != "auto") throw CommError("unknown comm backend '" + comm + "' (rccl | host | auto)");
+  // RCCL refuses two ranks on one device ("Duplicate GPU detected"): shared-device runs use host.
+  return (n > 1 && device_override >= 0) ? "host" : "rccl";
 }
 
-int launch_ranks(int n, const std::function<int(int, int, Comm&)>& body, bool use_rccl) {
+LaunchOptions LaunchOptions::from_env() {
+  LaunchOptions o;
+  if (const char* e = std::getenv("NM03_COMM"); e && *e) o.comm = e;
+  if (const char* e = std::getenv("NM03_DEVICE_OVERRIDE"); e && *e) o.device_override = std::atoi(e);
+  return o;
+}
+
+int launch_ranks(int n, const std::function<int(int, int, Comm&)>& body, const LaunchOptions& opts) {
   if (n <= 1) {
     auto c = make_self_comm();
     return body(0, 1, *c);
   }
-  std::vector<int> wfd;
+  const std::string backend = opts.resolve(n);
+  auto seg = ShmSegment::create_anonymous(n);
+  fflush(stdout);  // buffered output must not be duplicated into the children
+  fflush(stderr);
+  const pid_t supervisor = getpid();
   std::vector<pid_t> kids;
-  int my_rank = 0, rfd = -1;
-  for (int r = 1; r < n; ++r) {
-    int p[2];
-    if (pipe(p) != 0) throw std::runtime_error("pipe() failed");
-    pid_t pid = fork();
-    if (pid < 0) throw std::runtime_error("fork() failed");
-    if (pid == 0) {
-      ::close(p[1]);
-      for (int fd : wfd) ::close(fd);
-      my_rank = r;
-      rfd = p[0];
-      kids.clear();
-      break;
+  for (int r = 0; r < n; ++r) {
+    const pid_t pid = fork();
+    if (pid < 0) {
+      seg->raise_abort(-2);
+      for (pid_t k : kids) kill(k, SIGTERM);
+      for (pid_t k : kids) waitpid(k, nullptr, 0);
+      throw std::runtime_error("fork() failed");
     }
-    ::close(p[0]);
-    wfd.push_back(p[1]);
+    if (pid == 0) {
+      // Rank process: dies with the supervisor; runs the body on its own device.
+      prctl(PR_SET_PDEATHSIG, SIGTERM);
+      if (getppid() != supervisor) _exit(1);
+      int rc = 0;
+      try {
+        std::unique_ptr<Comm> comm;
+        if (backend == "rccl") {
+          std::vector<uint8_t> uid;
+          if (r == 0) {
+            uid = rccl_unique_id();
+            seg->publish_uid(uid);
+          } else {
+            uid = seg->wait_uid(r, opts.timeout_s > 0 ? opts.timeout_s : comm_timeout_s());
+          }
+          comm = make_rccl_comm(r, n, uid, opts.device_of(r), seg, opts.timeout_s);
+        } else {
+          comm = make_host_comm(seg, r, opts.timeout_s);
+        }
+        rc = body(r, n, *comm);
+      } catch (const CommError& e) {
+        fprintf(stderr, "Rank %d: communication failed: %s\n", r, e.what());
+        rc = 1;
+      } catch (const std::exception& e) {
+        fprintf(stderr, "Fatal error on rank %d: %s\n", r, e.what());
+        rc = 1;
+      }
+      if (rc != 0) seg->raise_abort(r);  // peers blocked in a collective fail now, not at the deadline
+      fflush(stdout);
+      fflush(stderr);
+      _exit(rc);
+    }
     kids.push_back(pid);
   }
-  int rc = 0;
-  try {
-    std::unique_ptr<Comm> comm;
-    if (my_rank == 0) {
-      std::vector<uint8_t> id = use_rccl ? rccl_unique_id() : std::vector<uint8_t>(128, 0);
-      for (int fd : wfd) {
-        if (!write_full(fd, id.data(), id.size())) throw std::runtime_error("cannot send unique id to a rank");
-        ::close(fd);
-      }
-      if (use_rccl) comm = make_rccl_comm(0, n, id, 0);
-    } else {
-      std::vector<uint8_t> id(128);
-      if (!read_full(rfd, id.data(), id.size())) throw std::runtime_error("cannot receive unique id");
-      ::close(rfd);
-      if (use_rccl) comm = make_rccl_comm(my_rank, n, id, my_rank);
-    }
-    if (!comm) comm = make_self_comm();
-    rc = body(my_rank, n, *comm);
-  } catch (const std::exception& e) {
-    fprintf(stderr, "Fatal error on rank %d: %s\n", my_rank, e.what());
-    rc = 1;
-  }
-  if (my_rank != 0) {
-    fflush(stdout);
-    fflush(stderr);
-    _exit(rc);
-  }
-  for (size_t i = 0; i < kids.size(); ++i) {
-    int st = 0;
-    if (waitpid(kids[i], &st, 0) < 0) {
-      rc = rc ? rc : 1;
-      continue;
-    }
-    const int code = WIFEXITED(st) ? WEXITSTATUS(st) : 128 + (WIFSIGNALED(st) ? WTERMSIG(st) : 0);
-    if (code != 0) {
-      fprintf(stderr, "Rank %zu exited with status %d\n", i + 1, code);
-      if (!rc) rc = code;
-    }
-  }
-  return rc;
+  return supervise(kids, *seg, opts.grace_s);
 }
 
 }  // namespace nm03

@@ -1,0 +1,187 @@
+// RCCL communicator (nm03/comm.h): collectives on a device staging buffer on a private stream,
+// i.e. over xGMI between the MI355X of one node. The communicator is created non-blocking
+// (ncclConfig_t.blocking = 0) so that initialisation, like every later wait, is a bounded poll:
+// a peer that died or never arrived ends in ncclCommAbort + CommError after NM03_COMM_TIMEOUT_S
+// (or at once when the launcher raised the job abort flag), never in a hang.
+#include <hip/hip_runtime_api.h>
+#include <rccl/rccl.h>
+#include <unistd.h>
+
+#include <chrono>
+#include <cstring>
+#include <thread>
+
+#include "nm03/comm.h"
+
+namespace nm03 {
+
+namespace {
+
+double mono_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+void hip_ck(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw CommError(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+class RcclComm final : public Comm {
+ public:
+  RcclComm(int rank, int size, const std::vector<uint8_t>& uid, int device, std::shared_ptr<ShmSegment> seg,
+           double timeout_s)
+      : rank_(rank), size_(size), dev_(device), seg_(std::move(seg)),
+        timeout_(timeout_s > 0 ? timeout_s : comm_timeout_s()) {
+    if (uid.size() != sizeof(ncclUniqueId)) throw CommError("bad ncclUniqueId size");
+    ncclUniqueId id;
+    std::memcpy(&id, uid.data(), sizeof(id));
+    hip_ck(hipSetDevice(dev_), "hipSetDevice");
+    hip_ck(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "hipStreamCreate");
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    cfg.blocking = 0;
+    ncclResult_t r = ncclCommInitRankConfig(&comm_, size_, id, rank_, &cfg);
+    if (r != ncclSuccess && r != ncclInProgress) {
+      release();
+      throw CommError(std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+    }
+    try {
+      settle("ncclCommInitRank");
+    } catch (...) {
+      release();
+      throw;
+    }
+  }
+  ~RcclComm() override { release(); }
+  int rank() const override { return rank_; }
+  int size() const override { return size_; }
+  const char* backend() const override { return "rccl"; }
+
+  void broadcast(void* buf, size_t bytes, int root) override {
+    if (!bytes) return;
+    uint8_t* d = stage(bytes);
+    if (rank_ == root) hip_ck(hipMemcpyAsync(d, buf, bytes, hipMemcpyHostToDevice, stream_), "H2D");
+    issue(ncclBroadcast(d, d, bytes, ncclUint8, root, comm_, stream_), "ncclBroadcast");
+    hip_ck(hipMemcpyAsync(buf, d, bytes, hipMemcpyDeviceToHost, stream_), "D2H");
+    wait("ncclBroadcast");
+  }
+  void allgather(const void* send, size_t bytes, void* recv) override {
+    if (!bytes) return;
+    uint8_t* d = stage(bytes * (size_t)(size_ + 1));
+    uint8_t* dsend = d + bytes * (size_t)size_;
+    hip_ck(hipMemcpyAsync(dsend, send, bytes, hipMemcpyHostToDevice, stream_), "H2D");
+    issue(ncclAllGather(dsend, d, bytes, ncclUint8, comm_, stream_), "ncclAllGather");
+    hip_ck(hipMemcpyAsync(recv, d, bytes * size_, hipMemcpyDeviceToHost, stream_), "D2H");
+    wait("ncclAllGather");
+  }
+  void allreduce_sum_i64(int64_t* v, size_t n) override { reduce(v, n, ncclInt64, ncclSum); }
+  void allreduce_max_f64(double* v, size_t n) override { reduce(v, n, ncclFloat64, ncclMax); }
+  void barrier() override {
+    int64_t one = 1;
+    allreduce_sum_i64(&one, 1);
+  }
+
+ private:
+  void reduce(void* v, size_t n, ncclDataType_t t, ncclRedOp_t op) {
+    if (!n) return;
+    const size_t bytes = n * 8;
+    uint8_t* d = stage(bytes);
+    hip_ck(hipMemcpyAsync(d, v, bytes, hipMemcpyHostToDevice, stream_), "H2D");
+    issue(ncclAllReduce(d, d, n, t, op, comm_, stream_), "ncclAllReduce");
+    hip_ck(hipMemcpyAsync(v, d, bytes, hipMemcpyDeviceToHost, stream_), "D2H");
+    wait("ncclAllReduce");
+  }
+  uint8_t* stage(size_t bytes) {
+    if (!comm_) throw CommError("RCCL communicator was aborted");
+    if (seg_) seg_->check_abort(rank_);
+    if (bytes > cap_) {
+      if (buf_) hip_ck(hipFree(buf_), "hipFree");
+      buf_ = nullptr;
+      cap_ = std::max<size_t>(bytes, 1 << 20);
+      hip_ck(hipMalloc(&buf_, cap_), "hipMalloc comm");
+    }
+    return (uint8_t*)buf_;
+  }
+  // A non-blocking communicator may return ncclInProgress from an enqueue: poll until settled.
+  void issue(ncclResult_t r, const char* what) {
+    if (r == ncclSuccess) return;
+    if (r != ncclInProgress) fail(std::string(what) + ": " + ncclGetErrorString(r));
+    settle(what);
+  }
+  void settle(const char* what) {
+    const double deadline = mono_s() + timeout_;
+    for (;;) {
+      ncclResult_t ar = ncclSuccess;
+      const ncclResult_t q = ncclCommGetAsyncError(comm_, &ar);
+      if (q != ncclSuccess) fail(std::string(what) + ": ncclCommGetAsyncError: " + ncclGetErrorString(q));
+      if (ar == ncclSuccess) return;
+      if (ar != ncclInProgress) fail(std::string(what) + ": " + ncclGetErrorString(ar));
+      poll_guards(what, deadline);
+    }
+  }
+  void wait(const char* what) {
+    const double deadline = mono_s() + timeout_;
+    for (;;) {
+      const hipError_t q = hipStreamQuery(stream_);
+      if (q == hipSuccess) return;
+      if (q != hipErrorNotReady) fail(std::string(what) + ": " + hipGetErrorString(q));
+      ncclResult_t ar = ncclSuccess;
+      if (ncclCommGetAsyncError(comm_, &ar) != ncclSuccess || (ar != ncclSuccess && ar != ncclInProgress))
+        fail(std::string(what) + ": RCCL async error: " + ncclGetErrorString(ar));
+      poll_guards(what, deadline);
+    }
+  }
+  void poll_guards(const char* what, double deadline) {
+    if (seg_ && seg_->aborted()) {
+      const int r = seg_->abort_rank();
+      fail(r == rank_ ? std::string(what) + ": aborted" : "rank " + std::to_string(r) + " failed; job aborted");
+    }
+    if (mono_s() > deadline) {
+      if (seg_) seg_->raise_abort(rank_);
+      fail(std::string(what) + " timed out after " + std::to_string((int)timeout_) + " s on rank " +
+           std::to_string(rank_) + "; set NM03_COMM_TIMEOUT_S to wait longer");
+    }
+    std::this_thread::sleep_for(std::chrono::microseconds(50));
+  }
+  [[noreturn]] void fail(const std::string& msg) {
+    if (comm_) {
+      (void)ncclCommAbort(comm_);
+      comm_ = nullptr;
+    }
+    throw CommError(msg);
+  }
+  void release() {
+    if (comm_) {
+      // A healthy communicator is destroyed; an aborted one was already released by fail().
+      (void)ncclCommDestroy(comm_);
+      comm_ = nullptr;
+    }
+    if (buf_) (void)hipFree(buf_);
+    buf_ = nullptr;
+    if (stream_) (void)hipStreamDestroy(stream_);
+    stream_ = nullptr;
+  }
+  int rank_, size_, dev_;
+  std::shared_ptr<ShmSegment> seg_;
+  double timeout_;
+  hipStream_t stream_ = nullptr;
+  ncclComm_t comm_ = nullptr;
+  void* buf_ = nullptr;
+  size_t cap_ = 0;
+};
+
+}  // namespace
+
+std::unique_ptr<Comm> make_rccl_comm(int rank, int size, const std::vector<uint8_t>& uid, int device,
+                                     std::shared_ptr<ShmSegment> seg, double timeout_s) {
+  return std::make_unique<RcclComm>(rank, size, uid, device, std::move(seg), timeout_s);
+}
+
+std::vector<uint8_t> rccl_unique_id() {
+  ncclUniqueId id;
+  const ncclResult_t r = ncclGetUniqueId(&id);
+  if (r != ncclSuccess) throw CommError(std::string("ncclGetUniqueId: ") + ncclGetErrorString(r));
+  std::vector<uint8_t> v(sizeof(id));
+  std::memcpy(v.data(), &id, sizeof(id));
+  return v;
+}
+
+}  // namespace nm03

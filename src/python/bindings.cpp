@@ -7,6 +7,9 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <unistd.h>
+
+#include <chrono>
 #include <cstring>
 #include <thread>
 
@@ -826,8 +829,132 @@ PYBIND11_MODULE(_nm03, m) {
     for (auto& t : th) t.join();
     return errors;
   });
-  m.def("launcher_selftest", [](int n) {
-    // Forks n-1 children (no RCCL, no HIP) and checks that every rank ran and exit codes propagate.
-    return launch_ranks(n, [](int rank, int size, Comm&) { return (rank == size - 1 && size > 2) ? 7 : 0; }, false);
+  m.def(
+      "launcher_selftest",
+      // Forks n rank processes over the host comm (no RCCL, no HIP): every rank checks the
+      // collectives, then `mode` decides the ending — "ok": all succeed; "exit": the last rank
+      // (n > 2) returns 7 after the collectives; "die": the last rank exits 3 while the others
+      // block in a barrier (abort flag); "hang": the last rank sleeps while the others wait in
+      // a barrier (deadline, then SIGTERM from the supervisor). Returns the job's exit status.
+      [](int n, const std::string& mode, double timeout_s, double grace_s) {
+        LaunchOptions o;
+        o.comm = "host";
+        o.timeout_s = timeout_s;
+        o.grace_s = grace_s;
+        py::gil_scoped_release nogil;
+        return launch_ranks(
+            n,
+            [mode](int rank, int size, Comm& c) {
+              std::vector<uint8_t> b;
+              if (rank == 0) b.assign(3 << 20, 0);  // larger than a slot: chunked broadcast
+              for (size_t i = 0; i < b.size(); ++i) b[i] = (uint8_t)(i * 7 + 1);
+              c.broadcast_bytes(b, 0);
+              for (size_t i = 0; i < b.size(); i += 4099)
+                if (b[i] != (uint8_t)(i * 7 + 1)) return 11;
+              if (b.size() != (3u << 20)) return 12;
+              auto all = c.allgather_bytes(std::vector<uint8_t>(rank + 1, (uint8_t)rank));
+              for (int q = 0; q < size; ++q)
+                if (all[q] != std::vector<uint8_t>(q + 1, (uint8_t)q)) return 13;
+              int64_t v[2] = {rank, 1};
+              c.allreduce_sum_i64(v, 2);
+              if (v[0] != (int64_t)size * (size - 1) / 2 || v[1] != size) return 14;
+              double f = rank * 1.5;
+              c.allreduce_max_f64(&f, 1);
+              if (f != (size - 1) * 1.5) return 15;
+              const bool last = rank == size - 1;
+              if (mode == "exit" && last && size > 2) return 7;
+              if (mode == "die" && last) _exit(3);
+              if (mode == "hang" && last) {
+                std::this_thread::sleep_for(std::chrono::seconds(600));
+                return 0;
+              }
+              c.barrier();
+              return 0;
+            },
+            o);
+      },
+      py::arg("n"), py::arg("mode") = "exit", py::arg("timeout_s") = -1.0, py::arg("grace_s") = 5.0);
+
+  // ---- native communicators (bench.py and other Python drivers) ------------------------------------
+  // Host/RCCL comms for ranks started by torchrun or bench.py's own launcher; the rendezvous
+  // (segment name or RCCL unique id) travels through the caller's store.
+  py::class_<ShmSegment, std::shared_ptr<ShmSegment>>(m, "ShmSegment")
+      .def_property_readonly("size", &ShmSegment::size)
+      .def("wait_attached_and_unlink", [](ShmSegment& s, double t) {
+        py::gil_scoped_release nogil;
+        s.wait_attached_and_unlink(t);
+      }, py::arg("timeout_s") = 120.0)
+      .def("raise_abort", &ShmSegment::raise_abort)
+      .def_property_readonly("aborted", &ShmSegment::aborted);
+  m.def("shm_create", [](int n) {
+    std::string name;
+    auto s = ShmSegment::create_named(n, &name);
+    return py::make_tuple(s, name);
   });
+  m.def("shm_attach", [](const std::string& name, int n, double t) {
+    py::gil_scoped_release nogil;
+    return ShmSegment::attach_named(name, n, t);
+  }, py::arg("name"), py::arg("n"), py::arg("timeout_s") = 120.0);
+  py::class_<Comm, std::unique_ptr<Comm>>(m, "Comm")
+      .def_property_readonly("rank", &Comm::rank)
+      .def_property_readonly("size", &Comm::size)
+      .def_property_readonly("backend", [](const Comm& c) { return std::string(c.backend()); })
+      .def("barrier", [](Comm& c) {
+        py::gil_scoped_release nogil;
+        c.barrier();
+      })
+      .def("broadcast_bytes", [](Comm& c, py::bytes data, int root) {
+        std::string s = data;
+        std::vector<uint8_t> v(s.begin(), s.end());
+        {
+          py::gil_scoped_release nogil;
+          c.broadcast_bytes(v, root);
+        }
+        return py::bytes((const char*)v.data(), v.size());
+      }, py::arg("data"), py::arg("root") = 0)
+      .def("allgather_bytes", [](Comm& c, py::bytes data) {
+        std::string s = data;
+        std::vector<std::vector<uint8_t>> all;
+        {
+          py::gil_scoped_release nogil;
+          all = c.allgather_bytes(std::vector<uint8_t>(s.begin(), s.end()));
+        }
+        py::list out;
+        for (auto& v : all) out.append(py::bytes((const char*)v.data(), v.size()));
+        return out;
+      })
+      .def("allreduce_sum", [](Comm& c, std::vector<int64_t> v) {
+        py::gil_scoped_release nogil;
+        c.allreduce_sum_i64(v.data(), v.size());
+        return v;
+      })
+      .def("allreduce_max", [](Comm& c, std::vector<double> v) {
+        py::gil_scoped_release nogil;
+        c.allreduce_max_f64(v.data(), v.size());
+        return v;
+      })
+      .def("allgather_f64", [](Comm& c, std::vector<double> v) {
+        std::vector<double> all(v.size() * (size_t)c.size());
+        {
+          py::gil_scoped_release nogil;
+          c.allgather(v.data(), v.size() * sizeof(double), all.data());
+        }
+        return all;
+      });
+  m.def("self_comm", &make_self_comm);
+  m.def("host_comm", [](std::shared_ptr<ShmSegment> seg, int rank, double t) { return make_host_comm(seg, rank, t); },
+        py::arg("segment"), py::arg("rank"), py::arg("timeout_s") = -1.0);
+  m.def("rccl_unique_id", [] {
+    auto v = rccl_unique_id();
+    return py::bytes((const char*)v.data(), v.size());
+  });
+  m.def("rccl_comm", [](int rank, int size, py::bytes uid, int device, std::shared_ptr<ShmSegment> seg, double t) {
+    std::string s = uid;
+    std::vector<uint8_t> v(s.begin(), s.end());
+    py::gil_scoped_release nogil;
+    return make_rccl_comm(rank, size, v, device, seg, t);
+  }, py::arg("rank"), py::arg("size"), py::arg("unique_id"), py::arg("device"), py::arg("segment") = nullptr,
+     py::arg("timeout_s") = -1.0);
+  m.def("comm_timeout_s", &comm_timeout_s);
+  py::register_exception<CommError>(m, "CommError", PyExc_RuntimeError);
 }

@@ -115,7 +115,7 @@ struct Slot {
   int max_w = 0, max_h = 0;
   // Captured kernel chains keyed by launch signature (see GraphKey in build_and_run). Every
   // pointer in the chain is fixed per slot, so a signature fully determines the launches.
-  std::map<std::array<int, 10>, hipGraphExec_t> graphs;
+  std::map<std::array<int, 11>, hipGraphExec_t> graphs;
 };
 
 void hip_free_all(Slot& s) {
@@ -624,7 +624,9 @@ struct Engine::Impl {
     if (!cfg.graphs || sync_launches()) {
       chain();
     } else {
-      const std::array<int, 10> key{nmed, nshp, nl, ncanv, s.max_w, s.max_h, (int)s.any_canvas, mode, cw, ch};
+      // The K0-vs-fused unpack switch changes the chain: part of the signature (it is read per batch).
+      const std::array<int, 11> key{nmed, nshp, nl, ncanv, s.max_w, s.max_h, (int)s.any_canvas, mode, cw, ch,
+                                    (int)separate_unpack()};
       auto it = s.graphs.find(key);
       if (it == s.graphs.end()) {
         hipGraph_t g = nullptr;

@@ -79,6 +79,7 @@ const FaultPlan& fault_plan() {
       if (k == "corrupt_dicom") f.corrupt_dicom = v;
       else if (k == "fail_batch") f.fail_batch = v;
       else if (k == "fail_write") f.fail_write = v;
+      else if (k == "rank_exit") f.rank_exit = v;
     }
     return f;
   }();

@@ -1,0 +1,77 @@
+"""bench.py's own rank launcher, rendezvous, native comm and JSON aggregation on the CPU
+(--dry-run: everything but the engine). The GPU twin is tests/test_gpu.py::test_bench_multirank."""
+import json
+import os
+import subprocess
+import sys
+import time
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _bench(tmp_path, *extra, env=None, timeout=240):
+    e = dict(os.environ, NM03_COMM_TIMEOUT_S="30", NM03_BENCH_NUMA_DATA="off")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
+        e.pop(k, None)
+    e.update(env or {})
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--dry-run", "--steps", "2", "--warmup", "1",
+           "--data-root", str(tmp_path / "data"), "--out-root", str(tmp_path / "out"), *extra]
+    return subprocess.run(cmd, cwd=str(tmp_path), env=e, capture_output=True, text=True, timeout=timeout)
+
+
+def _json_line(out):
+    lines = [l for l in out.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out
+    return json.loads(lines[0])
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_bench_self_launch_n_ranks(tmp_path, n):
+    """`python bench.py --gpus N` starts N ranks itself: n_gpus, per-rank arrays, weak + strong."""
+    r = _bench(tmp_path, "--gpus", str(n), "--comm", "host")
+    assert r.returncode == 0, r.stderr
+    rec = _json_line(r.stdout)
+    assert rec["n_gpus"] == n and rec["config"]["parallelism"] == f"dp{n}"
+    assert rec["config"]["comm"]["backend"] == "host"
+    assert rec["config"]["global_batch"] == n * rec["config"]["strong"]["global_batch"]  # weak: N replicas
+    pr = rec["config"]["per_rank"]
+    assert all(len(v) == n for v in pr.values())
+    # weak: every rank processes one full cohort per step
+    cohort = rec["config"]["strong"]["global_batch"]
+    assert pr["slices"] == [float(cohort * 2)] * n
+    # strong: one cohort sharded, every slice exactly once
+    assert sum(rec["config"]["strong"]["per_rank"]["slices"]) == cohort * 2
+
+
+def test_bench_auto_comm_records_rccl_failure(tmp_path):
+    """auto: RCCL cannot come up without a GPU; the run goes on over the host comm and says why."""
+    r = _bench(tmp_path, "--gpus", "2", "--no-secondary")
+    assert r.returncode == 0, r.stderr
+    comm = _json_line(r.stdout)["config"]["comm"]
+    assert comm["backend"] == "host" and "rccl_error" in comm
+
+
+def test_bench_dead_rank_fails_job(tmp_path):
+    """A rank that dies makes the job exit non-zero, naming the rank, well before the deadline."""
+    t0 = time.monotonic()
+    r = _bench(tmp_path, "--gpus", "3", "--comm", "host", env={"NM03_BENCH_FAIL_RANK": "1"})
+    dt = time.monotonic() - t0
+    assert r.returncode != 0
+    assert "rank 1 exited with status 5" in r.stderr
+    assert not [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert dt < 120, dt
+
+
+def test_bench_world_size_mismatch(tmp_path):
+    r = _bench(tmp_path, "--gpus", "4", env={"WORLD_SIZE": "2", "RANK": "0"})
+    assert r.returncode != 0 and "WORLD_SIZE=2 but --gpus 4" in r.stderr
+
+
+def test_bench_single_rank_dry(tmp_path):
+    r = _bench(tmp_path)
+    assert r.returncode == 0, r.stderr
+    rec = _json_line(r.stdout)
+    assert rec["n_gpus"] == 1 and rec["config"]["comm"]["backend"] == "self"
+    assert rec["steps"] == 2 and rec["warmup"] == 1

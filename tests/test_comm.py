@@ -17,8 +17,65 @@ def test_loopback_collectives(native, n):
 
 def test_launcher_exit_codes(native):
     assert native.launcher_selftest(1) == 0
-    assert native.launcher_selftest(2) == 0
+    assert native.launcher_selftest(2, "ok") == 0
+    assert native.launcher_selftest(4, "ok") == 0
     assert native.launcher_selftest(3) == 7  # a failing rank fails the job
+
+
+def test_launcher_dead_rank_fails_fast(native, capfd):
+    """Rank 2 of 3 dies while ranks 0/1 block in a collective: the supervisor raises the abort
+    flag, the blocked ranks fail within milliseconds (not at the deadline) and the job exits with
+    the dead rank's status, naming it on stderr."""
+    import time
+    t0 = time.monotonic()
+    rc = native.launcher_selftest(3, "die", 60.0, 5.0)
+    dt = time.monotonic() - t0
+    err = capfd.readouterr().err
+    assert rc == 3
+    assert "Rank 2 exited with status 3" in err
+    assert "rank 2 failed; job aborted" in err
+    assert dt < 20, dt  # far below the 60 s collective deadline
+
+
+def test_launcher_hung_rank_times_out(native, capfd):
+    """Rank 2 of 3 hangs outside any collective: the others hit the collective deadline, the job
+    is aborted, and the supervisor terminates the straggler after the grace period."""
+    import time
+    t0 = time.monotonic()
+    rc = native.launcher_selftest(3, "hang", 1.5, 1.0)
+    dt = time.monotonic() - t0
+    err = capfd.readouterr().err
+    assert rc != 0
+    assert "timed out after 1 s" in err
+    assert "sending SIGTERM" in err
+    assert dt < 30, dt
+
+
+def test_host_comm_named_segment(native):
+    """Named segment rendezvous (the bench.py / torchrun path): create, attach from a forked
+    process, collectives both ways, unlink once everyone attached."""
+    seg, name = native.shm_create(2)
+    pid = os.fork()
+    if pid == 0:  # child: rank 1
+        code = 1
+        try:
+            s1 = native.shm_attach(name, 2, 10.0)
+            c1 = native.host_comm(s1, 1, 10.0)
+            b = c1.broadcast_bytes(b"", 0)
+            g = c1.allgather_bytes(b"r1")
+            s = c1.allreduce_sum([5])
+            code = 0 if (b == b"plan" and g == [b"rank0", b"r1"] and s == [7]) else 2
+        finally:
+            os._exit(code)
+    seg.wait_attached_and_unlink(10.0)
+    assert not os.path.exists("/dev/shm" + name)
+    c0 = native.host_comm(seg, 0, 10.0)
+    assert c0.backend == "host" and c0.size == 2 and c0.rank == 0
+    assert c0.broadcast_bytes(b"plan", 0) == b"plan"
+    assert c0.allgather_bytes(b"rank0") == [b"rank0", b"r1"]
+    assert c0.allreduce_sum([2]) == [7]
+    _, st = os.waitpid(pid, 0)
+    assert os.WEXITSTATUS(st) == 0
 
 
 @pytest.mark.parametrize("n,world", [(0, 3), (1, 4), (466, 8), (25, 2), (7, 7)])

@@ -378,6 +378,83 @@ def test_cli_sequential_equals_parallel(native, cohort_root, tmp_path):
         assert line in r2.stdout, line
 
 
+# ---------------------------------------------------------------------------------------------
+# Multi-rank on one GPU: N rank processes share device 0 over the host comm (RCCL refuses two
+# ranks per device). Same launcher, plan broadcast, sharding, status gather and printing as an
+# N-GPU run.
+# ---------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("ranks", [2, 4])
+def test_cli_parallel_multirank_identical(native, cohort_root, tmp_path, ranks):
+    import json
+    g1, gn = tmp_path / "g1", tmp_path / f"g{ranks}"
+    one = run_bin("img_processing_parallel", "--data-root", cohort_root, "--out", str(g1), "--gpus", "1")
+    assert one.returncode == 0, one.stderr
+    many = run_bin("img_processing_parallel", "--data-root", cohort_root, "--out", str(gn), "--gpus", str(ranks),
+                   "--threads", "4", "--json", str(tmp_path / "m.json"),
+                   env={"NM03_DEVICE_OVERRIDE": "0", "NM03_COMM_TIMEOUT_S": "60"}, timeout=240)
+    assert many.returncode == 0, many.stderr
+    t1, tn = _tree(str(g1)), _tree(str(gn))
+    assert t1 == tn and len(t1) > 0
+    # rank 0 prints the whole cohort in patient order: identical apart from the paths and threads
+    norm = lambda s, d: s.replace(str(d), "OUT").replace("Using 4 threads", "Using 16 threads")  # noqa: E731
+    assert norm(one.stdout, g1) == norm(many.stdout, gn)
+    j = json.load(open(tmp_path / "m.json"))
+    assert j["gpus"] == ranks and j["backend"] == "host"
+    pr = j["per_rank"]
+    assert len(pr["slices"]) == ranks and sum(pr["slices"]) == len(t1) // 2
+    assert sum(pr["slices_ok"]) == len(t1) // 2
+
+
+def test_cli_parallel_dead_rank_fails_job(native, cohort_root, tmp_path):
+    """A rank that dies mid-job (after the plan broadcast) fails the job promptly with its id."""
+    import time
+    t0 = time.monotonic()
+    r = run_bin("img_processing_parallel", "--data-root", cohort_root, "--out", str(tmp_path / "o"), "--gpus", "3",
+                "--threads", "4", env={"NM03_DEVICE_OVERRIDE": "0", "NM03_FAULT": "rank_exit:2",
+                                       "NM03_COMM_TIMEOUT_S": "60"}, timeout=120)
+    assert r.returncode != 0
+    assert "Rank 2 exited with status 9" in r.stderr
+    assert time.monotonic() - t0 < 50
+
+
+def test_cli_parallel_rejects_more_gpus_than_visible(native, cohort_root, tmp_path):
+    r = run_bin("img_processing_parallel", "--data-root", cohort_root, "--out", str(tmp_path / "o"), "--gpus", "64")
+    assert r.returncode == 1 and "exceeds the" in r.stderr and "visible GPU" in r.stderr
+
+
+def test_rccl_comm_single_rank(native):
+    """The native RCCL communicator end to end on the GPU (non-blocking init, staged collectives,
+    bounded waits) with one rank — a second rank needs a second GPU."""
+    uid = native.rccl_unique_id()
+    c = native.rccl_comm(0, 1, uid, 0, None, 30.0)
+    assert c.backend == "rccl" and c.rank == 0 and c.size == 1
+    c.barrier()
+    assert c.broadcast_bytes(b"work-list" * 1000, 0) == b"work-list" * 1000
+    assert c.allgather_bytes(b"abc") == [b"abc"]
+    assert c.allreduce_sum([3, 4]) == [3, 4]
+    assert c.allreduce_max([1.5]) == [1.5]
+    assert c.allgather_f64([2.0, 3.0]) == [2.0, 3.0]
+
+
+def test_bench_multirank_one_gpu(native, tmp_path):
+    """bench.py --gpus 2 launches its own ranks (sharing GPU 0): n_gpus, weak + strong figures."""
+    import json
+    import subprocess
+    import sys
+    env = dict(os.environ, NM03_DEVICE_OVERRIDE="0", NM03_COMM_TIMEOUT_S="60", NM03_BENCH_NUMA_DATA="off")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, os.path.join(os.path.dirname(os.path.dirname(__file__)), "bench.py"),
+                        "--gpus", "2", "--steps", "2", "--warmup", "1", "--threads", "8",
+                        "--data-root", str(tmp_path / "d"), "--out-root", str(tmp_path / "o")],
+                       env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    rec = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
+    assert rec["n_gpus"] == 2 and rec["value"] > 0 and rec["config"]["comm"]["backend"] == "host"
+    assert rec["config"]["strong"]["value"] > 0 and rec["config"]["strong"]["global_batch"] * 2 == rec["config"]["global_batch"]
+    assert sum(rec["config"]["per_rank"]["slices_ok"]) == 2 * rec["config"]["global_batch"]
+
+
 def test_cli_test_pipeline_gpu_equals_cpu(native, cohort_root, tmp_path):
     a, b = tmp_path / "gpu", tmp_path / "cpu"
     r = run_bin("test_pipeline", "--data-root", cohort_root, "--out", str(a))

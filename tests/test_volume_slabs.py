@@ -100,3 +100,42 @@ def test_volume_pipeline_run_slabs_cpu(native):
     ref = native.golden_region_grow3d(band, seeds, 26)
     assert np.array_equal(r["region"].numpy().astype(np.uint8), ref)
     assert np.array_equal(r["dilated"].numpy().astype(np.uint8), native.golden_dilate3d(ref, 5))
+
+
+def _empty_slab_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    from nm03_capstone_project_amd.parallel import dist as D
+    from nm03_capstone_project_amd.parallel.volume_slabs import grow_slabs, run_volume_slabs
+    ctx = D.init_from_env(backend="gloo", use_gpu=False)
+    errs = []
+    try:
+        band = np.ones((2, 8, 8), dtype=bool)  # depth 2 < 3 ranks
+        for call in (lambda: run_volume_slabs(band=band, ctx=ctx, backend="cpu"),
+                     # a caller-built decomposition with an empty slab on the last rank
+                     lambda: grow_slabs(torch.from_numpy(band[:1] if rank < 2 else band[:0]), rank, [(1, 1, 0)], ctx)):
+            try:
+                call()
+                errs.append("no error")
+            except ValueError as e:
+                errs.append(str(e))
+        q.put((rank, errs))
+    finally:
+        torch.distributed.destroy_process_group()
+
+
+def test_empty_slabs_fail_on_every_rank(native):
+    """depth < world: every rank raises (no rank left waiting in a collective) — ADVICE r1."""
+    world, port = 3, _free_port()
+    mctx = mp.get_context("spawn")
+    q = mctx.Queue()
+    ps = [mctx.Process(target=_empty_slab_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = sorted((q.get(timeout=180) for _ in range(world)), key=lambda t: t[0])
+    for p in ps:
+        p.join(60)
+        assert p.exitcode == 0
+    for rank, errs in res:
+        assert "leaves empty slabs" in errs[0], (rank, errs)
+        assert "at least one plane" in errs[1], (rank, errs)

@@ -1,17 +1,24 @@
 #!/bin/bash
-# Multi-rank rehearsal on a one-GPU box (gpurun): bench.py under torchrun with 2 and 4 ranks that
-# all share device 0, collectives over gloo (RCCL refuses two ranks per device). Exercises the
-# plan broadcast, sharding, barriers, max/sum reductions and the rank-0 JSON line.
+# Multi-rank checks on a one-GPU box (gpurun): the GPU test-suite (incl. the N-rank CLI and bench
+# tests), then bench.py at 1 rank, 2 and 4 self-launched ranks sharing device 0 (host comm), and
+# the torchrun launch form the driver uses for N > 1. Logs in gpurun_out/.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-export NM03_DIST_BACKEND=gloo NM03_DEVICE_OVERRIDE=0
-for n in 2 4; do
-  timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n --master-addr 127.0.0.1 \
-    --master-port $((29500 + n)) bench.py --gpus $n --steps 5 --warmup 1 --threads $((16 / n)) --keep-output \
-    > gpurun_out/multirank_$n.log 2>&1 || exit $((90 + n))
-  find /dev/shm/nm03_bench_out -name "*.jpg" | wc -l > gpurun_out/multirank_${n}_files.txt
-  ls /dev/shm/nm03_bench_out >> gpurun_out/multirank_${n}_files.txt; rm -rf /dev/shm/nm03_bench_out
-done
+P=gpurun_out/progress_multirank.txt
+echo "start $(date)" > $P
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread -p no:cacheprovider \
+  > gpurun_out/pytest_gpu.log 2>&1 || exit 31
+echo "pytest ok $(date)" >> $P
+timeout -k 10 300 python bench.py --steps 20 --warmup 5 > gpurun_out/bench1.log 2>&1 || exit 32
+echo "bench1 ok $(date)" >> $P
+export NM03_DEVICE_OVERRIDE=0
+timeout -k 10 300 python bench.py --gpus 2 --steps 10 --warmup 2 > gpurun_out/bench2.log 2>&1 || exit 33
+echo "bench2 ok $(date)" >> $P
+timeout -k 10 300 python bench.py --gpus 4 --steps 10 --warmup 2 > gpurun_out/bench4.log 2>&1 || exit 34
+echo "bench4 ok $(date)" >> $P
+timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+  --master-port 29611 bench.py --gpus 2 --steps 10 --warmup 2 > gpurun_out/bench2_torchrun.log 2>&1 || exit 35
+echo "done $(date)" >> $P
 ls /dev/shm > gpurun_out/shm_after.txt
