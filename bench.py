@@ -95,6 +95,9 @@ def parse_args(argv=None):
     ap.add_argument("--keep-data", action="store_true", help="keep a generated dataset in tmpfs after the run")
     ap.add_argument("--keep-output", action="store_true")
     ap.add_argument("--graphs", action="store_true", help="hipGraph replay of the per-batch kernel chain")
+    ap.add_argument("--no-pipeline", action="store_true",
+                    help="one blocking engine call per pass; by default pass k+1 is submitted before pass k "
+                         "finished (Engine.submit/wait) so the slot ring never drains between passes")
     ap.add_argument("--stream-steps", action="store_true",
                     help="submit the K timed cohort passes as one work stream (the engine pipelines across pass "
                          "boundaries as it does across patients) instead of one engine call per pass; every pass "
@@ -168,6 +171,12 @@ def _pass_items(items, out_root, k):
 class _DryEngine:
     """--dry-run stand-in for the native Engine: every slice 'succeeds' instantly."""
 
+    def submit(self, work):
+        return work
+
+    def wait(self, work):
+        return self.run_list(work)
+
     def run_list(self, work):
         import numpy as np
         zero = {k: 0.0 for k in ("load_s", "load_cpu_s", "h2d_s", "kernels_s", "write_s", "write_cpu_s",
@@ -225,10 +234,28 @@ def run_rank(args):
     def measure(scaling, out_root, steps, warmup):
         mine, global_items = shard(scaling, out_root)
         work = n.WorkList(mine)  # the shard's work list in native form (built once, like the plan)
-        for _ in range(warmup):
-            codes, msgs, _ = engine.run_list(work)
+        # Pipelined passes alternate between two output trees: two runs in flight never write the
+        # same file (pass k+2 is submitted only after pass k finished).
+        works = [work, n.WorkList(_pass_items(mine, out_root, 1))] if not args.no_pipeline else [work]
+
+        def passes(k_total, sink):
+            if args.no_pipeline:
+                for _ in range(k_total):
+                    with _roctx_range("bench.step"):
+                        sink(*engine.run_list(work))
+                return
+            pending = []
+            for k in range(k_total):
+                pending.append(engine.submit(works[k % 2]))
+                if len(pending) == 2:
+                    sink(*engine.wait(pending.pop(0)))
+            for t in pending:
+                sink(*engine.wait(t))
+
+        def check_warm(codes, msgs, _):
             if msgs:
                 raise SystemExit(f"rank {rank}: {len(msgs)} slices failed in warmup: {list(msgs.items())[:3]}")
+        passes(warmup, check_warm)
         stream = None
         if args.stream_steps:
             stream = n.WorkList([it for k in range(steps) for it in _pass_items(mine, out_root, k)])
@@ -248,12 +275,13 @@ def run_rank(args):
             for k in stage:
                 stage[k] += times[k]
         else:
-            for _ in range(steps):
-                with _roctx_range("bench.step"):
-                    codes, msgs, times = engine.run_list(work)
+            def sink(codes, msgs, times):
+                nonlocal ok
                 ok += len(codes) - len(msgs)
                 for k in stage:
                     stage[k] += times[k]
+            with _roctx_range("bench.steps"):
+                passes(steps, sink)
         t_own = time.perf_counter() - t0  # this rank's own time, before waiting for the others
         if torch.cuda.is_available():
             torch.cuda.synchronize()
@@ -318,6 +346,7 @@ def run_rank(args):
                 "streams": args.streams,
                 "threads": args.threads,
                 "stream_steps": bool(args.stream_steps),
+                "pipelined_passes": not args.no_pipeline and not args.stream_steps,
                 "comm": comm_info,
                 "rank0_stage_s": primary["rank0_stage_s"],
                 "cgroup_cpu_ms_per_step": primary["cgroup_cpu_ms_per_step"],

@@ -89,6 +89,9 @@ struct SingleResult {
   std::vector<std::vector<uint8_t>> canvases, jpegs;
 };
 
+struct RunHandle;  // a submitted run (Engine::submit)
+using RunTicket = std::shared_ptr<RunHandle>;
+
 class Engine {
  public:
   explicit Engine(const EngineConfig& cfg);
@@ -101,13 +104,24 @@ class Engine {
   std::vector<SliceStatus> run(const std::vector<WorkItem>& items, StageTimes* times = nullptr,
                                const std::function<void(size_t)>& on_start = {});
 
+  // Asynchronous form: queue a run and return at once. Runs are processed in submission order,
+  // and the slots move on to a queued run's batches while the previous run drains, so a caller
+  // that keeps the next run submitted (double buffering) never pays the slot ring's fill/drain
+  // between runs. `items` stays shared with the engine until the run finished. Two runs in flight
+  // must not write the same output files.
+  RunTicket submit(std::shared_ptr<const std::vector<WorkItem>> items, std::function<void(size_t)> on_start = {});
+  // Blocks until the run finished; rethrows an engine error of that run.
+  std::vector<SliceStatus> wait(const RunTicket& ticket, StageTimes* times = nullptr);
+
   // One slice through every stage with all intermediate outputs copied back (test_pipeline).
+  // Waits for queued runs; not to be called concurrently with submit().
   SingleResult run_single(const golden::SliceInput& s);
 
   const EngineConfig& config() const;
 
- private:
   struct Impl;
+
+ private:
   std::unique_ptr<Impl> impl_;
 };
 

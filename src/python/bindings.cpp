@@ -535,18 +535,23 @@ PYBIND11_MODULE(_nm03, m) {
   });
 
   // ---- engine --------------------------------------------------------------------------------------
-  // A work list converted once to its native form (the cohort plan), reusable across runs.
+  // A work list converted once to its native form (the cohort plan), reusable across runs and
+  // shared with the engine while a submitted run is in flight.
   struct WorkList {
-    std::vector<WorkItem> items;
+    std::shared_ptr<std::vector<WorkItem>> items = std::make_shared<std::vector<WorkItem>>();
   };
   py::class_<WorkList>(m, "WorkList")
       .def(py::init([](const std::vector<std::pair<std::string, std::string>>& items) {
         WorkList w;
-        w.items.reserve(items.size());
-        for (auto& p : items) w.items.push_back({p.first, p.second});
+        w.items->reserve(items.size());
+        for (auto& p : items) w.items->push_back({p.first, p.second});
         return w;
       }))
-      .def("__len__", [](const WorkList& w) { return w.items.size(); });
+      .def("__len__", [](const WorkList& w) { return w.items->size(); });
+  struct Ticket {
+    RunTicket t;
+  };
+  py::class_<Ticket>(m, "RunTicket");
   auto times_dict = [](const StageTimes& t) {
     py::dict td;
     td["load_s"] = t.load_s;
@@ -564,6 +569,16 @@ PYBIND11_MODULE(_nm03, m) {
     td["bytes_out"] = t.bytes_out;
     td["jpeg_fallbacks"] = t.jpeg_fallbacks;
     return td;
+  };
+  auto compact = [times_dict](const std::vector<SliceStatus>& st, const StageTimes& t) {
+    py::array_t<int32_t> codes((py::ssize_t)st.size());
+    auto c = codes.mutable_unchecked<1>();
+    py::dict msgs;
+    for (size_t i = 0; i < st.size(); ++i) {
+      c((py::ssize_t)i) = st[i].code;
+      if (st[i].code != kSliceOk) msgs[py::int_(i)] = st[i].message;
+    }
+    return py::make_tuple(codes, msgs, times_dict(t));
   };
   py::class_<Engine>(m, "Engine")
       .def(py::init<const EngineConfig&>())
@@ -585,21 +600,34 @@ PYBIND11_MODULE(_nm03, m) {
       .def(
           "run_list",
           // Compact form for hot loops: (codes int32[n], {index: message} for non-OK slices, times).
-          [times_dict](Engine& e, const WorkList& wl) {
+          [compact](Engine& e, const WorkList& wl) {
             StageTimes t;
             std::vector<SliceStatus> st;
             {
               py::gil_scoped_release nogil;
-              st = e.run(wl.items, &t);
+              st = e.run(*wl.items, &t);
             }
-            py::array_t<int32_t> codes((py::ssize_t)st.size());
-            auto c = codes.mutable_unchecked<1>();
-            py::dict msgs;
-            for (size_t i = 0; i < st.size(); ++i) {
-              c((py::ssize_t)i) = st[i].code;
-              if (st[i].code != kSliceOk) msgs[py::int_(i)] = st[i].message;
+            return compact(st, t);
+          })
+      .def(
+          "submit",
+          // Queue a run and return at once (Engine::submit); the next run can be submitted before
+          // this one finished — the engine pipelines across them.
+          [](Engine& e, const WorkList& wl) {
+            py::gil_scoped_release nogil;
+            return Ticket{e.submit(wl.items)};
+          })
+      .def(
+          "wait",
+          // Result of a submitted run, in run_list's compact form.
+          [compact](Engine& e, const Ticket& t) {
+            StageTimes tm;
+            std::vector<SliceStatus> st;
+            {
+              py::gil_scoped_release nogil;
+              st = e.wait(t.t, &tm);
             }
-            return py::make_tuple(codes, msgs, times_dict(t));
+            return compact(st, tm);
           })
       .def("run_single",
            [](Engine& e, py::array_t<uint16_t, py::array::c_style | py::array::forcecast> raw, const std::string& type,

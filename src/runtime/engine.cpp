@@ -13,6 +13,7 @@
 #include <condition_variable>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <map>
 #include <mutex>
 #include <thread>
@@ -685,10 +686,11 @@ struct Engine::Impl {
     return false;
   }
 
-  void process_batch(Slot& s, const std::vector<WorkItem>& items, size_t batch, size_t first, size_t count,
-                     std::vector<SliceStatus>& status, StageTimes& acc, std::mutex& acc_m,
+  // `batch`: index within its run (fault injection); `prio`: engine-wide batch sequence number,
+  // the host-pool priority (earlier batches first, also across queued runs).
+  void process_batch(Slot& s, const std::vector<WorkItem>& items, size_t batch, uint64_t prio, size_t first,
+                     size_t count, std::vector<SliceStatus>& status, StageTimes& acc, std::mutex& acc_m,
                      const std::function<void(size_t)>& on_start) {
-    // `batch` doubles as the host-pool priority: earlier batches first.
     s.raw_used = 0;
     s.loaded.assign(count, LoadedSlice{});
     if (!s.allocs) s.allocs.reset(new Slot::Alloc[s.cap_slices]);
@@ -720,7 +722,7 @@ struct Engine::Impl {
               s.prog_cv.notify_one();
             }
           },
-          2 * batch);
+          2 * prio);
       if (upload_chunk_) {
         // A failed early upload fails the batch like any device error (below), not the run; the
         // loads still finish (tg.wait) before the blob is touched again.
@@ -790,7 +792,7 @@ struct Engine::Impl {
             write_ns += (int64_t)((now_s() - t0) * 1e9);
             write_cpu_ns += thread_cpu_ns() - c0;
           },
-          2 * batch + 1);
+          2 * prio + 1);
       tg.wait();
     }
     std::lock_guard<std::mutex> g(acc_m);
@@ -835,24 +837,31 @@ struct Engine::Impl {
     return out;
   }
 
-  // ---- persistent slot workers: one host thread per slot, parked between runs --------------
+  // ---- persistent slot workers: one host thread per slot --------------------------------------
+  // Runs are queued (submit): a slot that finishes a batch takes the next unclaimed batch of the
+  // oldest queued run, so consecutive runs pipeline — the slots of run k+1 load, upload and compute
+  // while run k's last batches drain — instead of every run paying the ring's fill and drain.
   struct Job {
-    const std::vector<WorkItem>* items = nullptr;
-    std::vector<SliceStatus>* status = nullptr;
-    StageTimes* acc = nullptr;
-    std::mutex* acc_m = nullptr;
-    const std::function<void(size_t)>* on_start = nullptr;
+    std::shared_ptr<const std::vector<WorkItem>> items;
+    std::function<void(size_t)> on_start;
+    std::vector<SliceStatus> status;
+    StageTimes acc;
+    std::mutex acc_m;
     std::vector<std::pair<size_t, size_t>> batches;  // (first, count)
-    std::atomic<size_t> next{0};
+    size_t next = 0;     // next unclaimed batch (guarded by job_m)
+    uint64_t seq0 = 0;   // engine-wide sequence number of batch 0
+    std::atomic<size_t> remaining{0};
+    double t0 = 0;
+    bool done = false;   // guarded by job_m
     std::exception_ptr err;
     std::mutex err_m;
   };
   std::vector<std::thread> workers;
-  std::mutex job_m, run_m;
+  std::mutex job_m, single_m;
   std::condition_variable job_cv, done_cv;
-  Job* job = nullptr;
-  uint64_t job_gen = 0;
-  int busy = 0;
+  std::deque<std::shared_ptr<Job>> queue;  // runs with unclaimed batches, oldest first
+  uint64_t seq_next = 0;
+  size_t inflight = 0;  // submitted runs not finished yet
   bool quit = false;
 
   void start_workers() {
@@ -860,7 +869,8 @@ struct Engine::Impl {
   }
   void stop_workers() {
     {
-      std::lock_guard<std::mutex> g(job_m);
+      std::unique_lock<std::mutex> g(job_m);
+      done_cv.wait(g, [&] { return inflight == 0; });  // queued runs finish first
       quit = true;
     }
     job_cv.notify_all();
@@ -868,74 +878,97 @@ struct Engine::Impl {
     workers.clear();
   }
 
+  void finish(Job& j) {
+    for (const auto& st : j.status) (st.code == kSliceOk ? j.acc.slices_ok : j.acc.slices_failed) += 1;
+    j.acc.wall_s = now_s() - j.t0;
+    if (j.acc.jpeg_fallbacks) log_warn(std::to_string(j.acc.jpeg_fallbacks) + " JPEG(s) exceeded GPU capacity; CPU-encoded");
+    log_info("run: " + std::to_string(j.items->size()) + " slices in " + std::to_string(j.acc.batches) + " batches, " +
+             std::to_string(j.acc.wall_s * 1e3) + " ms, " + std::to_string(j.acc.slices_failed) + " failed");
+    {
+      std::lock_guard<std::mutex> g(job_m);
+      j.done = true;
+      --inflight;
+    }
+    done_cv.notify_all();
+  }
+
   void worker(Slot* s) {
     place.bind_this_thread();
     (void)prctl(PR_SET_TIMERSLACK, 1000UL, 0, 0, 0);  // 1 µs: short poll sleeps stay short
     (void)hipSetDevice(cfg.device);
-    uint64_t seen = 0;
     for (;;) {
-      Job* j;
+      std::shared_ptr<Job> j;
+      size_t b;
       {
         std::unique_lock<std::mutex> g(job_m);
-        job_cv.wait(g, [&] { return quit || job_gen != seen; });
-        if (quit) return;
-        seen = job_gen;
-        j = job;
+        job_cv.wait(g, [&] { return quit || !queue.empty(); });
+        if (queue.empty()) return;  // quit
+        j = queue.front();
+        b = j->next++;
+        if (j->next == j->batches.size()) queue.pop_front();
       }
       const int64_t c0 = thread_cpu_ns();
       try {
-        for (size_t b; (b = j->next.fetch_add(1)) < j->batches.size();) {
-          const auto [first, count] = j->batches[b];
-          process_batch(*s, *j->items, b, first, count, *j->status, *j->acc, *j->acc_m, *j->on_start);
-        }
+        const auto [first, count] = j->batches[b];
+        process_batch(*s, *j->items, b, j->seq0 + b, first, count, j->status, j->acc, j->acc_m, j->on_start);
       } catch (...) {
         std::lock_guard<std::mutex> g(j->err_m);
         if (!j->err) j->err = std::current_exception();
       }
       {
-        std::lock_guard<std::mutex> g(*j->acc_m);
-        j->acc->slot_cpu_s += (thread_cpu_ns() - c0) * 1e-9;
+        std::lock_guard<std::mutex> g(j->acc_m);
+        j->acc.slot_cpu_s += (thread_cpu_ns() - c0) * 1e-9;
       }
-      std::lock_guard<std::mutex> g(job_m);
-      if (--busy == 0) done_cv.notify_all();
+      if (j->remaining.fetch_sub(1) == 1) finish(*j);
     }
+  }
+
+  std::shared_ptr<Job> submit(std::shared_ptr<const std::vector<WorkItem>> items, std::function<void(size_t)> on_start) {
+    auto j = std::make_shared<Job>();
+    j->t0 = now_s();
+    j->items = std::move(items);
+    j->on_start = std::move(on_start);
+    j->status.resize(j->items->size());
+    j->batches = plan_batches(j->items->size(), (size_t)cfg.batch_size, cfg.taper);
+    j->remaining = j->batches.size();
+    {
+      std::lock_guard<std::mutex> g(job_m);
+      j->seq0 = seq_next;
+      seq_next += j->batches.size();
+      ++inflight;
+      if (!j->batches.empty()) queue.push_back(j);
+    }
+    if (j->batches.empty())
+      finish(*j);
+    else
+      job_cv.notify_all();
+    return j;
+  }
+
+  std::vector<SliceStatus> wait(const std::shared_ptr<Job>& j, StageTimes* times) {
+    {
+      std::unique_lock<std::mutex> g(job_m);
+      done_cv.wait(g, [&] { return j->done; });
+    }
+    if (j->err) std::rethrow_exception(j->err);
+    if (times) *times = j->acc;
+    return j->status;
   }
 
   std::vector<SliceStatus> run(const std::vector<WorkItem>& items, StageTimes* times,
                                const std::function<void(size_t)>& on_start) {
-    std::lock_guard<std::mutex> serial(run_m);
-    const double t0 = now_s();
-    std::vector<SliceStatus> status(items.size());
-    StageTimes acc;
-    std::mutex acc_m;
-    Job j;
-    j.items = &items;
-    j.status = &status;
-    j.acc = &acc;
-    j.acc_m = &acc_m;
-    j.on_start = &on_start;
-    j.batches = plan_batches(items.size(), (size_t)cfg.batch_size, cfg.taper);
-    {
-      std::unique_lock<std::mutex> g(job_m);
-      job = &j;
-      busy = (int)workers.size();
-      ++job_gen;
-      job_cv.notify_all();
-      done_cv.wait(g, [&] { return busy == 0; });
-      job = nullptr;
-    }
-    if (j.err) std::rethrow_exception(j.err);
-    for (const auto& st : status) (st.code == kSliceOk ? acc.slices_ok : acc.slices_failed) += 1;
-    acc.wall_s = now_s() - t0;
-    if (acc.jpeg_fallbacks) log_warn(std::to_string(acc.jpeg_fallbacks) + " JPEG(s) exceeded GPU capacity; CPU-encoded");
-    log_info("run: " + std::to_string(items.size()) + " slices in " + std::to_string(acc.batches) + " batches, " +
-             std::to_string(acc.wall_s * 1e3) + " ms, " + std::to_string(acc.slices_failed) + " failed");
-    if (times) *times = acc;
-    return status;
+    // Blocking form: the caller's vector outlives the run.
+    std::shared_ptr<const std::vector<WorkItem>> view(&items, [](const std::vector<WorkItem>*) {});
+    return wait(submit(view, on_start), times);
   }
 
   SingleResult run_single(const golden::SliceInput& in) {
-    std::lock_guard<std::mutex> serial(run_m);
+    std::lock_guard<std::mutex> serial(single_m);
+    {
+      // Slot 0 is used directly: no queued run may be using it.
+      std::unique_lock<std::mutex> g(job_m);
+      done_cv.wait(g, [&] { return inflight == 0; });
+    }
     check_hip(hipSetDevice(cfg.device), "hipSetDevice");
     Slot& s = *slots[0];
     if (in.w > cfg.max_dim || in.h > cfg.max_dim) throw DeviceError("slice exceeds engine max_dim");
@@ -1008,6 +1041,13 @@ std::vector<SliceStatus> Engine::run(const std::vector<WorkItem>& items, StageTi
                                      const std::function<void(size_t)>& on_start) {
   return impl_->run(items, times, on_start);
 }
+struct RunHandle {
+  std::shared_ptr<Engine::Impl::Job> job;
+};
+RunTicket Engine::submit(std::shared_ptr<const std::vector<WorkItem>> items, std::function<void(size_t)> on_start) {
+  return std::make_shared<RunHandle>(RunHandle{impl_->submit(std::move(items), std::move(on_start))});
+}
+std::vector<SliceStatus> Engine::wait(const RunTicket& t, StageTimes* times) { return impl_->wait(t->job, times); }
 SingleResult Engine::run_single(const golden::SliceInput& s) { return impl_->run_single(s); }
 const EngineConfig& Engine::config() const { return impl_->cfg; }
 

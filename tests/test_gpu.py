@@ -249,6 +249,31 @@ def test_engine_cohort_configs_identical(native, cohort_root, tmp_path):
     assert trees[0][f"{pid}/{stem}_processed.jpg"] == g["jpeg_processed"]
 
 
+def test_engine_submit_pipelines_runs_identically(native, cohort_root, tmp_path):
+    """Queued runs (Engine.submit/wait, several in flight, the slots moving on to run k+1 while run
+    k drains) write exactly what blocking runs write, and report per-run statuses and times."""
+    ref_out = str(tmp_path / "ref")
+    ref_items = _items(native, cohort_root, ref_out)
+    eng = native.Engine(nm.PipelineConfig(batch_size=5, streams=3, threads=8).engine_config())
+    st, _ = eng.run(ref_items)
+    assert all(code == 0 for code, _ in st)
+    ref = _tree(ref_out)
+    outs = [str(tmp_path / f"q{k}") for k in range(4)]
+    works = [native.WorkList(_items(native, cohort_root, o)) for o in outs]
+    tickets = [eng.submit(w) for w in works]  # four runs queued at once
+    for t, w in zip(tickets, works):
+        codes, msgs, times = eng.wait(t)
+        assert len(codes) == len(w) and not msgs and times["slices_ok"] == len(w)
+        assert times["batches"] == -(-len(w) // 5)
+    for o in outs:
+        assert _tree(o) == ref
+    # an empty run completes at once; a run after the queue drained still works
+    codes, msgs, times = eng.wait(eng.submit(native.WorkList([])))
+    assert len(codes) == 0 and times["batches"] == 0
+    codes, msgs, _ = eng.run_list(works[0])
+    assert not msgs
+
+
 def test_engine_fault_isolation(native, tmp_path):
     d = tmp_path / "series"
     d.mkdir()
