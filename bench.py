@@ -122,11 +122,12 @@ def _free_port():
 
 def launch(args, argv, grace_s=5.0):
     n = args.gpus
-    port = _free_port()
+    port = _free_port()  # only for code that wants an env:// store; the native comm uses the job id
+    job = os.urandom(8).hex()
     procs = []
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
-                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), NM03_COMM_JOB=job)
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env))
     rc, failed_at = 0, None
     while any(p.poll() is None for p in procs):

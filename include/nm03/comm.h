@@ -69,7 +69,8 @@ class ShmSegment {
   // Anonymous MAP_SHARED mapping: create BEFORE fork, every child inherits it.
   static std::shared_ptr<ShmSegment> create_anonymous(int n, size_t slot_bytes = 1 << 20);
   // Named segment for independently launched ranks (torchrun): rank 0 creates it under a fresh
-  // random name and publishes the name out of band (e.g. the torch TCPStore); the others attach.
+  // random name (or under *name when non-empty, e.g. a job id handed out by a launcher) and
+  // publishes the name out of band (e.g. the torch TCPStore); the others attach.
   // Rank 0's object unlinks the name once every rank has attached (the mapping stays valid).
   static std::shared_ptr<ShmSegment> create_named(int n, std::string* name, size_t slot_bytes = 1 << 20);
   static std::shared_ptr<ShmSegment> attach_named(const std::string& name, int n, double timeout_s);

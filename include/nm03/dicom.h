@@ -67,10 +67,22 @@ enum class ReadMode { kDirect, kStaged, kMapped };
 class SliceFile {
  public:
   explicit SliceFile(const std::string& path, ReadMode mode = ReadMode::kDirect, size_t prefix = 16384);
+  // `name` relative to the directory fd `dirfd` (openat: no path walk from the root per file);
+  // `path` is only used in messages.
+  SliceFile(int dirfd, const char* name, const std::string& path, ReadMode mode = ReadMode::kDirect,
+            size_t prefix = 16384);
   ~SliceFile();
   SliceFile(const SliceFile&) = delete;
   SliceFile& operator=(const SliceFile&) = delete;
   size_t size() const { return size_; }
+  // kMapped only: map the file at `addr` (MAP_FIXED inside a caller-reserved region of `cap`
+  // bytes) instead of a fresh address, and leave it mapped: the caller unmaps the whole region in
+  // one call (one TLB shootdown for a batch of files instead of one per file). Files larger than
+  // `cap` get an ordinary mapping.
+  void map_at(void* addr, size_t cap) {
+    map_at_ = addr;
+    map_cap_ = cap;
+  }
   // Parses the header (`buf` is scratch space owned by the caller and must outlive pixels16).
   const Header& header(std::vector<uint8_t>& buf);
   // First frame as 16-bit words into dst (rows*cols elements).
@@ -86,6 +98,9 @@ class SliceFile {
   const uint8_t* data() const { return map_ ? map_ : buf_->data(); }
   std::string path_;
   const uint8_t* map_ = nullptr;  // kMapped: the whole file
+  bool own_map_ = true;           // false: mapped at map_at_, the caller unmaps
+  void* map_at_ = nullptr;
+  size_t map_cap_ = 0;
   int fd_ = -1;
   size_t size_ = 0;
   ReadMode mode_ = ReadMode::kDirect;

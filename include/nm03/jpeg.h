@@ -38,5 +38,9 @@ std::vector<uint8_t> encode_scan_gray420(const uint8_t* gray, int width, int hei
 // Write header + scan + EOI to a file (single writev-style write).
 void write_jpeg_file(const std::string& path, const std::vector<uint8_t>& header, const uint8_t* scan,
                      size_t scan_len);
+// Same, `name` relative to the directory fd `dirfd` (openat: no path walk per file); `dir` only
+// names the file in error messages.
+void write_jpeg_at(int dirfd, const std::string& dir, const std::string& name, const std::vector<uint8_t>& header,
+                   const uint8_t* scan, size_t scan_len);
 
 }  // namespace nm03::jpeg

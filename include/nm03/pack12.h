@@ -24,6 +24,14 @@ bool available();
 // 0 (dst untouched beyond scratch use) when some sample needs more bits or n % 16 != 0.
 size_t pack(const uint16_t* src, size_t n, uint8_t* dst);
 
+// True when n % 16 == 0, the packer is available and every sample fits in 12 bits.
+bool fits12(const uint16_t* src, size_t n);
+
+// Packs n samples that passed fits12() straight into dst — pinned upload memory — through an
+// L1-sized bounce buffer and streaming stores: no full-size intermediate, and exactly n * 3 / 2
+// bytes are written (nothing past the end: neighbouring slices may be written concurrently).
+void pack_stream(const uint16_t* src, size_t n, uint8_t* dst);
+
 // Scalar reference of the inverse (tests; the device expands with k0_unpack.hip).
 void unpack(const uint8_t* src, size_t n, uint16_t* dst);
 

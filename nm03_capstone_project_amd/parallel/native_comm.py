@@ -1,10 +1,11 @@
 """Native communicators for independently launched rank processes (torchrun or bench.py's own
 launcher): the same C++ `Comm` the CLI uses (src/dist/: RcclComm over xGMI, HostComm over a
-process-shared segment), bootstrapped through the torch rendezvous store.
+process-shared segment).
 
-Only the rendezvous uses torch (the env:// TCPStore at MASTER_ADDR:MASTER_PORT, shared with the
-torchrun agent when TORCHELASTIC_USE_AGENT_STORE is set); every collective runs in native code
-with deadlines (NM03_COMM_TIMEOUT_S) and the job abort flag of the shared segment.
+Rendezvous: bench.py's launcher hands every rank a job id (NM03_COMM_JOB) that names the segment;
+under torchrun, rank 0 publishes the segment name through the env:// TCPStore (shared with the
+torchrun agent when TORCHELASTIC_USE_AGENT_STORE is set) — the only use of torch here. Every
+collective runs in native code with deadlines (NM03_COMM_TIMEOUT_S).
 
 Backend choice (`backend` or NM03_COMM): "rccl" | "host" | "auto". auto = RCCL when every rank has
 its own GPU, host when ranks share one (NM03_DEVICE_OVERRIDE; RCCL refuses two ranks per device),
@@ -54,47 +55,61 @@ def _store(rank, world, timeout_s):
 def make_native_comm(rank, world, device, backend=None, timeout_s=None):
     """Returns (comm, info). `comm` is a native `Comm` (rank/size/backend, barrier,
     broadcast_bytes, allgather_bytes, allreduce_sum/max, allgather_f64); `info` records the backend
-    used and, if RCCL was abandoned under auto, why."""
+    used and, if RCCL was abandoned under auto, why.
+
+    Rendezvous: with NM03_COMM_JOB set (bench.py's launcher hands every rank the same job id) the
+    segment name derives from it; otherwise (torchrun) rank 0 publishes a fresh name through the
+    env:// rendezvous store. Everything after that — the RCCL unique id, the agreement on whether
+    RCCL came up on every rank — goes over the shared segment."""
     n = native()
     if world <= 1:
         return n.self_comm(), {"backend": "self"}
     timeout_s = float(timeout_s or n.comm_timeout_s())
     be, may_fall_back = resolve_backend(world, backend)
-    store = _store(rank, world, timeout_s)
-    # Every job has a shared segment: the host collectives, and the abort flag RCCL waits watch.
-    if rank == 0:
-        seg, name = n.shm_create(world)
-        store.set("shm", name)
-        seg.wait_attached_and_unlink(timeout_s)
+    job = os.environ.get("NM03_COMM_JOB", "")
+    if job:
+        name = f"/nm03-comm-{job}"
+        seg = n.shm_create(world, name)[0] if rank == 0 else n.shm_attach(name, world, timeout_s)
     else:
-        store.wait(["shm"], timedelta(seconds=timeout_s))
-        seg = n.shm_attach(store.get("shm").decode(), world, timeout_s)
+        store = _store(rank, world, timeout_s)
+        if rank == 0:
+            seg, name = n.shm_create(world)
+            store.set("shm", name)
+        else:
+            store.wait(["shm"], timedelta(seconds=timeout_s))
+            seg = n.shm_attach(store.get("shm").decode(), world, timeout_s)
+    if rank == 0:
+        seg.wait_attached_and_unlink(timeout_s)
+    host = n.host_comm(seg, rank, timeout_s)
     info = {"backend": be}
-    if be == "rccl":
-        comm, err = None, ""
+    if be == "host":
+        return host, info
+    # RCCL: unique id from rank 0 over the segment, then every rank reports whether its
+    # communicator came up (a slow init may use its whole deadline: the agreement waits longer).
+    uid, err = b"", ""
+    if rank == 0:
         try:
-            if rank == 0:
-                uid = b""
-                try:
-                    uid = n.rccl_unique_id()
-                finally:
-                    store.set("uid", uid)  # empty on failure: peers fail fast instead of waiting
-            else:
-                store.wait(["uid"], timedelta(seconds=timeout_s))
-                uid = store.get("uid")
-            comm = n.rccl_comm(rank, world, uid, device, seg, timeout_s)
+            uid = n.rccl_unique_id()
         except Exception as e:  # noqa: BLE001 - reported below, on every rank
             err = f"{type(e).__name__}: {e}"
-        store.set(f"rccl_status_{rank}", err or "ok")
-        keys = [f"rccl_status_{r}" for r in range(world)]
-        store.wait(keys, timedelta(seconds=timeout_s))
-        bad = [(r, store.get(k).decode()) for r, k in enumerate(keys)]
-        bad = [(r, s) for r, s in bad if s != "ok"]
-        if not bad:
-            return comm, info
-        if not may_fall_back:
-            raise RuntimeError(f"RCCL initialisation failed on rank(s) {bad}")
-        info = {"backend": "host", "rccl_error": f"rank {bad[0][0]}: {bad[0][1]}"}
-        if comm is not None:
-            _ABANDONED.append(comm)
-    return n.host_comm(seg, rank, timeout_s), info
+    uid = host.broadcast_bytes(uid, 0)
+    comm = None
+    if uid:
+        try:
+            # No segment for RCCL's own waits: a timed-out init must not raise the segment's abort
+            # flag, which would also fail the agreement below and with it the host fallback.
+            comm = n.rccl_comm(rank, world, uid, device, None, timeout_s)
+        except Exception as e:  # noqa: BLE001
+            err = f"{type(e).__name__}: {e}"
+    elif not err:
+        err = "no RCCL unique id from rank 0"
+    agree = n.host_comm(seg, rank, 2 * timeout_s + 10)
+    errs = [e.decode() for e in agree.allgather_bytes(err.encode())]
+    bad = [(r, e) for r, e in enumerate(errs) if e]
+    if not bad:
+        return comm, info
+    if not may_fall_back:
+        raise RuntimeError(f"RCCL initialisation failed on rank(s) {bad}")
+    if comm is not None:
+        _ABANDONED.append(comm)
+    return host, {"backend": "host", "rccl_error": f"rank {bad[0][0]}: {bad[0][1]}"}

@@ -227,6 +227,7 @@ int exit_code(int st) { return WIFEXITED(st) ? WEXITSTATUS(st) : 128 + (WIFSIGNA
 int supervise(std::vector<pid_t>& kids, ShmSegment& seg, double grace) {
   const int n = (int)kids.size();
   int alive = n, rc = 0;
+  std::vector<int> codes((size_t)n, 0);
   double fail_t = -1;
   int signals_sent = 0;
   while (alive > 0) {
@@ -241,6 +242,7 @@ int supervise(std::vector<pid_t>& kids, ShmSegment& seg, double grace) {
       --alive;
       reaped = true;
       const int code = p < 0 ? 1 : exit_code(st);
+      codes[r] = code;
       if (code != 0) {
         fprintf(stderr, "Rank %d exited with status %d\n", r, code);
         fflush(stderr);
@@ -271,6 +273,10 @@ int supervise(std::vector<pid_t>& kids, ShmSegment& seg, double grace) {
     }
     std::this_thread::sleep_for(std::chrono::milliseconds(5));
   }
+  // The job's status is the root cause's: the rank that raised the abort first (peers that only
+  // failed because of it exit 1, possibly before the supervisor reaped the culprit).
+  const int root = seg.abort_rank();
+  if (rc && root >= 0 && root < n && codes[root] != 0) rc = codes[root];
   return rc;
 }
 

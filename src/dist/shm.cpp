@@ -108,9 +108,13 @@ std::shared_ptr<ShmSegment> ShmSegment::create_named(int n, std::string* name, s
   slot_bytes = (slot_bytes + 4095) / 4096 * 4096;
   const size_t bytes = kHeaderBytes + (size_t)n * slot_bytes;
   std::random_device rd;
-  for (int attempt = 0; attempt < 8; ++attempt) {
-    char buf[64];
-    snprintf(buf, sizeof(buf), "/nm03-comm-%d-%08x%08x", (int)getpid(), rd(), rd());
+  const bool given = !name->empty();
+  for (int attempt = 0; attempt < (given ? 1 : 8); ++attempt) {
+    char buf[96];
+    if (given)
+      snprintf(buf, sizeof(buf), "%s", name->c_str());
+    else
+      snprintf(buf, sizeof(buf), "/nm03-comm-%d-%08x%08x", (int)getpid(), rd(), rd());
     const int fd = shm_open(buf, O_CREAT | O_EXCL | O_RDWR, 0600);
     if (fd < 0) continue;
     if (ftruncate(fd, (off_t)bytes) != 0) {

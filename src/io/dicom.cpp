@@ -334,8 +334,11 @@ size_t read_file_into(const std::string& path, std::vector<uint8_t>& buf) {
 // SliceFile: header from a 16 KiB prefix, pixels read straight into the caller's buffer.
 // ------------------------------------------------------------------------------------------------
 SliceFile::SliceFile(const std::string& path, ReadMode mode, size_t prefix)
+    : SliceFile(AT_FDCWD, path.c_str(), path, mode, prefix) {}
+
+SliceFile::SliceFile(int dirfd, const char* name, const std::string& path, ReadMode mode, size_t prefix)
     : path_(path), mode_(mode), prefix_(prefix < 1024 ? 1024 : prefix) {
-  fd_ = ::open(path.c_str(), O_RDONLY | O_CLOEXEC);
+  fd_ = ::openat(dirfd, name, O_RDONLY | O_CLOEXEC);
   if (fd_ < 0) throw SliceError("Cannot open file: " + path + " (" + std::strerror(errno) + ")");
   struct stat st;
   if (fstat(fd_, &st) != 0) {
@@ -347,7 +350,7 @@ SliceFile::SliceFile(const std::string& path, ReadMode mode, size_t prefix)
 }
 
 SliceFile::~SliceFile() {
-  if (map_) ::munmap(const_cast<uint8_t*>(map_), size_);
+  if (map_ && own_map_) ::munmap(const_cast<uint8_t*>(map_), size_);
   if (fd_ >= 0) ::close(fd_);
 }
 
@@ -364,8 +367,11 @@ void SliceFile::pread_all(void* dst, size_t n, size_t off) {
 const Header& SliceFile::header(std::vector<uint8_t>& buf) {
   buf_ = &buf;
   if (mode_ == ReadMode::kMapped && size_ > 0) {
-    void* m = ::mmap(nullptr, size_, PROT_READ, MAP_PRIVATE | MAP_POPULATE, fd_, 0);
+    const bool fixed = map_at_ && size_ <= map_cap_;
+    void* m = ::mmap(fixed ? map_at_ : nullptr, size_, PROT_READ, MAP_PRIVATE | MAP_POPULATE | (fixed ? MAP_FIXED : 0),
+                     fd_, 0);
     if (m == MAP_FAILED) throw SliceError("Cannot map file: " + path_);
+    own_map_ = !fixed;
     map_ = static_cast<const uint8_t*>(m);
     have_ = size_;
     h_ = parse(map_, size_);

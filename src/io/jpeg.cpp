@@ -194,11 +194,17 @@ std::vector<uint8_t> encode_gray420(const uint8_t* gray, int width, int height, 
 }
 
 void write_jpeg_file(const std::string& path, const std::vector<uint8_t>& header, const uint8_t* scan, size_t scan_len) {
+  write_jpeg_at(AT_FDCWD, "", path, header, scan, scan_len);
+}
+
+void write_jpeg_at(int dirfd, const std::string& dir, const std::string& name, const std::vector<uint8_t>& header,
+                   const uint8_t* scan, size_t scan_len) {
+  auto path = [&] { return dir.empty() ? name : dir + "/" + name; };
   // Overwrite in place instead of O_TRUNC: re-exporting a cohort rewrites files of (nearly) the
   // same size, and truncate + reallocate costs 4-12x more than pwrite on ext4/overlayfs. The old
   // tail is cut only when the previous file was longer, so the bytes on disk are identical.
-  int fd = ::open(path.c_str(), O_WRONLY | O_CREAT | O_CLOEXEC, 0644);
-  if (fd < 0) throw std::runtime_error("Cannot create " + path + ": " + std::strerror(errno));
+  int fd = ::openat(dirfd, name.c_str(), O_WRONLY | O_CREAT | O_CLOEXEC, 0644);
+  if (fd < 0) throw std::runtime_error("Cannot create " + path() + ": " + std::strerror(errno));
   static const uint8_t eoi[2] = {0xFF, 0xD9};
   struct iovec iov[3] = {{(void*)header.data(), header.size()}, {(void*)scan, scan_len}, {(void*)eoi, 2}};
   const size_t total = header.size() + scan_len + 2;
@@ -209,7 +215,7 @@ void write_jpeg_file(const std::string& path, const std::vector<uint8_t>& header
     if (w < 0 && errno == EINTR) continue;
     if (w <= 0) {
       ::close(fd);
-      throw std::runtime_error("Write failed: " + path);
+      throw std::runtime_error("Write failed: " + path());
     }
     done += (size_t)w;
     size_t adv = (size_t)w;
@@ -225,7 +231,7 @@ void write_jpeg_file(const std::string& path, const std::vector<uint8_t>& header
   struct stat st;
   if (fstat(fd, &st) == 0 && (size_t)st.st_size > total && ftruncate(fd, (off_t)total) != 0) {
     ::close(fd);
-    throw std::runtime_error("Truncate failed: " + path);
+    throw std::runtime_error("Truncate failed: " + path());
   }
   ::close(fd);
 }

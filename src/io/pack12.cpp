@@ -3,6 +3,10 @@
 
 #include <immintrin.h>
 
+#include <cstring>
+
+#include "nm03/dicom.h"
+
 namespace nm03::pack12 {
 
 namespace {
@@ -28,7 +32,39 @@ __attribute__((target("avx2"))) size_t pack_avx2(const uint16_t* src, size_t n, 
   return n / 2 * 3;
 }
 
+__attribute__((target("avx2"))) bool fits_avx2(const uint16_t* src, size_t n) {
+  __m256i acc = _mm256_setzero_si256();
+  for (size_t i = 0; i < n; i += 16) acc = _mm256_or_si256(acc, _mm256_loadu_si256(reinterpret_cast<const __m256i*>(src + i)));
+  return _mm256_testz_si256(acc, _mm256_set1_epi16((short)0xF000));
+}
+
+// 16 samples → 24 bytes at d (stores 28: callers keep 4 bytes of slack).
+__attribute__((target("avx2"))) inline void pack16(const uint16_t* src, uint8_t* d) {
+  const __m256i lo_mask = _mm256_set1_epi32(0x00000FFF), hi_mask = _mm256_set1_epi32(0x00FFF000);
+  const __m256i shuf = _mm256_setr_epi8(0, 1, 2, 4, 5, 6, 8, 9, 10, 12, 13, 14, -1, -1, -1, -1,  //
+                                        0, 1, 2, 4, 5, 6, 8, 9, 10, 12, 13, 14, -1, -1, -1, -1);
+  const __m256i v = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(src));
+  const __m256i p = _mm256_or_si256(_mm256_and_si256(v, lo_mask), _mm256_and_si256(_mm256_srli_epi32(v, 4), hi_mask));
+  const __m256i c = _mm256_shuffle_epi8(p, shuf);
+  _mm_storeu_si128(reinterpret_cast<__m128i*>(d), _mm256_castsi256_si128(c));
+  _mm_storeu_si128(reinterpret_cast<__m128i*>(d + 12), _mm256_extracti128_si256(c, 1));
+}
+
+__attribute__((target("avx2"))) void pack_stream_avx2(const uint16_t* src, size_t n, uint8_t* dst) {
+  constexpr size_t kChunk = 2048;  // samples per bounce (3 KiB packed: stays in L1)
+  alignas(64) uint8_t bounce[kChunk / 2 * 3 + 32];
+  for (size_t i = 0; i < n; i += kChunk) {
+    const size_t m = n - i < kChunk ? n - i : kChunk;
+    for (size_t k = 0; k < m; k += 16) pack16(src + i + k, bounce + k / 2 * 3);
+    dicom::stream_copy(dst + i / 2 * 3, bounce, m / 2 * 3);
+  }
+}
+
 }  // namespace
+
+bool fits12(const uint16_t* src, size_t n) { return n && !(n & 15) && available() && fits_avx2(src, n); }
+
+void pack_stream(const uint16_t* src, size_t n, uint8_t* dst) { pack_stream_avx2(src, n, dst); }
 
 bool available() {
   static const bool ok = __builtin_cpu_supports("avx2");

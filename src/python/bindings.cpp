@@ -914,11 +914,10 @@ PYBIND11_MODULE(_nm03, m) {
       }, py::arg("timeout_s") = 120.0)
       .def("raise_abort", &ShmSegment::raise_abort)
       .def_property_readonly("aborted", &ShmSegment::aborted);
-  m.def("shm_create", [](int n) {
-    std::string name;
+  m.def("shm_create", [](int n, std::string name) {
     auto s = ShmSegment::create_named(n, &name);
     return py::make_tuple(s, name);
-  });
+  }, py::arg("n"), py::arg("name") = std::string());
   m.def("shm_attach", [](const std::string& name, int n, double t) {
     py::gil_scoped_release nogil;
     return ShmSegment::attach_named(name, n, t);

@@ -2,6 +2,8 @@
 #include "nm03/engine.h"
 
 #include <hip/hip_runtime_api.h>
+#include <fcntl.h>
+#include <sys/mman.h>
 #include <sys/prctl.h>
 #include <unistd.h>
 
@@ -14,6 +16,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <deque>
+#include <unordered_map>
 #include <map>
 #include <mutex>
 #include <thread>
@@ -114,9 +117,59 @@ struct Slot {
   int ncanvas = 0;
   bool any_canvas = false;  // some image of the batch needs the generic render → canvas path
   int max_w = 0, max_h = 0;
+  double batch_ema_s = 0;  // enqueue → completion time of recent batches (wait_batch)
+  // NM03_LOAD_MODE=mapped: per-slot reserved address range; slice i of a batch maps its file at
+  // map_region + i * map_stride and the whole range is unmapped once after the batch's loads.
+  uint8_t* map_region = nullptr;
+  size_t map_stride = 0;
   // Captured kernel chains keyed by launch signature (see GraphKey in build_and_run). Every
   // pointer in the chain is fixed per slot, so a signature fully determines the launches.
   std::map<std::array<int, 11>, hipGraphExec_t> graphs;
+};
+
+// Directory fds of one run: every item's input series directory and output directory opened once
+// (O_PATH), so loads and writes use openat on the bare file name instead of walking the full path
+// per file. Opened per run, never cached across runs: a caller may wipe and re-create output
+// directories between runs (the CLIs do).
+struct IoDirs {
+  std::vector<int> fds;
+  std::vector<int32_t> in_fd, out_fd;  // per item: fd index, -1 = fall back to the full path
+  std::vector<uint32_t> in_name;       // per item: offset of the file name in its path
+  IoDirs(const std::vector<WorkItem>& items) {
+    std::unordered_map<std::string, int32_t> idx;
+    auto dir_index = [&](const std::string& d) -> int32_t {
+      auto it = idx.find(d);
+      if (it != idx.end()) return it->second;
+      const int fd = ::open(d.empty() ? "/" : d.c_str(), O_PATH | O_DIRECTORY | O_CLOEXEC);
+      int32_t k = -1;
+      if (fd >= 0) {
+        k = (int32_t)fds.size();
+        fds.push_back(fd);
+      }
+      idx.emplace(d, k);
+      return k;
+    };
+    in_fd.resize(items.size());
+    out_fd.resize(items.size());
+    in_name.resize(items.size());
+    for (size_t i = 0; i < items.size(); ++i) {
+      const std::string& p = items[i].path;
+      const size_t slash = p.rfind('/');
+      if (slash == std::string::npos) {
+        in_fd[i] = -1;
+        in_name[i] = 0;
+      } else {
+        in_fd[i] = dir_index(p.substr(0, slash));
+        in_name[i] = (uint32_t)(slash + 1);
+      }
+      out_fd[i] = dir_index(items[i].out_dir);
+    }
+  }
+  ~IoDirs() {
+    for (int fd : fds) ::close(fd);
+  }
+  IoDirs(const IoDirs&) = delete;
+  IoDirs& operator=(const IoDirs&) = delete;
 };
 
 void hip_free_all(Slot& s) {
@@ -127,6 +180,7 @@ void hip_free_all(Slot& s) {
                   (void*)s.jw.stage, (void*)s.jw.look, (void*)s.jw.ticket, (void*)s.jw.spill,
                   (void*)s.jw.total, (void*)s.jw.chunk_ff})
     if (p) (void)hipFree(p);
+  if (s.map_region) munmap(s.map_region, (size_t)s.cap_slices * s.map_stride);
   for (auto& kv : s.graphs) (void)hipGraphExecDestroy(kv.second);
   s.graphs.clear();
   if (s.ev0) (void)hipEventDestroy(s.ev0);
@@ -250,6 +304,12 @@ struct Engine::Impl {
     s.raw_base = o;
     s.blob_bytes = o + s.cap_pixels * sizeof(uint16_t);
     try {
+      if (read_mode_ == dicom::ReadMode::kMapped) {
+        s.map_stride = align_up((size_t)md * md * 2 + (1u << 20), 1u << 21);  // pixels + 1 MiB of header room
+        void* r = mmap(nullptr, (size_t)B * s.map_stride, PROT_NONE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
+        if (r == MAP_FAILED) throw DeviceError("cannot reserve the loader's mapping range");
+        s.map_region = static_cast<uint8_t*>(r);
+      }
       check_hip(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking), "hipStreamCreate");
       check_hip(hipEventCreate(&s.ev0), "hipEventCreate");
       check_hip(hipEventCreate(&s.ev1), "hipEventCreate");
@@ -365,21 +425,29 @@ struct Engine::Impl {
     }();
     return us;
   }
-  void wait_batch(hipEvent_t ev) {
+  // The slot first sleeps through most of the time its recent batches took from enqueue to
+  // completion (EMA), then polls: ~10 wake-ups per batch instead of one per poll interval over
+  // the whole batch (each wake-up is a context switch of host CPU the loaders/writers need).
+  void wait_batch(Slot& s, hipEvent_t ev, double t_enq) {
     if (wait_mode() != WaitMode::kPoll) {
       check_hip(hipEventSynchronize(ev), "batch sync");
       return;
     }
+    const double ahead = 0.8 * s.batch_ema_s - (now_s() - t_enq);
+    if (ahead > 100e-6 && hipEventQuery(ev) == hipErrorNotReady)
+      std::this_thread::sleep_for(std::chrono::duration<double>(ahead));
     for (;;) {
       const hipError_t e = hipEventQuery(ev);
-      if (e == hipSuccess) return;
+      if (e == hipSuccess) break;
       if (e != hipErrorNotReady) check_hip(e, "batch sync");
       std::this_thread::sleep_for(std::chrono::microseconds(poll_us()));
     }
+    const double took = now_s() - t_enq;
+    s.batch_ema_s = s.batch_ema_s > 0 ? 0.75 * s.batch_ema_s + 0.25 * took : took;
   }
 
   // ---- loading -------------------------------------------------------------------------------
-  void load_into(Slot& s, int i, size_t item, const std::string& path, SliceStatus& st,
+  void load_into(Slot& s, int i, size_t item, const std::string& path, int dirfd, const char* name, SliceStatus& st,
                  std::atomic<int64_t>& load_ns, std::atomic<int64_t>& load_cpu_ns, std::atomic<int64_t>& bytes_in) {
     thread_local std::vector<uint8_t> buf;
     TraceRange tr("nm03.load");
@@ -387,7 +455,8 @@ struct Engine::Impl {
     const int64_t c0 = thread_cpu_ns();
     try {
       if (fault_plan().corrupt_dicom == (int64_t)item) throw SliceError("injected fault: corrupt DICOM data");
-      dicom::SliceFile file(path, read_mode_, read_prefix_);
+      dicom::SliceFile file(dirfd, name, path, read_mode_, read_prefix_);
+      if (s.map_region) file.map_at(s.map_region + (size_t)i * s.map_stride, s.map_stride);
       const size_t n = file.size();
       const dicom::Header& h = file.header(buf);
       const int md = cfg.pipe.min_dim;
@@ -400,15 +469,11 @@ struct Engine::Impl {
                      " exceed the engine limit " + std::to_string(cfg.max_dim);
       } else {
         const size_t npix = (size_t)h.rows * h.cols;
-        // 12-bit transfer packing when every sample fits (staged reads of raw 16-bit data).
-        thread_local std::vector<uint8_t> pk;
+        // 12-bit transfer packing when every sample fits (staged or mapped raw 16-bit data),
+        // packed straight into the pinned blob (pack12::pack_stream).
         const uint16_t* samples = pack12_ ? file.staged_samples() : nullptr;
-        size_t pbytes = 0;
-        if (samples && (npix & 15) == 0) {
-          if (pk.size() < npix / 2 * 3 + 64) pk.resize(npix / 2 * 3 + 64);
-          pbytes = pack12::pack(samples, npix, pk.data());
-        }
-        const size_t alloc = pbytes ? align_up(pbytes / 2, 8) : align_up(npix, 8);
+        const bool packed = samples && pack12::fits12(samples, npix);
+        const size_t alloc = packed ? align_up(npix / 4 * 3, 8) : align_up(npix, 8);  // u16 elements
         size_t off, idx;
         {
           std::lock_guard<std::mutex> g(s.alloc_m);
@@ -422,8 +487,8 @@ struct Engine::Impl {
         }
         uint16_t* dst = reinterpret_cast<uint16_t*>(s.h_blob + s.raw_base) + off;
         try {
-          if (pbytes)
-            dicom::stream_copy(dst, pk.data(), pbytes);
+          if (packed)
+            pack12::pack_stream(samples, npix, reinterpret_cast<uint8_t*>(dst));
           else
             file.pixels16(dst);
         } catch (...) {
@@ -441,7 +506,7 @@ struct Engine::Impl {
         L.sx = h.spacing_x;
         L.sy = h.spacing_y;
         L.blob_off = (uint32_t)off;
-        L.packed = pbytes != 0;
+        L.packed = packed;
         L.ok = true;
         st.code = kSliceOk;
         bytes_in += (int64_t)n;
@@ -581,6 +646,7 @@ struct Engine::Impl {
     auto* d_raw = s.d_raw_x;
     auto plane = [&](Plane p) { return s.d_bits + p * s.plane_words; };
 
+    const double t_enq = now_s();
     if (!s.upload_started) check_hip(hipEventRecord(s.ev0, s.stream), "event");
     // Tables, then the raw pixels not already queued by upload_progress (all of them without it).
     check_hip(hipMemcpyAsync(s.d_blob, s.h_blob, s.raw_base, hipMemcpyHostToDevice, s.stream), "H2D tables");
@@ -653,7 +719,7 @@ struct Engine::Impl {
       check_hip(hipGraphLaunch(it->second, s.stream), "graph launch");
     }
     check_hip(hipEventRecord(s.ev2, s.stream), "event");
-    wait_batch(s.ev2);
+    wait_batch(s, s.ev2, t_enq);
     if (acc) {
       float a = 0, b = 0;
       (void)hipEventElapsedTime(&a, s.ev0, s.ev1);
@@ -688,9 +754,9 @@ struct Engine::Impl {
 
   // `batch`: index within its run (fault injection); `prio`: engine-wide batch sequence number,
   // the host-pool priority (earlier batches first, also across queued runs).
-  void process_batch(Slot& s, const std::vector<WorkItem>& items, size_t batch, uint64_t prio, size_t first,
-                     size_t count, std::vector<SliceStatus>& status, StageTimes& acc, std::mutex& acc_m,
-                     const std::function<void(size_t)>& on_start) {
+  void process_batch(Slot& s, const std::vector<WorkItem>& items, const IoDirs& dirs, size_t batch, uint64_t prio,
+                     size_t first, size_t count, std::vector<SliceStatus>& status, StageTimes& acc,
+                     std::mutex& acc_m, const std::function<void(size_t)>& on_start) {
     s.raw_used = 0;
     s.loaded.assign(count, LoadedSlice{});
     if (!s.allocs) s.allocs.reset(new Slot::Alloc[s.cap_slices]);
@@ -712,7 +778,10 @@ struct Engine::Impl {
             if (cfg.resume && outputs_exist(items[first + i])) {
               status[first + i] = SliceStatus{kSliceOk, "resumed: outputs already present"};
             } else {
-              load_into(s, (int)i, first + i, items[first + i].path, status[first + i], load_ns, load_cpu_ns, bytes_in);
+              const size_t it = first + i;
+              const int dfd = dirs.in_fd[it] >= 0 ? dirs.fds[dirs.in_fd[it]] : AT_FDCWD;
+              const char* nm = items[it].path.c_str() + (dirs.in_fd[it] >= 0 ? dirs.in_name[it] : 0);
+              load_into(s, (int)i, it, items[it].path, dfd, nm, status[it], load_ns, load_cpu_ns, bytes_in);
             }
             if (upload_chunk_) {
               {
@@ -733,6 +802,12 @@ struct Engine::Impl {
         }
       }
       tg.wait();
+    }
+    if (s.map_region) {
+      // One unmap for the batch's file mappings (they were only read by the loads above).
+      void* r = mmap(s.map_region, count * s.map_stride, PROT_NONE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE | MAP_FIXED,
+                     -1, 0);
+      if (r == MAP_FAILED) throw DeviceError("cannot release the loader's mappings");
     }
     s.live.clear();
     for (size_t i = 0; i < count; ++i)
@@ -777,13 +852,16 @@ struct Engine::Impl {
             TraceRange tr("nm03.export");
             try {
               if (fault_plan().fail_write == (int64_t)item) throw std::runtime_error("injected fault: export failure");
-              const std::string base = cohort::with_slash(items[item].out_dir) + cohort::stem(items[item].path);
+              const bool rel = dirs.out_fd[item] >= 0;
+              const int dfd = rel ? dirs.fds[dirs.out_fd[item]] : AT_FDCWD;
+              const std::string base = (rel ? std::string() : cohort::with_slash(items[item].out_dir)) +
+                                       cohort::stem(items[item].path);
               for (int k = 0; k < 2; ++k) {
                 const int cv = 2 * (int)c + k;
-                const std::string path = base + (k == 0 ? "_original.jpg" : "_processed.jpg");
+                const std::string name = base + (k == 0 ? "_original.jpg" : "_processed.jpg");
                 const uint8_t* seg = use_fb[cv] ? fb[cv].data() : s.h_out + (size_t)cv * kOutCap;
                 const size_t len = use_fb[cv] ? fb[cv].size() : (size_t)s.h_sizes[cv];
-                jpeg::write_jpeg_file(path, jpeg_header, seg, len);
+                jpeg::write_jpeg_at(dfd, rel ? items[item].out_dir : std::string(), name, jpeg_header, seg, len);
                 bytes_out += (int64_t)(jpeg_header.size() + len + 2);
               }
             } catch (const std::exception& e) {
@@ -843,6 +921,7 @@ struct Engine::Impl {
   // while run k's last batches drain — instead of every run paying the ring's fill and drain.
   struct Job {
     std::shared_ptr<const std::vector<WorkItem>> items;
+    std::unique_ptr<IoDirs> dirs;
     std::function<void(size_t)> on_start;
     std::vector<SliceStatus> status;
     StageTimes acc;
@@ -910,7 +989,8 @@ struct Engine::Impl {
       const int64_t c0 = thread_cpu_ns();
       try {
         const auto [first, count] = j->batches[b];
-        process_batch(*s, *j->items, b, j->seq0 + b, first, count, j->status, j->acc, j->acc_m, j->on_start);
+        process_batch(*s, *j->items, *j->dirs, b, j->seq0 + b, first, count, j->status, j->acc, j->acc_m,
+                      j->on_start);
       } catch (...) {
         std::lock_guard<std::mutex> g(j->err_m);
         if (!j->err) j->err = std::current_exception();
@@ -927,6 +1007,7 @@ struct Engine::Impl {
     auto j = std::make_shared<Job>();
     j->t0 = now_s();
     j->items = std::move(items);
+    j->dirs = std::make_unique<IoDirs>(*j->items);
     j->on_start = std::move(on_start);
     j->status.resize(j->items->size());
     j->batches = plan_batches(j->items->size(), (size_t)cfg.batch_size, cfg.taper);

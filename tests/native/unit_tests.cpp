@@ -219,6 +219,31 @@ TEST(pack12_round_trip_and_declines) {
   std::vector<uint16_t> odd(24, 5);
   std::vector<uint8_t> out(64);
   CHECK(pack(odd.data(), odd.size(), out.data()) == 0);  // n % 16 != 0
+  CHECK(!fits12(odd.data(), odd.size()));
+}
+
+TEST(pack12_stream_exact_bytes) {
+  // pack_stream (the engine's path into pinned memory): same bytes as pack(), at unaligned
+  // destinations, across bounce-chunk boundaries, and not one byte past n * 3 / 2.
+  using namespace nm03::pack12;
+  if (!available()) return;
+  std::mt19937 rng(3);
+  for (size_t n : {16u, 2048u, 2064u, 65536u, 262144u}) {
+    std::vector<uint16_t> px(n);
+    for (auto& v : px) v = (uint16_t)(rng() & 0xFFF);
+    CHECK(fits12(px.data(), n));
+    std::vector<uint8_t> ref(n / 2 * 3 + 32);
+    CHECK(pack(px.data(), n, ref.data()) == n / 2 * 3);
+    for (size_t mis : {0u, 1u, 8u, 13u}) {
+      std::vector<uint8_t> dst(n / 2 * 3 + 64, 0xAB);
+      pack_stream(px.data(), n, dst.data() + mis);
+      CHECK(std::equal(ref.begin(), ref.begin() + n / 2 * 3, dst.begin() + mis));
+      for (size_t k = 0; k < mis; ++k) CHECK(dst[k] == 0xAB);
+      for (size_t k = mis + n / 2 * 3; k < dst.size(); ++k) CHECK(dst[k] == 0xAB);
+    }
+    px[n / 2] = 0x1000;
+    CHECK(!fits12(px.data(), n));
+  }
 }
 
 // ---- JPEG container ------------------------------------------------------------------------------
