@@ -113,6 +113,9 @@ class SliceFile {
 
 // memcpy with non-temporal (streaming) stores for the 16-byte-aligned body of dst.
 void stream_copy(void* dst, const void* src, size_t n);
+// The same without the closing store fence: for a sequence of copies fenced once by the caller
+// (a fence per small copy drains the write-combining buffers every time).
+void stream_copy_unfenced(void* dst, const void* src, size_t n);
 
 struct WriteSpec {
   int rows = 256, cols = 256;

@@ -429,6 +429,11 @@ const uint16_t* SliceFile::staged_samples() const {
 }
 
 void stream_copy(void* dst, const void* src, size_t n) {
+  stream_copy_unfenced(dst, src, n);
+  _mm_sfence();  // streaming stores are weakly ordered: complete them before the upload is queued
+}
+
+void stream_copy_unfenced(void* dst, const void* src, size_t n) {
   auto* d = static_cast<uint8_t*>(dst);
   const auto* s = static_cast<const uint8_t*>(src);
   size_t head = (16 - ((uintptr_t)d & 15)) & 15;
@@ -448,7 +453,6 @@ void stream_copy(void* dst, const void* src, size_t n) {
     _mm_stream_si128(reinterpret_cast<__m128i*>(d + 48), e);
   }
   std::memcpy(d, s, n);
-  _mm_sfence();  // streaming stores are weakly ordered: complete them before the upload is queued
 }
 
 std::vector<uint8_t> read_file(const std::string& path) {

@@ -56,8 +56,9 @@ __attribute__((target("avx2"))) void pack_stream_avx2(const uint16_t* src, size_
   for (size_t i = 0; i < n; i += kChunk) {
     const size_t m = n - i < kChunk ? n - i : kChunk;
     for (size_t k = 0; k < m; k += 16) pack16(src + i + k, bounce + k / 2 * 3);
-    dicom::stream_copy(dst + i / 2 * 3, bounce, m / 2 * 3);
+    dicom::stream_copy_unfenced(dst + i / 2 * 3, bounce, m / 2 * 3);
   }
+  _mm_sfence();  // one fence for the whole slice
 }
 
 }  // namespace

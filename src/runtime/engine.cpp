@@ -214,6 +214,8 @@ struct Engine::Impl {
   size_t read_prefix_ = 16384;
   // 12-bit transfer packing of slices whose samples fit (nm03/pack12.h); NM03_PACK12=0 disables.
   bool pack12_ = pack12::available();
+  // NM03_PACK_BOUNCE=0: pack into a full-size intermediate and stream-copy it (A/B of pack_stream).
+  bool pack_bounce_ = true;
 
   explicit Impl(const EngineConfig& c) : cfg(c), place(c.device) {
     if (const char* e = std::getenv("NM03_BATCH_TAPER"); e && *e) cfg.taper = *e != '0';
@@ -223,6 +225,7 @@ struct Engine::Impl {
                                                 : dicom::ReadMode::kDirect;
     if (const char* e = std::getenv("NM03_LOAD_PREFIX"); e && *e) read_prefix_ = (size_t)std::atol(e);
     if (const char* e = std::getenv("NM03_PACK12"); e && *e && *e == '0') pack12_ = false;
+    if (const char* e = std::getenv("NM03_PACK_BOUNCE"); e && *e && *e == '0') pack_bounce_ = false;
     if (const char* e = std::getenv("NM03_UPLOAD_CHUNK_KB"); e && *e) upload_chunk_ = (size_t)std::atol(e) << 10;
     if (cfg.batch_size < 1) cfg.batch_size = 1;
     if (cfg.streams < 1) cfg.streams = 1;
@@ -487,9 +490,14 @@ struct Engine::Impl {
         }
         uint16_t* dst = reinterpret_cast<uint16_t*>(s.h_blob + s.raw_base) + off;
         try {
-          if (packed)
+          if (packed && pack_bounce_) {
             pack12::pack_stream(samples, npix, reinterpret_cast<uint8_t*>(dst));
-          else
+          } else if (packed) {  // A/B: full-size intermediate, then one streaming copy
+            thread_local std::vector<uint8_t> pk;
+            if (pk.size() < npix / 2 * 3 + 64) pk.resize(npix / 2 * 3 + 64);
+            const size_t pb = pack12::pack(samples, npix, pk.data());
+            dicom::stream_copy(dst, pk.data(), pb);
+          } else
             file.pixels16(dst);
         } catch (...) {
           s.allocs[idx].done.store(true, std::memory_order_release);  // space stays unused

@@ -72,6 +72,13 @@ int main(int argc, char** argv) {
     size_t b = nm03::pack12::pack(f.staged_samples(), (size_t)h.rows * h.cols, pk.data());
     nm03::dicom::stream_copy(dst.data(), pk.data(), b);
   });
+  run("staged header + fits12 + pack_stream", [&](size_t i) {
+    nm03::dicom::SliceFile f(files[i], nm03::dicom::ReadMode::kStaged);
+    const auto& h = f.header(stage);
+    const size_t npix = (size_t)h.rows * h.cols;
+    if (nm03::pack12::fits12(f.staged_samples(), npix))
+      nm03::pack12::pack_stream(f.staged_samples(), npix, reinterpret_cast<uint8_t*>(dst.data()));
+  });
   run("SliceFile direct header + pixels16", [&](size_t i) {
     nm03::dicom::SliceFile f(files[i], nm03::dicom::ReadMode::kDirect);
     f.header(stage);
