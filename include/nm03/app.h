@@ -31,6 +31,7 @@ struct AppConfig {
   std::string input;       // test_pipeline: explicit slice path
   std::string dump_mhd;    // test_pipeline: directory for MetaImage stage dumps (empty = off)
   int repeat = 1;
+  bool dilation_set = false;  // --dilation-size given (3D mode defaults to 7, BASELINE config 5)
 };
 
 // Parse the shared flag set; `which` selects CLI-specific defaults. Exits on --help.

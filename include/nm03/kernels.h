@@ -57,6 +57,8 @@ void launch_srg_morph(const uint64_t* band, const SliceDesc* descs, int nslices,
 // neighbouring slabs contributed boundary voxels.
 int srg_volume(const uint64_t* band, uint64_t* region, int w, int h, int d, const int32_t* seeds_xyz, int nseeds,
                int connectivity, uint32_t* d_flag, uint32_t* h_flag, hipStream_t stream, bool reset = true);
+// Per-plane renderer border of a bit volume: label ∧ ¬erode_{(2r+1)²}(label) (2D, every plane).
+void border_volume(const uint64_t* src, uint64_t* dst, int w, int h, int d, int radius, hipStream_t stream);
 // Cube dilation of a bit volume (size odd), separable; `tmp` same size as the volume.
 void dilate_volume(const uint64_t* src, uint64_t* dst, uint64_t* tmp, int w, int h, int d, int size,
                    hipStream_t stream);

@@ -32,6 +32,11 @@ struct VolumeResult {
   double kernels_s = 0;
 };
 
+struct VolumeExportStats {
+  double export_s = 0;         // wall time of render + encode (GPU) incl. D2H of the JPEG bytes
+  int64_t jpeg_fallbacks = 0;  // images re-encoded on the host (GPU capacity overflow)
+};
+
 struct VolumeParams {
   PipelineParams pipe;        // median/sharpen/band per slice, then 3D SRG
   int connectivity = 6;       // 6 | 26
@@ -50,6 +55,11 @@ class VolumeRunner {
   VolumeRunner(const VolumeRunner&) = delete;
   VolumeRunner& operator=(const VolumeRunner&) = delete;
   VolumeResult run(const VolumeInput& v, const VolumeParams& p, bool want_masks);
+  // After run() on the same volume: the 2·d exported JPEG files of the 3D cohort mode, in plane
+  // order (original, processed), rendered and encoded on the GPU (K3/K4) from the volume still on
+  // the device — byte-identical to the golden host renderer + encoder.
+  std::vector<std::vector<uint8_t>> export_jpegs(const VolumeInput& v, const VolumeParams& p, const RenderParams& rp,
+                                                 struct VolumeExportStats* stats = nullptr);
 
  private:
   struct Impl;

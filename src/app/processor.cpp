@@ -42,11 +42,11 @@ void usage(const std::string& which) {
             << "  --threads N            host I/O threads per rank (default 16)\n"
             << "  --median-window K      3|5|7|9 (default 7)\n"
             << "  --srg-connectivity C   4|8 (2D) / 6|26 (3D)\n"
-            << "  --dilation-size S      (default 3)    --erosion-size S (default 3)\n"
+            << "  --dilation-size S      (default 3; 7 in --mode 3d)    --erosion-size S (default 3)\n"
             << "  --quality Q            JPEG quality (default 75)\n"
             << "  --mode 2d|3d           3d: whole series as a volume (SRG 6-conn + cube dilation)\n"
             << "  --input FILE           test_pipeline: slice to process\n"
-            << "  --cpu                  test_pipeline: golden CPU model instead of the GPU\n"
+            << "  --cpu                  test_pipeline / --mode 3d: golden CPU model instead of the GPU\n"
             << "  --no-montage           test_pipeline: skip the 5-view montage JPEG\n"
             << "  --dump-mhd DIR         test_pipeline: write stage arrays as MetaImage (.mhd/.raw)\n"
             << "  --repeat N             process the cohort N times (benchmarking)\n"
@@ -132,7 +132,10 @@ AppConfig parse_args(int argc, char** argv, const std::string& which) {
     else if (a == "--threads") c.engine.threads = std::atoi(val().c_str());
     else if (a == "--median-window") c.engine.pipe.median_window = std::atoi(val().c_str());
     else if (a == "--srg-connectivity") c.engine.pipe.srg_connectivity = std::atoi(val().c_str());
-    else if (a == "--dilation-size") c.engine.pipe.dilation_size = std::atoi(val().c_str());
+    else if (a == "--dilation-size") {
+      c.engine.pipe.dilation_size = std::atoi(val().c_str());
+      c.dilation_set = true;
+    }
     else if (a == "--erosion-size") c.engine.pipe.erosion_size = std::atoi(val().c_str());
     else if (a == "--quality") c.engine.render.jpeg_quality = std::atoi(val().c_str());
     else if (a == "--mode") c.mode = val();

@@ -150,9 +150,19 @@ int main(int argc, char** argv) {
         sweeps = r.sweeps;
       }
       const double dt = now_s() - t0;
+      // + the GPU export of every plane (render + JPEG, both images), as the 3D CLI does
+      nm03::VolumeExportStats xs;
+      for (int w = 0; w < warmup; ++w) runner.export_jpegs(v, vp, ec.render);
+      const double t1 = now_s();
+      for (int k = 0; k < steps; ++k) {
+        runner.run(v, vp, false);
+        runner.export_jpegs(v, vp, ec.render, &xs);
+      }
+      const double dt2 = now_s() - t1;
       std::cout << "{\"config\": \"volume\", \"dims\": [" << v.w << ", " << v.h << ", " << v.d << "], \"steps\": " << steps
                 << ", \"ms_per_volume\": " << dt * 1e3 / steps << ", \"gpu_ms_per_volume\": " << ks * 1e3 / steps
-                << ", \"sweeps\": " << sweeps << "}" << std::endl;
+                << ", \"sweeps\": " << sweeps << ", \"ms_per_volume_with_export\": " << dt2 * 1e3 / steps
+                << ", \"export_ms_per_volume\": " << xs.export_s * 1e3 / steps << "}" << std::endl;
     } else if (config == "volume-cpu") {
       if (pids.empty()) throw std::runtime_error("no patients");
       auto s = nm03::cohort::list_patient_series(base, pids[0]);

@@ -98,6 +98,22 @@ __global__ __launch_bounds__(256) void dilate_plane_kernel(const uint64_t* __res
   for (int i = threadIdx.x; i < words; i += blockDim.x) dst[off + i] = B[i];
 }
 
+// Renderer border of every plane: label ∧ ¬erode_{size×size}(label) in 2D per plane (the
+// SegmentationRenderer outlines each displayed slice; size = 2·radius + 1).
+__global__ __launch_bounds__(256) void border_plane_kernel(const uint64_t* __restrict__ src, uint64_t* __restrict__ dst,
+                                                           int w, int h, int size, int plane_words) {
+  extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
+  const int n = (w + 63) >> 6, words = h * n;
+  const size_t off = (size_t)blockIdx.x * words;
+  uint64_t* A = smem;
+  uint64_t* B = A + plane_words;
+  uint64_t* T = B + plane_words;
+  for (int i = threadIdx.x; i < words; i += blockDim.x) A[i] = src[off + i];
+  __syncthreads();
+  morph(A, B, T, w, h, n, size, false);
+  for (int i = threadIdx.x; i < words; i += blockDim.x) dst[off + i] = A[i] & ~B[i];
+}
+
 __global__ void dilate_z_kernel(const uint64_t* __restrict__ src, uint64_t* __restrict__ dst, int words, int d, int r) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= (size_t)words * d) return;
@@ -143,6 +159,14 @@ int srg_volume(const uint64_t* band, uint64_t* region, int w, int h, int d, cons
     if (h_flag[0] == 0 || h_flag[1] == 0 || sweeps > 4 * (w + h + d)) break;
   }
   return sweeps;
+}
+
+void border_volume(const uint64_t* src, uint64_t* dst, int w, int h, int d, int radius, hipStream_t stream) {
+  const int n = (w + 63) / 64;
+  const int plane_words = (h * n + 1) & ~1;
+  border_plane_kernel<<<d, 256, (size_t)plane_words * 3 * sizeof(uint64_t), stream>>>(src, dst, w, h, 2 * radius + 1,
+                                                                                    plane_words);
+  check_launch("border_plane_kernel");
 }
 
 void dilate_volume(const uint64_t* src, uint64_t* dst, uint64_t* tmp, int w, int h, int d, int size, hipStream_t stream) {

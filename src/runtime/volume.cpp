@@ -8,9 +8,14 @@
 #include <chrono>
 #include <cstring>
 #include <memory>
+#include <fstream>
 #include <iostream>
+#include <sstream>
 
 #include "nm03/cohort.h"
+#include "nm03/comm.h"
+#include "nm03/golden.h"
+#include "nm03/thread_pool.h"
 #include "nm03/dicom.h"
 #include "nm03/gpu_types.h"
 #include "nm03/jpeg.h"
@@ -191,11 +196,70 @@ static void unpack_volume(const DevBuf& b, const VolumeDevice& V, std::vector<ui
         out[((size_t)z * V.h + y) * V.w + x] = (words[(size_t)z * V.words + (size_t)y * V.wpr + x / 64] >> (x % 64)) & 1;
 }
 
+// GPU export of a processed volume (K3/K4, like the 2D engine): per plane the original (gray render
+// of the raw plane, windowed by the median kernel's per-plane stats) and the processed image (the
+// 3D dilated mask with its per-plane renderer border), rendered — fused into the encoder for an
+// exact 2× fit — and JPEG-encoded in chunks of kExportSlices planes. Images the GPU encoder cannot
+// hold (capacity overflow, rare) are re-encoded on the host from their rendered canvas.
+constexpr int kExportSlices = 32;
+constexpr uint32_t kVolStageBytes = 256 * 1024;
+constexpr uint32_t kVolOutCap = 2 * kVolStageBytes + 64;
+
+struct ExportBufs {
+  int cap = 2 * kExportSlices;  // canvases per launch
+  int cw = 0, ch = 0;
+  DevBuf bits, canvas, tables, stage, look, ticket, spill, total, chunk_ff;
+  JpegWork jw;
+  uint8_t* h_tables = nullptr;
+  uint8_t* h_out = nullptr;
+  uint8_t* d_out = nullptr;
+  int32_t* h_sizes = nullptr;
+  int32_t* d_sizes = nullptr;
+  size_t bits_words = 0;
+  ExportBufs(int cw_, int ch_, size_t vol_words)
+      : cw(cw_), ch(ch_),
+        bits(2 * vol_words * 8),
+        canvas((size_t)cw_ * ch_ * 2 * kExportSlices),
+        tables(2 * kExportSlices * (sizeof(RenderDesc) + sizeof(JpegDesc)) + 256),
+        stage((size_t)kVolStageBytes * 2 * kExportSlices),
+        look(8 * (size_t)2 * kExportSlices * (((size_t)cw_ * ch_ / 64 + 255) / 256)),
+        ticket(4 * 2 * kExportSlices),
+        spill(4 * (size_t)2 * kExportSlices * (((size_t)cw_ * ch_ / 64 + 255) / 256) * 256 * 56),
+        total(4 * 2 * kExportSlices),
+        chunk_ff(4 * (size_t)2 * kExportSlices * (kVolStageBytes / kStuffChunk)),
+        bits_words(vol_words) {
+    const size_t blocks = (size_t)cw * ch / 64;
+    jw.stage = stage.as<uint32_t>();
+    jw.look = look.as<uint64_t>();
+    jw.look_cap = (size_t)cap * ((blocks + 255) / 256);
+    jw.ticket = ticket.as<uint32_t>();
+    jw.spill = spill.as<uint32_t>();
+    jw.total = total.as<uint32_t>();
+    jw.chunk_ff = chunk_ff.as<uint32_t>();
+    jw.max_chunks = (int)(kVolStageBytes / kStuffChunk);
+    check_hip(hipMemset(jw.stage, 0, (size_t)kVolStageBytes * cap), "memset stage");
+    check_hip(hipMemset(jw.look, 0, jw.look_cap * 8), "memset look-back");
+    check_hip(hipMemset(jw.ticket, 0, 4 * (size_t)cap), "memset tickets");
+    check_hip(hipHostMalloc((void**)&h_tables, cap * (sizeof(RenderDesc) + sizeof(JpegDesc)) + 256, hipHostMallocDefault),
+              "hipHostMalloc export tables");
+    check_hip(hipHostMalloc((void**)&h_out, (size_t)kVolOutCap * cap, hipHostMallocMapped), "hipHostMalloc out");
+    check_hip(hipHostGetDevicePointer((void**)&d_out, h_out, 0), "device pointer out");
+    check_hip(hipHostMalloc((void**)&h_sizes, 4 * (size_t)cap, hipHostMallocMapped), "hipHostMalloc sizes");
+    check_hip(hipHostGetDevicePointer((void**)&d_sizes, h_sizes, 0), "device pointer sizes");
+  }
+  ~ExportBufs() {
+    if (h_tables) (void)hipHostFree(h_tables);
+    if (h_out) (void)hipHostFree(h_out);
+    if (h_sizes) (void)hipHostFree(h_sizes);
+  }
+};
+
 // Device buffers, stream and events are cached across runs (allocation and stream creation cost
 // more than the kernels for a 256³ volume); they are rebuilt only when the volume shape changes.
 struct VolumeRunner::Impl {
   int device;
   std::unique_ptr<VolumeDevice> V;
+  std::unique_ptr<ExportBufs> X;
   hipEvent_t e0 = nullptr, e1 = nullptr;
   explicit Impl(int dev) : device(dev) {
     check_hip(hipSetDevice(device), "hipSetDevice");
@@ -204,6 +268,7 @@ struct VolumeRunner::Impl {
   }
   ~Impl() {
     (void)hipSetDevice(device);
+    X.reset();
     V.reset();
     if (e0) (void)hipEventDestroy(e0);
     if (e1) (void)hipEventDestroy(e1);
@@ -218,6 +283,7 @@ VolumeResult VolumeRunner::run(const VolumeInput& v, const VolumeParams& p, bool
   Impl& I = *impl_;
   check_hip(hipSetDevice(I.device), "hipSetDevice");
   if (!I.V || I.V->w != v.w || I.V->h != v.h || I.V->d != v.d) {
+    I.X.reset();
     I.V.reset();
     I.V = std::make_unique<VolumeDevice>(v);
   }
@@ -243,6 +309,115 @@ VolumeResult VolumeRunner::run(const VolumeInput& v, const VolumeParams& p, bool
   return r;
 }
 
+std::vector<std::vector<uint8_t>> VolumeRunner::export_jpegs(const VolumeInput& v, const VolumeParams& p,
+                                                             const RenderParams& rp, VolumeExportStats* st) {
+  Impl& I = *impl_;
+  if (!I.V || I.V->w != v.w || I.V->h != v.h || I.V->d != v.d) throw DeviceError("export_jpegs: run() this volume first");
+  check_hip(hipSetDevice(I.device), "hipSetDevice");
+  VolumeDevice& V = *I.V;
+  const int cw = rp.out_width, ch = rp.out_height;
+  if (cw % 16 || ch % 16) throw DeviceError("canvas size must be a multiple of 16");
+  if (!I.X || I.X->cw != cw || I.X->ch != ch) {
+    I.X.reset();
+    I.X = std::make_unique<ExportBufs>(cw, ch, V.words * V.d);
+  }
+  ExportBufs& X = *I.X;
+  const double t0 = std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+  // Label planes = the dilated mask, border planes right behind them in one bit buffer.
+  uint64_t* bits = X.bits.as<uint64_t>();
+  const size_t vol_words = V.words * V.d;
+  check_hip(hipMemcpyAsync(bits, V.dil.p, vol_words * 8, hipMemcpyDeviceToDevice, V.stream), "D2D labels");
+  border_volume(bits, bits + vol_words, v.w, v.h, v.d, rp.border_radius, V.stream);
+  const jpeg::Tables tables = jpeg::make_tables(rp.jpeg_quality);
+  const std::vector<uint8_t> header = jpeg::make_header(cw, ch, tables);
+  const RenderGeom g = make_render_geom(v.w, v.h, v.spacing_x, v.spacing_y, cw, ch);
+  const uint8_t fill = opacity_u8(rp.label_opacity), bval = opacity_u8(rp.border_opacity);
+  const size_t canvas_bytes = (size_t)cw * ch;
+  std::vector<std::vector<uint8_t>> files((size_t)2 * v.d);
+  for (int z0 = 0; z0 < v.d; z0 += kExportSlices) {
+    const int nz = std::min(kExportSlices, v.d - z0), nc = 2 * nz;
+    auto* rd = reinterpret_cast<RenderDesc*>(X.h_tables);
+    auto* jd = reinterpret_cast<JpegDesc*>(X.h_tables + (size_t)X.cap * sizeof(RenderDesc));
+    bool any_canvas = false;
+    for (int k = 0; k < nc; ++k) {
+      const int z = z0 + k / 2;
+      RenderDesc& r = rd[k];
+      std::memset(&r, 0, sizeof(r));
+      r.kind = (k & 1) ? kRenderLabels : kRenderRawGray;
+      r.type = (uint8_t)v.type;
+      r.stored_bits = (uint8_t)v.stored_bits;
+      r.fill = fill;
+      r.border_value = bval;
+      r.slice = (uint32_t)z;  // the median kernel's per-plane stats
+      r.src_w = (uint16_t)v.w;
+      r.src_h = (uint16_t)v.h;
+      r.wpr = (uint16_t)V.wpr;
+      r.ox = g.ox;
+      r.oy = g.oy;
+      r.invx = g.invx;
+      r.invy = g.invy;
+      r.slope = p.pipe.apply_rescale ? v.slope : 1.f;
+      r.intercept = p.pipe.apply_rescale ? v.intercept : 0.f;
+      r.src_off = (k & 1) ? (uint32_t)(z * V.words) : (uint32_t)(z * V.ps);
+      r.border_off = (uint32_t)(vol_words + z * V.words);
+      r.canvas_off = (uint32_t)(k * canvas_bytes);
+      JpegDesc& j = jd[k];
+      std::memset(&j, 0, sizeof(j));
+      j.canvas_off = (uint32_t)(k * canvas_bytes);
+      j.stage_off = (uint32_t)k * (kVolStageBytes / 4);
+      j.stage_words = kVolStageBytes / 4;
+      j.out_off = (uint64_t)k * kVolOutCap;
+      j.out_cap = kVolOutCap;
+      j.render = render_is_exact_2x(r, cw, ch) ? k : -1;
+      any_canvas |= j.render < 0;
+    }
+    auto* d_rd = X.tables.as<uint8_t>();
+    auto* d_jd = d_rd + (size_t)X.cap * sizeof(RenderDesc);
+    check_hip(hipMemcpyAsync(d_rd, X.h_tables, (size_t)X.cap * (sizeof(RenderDesc) + sizeof(JpegDesc)),
+                             hipMemcpyHostToDevice, V.stream),
+              "H2D export tables");
+    const auto* drd = reinterpret_cast<const RenderDesc*>(d_rd);
+    if (any_canvas)
+      launch_render(V.raw.as<uint16_t>(), nullptr, bits, V.stats.as<SliceStats>(), drd, nc, cw, ch,
+                    X.canvas.as<uint8_t>(), V.stream);
+    JpegRenderSrc rs;
+    rs.raw = V.raw.as<uint16_t>();
+    rs.bits = bits;
+    rs.stats = V.stats.as<SliceStats>();
+    rs.rd = drd;
+    launch_jpeg(X.canvas.as<uint8_t>(), reinterpret_cast<const JpegDesc*>(d_jd), nc, cw, ch, tables.div_luma, X.jw,
+                X.d_out, X.d_sizes, V.stream, &rs);
+    check_hip(hipStreamSynchronize(V.stream), "export sync");
+    bool rendered = any_canvas;
+    for (int k = 0; k < nc; ++k) {
+      std::vector<uint8_t>& f = files[(size_t)2 * z0 + k];
+      f = header;
+      if (X.h_sizes[k] >= 0) {
+        f.insert(f.end(), X.h_out + (size_t)k * kVolOutCap, X.h_out + (size_t)k * kVolOutCap + X.h_sizes[k]);
+      } else {  // capacity overflow: host encoder on the rendered canvas
+        if (!rendered) {
+          launch_render(V.raw.as<uint16_t>(), nullptr, bits, V.stats.as<SliceStats>(), drd, nc, cw, ch,
+                        X.canvas.as<uint8_t>(), V.stream);
+          check_hip(hipStreamSynchronize(V.stream), "fallback render");
+          rendered = true;
+        }
+        std::vector<uint8_t> canvas(canvas_bytes);
+        check_hip(hipMemcpy(canvas.data(), X.canvas.as<uint8_t>() + (size_t)k * canvas_bytes, canvas_bytes,
+                            hipMemcpyDeviceToHost),
+                  "canvas D2H");
+        const auto scan = jpeg::encode_scan_gray420(canvas.data(), cw, ch, cw, tables);
+        f.insert(f.end(), scan.begin(), scan.end());
+        if (st) ++st->jpeg_fallbacks;
+      }
+      f.push_back(0xFF);
+      f.push_back(0xD9);
+    }
+  }
+  if (st)
+    st->export_s += std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count() - t0;
+  return files;
+}
+
 VolumeResult run_volume(const VolumeInput& v, const VolumeParams& p, int device, bool want_masks) {
   VolumeRunner runner(device);
   return runner.run(v, p, want_masks);
@@ -250,73 +425,300 @@ VolumeResult run_volume(const VolumeInput& v, const VolumeParams& p, int device,
 
 namespace app {
 
-int run_volume_cohort(const AppConfig& cfg) {
-  // 3D variant of the cohort run: each patient's series becomes one volume; the exported images
-  // are the per-slice renders of the original and of the 3D dilated segmentation.
-  const std::string base = cohort::cohort_dir(cfg.data_root);
-  std::cout << "\n=== Starting 3D Volume Processing for All Patients ===\n" << std::endl;
-  std::vector<std::string> pids = cohort::find_patient_dirs(base);
-  std::cout << "Found " << pids.size() << " patient directories." << std::endl;
-  if (pids.empty()) {
-    std::cout << "No patient directories found. Exiting." << std::endl;
-    return 0;
+namespace {
+
+double wall_now() { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); }
+
+struct VolPatient {
+  std::string id, out_dir, series_dir, error;
+  bool setup_ok = false, listed = false;
+  std::vector<std::string> files;
+};
+
+struct VolOutcome {
+  int32_t ok = 0;
+  std::string message;
+  int32_t sweeps = 0;
+  double gpu_s = 0, export_s = 0, wall_s = 0;
+  int64_t slices = 0, fallbacks = 0;
+};
+
+std::vector<uint8_t> encode(const std::vector<VolPatient>& pl) {
+  ByteWriter w;
+  w.u32((uint32_t)pl.size());
+  for (const auto& p : pl) {
+    w.str(p.id);
+    w.str(p.out_dir);
+    w.str(p.series_dir);
+    w.str(p.error);
+    w.u32(p.setup_ok);
+    w.u32(p.listed);
+    w.u32((uint32_t)p.files.size());
+    for (const auto& f : p.files) w.str(f);
   }
+  return w.b;
+}
+
+std::vector<VolPatient> decode(const std::vector<uint8_t>& b) {
+  ByteReader r(b.data(), b.size());
+  std::vector<VolPatient> pl(r.u32());
+  for (auto& p : pl) {
+    p.id = r.str();
+    p.out_dir = r.str();
+    p.series_dir = r.str();
+    p.error = r.str();
+    p.setup_ok = r.u32();
+    p.listed = r.u32();
+    p.files.resize(r.u32());
+    for (auto& f : p.files) f = r.str();
+  }
+  return pl;
+}
+
+void write_file(const std::string& path, const std::vector<uint8_t>& jpg) {
+  // complete JPEG file (header + scan + EOI): write_jpeg_file appends the EOI itself
+  jpeg::write_jpeg_file(path, {}, jpg.data(), jpg.size() - 2);
+}
+
+// Golden 3D path (--cpu): per-plane preprocessing on a thread pool, 3D SRG + cube dilation, host
+// render + encoder — the oracle the GPU 3D export is checked against.
+std::vector<std::vector<uint8_t>> golden_volume_jpegs(const VolumeInput& v, const VolumeParams& vp,
+                                                      const RenderParams& rp) {
+  const size_t plane = (size_t)v.w * v.h;
+  std::vector<uint8_t> band(plane * v.d);
+  std::vector<std::vector<float>> vals((size_t)v.d);
+  auto slice = [&](int z) {
+    golden::SliceInput si;
+    si.w = v.w;
+    si.h = v.h;
+    si.type = v.type;
+    si.stored_bits = v.stored_bits;
+    si.slope = v.slope;
+    si.intercept = v.intercept;
+    si.spacing_x = v.spacing_x;
+    si.spacing_y = v.spacing_y;
+    si.raw.assign(v.raw.begin() + z * plane, v.raw.begin() + (z + 1) * plane);
+    return si;
+  };
+  {
+    ThreadPool pool(16);
+    TaskGroup tg(pool);
+    for (int z = 0; z < v.d; ++z)
+      tg.run([&, z] {
+        golden::SliceInput si = slice(z);
+        golden::SliceResult r = golden::run(si, vp.pipe, false);
+        std::copy(r.band.begin(), r.band.end(), band.begin() + z * plane);
+        vals[z] = golden::rescaled(si, vp.pipe);
+      });
+    tg.wait();
+  }
+  std::vector<Seed> seeds = vp.seeds;
+  if (seeds.empty()) {
+    seeds = reference_seeds(v.w, v.h);
+    for (auto& sd : seeds) sd.z = v.d / 2;
+  }
+  const auto region = golden::region_grow3d(band, v.w, v.h, v.d, seeds, vp.connectivity);
+  const auto dil = golden::dilate3d(region, v.w, v.h, v.d, vp.dilation_size);
+  const jpeg::Tables t = jpeg::make_tables(rp.jpeg_quality);
+  const RenderGeom g = make_render_geom(v.w, v.h, v.spacing_x, v.spacing_y, rp.out_width, rp.out_height);
+  std::vector<std::vector<uint8_t>> files((size_t)2 * v.d);
+  for (int z = 0; z < v.d; ++z) {
+    const auto mm = std::minmax_element(vals[z].begin(), vals[z].end());
+    std::vector<uint8_t> lab(dil.begin() + z * plane, dil.begin() + (z + 1) * plane);
+    const auto c0 = golden::render_gray(vals[z], g, *mm.first, *mm.second);
+    const auto c1 = golden::render_labels(lab, golden::border(lab, v.w, v.h, rp.border_radius), g,
+                                          opacity_u8(rp.label_opacity), opacity_u8(rp.border_opacity));
+    files[2 * z] = jpeg::encode_gray420(c0.data(), rp.out_width, rp.out_height, rp.out_width, rp.jpeg_quality);
+    files[2 * z + 1] = jpeg::encode_gray420(c1.data(), rp.out_width, rp.out_height, rp.out_width, rp.jpeg_quality);
+  }
+  return files;
+}
+
+int volume_rank(const AppConfig& cfg, int rank, int size, Comm& comm, int device) {
+  const std::string base = cohort::cohort_dir(cfg.data_root);
+  VolumeParams vp;
+  vp.pipe = cfg.engine.pipe;
+  vp.connectivity = cfg.engine.pipe.srg_connectivity == 26 ? 26 : 6;
+  // BASELINE config 5: 7×7×7 cube dilation unless --dilation-size was given.
+  vp.dilation_size = cfg.dilation_set ? cfg.engine.pipe.dilation_size : 7;
   const RenderParams& rp = cfg.engine.render;
-  jpeg::Tables t = jpeg::make_tables(rp.jpeg_quality);
-  int successful = 0;
-  VolumeRunner runner(cfg.engine.device);
-  for (const auto& pid : pids) {
+  const double t_start = wall_now();
+  // ---- plan on rank 0 -----------------------------------------------------------------------
+  std::vector<uint8_t> plan_bytes;
+  int64_t fatal = 0;
+  std::string fatal_msg;
+  if (rank == 0) {
+    std::cout << "\n=== Starting 3D Volume Processing for All Patients ===\n" << std::endl;
     try {
-      std::cout << "\n=== Processing Patient: " << pid << " as a 3D volume ===\n" << std::endl;
-      const std::string out = cfg.out_dir + "/" + pid;
-      cohort::setup_output_dir(out);
-      std::cout << "Created output directory: " + out << std::endl;
-      cohort::Series s = cohort::list_patient_series(base, pid);
-      std::cout << "Using series directory: " << s.series_dir << std::endl;
-      std::cout << "Found " << s.files.size() << " DICOM files for patient " << pid << std::endl;
-      VolumeInput v = load_volume(s.files);
-      VolumeParams vp;
-      vp.pipe = cfg.engine.pipe;
-      vp.connectivity = cfg.engine.pipe.srg_connectivity == 26 ? 26 : 6;
-      vp.dilation_size = cfg.engine.pipe.dilation_size;
-      VolumeResult r = runner.run(v, vp, true);
-      // Export per slice (golden renderer + encoder on the host; the 3D path is not the headline).
-      PipelineParams pp = cfg.engine.pipe;
-      for (int z = 0; z < v.d; ++z) {
-        golden::SliceInput si;
-        si.w = v.w;
-        si.h = v.h;
-        si.type = v.type;
-        si.stored_bits = v.stored_bits;
-        si.slope = v.slope;
-        si.intercept = v.intercept;
-        si.spacing_x = v.spacing_x;
-        si.spacing_y = v.spacing_y;
-        si.raw.assign(v.raw.begin() + (size_t)z * v.w * v.h, v.raw.begin() + (size_t)(z + 1) * v.w * v.h);
-        std::vector<float> val = golden::rescaled(si, pp);
-        auto mm = std::minmax_element(val.begin(), val.end());
-        const RenderGeom g = make_render_geom(v.w, v.h, v.spacing_x, v.spacing_y, rp.out_width, rp.out_height);
-        std::vector<uint8_t> lab(r.dilated.begin() + (size_t)z * v.w * v.h, r.dilated.begin() + (size_t)(z + 1) * v.w * v.h);
-        auto c0 = golden::render_gray(val, g, *mm.first, *mm.second);
-        auto c1 = golden::render_labels(lab, golden::border(lab, v.w, v.h, rp.border_radius), g,
-                                        opacity_u8(rp.label_opacity), opacity_u8(rp.border_opacity));
-        const std::string stem = out + "/" + cohort::stem(s.files[z]);
-        auto j0 = jpeg::encode_scan_gray420(c0.data(), rp.out_width, rp.out_height, rp.out_width, t);
-        auto j1 = jpeg::encode_scan_gray420(c1.data(), rp.out_width, rp.out_height, rp.out_width, t);
-        auto hdr = jpeg::make_header(rp.out_width, rp.out_height, t);
-        jpeg::write_jpeg_file(stem + "_original.jpg", hdr, j0.data(), j0.size());
-        jpeg::write_jpeg_file(stem + "_processed.jpg", hdr, j1.data(), j1.size());
+      std::vector<VolPatient> plan;
+      std::vector<std::string> pids = cohort::find_patient_dirs(base);
+      std::cout << "Found " << pids.size() << " patient directories." << std::endl;
+      for (const auto& pid : pids) {
+        VolPatient p;
+        p.id = pid;
+        p.out_dir = cfg.out_dir + "/" + pid;
+        try {
+          cohort::setup_output_dir(p.out_dir);
+          p.setup_ok = true;
+          cohort::Series s = cohort::list_patient_series(base, pid);
+          p.series_dir = s.series_dir;
+          p.files = std::move(s.files);
+          p.listed = true;
+        } catch (const std::exception& e) {
+          p.error = e.what();
+        }
+        plan.push_back(std::move(p));
       }
-      std::cout << "\nPatient " << pid << " completed. 3D region growing converged in " << r.sweeps
-                << " sweeps; GPU time " << r.kernels_s * 1e3 << " ms." << std::endl;
-      ++successful;
+      plan_bytes = encode(plan);
     } catch (const std::exception& e) {
-      std::cerr << "Error processing patient " << pid << ": " << e.what() << std::endl;
+      fatal = 1;
+      fatal_msg = e.what();
     }
   }
+  comm.allreduce_sum_i64(&fatal, 1);
+  if (fatal) {
+    if (rank == 0) std::cerr << "Error finding patient directories: " << fatal_msg << std::endl;
+    return 1;
+  }
+  comm.broadcast_bytes(plan_bytes, 0);
+  const std::vector<VolPatient> plan = decode(plan_bytes);
+  // ---- this rank's patients (contiguous blocks; one volume per patient) ----------------------
+  const size_t lo = plan.size() * rank / size, hi = plan.size() * (rank + 1) / size;
+  std::unique_ptr<VolumeRunner> runner;
+  std::string setup_error;
+  if (!cfg.cpu) {
+    try {
+      runner = std::make_unique<VolumeRunner>(device);
+    } catch (const std::exception& e) {
+      setup_error = e.what();
+    }
+  }
+  std::vector<VolOutcome> mine;
+  double my_wall = 0;
+  for (size_t i = lo; i < hi; ++i) {
+    const VolPatient& pp = plan[i];
+    VolOutcome o;
+    const double t0 = wall_now();
+    try {
+      if (!setup_error.empty()) throw std::runtime_error(setup_error);
+      if (!pp.listed) throw std::runtime_error(pp.error);
+      VolumeInput v = load_volume(pp.files);
+      o.slices = v.d;
+      std::vector<std::vector<uint8_t>> files;
+      if (cfg.cpu) {
+        files = golden_volume_jpegs(v, vp, rp);
+      } else {
+        VolumeResult r = runner->run(v, vp, false);
+        o.sweeps = r.sweeps;
+        o.gpu_s = r.kernels_s;
+        VolumeExportStats xs;
+        files = runner->export_jpegs(v, vp, rp, &xs);
+        o.export_s = xs.export_s;
+        o.fallbacks = xs.jpeg_fallbacks;
+      }
+      for (int z = 0; z < v.d; ++z) {
+        const std::string stem = pp.out_dir + "/" + cohort::stem(pp.files[z]);
+        write_file(stem + "_original.jpg", files[2 * z]);
+        write_file(stem + "_processed.jpg", files[2 * z + 1]);
+      }
+      o.ok = 1;
+    } catch (const std::exception& e) {
+      o.message = e.what();
+    }
+    o.wall_s = wall_now() - t0;
+    my_wall += o.wall_s;
+    mine.push_back(std::move(o));
+  }
+  // ---- gather outcomes, rank 0 prints in patient order ---------------------------------------
+  ByteWriter w;
+  w.u32((uint32_t)mine.size());
+  for (const auto& o : mine) {
+    w.i32(o.ok);
+    w.str(o.message);
+    w.i32(o.sweeps);
+    w.f64(o.gpu_s);
+    w.f64(o.export_s);
+    w.f64(o.wall_s);
+    w.u64((uint64_t)o.slices);
+    w.u64((uint64_t)o.fallbacks);
+  }
+  auto all = comm.allgather_bytes(w.b);
+  double tot = wall_now() - t_start;
+  comm.allreduce_max_f64(&tot, 1);
+  std::vector<double> walls((size_t)size);
+  comm.allgather(&my_wall, sizeof(double), walls.data());
+  if (rank != 0) return 0;
+  std::vector<VolOutcome> outs;
+  for (auto& b : all) {
+    ByteReader r(b.data(), b.size());
+    const uint32_t k = r.u32();
+    for (uint32_t i = 0; i < k; ++i) {
+      VolOutcome o;
+      o.ok = r.i32();
+      o.message = r.str();
+      o.sweeps = r.i32();
+      o.gpu_s = r.f64();
+      o.export_s = r.f64();
+      o.wall_s = r.f64();
+      o.slices = (int64_t)r.u64();
+      o.fallbacks = (int64_t)r.u64();
+      outs.push_back(std::move(o));
+    }
+  }
+  int successful = 0;
+  int64_t slices = 0, fallbacks = 0;
+  std::ostringstream pj;
+  for (size_t i = 0; i < plan.size(); ++i) {
+    const VolPatient& pp = plan[i];
+    const VolOutcome& o = outs[i];
+    std::cout << "\n=== Processing Patient: " << pp.id << " as a 3D volume ===\n" << std::endl;
+    if (pp.setup_ok) std::cout << "Created output directory: " + pp.out_dir << std::endl;
+    if (pp.listed) {
+      std::cout << "Using series directory: " << pp.series_dir << std::endl;
+      std::cout << "Found " << pp.files.size() << " DICOM files for patient " << pp.id << std::endl;
+    }
+    if (o.ok) {
+      ++successful;
+      slices += o.slices;
+      fallbacks += o.fallbacks;
+      if (cfg.cpu)
+        std::cout << "\nPatient " << pp.id << " completed on the CPU golden model." << std::endl;
+      else
+        std::cout << "\nPatient " << pp.id << " completed. 3D region growing converged in " << o.sweeps
+                  << " sweeps; GPU time " << o.gpu_s * 1e3 << " ms." << std::endl;
+    } else {
+      std::cerr << "Error processing patient " << pp.id << ": " << o.message << std::endl;
+    }
+    pj << (i ? ", " : "") << "{\"id\": \"" << pp.id << "\", \"ok\": " << (o.ok ? "true" : "false")
+       << ", \"slices\": " << o.slices << ", \"sweeps\": " << o.sweeps << ", \"gpu_s\": " << o.gpu_s
+       << ", \"export_s\": " << o.export_s << ", \"wall_s\": " << o.wall_s << "}";
+  }
   std::cout << "\n=== All Processing Completed ===\n" << std::endl;
-  std::cout << "Successfully processed " << successful << "/" << pids.size() << " patients." << std::endl;
+  std::cout << "Successfully processed " << successful << "/" << plan.size() << " patients." << std::endl;
+  if (!cfg.json.empty()) {
+    std::ofstream f(cfg.json, std::ios::trunc);
+    f << "{\"mode\": \"3d\", \"backend\": \"" << (cfg.cpu ? "cpu" : "gpu") << "\", \"gpus\": " << size
+      << ", \"comm\": \"" << comm.backend() << "\", \"dilation_size\": " << vp.dilation_size
+      << ", \"connectivity\": " << vp.connectivity << ", \"wall_s\": " << tot << ", \"slices\": " << slices
+      << ", \"jpeg_fallbacks\": " << fallbacks << ", \"per_rank_wall_s\": [";
+    for (int r = 0; r < size; ++r) f << (r ? ", " : "") << walls[r];
+    f << "], \"patients\": [" << pj.str() << "]}\n";
+  }
   return 0;
+}
+
+}  // namespace
+
+int run_volume_cohort(const AppConfig& cfg) {
+  // 3D variant of the cohort run (BASELINE config 5): each patient's series becomes one volume
+  // (3D SRG + cube dilation on the GPU), exported per plane like the 2D run; patients are sharded
+  // over the ranks (one process per MI355X) like the 2D work list.
+  LaunchOptions lo = LaunchOptions::from_env();
+  const int n = cfg.cpu ? 1 : resolve_gpus(cfg, lo);
+  return launch_ranks(n, [&](int rank, int size, Comm& comm) {
+    const int dev = size > 1 ? lo.device_of(rank) : lo.device_override >= 0 ? lo.device_override : cfg.engine.device;
+    return volume_rank(cfg, rank, size, comm, dev);
+  }, lo);
 }
 
 }  // namespace app

@@ -82,3 +82,26 @@ def test_test_pipeline_dump_mhd_cpu(native, cohort_root, tmp_path):
     for name, key in (("band", "band"), ("segmentation", "region"), ("dilation", "dilated")):
         m, _ = native.mhd_read(str(dump / f"{name}.mhd"))
         assert np.array_equal(m.astype(bool), np.asarray(g[key]).astype(bool)), name
+
+
+def test_volume_cli_cpu_golden(native, cohort_root, tmp_path):
+    """--mode 3d --cpu: the golden 3D oracle of the GPU 3D export (BASELINE config 5): one volume
+    per patient, 3D SRG + 7×7×7 dilation by default, two JPEGs per plane, JSON per patient."""
+    import json
+    out, js = tmp_path / "o", tmp_path / "v.json"
+    r = run_bin("img_processing_parallel", "--mode", "3d", "--cpu", "--data-root", cohort_root, "--out", str(out),
+                "--json", str(js))
+    assert r.returncode == 0, r.stderr
+    assert "=== Starting 3D Volume Processing for All Patients ===" in r.stdout
+    assert "Successfully processed 4/4 patients." in r.stdout
+    j = json.load(open(js))
+    assert j["dilation_size"] == 7 and j["connectivity"] == 6 and j["backend"] == "cpu"
+    base = native.cohort_dir(cohort_root)
+    n = sum(len(native.list_patient_series(base, p)[1]) for p in native.find_patient_dirs(base))
+    assert j["slices"] == n and len(list(out.rglob("*.jpg"))) == 2 * n
+    PIL = pytest.importorskip("PIL.Image")
+    for f in list(out.rglob("*_processed.jpg"))[:3]:
+        assert PIL.open(io.BytesIO(f.read_bytes())).size == (512, 512)
+    r = run_bin("img_processing_parallel", "--mode", "3d", "--cpu", "--dilation-size", "3", "--data-root", cohort_root,
+                "--out", str(tmp_path / "o3"), "--json", str(js))
+    assert r.returncode == 0 and json.load(open(js))["dilation_size"] == 3

@@ -509,6 +509,31 @@ def test_volume_vs_golden(native, conn):
     assert res["sweeps"] >= 1
 
 
+def test_volume_cli_gpu_equals_golden(native, cohort_root, tmp_path):
+    """img_processing_parallel --mode 3d: 3D SRG + 7³ dilation on the GPU and the per-plane render
+    + JPEG export on the GPU (K3/K4) are byte-identical to the golden CPU 3D path; the same with the
+    patients sharded over 2 ranks sharing the GPU."""
+    import json
+    g, c, m = tmp_path / "gpu", tmp_path / "cpu", tmp_path / "multi"
+    r = run_bin("img_processing_parallel", "--mode", "3d", "--data-root", cohort_root, "--out", str(g),
+                "--json", str(tmp_path / "g.json"))
+    assert r.returncode == 0, r.stderr
+    assert "3D region growing converged in" in r.stdout
+    r = run_bin("img_processing_parallel", "--mode", "3d", "--cpu", "--data-root", cohort_root, "--out", str(c))
+    assert r.returncode == 0, r.stderr
+    tg, tc = _tree(str(g)), _tree(str(c))
+    assert len(tg) > 0 and tg == tc
+    j = json.load(open(tmp_path / "g.json"))
+    assert j["backend"] == "gpu" and j["dilation_size"] == 7 and j["jpeg_fallbacks"] == 0
+    assert all(p["ok"] and p["sweeps"] >= 1 and p["export_s"] > 0 for p in j["patients"])
+    r = run_bin("img_processing_parallel", "--mode", "3d", "--gpus", "2", "--data-root", cohort_root, "--out", str(m),
+                "--json", str(tmp_path / "m.json"), env={"NM03_DEVICE_OVERRIDE": "0", "NM03_COMM_TIMEOUT_S": "60"})
+    assert r.returncode == 0, r.stderr
+    assert _tree(str(m)) == tg
+    j = json.load(open(tmp_path / "m.json"))
+    assert j["gpus"] == 2 and len(j["per_rank_wall_s"]) == 2
+
+
 def test_volume_runner_reuse_across_shapes(native):
     """One persistent VolumePipeline runner over volumes of changing shape and content: every
     result equals the golden of that volume (no stale buffers/tables from the previous run)."""
