@@ -67,23 +67,20 @@ void dilate_volume(const uint64_t* src, uint64_t* dst, uint64_t* tmp, int w, int
 void launch_render(const uint16_t* raw, const float* f32, const uint64_t* bits, const SliceStats* stats,
                    const RenderDesc* rd, int ncanvas, int out_w, int out_h, uint8_t* canvas, hipStream_t stream);
 
-// K4: JPEG. (1) single pass, workgroup per 256 luma blocks of an image: [fused 2× render or
-// canvas read] → islow FDCT → reciprocal quantisation → Huffman cost → workgroup scan →
-// decoupled look-back across the image → bit emission into the staging words; (2) per 4 KiB
-// chunk: 0xFF counting, then the stuffed copy straight into `out` (host-mapped pinned memory).
+// K4: JPEG in one pass, workgroup per 256 luma blocks of an image: [fused 2× render or canvas
+// read] → islow FDCT → reciprocal quantisation → Huffman coding → workgroup scan → bit range in
+// LDS → decoupled look-back across the image (bit offset and 0xFF-stuffing count) → the stuffed
+// bytes straight into `out` (host-mapped pinned memory, JpegDesc.out_off).
 // out_sizes[i] = bytes, or -1 when the image exceeded its staging/out capacity (caller
 // re-encodes on the CPU).
 struct JpegWork {
-  uint32_t* stage = nullptr;     // ncanvas × stage_words bit staging; all-zero between launches
-                                 // (zeroed once at allocation, then kept clear by the stuffing kernel)
-  uint64_t* look = nullptr;      // look_cap look-back status words (zeroed once; cleared after use)
-  size_t look_cap = 0;           // ≥ ncanvas × ceil(blocks / 256)
+  uint64_t* look = nullptr;      // 2 × 3 × look_cap record words, zeroed once at allocation: two
+                                 // halves, each launch uses one and clears the other (launch_jpeg)
+  size_t look_cap = 0;           // ≥ ncanvas × ceil(blocks / 256) workgroups
   size_t look_used = 0;          // set by launch_jpeg
+  size_t look_base = 0, clear_base = 0, clear_words = 0, prev_words = 0;  // launch_jpeg's bookkeeping
   uint32_t* ticket = nullptr;    // per-image part ticket counters (≥ ncanvas; zeroed once; self-resetting)
   uint32_t* spill = nullptr;     // look_cap × 256 × 56 words: Huffman bits of very detailed blocks
-  uint32_t* total = nullptr;     // ncanvas: total bits (0xFFFFFFFF = overflow)
-  uint32_t* chunk_ff = nullptr;  // ncanvas × max_chunks: 0xFF bytes per stuffing chunk
-  int max_chunks = 0;            // stage bytes / kStuffChunk
 };
 // Fused-render inputs (needed when any JpegDesc.render ≥ 0).
 struct JpegRenderSrc {

@@ -2,8 +2,9 @@
 // main_sequential.cpp:61-73). Output is byte-identical to libjpeg(-turbo) baseline q75 4:2:0
 // (nm03/jpeg_common.h; golden encoder src/io/jpeg.cpp; tests/test_jpeg.py vs Pillow).
 //
-// Two launches per batch (a batch of 64 slices = 128 canvases = 524k luma blocks):
-//  1 jpeg_fused_kernel   workgroup per 256 luma blocks (64 MCUs) of an image, thread per block.
+// One launch per batch (a batch of 64 slices = 128 canvases = 524k luma blocks), after a clear of
+// the look-back records:
+//    jpeg_fused_kernel   workgroup per 256 luma blocks (64 MCUs) of an image, thread per block.
 //                        Pixels come from the canvas or — for an exact 2× fit, the common case —
 //                        are rendered on the fly from the 6×6 source patch (render_core.h), so the
 //                        256 KiB canvas never exists. The workgroup first stages its source rows
@@ -11,12 +12,13 @@
 //                        and border bit rows) with coalesced loads: 76 → 67 µs per 64-slice batch.
 //                        islow FDCT (24-bit multiplies), quantisation by exact reciprocal (umulhi
 //                        by ceil(2^32/d): exact for |x|, d < 2^16),
-//                        Huffman cost, workgroup scan, decoupled look-back over the image's
-//                        earlier workgroups, then the codes are ORed into the zeroed stage words.
-//  2 jpeg_stuff_*        grid-stride over (chunk, image) 4 KiB chunks, chunk-major: count 0xFF
-//                        bytes; then prefix over previous chunks, in-chunk scan, stuffed bytes
-//                        staged in LDS and copied straight into host-mapped pinned memory; the
-//                        consumed stage words are cleared for the next launch.
+//                        Huffman cost, workgroup scan, the workgroup's bit range assembled in LDS,
+//                        its 0xFF-byte counts for all 8 byte alignments, a decoupled look-back
+//                        over the image's earlier workgroups that resolves both the bit offset and
+//                        the number of stuffing bytes before it, and the 0xFF-stuffed bytes it
+//                        owns written straight into host-mapped pinned memory. (Earlier versions
+//                        ORed the codes into an HBM stage and ran two more launches to count and
+//                        insert the stuffing: 2.65 MB written + read back per batch, two launches.)
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
@@ -55,30 +57,39 @@ __device__ __forceinline__ int wave_sum_i32(int v) {
 }
 
 
-// Look-back status word: hi = state (0 = not yet, 1 = aggregate, 2 = inclusive prefix), lo = bits.
-// The stuffing-count kernel (next in the stream) clears the words again for the next launch.
+// Look-back records: 3 words per workgroup, each tagged in its top 2 bits (0 = not yet, 1 =
+// aggregate, 2 = inclusive; word 0 is rewritten with the inclusive record). Cleared (memset)
+// before every launch.
 // Relaxed agent-scope atomics: the word itself carries the value, nothing else is published
 // through it (the stage bits are consumed by later kernels), and acquire/release would add an L2
 // writeback (buffer_wbl2) per store and an L2 invalidate (buffer_inv) per poll on gfx950.
 __device__ __forceinline__ uint64_t look_load(const uint64_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ __forceinline__ void look_store(uint64_t* p, uint32_t state, uint32_t v) {
-  __hip_atomic_store(p, ((uint64_t)state << 32) | v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+__device__ __forceinline__ void look_store64(uint64_t* p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ __forceinline__ uint32_t sat_add(uint32_t a, uint32_t b) {
-  const uint32_t s = a + b;
-  return s < a ? 0xFFFFFFFFu : s;
+// `n` ≤ 8 bits at bit offset `o` of an MSB-first word buffer (right-aligned). Reads word o/32 + 1:
+// the buffer is zeroed one word past its end.
+__device__ __forceinline__ uint32_t lds_bits(const uint32_t* buf, uint32_t o, uint32_t n) {
+  if (n == 0) return 0u;
+  const uint32_t w = o >> 5, sh = o & 31u;
+  uint32_t v = buf[w] << sh;
+  if (sh) v |= buf[w + 1] >> (32u - sh);
+  return v >> (32u - n);
 }
+__device__ __forceinline__ uint32_t lds_byte(const uint32_t* buf, uint32_t o) { return lds_bits(buf, o, 8); }
 
 constexpr int kJpegWG = 256;     // luma blocks (threads) per workgroup = 64 MCUs
-constexpr int kAsmWords = 2048;  // LDS assembly buffer for the workgroup's bit range (64 Kbit)
 
 // Gray source staging: the raw rows a workgroup's 64 MCUs read (8 per MCU row + a 1-row halo each
 // side, full width + 1-column halos, edge-clamped) are loaded once, coalesced, into LDS; the 6×6
 // patches of the exact-2× render then come from LDS instead of 36 scattered global loads per
 // block. Pixels are converted to f32 (rescale) once while staging, not once per patch use (2.25×).
 constexpr int kPatchLds = 4864;  // f32 elements (19 KiB; 256²: 18 × 258 = 4644); larger footprints use global loads
+// One LDS region serves the render (source patch above) and then, once every block is rendered,
+// the workgroup's assembled bit range followed by its staged stuffed output bytes.
+constexpr int kUnionWords = kPatchLds + 2048;  // 27 KiB: bit ranges up to ~220 Kbit
 
 constexpr int kPrivWords = 5;    // per-block Huffman bits kept in LDS (160 bits, odd stride) ...
 constexpr int kSpillWords = 56;  // ... the rest in the block's global spill slot (a block needs ≤ 1700)
@@ -131,19 +142,28 @@ __device__ __forceinline__ uint32_t priv_word(const uint32_t* pb, const uint32_t
 __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(4))) void jpeg_fused_kernel(const uint8_t* __restrict__ canvas,
                                                              const JpegDesc* __restrict__ jd, int ncanvas, int out_w,
                                                              int out_h, QuantRecip q, JpegWork w, JpegRenderSrc rs,
-                                                             int32_t* __restrict__ out_sizes, int dbg) {
+                                                             uint8_t* __restrict__ out, int32_t* __restrict__ out_sizes,
+                                                             int dbg) {
   __shared__ uint32_t actab[256];
   __shared__ uint32_t dctab[16];
   __shared__ int32_t sdc[kJpegWG];
   __shared__ uint32_t spriv[kJpegWG * kPrivWords];  // per-block AC Huffman bits
-  __shared__ uint32_t swg[kAsmWords + 2];           // the workgroup's bit range
   __shared__ uint32_t sh[17];
-  __shared__ uint32_t s_ticket, s_prefix;
+  __shared__ uint32_t sff[4 * 8];
+  __shared__ uint32_t s_ticket, s_obase, s_nown, s_strad_v, s_fin_v, s_f, s_nwords;
+  __shared__ bool s_bad, s_strad, s_fin;
   __shared__ int32_t s_prevdc;
-  __shared__ __attribute__((aligned(16))) float spatch[kPatchLds];
+  __shared__ __attribute__((aligned(16))) float spatch[kUnionWords];  // render patch, then swg + output
+  uint32_t* const swg = reinterpret_cast<uint32_t*>(spatch);             // the workgroup's bit range
   const int tid = threadIdx.x;
+  // Records of the previous launch (the other half of the look area) are dead: clear them here
+  // for the next launch instead of a separate memset launch.
+  if (w.clear_words) {
+    uint64_t* other = w.look + w.clear_base;
+    for (size_t i = (size_t)blockIdx.x * kJpegWG + tid; i < w.clear_words; i += (size_t)gridDim.x * kJpegWG) other[i] = 0ull;
+  }
   if (dbg == 8) {  // profiling variant: empty workgroup
-    if (tid == 999) w.total[0] = 1u;
+    if (tid == 999) out_sizes[0] = 1;
     return;
   }
   actab[tid] = kHuffAcLuma.e[tid];
@@ -179,7 +199,7 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(4))) vo
   // The part is workgroup-uniform: keep it in an SGPR.
   const int part = (int)__builtin_amdgcn_readfirstlane(s_ticket);
   if (dbg == 7) {  // profiling variant: tables + ticket only
-    if (part == 0x7FFFFFF1) w.total[0] = 1u;
+    if (part == 0x7FFFFFF1) out_sizes[0] = 1;
     return;
   }
   const int mcux = out_w >> 4;
@@ -302,7 +322,7 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(4))) vo
       int acc = 0;
 #pragma unroll
       for (int i = 0; i < 64; ++i) acc += blk[i] * (i + 1);
-      if (acc == 0x7FFFFFF1) w.total[0] = 1u;
+      if (acc == 0x7FFFFFF1) out_sizes[0] = 1;
       return;
     }
     // Level shift (x − 128) folded into the DC term: the islow FDCT is linear and its only
@@ -358,7 +378,7 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(4))) vo
     acbits = lw.bits;
   }
   if (dbg == 2) {  // profiling variant: stop after FDCT + quantisation + AC coding
-    if (dc0 == 0x7FFFFFF1 || acbits == 0x7FFFFFF1u) w.total[0] = 1u;
+    if (dc0 == 0x7FFFFFF1 || acbits == 0x7FFFFFF1u) out_sizes[0] = 1;
     return;
   }
   sdc[tid] = dc0;
@@ -384,58 +404,14 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(4))) vo
   const int dclen = valid ? (int)(dce >> 16) + dn : 0;
   const uint32_t dccode = ((dce & 0xFFFFu) << dn) | ((uint32_t)(diff < 0 ? diff - 1 : diff) & ((1u << dn) - 1u));
   const uint32_t bits = valid ? (uint32_t)dclen + acbits : 0u;
-  // ---- 3. workgroup scan + look-back --------------------------------------------------------
+  // ---- 3. workgroup scan, bit range assembled in LDS ----------------------------------------
   uint32_t agg = 0;
   const uint32_t excl = block_exclusive_scan(bits, sh, &agg);  // ends with a barrier
-  uint64_t* look = w.look + (size_t)img * parts;
-  if (tid < 64) {
-    // Wave 0 looks back through a window of 64 predecessors per round trip: lane l reads the
-    // status of part (hi - l); the nearest inclusive prefix ends the window and the aggregates up
-    // to it are summed across the wave. (A serial walk costs one device-scope load latency per
-    // predecessor — the critical path of images whose parts all run concurrently.)
-    const int lane = tid;
-    uint32_t prefix = 0;
-    if (part == 0 || dbg == 4) {  // dbg 4: profiling variant without the look-back wait
-      if (lane == 0) look_store(&look[part], 2u, agg);
-    } else {
-      if (lane == 0) look_store(&look[part], 1u, agg);
-      int hi = part - 1;
-      uint32_t spins = 0;
-      for (;;) {
-        const int p = hi - lane;
-        const uint64_t st = p >= 0 ? look_load(&look[p]) : (2ull << 32);  // before part 0: inclusive 0
-        const uint32_t state = (uint32_t)(st >> 32);
-        const uint64_t incl = __ballot(state == 2u);
-        const int stop = incl ? __builtin_ctzll(incl) : 64;  // nearest inclusive prefix
-        const uint64_t need = stop >= 63 ? ~0ull : ((2ull << stop) - 1ull);
-        if (__ballot(state == 0u) & need) {  // a needed predecessor has not published yet
-          if (++spins > (1u << 26)) {  // cannot happen with ordered tickets; never hang the GPU
-            prefix = 0xFFFFFFFFu;
-            break;
-          }
-          __builtin_amdgcn_s_sleep(1);
-          continue;
-        }
-        uint32_t lo32 = lane <= stop ? (uint32_t)st : 0u, hi32 = 0u;  // 64-bit wave sum
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-          const uint32_t l2 = __shfl_xor(lo32, o, 64), h2 = __shfl_xor(hi32, o, 64);
-          const uint32_t s = lo32 + l2;
-          hi32 += h2 + (s < lo32 ? 1u : 0u);
-          lo32 = s;
-        }
-        prefix = sat_add(prefix, hi32 ? 0xFFFFFFFFu : lo32);
-        if (stop < 64) break;
-        hi -= 64;
-      }
-      if (lane == 0) look_store(&look[part], 2u, sat_add(prefix, agg));
-    }
-    if (lane == 0) s_prefix = prefix;
-  }
-  // Meanwhile: assemble the workgroup's contiguous bit range in LDS: each block's DC code, then
-  // its AC words shifted behind it.
+  // Each block's DC code, then its AC words shifted behind it, into the workgroup's contiguous
+  // bit range (MSB-first words), in the LDS region the render patch used. A range too long for
+  // it (> ~220 Kbit: pathological detail) poisons the image, which the host then re-encodes.
   const uint32_t nlocal = (agg + 31) >> 5;
-  const bool in_lds = nlocal < (uint32_t)kAsmWords;  // workgroup-uniform
+  const bool in_lds = nlocal + 2u <= (uint32_t)kUnionWords;  // workgroup-uniform
   const uint32_t nwp = (acbits + 31) >> 5;
   const uint32_t acpos = excl + (uint32_t)dclen;
   if (in_lds) {
@@ -454,162 +430,208 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(4))) vo
     }
   }
   __syncthreads();
-  const uint32_t prefix = s_prefix;
-  const uint32_t end = sat_add(prefix, agg);
-  const uint32_t cap_bits = d.stage_words * 32u;
-  uint32_t* stage = w.stage + d.stage_off;
-  // ---- 4. emission: coalesced word stores (only the two edge words, shared with the
-  //         neighbouring workgroups, are atomic) --------------------------------------------------
-  if (end <= cap_bits && agg) {
-    if (in_lds) {
-      const uint32_t sft = prefix & 31u, base = prefix >> 5;
-      const uint32_t nw = ((prefix + agg + 31u) >> 5) - base;
-      for (uint32_t j = tid; j < nw; j += kJpegWG) {
-        uint32_t v = j < nlocal ? swg[j] >> sft : 0u;
-        if (sft && j > 0) v |= swg[j - 1] << (32u - sft);
-        if (j == 0 || j == nw - 1)
-          atomicOr(&stage[base + j], v);
-        else
-          stage[base + j] = v;
-      }
-    } else if (valid) {
-      // Very detailed workgroup (> 64 Kbit): each block ORs its bits straight into the stage.
-      const uint32_t p0 = prefix + excl;
-      const uint32_t dv = dclen ? dccode << (32 - dclen) : 0u;
-      atomicOr(&stage[p0 >> 5], dv >> (p0 & 31u));
-      if (p0 & 31u) atomicOr(&stage[(p0 >> 5) + 1], dv << (32u - (p0 & 31u)));
-      const uint32_t pa = prefix + acpos;
-      for (uint32_t i = 0; i < nwp; ++i) {
-        const uint32_t v = priv_word(pbuf, pspill, i), dst = pa + 32u * i, wi = dst >> 5, shf = dst & 31u;
-        atomicOr(&stage[wi], v >> shf);
-        if (shf) atomicOr(&stage[wi + 1], v << (32u - shf));
-      }
+  // ---- 4. this workgroup's stuffing record -------------------------------------------------
+  // Output byte k (bits 8k..8k+7 of the image's segment) belongs to the workgroup holding its
+  // last bit; its offset in the stuffed output is k + (0xFF bytes before k). Whether a byte is
+  // 0xFF depends on where the workgroup's range starts inside a byte (a = start mod 8), known only
+  // after the look-back — so the record carries, for all eight alignments, the number of 0xFF
+  // bytes lying wholly inside the range (ff[a]), plus its leading-ones count and last 7 bits
+  // (the byte that straddles two workgroups). Successors then resolve any chain of aggregates.
+  const uint32_t A = agg;
+  uint32_t ffc[8];
+#pragma unroll
+  for (int al = 0; al < 8; ++al) ffc[al] = 0;
+  if (in_lds) {
+#pragma unroll
+    for (int al = 0; al < 8; ++al) {
+      const uint32_t f = (uint32_t)((8 - al) & 7);
+      const uint32_t nfull = A >= f ? (A - f) >> 3 : 0u;
+      for (uint32_t i = tid; i < nfull; i += kJpegWG) ffc[al] += lds_byte(swg, f + 8u * i) == 0xFFu;
     }
   }
-  if (part == parts - 1 && tid == 0) {
-    const uint32_t nbytes = (end + 7) >> 3;
-    const bool overflow = end == 0xFFFFFFFFu || end > cap_bits || 2u * nbytes + 16u > d.out_cap ||
-                          (nbytes + kStuffChunk - 1) / kStuffChunk > (uint32_t)w.max_chunks;
-    w.total[img] = overflow ? 0xFFFFFFFFu : end;
-    if (overflow) out_sizes[img] = -1;
+  const int lane = tid & 63, wv = tid >> 6;
+#pragma unroll
+  for (int al = 0; al < 8; ++al) ffc[al] = (uint32_t)wave_sum_i32((int)ffc[al]);
+  if (lane == 0) {
+#pragma unroll
+    for (int al = 0; al < 8; ++al) sff[wv * 8 + al] = ffc[al];
   }
-}
-
-// Byte i of the entropy-coded segment (MSB-first words), final byte padded with 1-bits.
-__device__ __forceinline__ uint32_t seg_byte(const uint32_t* stage, uint32_t i, uint32_t nbytes, uint32_t padbits) {
-  uint32_t v = (stage[i >> 2] >> (24 - 8 * (i & 3))) & 0xFFu;
-  if (padbits && i == nbytes - 1) v |= 0xFFu >> padbits;
-  return v;
-}
-
-constexpr int kStuffThreads = 256;
-constexpr int kBytesPerThread = kStuffChunk / kStuffThreads;  // 16
-constexpr int kStuffGrid = 512;                               // persistent-style: 2 workgroups per CU
-
-// Bytes of the largest image of the launch (an overflowed image forces the full sweep: its
-// partially written stage must be cleared). Every workgroup reduces the ≤ few hundred totals.
-__device__ __forceinline__ uint32_t launch_max_bytes(const JpegWork& w, int ncanvas, uint32_t* sh) {
-  uint32_t m = 0;
-  for (int i = threadIdx.x; i < ncanvas; i += blockDim.x) {
-    const uint32_t t = w.total[i];
-    m = max(m, t == 0xFFFFFFFFu ? 0x7FFFFFFFu : (t + 7) >> 3);
-  }
-  m = wave_max_u32(m);
-  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = m;
   __syncthreads();
-  uint32_t r = 0;
-  for (int i = 0; i < (int)(blockDim.x >> 6); ++i) r = max(r, sh[i]);
-  __syncthreads();
-  return r;
-}
-
-// Work items are (chunk, image) in chunk-major order, so the valid chunks of every image come first
-// and the grid-stride loop stops at the largest image instead of sweeping max_chunks × images.
-__global__ __launch_bounds__(kStuffThreads) void jpeg_stuff_count_kernel(const JpegDesc* __restrict__ jd, int ncanvas,
-                                                                         JpegWork w) {
-  __shared__ uint32_t cnt;
-  __shared__ uint32_t shm[16];
-  // The encoder's look-back words are done with: clear them for the next launch.
-  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < w.look_used; i += (size_t)gridDim.x * blockDim.x)
-    w.look[i] = 0ull;
-  const uint32_t maxb = launch_max_bytes(w, ncanvas, shm);
-  const int n = ncanvas * w.max_chunks;
-  for (int it = blockIdx.x; it < n; it += gridDim.x) {
-    const int chunk = it / ncanvas, img = it - chunk * ncanvas;
-    const uint32_t c0 = (uint32_t)chunk * kStuffChunk;
-    if (c0 >= maxb) break;
-    const uint32_t total = w.total[img];
-    if (total == 0xFFFFFFFFu) continue;
-    const uint32_t nbytes = (total + 7) >> 3;
-    if (c0 >= nbytes) continue;
-    const uint32_t* stage = w.stage + jd[img].stage_off;
-    if (threadIdx.x == 0) cnt = 0;
-    __syncthreads();
-    uint32_t ff = 0;
-    const uint32_t b0 = c0 + threadIdx.x * kBytesPerThread;
+  uint64_t* look = w.look + w.look_base + (size_t)img * parts * 3;
+  if (tid < 64) {
+    uint32_t ff[8];
 #pragma unroll
-    for (int k = 0; k < kBytesPerThread; ++k) {
-      const uint32_t i = b0 + k;
-      if (i < nbytes) ff += seg_byte(stage, i, nbytes, total & 7u) == 0xFFu;
+    for (int al = 0; al < 8; ++al) ff[al] = sff[al] + sff[8 + al] + sff[16 + al] + sff[24 + al];
+    const uint32_t w0 = in_lds ? swg[0] : 0u;
+    const uint32_t lead = ~w0 ? (uint32_t)__builtin_clz(~w0) : 32u;
+    const uint32_t head = min(min(lead, 8u), A);  // leading ones of the range
+    const uint32_t tail = in_lds && A >= 7 ? lds_bits(swg, A - 7, 7) : (in_lds ? lds_bits(swg, 0, A) : 0u);
+    const bool poison = !in_lds || A >= (1u << 20) || ff[0] > 0x7FFFu;
+    // ---- 5. publish the aggregate (3 words), then the decoupled look-back ----------------------
+    if (lane == 0 && part < parts - 1) {
+      look_store64(&look[3 * part + 1], (1ull << 62) | ((uint64_t)(ff[2] & 0x7FFF) << 45) |
+                                            ((uint64_t)(ff[3] & 0x7FFF) << 30) | ((uint64_t)(ff[4] & 0x7FFF) << 15) |
+                                            (uint64_t)(ff[5] & 0x7FFF));
+      look_store64(&look[3 * part + 2], (1ull << 62) | ((uint64_t)(ff[6] & 0x7FFF) << 15) | (uint64_t)(ff[7] & 0x7FFF));
+      look_store64(&look[3 * part], (1ull << 62) | ((uint64_t)poison << 61) | ((uint64_t)(A & 0xFFFFF) << 41) |
+                                        ((uint64_t)tail << 34) | ((uint64_t)head << 30) |
+                                        ((uint64_t)(ff[0] & 0x7FFF) << 15) | (uint64_t)(ff[1] & 0x7FFF));
     }
-    if (ff) atomicAdd(&cnt, ff);
-    __syncthreads();
-    if (threadIdx.x == 0) w.chunk_ff[(size_t)img * w.max_chunks + chunk] = cnt;
+    // Lane l looks at part (hi − l): the nearest inclusive record ends the window; the aggregates
+    // after it are resolved in order (their start bits are the inclusive end plus a suffix sum of
+    // aggregate lengths, which fixes every alignment). Part −1 is an inclusive (0, 0) sentinel.
+    uint32_t p_start = 0, ff_before = 0, tail_prev = 0;
+    bool bad = poison;
+    if (part > 0) {
+      const int hi = part - 1;
+      uint32_t spins = 0;
+      uint64_t r0 = 0, r1 = 0, r2 = 0;
+      int stop;
+      for (;;) {
+        const int q = hi - lane;
+        uint32_t tag = 2;
+        r0 = 2ull << 62;
+        r1 = r2 = 0;
+        if (q >= 0) {
+          r0 = look_load(&look[3 * q]);
+          tag = (uint32_t)(r0 >> 62);
+          if (tag == 1u) {
+            r1 = look_load(&look[3 * q + 1]);
+            r2 = look_load(&look[3 * q + 2]);
+            if ((r1 >> 62) != 1u || (r2 >> 62) != 1u) tag = 0;  // words land one by one
+          }
+        }
+        const uint64_t incl = __ballot(tag == 2u);
+        stop = incl ? __builtin_ctzll(incl) : 64;
+        const uint64_t need = stop >= 63 ? ~0ull : ((2ull << stop) - 1ull);
+        if ((__ballot(tag == 0u) & need) || stop == 64) {  // a needed record is not published yet
+          if (++spins > (1u << 26)) {  // cannot happen with ordered tickets; never hang the GPU
+            bad = true;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+          continue;
+        }
+        break;
+      }
+      if (!bad) {
+        const bool isagg = lane < stop;
+        const uint32_t alen = isagg ? (uint32_t)(r0 >> 41) & 0xFFFFFu : 0u;
+        uint32_t suf = alen;  // inclusive suffix sum over lanes l..63
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+          const uint32_t t = (uint32_t)__shfl_down((int)suf, o, 64);
+          if (lane + o < 64) suf += t;
+        }
+        // Inclusive record at lane `stop`: end bit, 0xFF count, last 7 bits.
+        const uint32_t iend = (uint32_t)__shfl((int)((uint32_t)(r0 >> 39) & 0x3FFFFFu), stop, 64);
+        const uint32_t iff = (uint32_t)__shfl((int)((uint32_t)(r0 >> 19) & 0xFFFFFu), stop, 64);
+        const uint32_t mytail = isagg ? (uint32_t)(r0 >> 34) & 0x7Fu : (uint32_t)(r0 >> 12) & 0x7Fu;
+        const uint32_t prevtail = (uint32_t)__shfl_down((int)mytail, 1, 64);  // part q − 1's last bits
+        const uint32_t qstart = iend + (suf - alen);
+        const uint32_t al = qstart & 7u;
+        uint32_t fq = 0;
+        if (isagg) {
+          const uint32_t sel = al < 2 ? (uint32_t)(r0 >> (al ? 0 : 15)) : al < 6 ? (uint32_t)(r1 >> (15 * (5 - al)))
+                                                                                : (uint32_t)(r2 >> (15 * (7 - al)));
+          fq = sel & 0x7FFFu;
+          const uint32_t hq = (uint32_t)(r0 >> 30) & 0xFu, m = (1u << al) - 1u;
+          if (al && (prevtail & m) == m && hq >= 8u - al) ++fq;  // the straddling byte
+        }
+        const bool pois = __ballot(lane <= stop && ((r0 >> 61) & 1ull)) != 0;
+        bad = bad || pois;
+        ff_before = iff + (uint32_t)wave_sum_i32((int)fq);
+        p_start = iend + (uint32_t)__shfl((int)suf, 0, 64);
+        tail_prev = (uint32_t)__shfl((int)mytail, 0, 64);
+      }
+    }
+    // ---- 6. own 0xFF count, inclusive record ---------------------------------------------------
+    const uint32_t al = p_start & 7u, f = (8u - al) & 7u;
+    const bool last = part == parts - 1;
+    uint32_t own = ff[al], nown = 0;
+    bool strad = false, fin = false;
+    uint32_t strad_v = 0, fin_v = 0;
+    if (al) {  // the byte shared with the previous workgroup
+      strad = true;
+      const uint32_t take = min(8u - al, A);
+      strad_v = ((tail_prev & ((1u << al) - 1u)) << (8u - al)) | (lds_bits(swg, 0, take) << (8u - al - take));
+      if (take < 8u - al) strad_v |= (1u << (8u - al - take)) - 1u;  // final byte: pad with ones
+      own += strad_v == 0xFFu;
+    }
+    const uint32_t nfull = A >= f ? (A - f) >> 3 : 0u;
+    const uint32_t rem = A >= f ? A - f - 8u * nfull : 0u;
+    if (last && rem) {  // the image's final partial byte, padded with 1-bits
+      fin = true;
+      fin_v = (lds_bits(swg, f + 8u * nfull, rem) << (8u - rem)) | ((1u << (8u - rem)) - 1u);
+      own += fin_v == 0xFFu;
+    }
+    nown = (uint32_t)strad + nfull + (uint32_t)fin;
+    const uint32_t end = p_start + A;
+    bad = bad || end >= (1u << 22) || ff_before + own >= (1u << 20);
+    const uint32_t obase = (p_start >> 3) + ff_before;
+    bad = bad || obase + 2u * nown > d.out_cap;
+    if (lane == 0) {
+      look_store64(&look[3 * part], (2ull << 62) | ((uint64_t)bad << 61) | ((uint64_t)(end & 0x3FFFFF) << 39) |
+                                        ((uint64_t)((ff_before + own) & 0xFFFFF) << 19) |
+                                        ((uint64_t)(in_lds ? (A >= 7 ? lds_bits(swg, A - 7, 7) : 0u) : 0u) << 12));
+      s_bad = bad;
+      s_obase = obase;
+      s_nown = nown;
+      s_strad = strad;
+      s_fin = fin;
+      s_strad_v = strad_v;
+      s_fin_v = fin_v;
+      s_f = f;
+      s_nwords = nlocal + 2u;
+      if (last) out_sizes[img] = bad ? -1 : (int32_t)(((end + 7u) >> 3) + ff_before + own);
+    }
   }
-}
-
-// Writes the stuffed chunk into host-mapped memory and clears the stage words it consumed, so the
-// stage is all-zero again for the next launch (the encoder ORs bits into it).
-__global__ __launch_bounds__(kStuffThreads) void jpeg_stuff_write_kernel(const JpegDesc* __restrict__ jd, int ncanvas,
-                                                                         JpegWork w, uint8_t* __restrict__ out,
-                                                                         int32_t* __restrict__ out_sizes) {
-  __shared__ uint32_t sh[17];
-  __shared__ uint8_t buf[2 * kStuffChunk];
-  const uint32_t maxb = launch_max_bytes(w, ncanvas, sh);
-  const int n = ncanvas * w.max_chunks;
-  for (int it = blockIdx.x; it < n; it += gridDim.x) {
-    const int chunk = it / ncanvas, img = it - chunk * ncanvas;
-    const uint32_t c0 = (uint32_t)chunk * kStuffChunk;
-    if (c0 >= maxb) break;
-    const JpegDesc d = jd[img];
-    uint32_t* stage = w.stage + d.stage_off;
-    const uint32_t total = w.total[img];
-    if (total == 0xFFFFFFFFu) {  // overflowed image (rare): clear whatever the encoder wrote
-      for (uint32_t i = c0 / 4 + threadIdx.x; i < (c0 + kStuffChunk) / 4 && i < d.stage_words; i += blockDim.x)
-        stage[i] = 0u;
-      continue;
+  __syncthreads();
+  if (dbg == 4 || s_bad) return;
+  // ---- 7. stuffed bytes straight into the host-mapped output --------------------------------
+  // Thread t takes a contiguous run of the owned bytes; a block scan of (bytes + 0xFF count) gives
+  // every run its output position; the stuffed bytes are staged in LDS behind the bit range and
+  // copied out with consecutive lanes on consecutive bytes.
+  const uint32_t nown = s_nown, f = s_f, hs = s_strad ? 1u : 0u;
+  const uint32_t per = (nown + kJpegWG - 1) / kJpegWG;
+  const uint32_t j0 = min(nown, tid * per), j1 = min(nown, j0 + per);
+  auto owned = [&](uint32_t j) -> uint32_t {
+    if (j < hs) return s_strad_v;
+    const uint32_t i = j - hs;
+    const uint32_t nfull = nown - hs - (s_fin ? 1u : 0u);
+    return i < nfull ? lds_byte(swg, f + 8u * i) : s_fin_v;
+  };
+  uint32_t cnt = 0;
+  for (uint32_t j = j0; j < j1; ++j) cnt += owned(j) == 0xFFu ? 2u : 1u;
+  uint32_t tot = 0;
+  uint32_t o = block_exclusive_scan(cnt, sh, &tot);
+  uint8_t* sbuf = reinterpret_cast<uint8_t*>(swg + ((s_nwords + 3u) & ~3u));  // behind the bit range
+  const bool staged_out = tot <= (uint32_t)(kUnionWords - ((s_nwords + 3u) & ~3u)) * 4u;
+  uint8_t* dst = out + d.out_off + s_obase;
+  for (uint32_t j = j0; j < j1; ++j) {
+    const uint32_t v = owned(j);
+    if (staged_out) {
+      sbuf[o++] = (uint8_t)v;
+      if (v == 0xFFu) sbuf[o++] = 0;
+    } else {
+      dst[o++] = (uint8_t)v;
+      if (v == 0xFFu) dst[o++] = 0;
     }
-    const uint32_t nbytes = (total + 7) >> 3;
-    if (c0 >= nbytes) continue;
-    const uint32_t* ffc = w.chunk_ff + (size_t)img * w.max_chunks;
-    // Output offset of this chunk = bytes before it + 0xFF stuffing inserted before it.
-    uint32_t before = 0;
-    for (int c = 0; c < chunk; ++c) before += ffc[c];
-    const uint32_t obase = c0 + before;
-    const uint32_t b0 = c0 + threadIdx.x * kBytesPerThread;
-    uint32_t v[kBytesPerThread];
-    uint32_t mine = 0;
-#pragma unroll
-    for (int k = 0; k < kBytesPerThread; ++k) {
-      const uint32_t i = b0 + k;
-      v[k] = i < nbytes ? seg_byte(stage, i, nbytes, total & 7u) : 0x100u;  // 0x100 = past the end
-      mine += v[k] < 0x100u ? (v[k] == 0xFFu ? 2u : 1u) : 0u;
-    }
-    uint32_t chunk_len = 0;
-    uint32_t o = block_exclusive_scan(mine, sh, &chunk_len);  // ends with a barrier: stage reads done
-#pragma unroll
-    for (int k = 0; k < kBytesPerThread; ++k) {
-      if (v[k] >= 0x100u) continue;
-      buf[o++] = (uint8_t)v[k];
-      if (v[k] == 0xFFu) buf[o++] = 0;
-    }
-    const uint32_t w0 = c0 / 4, w1 = min((nbytes + 3) / 4, (c0 + kStuffChunk) / 4);
-    for (uint32_t i = w0 + threadIdx.x; i < w1; i += blockDim.x) stage[i] = 0u;
+  }
+  if (staged_out) {
     __syncthreads();
-    uint8_t* dst = out + d.out_off + obase;
-    for (uint32_t i = threadIdx.x; i < chunk_len; i += blockDim.x) dst[i] = buf[i];
-    if (c0 + kStuffChunk >= nbytes && threadIdx.x == 0) out_sizes[img] = (int32_t)(obase + chunk_len);
-    __syncthreads();  // buf is reused by the next iteration
+    // Dword stores into host memory (4× fewer PCIe write requests than bytes): byte head up to
+    // the first 4-aligned address, dwords assembled from LDS bytes, byte tail.
+    const uint32_t head = min(tot, (uint32_t)((4u - ((uintptr_t)dst & 3u)) & 3u));
+    if (tid < head) dst[tid] = sbuf[tid];
+    const uint32_t nd = (tot - head) >> 2;
+    uint32_t* dw = reinterpret_cast<uint32_t*>(dst + head);
+    for (uint32_t i = tid; i < nd; i += kJpegWG) {
+      const uint8_t* b = sbuf + head + 4u * i;
+      dw[i] = (uint32_t)b[0] | ((uint32_t)b[1] << 8) | ((uint32_t)b[2] << 16) | ((uint32_t)b[3] << 24);
+    }
+    const uint32_t t0 = head + 4u * nd;
+    if (t0 + tid < tot) dst[t0 + tid] = sbuf[t0 + tid];
   }
 }
 
@@ -622,8 +644,8 @@ void launch_jpeg(const uint8_t* canvas, const JpegDesc* jd, int ncanvas, int out
                  JpegWork& w, uint8_t* out, int32_t* out_sizes, hipStream_t stream, const JpegRenderSrc* fused) {
   if (ncanvas <= 0) return;
   if (out_w % 16 || out_h % 16) throw DeviceError("GPU JPEG encoder needs canvas dims that are multiples of 16");
-  if (w.max_chunks <= 0 || !w.total || !w.chunk_ff || !w.stage || !w.look || !w.ticket || !w.spill)
-    throw DeviceError("launch_jpeg: JpegWork incomplete");
+  if (!w.look || !w.ticket || !w.spill) throw DeviceError("launch_jpeg: JpegWork incomplete");
+  if (w.look_base && w.look_base != 3 * w.look_cap) throw DeviceError("launch_jpeg: look area state corrupt");
   QuantRecip q;
   for (int i = 0; i < 64; ++i) {
     const uint32_t dv = (uint32_t)div_luma[i];
@@ -647,13 +669,27 @@ void launch_jpeg(const uint8_t* canvas, const JpegDesc* jd, int ncanvas, int out
     const char* e = std::getenv("NM03_JPEG_LDS_PAD");
     return e ? std::atoi(e) : 0;
   }();
-  jpeg_fused_kernel<<<parts * ncanvas, kJpegWG, pad, stream>>>(canvas, jd, ncanvas, out_w, out_h, q, w, rs,
+  // The look-back records (3 words per workgroup) start unpublished. Eager launches alternate
+  // between two halves of the look area, each launch clearing the half the previous one used
+  // (stream order makes that safe); captured launches (hipGraph replay repeats the arguments)
+  // clear their own half with a memset node instead.
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  (void)hipStreamIsCapturing(stream, &cap);
+  const size_t words = (size_t)parts * ncanvas * 3;
+  if (cap != hipStreamCaptureStatusNone) {
+    w.look_base = 0;
+    w.clear_words = 0;
+    check_hip(hipMemsetAsync(w.look, 0, words * sizeof(uint64_t), stream), "clear look-back");
+  } else {
+    const size_t half = 3 * w.look_cap;
+    w.clear_base = w.look_base;
+    w.clear_words = w.prev_words;
+    w.look_base = w.look_base ? 0 : half;
+    w.prev_words = words;
+  }
+  jpeg_fused_kernel<<<parts * ncanvas, kJpegWG, pad, stream>>>(canvas, jd, ncanvas, out_w, out_h, q, w, rs, out,
                                                                 out_sizes, dbg);
   check_launch("jpeg_fused_kernel");
-  jpeg_stuff_count_kernel<<<kStuffGrid, kStuffThreads, 0, stream>>>(jd, ncanvas, w);
-  check_launch("jpeg_stuff_count_kernel");
-  jpeg_stuff_write_kernel<<<kStuffGrid, kStuffThreads, 0, stream>>>(jd, ncanvas, w, out, out_sizes);
-  check_launch("jpeg_stuff_write_kernel");
 }
 
 }  // namespace nm03::gpu

@@ -769,13 +769,11 @@ PYBIND11_MODULE(_nm03, m) {
   m.def("k_jpeg", [](uintptr_t canvas, int n, int h, int w, int quality, uintptr_t stream) {
     hipStream_t st = as_stream(stream);
     const int blocks = (w / 8) * (h / 8);
-    const uint32_t stage_bytes = 256 * 1024, out_cap = 2 * stage_bytes + 64;
+    const uint32_t out_cap = 512 * 1024 + 64;
     std::vector<gpu::JpegDesc> jd(n);
     for (int i = 0; i < n; ++i) {
       std::memset(&jd[i], 0, sizeof(jd[i]));
       jd[i].canvas_off = (uint32_t)((size_t)i * w * h);
-      jd[i].stage_off = (uint32_t)(i * (stage_bytes / 4));
-      jd[i].stage_words = stage_bytes / 4;
       jd[i].out_off = (uint64_t)i * out_cap;
       jd[i].out_cap = out_cap;
       jd[i].render = -1;
@@ -786,25 +784,18 @@ PYBIND11_MODULE(_nm03, m) {
       off += (bytes + 255) / 256 * 256;
       return o;
     };
-    const int max_chunks = (int)(stage_bytes / gpu::kStuffChunk);
     const size_t look_cap = (size_t)n * ((blocks + 255) / 256);
-    const size_t o_jd = take(sizeof(gpu::JpegDesc) * n), o_stage = take((size_t)n * stage_bytes),
-                 o_look = take(look_cap * 8), o_ticket = take(4 * (size_t)n), o_zero_end = off,
-                 o_spill = take(look_cap * 256 * 56 * 4),
-                 o_tot = take((size_t)n * 4), o_cff = take((size_t)n * max_chunks * 4),
-                 o_out = take((size_t)n * out_cap), o_sz = take((size_t)n * 4);
+    const size_t o_jd = take(sizeof(gpu::JpegDesc) * n), o_look = take(6 * look_cap * 8), o_ticket = take(4 * (size_t)n),
+                 o_spill = take(look_cap * 256 * 56 * 4), o_out = take((size_t)n * out_cap), o_sz = take((size_t)n * 4);
     uint8_t* dev = (uint8_t*)scratch().get(off);
     gpu::check_hip(hipMemcpyAsync(dev + o_jd, jd.data(), sizeof(gpu::JpegDesc) * n, hipMemcpyHostToDevice, st), "H2D");
-    gpu::check_hip(hipMemsetAsync(dev + o_stage, 0, o_zero_end - o_stage, st), "memset jpeg work");
+    gpu::check_hip(hipMemsetAsync(dev + o_ticket, 0, 4 * (size_t)n, st), "memset tickets");
+    gpu::check_hip(hipMemsetAsync(dev + o_look, 0, 6 * look_cap * 8, st), "memset look-back");
     gpu::JpegWork wk;
-    wk.stage = (uint32_t*)(dev + o_stage);
     wk.look = (uint64_t*)(dev + o_look);
     wk.look_cap = look_cap;
     wk.ticket = (uint32_t*)(dev + o_ticket);
     wk.spill = (uint32_t*)(dev + o_spill);
-    wk.total = (uint32_t*)(dev + o_tot);
-    wk.chunk_ff = (uint32_t*)(dev + o_cff);
-    wk.max_chunks = max_chunks;
     int32_t divs[64];
     gpu::jpeg_divisors(quality, divs);
     gpu::launch_jpeg((const uint8_t*)canvas, (const gpu::JpegDesc*)(dev + o_jd), n, w, h, divs, wk, dev + o_out,

@@ -177,8 +177,7 @@ void hip_free_all(Slot& s) {
   if (s.h_out) (void)hipHostFree(s.h_out);
   if (s.h_sizes) (void)hipHostFree(s.h_sizes);
   for (void* p : {(void*)s.d_blob, (void*)s.d_raw_x, (void*)s.d_med, (void*)s.d_tile_mm, (void*)s.d_f32, (void*)s.d_bits, (void*)s.d_canvas,
-                  (void*)s.jw.stage, (void*)s.jw.look, (void*)s.jw.ticket, (void*)s.jw.spill,
-                  (void*)s.jw.total, (void*)s.jw.chunk_ff})
+                  (void*)s.jw.look, (void*)s.jw.ticket, (void*)s.jw.spill})
     if (p) (void)hipFree(p);
   if (s.map_region) munmap(s.map_region, (size_t)s.cap_slices * s.map_stride);
   for (auto& kv : s.graphs) (void)hipGraphExecDestroy(kv.second);
@@ -332,17 +331,11 @@ struct Engine::Impl {
       const size_t canvas_bytes = (size_t)cw * ch;
       const size_t blocks = canvas_bytes / 64;
       s.d_canvas = dmalloc<uint8_t>(canvas_bytes * s.cap_canvases, "hipMalloc canvas");
-      s.jw.stage = dmalloc<uint32_t>((size_t)kStageBytes / 4 * s.cap_canvases, "hipMalloc stage");
       s.jw.look_cap = (size_t)s.cap_canvases * ((blocks + 255) / 256);
-      s.jw.look = dmalloc<uint64_t>(s.jw.look_cap, "hipMalloc look-back");
+      s.jw.look = dmalloc<uint64_t>(6 * s.jw.look_cap, "hipMalloc look-back");
+      check_hip(hipMemset(s.jw.look, 0, 6 * s.jw.look_cap * sizeof(uint64_t)), "memset look-back");
       s.jw.ticket = dmalloc<uint32_t>(s.cap_canvases, "hipMalloc tickets");
       s.jw.spill = dmalloc<uint32_t>(s.jw.look_cap * 256 * 56, "hipMalloc jpeg spill");
-      s.jw.total = dmalloc<uint32_t>(s.cap_canvases, "hipMalloc total");
-      s.jw.max_chunks = (int)(kStageBytes / kStuffChunk);
-      s.jw.chunk_ff = dmalloc<uint32_t>((size_t)s.jw.max_chunks * s.cap_canvases, "hipMalloc chunk_ff");
-      // The encoder ORs bits into the stage and polls look-back states: both start clear.
-      check_hip(hipMemset(s.jw.stage, 0, (size_t)kStageBytes * s.cap_canvases), "memset stage");
-      check_hip(hipMemset(s.jw.look, 0, s.jw.look_cap * sizeof(uint64_t)), "memset look-back");
       check_hip(hipMemset(s.jw.ticket, 0, sizeof(uint32_t) * s.cap_canvases), "memset tickets");
       check_hip(hipHostMalloc((void**)&s.h_out, (size_t)kOutCap * s.cap_canvases, hipHostMallocMapped),
                 "hipHostMalloc out");

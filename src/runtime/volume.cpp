@@ -202,13 +202,12 @@ static void unpack_volume(const DevBuf& b, const VolumeDevice& V, std::vector<ui
 // exact 2× fit — and JPEG-encoded in chunks of kExportSlices planes. Images the GPU encoder cannot
 // hold (capacity overflow, rare) are re-encoded on the host from their rendered canvas.
 constexpr int kExportSlices = 32;
-constexpr uint32_t kVolStageBytes = 256 * 1024;
-constexpr uint32_t kVolOutCap = 2 * kVolStageBytes + 64;
+constexpr uint32_t kVolOutCap = 512 * 1024 + 64;  // per image, as the 2D engine
 
 struct ExportBufs {
   int cap = 2 * kExportSlices;  // canvases per launch
   int cw = 0, ch = 0;
-  DevBuf bits, canvas, tables, stage, look, ticket, spill, total, chunk_ff;
+  DevBuf bits, canvas, tables, look, ticket, spill;
   JpegWork jw;
   uint8_t* h_tables = nullptr;
   uint8_t* h_out = nullptr;
@@ -221,25 +220,17 @@ struct ExportBufs {
         bits(2 * vol_words * 8),
         canvas((size_t)cw_ * ch_ * 2 * kExportSlices),
         tables(2 * kExportSlices * (sizeof(RenderDesc) + sizeof(JpegDesc)) + 256),
-        stage((size_t)kVolStageBytes * 2 * kExportSlices),
-        look(8 * (size_t)2 * kExportSlices * (((size_t)cw_ * ch_ / 64 + 255) / 256)),
+        look(6 * 8 * (size_t)2 * kExportSlices * (((size_t)cw_ * ch_ / 64 + 255) / 256)),
         ticket(4 * 2 * kExportSlices),
         spill(4 * (size_t)2 * kExportSlices * (((size_t)cw_ * ch_ / 64 + 255) / 256) * 256 * 56),
-        total(4 * 2 * kExportSlices),
-        chunk_ff(4 * (size_t)2 * kExportSlices * (kVolStageBytes / kStuffChunk)),
         bits_words(vol_words) {
     const size_t blocks = (size_t)cw * ch / 64;
-    jw.stage = stage.as<uint32_t>();
     jw.look = look.as<uint64_t>();
     jw.look_cap = (size_t)cap * ((blocks + 255) / 256);
     jw.ticket = ticket.as<uint32_t>();
     jw.spill = spill.as<uint32_t>();
-    jw.total = total.as<uint32_t>();
-    jw.chunk_ff = chunk_ff.as<uint32_t>();
-    jw.max_chunks = (int)(kVolStageBytes / kStuffChunk);
-    check_hip(hipMemset(jw.stage, 0, (size_t)kVolStageBytes * cap), "memset stage");
-    check_hip(hipMemset(jw.look, 0, jw.look_cap * 8), "memset look-back");
     check_hip(hipMemset(jw.ticket, 0, 4 * (size_t)cap), "memset tickets");
+    check_hip(hipMemset(jw.look, 0, 6 * jw.look_cap * 8), "memset look-back");
     check_hip(hipHostMalloc((void**)&h_tables, cap * (sizeof(RenderDesc) + sizeof(JpegDesc)) + 256, hipHostMallocDefault),
               "hipHostMalloc export tables");
     check_hip(hipHostMalloc((void**)&h_out, (size_t)kVolOutCap * cap, hipHostMallocMapped), "hipHostMalloc out");
@@ -364,8 +355,6 @@ std::vector<std::vector<uint8_t>> VolumeRunner::export_jpegs(const VolumeInput& 
       JpegDesc& j = jd[k];
       std::memset(&j, 0, sizeof(j));
       j.canvas_off = (uint32_t)(k * canvas_bytes);
-      j.stage_off = (uint32_t)k * (kVolStageBytes / 4);
-      j.stage_words = kVolStageBytes / 4;
       j.out_off = (uint64_t)k * kVolOutCap;
       j.out_cap = kVolOutCap;
       j.render = render_is_exact_2x(r, cw, ch) ? k : -1;
