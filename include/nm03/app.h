@@ -31,7 +31,8 @@ struct AppConfig {
   std::string input;       // test_pipeline: explicit slice path
   std::string dump_mhd;    // test_pipeline: directory for MetaImage stage dumps (empty = off)
   int repeat = 1;
-  bool dilation_set = false;  // --dilation-size given (3D mode defaults to 7, BASELINE config 5)
+  bool dilation_set = false;
+  bool max_dim_set = false;   // --max-dim given (else the parallel CLI sizes buffers from the slice headers)  // --dilation-size given (3D mode defaults to 7, BASELINE config 5)
 };
 
 // Parse the shared flag set; `which` selects CLI-specific defaults. Exits on --help.

@@ -1,9 +1,11 @@
 // Cohort processors behind the three CLIs. Message texts are the reference's;
 // file:line citations point at the reference statement each message reproduces.
 #include <dirent.h>
+#include <hip/hip_runtime_api.h>
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -12,12 +14,14 @@
 #include <iomanip>
 #include <iostream>
 #include <sstream>
+#include <thread>
 
 #include "nm03/app.h"
 #include "nm03/cohort.h"
 #include "nm03/comm.h"
 #include "nm03/dicom.h"
 #include "nm03/golden.h"
+#include "nm03/gpu_types.h"
 #include "nm03/jpeg.h"
 #include "nm03/log.h"
 #include "nm03/metaimage.h"
@@ -146,7 +150,10 @@ AppConfig parse_args(int argc, char** argv, const std::string& which) {
     else if (a == "--repeat") c.repeat = std::max(1, std::atoi(val().c_str()));
     else if (a == "--json") c.json = val();
     else if (a == "--quiet") c.quiet = true;
-    else if (a == "--max-dim") c.engine.max_dim = std::atoi(val().c_str());
+    else if (a == "--max-dim") {
+      c.engine.max_dim = std::atoi(val().c_str());
+      c.max_dim_set = true;
+    }
     else if (a == "--resume") c.engine.resume = true;
     else {
       std::cerr << "unknown option " << a << " (see --help)" << std::endl;
@@ -339,29 +346,57 @@ std::string per_rank_json(const std::vector<std::vector<double>>& rows) {
   return o.str();
 }
 
+// Largest slice dimension over the plan's files (16 KiB header prefix per file, parsed on a small
+// thread pool); unreadable files are skipped (they fail in the engine's loader as usual).
+int scan_max_dim(const std::vector<PatientPlan>& plan, int threads) {
+  std::vector<const std::string*> files;
+  for (const auto& p : plan)
+    for (const auto& f : p.files) files.push_back(&f);
+  std::atomic<int> md{0};
+  std::atomic<size_t> next{0};
+  auto work = [&] {
+    std::vector<uint8_t> buf;
+    for (size_t i; (i = next.fetch_add(1)) < files.size();) {
+      try {
+        dicom::SliceFile f(*files[i], dicom::ReadMode::kDirect, 16384);
+        const dicom::Header& h = f.header(buf);
+        const int m = std::max(h.rows, h.cols);
+        int cur = md.load();
+        while (m > cur && !md.compare_exchange_weak(cur, m)) {
+        }
+      } catch (const std::exception&) {
+      }
+    }
+  };
+  const int nt = std::max(1, std::min({threads, 16, (int)files.size()}));
+  std::vector<std::thread> th;
+  for (int t = 1; t < nt; ++t) th.emplace_back(work);
+  work();
+  for (auto& t : th) t.join();
+  return md.load();
+}
+
 int parallel_rank(const AppConfig& cfg, int rank, int size, Comm& comm, int device) {
   const std::string base = cohort::cohort_dir(cfg.data_root);
   EngineConfig ec = cfg.engine;
   ec.device = device;
   const double t_setup = now_s();
-  // An engine that fails to come up on one rank must not leave the others blocked in the first
-  // collective: agree on it before going on.
+  // Cold start: the HIP runtime and the device context come up on a helper thread while rank 0
+  // plans the cohort (and scans the slice headers for the buffer size); the engine is built once
+  // both are done.
+  std::thread warm([device] {
+    (void)hipSetDevice(device);
+    void* p = nullptr;
+    if (hipMalloc(&p, 4096) == hipSuccess) (void)hipFree(p);
+  });
+  struct Joiner {
+    std::thread& t;
+    ~Joiner() {
+      if (t.joinable()) t.join();
+    }
+  } joiner{warm};
   std::unique_ptr<Engine> engine_p;
-  std::string setup_error;
-  try {
-    engine_p = std::make_unique<Engine>(ec);
-  } catch (const std::exception& e) {
-    setup_error = e.what();
-  }
-  int64_t setup_failed = setup_error.empty() ? 0 : 1;
-  comm.allreduce_sum_i64(&setup_failed, 1);
-  if (setup_failed) {
-    if (!setup_error.empty()) std::cerr << "Fatal error: rank " << rank << " (device " << device << "): " << setup_error << std::endl;
-    return 1;
-  }
-  Engine& engine = *engine_p;
-  const double t_start = now_s();
-  const double setup_s = t_start - t_setup;
+  double t_start = 0, setup_s = 0;
   double proc_wall = 0, my_wall = 0;
   int64_t total_ok = 0, total_slices = 0, my_slices = 0, my_ok = 0;
   StageTimes agg;
@@ -406,6 +441,9 @@ int parallel_rank(const AppConfig& cfg, int rank, int size, Comm& comm, int devi
         fatal_msg = e.what();
       }
       plan_bytes = encode_plan(plan);
+      ByteWriter dims;
+      dims.u32(!engine_p && !cfg.max_dim_set ? (uint32_t)scan_max_dim(plan, cfg.engine.threads) : 0u);
+      plan_bytes.insert(plan_bytes.end(), dims.b.begin(), dims.b.end());
     }
     comm.allreduce_sum_i64(&fatal, 1);
     if (fatal) {
@@ -413,6 +451,36 @@ int parallel_rank(const AppConfig& cfg, int rank, int size, Comm& comm, int devi
       return 1;
     }
     comm.broadcast_bytes(plan_bytes, 0);  // ncclBroadcast of the serialized work list
+    uint32_t seen_dim = 0;
+    if (plan_bytes.size() >= 4) {
+      ByteReader dr(plan_bytes.data() + plan_bytes.size() - 4, 4);
+      seen_dim = dr.u32();
+      plan_bytes.resize(plan_bytes.size() - 4);
+    }
+    if (!engine_p) {
+      // Buffers sized for the largest slice of the cohort (headers scanned by rank 0) instead of
+      // the 512² maximum: less pinned memory to allocate and register at start-up.
+      if (seen_dim > 0) ec.max_dim = std::min(gpu::kSrgMaxDim, std::max(64, (int)((seen_dim + 63) / 64 * 64)));
+      warm.join();
+      // An engine that fails to come up on one rank must not leave the others blocked in the next
+      // collective: agree on it before going on.
+      std::string setup_error;
+      try {
+        engine_p = std::make_unique<Engine>(ec);
+      } catch (const std::exception& e) {
+        setup_error = e.what();
+      }
+      int64_t setup_failed = setup_error.empty() ? 0 : 1;
+      comm.allreduce_sum_i64(&setup_failed, 1);
+      if (setup_failed) {
+        if (!setup_error.empty())
+          std::cerr << "Fatal error: rank " << rank << " (device " << device << "): " << setup_error << std::endl;
+        return 1;
+      }
+      t_start = now_s();
+      setup_s = t_start - t_setup;
+    }
+    Engine& engine = *engine_p;
     if (fault_plan().rank_exit == rank && size > 1) {  // NM03_FAULT=rank_exit:<r>: a rank dies mid-job
       std::cerr << "injected fault: rank " << rank << " exits" << std::endl;
       _exit(9);

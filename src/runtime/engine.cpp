@@ -70,8 +70,6 @@ struct LoadedSlice {
 
 // Per-image JPEG capacities. The entropy-coded segment of a 512² canvas is a few tens of KB;
 // anything past these caps falls back to the CPU encoder (counted in StageTimes).
-constexpr uint32_t kStageBytes = 256 * 1024;
-constexpr uint32_t kOutCap = 2 * kStageBytes + 64;
 
 struct Slot {
   hipStream_t stream = nullptr;
@@ -213,6 +211,10 @@ struct Engine::Impl {
   size_t read_prefix_ = 16384;
   // 12-bit transfer packing of slices whose samples fit (nm03/pack12.h); NM03_PACK12=0 disables.
   bool pack12_ = pack12::available();
+  // Host-mapped bytes per image for the GPU encoder's stuffed output: half the canvas (128 KiB for
+  // 512², ~5× a typical medical render; anything larger is CPU re-encoded, counted in StageTimes).
+  // NM03_JPEG_OUT_CAP=<bytes> overrides (tests force the fallback with a tiny cap).
+  uint32_t out_cap_ = 0;
   // NM03_PACK_BOUNCE=0: pack into a full-size intermediate and stream-copy it (A/B of pack_stream).
   bool pack_bounce_ = true;
 
@@ -225,6 +227,8 @@ struct Engine::Impl {
     if (const char* e = std::getenv("NM03_LOAD_PREFIX"); e && *e) read_prefix_ = (size_t)std::atol(e);
     if (const char* e = std::getenv("NM03_PACK12"); e && *e && *e == '0') pack12_ = false;
     if (const char* e = std::getenv("NM03_PACK_BOUNCE"); e && *e && *e == '0') pack_bounce_ = false;
+    out_cap_ = (uint32_t)std::max<size_t>(64 * 1024, (size_t)cfg.render.out_width * cfg.render.out_height / 2) + 64;
+    if (const char* e = std::getenv("NM03_JPEG_OUT_CAP"); e && *e) out_cap_ = (uint32_t)std::max(64L, std::atol(e));
     if (const char* e = std::getenv("NM03_UPLOAD_CHUNK_KB"); e && *e) upload_chunk_ = (size_t)std::atol(e) << 10;
     if (cfg.batch_size < 1) cfg.batch_size = 1;
     if (cfg.streams < 1) cfg.streams = 1;
@@ -337,7 +341,7 @@ struct Engine::Impl {
       s.jw.ticket = dmalloc<uint32_t>(s.cap_canvases, "hipMalloc tickets");
       s.jw.spill = dmalloc<uint32_t>(s.jw.look_cap * 256 * 56, "hipMalloc jpeg spill");
       check_hip(hipMemset(s.jw.ticket, 0, sizeof(uint32_t) * s.cap_canvases), "memset tickets");
-      check_hip(hipHostMalloc((void**)&s.h_out, (size_t)kOutCap * s.cap_canvases, hipHostMallocMapped),
+      check_hip(hipHostMalloc((void**)&s.h_out, (size_t)out_cap_ * s.cap_canvases, hipHostMallocMapped),
                 "hipHostMalloc out");
       check_hip(hipHostGetDevicePointer((void**)&s.d_out, s.h_out, 0), "hipHostGetDevicePointer out");
       check_hip(hipHostMalloc((void**)&s.h_sizes, sizeof(int32_t) * s.cap_canvases, hipHostMallocMapped),
@@ -429,7 +433,11 @@ struct Engine::Impl {
       check_hip(hipEventSynchronize(ev), "batch sync");
       return;
     }
-    const double ahead = 0.8 * s.batch_ema_s - (now_s() - t_enq);
+    static const bool adapt = [] {
+      const char* e = std::getenv("NM03_EVENT_ADAPT");  // 0: plain polling (A/B)
+      return !(e && *e == '0');
+    }();
+    const double ahead = adapt ? 0.8 * s.batch_ema_s - (now_s() - t_enq) : 0.0;
     if (ahead > 100e-6 && hipEventQuery(ev) == hipErrorNotReady)
       std::this_thread::sleep_for(std::chrono::duration<double>(ahead));
     for (;;) {
@@ -623,10 +631,8 @@ struct Engine::Impl {
       JpegDesc& j = jd[k];
       std::memset(&j, 0, sizeof(j));
       j.canvas_off = (uint32_t)k * canvas_bytes;
-      j.stage_off = (uint32_t)k * (kStageBytes / 4);
-      j.stage_words = kStageBytes / 4;
-      j.out_off = (uint64_t)k * kOutCap;
-      j.out_cap = kOutCap;
+      j.out_off = (uint64_t)k * out_cap_;
+      j.out_cap = out_cap_;
       // Export runs render straight into the JPEG block kernel when the fit is an exact 2× (the
       // canvas is never materialised); test runs keep canvases for inspection.
       j.render = (mode == 0 && render_is_exact_2x(rd[k], cw, ch)) ? k : -1;
@@ -860,7 +866,7 @@ struct Engine::Impl {
               for (int k = 0; k < 2; ++k) {
                 const int cv = 2 * (int)c + k;
                 const std::string name = base + (k == 0 ? "_original.jpg" : "_processed.jpg");
-                const uint8_t* seg = use_fb[cv] ? fb[cv].data() : s.h_out + (size_t)cv * kOutCap;
+                const uint8_t* seg = use_fb[cv] ? fb[cv].data() : s.h_out + (size_t)cv * out_cap_;
                 const size_t len = use_fb[cv] ? fb[cv].size() : (size_t)s.h_sizes[cv];
                 jpeg::write_jpeg_at(dfd, rel ? items[item].out_dir : std::string(), name, jpeg_header, seg, len);
                 bytes_out += (int64_t)(jpeg_header.size() + len + 2);
@@ -1106,7 +1112,7 @@ struct Engine::Impl {
       const bool gpu_ok = jpeg_segment(s, k, fb, nullptr);
       std::vector<uint8_t> f = jpeg_header;
       if (gpu_ok)
-        f.insert(f.end(), s.h_out + (size_t)k * kOutCap, s.h_out + (size_t)k * kOutCap + s.h_sizes[k]);
+        f.insert(f.end(), s.h_out + (size_t)k * out_cap_, s.h_out + (size_t)k * out_cap_ + s.h_sizes[k]);
       else
         f.insert(f.end(), fb.begin(), fb.end());
       f.push_back(0xFF);

@@ -274,6 +274,23 @@ def test_engine_submit_pipelines_runs_identically(native, cohort_root, tmp_path)
     assert not msgs
 
 
+def test_engine_jpeg_cpu_fallback_identical(native, cohort_root, tmp_path, monkeypatch):
+    """Every image overflowing the GPU encoder's output capacity (NM03_JPEG_OUT_CAP forced tiny)
+    goes through the host re-encode fallback — under 4 concurrent slots — and the files are
+    byte-identical to the GPU-encoded ones; the fallbacks are counted."""
+    ref_out = str(tmp_path / "ref")
+    items = _items(native, cohort_root, ref_out)
+    cfg = nm.PipelineConfig(batch_size=6, streams=4, threads=8).engine_config()
+    st, t = native.Engine(cfg).run(items)
+    assert all(c == 0 for c, _ in st) and t["jpeg_fallbacks"] == 0
+    monkeypatch.setenv("NM03_JPEG_OUT_CAP", "2048")
+    fb_out = str(tmp_path / "fb")
+    st, t = native.Engine(cfg).run(_items(native, cohort_root, fb_out))
+    assert all(c == 0 for c, _ in st)
+    assert t["jpeg_fallbacks"] == 2 * len(items)
+    assert _tree(fb_out) == _tree(ref_out)
+
+
 def test_engine_fault_isolation(native, tmp_path):
     d = tmp_path / "series"
     d.mkdir()
@@ -689,3 +706,25 @@ def test_volume_slabs_two_ranks_on_one_gpu(native):
         assert np.array_equal(region, ref["region"]), rank
         assert np.array_equal(dil, ref["dilated"]), rank
         assert rounds >= 2  # the lesion spans the slab boundary: at least one exchange added voxels
+
+
+def test_cli_parallel_sizes_buffers_from_headers(native, cohort_root, tmp_path):
+    """The parallel CLI sizes its engine from the cohort's slice headers (cold start): a larger
+    slice added to one series still goes through, with the same bytes as the golden model."""
+    import shutil
+    root = tmp_path / "data"
+    shutil.copytree(cohort_root, root)
+    base = native.cohort_dir(str(root) + "/")
+    pid = native.find_patient_dirs(base)[0]
+    series, files = native.list_patient_series(base, pid)
+    big = native.phantom_slice(320, 320, 1, 3, 9, 11)
+    open(os.path.join(series, "1-99.dcm"), "wb").write(native.dicom_bytes(big))
+    out = tmp_path / "o"
+    r = run_bin("img_processing_parallel", "--data-root", str(root), "--out", str(out), "--quiet",
+                env={"NM03_LOG": "info"})
+    assert r.returncode == 0, r.stderr
+    assert "max_dim 320" in r.stdout
+    assert f"Patient {pid} completed. Successfully processed {len(files) + 1}/{len(files) + 1} images." in r.stdout
+    g = native.golden_run(big)
+    assert (out / pid / "1-99_processed.jpg").read_bytes() == g["jpeg_processed"]
+    assert (out / pid / "1-99_original.jpg").read_bytes() == g["jpeg_original"]

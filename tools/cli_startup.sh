@@ -25,8 +25,8 @@ t2 = time.perf_counter()
 print(f"hip: dlopen {1e3*(t1-t0):.1f} ms, init+first malloc {1e3*(t2-t1):.1f} ms")
 PY
 done
-for r in 1 2 3; do
-  for extra in "" "--max-dim 256" "--max-dim 256 --streams 1"; do
+for r in 1 2 3 4 5 6; do
+  for extra in "" "--max-dim 512"; do
     s=$(date +%s.%N)
     (cd /tmp && timeout -k 10 60 $GRAFT_REPO_ROOT/build/bin/img_processing_parallel --data-root $D/ --out /dev/shm/nm03_cli_out --json /tmp/cli.json --quiet $extra > /dev/null 2>&1) || exit 3
     e=$(date +%s.%N)
