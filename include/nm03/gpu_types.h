@@ -14,6 +14,9 @@ inline constexpr int kMedTileW = 64, kMedTileH = 64;
 inline constexpr int kShpTileW = 64, kShpTileH = 64;
 // Largest slice the LDS-resident region-growing kernel handles (bit-planes in LDS).
 inline constexpr int kSrgMaxDim = 512;
+// Largest 2D slice side the engine accepts. Slices above kSrgMaxDim keep K1/K3/K4 unchanged and
+// run K2 with its bit planes in a global-memory scratch instead of LDS (launch_srg_morph).
+inline constexpr int kMaxSliceDim = 4096;
 
 struct SliceDesc {
   uint32_t raw_off;    // u16 element offset of the slice in the raw/median buffers

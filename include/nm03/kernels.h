@@ -41,11 +41,16 @@ struct SrgOutputs {
   uint64_t* border_eroded = nullptr;
   uint64_t* border_dilated = nullptr;
   int32_t* iterations = nullptr;  // per-slice fixpoint iteration count (diagnostics)
+  // Slices larger than kSrgMaxDim: 4 × srg_scratch_words(max_w, max_h) words per slice of device
+  // scratch for the bit planes (the LDS-resident form cannot hold them).
+  uint64_t* scratch = nullptr;
 };
+// Words per bit plane of the K2 kernel for slices up to max_w × max_h (odd row strides).
+size_t srg_plane_words(int max_w, int max_h);
 
 // K2: LDS-resident seeded region growing (bit-parallel run fills on rows and on the transposed
-// bitmap until fixpoint) + dilation/erosion + renderer borders. One workgroup per slice;
-// slices must be ≤ kSrgMaxDim in both dimensions (larger ones go through launch_srg_global).
+// bitmap until fixpoint) + dilation/erosion + renderer borders. One workgroup per slice; the four
+// bit planes live in LDS for slices ≤ kSrgMaxDim, else in `out.scratch` (same code, global memory).
 void launch_srg_morph(const uint64_t* band, const SliceDesc* descs, int nslices, const SeedXY* seeds,
                       const PipeConsts& pc, const SrgOutputs& out, int max_w, int max_h, hipStream_t stream);
 

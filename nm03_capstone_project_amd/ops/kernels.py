@@ -84,7 +84,7 @@ def sharpen_band(median_keys, config: PipelineConfig = None, pixel_type="u16", s
 
 
 def region_grow(band, seeds=None, config: PipelineConfig = None):
-    """Seeded region growing on bool band [N,H,W] (LDS kernel, ≤512²) + dilation, erosion and the
+    """Seeded region growing on bool band [N,H,W] (LDS-resident ≤ 512², global-memory planes above) + dilation, erosion and the
     renderer border. Returns dict of bool tensors: region, dilated, eroded, border_region."""
     cfg = config or PipelineConfig()
     b = _as3d(band)

@@ -460,7 +460,7 @@ int parallel_rank(const AppConfig& cfg, int rank, int size, Comm& comm, int devi
     if (!engine_p) {
       // Buffers sized for the largest slice of the cohort (headers scanned by rank 0) instead of
       // the 512² maximum: less pinned memory to allocate and register at start-up.
-      if (seen_dim > 0) ec.max_dim = std::min(gpu::kSrgMaxDim, std::max(64, (int)((seen_dim + 63) / 64 * 64)));
+      if (seen_dim > 0) ec.max_dim = std::min(gpu::kMaxSliceDim, std::max(64, (int)((seen_dim + 63) / 64 * 64)));
       warm.join();
       // An engine that fails to come up on one rank must not leave the others blocked in the next
       // collective: agree on it before going on.

@@ -34,12 +34,16 @@ namespace nm03::gpu {
 constexpr int kSrgThreads = NM03_SRG_THREADS;
 
 
+// kGlobal: slices above kSrgMaxDim — the same algorithm on bit planes in a per-slice global scratch
+// (L2-resident for a 1024² slice: 4 × 128 KiB), for capability rather than speed.
+template <bool kGlobal>
 __global__ __launch_bounds__(kSrgThreads) void srg_morph_kernel(const uint64_t* __restrict__ band,
                                                         const SliceDesc* __restrict__ descs,
                                                         const SeedXY* __restrict__ seeds, PipeConsts pc,
                                                         SrgOutputs out, int plane_words) {
-  extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
+  extern __shared__ __attribute__((aligned(16))) uint64_t lds_planes[];
   __shared__ int flag;
+  uint64_t* const smem = kGlobal ? out.scratch + (size_t)blockIdx.x * 4 * plane_words : lds_planes;
   const SliceDesc d = descs[blockIdx.x];
   const int W = d.w, H = d.h, n = d.wpr, hb = (H + 63) >> 6;
   const int words = H * n;
@@ -98,18 +102,27 @@ __global__ __launch_bounds__(kSrgThreads) void srg_morph_kernel(const uint64_t* 
   }
 }
 
+size_t srg_plane_words(int max_w, int max_h) {
+  // Planes hold rows at the kernel's odd strides (n | 1 and hb | 1 words); a slice's n ≤ this n.
+  const int n = (max_w + 63) / 64, hb = (max_h + 63) / 64;
+  size_t plane_words = (size_t)max_h * (n | 1);
+  if ((size_t)max_w * (hb | 1) > plane_words) plane_words = (size_t)max_w * (hb | 1);
+  return (plane_words + 1) & ~(size_t)1;
+}
+
 void launch_srg_morph(const uint64_t* band, const SliceDesc* descs, int nslices, const SeedXY* seeds,
                       const PipeConsts& pc, const SrgOutputs& out, int max_w, int max_h, hipStream_t stream) {
   if (nslices <= 0) return;
-  if (max_w > kSrgMaxDim || max_h > kSrgMaxDim)
-    throw DeviceError("launch_srg_morph: slice larger than " + std::to_string(kSrgMaxDim));
-  // Planes hold rows at the kernel's odd strides (n | 1 and hb | 1 words); a slice's n ≤ this n.
-  const int n = (max_w + 63) / 64, hb = (max_h + 63) / 64;
-  int plane_words = max_h * (n | 1);
-  if (max_w * (hb | 1) > plane_words) plane_words = max_w * (hb | 1);
-  plane_words = (plane_words + 1) & ~1;
-  const size_t lds = (size_t)plane_words * 4 * sizeof(uint64_t);
-  srg_morph_kernel<<<nslices, kSrgThreads, lds, stream>>>(band, descs, seeds, pc, out, plane_words);
+  if (max_w > kMaxSliceDim || max_h > kMaxSliceDim)
+    throw DeviceError("launch_srg_morph: slice larger than " + std::to_string(kMaxSliceDim));
+  const int plane_words = (int)srg_plane_words(max_w, max_h);
+  if (max_w > kSrgMaxDim || max_h > kSrgMaxDim) {
+    if (!out.scratch) throw DeviceError("launch_srg_morph: slices above 512 need SrgOutputs.scratch");
+    srg_morph_kernel<true><<<nslices, kSrgThreads, 0, stream>>>(band, descs, seeds, pc, out, plane_words);
+  } else {
+    const size_t lds = (size_t)plane_words * 4 * sizeof(uint64_t);
+    srg_morph_kernel<false><<<nslices, kSrgThreads, lds, stream>>>(band, descs, seeds, pc, out, plane_words);
+  }
   check_launch("srg_morph_kernel");
 }
 

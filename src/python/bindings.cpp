@@ -717,8 +717,22 @@ PYBIND11_MODULE(_nm03, m) {
     o.dilated = (uint64_t*)dilated;
     o.eroded = (uint64_t*)eroded;
     o.border_region = (uint64_t*)border_region;
-    gpu::launch_srg_morph((const uint64_t*)band, t.desc, n, t.seeds, consts_from(p, border_radius), o, w, h, st);
-    gpu::check_hip(hipStreamSynchronize(st), "k_srg_morph");
+    void* scr = nullptr;  // bit planes of slices above the LDS limit
+    if (w > gpu::kSrgMaxDim || h > gpu::kSrgMaxDim) {
+      gpu::check_hip(hipMalloc(&scr, (size_t)n * 4 * gpu::srg_plane_words(w, h) * 8), "hipMalloc srg scratch");
+      o.scratch = (uint64_t*)scr;
+    }
+    try {
+      gpu::launch_srg_morph((const uint64_t*)band, t.desc, n, t.seeds, consts_from(p, border_radius), o, w, h, st);
+      gpu::check_hip(hipStreamSynchronize(st), "k_srg_morph");
+    } catch (...) {
+      if (scr) {
+        (void)hipStreamSynchronize(st);
+        (void)hipFree(scr);
+      }
+      throw;
+    }
+    if (scr) (void)hipFree(scr);
   });
   // 3D region growing on bit volumes [d][h][ceil(w/64)] (int64 words), continuing from the region
   // already present when reset is false; returns the sweep count. Synchronous on `stream`.

@@ -87,6 +87,7 @@ struct Slot {
   uint32_t* d_tile_mm = nullptr;  // per median tile (min, max) key
   float* d_f32 = nullptr;
   uint64_t* d_bits = nullptr;
+  uint64_t* d_srg_scratch = nullptr;  // K2 bit planes of slices above kSrgMaxDim (global-memory form)
   size_t plane_words = 0;
   uint8_t* d_canvas = nullptr;
   JpegWork jw;
@@ -174,7 +175,7 @@ void hip_free_all(Slot& s) {
   if (s.h_blob) (void)hipHostFree(s.h_blob);
   if (s.h_out) (void)hipHostFree(s.h_out);
   if (s.h_sizes) (void)hipHostFree(s.h_sizes);
-  for (void* p : {(void*)s.d_blob, (void*)s.d_raw_x, (void*)s.d_med, (void*)s.d_tile_mm, (void*)s.d_f32, (void*)s.d_bits, (void*)s.d_canvas,
+  for (void* p : {(void*)s.d_blob, (void*)s.d_raw_x, (void*)s.d_med, (void*)s.d_tile_mm, (void*)s.d_f32, (void*)s.d_bits, (void*)s.d_srg_scratch, (void*)s.d_canvas,
                   (void*)s.jw.look, (void*)s.jw.ticket, (void*)s.jw.spill})
     if (p) (void)hipFree(p);
   if (s.map_region) munmap(s.map_region, (size_t)s.cap_slices * s.map_stride);
@@ -233,7 +234,7 @@ struct Engine::Impl {
     if (cfg.batch_size < 1) cfg.batch_size = 1;
     if (cfg.streams < 1) cfg.streams = 1;
     if (cfg.max_dim < 16) cfg.max_dim = 16;
-    if (cfg.max_dim > kSrgMaxDim) throw DeviceError("max_dim above " + std::to_string(kSrgMaxDim) + " not supported");
+    if (cfg.max_dim > kMaxSliceDim) throw DeviceError("max_dim above " + std::to_string(kMaxSliceDim) + " not supported");
     const auto& p = cfg.pipe;
     if (p.median_window != 3 && p.median_window != 5 && p.median_window != 7 && p.median_window != 9)
       throw DeviceError("median window must be 3, 5, 7 or 9");
@@ -331,6 +332,7 @@ struct Engine::Impl {
       s.d_f32 = dmalloc<float>(s.cap_pixels, "hipMalloc f32");
       s.plane_words = (size_t)B * md * ((md + 63) / 64);
       s.d_bits = dmalloc<uint64_t>(s.plane_words * kNumPlanes, "hipMalloc bits");
+      if (md > kSrgMaxDim) s.d_srg_scratch = dmalloc<uint64_t>((size_t)B * 4 * srg_plane_words(md, md), "hipMalloc srg scratch");
       const int cw = cfg.render.out_width, ch = cfg.render.out_height;
       const size_t canvas_bytes = (size_t)cw * ch;
       const size_t blocks = canvas_bytes / 64;
@@ -676,6 +678,7 @@ struct Engine::Impl {
       launch_sharpen_band(s.d_med, plane(kPBand), mode == 1 ? s.d_f32 : nullptr, d_desc, d_shpt, nshp, pc, d_stats,
                           s.stream, s.d_tile_mm);
       SrgOutputs o;
+      o.scratch = s.d_srg_scratch;
       o.dilated = plane(kPDilated);
       o.border_dilated = plane(kPBorderD);
       if (mode == 1) {

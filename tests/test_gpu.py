@@ -111,6 +111,33 @@ def test_region_grow_kernel_vs_golden(native, conn, shape, density):
     assert np.array_equal(out["region"].cpu().numpy(), ref)
 
 
+@pytest.mark.parametrize("shape", [(600, 520), (1024, 768)])
+def test_region_grow_above_lds_limit(native, shape):
+    """Slices above 512: K2 runs on global-memory bit planes, same results as the golden model."""
+    h, w = shape
+    rng = np.random.default_rng(h + w)
+    band = rng.random(shape) < 0.58
+    seeds = [(x, y, 0) for (x, y) in native.reference_seeds(w, h)]
+    out = ops.region_grow(torch.from_numpy(band).cuda(), seeds)
+    g = native.golden_region_grow(band.astype(np.uint8), seeds, 4)
+    assert np.array_equal(out["region"].cpu().numpy(), g.astype(bool))
+    assert np.array_equal(out["dilated"].cpu().numpy(), native.golden_morph(g, 3, True).astype(bool))
+    assert np.array_equal(out["border_region"].cpu().numpy(), native.golden_border(g, 2).astype(bool))
+
+
+def test_engine_large_slice_bit_exact(native):
+    """A 768×1024 slice end to end (every stage, renders, JPEGs) on the engine = golden model."""
+    raw = native.phantom_slice(768, 1024, 2, 5, 11, 3)
+    meta = {"type": "u16", "stored_bits": 16, "slope": 1.0, "intercept": 0.0, "spacing_x": 1.0, "spacing_y": 1.0}
+    pipe = nm.SlicePipeline(nm.PipelineConfig(batch_size=1, streams=1, threads=2, max_dim=1024))
+    gpu = pipe.run_array(raw, meta)
+    ref = pipe.golden(raw, meta)
+    for k in ("band", "region", "dilated", "eroded"):
+        assert np.array_equal(gpu[k], ref[k]), k
+    assert gpu["jpegs"][0] == ref["jpeg_original"]
+    assert gpu["jpegs"][4] == ref["jpeg_processed"]
+
+
 def test_region_grow_spiral_needs_many_turns(native):
     """A 1-pixel spiral corridor forces many alternations of horizontal/vertical run fills."""
     h = w = 128
@@ -728,3 +755,19 @@ def test_cli_parallel_sizes_buffers_from_headers(native, cohort_root, tmp_path):
     g = native.golden_run(big)
     assert (out / pid / "1-99_processed.jpg").read_bytes() == g["jpeg_processed"]
     assert (out / pid / "1-99_original.jpg").read_bytes() == g["jpeg_original"]
+
+
+def test_cli_sequential_error_messages(native, cohort_root, tmp_path):
+    """img_processing_sequential reports failures with the reference's message pairs: an export
+    error prints `Error in export stage: E` then `Error processing file F:` / `Detailed error: E`
+    (main_sequential.cpp:74-76, 267-269); a device (non-pipeline) error prints
+    `Failed to process image i for patient P. Moving to next image.` (:291-293)."""
+    r = run_bin("img_processing_sequential", "--data-root", cohort_root, "--out", str(tmp_path / "o"),
+                env={"NM03_FAULT": "fail_write:1,fail_batch:2"})
+    assert r.returncode == 0, r.stderr
+    err = r.stderr
+    assert "Error in export stage: injected fault: export failure" in err
+    i = err.index("Error in export stage: injected fault: export failure")
+    assert "Detailed error: injected fault: export failure" in err[i:]
+    assert "Error processing file " in err[i:]
+    assert "Failed to process image 3 for patient PGBM-001. Moving to next image." in err
