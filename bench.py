@@ -86,6 +86,9 @@ def parse_args(argv=None):
     ap.add_argument("--scaling", choices=("weak", "strong"), default="weak",
                     help="which figure is the headline value; the other is reported next to it")
     ap.add_argument("--no-secondary", action="store_true", help="skip the other scaling mode's measurement")
+    ap.add_argument("--wipe-passes", type=int, default=20,
+                    help="also time this many passes that each first wipe their output directories (the "
+                         "reference's per-run rm -rf; reported as config.wipe_each_pass; 0 = skip)")
     ap.add_argument("--batch-size", type=int, default=64)
     ap.add_argument("--streams", type=int, default=6)
     ap.add_argument("--threads", type=int, default=0, help="host I/O threads per rank (0 = CPU budget / ranks, ≤16)")
@@ -232,21 +235,32 @@ def run_rank(args):
         lo, hi = shard_bounds(len(items), rank, world)
         return localize_items(items[lo:hi], roots[0], local_root), len(items)
 
-    def measure(scaling, out_root, steps, warmup):
+    def measure(scaling, out_root, steps, warmup, wipe=False):
         mine, global_items = shard(scaling, out_root)
         work = n.WorkList(mine)  # the shard's work list in native form (built once, like the plan)
         # Pipelined passes alternate between two output trees: two runs in flight never write the
         # same file (pass k+2 is submitted only after pass k finished).
-        works = [work, n.WorkList(_pass_items(mine, out_root, 1))] if not args.no_pipeline else [work]
+        trees = [mine, _pass_items(mine, out_root, 1)] if not args.no_pipeline else [mine]
+        works = [work, n.WorkList(trees[1])] if not args.no_pipeline else [work]
+        # wipe: every pass first empties its patients' output directories, as every reference run
+        # does (setupOutputDirectory, main_sequential.cpp:32-47), so files are created, not rewritten.
+        tree_dirs = [sorted({od for _, od in t}) for t in trees]
+
+        def wipe_tree(k):
+            if wipe:
+                for d in tree_dirs[k % len(tree_dirs)]:
+                    n.setup_output_dir(d)
 
         def passes(k_total, sink):
             if args.no_pipeline:
-                for _ in range(k_total):
+                for k in range(k_total):
+                    wipe_tree(k)
                     with _roctx_range("bench.step"):
                         sink(*engine.run_list(work))
                 return
             pending = []
             for k in range(k_total):
+                wipe_tree(k)
                 pending.append(engine.submit(works[k % 2]))
                 if len(pending) == 2:
                     sink(*engine.wait(pending.pop(0)))
@@ -321,6 +335,9 @@ def run_rank(args):
     elif not args.no_secondary:
         secondary = {"value": primary["value"], "ms_per_step": primary["ms_per_step"],
                      "global_batch": primary["global_batch"], "note": "1 rank: weak and strong coincide"}
+    wiped = None
+    if args.wipe_passes > 0:
+        wiped = measure(args.scaling, os.path.join(args.out_root, "wipe"), args.wipe_passes, 1, wipe=True)
 
     if is_root:
         value = primary["value"]
@@ -357,6 +374,10 @@ def run_rank(args):
                 "storage": {"data": local_root, "input_copies": len(roots), "out": args.out_root},
             },
         }
+        if wiped is not None:
+            rec["config"]["wipe_each_pass"] = {"value": round(wiped["value"], 2),
+                                               "ms_per_step": round(wiped["ms_per_step"], 3),
+                                               "steps": args.wipe_passes}
         if secondary is not None:
             rec["config"][other] = {k: (round(v, 3) if isinstance(v, float) else v) for k, v in secondary.items()
                                     if k in ("value", "ms_per_step", "global_batch", "per_rank", "note",

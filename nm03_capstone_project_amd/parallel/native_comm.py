@@ -98,7 +98,7 @@ def make_native_comm(rank, world, device, backend=None, timeout_s=None):
         try:
             # No segment for RCCL's own waits: a timed-out init must not raise the segment's abort
             # flag, which would also fail the agreement below and with it the host fallback.
-            comm = n.rccl_comm(rank, world, uid, device, None, timeout_s)
+            comm = n.rccl_comm(rank, world, uid, device, None, min(timeout_s, 60.0))  # init is seconds
         except Exception as e:  # noqa: BLE001
             err = f"{type(e).__name__}: {e}"
     elif not err:
