@@ -248,8 +248,7 @@ def run_rank(args):
 
         def wipe_tree(k):
             if wipe:
-                for d in tree_dirs[k % len(tree_dirs)]:
-                    n.setup_output_dir(d)
+                n.setup_output_dirs(tree_dirs[k % len(tree_dirs)], 8)
 
         def passes(k_total, sink):
             if args.no_pipeline:

@@ -36,6 +36,8 @@ Series list_patient_series(const std::string& cohort_root, const std::string& pa
 // mkdir -p <dir> and remove everything inside it (the reference's "mkdir -p && cd && rm -rf *"
 // via system(), done with std::filesystem — no shell).
 void setup_output_dir(const std::string& dir);
+// setup_output_dir for several directories on up to `threads` threads (first error rethrown).
+void setup_output_dirs(const std::vector<std::string>& dirs, int threads);
 void make_dirs(const std::string& dir);
 
 // File stem ("…/1-14.dcm" → "1-14") and file name.

@@ -1,6 +1,14 @@
 #include "nm03/cohort.h"
 
+#include <dirent.h>
+#include <fcntl.h>
+#include <unistd.h>
+
 #include <algorithm>
+#include <atomic>
+#include <cerrno>
+#include <mutex>
+#include <thread>
 #include <cstdlib>
 #include <filesystem>
 #include <stdexcept>
@@ -83,13 +91,60 @@ void make_dirs(const std::string& dir) {
 }
 
 void setup_output_dir(const std::string& dir) {
+  // The reference's `mkdir -p dir && cd dir && rm -rf *` (main_sequential.cpp:32-47) without a
+  // shell: names listed first, then one unlinkat per file (std::filesystem::remove_all costs
+  // several stat calls per entry); subdirectories go through remove_all.
   make_dirs(dir);
-  std::error_code ec;
-  for (const auto& e : fs::directory_iterator(dir, ec)) {
-    fs::remove_all(e.path(), ec);
-    if (ec) throw std::runtime_error("Failed to setup output directory: " + dir);
+  const int dfd = ::open(dir.c_str(), O_RDONLY | O_DIRECTORY | O_CLOEXEC);
+  if (dfd < 0) throw std::runtime_error("Failed to setup output directory: " + dir);
+  DIR* d = ::fdopendir(dfd);
+  if (!d) {
+    ::close(dfd);
+    throw std::runtime_error("Failed to setup output directory: " + dir);
   }
-  if (ec) throw std::runtime_error("Failed to setup output directory: " + dir);
+  std::vector<std::string> files, subdirs;
+  while (dirent* e = ::readdir(d)) {
+    const char* nm = e->d_name;
+    if (nm[0] == '.' && (nm[1] == 0 || (nm[1] == '.' && nm[2] == 0))) continue;
+    (e->d_type == DT_DIR ? subdirs : files).push_back(nm);
+  }
+  bool ok = true;
+  for (const auto& f : files)
+    if (::unlinkat(dfd, f.c_str(), 0) != 0) {
+      if (errno == EISDIR)
+        subdirs.push_back(f);
+      else if (errno != ENOENT)
+        ok = false;
+    }
+  ::closedir(d);  // closes dfd
+  std::error_code ec;
+  for (const auto& sd : subdirs) {
+    fs::remove_all(fs::path(dir) / sd, ec);
+    if (ec) ok = false;
+  }
+  if (!ok) throw std::runtime_error("Failed to setup output directory: " + dir);
+}
+
+void setup_output_dirs(const std::vector<std::string>& dirs, int threads) {
+  std::atomic<size_t> next{0};
+  std::string err;
+  std::mutex m;
+  auto work = [&] {
+    for (size_t i; (i = next.fetch_add(1)) < dirs.size();) {
+      try {
+        setup_output_dir(dirs[i]);
+      } catch (const std::exception& e) {
+        std::lock_guard<std::mutex> g(m);
+        if (err.empty()) err = e.what();
+      }
+    }
+  };
+  const int nt = std::max(1, std::min<int>(threads, (int)dirs.size()));
+  std::vector<std::thread> th;
+  for (int t = 1; t < nt; ++t) th.emplace_back(work);
+  work();
+  for (auto& t : th) t.join();
+  if (!err.empty()) throw std::runtime_error(err);
 }
 
 std::string stem(const std::string& path) { return fs::path(path).stem().string(); }

@@ -400,6 +400,10 @@ PYBIND11_MODULE(_nm03, m) {
     return py::make_tuple(s.series_dir, s.files);
   });
   m.def("setup_output_dir", &cohort::setup_output_dir);
+  m.def("setup_output_dirs", [](const std::vector<std::string>& dirs, int threads) {
+    py::gil_scoped_release nogil;
+    cohort::setup_output_dirs(dirs, threads);
+  }, py::arg("dirs"), py::arg("threads") = 8);
   m.def(
       "synth_cohort",
       [](const std::string& root, int patients, int min_slices, int max_slices, int rows, int cols, uint64_t seed,

@@ -50,3 +50,22 @@ def test_missing_series_raises(native, tmp_path):
     base.mkdir(parents=True)
     with pytest.raises(Exception, match="No series directories"):
         native.list_patient_series(str(base.parent), "PGBM-009")
+
+
+def test_setup_output_dirs_wipes_files_and_subdirs(native, tmp_path):
+    """setup_output_dir(s): the reference's `mkdir -p d && rm -rf d/*` (main_sequential.cpp:32-47):
+    every entry goes, files and nested directories alike; the directories themselves stay."""
+    dirs = []
+    for k in range(5):
+        d = tmp_path / f"PGBM-{k:03d}"
+        (d / "nested" / "deeper").mkdir(parents=True)
+        (d / "nested" / "deeper" / "x.jpg").write_bytes(b"x")
+        for i in range(30):
+            (d / f"1-{i}_original.jpg").write_bytes(b"y" * 10)
+        dirs.append(str(d))
+    dirs.append(str(tmp_path / "new" / "PGBM-999"))  # created on the way
+    native.setup_output_dirs(dirs, 4)
+    for d in dirs:
+        assert os.path.isdir(d) and os.listdir(d) == []
+    native.setup_output_dir(dirs[0])
+    assert os.listdir(dirs[0]) == []
