@@ -771,3 +771,38 @@ def test_cli_sequential_error_messages(native, cohort_root, tmp_path):
     assert "Detailed error: injected fault: export failure" in err[i:]
     assert "Error processing file " in err[i:]
     assert "Failed to process image 3 for patient PGBM-001. Moving to next image." in err
+
+
+def test_cli_parallel_patient_level_failures(native, cohort_root, tmp_path):
+    """SURVEY §4.2 T5 on the parallel CLI: a patient without a series directory, a patient whose
+    series holds no .dcm, and a slice in an unsupported (compressed) transfer syntax are reported
+    with the reference's messages (main_parallel.cpp:304, 353, 165-166) and isolated: every other
+    slice is exported and every patient is counted, as the reference's catch blocks do."""
+    import re
+    import shutil
+    root = tmp_path / "data"
+    shutil.copytree(cohort_root, root)
+    base = native.cohort_dir(str(root) + "/")
+    pids = native.find_patient_dirs(base)
+    # PGBM-9xx: no series directory at all; PGBM-8xx: an empty series directory
+    os.makedirs(os.path.join(base, "PGBM-901"))
+    os.makedirs(os.path.join(base, "PGBM-801", "1.000000-empty-1"))
+    series, files = native.list_patient_series(base, pids[0])
+    b = bytearray(native.dicom_bytes(native.phantom_slice(128, 128, 1, 1, 5, 2), syntax="explicit"))
+    ts = b"1.2.840.10008.1.2.1\x00"
+    i = b.find(ts)
+    assert i > 0
+    b[i:i + len(ts)] = b"1.2.840.10008.1.2.4.50"[:len(ts)]  # JPEG baseline: not supported
+    open(os.path.join(series, "1-77.dcm"), "wb").write(bytes(b))
+    out = tmp_path / "o"
+    r = run_bin("img_processing_parallel", "--data-root", str(root), "--out", str(out))
+    assert r.returncode == 0, r.stderr
+    assert "Error loading DICOM files for patient PGBM-901: No series directories found for patient: PGBM-901" in r.stderr
+    assert "Error processing patient PGBM-901:" in r.stderr
+    assert "Found 0 DICOM files for patient PGBM-801" in r.stdout
+    assert "Patient PGBM-801 completed. Successfully processed 0/0 images." in r.stdout
+    assert re.search(r"Error processing file .*1-77\.dcm:\nDetailed error: .*transfer syntax", r.stderr)
+    n0 = len(files)
+    assert f"Patient {pids[0]} completed. Successfully processed {n0}/{n0 + 1} images." in r.stdout
+    assert f"Successfully processed {len(pids) + 2}/{len(pids) + 2} patients." in r.stdout
+    assert not (out / pids[0] / "1-77_original.jpg").exists()
