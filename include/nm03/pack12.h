@@ -32,6 +32,10 @@ bool fits12(const uint16_t* src, size_t n);
 // bytes are written (nothing past the end: neighbouring slices may be written concurrently).
 void pack_stream(const uint16_t* src, size_t n, uint8_t* dst);
 
+// pack_stream and the range check in one pass over the samples (the engine's path): returns
+// whether every sample fit in 12 bits; if not, the n * 3 / 2 bytes written to dst are garbage.
+bool pack_stream_checked(const uint16_t* src, size_t n, uint8_t* dst);
+
 // Scalar reference of the inverse (tests; the device expands with k0_unpack.hip).
 void unpack(const uint8_t* src, size_t n, uint16_t* dst);
 

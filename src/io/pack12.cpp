@@ -50,22 +50,33 @@ __attribute__((target("avx2"))) inline void pack16(const uint16_t* src, uint8_t*
   _mm_storeu_si128(reinterpret_cast<__m128i*>(d + 12), _mm256_extracti128_si256(c, 1));
 }
 
-__attribute__((target("avx2"))) void pack_stream_avx2(const uint16_t* src, size_t n, uint8_t* dst) {
+// Packs and range-checks in the same pass (one read of the samples): returns false — dst then
+// holds garbage the caller must not use — when some sample needs more than 12 bits.
+__attribute__((target("avx2"))) bool pack_stream_avx2(const uint16_t* src, size_t n, uint8_t* dst) {
   constexpr size_t kChunk = 2048;  // samples per bounce (3 KiB packed: stays in L1)
   alignas(64) uint8_t bounce[kChunk / 2 * 3 + 32];
+  __m256i acc = _mm256_setzero_si256();
   for (size_t i = 0; i < n; i += kChunk) {
     const size_t m = n - i < kChunk ? n - i : kChunk;
-    for (size_t k = 0; k < m; k += 16) pack16(src + i + k, bounce + k / 2 * 3);
+    for (size_t k = 0; k < m; k += 16) {
+      acc = _mm256_or_si256(acc, _mm256_loadu_si256(reinterpret_cast<const __m256i*>(src + i + k)));
+      pack16(src + i + k, bounce + k / 2 * 3);
+    }
     dicom::stream_copy_unfenced(dst + i / 2 * 3, bounce, m / 2 * 3);
   }
   _mm_sfence();  // one fence for the whole slice
+  return _mm256_testz_si256(acc, _mm256_set1_epi16((short)0xF000));
 }
 
 }  // namespace
 
 bool fits12(const uint16_t* src, size_t n) { return n && !(n & 15) && available() && fits_avx2(src, n); }
 
-void pack_stream(const uint16_t* src, size_t n, uint8_t* dst) { pack_stream_avx2(src, n, dst); }
+void pack_stream(const uint16_t* src, size_t n, uint8_t* dst) { (void)pack_stream_avx2(src, n, dst); }
+
+bool pack_stream_checked(const uint16_t* src, size_t n, uint8_t* dst) {
+  return n && !(n & 15) && available() && pack_stream_avx2(src, n, dst);
+}
 
 bool available() {
   static const bool ok = __builtin_cpu_supports("avx2");

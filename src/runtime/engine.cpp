@@ -476,34 +476,46 @@ struct Engine::Impl {
       } else {
         const size_t npix = (size_t)h.rows * h.cols;
         // 12-bit transfer packing when every sample fits (staged or mapped raw 16-bit data),
-        // packed straight into the pinned blob (pack12::pack_stream).
+        // packed straight into the pinned blob in the same pass as the range check
+        // (pack12::pack_stream_checked). A slice with a wider sample (rare: MR data is 12-bit)
+        // leaves its packed reservation unused and takes a 16-bit one.
         const uint16_t* samples = pack12_ ? file.staged_samples() : nullptr;
-        const bool packed = samples && pack12::fits12(samples, npix);
-        const size_t alloc = packed ? align_up(npix / 4 * 3, 8) : align_up(npix, 8);  // u16 elements
-        size_t off, idx;
-        {
+        bool packed = samples && pack12::available() && (npix & 15) == 0;
+        auto reserve = [&](size_t len, size_t& idx) {
           std::lock_guard<std::mutex> g(s.alloc_m);
-          off = s.raw_used.load(std::memory_order_relaxed);
-          if (off + alloc > s.cap_pixels) throw SliceError("batch pixel capacity exceeded");
-          s.raw_used.store(off + alloc, std::memory_order_relaxed);
+          const size_t off = s.raw_used.load(std::memory_order_relaxed);
+          if (off + len > s.cap_pixels) throw SliceError("batch pixel capacity exceeded");
+          s.raw_used.store(off + len, std::memory_order_relaxed);
           idx = s.n_allocs++;
           s.allocs[idx].off = off;
-          s.allocs[idx].len = alloc;
+          s.allocs[idx].len = len;
           s.allocs[idx].done.store(false, std::memory_order_relaxed);
-        }
-        uint16_t* dst = reinterpret_cast<uint16_t*>(s.h_blob + s.raw_base) + off;
+          return off;
+        };
+        size_t idx = 0, off = 0;
+        uint16_t* dst = nullptr;
         try {
-          if (packed && pack_bounce_) {
-            pack12::pack_stream(samples, npix, reinterpret_cast<uint8_t*>(dst));
-          } else if (packed) {  // A/B: full-size intermediate, then one streaming copy
-            thread_local std::vector<uint8_t> pk;
-            if (pk.size() < npix / 2 * 3 + 64) pk.resize(npix / 2 * 3 + 64);
-            const size_t pb = pack12::pack(samples, npix, pk.data());
-            dicom::stream_copy(dst, pk.data(), pb);
-          } else
+          if (packed) {
+            off = reserve(align_up(npix / 4 * 3, 8), idx);
+            dst = reinterpret_cast<uint16_t*>(s.h_blob + s.raw_base) + off;
+            if (pack_bounce_) {
+              packed = pack12::pack_stream_checked(samples, npix, reinterpret_cast<uint8_t*>(dst));
+            } else {  // A/B: full-size intermediate, then one streaming copy
+              thread_local std::vector<uint8_t> pk;
+              if (pk.size() < npix / 2 * 3 + 64) pk.resize(npix / 2 * 3 + 64);
+              const size_t pb = pack12::pack(samples, npix, pk.data());
+              packed = pb != 0;
+              if (packed) dicom::stream_copy(dst, pk.data(), pb);
+            }
+            if (!packed) s.allocs[idx].done.store(true, std::memory_order_release);  // space stays unused
+          }
+          if (!packed) {
+            off = reserve(align_up(npix, 8), idx);
+            dst = reinterpret_cast<uint16_t*>(s.h_blob + s.raw_base) + off;
             file.pixels16(dst);
+          }
         } catch (...) {
-          s.allocs[idx].done.store(true, std::memory_order_release);  // space stays unused
+          if (dst) s.allocs[idx].done.store(true, std::memory_order_release);  // space stays unused
           throw;
         }
         s.allocs[idx].done.store(true, std::memory_order_release);

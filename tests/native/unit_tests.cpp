@@ -240,9 +240,19 @@ TEST(pack12_stream_exact_bytes) {
       CHECK(std::equal(ref.begin(), ref.begin() + n / 2 * 3, dst.begin() + mis));
       for (size_t k = 0; k < mis; ++k) CHECK(dst[k] == 0xAB);
       for (size_t k = mis + n / 2 * 3; k < dst.size(); ++k) CHECK(dst[k] == 0xAB);
+      std::vector<uint8_t> dc(n / 2 * 3 + 64, 0xAB);  // the checked single-pass form
+      CHECK(pack_stream_checked(px.data(), n, dc.data() + mis));
+      CHECK(std::equal(dst.begin(), dst.end(), dc.begin()));
     }
-    px[n / 2] = 0x1000;
-    CHECK(!fits12(px.data(), n));
+    std::vector<uint8_t> dc(n / 2 * 3 + 64);
+    for (size_t at : {(size_t)0, n / 2, n - 1}) {  // one wide sample anywhere fails the check
+      const uint16_t keep = px[at];
+      px[at] = 0x1000;
+      CHECK(!fits12(px.data(), n));
+      CHECK(!pack_stream_checked(px.data(), n, dc.data()));
+      px[at] = keep;
+    }
+    CHECK(!pack_stream_checked(px.data(), n - 8, dc.data()));  // not a multiple of 16: refused
   }
 }
 
