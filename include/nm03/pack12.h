@@ -5,8 +5,10 @@
 // upload engine is the step's bottleneck (ARCHITECTURE.md §6). When every sample of a slice fits in
 // 12 bits, the loader ships it as 12-bit pairs — 3 bytes per 2 samples, 25% fewer bytes on PCIe
 // and in host memory — and the GPU expands it back to the identical 16-bit words before the first
-// kernel (k0_unpack.hip). Slices with any sample ≥ 4096 are shipped unchanged. Lossless by
-// construction: the pipeline sees bit-identical input either way.
+// kernel (k0_unpack.hip). With BitsStored ≤ 12 the low 12 bits are the sample — every consumer
+// masks to the stored bits (key_from_raw) — so such slices are always packed; wider slices are
+// packed when every sample fits and otherwise shipped unchanged. Lossless by construction: every
+// stage sees the same keys either way.
 //
 // Layout: pair k = samples (2k, 2k+1) → 24-bit little-endian value s[2k] | s[2k+1] << 12 at byte 3k.
 #pragma once
@@ -27,7 +29,7 @@ size_t pack(const uint16_t* src, size_t n, uint8_t* dst);
 // True when n % 16 == 0, the packer is available and every sample fits in 12 bits.
 bool fits12(const uint16_t* src, size_t n);
 
-// Packs n samples that passed fits12() straight into dst — pinned upload memory — through an
+// Packs the low 12 bits of n samples (n % 16 == 0) straight into dst — pinned upload memory — through an
 // L1-sized bounce buffer and streaming stores: no full-size intermediate, and exactly n * 3 / 2
 // bytes are written (nothing past the end: neighbouring slices may be written concurrently).
 void pack_stream(const uint16_t* src, size_t n, uint8_t* dst);

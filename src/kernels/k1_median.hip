@@ -39,7 +39,7 @@ __device__ __forceinline__ void run_net(const uint32_t* P, int stride, int r, in
 }
 
 template <int K>
-__global__ __launch_bounds__(256) void median_kernel(const uint16_t* __restrict__ raw, uint16_t* __restrict__ med,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K <= 7 ? 4 : 2))) void median_kernel(const uint16_t* __restrict__ raw, uint16_t* __restrict__ med,
                                                      const SliceDesc* __restrict__ descs,
                                                      const TileDesc* __restrict__ tiles, SliceStats* stats,
                                                      uint32_t* __restrict__ tile_mm, int dbg,
@@ -75,56 +75,72 @@ __global__ __launch_bounds__(256) void median_kernel(const uint16_t* __restrict_
   if ((W & 3) == 0 && (d.raw_off & 3) == 0 && (!from_blob || packed || (d.blob_off & 3) == 0)) {
     // Vector path: window pixels p = 0..71 are image columns x0-4+p (8-byte aligned groups of
     // 4). Pair column c holds window pixels c+4-R (low half) and c+36-R (high half), so a task
-    // (row, group gi < 10) loads groups gi and gi+8 — one 8-byte load each, per-pixel clamped
-    // loads only where a group leaves the image — and writes up to 4 pair words.
-    for (int i = threadIdx.x; i < PR * 10; i += 256) {
+    // (row, group gi < 10) takes groups gi and gi+8 and writes up to 4 pair words. W % 4 == 0 and
+    // xs ≡ x0 (mod 4), so a group is wholly inside the image or wholly outside — then every pixel
+    // clamps to one edge pixel, which the clamped edge group holds: one 8-byte (or, 12-bit packed,
+    // two dword) load per group and no per-pixel path. All of a thread's loads are issued first
+    // (phase A), then decoded (phase B): every wave of the launch is loading at the same time, so
+    // load → use chains would expose the memory latency once per task.
+    constexpr int NT = (PR * 10 + 255) / 256;  // tasks per thread
+    uint2 ld[NT][2];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int i = threadIdx.x + 256 * t;
+      if (i >= PR * 10) break;
+      const int r = i / 10, gi = i - r * 10;
+      const int y = clampi(y0 - R + r, 0, H - 1);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int xs = clampi(x0 - 4 + 4 * (gi + 8 * h), 0, W - 4);
+        if (packed) {
+          // 4 samples = 48 bits at byte o = 1.5·p (p = y·W + xs ≡ 0 mod 4, so o is even): two
+          // aligned dword loads from o & ~3 cover them (the device blob has tail slack for the
+          // 2 bytes this can read past a slice that ends the blob).
+          const size_t o = ((size_t)y * W + xs) * 3 >> 1;
+          ld[t][h] = *reinterpret_cast<const uint2*>(pb + (o & ~(size_t)3));
+        } else {
+          ld[t][h] = *reinterpret_cast<const uint2*>(src + (size_t)y * W + xs);
+        }
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int i = threadIdx.x + 256 * t;
+      if (i >= PR * 10) break;
       const int r = i / 10, gi = i - r * 10;
       const int yy = y0 - R + r;
       const int y = clampi(yy, 0, H - 1);
-      const uint16_t* row = src + (size_t)y * W;
       const bool row_in = rdst && yy >= y0 && yy < yin_hi;
-      auto group = [&](int g4, uint16_t* px, bool store) {
+      uint16_t px[2][4];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int g4 = gi + 8 * h;
         const int xs = x0 - 4 + 4 * g4;
-        if (xs >= 0 && xs + 4 <= W) {
-          uint2 v;
-          if (packed) {
-            // 4 samples = 48 bits at byte o = 1.5·p (p = y·W + xs ≡ 0 mod 4, so o is even): two
-            // aligned dword loads from o & ~3 cover them (the device blob has tail slack for the
-            // 2 bytes this can read past a slice that ends the blob).
-            const size_t o = ((size_t)y * W + xs) * 3 >> 1;
-            const uint32_t* q = reinterpret_cast<const uint32_t*>(pb + (o & ~(size_t)3));
-            const uint64_t b = ((uint64_t)q[0] | ((uint64_t)q[1] << 32)) >> ((o & 2) * 8);
-            v.x = ((uint32_t)b & 0xFFFu) | (((uint32_t)(b >> 12) & 0xFFFu) << 16);
-            v.y = ((uint32_t)(b >> 24) & 0xFFFu) | (((uint32_t)(b >> 36) & 0xFFFu) << 16);
-          } else {
-            v = *reinterpret_cast<const uint2*>(row + xs);
-          }
-          px[0] = (uint16_t)v.x;
-          px[1] = (uint16_t)(v.x >> 16);
-          px[2] = (uint16_t)v.y;
-          px[3] = (uint16_t)(v.y >> 16);
-          if (store && row_in && xs >= x0 && xs < xin_hi)
-            *reinterpret_cast<uint2*>(rdst + (size_t)yy * W + xs) = v;
-        } else {
-#pragma unroll
-          for (int q = 0; q < 4; ++q) px[q] = sample(y, clampi(xs + q, 0, W - 1));
-          if (store && row_in) {
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-              if (xs + q >= x0 && xs + q < xin_hi) rdst[(size_t)yy * W + xs + q] = px[q];
-          }
+        uint2 v = ld[t][h];
+        if (packed) {
+          const size_t o = ((size_t)y * W + clampi(xs, 0, W - 4)) * 3 >> 1;
+          const uint64_t b = ((uint64_t)v.x | ((uint64_t)v.y << 32)) >> ((o & 2) * 8);
+          v.x = ((uint32_t)b & 0xFFFu) | (((uint32_t)(b >> 12) & 0xFFFu) << 16);
+          v.y = ((uint32_t)(b >> 24) & 0xFFFu) | (((uint32_t)(b >> 36) & 0xFFFu) << 16);
         }
-      };
-      uint16_t lo[4], hi[4];
-      // Groups 8 and 9 are loaded twice (as lo and as hi): only the lo load stores them.
-      group(gi, lo, gi >= 1);
-      group(gi + 8, hi, gi + 8 >= 10 && gi + 8 <= 16);
+        px[h][0] = (uint16_t)v.x;
+        px[h][1] = (uint16_t)(v.x >> 16);
+        px[h][2] = (uint16_t)v.y;
+        px[h][3] = (uint16_t)(v.y >> 16);
+        if (xs < 0) px[h][1] = px[h][2] = px[h][3] = px[h][0];
+        if (xs >= W) px[h][0] = px[h][1] = px[h][2] = px[h][3];
+        // Expanded-sample side output: groups 8 and 9 are taken twice (as lo and as hi); only the
+        // lo copy stores them.
+        const bool store = h == 0 ? gi >= 1 : (g4 >= 10 && g4 <= 16);
+        if (store && row_in && xs >= x0 && xs < xin_hi)
+          *reinterpret_cast<uint2*>(rdst + (size_t)yy * W + xs) = v;
+      }
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int c = 4 * gi + q - (4 - R);
         if (c < 0 || c >= PW) continue;
-        const uint32_t kl = key_from_raw(lo[q], d.type, d.stored_bits);
-        const uint32_t kh = key_from_raw(hi[q], d.type, d.stored_bits);
+        const uint32_t kl = key_from_raw(px[0][q], d.type, d.stored_bits);
+        const uint32_t kh = key_from_raw(px[1][q], d.type, d.stored_bits);
         P[r * PS + c] = kl | (kh << 16);
         kmin = min(kmin, min(kl, kh));
         kmax = max(kmax, max(kl, kh));

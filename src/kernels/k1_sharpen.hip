@@ -7,10 +7,11 @@
 //  1. the clamp-to-edge (64+2R)² input tile is loaded in 8-byte groups of 4 median keys
 //     (per-key clamped loads only where a group leaves the image), normalised+clipped once per
 //     key and kept in LDS as f32;
-//  2. vertical pass: a thread owns a column × 16 rows and slides a (16+2R)-value window held in
-//     registers (each LDS value read once instead of 2R+1 times);
-//  3. horizontal pass + combine + band: a thread owns 16 columns of a row (register window
-//     again); the band bits of the four 16-column segments form the row's 64-bit mask word.
+//  2. vertical pass: a thread owns a column pair × 16 rows and slides a (16+2R)-value window of
+//     pairs held in registers (each LDS value read once instead of 2R+1 times);
+//  3. horizontal pass + combine + band: a thread owns 16 columns of a row (register window of
+//     overlapping pairs); the band bits of the four 16-column segments form the row's mask word.
+// Both passes compute two outputs per packed f32 instruction.
 // The Gaussian is applied separably in the contract order of golden::sharpen (vertical, then
 // horizontal, taps ascending, no FMA contraction), so the result is bit-identical to the CPU
 // golden model.
@@ -24,6 +25,12 @@
 namespace nm03::gpu {
 
 constexpr int kMaxR = 7;
+
+// Two adjacent f32 in one register pair: the stencil passes run on packed f32 (v_pk_mul_f32 /
+// v_pk_add_f32, per-lane IEEE rounding, so results are those of the scalar ops). The LDS row
+// stride is odd, so a pair is read with ds_read2_b32 (4-byte alignment) rather than a b64 load.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2 lds_pair(const float* p) { return f32x2{p[0], p[1]}; }
 static_assert(kShpTileW == 64 && kShpTileH == 64, "sharpen tile is 64x64");
 
 template <int R>
@@ -73,23 +80,32 @@ __global__ __launch_bounds__(256) void sharpen_band_kernel(const uint16_t* __res
 
   // ---- 1. input tile → normalised+clipped f32 in LDS ------------------------------------------
   if ((W & 3) == 0 && (d.raw_off & 3) == 0) {
-    // Window columns x0 - 4·RA + 4g + q; tile column c = 4g + q - (4·RA - R).
-    for (int i = threadIdx.x; i < CH * G; i += 256) {
+    // Window columns x0 - 4·RA + 4g + q; tile column c = 4g + q - (4·RA - R). All of a thread's
+    // loads are issued before any is consumed: every wave of the launch is in this phase at the
+    // same time, so a load → use → load chain would expose the memory latency once per task.
+    constexpr int NT = (CH * G + 255) / 256;  // tasks per thread
+    uint2 v[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int i = threadIdx.x + 256 * t;
+      if (i >= CH * G) break;
       const int r = i / G, g = i - r * G;
       const int y = clampi(y0 - R + r, 0, H - 1);
       const uint16_t* row = src + (size_t)y * W;
+      // W % 4 == 0 and xs ≡ x0 (mod 4): a group is wholly inside or wholly outside the image, and
+      // an outside group clamps to one edge pixel — loaded with the edge group (no scalar path).
       const int xs = x0 - 4 * RA + 4 * g;
-      uint16_t px[4];
-      if (xs >= 0 && xs + 4 <= W) {
-        const uint2 v = *reinterpret_cast<const uint2*>(row + xs);
-        px[0] = (uint16_t)v.x;
-        px[1] = (uint16_t)(v.x >> 16);
-        px[2] = (uint16_t)v.y;
-        px[3] = (uint16_t)(v.y >> 16);
-      } else {
+      v[t] = *reinterpret_cast<const uint2*>(row + clampi(xs, 0, W - 4));
+    }
 #pragma unroll
-        for (int q = 0; q < 4; ++q) px[q] = row[clampi(xs + q, 0, W - 1)];
-      }
+    for (int t = 0; t < NT; ++t) {
+      const int i = threadIdx.x + 256 * t;
+      if (i >= CH * G) break;
+      const int r = i / G, g = i - r * G;
+      const int xs = x0 - 4 * RA + 4 * g;
+      uint16_t px[4] = {(uint16_t)v[t].x, (uint16_t)(v[t].x >> 16), (uint16_t)v[t].y, (uint16_t)(v[t].y >> 16)};
+      if (xs < 0) px[1] = px[2] = px[3] = px[0];
+      if (xs >= W) px[0] = px[1] = px[2] = px[3];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int c = 4 * g + q - (4 * RA - R);
@@ -105,56 +121,66 @@ __global__ __launch_bounds__(256) void sharpen_band_kernel(const uint16_t* __res
   }
   __syncthreads();
 
-  // ---- 2. vertical pass: column c, rows [RB·rb, RB·rb + RB) from a register window -----------
-  for (int task = threadIdx.x; task < CW * (TH / RB); task += 256) {
-    const int rb = task / CW, c = task - rb * CW;
-    float win[RB + 2 * R];
+  // ---- 2. vertical pass: columns (c, c+1), rows [RB·rb, RB·rb + RB) from a register window of
+  //         column pairs; every tap is one v_pk_mul_f32 + one v_pk_add_f32 for two outputs --------
+  constexpr int CP = CW / 2;  // CW = 64 + 2R is even
+  for (int task = threadIdx.x; task < CP * (TH / RB); task += 256) {
+    const int rb = task / CP, c = 2 * (task - rb * CP);
+    f32x2 win[RB + 2 * R];
 #pragma unroll
-    for (int k = 0; k < RB + 2 * R; ++k) win[k] = C[(rb * RB + k) * CS + c];
+    for (int k = 0; k < RB + 2 * R; ++k) win[k] = lds_pair(C + (rb * RB + k) * CS + c);
 #pragma unroll
     for (int rr = 0; rr < RB; ++rr) {
-      float acc = 0.0f;
+      f32x2 acc = 0.0f;
 #pragma unroll
       for (int k = 0; k <= 2 * R; ++k) {
-        const float p = pc.taps[k] * win[rr + k];
+        const f32x2 p = pc.taps[k] * win[rr + k];
         acc = acc + p;
       }
-      T[(rb * RB + rr) * CS + c] = acc;
+      T[(rb * RB + rr) * CS + c] = acc.x;
+      T[(rb * RB + rr) * CS + c + 1] = acc.y;
     }
   }
   __syncthreads();
 
   // ---- 3. horizontal pass + combine + band: a thread owns row r, columns [16·seg, 16·seg + 16)
-  //         and slides a (16+2R)-value register window; band bits go through LDS to form the
-  //         64-bit row words. Wave = segment, lane = row: a half-wave reads 32 rows at the odd
-  //         stride CS, i.e. 32 distinct banks (row-major lanes put segments 0/2 and 1/3 of a row
-  //         on one bank: 2-way conflicts on every read).
+  //         and keeps the overlapping column pairs (a, a+1) of its (16+2R)-value window in
+  //         registers, so output pairs (j, j+1) take packed f32 ops as in the vertical pass; band
+  //         bits go through LDS to form the 64-bit row words. Wave = segment, lane = row: a
+  //         half-wave reads 32 rows at the odd stride CS, i.e. 32 distinct banks.
   __shared__ uint16_t bm[4 * TH];
   const int r = threadIdx.x & (TH - 1), seg = threadIdx.x / TH;
   const int y = y0 + r;
   float smin = INFINITY, smax = -INFINITY;
   {
-    float win[16 + 2 * R];
+    f32x2 pw[16 + 2 * R - 1];
 #pragma unroll
-    for (int k = 0; k < 16 + 2 * R; ++k) win[k] = T[r * CS + 16 * seg + k];
+    for (int a = 0; a < 16 + 2 * R - 1; ++a) pw[a] = lds_pair(T + r * CS + 16 * seg + a);
     uint32_t bits = 0;
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      float acc = 0.0f;
+    for (int j = 0; j < 16; j += 2) {
+      f32x2 acc = 0.0f;
 #pragma unroll
       for (int k = 0; k <= 2 * R; ++k) {
-        const float p = pc.taps[k] * win[j + k];
+        const f32x2 p = pc.taps[k] * pw[j + k];
         acc = acc + p;
       }
-      const int xj = x0 + 16 * seg + j;
-      const float cv = C[(r + R) * CS + 16 * seg + j + R];
-      const float sv = sharpen_combine(cv, acc, pc.gain);
-      const bool inside = xj < W && y < H;
-      bits |= (inside && in_band(sv, pc.band_lo, pc.band_hi)) ? (1u << j) : 0u;
-      if (sharpened && inside) {
-        sharpened[d.f32_off + (size_t)y * W + xj] = sv;
-        smin = fminf(smin, sv);
-        smax = fmaxf(smax, sv);
+      // sharpen_combine (pixel_math.h) on both lanes: s = c + gain·(c − b), same rounding steps.
+      const f32x2 cv = lds_pair(C + (r + R) * CS + 16 * seg + j + R);
+      const f32x2 dd = cv - acc;
+      const f32x2 gg = pc.gain * dd;
+      const f32x2 sv = cv + gg;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const float v = h ? sv.y : sv.x;
+        const int xj = x0 + 16 * seg + j + h;
+        const bool inside = xj < W && y < H;
+        bits |= (inside && in_band(v, pc.band_lo, pc.band_hi)) ? (1u << (j + h)) : 0u;
+        if (sharpened && inside) {
+          sharpened[d.f32_off + (size_t)y * W + xj] = v;
+          smin = fminf(smin, v);
+          smax = fmaxf(smax, v);
+        }
       }
     }
     bm[seg * TH + r] = (uint16_t)bits;

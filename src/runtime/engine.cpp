@@ -75,7 +75,11 @@ struct Slot {
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
   int cap_slices = 0, cap_canvases = 0;
-  size_t cap_pixels = 0;  // u16 elements in the raw region
+  size_t cap_pixels = 0;  // u16 elements of expanded samples per batch (device raw/median buffers)
+  // The blob's raw region also holds `hole_slack` u16 of slack for abandoned 12-bit reservations
+  // (a checked single-pass pack that found a wide sample, see load_one); `hole_credit` is what is
+  // left of it in the current batch (under alloc_m).
+  size_t hole_slack = 0, hole_credit = 0;
   // blob layout (byte offsets)
   size_t off_stats = 0, off_desc = 0, off_medt = 0, off_shpt = 0, off_seeds = 0, off_render = 0, off_jpeg = 0,
          raw_base = 0, blob_bytes = 0;
@@ -309,7 +313,8 @@ struct Engine::Impl {
     s.off_jpeg = o;
     o = align_up(o + (size_t)s.cap_canvases * sizeof(JpegDesc), kAlign);
     s.raw_base = o;
-    s.blob_bytes = o + s.cap_pixels * sizeof(uint16_t);
+    s.hole_slack = (size_t)std::max(cfg.threads, 1) * align_up((size_t)md * md / 4 * 3, 8);
+    s.blob_bytes = o + (s.cap_pixels + s.hole_slack) * sizeof(uint16_t);
     try {
       if (read_mode_ == dicom::ReadMode::kMapped) {
         s.map_stride = align_up((size_t)md * md * 2 + (1u << 20), 1u << 21);  // pixels + 1 MiB of header room
@@ -475,47 +480,79 @@ struct Engine::Impl {
                      " exceed the engine limit " + std::to_string(cfg.max_dim);
       } else {
         const size_t npix = (size_t)h.rows * h.cols;
-        // 12-bit transfer packing when every sample fits (staged or mapped raw 16-bit data),
-        // packed straight into the pinned blob in the same pass as the range check
-        // (pack12::pack_stream_checked). A slice with a wider sample (rare: MR data is 12-bit)
-        // leaves its packed reservation unused and takes a 16-bit one.
+        // 12-bit transfer packing (staged or mapped raw 16-bit data), written straight into the
+        // pinned blob with streaming stores:
+        //  * BitsStored ≤ 12: every consumer masks samples to the stored bits (key_from_raw), so the
+        //    low 12 bits are the slice — packed unconditionally, one pass;
+        //  * wider: packed and range-checked in the same pass (pack_stream_checked) under a hole
+        //    credit — if a sample needs more bits, the packed reservation is grown in place to the
+        //    16-bit size when it is still the last one, or else abandoned (a hole, paid from the
+        //    credit) for a new 16-bit one. Without credit left: range check first (fits12), then
+        //    pack — two passes, no hole.
         const uint16_t* samples = pack12_ ? file.staged_samples() : nullptr;
-        bool packed = samples && pack12::available() && (npix & 15) == 0;
-        auto reserve = [&](size_t len, size_t& idx) {
-          std::lock_guard<std::mutex> g(s.alloc_m);
-          const size_t off = s.raw_used.load(std::memory_order_relaxed);
-          if (off + len > s.cap_pixels) throw SliceError("batch pixel capacity exceeded");
-          s.raw_used.store(off + len, std::memory_order_relaxed);
+        const size_t plen = align_up(npix / 4 * 3, 8), ulen = align_up(npix, 8);  // u16 elements
+        const bool packable = samples && pack12::available() && (npix & 15) == 0;
+        const size_t cap = s.cap_pixels + s.hole_slack;
+        size_t idx = 0, off = 0;
+        bool packed = false, reserved = false, credit = false;
+        auto reserve_locked = [&](size_t len) {
+          const size_t o = s.raw_used.load(std::memory_order_relaxed);
+          if (o + len > cap) throw SliceError("batch pixel capacity exceeded");
+          s.raw_used.store(o + len, std::memory_order_relaxed);
           idx = s.n_allocs++;
-          s.allocs[idx].off = off;
+          s.allocs[idx].off = o;
           s.allocs[idx].len = len;
           s.allocs[idx].done.store(false, std::memory_order_relaxed);
-          return off;
+          off = o;
+          reserved = true;
         };
-        size_t idx = 0, off = 0;
-        uint16_t* dst = nullptr;
         try {
-          if (packed) {
-            off = reserve(align_up(npix / 4 * 3, 8), idx);
-            dst = reinterpret_cast<uint16_t*>(s.h_blob + s.raw_base) + off;
-            if (pack_bounce_) {
-              packed = pack12::pack_stream_checked(samples, npix, reinterpret_cast<uint8_t*>(dst));
-            } else {  // A/B: full-size intermediate, then one streaming copy
+          const bool low12 = h.bits_stored <= 12;
+          if (packable && !low12) {
+            std::lock_guard<std::mutex> g(s.alloc_m);
+            credit = pack_bounce_ && s.hole_credit >= plen;
+            if (credit) {
+              s.hole_credit -= plen;
+              reserve_locked(plen);
+            }
+          }
+          if (credit) {
+            uint8_t* dst = reinterpret_cast<uint8_t*>(reinterpret_cast<uint16_t*>(s.h_blob + s.raw_base) + off);
+            packed = pack12::pack_stream_checked(samples, npix, dst);
+            {
+              std::lock_guard<std::mutex> g(s.alloc_m);
+              if (packed) {
+                s.hole_credit += plen;
+              } else if (s.raw_used.load(std::memory_order_relaxed) == off + plen && off + ulen <= cap) {
+                s.raw_used.store(off + ulen, std::memory_order_relaxed);  // grow in place
+                s.allocs[idx].len = ulen;
+                s.hole_credit += plen;
+              } else {
+                s.allocs[idx].done.store(true, std::memory_order_release);  // a hole: uploaded, unused
+                reserve_locked(ulen);
+              }
+            }
+            if (!packed) file.pixels16(reinterpret_cast<uint16_t*>(s.h_blob + s.raw_base) + off);
+          } else {
+            packed = packable && (low12 || pack12::fits12(samples, npix));
+            {
+              std::lock_guard<std::mutex> g(s.alloc_m);
+              reserve_locked(packed ? plen : ulen);
+            }
+            uint16_t* dst = reinterpret_cast<uint16_t*>(s.h_blob + s.raw_base) + off;
+            if (packed && pack_bounce_) {
+              pack12::pack_stream(samples, npix, reinterpret_cast<uint8_t*>(dst));
+            } else if (packed) {  // A/B: full-size intermediate, then one streaming copy
               thread_local std::vector<uint8_t> pk;
               if (pk.size() < npix / 2 * 3 + 64) pk.resize(npix / 2 * 3 + 64);
-              const size_t pb = pack12::pack(samples, npix, pk.data());
-              packed = pb != 0;
-              if (packed) dicom::stream_copy(dst, pk.data(), pb);
+              pack12::pack_stream(samples, npix, pk.data());
+              dicom::stream_copy(dst, pk.data(), npix / 2 * 3);
+            } else {
+              file.pixels16(dst);
             }
-            if (!packed) s.allocs[idx].done.store(true, std::memory_order_release);  // space stays unused
-          }
-          if (!packed) {
-            off = reserve(align_up(npix, 8), idx);
-            dst = reinterpret_cast<uint16_t*>(s.h_blob + s.raw_base) + off;
-            file.pixels16(dst);
           }
         } catch (...) {
-          if (dst) s.allocs[idx].done.store(true, std::memory_order_release);  // space stays unused
+          if (reserved) s.allocs[idx].done.store(true, std::memory_order_release);  // space stays unused
           throw;
         }
         s.allocs[idx].done.store(true, std::memory_order_release);
@@ -781,8 +818,9 @@ struct Engine::Impl {
                      std::mutex& acc_m, const std::function<void(size_t)>& on_start) {
     s.raw_used = 0;
     s.loaded.assign(count, LoadedSlice{});
-    if (!s.allocs) s.allocs.reset(new Slot::Alloc[s.cap_slices]);
+    if (!s.allocs) s.allocs.reset(new Slot::Alloc[2 * (size_t)s.cap_slices]);  // ≤ 2 per slice (a hole)
     s.n_allocs = 0;
+    s.hole_credit = s.hole_slack;
     s.uploaded = 0;
     s.upload_started = false;
     {

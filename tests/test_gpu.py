@@ -368,6 +368,47 @@ def test_engine_pack12_identical(native, cohort_root, tmp_path, monkeypatch):
     assert runs[0][1] == runs[1][1]
 
 
+def test_engine_pack12_holes_and_stored_bits(native, cohort_root, tmp_path, monkeypatch):
+    """Loader packing paths (engine.cpp load_one) vs no packing: wide 16-bit slices interleaved with
+    fitting ones in the same batches (the checked single-pass pack then grows its reservation in
+    place or abandons it as a hole), BitsStored = 12 slices whose high 4 bits hold garbage (packed
+    unconditionally: every consumer masks to the stored bits), a signed 12-bit slice, and a batch
+    with more wide slices than loader threads. Same statuses, byte-identical JPEGs."""
+    d = tmp_path / "mixed"
+    d.mkdir()
+    rng = np.random.default_rng(7)
+    files = []
+    for k in range(12):
+        base = native.phantom_slice(256, 256, 4, 11, 25, 9 + k).astype(np.uint32)
+        if k % 3 == 0:  # wide: one sample (anywhere) above 12 bits
+            px = base.copy()
+            px.flat[int(rng.integers(0, px.size))] = 4096 + k
+            blob = native.dicom_bytes(np.minimum(px, 65535).astype(np.uint16))
+        elif k % 3 == 1:  # BitsStored 12, garbage in the high nibble
+            px = (base & 0xFFF) | (rng.integers(0, 16, size=base.shape, dtype=np.uint32) << 12)
+            blob = native.dicom_bytes(px.astype(np.uint16), "u16", 12)
+        else:  # signed 12-bit, sign-extended words
+            v = (base.astype(np.int32) % 4096) - 2048
+            blob = native.dicom_bytes((v & 0xFFFF).astype(np.uint16), "i16", 12)
+        f = d / f"1-{k + 1}.dcm"
+        f.write_bytes(blob)
+        files.append(f)
+    runs = []
+    for i, flag in enumerate(["0", "1"]):
+        out = str(tmp_path / f"o{i}")
+        items = _items(native, cohort_root, out)[:12]
+        os.makedirs(os.path.join(out, "mixed"), exist_ok=True)
+        extra = [(str(f), os.path.join(out, "mixed")) for f in files]
+        items = [x for pair in zip(items, extra) for x in pair]
+        monkeypatch.setenv("NM03_PACK12", flag)
+        eng = native.Engine(nm.PipelineConfig(batch_size=16, streams=2, threads=8).engine_config())
+        st, _ = eng.run(items)
+        del eng
+        runs.append(([c for c, _ in st], _tree(out)))
+    assert runs[0][0] == runs[1][0] and runs[0][0].count(0) == len(runs[0][0])
+    assert runs[0][1] == runs[1][1]
+
+
 def test_engine_fused_unpack_identical(native, cohort_root, tmp_path, monkeypatch):
     """Upload expansion inside the median's tile load (default) vs the standalone K0 pass
     (NM03_SEPARATE_UNPACK=1), with 12-bit packing on: byte-identical JPEGs on batches mixing packed

@@ -198,6 +198,34 @@ def live_ops(net, outs):
     return ops, ins
 
 
+def demand_order(net, outs):
+    """Post-order DFS from the outputs in output order: every value (input load included) is
+    produced just before its first consumer, so the live set stays near the sorted columns the
+    remaining outputs still need — instead of creation order, which loads every input and sorts
+    every column before the first horizontal merge (peak ≈ all inputs live; the k=7 kernel needed
+    139 VGPRs = 3 waves/SIMD)."""
+    order, seen = [], set()
+    for _, root in sorted(outs.items()):
+        if not isinstance(root, int) or root in seen:
+            continue
+        stack = [(root, False)]
+        while stack:
+            x, done = stack.pop()
+            if done:
+                order.append(x)
+                continue
+            if x in seen:
+                continue
+            seen.add(x)
+            stack.append((x, True))
+            n = net.nodes[x]
+            if n[0] != "in":
+                for y in (n[2], n[1]):
+                    if isinstance(y, int) and y not in seen:
+                        stack.append((y, False))
+    return order
+
+
 def emit(k, TW, TH, f):
     net, outs = build(k, TW, TH)
     ops, ins = live_ops(net, outs)
@@ -208,12 +236,13 @@ def emit(k, TW, TH, f):
     f.write("template <class V, class LD>\n")
     f.write(f"NM03_HD void {name}(const LD& ld, V* out) {{\n")
     var = {}
-    for x in ins:
-        _, r, c = net.nodes[x]
-        var[x] = f"i{r}_{c}"
-        f.write(f"  const V {var[x]} = ld({r}, {c});\n")
-    for x in ops:
-        op, a, b = net.nodes[x]
+    for x in demand_order(net, outs):
+        n = net.nodes[x]
+        if n[0] == "in":
+            var[x] = f"i{n[1]}_{n[2]}"
+            f.write(f"  const V {var[x]} = ld({n[1]}, {n[2]});\n")
+            continue
+        op, a, b = n
         var[x] = f"t{x}"
         fn = "vmin" if op == "min" else "vmax"
         f.write(f"  const V {var[x]} = {fn}({var[a]}, {var[b]});\n")
