@@ -548,7 +548,9 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(4))) vo
     // ---- 6. own 0xFF count, inclusive record ---------------------------------------------------
     const uint32_t al = p_start & 7u, f = (8u - al) & 7u;
     const bool last = part == parts - 1;
-    uint32_t own = ff[al], nown = 0;
+    uint32_t own = 0, nown = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) own = al == (uint32_t)k ? ff[k] : own;  // select: ff stays in VGPRs (no scratch)
     bool strad = false, fin = false;
     uint32_t strad_v = 0, fin_v = 0;
     if (al) {  // the byte shared with the previous workgroup
