@@ -7,5 +7,5 @@
 
 int main(int argc, char** argv) {
   nm03::app::AppConfig cfg = nm03::app::parse_args(argc, argv, "img_processing_parallel");
-  return nm03::app::run_parallel(cfg);
+  return nm03::app::cli_exit(nm03::app::run_parallel(cfg));
 }

@@ -6,5 +6,5 @@
 
 int main(int argc, char** argv) {
   nm03::app::AppConfig cfg = nm03::app::parse_args(argc, argv, "test_pipeline");
-  return nm03::app::run_test_pipeline(cfg);
+  return nm03::app::cli_exit(nm03::app::run_test_pipeline(cfg));
 }

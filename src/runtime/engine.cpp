@@ -267,22 +267,42 @@ struct Engine::Impl {
     jpeg_header = jpeg::make_header(cfg.render.out_width, cfg.render.out_height, t);
     if (cfg.render.out_width % 16 || cfg.render.out_height % 16)
       throw DeviceError("canvas size must be a multiple of 16");
+    const double t0 = now_s();
     check_hip(hipSetDevice(cfg.device), "hipSetDevice");
+    const double t1 = now_s();
     // Host threads and pinned buffers on the GPU's socket (numa.h).
     pool = std::make_unique<ThreadPool>(cfg.threads, [this] { place.bind_this_thread(); });
+    const double t2 = now_s();
+    // Slot 0 is built here (its failure fails the constructor); the others are built by their own
+    // worker threads while slot 0 already runs batches — a slot costs ≈11–18 ms of pinned and
+    // device allocations and stream creation, the first one more (runtime queues), which a cold
+    // CLI run would otherwise wait for in full. NM03_EAGER_SLOTS=1 builds them all here.
+    const char* eager_env = std::getenv("NM03_EAGER_SLOTS");
+    const bool eager = eager_env && *eager_env == '1';
+    std::string slot_ms;
+    slots.resize((size_t)cfg.streams);
     place.run_bound([&] {
-      for (int i = 0; i < cfg.streams; ++i) slots.push_back(make_slot());
+      for (int i = 0; i < (eager ? cfg.streams : 1); ++i) {
+        const double ts = now_s();
+        slots[(size_t)i] = make_slot();
+        slot_ms += (i ? "/" : "") + std::to_string((int)((now_s() - ts) * 1e4) / 10.0).substr(0, 5);
+      }
     });
+    const double t3 = now_s();
     start_workers();
+    const double t4 = now_s();
     log_info("engine on device " + std::to_string(cfg.device) + ": batch " + std::to_string(cfg.batch_size) + ", " +
              std::to_string(cfg.streams) + " streams, " + std::to_string(cfg.threads) + " host threads, max_dim " +
-             std::to_string(cfg.max_dim) + ", " + place.describe());
+             std::to_string(cfg.max_dim) + ", " + place.describe() + "; set-up ms: device " +
+             std::to_string((t1 - t0) * 1e3) + ", pool " + std::to_string((t2 - t1) * 1e3) + ", slots " + slot_ms +
+             ", workers " + std::to_string((t4 - t3) * 1e3));
   }
 
   ~Impl() {
     stop_workers();
     (void)hipSetDevice(cfg.device);
-    for (auto& s : slots) hip_free_all(*s);
+    for (auto& s : slots)
+      if (s) hip_free_all(*s);
   }
 
   std::unique_ptr<Slot> make_slot() {
@@ -1004,7 +1024,7 @@ struct Engine::Impl {
   bool quit = false;
 
   void start_workers() {
-    for (auto& sp : slots) workers.emplace_back([this, s = sp.get()] { worker(s); });
+    for (size_t i = 0; i < slots.size(); ++i) workers.emplace_back([this, i] { worker(i); });
   }
   void stop_workers() {
     {
@@ -1031,10 +1051,19 @@ struct Engine::Impl {
     done_cv.notify_all();
   }
 
-  void worker(Slot* s) {
+  void worker(size_t slot_index) {
     place.bind_this_thread();
     (void)prctl(PR_SET_TIMERSLACK, 1000UL, 0, 0, 0);  // 1 µs: short poll sleeps stay short
     (void)hipSetDevice(cfg.device);
+    if (!slots[slot_index]) {  // built lazily (see the constructor); this thread is its only user
+      try {
+        slots[slot_index] = make_slot();
+      } catch (const std::exception& e) {
+        log_warn("engine slot " + std::to_string(slot_index) + " unavailable, running with fewer streams: " + e.what());
+        return;
+      }
+    }
+    Slot* s = slots[slot_index].get();
     for (;;) {
       std::shared_ptr<Job> j;
       size_t b;
