@@ -1,6 +1,7 @@
 """CLIs on CPU: test_pipeline --cpu (BASELINE config 1, golden plumbing) and argument handling."""
 import io
 import os
+import re
 
 import numpy as np
 import pytest
@@ -105,3 +106,26 @@ def test_volume_cli_cpu_golden(native, cohort_root, tmp_path):
     r = run_bin("img_processing_parallel", "--mode", "3d", "--cpu", "--dilation-size", "3", "--data-root", cohort_root,
                 "--out", str(tmp_path / "o3"), "--json", str(js))
     assert r.returncode == 0 and json.load(open(js))["dilation_size"] == 3
+
+
+@pytest.mark.parametrize("cli,args", [
+    ("test_pipeline", ["--cpu"]),
+    ("img_processing_parallel", ["--mode", "3d", "--cpu"]),
+    ("test_pipeline", ["--cpu", "--input", "/nonexistent/slice.dcm"]),
+])
+def test_fast_exit_same_output(native, cohort_root, tmp_path, cli, args):
+    """The CLIs end with cli_exit (flush, then _exit without teardown): stdout, stderr, exit code and
+    the output tree are the same as with the normal return (NM03_FAST_EXIT=0), also on failure."""
+    res = []
+    for fx in ("1", "0"):
+        out = tmp_path / f"o{fx}"
+        r = run_bin(cli, *args, "--data-root", cohort_root, "--out", str(out), env={"NM03_FAST_EXIT": fx})
+        tree = {}
+        if out.exists():
+            for p in sorted(out.rglob("*")):
+                if p.is_file():
+                    tree[str(p.relative_to(out))] = p.read_bytes()
+        norm = lambda t: re.sub(r"\d+(\.\d+)? (ms|s)\b", "T", t.replace(str(out), "OUT"))  # timings
+        res.append((r.returncode, norm(r.stdout), norm(r.stderr), tree))
+    assert res[0] == res[1]
+    assert res[0][1] or res[0][2]  # something was printed and survived the fast exit
