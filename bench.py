@@ -123,6 +123,22 @@ def _free_port():
         return s.getsockname()[1]
 
 
+def thread_cpu_by_name():
+    """CPU seconds (user + system) of this process's live threads, summed per thread name."""
+    tick = os.sysconf("SC_CLK_TCK")
+    out = {}
+    for tid in os.listdir("/proc/self/task"):
+        try:
+            with open(f"/proc/self/task/{tid}/stat") as f:
+                st = f.read()
+        except OSError:
+            continue
+        name = st[st.index("(") + 1:st.rindex(")")]
+        fields = st[st.rindex(")") + 2:].split()
+        out[name] = out.get(name, 0.0) + (int(fields[11]) + int(fields[12])) / tick
+    return out
+
+
 def launch(args, argv, grace_s=5.0):
     n = args.gpus
     port = _free_port()  # only for code that wants an env:// store; the native comm uses the job id
@@ -281,6 +297,7 @@ def run_rank(args):
             torch.cuda.synchronize()
         cg0 = cgroup_cpu_stat()
         ru0 = resource.getrusage(resource.RUSAGE_SELF)
+        th0 = thread_cpu_by_name()
         t0 = time.perf_counter()
         if stream is not None:
             with _roctx_range("bench.steps"):
@@ -303,6 +320,7 @@ def run_rank(args):
         dt = time.perf_counter() - t0
         cg1 = cgroup_cpu_stat()
         ru1 = resource.getrusage(resource.RUSAGE_SELF)
+        th1 = thread_cpu_by_name()
         cpu_ms = (ru1.ru_utime + ru1.ru_stime - ru0.ru_utime - ru0.ru_stime) * 1e3 / steps
         dt = comm.allreduce_max([dt])[0]
         total_ok = comm.allreduce_sum([ok])[0]
@@ -321,6 +339,11 @@ def run_rank(args):
             "own_time_imbalance": round(max(own) / max(min(own), 1e-12), 4),
             "rank0_stage_s": {k: round(v, 4) for k, v in stage.items()},
             "rank0_process_cpu_ms_per_step": round(cpu_ms, 3),
+            # rank 0's CPU per step by thread name (nm03-pool: loads + writes, nm03-slot: batch
+            # threads; other names are the interpreter's and the HIP runtime's threads)
+            "rank0_thread_cpu_ms_per_step": {k: round((th1.get(k, 0.0) - th0.get(k, 0.0)) * 1e3 / steps, 3)
+                                             for k in sorted(set(th0) | set(th1))
+                                             if th1.get(k, 0.0) - th0.get(k, 0.0) > 0},
             # host CPU of the whole cgroup over the timed region (all ranks of this container)
             "cgroup_cpu_ms_per_step": {k[:-5]: round((cg1[k] - cg0.get(k, 0)) / 1e3 / steps, 3)
                                        for k in ("usage_usec", "throttled_usec") if k in cg1},
@@ -368,6 +391,7 @@ def run_rank(args):
                 "rank0_stage_s": primary["rank0_stage_s"],
                 "cgroup_cpu_ms_per_step": primary["cgroup_cpu_ms_per_step"],
                 "rank0_process_cpu_ms_per_step": primary["rank0_process_cpu_ms_per_step"],
+                "rank0_thread_cpu_ms_per_step": primary["rank0_thread_cpu_ms_per_step"],
                 "per_rank": primary["per_rank"],
                 "own_time_imbalance": primary["own_time_imbalance"],
                 "storage": {"data": local_root, "input_copies": len(roots), "out": args.out_root},

@@ -4,6 +4,8 @@
 // so patient and batch boundaries never idle the workers.
 #pragma once
 
+#include <pthread.h>
+
 #include <algorithm>
 #include <atomic>
 #include <condition_variable>
@@ -28,6 +30,7 @@ class ThreadPool {
     if (n < 1) n = 1;
     for (int i = 0; i < n; ++i)
       workers_.emplace_back([this, on_start] {
+        pthread_setname_np(pthread_self(), "nm03-pool");  // per-thread CPU accounting (bench.py)
         if (on_start) on_start();
         loop();
       });

@@ -1052,6 +1052,7 @@ struct Engine::Impl {
   }
 
   void worker(size_t slot_index) {
+    pthread_setname_np(pthread_self(), "nm03-slot");
     place.bind_this_thread();
     (void)prctl(PR_SET_TIMERSLACK, 1000UL, 0, 0, 0);  // 1 µs: short poll sleeps stay short
     (void)hipSetDevice(cfg.device);
