@@ -75,3 +75,25 @@ def test_bench_single_rank_dry(tmp_path):
     rec = _json_line(r.stdout)
     assert rec["n_gpus"] == 1 and rec["config"]["comm"]["backend"] == "self"
     assert rec["steps"] == 2 and rec["warmup"] == 1
+
+
+def test_bench_under_torchrun(tmp_path):
+    """The driver's multi-GPU form: `python -m torch.distributed.run --nproc-per-node N ... bench.py
+    --gpus N` — ranks from torchrun, segment name through the env:// store, one JSON line."""
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    e = dict(os.environ, NM03_COMM_TIMEOUT_S="30", NM03_BENCH_NUMA_DATA="off")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT", "NM03_COMM_JOB"):
+        e.pop(k, None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--dry-run", "--steps", "2", "--warmup", "1",
+           "--data-root", str(tmp_path / "data"), "--out-root", str(tmp_path / "out")]
+    r = subprocess.run(cmd, cwd=str(tmp_path), env=e, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    rec = _json_line(r.stdout)
+    assert rec["n_gpus"] == 2 and all(len(v) == 2 for v in rec["config"]["per_rank"].values())
+    assert rec["config"]["comm"]["backend"] == "host"  # auto: no RCCL without a GPU, recorded
+    assert "rccl_error" in rec["config"]["comm"]
