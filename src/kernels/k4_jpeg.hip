@@ -139,7 +139,11 @@ __device__ __forceinline__ uint32_t priv_word(const uint32_t* pb, const uint32_t
 //     times out is re-encoded on the CPU);
 //  4. each thread writes its block's codes at its bit offset (atomicOr into the zeroed stage).
 // The last workgroup of an image publishes the total (or the overflow marker).
-__global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(4))) void jpeg_fused_kernel(const uint8_t* __restrict__ canvas,
+// kOcc: target waves per SIMD (= workgroups per CU); kUnion: LDS words of the patch / bit-range
+// union. <4, kUnionWords> is the default; <5, kPatchLds + 1200> fits 5 workgroups per CU (31.7 KiB)
+// at ≤ 96 VGPRs (NM03_JPEG_OCC=5, A/B).
+template <int kOcc, int kUnion>
+__global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(kOcc))) void jpeg_fused_kernel(const uint8_t* __restrict__ canvas,
                                                              const JpegDesc* __restrict__ jd, int ncanvas, int out_w,
                                                              int out_h, QuantRecip q, JpegWork w, JpegRenderSrc rs,
                                                              uint8_t* __restrict__ out, int32_t* __restrict__ out_sizes,
@@ -153,7 +157,7 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(4))) vo
   __shared__ uint32_t s_ticket, s_obase, s_nown, s_strad_v, s_fin_v, s_f, s_nwords;
   __shared__ bool s_bad, s_strad, s_fin;
   __shared__ int32_t s_prevdc;
-  __shared__ __attribute__((aligned(16))) float spatch[kUnionWords];  // render patch, then swg + output
+  __shared__ __attribute__((aligned(16))) float spatch[kUnion];  // render patch, then swg + output
   uint32_t* const swg = reinterpret_cast<uint32_t*>(spatch);             // the workgroup's bit range
   const int tid = threadIdx.x;
   // Records of the previous launch (the other half of the look area) are dead: clear them here
@@ -411,7 +415,7 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(4))) vo
   // bit range (MSB-first words), in the LDS region the render patch used. A range too long for
   // it (> ~220 Kbit: pathological detail) poisons the image, which the host then re-encodes.
   const uint32_t nlocal = (agg + 31) >> 5;
-  const bool in_lds = nlocal + 2u <= (uint32_t)kUnionWords;  // workgroup-uniform
+  const bool in_lds = nlocal + 2u <= (uint32_t)kUnion;  // workgroup-uniform
   const uint32_t nwp = (acbits + 31) >> 5;
   const uint32_t acpos = excl + (uint32_t)dclen;
   if (in_lds) {
@@ -608,7 +612,7 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(4))) vo
   uint32_t tot = 0;
   uint32_t o = block_exclusive_scan(cnt, sh, &tot);
   uint8_t* sbuf = reinterpret_cast<uint8_t*>(swg + ((s_nwords + 3u) & ~3u));  // behind the bit range
-  const bool staged_out = tot <= (uint32_t)(kUnionWords - ((s_nwords + 3u) & ~3u)) * 4u;
+  const bool staged_out = tot <= (uint32_t)(kUnion - ((s_nwords + 3u) & ~3u)) * 4u;
   uint8_t* dst = out + d.out_off + s_obase;
   for (uint32_t j = j0; j < j1; ++j) {
     const uint32_t v = owned(j);
@@ -689,8 +693,16 @@ void launch_jpeg(const uint8_t* canvas, const JpegDesc* jd, int ncanvas, int out
     w.look_base = w.look_base ? 0 : half;
     w.prev_words = words;
   }
-  jpeg_fused_kernel<<<parts * ncanvas, kJpegWG, pad, stream>>>(canvas, jd, ncanvas, out_w, out_h, q, w, rs, out,
-                                                                out_sizes, dbg);
+  static const int occ = [] {
+    const char* e = std::getenv("NM03_JPEG_OCC");
+    return e && std::atoi(e) == 5 ? 5 : 4;
+  }();
+  if (occ == 5)
+    jpeg_fused_kernel<5, kPatchLds + 1200><<<parts * ncanvas, kJpegWG, pad, stream>>>(
+        canvas, jd, ncanvas, out_w, out_h, q, w, rs, out, out_sizes, dbg);
+  else
+    jpeg_fused_kernel<4, kUnionWords><<<parts * ncanvas, kJpegWG, pad, stream>>>(canvas, jd, ncanvas, out_w, out_h, q, w,
+                                                                                  rs, out, out_sizes, dbg);
   check_launch("jpeg_fused_kernel");
 }
 
