@@ -398,6 +398,13 @@ int parallel_rank(const AppConfig& cfg, int rank, int size, Comm& comm, int devi
     (void)hipSetDevice(device);
     void* p = nullptr;
     if (hipMalloc(&p, 4096) == hipSuccess) (void)hipFree(p);
+    // Also the runtime's first stream (hardware queue) and first pinned allocation, which the
+    // engine's first slot would otherwise pay for after planning: the queue goes back to the
+    // runtime's pool on destroy and is reused by the engine's streams.
+    hipStream_t st = nullptr;
+    if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) == hipSuccess) (void)hipStreamDestroy(st);
+    void* h = nullptr;
+    if (hipHostMalloc(&h, 4096, hipHostMallocDefault) == hipSuccess) (void)hipHostFree(h);
     hip_init_s = now_s() - t0;
   });
   struct Joiner {
