@@ -6,6 +6,7 @@
 // `make_header` and appends EOI. `encode_gray420` is the single-threaded golden encoder.
 #pragma once
 
+#include <atomic>
 #include <cstdint>
 #include <string>
 #include <vector>
@@ -41,6 +42,7 @@ void write_jpeg_file(const std::string& path, const std::vector<uint8_t>& header
 // Same, `name` relative to the directory fd `dirfd` (openat: no path walk per file); `dir` only
 // names the file in error messages.
 void write_jpeg_at(int dirfd, const std::string& dir, const std::string& name, const std::vector<uint8_t>& header,
-                   const uint8_t* scan, size_t scan_len);
+                   const uint8_t* scan, size_t scan_len,
+                   std::atomic<uint8_t>* creating = nullptr);
 
 }  // namespace nm03::jpeg

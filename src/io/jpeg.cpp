@@ -3,6 +3,8 @@
 #include "nm03/jpeg.h"
 
 #include <fcntl.h>
+
+#include <atomic>
 #include <sys/stat.h>
 #include <sys/uio.h>
 #include <unistd.h>
@@ -198,12 +200,21 @@ void write_jpeg_file(const std::string& path, const std::vector<uint8_t>& header
 }
 
 void write_jpeg_at(int dirfd, const std::string& dir, const std::string& name, const std::vector<uint8_t>& header,
-                   const uint8_t* scan, size_t scan_len) {
+                   const uint8_t* scan, size_t scan_len, std::atomic<uint8_t>* creating) {
   auto path = [&] { return dir.empty() ? name : dir + "/" + name; };
   // Overwrite in place instead of O_TRUNC: re-exporting a cohort rewrites files of (nearly) the
   // same size, and truncate + reallocate costs 4-12x more than pwrite on ext4/overlayfs. The old
   // tail is cut only when the previous file was longer, so the bytes on disk are identical.
-  int fd = ::openat(dirfd, name.c_str(), O_WRONLY | O_CREAT | O_CLOEXEC, 0644);
+  // O_CREAT makes open() take the directory's inode lock exclusively (kernels before 6.12 even
+  // when the file exists), which serialises every writer of a patient directory: with a
+  // per-directory hint, existing files are opened without it first, and once a directory is seen
+  // to be empty (a fresh or wiped output tree) its files are created directly.
+  int fd = -1;
+  if (creating && !creating->load(std::memory_order_relaxed)) {
+    fd = ::openat(dirfd, name.c_str(), O_WRONLY | O_CLOEXEC);
+    if (fd < 0 && errno == ENOENT) creating->store(1, std::memory_order_relaxed);
+  }
+  if (fd < 0) fd = ::openat(dirfd, name.c_str(), O_WRONLY | O_CREAT | O_CLOEXEC, 0644);
   if (fd < 0) throw std::runtime_error("Cannot create " + path() + ": " + std::strerror(errno));
   static const uint8_t eoi[2] = {0xFF, 0xD9};
   struct iovec iov[3] = {{(void*)header.data(), header.size()}, {(void*)scan, scan_len}, {(void*)eoi, 2}};

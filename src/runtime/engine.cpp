@@ -136,6 +136,9 @@ struct Slot {
 // directories between runs (the CLIs do).
 struct IoDirs {
   std::vector<int> fds;
+  // Per directory: 1 once a file was missing there (files are then created directly, see
+  // jpeg::write_jpeg_at); 0 = try opening existing files without O_CREAT first.
+  std::unique_ptr<std::atomic<uint8_t>[]> creating;
   std::vector<int32_t> in_fd, out_fd;  // per item: fd index, -1 = fall back to the full path
   std::vector<uint32_t> in_name;       // per item: offset of the file name in its path
   IoDirs(const std::vector<WorkItem>& items) {
@@ -167,6 +170,8 @@ struct IoDirs {
       }
       out_fd[i] = dir_index(items[i].out_dir);
     }
+    creating.reset(new std::atomic<uint8_t>[std::max<size_t>(fds.size(), 1)]);
+    for (size_t k = 0; k < fds.size(); ++k) creating[k].store(0, std::memory_order_relaxed);
   }
   ~IoDirs() {
     for (int fd : fds) ::close(fd);
@@ -941,7 +946,8 @@ struct Engine::Impl {
                 const std::string name = base + (k == 0 ? "_original.jpg" : "_processed.jpg");
                 const uint8_t* seg = use_fb[cv] ? fb[cv].data() : s.h_out + (size_t)cv * out_cap_;
                 const size_t len = use_fb[cv] ? fb[cv].size() : (size_t)s.h_sizes[cv];
-                jpeg::write_jpeg_at(dfd, rel ? items[item].out_dir : std::string(), name, jpeg_header, seg, len);
+                jpeg::write_jpeg_at(dfd, rel ? items[item].out_dir : std::string(), name, jpeg_header, seg, len,
+                                    rel ? &dirs.creating[dirs.out_fd[item]] : nullptr);
                 bytes_out += (int64_t)(jpeg_header.size() + len + 2);
               }
             } catch (const std::exception& e) {
