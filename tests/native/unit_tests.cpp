@@ -5,6 +5,7 @@
 // Host code only — no GPU is touched, so this runs in CPU-only CI.
 //
 //   build/bin/nm03_unit_tests [filter]      (exit status = number of failed checks)
+#include <fcntl.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -271,6 +272,55 @@ TEST(jpeg_container) {
   for (size_t i = hdr.size(); i + 2 < j.size(); ++i)
     if (j[i] == 0xFF && j[i + 1] != 0x00) ok = false;
   CHECK(ok);
+}
+
+TEST(jpeg_write_in_place_and_create_hint) {
+  // write_jpeg_at: overwrite in place (longer old file cut, shorter grown), and the per-directory
+  // hint — existing files opened without O_CREAT, the first missing one flips the directory to
+  // create mode — never changes the bytes on disk.
+  char tmpl[] = "/tmp/nm03_jw_XXXXXX";
+  const char* dir = mkdtemp(tmpl);
+  CHECK(dir != nullptr);
+  if (!dir) return;
+  const int dfd = ::open(dir, O_PATH | O_DIRECTORY | O_CLOEXEC);
+  CHECK(dfd >= 0);
+  const std::vector<uint8_t> hdr = {0xFF, 0xD8, 1, 2, 3};
+  std::vector<uint8_t> big(5000, 0x11), small(7, 0x22);
+  auto read_all = [&](const std::string& name) {
+    std::vector<uint8_t> b;
+    FILE* f = std::fopen((std::string(dir) + "/" + name).c_str(), "rb");
+    if (!f) return b;
+    int c;
+    while ((c = std::fgetc(f)) != EOF) b.push_back((uint8_t)c);
+    std::fclose(f);
+    return b;
+  };
+  auto expect = [&](const std::vector<uint8_t>& scan) {
+    std::vector<uint8_t> e = hdr;
+    e.insert(e.end(), scan.begin(), scan.end());
+    e.push_back(0xFF);
+    e.push_back(0xD9);
+    return e;
+  };
+  std::atomic<uint8_t> hint{0};
+  nm03::jpeg::write_jpeg_at(dfd, dir, "a.jpg", hdr, big.data(), big.size(), &hint);  // missing: created
+  CHECK(hint.load() == 1);
+  CHECK(read_all("a.jpg") == expect(big));
+  std::atomic<uint8_t> hint2{0};
+  nm03::jpeg::write_jpeg_at(dfd, dir, "a.jpg", hdr, small.data(), small.size(), &hint2);  // exists: cut
+  CHECK(hint2.load() == 0);
+  CHECK(read_all("a.jpg") == expect(small));
+  nm03::jpeg::write_jpeg_at(dfd, dir, "a.jpg", hdr, big.data(), big.size(), &hint2);  // grown again
+  CHECK(read_all("a.jpg") == expect(big));
+  nm03::jpeg::write_jpeg_at(dfd, dir, "b.jpg", hdr, small.data(), small.size(), &hint2);  // flips the hint
+  CHECK(hint2.load() == 1 && read_all("b.jpg") == expect(small));
+  nm03::jpeg::write_jpeg_at(dfd, dir, "a.jpg", hdr, small.data(), small.size(), &hint2);  // create mode, existing
+  CHECK(read_all("a.jpg") == expect(small));
+  nm03::jpeg::write_jpeg_at(dfd, dir, "c.jpg", hdr, small.data(), small.size(), nullptr);  // no hint
+  CHECK(read_all("c.jpg") == expect(small));
+  for (const char* n : {"a.jpg", "b.jpg", "c.jpg"}) ::unlinkat(dfd, n, 0);
+  ::close(dfd);
+  ::rmdir(dir);
 }
 
 // ---- golden operators vs brute-force definitions --------------------------------------------------
