@@ -281,9 +281,12 @@ struct Engine::Impl {
     // Slot 0 is built here (its failure fails the constructor); the others are built by their own
     // worker threads while slot 0 already runs batches — a slot costs ≈11–18 ms of pinned and
     // device allocations and stream creation, the first one more (runtime queues), which a cold
-    // CLI run would otherwise wait for in full. NM03_EAGER_SLOTS=1 builds them all here.
+    // CLI run would otherwise wait for in full. NM03_EAGER_SLOTS=1 (or graphs) builds them all here.
+    // With hipGraph capture on, all slots are built here: a slot being built (device/pinned
+    // allocations, a memset on the null stream) while another slot's thread captures its batch
+    // chain invalidates that capture.
     const char* eager_env = std::getenv("NM03_EAGER_SLOTS");
-    const bool eager = eager_env && *eager_env == '1';
+    const bool eager = (eager_env && *eager_env == '1') || cfg.graphs;
     std::string slot_ms;
     slots.resize((size_t)cfg.streams);
     place.run_bound([&] {
@@ -469,14 +472,22 @@ struct Engine::Impl {
       const char* e = std::getenv("NM03_EVENT_ADAPT");  // 0: plain polling (A/B)
       return !(e && *e == '0');
     }();
-    const double ahead = adapt ? 0.8 * s.batch_ema_s - (now_s() - t_enq) : 0.0;
-    if (ahead > 100e-6 && hipEventQuery(ev) == hipErrorNotReady)
-      std::this_thread::sleep_for(std::chrono::duration<double>(ahead));
+    // Sleep through most of the batch's expected time (0.8 × the recent mean), in chunks of at
+    // most 250 µs with an event check between them, then poll. One long sleep would feed itself:
+    // a slow batch (GPU shared with another process, host CPU stolen) raises the mean, the next
+    // batches oversleep by the same amount, and the mean — measured from these overslept waits —
+    // decays by only ≈5% per batch. Chunked, a wait ends within one chunk of the batch's real
+    // completion, so the mean tracks the GPU again after a few batches.
+    const double target = adapt ? 0.8 * s.batch_ema_s : 0.0;
     for (;;) {
       const hipError_t e = hipEventQuery(ev);
       if (e == hipSuccess) break;
       if (e != hipErrorNotReady) check_hip(e, "batch sync");
-      std::this_thread::sleep_for(std::chrono::microseconds(poll_us()));
+      const double ahead = target - (now_s() - t_enq);
+      if (ahead > 100e-6)
+        std::this_thread::sleep_for(std::chrono::duration<double>(std::min(ahead, 250e-6)));
+      else
+        std::this_thread::sleep_for(std::chrono::microseconds(poll_us()));
     }
     const double took = now_s() - t_enq;
     s.batch_ema_s = s.batch_ema_s > 0 ? 0.75 * s.batch_ema_s + 0.25 * took : took;
