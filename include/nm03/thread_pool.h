@@ -5,6 +5,7 @@
 #pragma once
 
 #include <pthread.h>
+#include <time.h>
 
 #include <algorithm>
 #include <atomic>
@@ -98,6 +99,12 @@ class ThreadPool {
   bool stop_ = false;
 };
 
+inline int64_t thread_cpu_now_ns() {
+  timespec ts;
+  clock_gettime(CLOCK_THREAD_CPUTIME_ID, &ts);
+  return (int64_t)ts.tv_sec * 1000000000 + ts.tv_nsec;
+}
+
 // Counts outstanding tasks; wait() blocks until all submitted through it finished.
 class TaskGroup {
  public:
@@ -114,8 +121,10 @@ class TaskGroup {
         },
         prio);
   }
-  // fn(i) for i in [0, n): min(n, pool size) runners pull indices from a shared counter.
-  void for_each(size_t n, std::function<void(size_t)> fn, uint64_t prio = 0) {
+  // fn(i) for i in [0, n): min(n, pool size) runners pull indices from a shared counter. With
+  // `cpu_ns`, each runner adds the thread CPU time of its whole share (two clock reads per runner
+  // instead of two per item: a thread-CPU clock read is a system call, ≈0.3 µs).
+  void for_each(size_t n, std::function<void(size_t)> fn, uint64_t prio = 0, std::atomic<int64_t>* cpu_ns = nullptr) {
     if (n == 0) return;
     const int runners = (int)std::min<size_t>(n, (size_t)pool_.size());
     auto st = std::make_shared<ForEach>();
@@ -127,8 +136,10 @@ class TaskGroup {
     }
     pool_.submit_n(
         runners,
-        [this, st] {
+        [this, st, cpu_ns] {
+          const int64_t c0 = cpu_ns ? thread_cpu_now_ns() : 0;
           for (size_t i; (i = st->next.fetch_add(1)) < st->n;) st->fn(i);
+          if (cpu_ns) cpu_ns->fetch_add(thread_cpu_now_ns() - c0, std::memory_order_relaxed);
           done(1);
         },
         prio);

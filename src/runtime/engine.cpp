@@ -495,11 +495,10 @@ struct Engine::Impl {
 
   // ---- loading -------------------------------------------------------------------------------
   void load_into(Slot& s, int i, size_t item, const std::string& path, int dirfd, const char* name, SliceStatus& st,
-                 std::atomic<int64_t>& load_ns, std::atomic<int64_t>& load_cpu_ns, std::atomic<int64_t>& bytes_in) {
+                 std::atomic<int64_t>& load_ns, std::atomic<int64_t>& bytes_in) {
     thread_local std::vector<uint8_t> buf;
     TraceRange tr("nm03.load");
     const double t0 = now_s();
-    const int64_t c0 = thread_cpu_ns();
     try {
       if (fault_plan().corrupt_dicom == (int64_t)item) throw SliceError("injected fault: corrupt DICOM data");
       dicom::SliceFile file(dirfd, name, path, read_mode_, read_prefix_);
@@ -612,7 +611,6 @@ struct Engine::Impl {
       st.message = e.what();
     }
     load_ns += (int64_t)((now_s() - t0) * 1e9);
-    load_cpu_ns += thread_cpu_ns() - c0;
   }
 
   static bool outputs_exist(const WorkItem& w) {
@@ -877,7 +875,7 @@ struct Engine::Impl {
               const size_t it = first + i;
               const int dfd = dirs.in_fd[it] >= 0 ? dirs.fds[dirs.in_fd[it]] : AT_FDCWD;
               const char* nm = items[it].path.c_str() + (dirs.in_fd[it] >= 0 ? dirs.in_name[it] : 0);
-              load_into(s, (int)i, it, items[it].path, dfd, nm, status[it], load_ns, load_cpu_ns, bytes_in);
+              load_into(s, (int)i, it, items[it].path, dfd, nm, status[it], load_ns, bytes_in);
             }
             if (upload_chunk_) {
               {
@@ -887,7 +885,7 @@ struct Engine::Impl {
               s.prog_cv.notify_one();
             }
           },
-          2 * prio);
+          2 * prio, &load_cpu_ns);
       if (upload_chunk_) {
         // A failed early upload fails the batch like any device error (below), not the run; the
         // loads still finish (tg.wait) before the blob is touched again.
@@ -944,7 +942,6 @@ struct Engine::Impl {
             const size_t item = first + s.live[c];
             if (status[item].code != kSliceOk) return;
             const double t0 = now_s();
-            const int64_t c0 = thread_cpu_ns();
             TraceRange tr("nm03.export");
             try {
               if (fault_plan().fail_write == (int64_t)item) throw std::runtime_error("injected fault: export failure");
@@ -965,9 +962,8 @@ struct Engine::Impl {
               status[item] = SliceStatus{kSliceExportError, std::string("Error in export stage: ") + e.what()};
             }
             write_ns += (int64_t)((now_s() - t0) * 1e9);
-            write_cpu_ns += thread_cpu_ns() - c0;
           },
-          2 * prio + 1);
+          2 * prio + 1, &write_cpu_ns);
       tg.wait();
     }
     std::lock_guard<std::mutex> g(acc_m);
