@@ -446,11 +446,23 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(kOcc)))
 #pragma unroll
   for (int al = 0; al < 8; ++al) ffc[al] = 0;
   if (in_lds) {
+    // All eight alignments in one pass over the range's 32-bit words: bit q (MSB first) of
+    // `r` says whether the 8 bits starting at range bit 32j + q are all ones (three shift-ANDs on
+    // the word and the next one); a byte of alignment `al` starts at f + 8i, f = (8 − al) & 7, and
+    // must end within the range (p + 8 ≤ A), so its count is popcount(r & (0x80808080 >> f)) over
+    // the valid positions — instead of one LDS byte extraction per byte and alignment.
+    const uint32_t nw = (A + 31u) >> 5;  // the range buffer has ≥ 2 words of slack (in_lds)
+    for (uint32_t j = tid; j < nw; j += kJpegWG) {
+      const int32_t lim = (int32_t)A - 8 - 32 * (int32_t)j;  // last q whose byte fits in the range
+      if (lim < 0) continue;
+      const uint64_t v = ((uint64_t)swg[j] << 32) | swg[j + 1];
+      uint64_t run = v & (v << 1);
+      run &= run << 2;
+      run &= run << 4;  // bit k: bits k .. k−7 of v all set
+      uint32_t r = (uint32_t)(run >> 32);
+      if (lim < 31) r &= ~((1u << (31 - lim)) - 1u);
 #pragma unroll
-    for (int al = 0; al < 8; ++al) {
-      const uint32_t f = (uint32_t)((8 - al) & 7);
-      const uint32_t nfull = A >= f ? (A - f) >> 3 : 0u;
-      for (uint32_t i = tid; i < nfull; i += kJpegWG) ffc[al] += lds_byte(swg, f + 8u * i) == 0xFFu;
+      for (int al = 0; al < 8; ++al) ffc[al] += (uint32_t)__popc(r & (0x80808080u >> ((8 - al) & 7)));
     }
   }
   const int lane = tid & 63, wv = tid >> 6;
