@@ -98,6 +98,12 @@ struct JpegRenderSrc {
 void launch_jpeg(const uint8_t* canvas, const JpegDesc* jd, int ncanvas, int out_w, int out_h, const int32_t* div_luma,
                  JpegWork& w, uint8_t* out, int32_t* out_sizes, hipStream_t stream,
                  const JpegRenderSrc* fused = nullptr);
+// Compacts the encoder's per-canvas HBM segments (canvas k at k × stride) to 16-byte-aligned prefix
+// offsets in dst and mirrors the sizes into host_sizes (host-mapped); see jpeg_compact_offset.
+void launch_jpeg_gather(const uint8_t* src, uint32_t stride, const int32_t* sizes, int ncanvas, uint8_t* dst,
+                        int32_t* host_sizes, hipStream_t stream);
+// Host side of the same layout: offset of canvas k = Σ_{i<k} align16(max(size_i, 0)).
+inline size_t jpeg_compact_bytes(int32_t size) { return size > 0 ? ((size_t)size + 15) & ~(size_t)15 : 0; }
 // K6: binary threshold lo ≤ x ≤ hi → u8 0/1 (in 16-byte aligned, out 4-byte aligned).
 void launch_threshold(const float* in, uint8_t* out, size_t n, float lo, float hi, hipStream_t stream);
 

@@ -587,7 +587,13 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(kOcc)))
     const uint32_t end = p_start + A;
     bad = bad || end >= (1u << 22) || ff_before + own >= (1u << 20);
     const uint32_t obase = (p_start >> 3) + ff_before;
-    bad = bad || obase + 2u * nown > d.out_cap;
+    // Exact end of this workgroup's stuffed bytes (own = its 0xFF count). It must be exact, not a
+    // bound: a later workgroup that saw this one only as an aggregate never learns its flag, so the
+    // flag has to follow from positions alone (ends are monotone along the image: once one
+    // workgroup's end passes the capacity every later start does, and the last part reports -1).
+    // A conservative 2 × nown bound let a workgroup drop its bytes while the image still reported
+    // a size (tests/test_gpu.py::test_engine_jpeg_d2h_identical, capacity 20000).
+    bad = bad || obase + nown + own > d.out_cap;
     if (lane == 0) {
       look_store64(&look[3 * part], (2ull << 62) | ((uint64_t)bad << 61) | ((uint64_t)(end & 0x3FFFFF) << 39) |
                                         ((uint64_t)((ff_before + own) & 0xFFFFF) << 19) |
@@ -716,6 +722,46 @@ void launch_jpeg(const uint8_t* canvas, const JpegDesc* jd, int ncanvas, int out
     jpeg_fused_kernel<4, kUnionWords><<<parts * ncanvas, kJpegWG, pad, stream>>>(canvas, jd, ncanvas, out_w, out_h, q, w,
                                                                                   rs, out, out_sizes, dbg);
   check_launch("jpeg_fused_kernel");
+}
+
+// Compaction of the encoder's HBM output for one SDMA copy to the host (engine NM03_JPEG_D2H=1/2, opt-in): canvas k's
+// segment moves from k × stride to the 16-byte-aligned prefix sum of the earlier segments' sizes
+// (a negative size — capacity overflow, re-encoded on the CPU — counts as 0). One workgroup per
+// (16 KiB column, canvas); wave 0 of every workgroup sums the ≤ cap earlier sizes from HBM, which is
+// cheaper than a separate scan launch. The sizes are mirrored into host-mapped memory for the host,
+// which derives the same offsets (jpeg_compact_bytes). Motivation: the encoder takes 96 µs per
+// 64-slice batch storing into host-mapped memory and 75 µs storing into HBM (profiles/r2/jpeg_devout/);
+// the copy that then has to follow costs more than it saves (engine.cpp, jpeg_d2h_).
+__global__ __launch_bounds__(256) void jpeg_gather_kernel(const uint8_t* __restrict__ src, uint32_t stride,
+                                                          const int32_t* __restrict__ sizes,
+                                                          uint8_t* __restrict__ dst, int32_t* __restrict__ host_sizes) {
+  const int k = blockIdx.y;
+  __shared__ uint32_t s_off;
+  if (threadIdx.x < 64) {
+    uint32_t acc = 0;
+    for (int i = threadIdx.x; i < k; i += 64) {
+      const int32_t z = sizes[i];
+      acc += z > 0 ? ((uint32_t)z + 15u) & ~15u : 0u;
+    }
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+    if (threadIdx.x == 0) s_off = acc;
+  }
+  const int32_t z = sizes[k];
+  if (blockIdx.x == 0 && threadIdx.x == 0) host_sizes[k] = z;
+  __syncthreads();
+  if (z <= 0) return;
+  const uint32_t n16 = ((uint32_t)z + 15u) >> 4;
+  const uint4* s4 = reinterpret_cast<const uint4*>(src + (size_t)k * stride);
+  uint4* d4 = reinterpret_cast<uint4*>(dst + s_off);
+  for (uint32_t w = blockIdx.x * 256 + threadIdx.x; w < n16; w += gridDim.x * 256) d4[w] = s4[w];
+}
+
+void launch_jpeg_gather(const uint8_t* src, uint32_t stride, const int32_t* sizes, int ncanvas, uint8_t* dst,
+                        int32_t* host_sizes, hipStream_t stream) {
+  if (ncanvas <= 0) return;
+  if (stride % 16) throw DeviceError("launch_jpeg_gather: canvas stride must be a multiple of 16");
+  jpeg_gather_kernel<<<dim3(4, ncanvas), 256, 0, stream>>>(src, stride, sizes, dst, host_sizes);
+  check_launch("jpeg_gather_kernel");
 }
 
 }  // namespace nm03::gpu

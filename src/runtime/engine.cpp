@@ -97,6 +97,15 @@ struct Slot {
   JpegWork jw;
   uint8_t* h_out = nullptr;
   uint8_t* d_out = nullptr;
+  // JPEG D2H mode (default): the encoder writes its segments to d_jraw (HBM, canvas k at k × out_cap),
+  // jpeg_gather_kernel packs them into d_jcomp and one SDMA copy moves the packed bytes into h_out
+  // (plain pinned memory); h_sizes stays host-mapped. Off (NM03_JPEG_D2H=0): the encoder stores
+  // straight into host-mapped h_out over PCIe.
+  uint8_t* d_jraw = nullptr;
+  uint8_t* d_jcomp = nullptr;
+  int32_t* d_jsizes = nullptr;
+  size_t jcopied = 0;              // bytes of d_jcomp copied by the batch's first D2H
+  std::vector<size_t> jofs;        // per-canvas offsets into h_out (D2H mode)
   int32_t* h_sizes = nullptr;
   int32_t* d_sizes = nullptr;
   std::atomic<size_t> raw_used{0};
@@ -185,7 +194,8 @@ void hip_free_all(Slot& s) {
   if (s.h_out) (void)hipHostFree(s.h_out);
   if (s.h_sizes) (void)hipHostFree(s.h_sizes);
   for (void* p : {(void*)s.d_blob, (void*)s.d_raw_x, (void*)s.d_med, (void*)s.d_tile_mm, (void*)s.d_f32, (void*)s.d_bits, (void*)s.d_srg_scratch, (void*)s.d_canvas,
-                  (void*)s.jw.look, (void*)s.jw.ticket, (void*)s.jw.spill})
+                  (void*)s.jw.look, (void*)s.jw.ticket, (void*)s.jw.spill, (void*)s.d_jraw,
+                  (void*)s.d_jcomp, (void*)s.d_jsizes})
     if (p) (void)hipFree(p);
   if (s.map_region) munmap(s.map_region, (size_t)s.cap_slices * s.map_stride);
   for (auto& kv : s.graphs) (void)hipGraphExecDestroy(kv.second);
@@ -225,6 +235,16 @@ struct Engine::Impl {
   // 512², ~5× a typical medical render; anything larger is CPU re-encoded, counted in StageTimes).
   // NM03_JPEG_OUT_CAP=<bytes> overrides (tests force the fallback with a tiny cap).
   uint32_t out_cap_ = 0;
+  // JPEG export path (NM03_JPEG_D2H): 0 = the encoder stores into host-mapped memory (default);
+  // 1 = HBM + gather + one SDMA copy; 2 = HBM + a gather kernel storing the packed bytes into
+  // host-mapped memory. Measured (profiles/r2/jpeg_d2h/): 1 cuts GPU time per 64-slice batch from
+  // 96 to 75 + 4.5 µs but its D2H copies share the copy engines with the uploads (H2D time
+  // doubles) and the headline drops (138-242k vs 286-340k slices/s); 2 moves the PCIe stores into
+  // the gather (75 + 25.6 µs) for no gain. Both stay selectable for A/B runs.
+  int jpeg_d2h_ = 0;
+  // Bytes per canvas the first D2H of a batch copies (1.25 × the largest packed average seen so
+  // far, 4 KiB granules; a batch that packs more copies the rest after its completion event).
+  std::atomic<uint32_t> jpeg_est_{24u << 10};
   // NM03_PACK_BOUNCE=0: pack into a full-size intermediate and stream-copy it (A/B of pack_stream).
   bool pack_bounce_ = true;
 
@@ -239,6 +259,10 @@ struct Engine::Impl {
     if (const char* e = std::getenv("NM03_PACK_BOUNCE"); e && *e && *e == '0') pack_bounce_ = false;
     out_cap_ = (uint32_t)std::max<size_t>(64 * 1024, (size_t)cfg.render.out_width * cfg.render.out_height / 2) + 64;
     if (const char* e = std::getenv("NM03_JPEG_OUT_CAP"); e && *e) out_cap_ = (uint32_t)std::max(64L, std::atol(e));
+    out_cap_ = (out_cap_ + 15u) & ~15u;  // jpeg_gather_kernel moves 16-byte words
+    if (const char* e = std::getenv("NM03_JPEG_D2H"); e && *e) jpeg_d2h_ = std::clamp(std::atoi(e), 0, 2);
+    if (const char* e = std::getenv("NM03_JPEG_D2H_EST_KB"); e && *e)  // tests: force short first copies
+      jpeg_est_ = (uint32_t)std::max(1L, std::atol(e)) << 10;
     if (const char* e = std::getenv("NM03_UPLOAD_CHUNK_KB"); e && *e) upload_chunk_ = (size_t)std::atol(e) << 10;
     if (cfg.batch_size < 1) cfg.batch_size = 1;
     if (cfg.streams < 1) cfg.streams = 1;
@@ -376,9 +400,19 @@ struct Engine::Impl {
       s.jw.ticket = dmalloc<uint32_t>(s.cap_canvases, "hipMalloc tickets");
       s.jw.spill = dmalloc<uint32_t>(s.jw.look_cap * 256 * 56, "hipMalloc jpeg spill");
       check_hip(hipMemset(s.jw.ticket, 0, sizeof(uint32_t) * s.cap_canvases), "memset tickets");
-      check_hip(hipHostMalloc((void**)&s.h_out, (size_t)out_cap_ * s.cap_canvases, hipHostMallocMapped),
-                "hipHostMalloc out");
-      check_hip(hipHostGetDevicePointer((void**)&s.d_out, s.h_out, 0), "hipHostGetDevicePointer out");
+      const size_t out_bytes = (size_t)out_cap_ * s.cap_canvases;
+      if (jpeg_d2h_) {
+        check_hip(hipHostMalloc((void**)&s.h_out, out_bytes, jpeg_d2h_ == 2 ? hipHostMallocMapped : hipHostMallocDefault),
+                  "hipHostMalloc out");
+        if (jpeg_d2h_ == 2) check_hip(hipHostGetDevicePointer((void**)&s.d_out, s.h_out, 0), "hipHostGetDevicePointer out");
+        s.d_jraw = dmalloc<uint8_t>(out_bytes, "hipMalloc jpeg out");
+        if (jpeg_d2h_ == 1) s.d_jcomp = dmalloc<uint8_t>(out_bytes, "hipMalloc jpeg packed");
+        s.d_jsizes = dmalloc<int32_t>(s.cap_canvases, "hipMalloc jpeg sizes");
+        s.jofs.assign(s.cap_canvases, 0);
+      } else {
+        check_hip(hipHostMalloc((void**)&s.h_out, out_bytes, hipHostMallocMapped), "hipHostMalloc out");
+        check_hip(hipHostGetDevicePointer((void**)&s.d_out, s.h_out, 0), "hipHostGetDevicePointer out");
+      }
       check_hip(hipHostMalloc((void**)&s.h_sizes, sizeof(int32_t) * s.cap_canvases, hipHostMallocMapped),
                 "hipHostMalloc sizes");
       check_hip(hipHostGetDevicePointer((void**)&s.d_sizes, s.h_sizes, 0), "hipHostGetDevicePointer sizes");
@@ -779,7 +813,13 @@ struct Engine::Impl {
       rsrc.bits = s.d_bits;
       rsrc.stats = d_stats;
       rsrc.rd = d_rd;
-      launch_jpeg(s.d_canvas, d_jd, ncanv, cw, ch, divs, s.jw, s.d_out, s.d_sizes, s.stream, &rsrc);
+      if (jpeg_d2h_) {
+        launch_jpeg(s.d_canvas, d_jd, ncanv, cw, ch, divs, s.jw, s.d_jraw, s.d_jsizes, s.stream, &rsrc);
+        launch_jpeg_gather(s.d_jraw, out_cap_, s.d_jsizes, ncanv, jpeg_d2h_ == 2 ? s.d_out : s.d_jcomp, s.d_sizes,
+                           s.stream);
+      } else {
+        launch_jpeg(s.d_canvas, d_jd, ncanv, cw, ch, divs, s.jw, s.d_out, s.d_sizes, s.stream, &rsrc);
+      }
     };
     if (!cfg.graphs || sync_launches()) {
       chain();
@@ -811,8 +851,13 @@ struct Engine::Impl {
       }
       check_hip(hipGraphLaunch(it->second, s.stream), "graph launch");
     }
+    if (jpeg_d2h_ == 1 && ncanv > 0) {
+      s.jcopied = std::min((size_t)out_cap_ * ncanv, (size_t)jpeg_est_.load(std::memory_order_relaxed) * ncanv);
+      check_hip(hipMemcpyAsync(s.h_out, s.d_jcomp, s.jcopied, hipMemcpyDeviceToHost, s.stream), "jpeg D2H");
+    }
     check_hip(hipEventRecord(s.ev2, s.stream), "event");
     wait_batch(s, s.ev2, t_enq);
+    if (jpeg_d2h_ && ncanv > 0) finish_jpeg_d2h(s, ncanv);
     if (acc) {
       float a = 0, b = 0;
       (void)hipEventElapsedTime(&a, s.ev0, s.ev1);
@@ -820,6 +865,33 @@ struct Engine::Impl {
       acc->h2d_s += a * 1e-3;
       acc->kernels_s += b * 1e-3;
     }
+  }
+
+  // D2H mode, after the batch's completion event: packed offsets from the mirrored sizes (the
+  // gather kernel's layout), the rest of the packed bytes if the first copy was short, and the
+  // estimate for later batches.
+  void finish_jpeg_d2h(Slot& s, int ncanv) {
+    size_t total = 0;
+    for (int k = 0; k < ncanv; ++k) {
+      s.jofs[k] = total;
+      total += jpeg_compact_bytes(s.h_sizes[k]);
+    }
+    if (jpeg_d2h_ == 2) return;
+    if (total > s.jcopied) {
+      check_hip(hipMemcpyAsync(s.h_out + s.jcopied, s.d_jcomp + s.jcopied, total - s.jcopied, hipMemcpyDeviceToHost,
+                               s.stream),
+                "jpeg D2H rest");
+      check_hip(hipStreamSynchronize(s.stream), "jpeg D2H rest");
+    }
+    const uint32_t want = (uint32_t)std::min<size_t>(out_cap_, ((total / ncanv) * 5 / 4 + 4095) & ~(size_t)4095);
+    uint32_t cur = jpeg_est_.load(std::memory_order_relaxed);
+    while (want > cur && !jpeg_est_.compare_exchange_weak(cur, want, std::memory_order_relaxed)) {
+    }
+  }
+
+  // Host bytes of canvas k's GPU-encoded segment (valid when h_sizes[k] ≥ 0).
+  const uint8_t* jpeg_bytes(const Slot& s, int k) const {
+    return jpeg_d2h_ ? s.h_out + s.jofs[k] : s.h_out + (size_t)k * out_cap_;
   }
 
   // Bytes of canvas k's JPEG (header + segment + EOI); falls back to the CPU encoder when the
@@ -952,7 +1024,7 @@ struct Engine::Impl {
               for (int k = 0; k < 2; ++k) {
                 const int cv = 2 * (int)c + k;
                 const std::string name = base + (k == 0 ? "_original.jpg" : "_processed.jpg");
-                const uint8_t* seg = use_fb[cv] ? fb[cv].data() : s.h_out + (size_t)cv * out_cap_;
+                const uint8_t* seg = use_fb[cv] ? fb[cv].data() : jpeg_bytes(s, cv);
                 const size_t len = use_fb[cv] ? fb[cv].size() : (size_t)s.h_sizes[cv];
                 jpeg::write_jpeg_at(dfd, rel ? items[item].out_dir : std::string(), name, jpeg_header, seg, len,
                                     rel ? &dirs.creating[dirs.out_fd[item]] : nullptr);
@@ -1208,7 +1280,7 @@ struct Engine::Impl {
       const bool gpu_ok = jpeg_segment(s, k, fb, nullptr);
       std::vector<uint8_t> f = jpeg_header;
       if (gpu_ok)
-        f.insert(f.end(), s.h_out + (size_t)k * out_cap_, s.h_out + (size_t)k * out_cap_ + s.h_sizes[k]);
+        f.insert(f.end(), jpeg_bytes(s, k), jpeg_bytes(s, k) + s.h_sizes[k]);
       else
         f.insert(f.end(), fb.begin(), fb.end());
       f.push_back(0xFF);

@@ -437,6 +437,32 @@ def test_engine_fused_unpack_identical(native, cohort_root, tmp_path, monkeypatc
     assert runs[0][1] == runs[1][1]
 
 
+def test_engine_jpeg_d2h_identical(native, cohort_root, tmp_path, monkeypatch):
+    """JPEG export through HBM + gather + one SDMA copy (NM03_JPEG_D2H=1), through HBM + a gather
+    kernel storing into host-mapped memory (2) and with the encoder storing straight into
+    host-mapped memory (0): same statuses, byte-identical trees. The D2H runs
+    start with a 1 KiB-per-canvas copy estimate, so the first batches take the short-copy path (the
+    rest copied after the completion event) and later ones the grown estimate; eager and hipGraph
+    launches; a forced capacity overflow (CPU re-encode, negative sizes in the packed layout)."""
+    runs = []
+    for i, (d2h, graphs, cap) in enumerate([("0", False, ""), ("1", False, ""), ("1", True, ""), ("2", False, ""),
+                                            ("0", False, "20000"), ("1", False, "20000"), ("2", True, "20000")]):
+        out = str(tmp_path / f"o{i}")
+        items = _items(native, cohort_root, out)[:40]
+        monkeypatch.setenv("NM03_JPEG_D2H", d2h)
+        monkeypatch.setenv("NM03_JPEG_D2H_EST_KB", "1")
+        monkeypatch.setenv("NM03_JPEG_OUT_CAP", cap)
+        eng = native.Engine(nm.PipelineConfig(batch_size=8, streams=2, threads=4, graphs=graphs).engine_config())
+        st, _ = eng.run(items)
+        del eng
+        runs.append(([c for c, _ in st], _tree(out)))
+    for r in runs[1:]:
+        assert r[0] == runs[0][0] and r[0].count(0) == len(r[0])
+    diffs = {i: sorted(k for k in runs[0][1] if r[1].get(k) != runs[0][1][k])[:4]
+             for i, r in enumerate(runs) if r[1] != runs[0][1]}
+    assert not diffs, diffs
+
+
 def test_engine_progressive_upload_identical(native, cohort_root, tmp_path, monkeypatch):
     """Progressive H2D (finished prefixes of a batch's raw region queued while loads run) with
     1 KiB / 64 KiB chunks vs one upload per batch: same statuses, byte-identical JPEGs, on a work
