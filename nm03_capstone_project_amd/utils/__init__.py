@@ -1,5 +1,5 @@
 """DICOM / JPEG / cohort helpers and the synthetic T1+C cohort."""
-from .cohort import (cohort_dir, extract_file_number, find_patient_dirs, list_patient_series,  # noqa: F401
-                     synth_cohort, test_slice_path)
-from .dicom import dicom_bytes, parse_dicom, read_slice  # noqa: F401
+from .cohort import (Cohort, Patient, cohort_dir, extract_file_number, find_patient_dirs,  # noqa: F401
+                     list_patient_series, synth_cohort, test_slice_path)
+from .dicom import Slice, dicom_bytes, load_slice, parse_dicom, read_series, read_slice, series_files  # noqa: F401
 from .timing import Timer  # noqa: F401
