@@ -247,9 +247,11 @@ struct Engine::Impl {
   std::atomic<uint32_t> jpeg_est_{24u << 10};
   // NM03_PACK_BOUNCE=0: pack into a full-size intermediate and stream-copy it (A/B of pack_stream).
   bool pack_bounce_ = true;
+  bool spread_ = false;  // plan_batches' spread schedule (NM03_BATCH_SPREAD)
 
   explicit Impl(const EngineConfig& c) : cfg(c), place(c.device) {
     if (const char* e = std::getenv("NM03_BATCH_TAPER"); e && *e) cfg.taper = *e != '0';
+    if (const char* e = std::getenv("NM03_BATCH_SPREAD"); e && *e) spread_ = *e != '0';
     if (const char* e = std::getenv("NM03_LOAD_MODE"); e && *e)
       read_mode_ = std::string(e) == "staged" ? dicom::ReadMode::kStaged
                    : std::string(e) == "mapped" ? dicom::ReadMode::kMapped
@@ -1055,7 +1057,14 @@ struct Engine::Impl {
   // engine starts after a few loads instead of a full batch (pipeline fill), full batches in the
   // middle, and a remainder split into shrinking batches so the last kernels and exports after
   // the final upload are short (drain). Uniform otherwise.
-  static std::vector<std::pair<size_t, size_t>> plan_batches(size_t n, size_t B, bool taper) {
+  //
+  // Spread (spread_slots = slot count, NM03_BATCH_SPREAD): equal-size batches instead of full ones
+  // plus a remainder (465 slices at B = 64: 8 × 58–59 instead of 7 × 64 + 17), and a list shorter
+  // than one batch per slot (a rank's shard under strong scaling, one patient) split over up to
+  // that many slots with at least kSpreadMin slices each, so its loads, uploads, kernels and
+  // writes overlap across slots instead of running as one batch.
+  static constexpr size_t kSpreadMin = 8;
+  static std::vector<std::pair<size_t, size_t>> plan_batches(size_t n, size_t B, bool taper, size_t spread_slots = 0) {
     std::vector<std::pair<size_t, size_t>> out;
     size_t first = 0;
     auto take = [&](size_t c) {
@@ -1063,6 +1072,12 @@ struct Engine::Impl {
       if (c) out.push_back({first, c});
       first += c;
     };
+    if (spread_slots > 0 && !taper && n > 0) {
+      size_t nb = (n + B - 1) / B;
+      if (nb < spread_slots) nb = std::max<size_t>(nb, std::min(spread_slots, n / kSpreadMin));
+      for (size_t b = 0; b < nb; ++b) take(n * (b + 1) / nb - n * b / nb);
+      return out;
+    }
     if (!taper || B < 16 || n <= 2 * B) {
       while (first < n) take(B);
       return out;
@@ -1185,7 +1200,8 @@ struct Engine::Impl {
     j->dirs = std::make_unique<IoDirs>(*j->items);
     j->on_start = std::move(on_start);
     j->status.resize(j->items->size());
-    j->batches = plan_batches(j->items->size(), (size_t)cfg.batch_size, cfg.taper);
+    j->batches = plan_batches(j->items->size(), (size_t)cfg.batch_size, cfg.taper,
+                              spread_ ? (size_t)cfg.streams : 0);
     j->remaining = j->batches.size();
     {
       std::lock_guard<std::mutex> g(job_m);
