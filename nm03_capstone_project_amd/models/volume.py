@@ -26,6 +26,13 @@ class VolumePipeline:
             runner = self._runners[dev] = native().VolumeRunner(dev)
         return runner.run(vol, self.config.pipeline_params(), self.connectivity, self.dilation, s)
 
+    def run_series(self, series_dir, seeds=None, device=None):
+        """A DICOM series directory as one volume (utils.read_series: the reference's file-number
+        order, every slice of one shape) through `run`."""
+        from ..utils.dicom import read_series
+        vol, _ = read_series(series_dir)
+        return self.run(vol, seeds=seeds, device=device)
+
     def run_slabs(self, volume=None, ctx=None, seeds=None, band=None, backend="auto", gather=True):
         """The same pipeline on a volume split into z-slabs over the ranks of `ctx` (one process per
         GPU, torch.distributed; parallel/volume_slabs.py). Returns the masks of the whole volume on

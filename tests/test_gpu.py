@@ -645,6 +645,23 @@ def test_volume_cli_gpu_equals_golden(native, cohort_root, tmp_path):
     assert j["gpus"] == 2 and len(j["per_rank_wall_s"]) == 2
 
 
+def test_volume_run_series_equals_golden(native, tmp_path):
+    """VolumePipeline.run_series on a DICOM series directory (written out of order on disk, 1-10
+    after 1-9) equals run() on the stacked planes and the golden 3D model."""
+    d, h, w = 12, 64, 80
+    planes = [native.phantom_slice(h, w, 2, z, d, 4) for z in range(d)]
+    for z in reversed(range(d)):
+        (tmp_path / f"1-{z + 1}.dcm").write_bytes(native.dicom_bytes(planes[z], instance=z + 1))
+    vp = nm.VolumePipeline(connectivity=6, dilation=7)
+    vol = np.stack(planes)
+    res = vp.run_series(str(tmp_path))
+    ref = vp.run(vol)
+    for k in ("band", "region", "dilated"):
+        assert np.array_equal(res[k], ref[k]), k
+    region, dil = vp.golden(res["band"], vp.default_seeds(vol))
+    assert np.array_equal(res["region"], region) and np.array_equal(res["dilated"], dil)
+
+
 def test_volume_runner_reuse_across_shapes(native):
     """One persistent VolumePipeline runner over volumes of changing shape and content: every
     result equals the golden of that volume (no stale buffers/tables from the previous run)."""
