@@ -89,8 +89,11 @@ def parse_args(argv=None):
     ap.add_argument("--wipe-passes", type=int, default=20,
                     help="also time this many passes that each first wipe their output directories (the "
                          "reference's per-run rm -rf; reported as config.wipe_each_pass; 0 = skip)")
-    ap.add_argument("--batch-size", type=int, default=64)
-    ap.add_argument("--streams", type=int, default=6)
+    # 96 slices × 4 slots: 5 batches per 465-slice pass instead of 8 at 64 × 6; won 10 of 11
+    # interleaved pairs on two boxes (median 324k vs 297k and 354k vs 324k slices/s) with less host
+    # CPU per step (profiles/r2/batch_streams/).
+    ap.add_argument("--batch-size", type=int, default=96)
+    ap.add_argument("--streams", type=int, default=4)
     ap.add_argument("--threads", type=int, default=0, help="host I/O threads per rank (0 = CPU budget / ranks, ≤16)")
     ap.add_argument("--comm", choices=("auto", "rccl", "host"), default=os.environ.get("NM03_COMM", "auto"))
     ap.add_argument("--data-root", default=os.environ.get("NM03_BENCH_DATA", os.path.join(_scratch(), "nm03_bench_data")))
