@@ -248,10 +248,12 @@ struct Engine::Impl {
   // NM03_PACK_BOUNCE=0: pack into a full-size intermediate and stream-copy it (A/B of pack_stream).
   bool pack_bounce_ = true;
   bool spread_ = false;  // plan_batches' spread schedule (NM03_BATCH_SPREAD)
+  bool interleave_exports_ = true;  // NM03_EXPORT_INTERLEAVE: writers round-robin over output directories
 
   explicit Impl(const EngineConfig& c) : cfg(c), place(c.device) {
     if (const char* e = std::getenv("NM03_BATCH_TAPER"); e && *e) cfg.taper = *e != '0';
     if (const char* e = std::getenv("NM03_BATCH_SPREAD"); e && *e) spread_ = *e != '0';
+    if (const char* e = std::getenv("NM03_EXPORT_INTERLEAVE"); e && *e) interleave_exports_ = *e != '0';
     if (const char* e = std::getenv("NM03_LOAD_MODE"); e && *e)
       read_mode_ = std::string(e) == "staged" ? dicom::ReadMode::kStaged
                    : std::string(e) == "mapped" ? dicom::ReadMode::kMapped
@@ -1009,10 +1011,37 @@ struct Engine::Impl {
           status[item] = SliceStatus{kSliceExportError, e.what()};
         }
       }
+      // Export order: round-robin over the batch's output directories, so the pool's concurrent
+      // writers spread over several patient directories. Creating a file takes its directory's
+      // lock exclusively; in slice order every writer would create in the same directory.
+      std::vector<int> order(s.live.size());
+      if (interleave_exports_ && dirs.fds.size() > 1) {
+        std::vector<std::pair<int32_t, std::vector<int>>> groups;  // (dir, live indices), first-seen order
+        for (size_t c = 0; c < s.live.size(); ++c) {
+          const int32_t d = dirs.out_fd[first + s.live[c]];
+          if (groups.empty() || groups.back().first != d) {
+            auto it = std::find_if(groups.begin(), groups.end(), [&](const auto& g) { return g.first == d; });
+            if (it == groups.end()) {
+              groups.push_back({d, {}});
+              it = groups.end() - 1;
+            }
+            it->second.push_back((int)c);
+          } else {
+            groups.back().second.push_back((int)c);
+          }
+        }
+        size_t o = 0;
+        for (size_t r = 0; o < order.size(); ++r)
+          for (auto& g : groups)
+            if (r < g.second.size()) order[o++] = g.second[r];
+      } else {
+        for (size_t c = 0; c < order.size(); ++c) order[c] = (int)c;
+      }
       TaskGroup tg(*pool);
       tg.for_each(
           s.live.size(),
-          [&](size_t c) {
+          [&](size_t oc) {
+            const size_t c = (size_t)order[oc];
             const size_t item = first + s.live[c];
             if (status[item].code != kSliceOk) return;
             const double t0 = now_s();
