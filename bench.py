@@ -101,6 +101,10 @@ def parse_args(argv=None):
     ap.add_argument("--keep-data", action="store_true", help="keep a generated dataset in tmpfs after the run")
     ap.add_argument("--keep-output", action="store_true")
     ap.add_argument("--graphs", action="store_true", help="hipGraph replay of the per-batch kernel chain")
+    ap.add_argument("--pipeline-depth", type=int, default=int(os.environ.get("NM03_BENCH_DEPTH", "0")),
+                    help="passes in flight (each with its own output tree); 0 = auto: 2, or 4 when the rank's "
+                         "shard is smaller than one batch per slot (strong scaling: a pass is then mostly "
+                         "latency, and more passes in flight overlap it)")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="one blocking engine call per pass; by default pass k+1 is submitted before pass k "
                          "finished (Engine.submit/wait) so the slot ring never drains between passes")
@@ -245,6 +249,11 @@ def run_rank(args):
                             device=device, graphs=args.graphs)
     engine = _DryEngine() if args.dry_run else n.Engine(cfg.engine_config())
 
+    def pipeline_depth(shard_len):
+        if args.pipeline_depth > 0:
+            return args.pipeline_depth
+        return 4 if shard_len < args.streams * args.batch_size else 2
+
     def shard(scaling, out_root):
         """This rank's work list: weak = its own cohort replica, strong = its block of one cohort."""
         replicas = world if scaling == "weak" else 1
@@ -257,10 +266,11 @@ def run_rank(args):
     def measure(scaling, out_root, steps, warmup, wipe=False):
         mine, global_items = shard(scaling, out_root)
         work = n.WorkList(mine)  # the shard's work list in native form (built once, like the plan)
-        # Pipelined passes alternate between two output trees: two runs in flight never write the
-        # same file (pass k+2 is submitted only after pass k finished).
-        trees = [mine, _pass_items(mine, out_root, 1)] if not args.no_pipeline else [mine]
-        works = [work, n.WorkList(trees[1])] if not args.no_pipeline else [work]
+        # Pipelined passes rotate over `depth` output trees: runs in flight never write the same
+        # file (pass k+depth is submitted only after pass k finished).
+        depth = 1 if args.no_pipeline else pipeline_depth(len(mine))
+        trees = [mine] + [_pass_items(mine, out_root, j) for j in range(1, depth)]
+        works = [work] + [n.WorkList(t) for t in trees[1:]]
         # wipe: every pass first empties its patients' output directories, as every reference run
         # does (setupOutputDirectory, main_sequential.cpp:32-47), so files are created, not rewritten.
         tree_dirs = [sorted({od for _, od in t}) for t in trees]
@@ -279,8 +289,8 @@ def run_rank(args):
             pending = []
             for k in range(k_total):
                 wipe_tree(k)
-                pending.append(engine.submit(works[k % 2]))
-                if len(pending) == 2:
+                pending.append(engine.submit(works[k % depth]))
+                if len(pending) == depth:
                     sink(*engine.wait(pending.pop(0)))
             for t in pending:
                 sink(*engine.wait(t))
@@ -340,6 +350,7 @@ def run_rank(args):
             "slices_ok": int(total_ok),
             "per_rank": per_rank,
             "own_time_imbalance": round(max(own) / max(min(own), 1e-12), 4),
+            "pipeline_depth": depth,
             "rank0_stage_s": {k: round(v, 4) for k, v in stage.items()},
             "rank0_process_cpu_ms_per_step": round(cpu_ms, 3),
             # rank 0's CPU per step by thread name (nm03-pool: loads + writes, nm03-slot: batch
@@ -390,6 +401,7 @@ def run_rank(args):
                 "threads": args.threads,
                 "stream_steps": bool(args.stream_steps),
                 "pipelined_passes": not args.no_pipeline and not args.stream_steps,
+                "pipeline_depth": primary["pipeline_depth"],
                 "comm": comm_info,
                 "rank0_stage_s": primary["rank0_stage_s"],
                 "cgroup_cpu_ms_per_step": primary["cgroup_cpu_ms_per_step"],
@@ -407,7 +419,7 @@ def run_rank(args):
         if secondary is not None:
             rec["config"][other] = {k: (round(v, 3) if isinstance(v, float) else v) for k, v in secondary.items()
                                     if k in ("value", "ms_per_step", "global_batch", "per_rank", "note",
-                                             "own_time_imbalance")}
+                                             "own_time_imbalance", "pipeline_depth")}
         print(json.dumps(rec), flush=True)
     comm.barrier()
     del engine
