@@ -209,10 +209,16 @@ void write_jpeg_at(int dirfd, const std::string& dir, const std::string& name, c
   // when the file exists), which serialises every writer of a patient directory: with a
   // per-directory hint, existing files are opened without it first, and once a directory is seen
   // to be empty (a fresh or wiped output tree) its files are created directly.
+  // A file this call creates (O_EXCL) is empty, so its size needs no fstat afterwards.
   int fd = -1;
+  bool fresh = false;
   if (creating && !creating->load(std::memory_order_relaxed)) {
     fd = ::openat(dirfd, name.c_str(), O_WRONLY | O_CLOEXEC);
     if (fd < 0 && errno == ENOENT) creating->store(1, std::memory_order_relaxed);
+  }
+  if (fd < 0 && creating) {
+    fd = ::openat(dirfd, name.c_str(), O_WRONLY | O_CREAT | O_EXCL | O_CLOEXEC, 0644);
+    fresh = fd >= 0;
   }
   if (fd < 0) fd = ::openat(dirfd, name.c_str(), O_WRONLY | O_CREAT | O_CLOEXEC, 0644);
   if (fd < 0) throw std::runtime_error("Cannot create " + path() + ": " + std::strerror(errno));
@@ -240,7 +246,7 @@ void write_jpeg_at(int dirfd, const std::string& dir, const std::string& name, c
     }
   }
   struct stat st;
-  if (fstat(fd, &st) == 0 && (size_t)st.st_size > total && ftruncate(fd, (off_t)total) != 0) {
+  if (!fresh && fstat(fd, &st) == 0 && (size_t)st.st_size > total && ftruncate(fd, (off_t)total) != 0) {
     ::close(fd);
     throw std::runtime_error("Truncate failed: " + path());
   }
