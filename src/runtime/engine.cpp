@@ -97,10 +97,10 @@ struct Slot {
   JpegWork jw;
   uint8_t* h_out = nullptr;
   uint8_t* d_out = nullptr;
-  // JPEG D2H mode (default): the encoder writes its segments to d_jraw (HBM, canvas k at k × out_cap),
-  // jpeg_gather_kernel packs them into d_jcomp and one SDMA copy moves the packed bytes into h_out
-  // (plain pinned memory); h_sizes stays host-mapped. Off (NM03_JPEG_D2H=0): the encoder stores
-  // straight into host-mapped h_out over PCIe.
+  // JPEG D2H modes (opt-in, NM03_JPEG_D2H=1/2, see jpeg_d2h_): the encoder writes its segments to
+  // d_jraw (HBM, canvas k at k × out_cap) and jpeg_gather_kernel packs them — into d_jcomp for one
+  // SDMA copy into h_out (plain pinned memory), or straight into host-mapped h_out; h_sizes stays
+  // host-mapped. Default (0): the encoder stores straight into host-mapped h_out over PCIe.
   uint8_t* d_jraw = nullptr;
   uint8_t* d_jcomp = nullptr;
   int32_t* d_jsizes = nullptr;
@@ -1019,16 +1019,12 @@ struct Engine::Impl {
         std::vector<std::pair<int32_t, std::vector<int>>> groups;  // (dir, live indices), first-seen order
         for (size_t c = 0; c < s.live.size(); ++c) {
           const int32_t d = dirs.out_fd[first + s.live[c]];
-          if (groups.empty() || groups.back().first != d) {
-            auto it = std::find_if(groups.begin(), groups.end(), [&](const auto& g) { return g.first == d; });
-            if (it == groups.end()) {
-              groups.push_back({d, {}});
-              it = groups.end() - 1;
-            }
-            it->second.push_back((int)c);
-          } else {
-            groups.back().second.push_back((int)c);
+          auto it = std::find_if(groups.rbegin(), groups.rend(), [&](const auto& g) { return g.first == d; });
+          if (it == groups.rend()) {
+            groups.push_back({d, {}});
+            it = groups.rbegin();
           }
+          it->second.push_back((int)c);
         }
         size_t o = 0;
         for (size_t r = 0; o < order.size(); ++r)
@@ -1091,7 +1087,8 @@ struct Engine::Impl {
   // plus a remainder (465 slices at B = 64: 8 × 58–59 instead of 7 × 64 + 17), and a list shorter
   // than one batch per slot (a rank's shard under strong scaling, one patient) split over up to
   // that many slots with at least kSpreadMin slices each, so its loads, uploads, kernels and
-  // writes overlap across slots instead of running as one batch.
+  // writes overlap across slots instead of running as one batch. Measured slower on the headline,
+  // config 2 and strong-scaling shards (profiles/r2/spread/): off by default.
   static constexpr size_t kSpreadMin = 8;
   static std::vector<std::pair<size_t, size_t>> plan_batches(size_t n, size_t B, bool taper, size_t spread_slots = 0) {
     std::vector<std::pair<size_t, size_t>> out;
