@@ -24,7 +24,7 @@ timeout -k 10 120 $B/nm03_bench --config cohort --data-root $T/patient/ --out /t
 timeout -k 10 120 $B/nm03_bench --config cpu-reference --data-root $T/patient/ --out /tmp/bl_o2c --steps 3 --warmup 1 --batch-size 25 --threads 16 > $O/c2_cpu.json || exit 122
 # config 3: full cohort (bench.py is the headline; native driver for the same work)
 timeout -k 10 300 python bench.py --steps 20 --warmup 3 --data-root $T/cohort > $O/c3_gpu_bench.json || exit 131
-timeout -k 10 120 $B/nm03_bench --config cohort --data-root $T/cohort/ --out /tmp/bl_o3 --steps 20 --warmup 3 --batch-size 64 --streams 6 > $O/c3_gpu_native.json || exit 132
+timeout -k 10 120 $B/nm03_bench --config cohort --data-root $T/cohort/ --out /tmp/bl_o3 --steps 20 --warmup 3 --batch-size 96 --streams 4 > $O/c3_gpu_native.json || exit 132
 timeout -k 10 300 $B/nm03_bench --config cpu-reference --data-root $T/cohort/ --out /tmp/bl_o3c --steps 2 --warmup 1 --batch-size 25 --threads 16 > $O/c3_cpu.json || exit 133
 echo "c3 done $(date)" >> $O/progress.txt
 # config 4: 512² × 10k, 5×5 median (CPU reference on a 400-slice subset of the same shape)
