@@ -43,6 +43,9 @@ def test_bench_self_launch_n_ranks(tmp_path, n):
     assert pr["slices"] == [float(cohort * 2)] * n
     # strong: one cohort sharded, every slice exactly once
     assert sum(rec["config"]["strong"]["per_rank"]["slices"]) == cohort * 2
+    # passes in flight: 2 for a full cohort per rank (465 ≥ 4 slots × 96), 4 for a shard below one
+    # batch per slot
+    assert rec["config"]["pipeline_depth"] == 2 and rec["config"]["strong"]["pipeline_depth"] == 4
 
 
 def test_bench_auto_comm_records_rccl_failure(tmp_path):
@@ -75,6 +78,10 @@ def test_bench_single_rank_dry(tmp_path):
     rec = _json_line(r.stdout)
     assert rec["n_gpus"] == 1 and rec["config"]["comm"]["backend"] == "self"
     assert rec["steps"] == 2 and rec["warmup"] == 1
+    r = _bench(tmp_path, "--pipeline-depth", "3", "--steps", "4", "--wipe-passes", "3")
+    assert r.returncode == 0, r.stderr
+    rec = _json_line(r.stdout)
+    assert rec["config"]["pipeline_depth"] == 3 and rec["config"]["per_rank"]["slices"] == [4.0 * 465]
 
 
 def test_bench_under_torchrun(tmp_path):
