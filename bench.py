@@ -94,7 +94,11 @@ def parse_args(argv=None):
     # CPU per step (profiles/r2/batch_streams/).
     ap.add_argument("--batch-size", type=int, default=96)
     ap.add_argument("--streams", type=int, default=4)
-    ap.add_argument("--threads", type=int, default=0, help="host I/O threads per rank (0 = CPU budget / ranks, ≤16)")
+    ap.add_argument("--threads", type=int, default=0,
+                    help="host I/O threads per rank (0 = the rank's CPU partition and budget share, ≤16)")
+    ap.add_argument("--single-passes", type=int, default=10,
+                    help="also time this many single strong-scaling passes (one cohort sharded over the "
+                         "ranks, nothing else in flight; config.strong.single_pass_ms; 0 = skip)")
     ap.add_argument("--comm", choices=("auto", "rccl", "host"), default=os.environ.get("NM03_COMM", "auto"))
     ap.add_argument("--data-root", default=os.environ.get("NM03_BENCH_DATA", os.path.join(_scratch(), "nm03_bench_data")))
     ap.add_argument("--out-root", default=os.environ.get("NM03_BENCH_OUT", os.path.join(_scratch(), "nm03_bench_out")))
@@ -112,6 +116,10 @@ def parse_args(argv=None):
                     help="submit the K timed cohort passes as one work stream (the engine pipelines across pass "
                          "boundaries as it does across patients) instead of one engine call per pass; every pass "
                          "writes its own output tree")
+    ap.add_argument("--host-only", action="store_true",
+                    help="host path only (EngineConfig.host_only): every DICOM load and JPEG write of a real "
+                         "run, the GPU stages replaced by fixed JPEG segments; measures slices per host "
+                         "CPU-second, no GPU needed. Not the headline metric (the JSON says so)")
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU rehearsal of the launcher, rendezvous, comm, sharding and aggregation: every step "
                          "of a real run except the engine (no GPU); the JSON value is meaningless")
@@ -176,6 +184,11 @@ def launch(args, argv, grace_s=5.0):
         if p.returncode not in (0, None) and rc == 0:
             rc = p.returncode if p.returncode > 0 else 128 - p.returncode
             print(f"bench: rank {r} exited with status {p.returncode}", file=sys.stderr, flush=True)
+    # A rank 0 killed before it unlinked the job's segment leaves it in /dev/shm (RAM): remove it.
+    try:
+        os.unlink(f"/dev/shm/nm03-comm-{job}")
+    except FileNotFoundError:
+        pass
     return rc
 
 
@@ -198,13 +211,13 @@ def _pass_items(items, out_root, k):
 class _DryEngine:
     """--dry-run stand-in for the native Engine: every slice 'succeeds' instantly."""
 
-    def submit(self, work):
+    def submit(self, work, batch_cap=0):
         return work
 
     def wait(self, work):
         return self.run_list(work)
 
-    def run_list(self, work):
+    def run_list(self, work, batch_cap=0):
         import numpy as np
         zero = {k: 0.0 for k in ("load_s", "load_cpu_s", "h2d_s", "kernels_s", "write_s", "write_cpu_s",
                                  "slot_cpu_s")}
@@ -216,20 +229,39 @@ def run_rank(args):
 
     import nm03_capstone_project_amd as nm
     from nm03_capstone_project_amd.parallel.cohort_runner import CohortPlan, plan_cohort
-    from nm03_capstone_project_amd.parallel.dist import auto_threads, cgroup_cpu_stat, shard_bounds
+    from nm03_capstone_project_amd.parallel.dist import cgroup_cpu_stat, shard_bounds
     from nm03_capstone_project_amd.parallel.native_comm import make_native_comm, rank_device, rank_env
     from nm03_capstone_project_amd.parallel.numa_data import (ensure_node_replicas, localize_items, numa_nodes,
                                                               replica_root)
 
     rank, world, local_rank, local_world = rank_env()
     device = rank_device(local_rank)
-    if args.threads <= 0:
-        args.threads = auto_threads(local_world)
     n = nm.native()
-    if torch.cuda.is_available():
+    gpu = torch.cuda.is_available()
+    if gpu:
         torch.cuda.set_device(device)
     comm, comm_info = make_native_comm(rank, world, device, args.comm)
     is_root = rank == 0
+
+    # Where this rank runs: its GPU's PCI bus id, and a CPU partition of that GPU's NUMA node that no
+    # other local rank shares, with a pool sized to it and to the rank's share of the CPU budget
+    # (numa.h; the reference has one machine-wide budget, main_parallel.cpp:401). All-gathered: the
+    # record shows N distinct devices, or the job fails when two ranks resolved to the same GPU
+    # without NM03_DEVICE_OVERRIDE asking for that.
+    shared_device = os.environ.get("NM03_DEVICE_OVERRIDE", "") != ""
+    rank_nodes = [n.numa_device_node(rank_device(r)) if gpu else -1 for r in range(local_world)]
+    part = n.rank_partition(rank_nodes, local_rank, n.cpu_budget())
+    if args.threads <= 0:
+        args.threads = part["threads"]
+    bus = n.device_bus_id(device) if gpu else ""
+    devices = comm.gather_rank_devices(device, bus, part["node"], n.format_cpulist(part["cpus"]), args.threads)
+    comm_info["nranks"] = comm.transport_size
+    dup = [(a, b) for a in range(world) for b in range(a + 1, world)
+           if devices[a]["bus_id"] and devices[a]["bus_id"] == devices[b]["bus_id"]]
+    if dup and not shared_device:
+        a, b = dup[0]
+        raise SystemExit(f"bench: ranks {a} and {b} resolved to the same GPU {devices[a]['bus_id']} "
+                         "(set NM03_DEVICE_OVERRIDE=<device> to share one GPU deliberately)")
 
     # Input cohort in tmpfs: one copy per NUMA node on multi-socket hosts (numa_data.py), so every
     # rank reads the copy on its own GPU's node.
@@ -247,7 +279,10 @@ def run_rank(args):
         os._exit(5)
     cfg = nm.PipelineConfig(batch_size=args.batch_size, streams=args.streams, threads=args.threads,
                             device=device, graphs=args.graphs)
-    engine = _DryEngine() if args.dry_run else n.Engine(cfg.engine_config())
+    ecfg = cfg.engine_config()
+    ecfg.cpus = part["cpus"]
+    ecfg.host_only = args.host_only
+    engine = _DryEngine() if args.dry_run else n.Engine(ecfg)
 
     def pipeline_depth(shard_len):
         if args.pipeline_depth > 0:
@@ -363,7 +398,33 @@ def run_rank(args):
                                        for k in ("usage_usec", "throttled_usec") if k in cg1},
         }
 
+    def single_pass(out_root, passes, capped):
+        """BASELINE config 3 as written, as a latency: ONE cohort sharded over the ranks, one engine
+        pass per rank, nothing else in flight; each pass bracketed by barriers, max over ranks.
+        `capped`: the shard cut into ⌈shard / streams⌉-slice batches, so its loads, uploads,
+        kernels and writes overlap across the slots (a 58-slice shard at 8 ranks is otherwise one
+        batch run stage after stage). Returns (median ms, min ms)."""
+        mine, _ = shard("strong", out_root)
+        work = n.WorkList(mine)
+        cap = -(-len(mine) // args.streams) if capped else 0
+        times = []
+        for k in range(passes + 1):  # pass 0 warms the output files
+            comm.barrier()
+            if gpu:
+                torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            codes, msgs, _ = engine.run_list(work, cap)
+            dt = time.perf_counter() - t0
+            if msgs:
+                raise SystemExit(f"rank {rank}: {len(msgs)} slices failed in the single pass")
+            dt = comm.allreduce_max([dt])[0]
+            if k:
+                times.append(dt)
+        times.sort()
+        return round(times[len(times) // 2] * 1e3, 4), round(times[0] * 1e3, 4)
+
     primary = measure(args.scaling, args.out_root, args.steps, args.warmup)
+    len_mine_primary = [primary["per_rank"]["slices"][rank] / args.steps]
     secondary = None
     other = "strong" if args.scaling == "weak" else "weak"
     if not args.no_secondary and world > 1:
@@ -374,6 +435,14 @@ def run_rank(args):
     wiped = None
     if args.wipe_passes > 0:
         wiped = measure(args.scaling, os.path.join(args.out_root, "wipe"), args.wipe_passes, 1, wipe=True)
+    sp = None
+    if args.single_passes > 0:
+        sp_root = os.path.join(args.out_root, "single")
+        med, best = single_pass(sp_root, args.single_passes, capped=True)
+        med_u, best_u = single_pass(sp_root, args.single_passes, capped=False)
+        sp = {"single_pass_ms": med, "single_pass_min_ms": best, "single_pass_batch_cap": "ceil(shard/streams)",
+              "single_pass_uncapped_ms": med_u, "single_pass_uncapped_min_ms": best_u,
+              "single_pass_passes": args.single_passes}
 
     if is_root:
         value = primary["value"]
@@ -420,6 +489,25 @@ def run_rank(args):
             rec["config"][other] = {k: (round(v, 3) if isinstance(v, float) else v) for k, v in secondary.items()
                                     if k in ("value", "ms_per_step", "global_batch", "per_rank", "note",
                                              "own_time_imbalance", "pipeline_depth")}
+        if sp is not None:
+            rec["config"].setdefault("strong", {}).update(sp)
+        if args.host_only:
+            rec["metric"] = "host path only: DICOM loads + JPEG writes per s (GPU stages replaced by fixed segments)"
+            rec["vs_baseline"] = None
+            rec["config"]["host_only"] = True
+        # Host efficiency: slices per second of this process's CPU time (rank 0).
+        cpu = primary["rank0_process_cpu_ms_per_step"]
+        rec["config"]["rank0_slices_per_cpu_s"] = round(len_mine_primary[0] / (cpu * 1e-3), 1) if cpu > 0 else None
+        # Device identity of every rank (PCI bus id, HIP index, NUMA node, CPU partition, pool size,
+        # and the communicator's own view: RCCL's ncclCommCount / ncclCommCuDevice).
+        pr = rec["config"]["per_rank"]
+        pr["device"] = [d["bus_id"] for d in devices]
+        pr["hip_device"] = [d["device"] for d in devices]
+        pr["numa_node"] = [d["numa_node"] for d in devices]
+        pr["cpus"] = [d["cpus"] for d in devices]
+        pr["threads"] = [d["threads"] for d in devices]
+        pr["transport_device"] = [d["transport_device"] for d in devices]
+        rec["config"]["comm"]["distinct_devices"] = len({d["bus_id"] for d in devices if d["bus_id"]})
         print(json.dumps(rec), flush=True)
     comm.barrier()
     del engine

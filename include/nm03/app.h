@@ -33,6 +33,9 @@ struct AppConfig {
   int repeat = 1;
   bool dilation_set = false;  // --dilation-size given (3D mode defaults to 7, BASELINE config 5)
   bool max_dim_set = false;   // --max-dim given (else the parallel CLI sizes buffers from the slice headers)
+  // --threads given. Otherwise every rank of the parallel CLI sizes its pool to its CPU partition
+  // and its share of the CPU budget (numa::rank_partition), at most the reference's 16.
+  bool threads_set = false;
 };
 
 // Parse the shared flag set; `which` selects CLI-specific defaults. Exits on --help.

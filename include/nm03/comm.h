@@ -38,6 +38,8 @@ class CommError : public std::runtime_error {
   explicit CommError(const std::string& m) : std::runtime_error(m) {}
 };
 
+class ShmSegment;
+
 class Comm {
  public:
   virtual ~Comm() = default;
@@ -50,6 +52,21 @@ class Comm {
   virtual void allreduce_sum_i64(int64_t* v, size_t n) = 0;
   virtual void allreduce_max_f64(double* v, size_t n) = 0;
   virtual void barrier() = 0;
+  // Neighbour exchange (collective: every rank calls it): send `sbytes` to rank `dst` and receive
+  // `rbytes` from rank `src`; -1 = no such peer. Used for z-slab halo planes. RCCL:
+  // grouped ncclSend/ncclRecv over xGMI; host comms: through the segment slots.
+  virtual void sendrecv(const void* send, size_t sbytes, int dst, void* recv, size_t rbytes, int src) = 0;
+
+  // What the transport itself reports — RCCL: ncclCommCount / ncclCommUserRank / ncclCommCuDevice —
+  // so a run record can show that N ranks really formed one communicator over N devices. Host
+  // comms report size() / rank() / -1.
+  virtual int transport_size() const { return size(); }
+  virtual int transport_rank() const { return rank(); }
+  virtual int transport_device() const { return -1; }
+  // Watch this segment's job abort flag in every bounded wait from now on (RCCL; the host comms
+  // always do). Lets a driver bring a communicator up without the flag — a failed init must not
+  // abort the job when a fallback exists — and attach it once every rank agreed.
+  virtual void set_abort_segment(std::shared_ptr<ShmSegment>) {}
 
   // Helpers built on the primitives.
   void broadcast_bytes(std::vector<uint8_t>& buf, int root);                        // resizes on non-roots
@@ -145,6 +162,25 @@ struct LaunchOptions {
 // (PR_SET_PDEATHSIG). Rank r runs body(r, n, comm) on device opts.device_of(r).
 int launch_ranks(int n, const std::function<int(int rank, int size, Comm& comm)>& body,
                  const LaunchOptions& opts = LaunchOptions::from_env());
+
+// ---- rank ↔ device identity ----------------------------------------------------------------------
+// What every rank records about where it runs, all-gathered before the engines start, so a run
+// record (CLI --json, bench JSON) answers "did N ranks really drive N distinct GPUs?" by itself.
+struct RankDevice {
+  int device = -1;          // HIP device index
+  std::string bus_id;       // PCI bus id of that device (numa::device_bus_id)
+  int node = -1;            // its NUMA node
+  std::string cpus;         // the rank's CPU partition (cpulist form)
+  int threads = 0;          // host pool threads
+  int transport_size = 0;   // Comm::transport_size() (RCCL: ncclCommCount)
+  int transport_device = -1;  // Comm::transport_device() (RCCL: ncclCommCuDevice)
+  std::string error;        // set-up failure on this rank ("" = fine)
+};
+std::vector<RankDevice> gather_rank_devices(Comm& comm, const RankDevice& mine);
+// "ranks a and b resolved to the same GPU <bus>" for the first duplicate bus id, "" if none.
+std::string duplicate_device(const std::vector<RankDevice>& all);
+// JSON object of per-rank arrays {"device": [...], "bus_id": [...], ...}.
+std::string rank_devices_json(const std::vector<RankDevice>& all);
 
 // Simple binary (de)serialisation helpers for messages.
 struct ByteWriter {

@@ -60,6 +60,9 @@ struct EngineConfig {
   int batch_size = 25;  // main_parallel.cpp:33
   int streams = 3;      // batches in flight
   int threads = 16;     // host pool (omp_set_num_threads(16), main_parallel.cpp:401)
+  // CPUs the pool, slot threads and pinned allocations are bound to (a rank's partition of its
+  // GPU's NUMA node, numa::rank_partition). Empty: the whole node of the GPU (multi-node hosts).
+  std::vector<int> cpus;
   int max_dim = 512;    // buffers sized for slices up to max_dim × max_dim
   PipelineParams pipe;
   RenderParams render;
@@ -75,6 +78,12 @@ struct EngineConfig {
   // measured 209k vs 220k slices/s (4 interleaved runs each) — the extra batches cost more than the
   // shorter fill/drain gains. NM03_BATCH_TAPER=1 turns it on.
   bool taper = false;
+  // Host path only (NM03_HOST_ONLY=1 also turns it on): no HIP call at all. Every load, parse,
+  // 12-bit pack into the (pageable) upload blob and every JPEG file write runs exactly as in a
+  // GPU run; the GPU stages are replaced by streaming a fixed pair of pre-encoded JPEG segments
+  // into the output buffer (what the encoder's PCIe stores would leave in memory). Measures the
+  // host side's CPU per slice on its own, on any machine (bench.py --host-only).
+  bool host_only = false;
 };
 
 // Everything test_pipeline exports / tests inspect for one slice (host copies).
@@ -101,15 +110,19 @@ class Engine {
 
   // Process all items (blocking). on_start(i) is called when item i starts loading (used by the
   // sequential CLI to print "Processing: ..." at the right moment).
+  // `batch_cap` > 0: batches of at most that many slices for this run (≤ batch_size). A short list
+  // (a rank's shard under strong scaling) cut into ⌈n / streams⌉-slice batches spreads over every
+  // slot, so its loads, uploads, kernels and writes overlap instead of running as one batch.
   std::vector<SliceStatus> run(const std::vector<WorkItem>& items, StageTimes* times = nullptr,
-                               const std::function<void(size_t)>& on_start = {});
+                               const std::function<void(size_t)>& on_start = {}, int batch_cap = 0);
 
   // Asynchronous form: queue a run and return at once. Runs are processed in submission order,
   // and the slots move on to a queued run's batches while the previous run drains, so a caller
   // that keeps the next run submitted (double buffering) never pays the slot ring's fill/drain
   // between runs. `items` stays shared with the engine until the run finished. Two runs in flight
   // must not write the same output files.
-  RunTicket submit(std::shared_ptr<const std::vector<WorkItem>> items, std::function<void(size_t)> on_start = {});
+  RunTicket submit(std::shared_ptr<const std::vector<WorkItem>> items, std::function<void(size_t)> on_start = {},
+                   int batch_cap = 0);
   // Blocks until the run finished; rethrows an engine error of that run.
   std::vector<SliceStatus> wait(const RunTicket& ticket, StageTimes* times = nullptr);
 

@@ -26,13 +26,13 @@ namespace nm03 {
 // last batches' exports are not queued behind anything (drain).
 class ThreadPool {
  public:
-  // `on_start` runs first on every worker thread (e.g. NUMA pinning).
-  explicit ThreadPool(int n, std::function<void()> on_start = {}) {
+  // `on_start(i)` runs first on worker thread i (e.g. CPU pinning).
+  explicit ThreadPool(int n, std::function<void(int)> on_start = {}) {
     if (n < 1) n = 1;
     for (int i = 0; i < n; ++i)
-      workers_.emplace_back([this, on_start] {
+      workers_.emplace_back([this, on_start, i] {
         pthread_setname_np(pthread_self(), "nm03-pool");  // per-thread CPU accounting (bench.py)
-        if (on_start) on_start();
+        if (on_start) on_start(i);
         loop();
       });
   }

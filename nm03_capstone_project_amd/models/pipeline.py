@@ -51,6 +51,7 @@ class PipelineConfig:
     resume: bool = False
     graphs: bool = False  # replay per-batch kernel chains from captured hipGraphs (slower, see engine.h)
     taper: bool = False  # small first/last batches (measured slower, see engine.h)
+    host_only: bool = False  # host path only, no GPU (loads + JPEG writes with fixed segments, engine.h)
 
     _PIPE = ("norm_low", "norm_high", "norm_min", "norm_max", "clip_min", "clip_max", "median_window",
              "sharpen_gain", "sharpen_sigma", "sharpen_mask", "srg_min", "srg_max", "srg_connectivity",
@@ -82,6 +83,7 @@ class PipelineConfig:
         c.resume = self.resume
         c.graphs = self.graphs
         c.taper = self.taper
+        c.host_only = self.host_only
         return c
 
     def replace(self, **kw):

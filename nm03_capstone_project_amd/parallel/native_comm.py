@@ -1,18 +1,19 @@
 """Native communicators for independently launched rank processes (torchrun or bench.py's own
 launcher): the same C++ `Comm` the CLI uses (src/dist/: RcclComm over xGMI, HostComm over a
-process-shared segment).
+process-shared segment). No torch.distributed anywhere.
 
-Rendezvous: bench.py's launcher hands every rank a job id (NM03_COMM_JOB) that names the segment;
-under torchrun, rank 0 publishes the segment name through the env:// TCPStore (shared with the
-torchrun agent when TORCHELASTIC_USE_AGENT_STORE is set) — the only use of torch here. Every
-collective runs in native code with deadlines (NM03_COMM_TIMEOUT_S).
+Rendezvous (one node): every rank derives the same segment name without talking to the others —
+from bench.py's job id (NM03_COMM_JOB), or under torchrun from the agent that spawned the local
+ranks (its pid and start time, which no other process shares, plus MASTER_PORT). Rank 0 creates the
+segment, the others attach; the RCCL unique id and the agreement on whether RCCL came up on every
+rank go over it. Every collective runs in native code with deadlines (NM03_COMM_TIMEOUT_S).
 
 Backend choice (`backend` or NM03_COMM): "rccl" | "host" | "auto". auto = RCCL when every rank has
 its own GPU, host when ranks share one (NM03_DEVICE_OVERRIDE; RCCL refuses two ranks per device),
 and — auto only — the host comm when RCCL initialisation fails on any rank, with the failure
 recorded in the returned info (never silent)."""
+import atexit
 import os
-from datetime import timedelta
 
 from .._native import native
 
@@ -45,39 +46,46 @@ def resolve_backend(world, backend=None):
     return ("rccl", True) if be == "auto" else (be, False)
 
 
-def _store(rank, world, timeout_s):
-    import torch.distributed as dist
-    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-    store, _, _ = next(dist.rendezvous("env://", rank=rank, world_size=world, timeout=timedelta(seconds=timeout_s)))
-    return dist.PrefixStore("nm03_comm", store)
+def _proc_start_time(pid):
+    """Start time of `pid` in clock ticks since boot (field 22 of /proc/<pid>/stat)."""
+    with open(f"/proc/{pid}/stat") as f:
+        st = f.read()
+    return st[st.rindex(")") + 2:].split()[19]
+
+
+def segment_name():
+    """Segment name every local rank of this job derives on its own: bench.py's job id, or the
+    spawning agent's (pid, start time) + MASTER_PORT under torchrun. (pid, start time) names one
+    process since boot, so a segment left behind by an earlier job can never be picked up."""
+    job = os.environ.get("NM03_COMM_JOB", "")
+    if job:
+        return f"/nm03-comm-{job}"
+    ppid = os.getppid()
+    return f"/nm03-comm-{ppid}-{_proc_start_time(ppid)}-{os.environ.get('MASTER_PORT', '0')}"
+
+
+def unlink_segment(name):
+    """Remove a job's named segment if it is still there (a rank 0 that died before unlinking)."""
+    try:
+        os.unlink("/dev/shm" + name)
+    except FileNotFoundError:
+        pass
 
 
 def make_native_comm(rank, world, device, backend=None, timeout_s=None):
     """Returns (comm, info). `comm` is a native `Comm` (rank/size/backend, barrier,
-    broadcast_bytes, allgather_bytes, allreduce_sum/max, allgather_f64); `info` records the backend
-    used and, if RCCL was abandoned under auto, why.
-
-    Rendezvous: with NM03_COMM_JOB set (bench.py's launcher hands every rank the same job id) the
-    segment name derives from it; otherwise (torchrun) rank 0 publishes a fresh name through the
-    env:// rendezvous store. Everything after that — the RCCL unique id, the agreement on whether
-    RCCL came up on every rank — goes over the shared segment."""
+    broadcast_bytes, allgather_bytes, allreduce_sum/max, allgather_f64, sendrecv); `info` records the
+    backend used and, if RCCL was abandoned under auto, why."""
     n = native()
     if world <= 1:
         return n.self_comm(), {"backend": "self"}
     timeout_s = float(timeout_s or n.comm_timeout_s())
     be, may_fall_back = resolve_backend(world, backend)
-    job = os.environ.get("NM03_COMM_JOB", "")
-    if job:
-        name = f"/nm03-comm-{job}"
-        seg = n.shm_create(world, name)[0] if rank == 0 else n.shm_attach(name, world, timeout_s)
-    else:
-        store = _store(rank, world, timeout_s)
-        if rank == 0:
-            seg, name = n.shm_create(world)
-            store.set("shm", name)
-        else:
-            store.wait(["shm"], timedelta(seconds=timeout_s))
-            seg = n.shm_attach(store.get("shm").decode(), world, timeout_s)
+    name = segment_name()
+    seg = n.shm_create(world, name)[0] if rank == 0 else n.shm_attach(name, world, timeout_s)
+    # Every rank removes the name at exit in case rank 0 died before unlinking it (all ranks have
+    # attached before any collective returns, so this never races an attach).
+    atexit.register(unlink_segment, name)
     if rank == 0:
         seg.wait_attached_and_unlink(timeout_s)
     host = n.host_comm(seg, rank, timeout_s)
@@ -96,8 +104,9 @@ def make_native_comm(rank, world, device, backend=None, timeout_s=None):
     comm = None
     if uid:
         try:
-            # No segment for RCCL's own waits: a timed-out init must not raise the segment's abort
-            # flag, which would also fail the agreement below and with it the host fallback.
+            # No segment for RCCL's own waits during init: a timed-out init must not raise the
+            # segment's abort flag, which would also fail the agreement below and with it the
+            # host fallback. The segment is attached once every rank agreed.
             comm = n.rccl_comm(rank, world, uid, device, None, min(timeout_s, 60.0))  # init is seconds
         except Exception as e:  # noqa: BLE001
             err = f"{type(e).__name__}: {e}"
@@ -107,6 +116,9 @@ def make_native_comm(rank, world, device, backend=None, timeout_s=None):
     errs = [e.decode() for e in agree.allgather_bytes(err.encode())]
     bad = [(r, e) for r, e in enumerate(errs) if e]
     if not bad:
+        # From here on a peer that dies is noticed through the abort flag within milliseconds,
+        # not at the collective deadline.
+        comm.set_abort_segment(seg)
         return comm, info
     if not may_fall_back:
         raise RuntimeError(f"RCCL initialisation failed on rank(s) {bad}")

@@ -25,6 +25,7 @@
 #include "nm03/jpeg.h"
 #include "nm03/log.h"
 #include "nm03/metaimage.h"
+#include "nm03/numa.h"
 #include "nm03/volume.h"
 
 namespace nm03::app {
@@ -43,7 +44,7 @@ void usage(const std::string& which) {
             << "  --device N             GPU for a single-rank run\n"
             << "  --batch-size N         slices per GPU batch (default 25)\n"
             << "  --streams N            batches in flight per GPU (default 3)\n"
-            << "  --threads N            host I/O threads per rank (default 16)\n"
+            << "  --threads N            host I/O threads per rank (parallel default: the rank's CPU share, ≤ 16)\n"
             << "  --median-window K      3|5|7|9 (default 7)\n"
             << "  --srg-connectivity C   4|8 (2D) / 6|26 (3D)\n"
             << "  --dilation-size S      (default 3; 7 in --mode 3d)    --erosion-size S (default 3)\n"
@@ -133,7 +134,10 @@ AppConfig parse_args(int argc, char** argv, const std::string& which) {
     } else if (a == "--device") c.engine.device = std::atoi(val().c_str());
     else if (a == "--batch-size") c.engine.batch_size = std::atoi(val().c_str());
     else if (a == "--streams") c.engine.streams = std::atoi(val().c_str());
-    else if (a == "--threads") c.engine.threads = std::atoi(val().c_str());
+    else if (a == "--threads") {
+      c.engine.threads = std::atoi(val().c_str());
+      c.threads_set = true;
+    }
     else if (a == "--median-window") c.engine.pipe.median_window = std::atoi(val().c_str());
     else if (a == "--srg-connectivity") c.engine.pipe.srg_connectivity = std::atoi(val().c_str());
     else if (a == "--dilation-size") {
@@ -384,7 +388,8 @@ int scan_max_dim(const std::vector<PatientPlan>& plan, int threads) {
   return md.load();
 }
 
-int parallel_rank(const AppConfig& cfg, int rank, int size, Comm& comm, int device) {
+// `rank_devices`: the HIP device of every rank (one node), for the CPU partition of this rank.
+int parallel_rank(const AppConfig& cfg, int rank, int size, Comm& comm, int device, const std::vector<int>& rank_devices) {
   const std::string base = cohort::cohort_dir(cfg.data_root);
   EngineConfig ec = cfg.engine;
   ec.device = device;
@@ -414,6 +419,7 @@ int parallel_rank(const AppConfig& cfg, int rank, int size, Comm& comm, int devi
     }
   } joiner{warm};
   std::unique_ptr<Engine> engine_p;
+  std::vector<RankDevice> devices;
   double t_start = 0, setup_s = 0;
   double proc_wall = 0, my_wall = 0;
   int64_t total_ok = 0, total_slices = 0, my_slices = 0, my_ok = 0;
@@ -480,6 +486,34 @@ int parallel_rank(const AppConfig& cfg, int rank, int size, Comm& comm, int devi
       // the 512² maximum: less pinned memory to allocate and register at start-up.
       if (seen_dim > 0) ec.max_dim = std::min(gpu::kMaxSliceDim, std::max(64, (int)((seen_dim + 63) / 64 * 64)));
       warm.join();
+      // Where this rank runs: its GPU's PCI bus id, and a CPU partition of that GPU's NUMA node
+      // disjoint from every other rank's, with a pool sized to it and to the rank's share of the
+      // CPU budget (the reference's one machine-wide omp_set_num_threads(16), main_parallel.cpp:401).
+      // All-gathered: a record of N distinct devices, or a fatal error when two ranks resolved to
+      // the same GPU without NM03_DEVICE_OVERRIDE asking for that.
+      {
+        RankDevice me;
+        me.device = device;
+        me.bus_id = numa::device_bus_id(device);
+        std::vector<int> rank_nodes;
+        for (int d : rank_devices) rank_nodes.push_back(numa::device_node(d));
+        const numa::RankCpus part = numa::rank_partition(numa::read_topology(), rank_nodes, rank, numa::cpu_budget());
+        if (!cfg.threads_set) ec.threads = part.threads;
+        ec.cpus = part.cpus;
+        me.node = part.node;
+        me.cpus = numa::format_cpulist(part.cpus);
+        me.threads = ec.threads;
+        me.transport_size = comm.transport_size();
+        me.transport_device = comm.transport_device();
+        devices = gather_rank_devices(comm, me);
+        const std::string dup = duplicate_device(devices);
+        if (!dup.empty() && LaunchOptions::from_env().device_override < 0) {
+          if (rank == 0)
+            std::cerr << "Fatal error: " << dup << " (set NM03_DEVICE_OVERRIDE=<device> to share one GPU deliberately)"
+                      << std::endl;
+          return 1;
+        }
+      }
       // An engine that fails to come up on one rank must not leave the others blocked in the next
       // collective: agree on it before going on.
       std::string setup_error;
@@ -572,7 +606,7 @@ int parallel_rank(const AppConfig& cfg, int rank, int size, Comm& comm, int devi
         std::cout << "Using series directory: " << pp.series_dir << std::endl;                                 // :280
         std::cout << "Found " << pp.files.size() << " DICOM files for patient " << pp.id << std::endl;          // :301
         std::cout << "Found " << pp.files.size() << " images to process for patient " << pp.id << std::endl;    // :324
-        std::cout << "Using " << cfg.engine.threads << " threads\n" << std::endl;                              // :326
+        std::cout << "Using " << engine.config().threads << " threads\n" << std::endl;                         // :326
         int ok = 0;
         for (size_t i = 0; i < pp.files.size(); ++i, ++cursor) {
           if (!cfg.quiet) std::cout << "Processing: \"" << cohort::filename(pp.files[i]) << "\"" << std::endl;  // :72-73
@@ -620,7 +654,9 @@ int parallel_rank(const AppConfig& cfg, int rank, int size, Comm& comm, int devi
                              fmt(total_ok / std::max(proc_wall, 1e-9)) + ", \"rank0\": {\"load_s\": " + fmt(agg.load_s) +
                              ", \"h2d_s\": " + fmt(agg.h2d_s) + ", \"kernels_s\": " + fmt(agg.kernels_s) +
                              ", \"write_s\": " + fmt(agg.write_s) + ", \"jpeg_fallbacks\": " +
-                             std::to_string(agg.jpeg_fallbacks) + "}, \"per_rank\": " + per_rank_json(rows) + "}");
+                             std::to_string(agg.jpeg_fallbacks) + "}, \"per_rank\": " + per_rank_json(rows) +
+                             ", \"comm\": {\"backend\": \"" + comm.backend() + "\", \"nranks\": " +
+                             std::to_string(comm.transport_size()) + "}, \"devices\": " + rank_devices_json(devices) + "}");
   }
   if (fast_exit_enabled()) (void)engine_p.release();  // the process ends in cli_exit: no teardown
   return 0;
@@ -659,9 +695,11 @@ int run_parallel(const AppConfig& cfg) {
     if (cfg.mode == "3d") return run_volume_cohort(cfg);
     LaunchOptions lo = LaunchOptions::from_env();
     const int n = resolve_gpus(cfg, lo);
+    std::vector<int> rank_devices;
+    for (int r = 0; r < n; ++r)
+      rank_devices.push_back(n > 1 ? lo.device_of(r) : lo.device_override >= 0 ? lo.device_override : cfg.engine.device);
     return launch_ranks(n, [&](int rank, int size, Comm& comm) {
-      const int dev = size > 1 ? lo.device_of(rank) : lo.device_override >= 0 ? lo.device_override : cfg.engine.device;
-      return parallel_rank(cfg, rank, size, comm, dev);
+      return parallel_rank(cfg, rank, size, comm, rank_devices[(size_t)rank], rank_devices);
     }, lo);
   } catch (const std::exception& e) {
     std::cerr << "Fatal error: " << e.what() << std::endl;  // :407-408

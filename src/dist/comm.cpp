@@ -87,6 +87,67 @@ std::vector<std::vector<uint8_t>> Comm::allgather_bytes(const std::vector<uint8_
   return out;
 }
 
+std::vector<RankDevice> gather_rank_devices(Comm& comm, const RankDevice& m) {
+  ByteWriter w;
+  w.i32(m.device);
+  w.str(m.bus_id);
+  w.i32(m.node);
+  w.str(m.cpus);
+  w.i32(m.threads);
+  w.i32(m.transport_size);
+  w.i32(m.transport_device);
+  w.str(m.error);
+  std::vector<RankDevice> out;
+  for (const auto& b : comm.allgather_bytes(w.b)) {
+    ByteReader r(b.data(), b.size());
+    RankDevice d;
+    d.device = r.i32();
+    d.bus_id = r.str();
+    d.node = r.i32();
+    d.cpus = r.str();
+    d.threads = r.i32();
+    d.transport_size = r.i32();
+    d.transport_device = r.i32();
+    d.error = r.str();
+    out.push_back(std::move(d));
+  }
+  return out;
+}
+
+std::string duplicate_device(const std::vector<RankDevice>& all) {
+  for (size_t a = 0; a < all.size(); ++a)
+    for (size_t b = a + 1; b < all.size(); ++b)
+      if (!all[a].bus_id.empty() && all[a].bus_id == all[b].bus_id)
+        return "ranks " + std::to_string(a) + " and " + std::to_string(b) + " resolved to the same GPU " + all[a].bus_id;
+  return "";
+}
+
+namespace {
+std::string json_str(const std::string& s) {
+  std::string o = "\"";
+  for (char c : s) {
+    if (c == '"' || c == '\\') o += '\\';
+    if ((unsigned char)c >= 0x20) o += c;
+  }
+  return o + "\"";
+}
+}  // namespace
+
+std::string rank_devices_json(const std::vector<RankDevice>& all) {
+  auto arr = [&](const char* key, auto get) {
+    std::string o = std::string("\"") + key + "\": [";
+    for (size_t r = 0; r < all.size(); ++r) o += (r ? ", " : "") + get(all[r]);
+    return o + "]";
+  };
+  return "{" + arr("device", [](const RankDevice& d) { return std::to_string(d.device); }) + ", " +
+         arr("bus_id", [](const RankDevice& d) { return json_str(d.bus_id); }) + ", " +
+         arr("numa_node", [](const RankDevice& d) { return std::to_string(d.node); }) + ", " +
+         arr("cpus", [](const RankDevice& d) { return json_str(d.cpus); }) + ", " +
+         arr("threads", [](const RankDevice& d) { return std::to_string(d.threads); }) + ", " +
+         arr("transport_size", [](const RankDevice& d) { return std::to_string(d.transport_size); }) + ", " +
+         arr("transport_device", [](const RankDevice& d) { return std::to_string(d.transport_device); }) + "}";
+}
+
 namespace {
 
 // Reductions shared by the host-memory comms: all-gather, then fold in rank order.
@@ -150,6 +211,15 @@ class LoopbackComm final : public Comm {
     fold_allgather(*this, v, n, [](double a, double b) { return std::max(a, b); });
   }
   void barrier() override { hub_->sync(); }
+  void sendrecv(const void* send, size_t sbytes, int dst, void* recv, size_t rbytes, int src) override {
+    hub_->slots[rank_].assign((const uint8_t*)send, (const uint8_t*)send + (dst >= 0 ? sbytes : 0));
+    hub_->sync();
+    if (src >= 0) {
+      if (hub_->slots[src].size() != rbytes) throw CommError("sendrecv: size mismatch with the sender");
+      std::memcpy(recv, hub_->slots[src].data(), rbytes);
+    }
+    hub_->sync();
+  }
 
  private:
   std::shared_ptr<Hub> hub_;
@@ -166,6 +236,12 @@ class SelfComm final : public Comm {
   void allreduce_sum_i64(int64_t*, size_t) override {}
   void allreduce_max_f64(double*, size_t) override {}
   void barrier() override {}
+  void sendrecv(const void* send, size_t sbytes, int dst, void* recv, size_t rbytes, int src) override {
+    if (dst == 0 && src == 0) {
+      if (sbytes != rbytes) throw CommError("sendrecv: size mismatch with the sender");
+      std::memmove(recv, send, rbytes);
+    }
+  }
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -209,6 +285,21 @@ class HostComm final : public Comm {
     fold_allgather(*this, v, n, [](double a, double b) { return std::max(a, b); });
   }
   void barrier() override { seg_->barrier(rank_, timeout_); }
+  void sendrecv(const void* send, size_t sbytes, int dst, void* recv, size_t rbytes, int src) override {
+    // Every rank must run the same number of slot rounds: agree on the largest message first.
+    int64_t len = dst >= 0 ? (int64_t)sbytes : 0;
+    std::vector<int64_t> lens((size_t)size());
+    allgather(&len, sizeof(len), lens.data());
+    if (src >= 0 && lens[(size_t)src] != (int64_t)rbytes) throw CommError("sendrecv: size mismatch with the sender");
+    const size_t mx = (size_t)*std::max_element(lens.begin(), lens.end());
+    const size_t cap = seg_->slot_bytes();
+    for (size_t off = 0; off < mx; off += cap) {
+      if (off < (size_t)len) std::memcpy(seg_->slot(rank_), (const uint8_t*)send + off, std::min(cap, (size_t)len - off));
+      seg_->barrier(rank_, timeout_);
+      if (src >= 0 && off < rbytes) std::memcpy((uint8_t*)recv + off, seg_->slot(src), std::min(cap, rbytes - off));
+      seg_->barrier(rank_, timeout_);
+    }
+  }
 
  private:
   std::shared_ptr<ShmSegment> seg_;

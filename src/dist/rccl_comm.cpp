@@ -78,6 +78,38 @@ class RcclComm final : public Comm {
     int64_t one = 1;
     allreduce_sum_i64(&one, 1);
   }
+  void sendrecv(const void* send, size_t sbytes, int dst, void* recv, size_t rbytes, int src) override {
+    if (dst < 0) sbytes = 0;
+    if (src < 0) rbytes = 0;
+    if (!sbytes && !rbytes) return;
+    uint8_t* d = stage(sbytes + rbytes);
+    uint8_t* drecv = d + sbytes;
+    if (sbytes) hip_ck(hipMemcpyAsync(d, send, sbytes, hipMemcpyHostToDevice, stream_), "H2D");
+    // One group: the send to the successor and the receive from the predecessor progress
+    // together (a halo exchange where every rank sends first would otherwise deadlock).
+    issue(ncclGroupStart(), "ncclGroupStart");
+    if (sbytes) issue(ncclSend(d, sbytes, ncclUint8, dst, comm_, stream_), "ncclSend");
+    if (rbytes) issue(ncclRecv(drecv, rbytes, ncclUint8, src, comm_, stream_), "ncclRecv");
+    issue(ncclGroupEnd(), "ncclGroupEnd");
+    if (rbytes) hip_ck(hipMemcpyAsync(recv, drecv, rbytes, hipMemcpyDeviceToHost, stream_), "D2H");
+    wait("ncclSend/ncclRecv");
+  }
+  int transport_size() const override {
+    int n = -1;
+    if (!comm_ || ncclCommCount(comm_, &n) != ncclSuccess) return -1;
+    return n;
+  }
+  int transport_rank() const override {
+    int r = -1;
+    if (!comm_ || ncclCommUserRank(comm_, &r) != ncclSuccess) return -1;
+    return r;
+  }
+  int transport_device() const override {
+    int d = -1;
+    if (!comm_ || ncclCommCuDevice(comm_, &d) != ncclSuccess) return -1;
+    return d;
+  }
+  void set_abort_segment(std::shared_ptr<ShmSegment> seg) override { seg_ = std::move(seg); }
 
  private:
   void reduce(void* v, size_t n, ncclDataType_t t, ncclRedOp_t op) {

@@ -264,13 +264,15 @@ PYBIND11_MODULE(_nm03, m) {
       .def_readwrite("batch_size", &EngineConfig::batch_size)
       .def_readwrite("streams", &EngineConfig::streams)
       .def_readwrite("threads", &EngineConfig::threads)
+      .def_readwrite("cpus", &EngineConfig::cpus)
       .def_readwrite("max_dim", &EngineConfig::max_dim)
       .def_readwrite("pipe", &EngineConfig::pipe)
       .def_readwrite("render", &EngineConfig::render)
       .def_readwrite("export_jpeg", &EngineConfig::export_jpeg)
       .def_readwrite("resume", &EngineConfig::resume)
       .def_readwrite("graphs", &EngineConfig::graphs)
-      .def_readwrite("taper", &EngineConfig::taper);
+      .def_readwrite("taper", &EngineConfig::taper)
+      .def_readwrite("host_only", &EngineConfig::host_only);
 
   m.def("reference_seeds", [](int w, int h) {
     std::vector<std::pair<int, int>> v;
@@ -361,6 +363,28 @@ PYBIND11_MODULE(_nm03, m) {
   });
   m.def("numa_node_cpus", &numa::node_cpus);
   m.def("numa_device_node", &numa::device_node, py::arg("device"));
+  m.def("device_bus_id", &numa::device_bus_id, py::arg("device"));
+  m.def("cpu_budget", &numa::cpu_budget, py::arg("cgroup_root") = "/sys/fs/cgroup");
+  m.def("allowed_cpus", &numa::allowed_cpus);
+  m.def("format_cpulist", &numa::format_cpulist);
+  // Per-rank CPU partition (numa.h): {node, index, count, cpus, threads}. `sysfs` / `allowed` let
+  // tests describe a fake host.
+  m.def(
+      "rank_partition",
+      [](const std::vector<int>& rank_nodes, int local_rank, int budget, int cap, const std::string& sysfs,
+         const std::vector<int>& allowed) {
+        const numa::Topology t = numa::read_topology(sysfs, allowed);
+        const numa::RankCpus r = numa::rank_partition(t, rank_nodes, local_rank, budget, cap);
+        py::dict d;
+        d["node"] = r.node;
+        d["index"] = r.index;
+        d["count"] = r.count;
+        d["cpus"] = r.cpus;
+        d["threads"] = r.threads;
+        return d;
+      },
+      py::arg("rank_nodes"), py::arg("local_rank"), py::arg("budget"), py::arg("cap") = 16,
+      py::arg("sysfs") = "/sys", py::arg("allowed") = std::vector<int>{});
   m.def(
       "read_pixels_direct",
       [](const std::string& path, const std::string& mode, size_t prefix) {
@@ -604,23 +628,25 @@ PYBIND11_MODULE(_nm03, m) {
       .def(
           "run_list",
           // Compact form for hot loops: (codes int32[n], {index: message} for non-OK slices, times).
-          [compact](Engine& e, const WorkList& wl) {
+          [compact](Engine& e, const WorkList& wl, int batch_cap) {
             StageTimes t;
             std::vector<SliceStatus> st;
             {
               py::gil_scoped_release nogil;
-              st = e.run(*wl.items, &t);
+              st = e.run(*wl.items, &t, {}, batch_cap);
             }
             return compact(st, t);
-          })
+          },
+          py::arg("work"), py::arg("batch_cap") = 0)
       .def(
           "submit",
           // Queue a run and return at once (Engine::submit); the next run can be submitted before
           // this one finished — the engine pipelines across them.
-          [](Engine& e, const WorkList& wl) {
+          [](Engine& e, const WorkList& wl, int batch_cap) {
             py::gil_scoped_release nogil;
-            return Ticket{e.submit(wl.items)};
-          })
+            return Ticket{e.submit(wl.items, {}, batch_cap)};
+          },
+          py::arg("work"), py::arg("batch_cap") = 0)
       .def(
           "wait",
           // Result of a submitted run, in run_list's compact form.
@@ -969,6 +995,51 @@ PYBIND11_MODULE(_nm03, m) {
         c.allreduce_max_f64(v.data(), v.size());
         return v;
       })
+      .def_property_readonly("transport_size", &Comm::transport_size)
+      .def_property_readonly("transport_rank", &Comm::transport_rank)
+      .def_property_readonly("transport_device", &Comm::transport_device)
+      .def("set_abort_segment", &Comm::set_abort_segment, py::arg("segment"))
+      .def("sendrecv", [](Comm& c, py::bytes data, int dst, size_t rbytes, int src) {
+        std::string s = data;
+        std::string out(rbytes, '\0');
+        {
+          py::gil_scoped_release nogil;
+          c.sendrecv(s.data(), s.size(), dst, out.data(), rbytes, src);
+        }
+        return py::bytes(out);
+      }, py::arg("data"), py::arg("dst"), py::arg("rbytes"), py::arg("src"))
+      .def("gather_rank_devices", [](Comm& c, int device, const std::string& bus_id, int node, const std::string& cpus,
+                                     int threads, const std::string& error) {
+        RankDevice me;
+        me.device = device;
+        me.bus_id = bus_id;
+        me.node = node;
+        me.cpus = cpus;
+        me.threads = threads;
+        me.transport_size = c.transport_size();
+        me.transport_device = c.transport_device();
+        me.error = error;
+        std::vector<RankDevice> all;
+        {
+          py::gil_scoped_release nogil;
+          all = gather_rank_devices(c, me);
+        }
+        py::list out;
+        for (const auto& d : all) {
+          py::dict x;
+          x["device"] = d.device;
+          x["bus_id"] = d.bus_id;
+          x["numa_node"] = d.node;
+          x["cpus"] = d.cpus;
+          x["threads"] = d.threads;
+          x["transport_size"] = d.transport_size;
+          x["transport_device"] = d.transport_device;
+          x["error"] = d.error;
+          out.append(x);
+        }
+        return out;
+      }, py::arg("device"), py::arg("bus_id"), py::arg("node"), py::arg("cpus"), py::arg("threads"),
+         py::arg("error") = "")
       .def("allgather_f64", [](Comm& c, std::vector<double> v) {
         std::vector<double> all(v.size() * (size_t)c.size());
         {

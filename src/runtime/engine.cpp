@@ -23,12 +23,14 @@
 
 #include "nm03/cohort.h"
 #include "nm03/dicom.h"
+#include "nm03/golden.h"
 #include "nm03/gpu_types.h"
 #include "nm03/jpeg.h"
 #include "nm03/kernels.h"
 #include "nm03/log.h"
 #include "nm03/numa.h"
 #include "nm03/pack12.h"
+#include "nm03/synth.h"
 #include "nm03/thread_pool.h"
 
 namespace nm03 {
@@ -134,6 +136,9 @@ struct Slot {
   // map_region + i * map_stride and the whole range is unmapped once after the batch's loads.
   uint8_t* map_region = nullptr;
   size_t map_stride = 0;
+  // Host-only engine (EngineConfig::host_only): h_blob / h_out are plain mappings, no device side.
+  bool host_only = false;
+  size_t out_bytes = 0;
   // Captured kernel chains keyed by launch signature (see GraphKey in build_and_run). Every
   // pointer in the chain is fixed per slot, so a signature fully determines the launches.
   std::map<std::array<int, 11>, hipGraphExec_t> graphs;
@@ -190,6 +195,13 @@ struct IoDirs {
 };
 
 void hip_free_all(Slot& s) {
+  if (s.host_only) {
+    if (s.h_blob) munmap(s.h_blob, s.blob_bytes);
+    if (s.h_out) munmap(s.h_out, s.out_bytes);
+    delete[] s.h_sizes;
+    if (s.map_region) munmap(s.map_region, (size_t)s.cap_slices * s.map_stride);
+    return;
+  }
   if (s.h_blob) (void)hipHostFree(s.h_blob);
   if (s.h_out) (void)hipHostFree(s.h_out);
   if (s.h_sizes) (void)hipHostFree(s.h_sizes);
@@ -249,8 +261,12 @@ struct Engine::Impl {
   bool pack_bounce_ = true;
   bool spread_ = false;  // plan_batches' spread schedule (NM03_BATCH_SPREAD)
   bool interleave_exports_ = true;  // NM03_EXPORT_INTERLEAVE: writers round-robin over output directories
+  bool host_only_ = false;  // EngineConfig::host_only / NM03_HOST_ONLY
+  // Host-only: the entropy-coded segments standing in for the GPU encoder's output (original,
+  // processed) — the golden export of a phantom slice, so sizes match a real run.
+  std::vector<uint8_t> tmpl_[2];
 
-  explicit Impl(const EngineConfig& c) : cfg(c), place(c.device) {
+  explicit Impl(const EngineConfig& c) : cfg(c), place(c.device, c.cpus) {
     if (const char* e = std::getenv("NM03_BATCH_TAPER"); e && *e) cfg.taper = *e != '0';
     if (const char* e = std::getenv("NM03_BATCH_SPREAD"); e && *e) spread_ = *e != '0';
     if (const char* e = std::getenv("NM03_EXPORT_INTERLEAVE"); e && *e) interleave_exports_ = *e != '0';
@@ -268,6 +284,13 @@ struct Engine::Impl {
     if (const char* e = std::getenv("NM03_JPEG_D2H_EST_KB"); e && *e)  // tests: force short first copies
       jpeg_est_ = (uint32_t)std::max(1L, std::atol(e)) << 10;
     if (const char* e = std::getenv("NM03_UPLOAD_CHUNK_KB"); e && *e) upload_chunk_ = (size_t)std::atol(e) << 10;
+    host_only_ = cfg.host_only;
+    if (const char* e = std::getenv("NM03_HOST_ONLY"); e && *e) host_only_ = *e != '0';
+    if (host_only_) {
+      upload_chunk_ = 0;  // nothing to upload
+      jpeg_d2h_ = 0;
+      cfg.graphs = false;
+    }
     if (cfg.batch_size < 1) cfg.batch_size = 1;
     if (cfg.streams < 1) cfg.streams = 1;
     if (cfg.max_dim < 16) cfg.max_dim = 16;
@@ -300,11 +323,12 @@ struct Engine::Impl {
     jpeg_header = jpeg::make_header(cfg.render.out_width, cfg.render.out_height, t);
     if (cfg.render.out_width % 16 || cfg.render.out_height % 16)
       throw DeviceError("canvas size must be a multiple of 16");
+    if (host_only_) make_templates();
     const double t0 = now_s();
-    check_hip(hipSetDevice(cfg.device), "hipSetDevice");
+    if (!host_only_) check_hip(hipSetDevice(cfg.device), "hipSetDevice");
     const double t1 = now_s();
     // Host threads and pinned buffers on the GPU's socket (numa.h).
-    pool = std::make_unique<ThreadPool>(cfg.threads, [this] { place.bind_this_thread(); });
+    pool = std::make_unique<ThreadPool>(cfg.threads, [this](int i) { place.bind_worker(i, cfg.threads); });
     const double t2 = now_s();
     // Slot 0 is built here (its failure fails the constructor); the others are built by their own
     // worker threads while slot 0 already runs batches — a slot costs ≈11–18 ms of pinned and
@@ -336,9 +360,26 @@ struct Engine::Impl {
 
   ~Impl() {
     stop_workers();
-    (void)hipSetDevice(cfg.device);
+    if (!host_only_) (void)hipSetDevice(cfg.device);
     for (auto& s : slots)
       if (s) hip_free_all(*s);
+  }
+
+  void make_templates() {
+    golden::SliceInput in;
+    in.w = in.h = 256;
+    in.raw.resize(256 * 256);
+    synth::phantom_slice(256, 256, 3, 12, 25, 20250404, in.raw.data());
+    const golden::SliceResult r = golden::run(in, cfg.pipe, false);
+    const golden::SliceJpegs j = golden::export_jpegs(in, r, cfg.pipe, cfg.render);
+    const std::vector<uint8_t>* files[2] = {&j.original, &j.processed};
+    for (int k = 0; k < 2; ++k) {
+      const auto& f = *files[k];
+      if (f.size() < jpeg_header.size() + 2 || !std::equal(jpeg_header.begin(), jpeg_header.end(), f.begin()))
+        throw DeviceError("host-only engine: unexpected template JPEG layout");
+      tmpl_[k].assign(f.begin() + (long)jpeg_header.size(), f.end() - 2);
+      if (tmpl_[k].size() > out_cap_) throw DeviceError("host-only engine: template exceeds the output capacity");
+    }
   }
 
   std::unique_ptr<Slot> make_slot() {
@@ -371,6 +412,24 @@ struct Engine::Impl {
     s.raw_base = o;
     s.hole_slack = (size_t)std::max(cfg.threads, 1) * align_up((size_t)md * md / 4 * 3, 8);
     s.blob_bytes = o + (s.cap_pixels + s.hole_slack) * sizeof(uint16_t);
+    if (host_only_) {
+      s.host_only = true;
+      s.out_bytes = (size_t)out_cap_ * s.cap_canvases;
+      auto map = [](size_t bytes) {
+        void* p = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_POPULATE, -1, 0);
+        if (p == MAP_FAILED) throw DeviceError("host-only engine: cannot map slot buffers");
+        return static_cast<uint8_t*>(p);
+      };
+      try {
+        s.h_blob = map(s.blob_bytes);
+        s.h_out = map(s.out_bytes);
+        s.h_sizes = new int32_t[(size_t)s.cap_canvases];
+      } catch (...) {
+        hip_free_all(s);
+        throw;
+      }
+      return sp;
+    }
     try {
       if (read_mode_ == dicom::ReadMode::kMapped) {
         s.map_stride = align_up((size_t)md * md * 2 + (1u << 20), 1u << 21);  // pixels + 1 MiB of header room
@@ -763,6 +822,18 @@ struct Engine::Impl {
     }
     s.ncanvas = ncanv;
     if (nl == 0) return;
+    if (host_only_) {
+      // The GPU stages' host-visible result: each canvas's segment lands in h_out (the encoder
+      // stores over PCIe, so the writers read it from DRAM, not from their caches).
+      if (mode != 0) throw DeviceError("host-only engine: export runs only");
+      for (int k = 0; k < ncanv; ++k) {
+        const auto& t = tmpl_[k & 1];
+        dicom::stream_copy_unfenced(s.h_out + (size_t)k * out_cap_, t.data(), t.size());
+        s.h_sizes[k] = (int32_t)t.size();
+      }
+      dicom::stream_copy(s.h_out, tmpl_[0].data(), 0);  // fence
+      return;
+    }
 
     uint8_t* db = s.d_blob;
     const auto* d_stats_c = reinterpret_cast<SliceStats*>(db + s.off_stats);
@@ -1181,7 +1252,7 @@ struct Engine::Impl {
     pthread_setname_np(pthread_self(), "nm03-slot");
     place.bind_this_thread();
     (void)prctl(PR_SET_TIMERSLACK, 1000UL, 0, 0, 0);  // 1 µs: short poll sleeps stay short
-    (void)hipSetDevice(cfg.device);
+    if (!host_only_) (void)hipSetDevice(cfg.device);
     if (!slots[slot_index]) {  // built lazily (see the constructor); this thread is its only user
       try {
         slots[slot_index] = make_slot();
@@ -1219,14 +1290,16 @@ struct Engine::Impl {
     }
   }
 
-  std::shared_ptr<Job> submit(std::shared_ptr<const std::vector<WorkItem>> items, std::function<void(size_t)> on_start) {
+  std::shared_ptr<Job> submit(std::shared_ptr<const std::vector<WorkItem>> items, std::function<void(size_t)> on_start,
+                              int batch_cap = 0) {
     auto j = std::make_shared<Job>();
     j->t0 = now_s();
     j->items = std::move(items);
     j->dirs = std::make_unique<IoDirs>(*j->items);
     j->on_start = std::move(on_start);
     j->status.resize(j->items->size());
-    j->batches = plan_batches(j->items->size(), (size_t)cfg.batch_size, cfg.taper,
+    const size_t B = batch_cap > 0 ? std::min<size_t>((size_t)batch_cap, (size_t)cfg.batch_size) : (size_t)cfg.batch_size;
+    j->batches = plan_batches(j->items->size(), B, cfg.taper,
                               spread_ ? (size_t)cfg.streams : 0);
     j->remaining = j->batches.size();
     {
@@ -1254,14 +1327,15 @@ struct Engine::Impl {
   }
 
   std::vector<SliceStatus> run(const std::vector<WorkItem>& items, StageTimes* times,
-                               const std::function<void(size_t)>& on_start) {
+                               const std::function<void(size_t)>& on_start, int batch_cap = 0) {
     // Blocking form: the caller's vector outlives the run.
     std::shared_ptr<const std::vector<WorkItem>> view(&items, [](const std::vector<WorkItem>*) {});
-    return wait(submit(view, on_start), times);
+    return wait(submit(view, on_start, batch_cap), times);
   }
 
   SingleResult run_single(const golden::SliceInput& in) {
     std::lock_guard<std::mutex> serial(single_m);
+    if (host_only_) throw DeviceError("host-only engine: run_single needs the GPU");
     {
       // Slot 0 is used directly: no queued run may be using it.
       std::unique_lock<std::mutex> g(job_m);
@@ -1336,14 +1410,15 @@ struct Engine::Impl {
 Engine::Engine(const EngineConfig& cfg) : impl_(std::make_unique<Impl>(cfg)) {}
 Engine::~Engine() = default;
 std::vector<SliceStatus> Engine::run(const std::vector<WorkItem>& items, StageTimes* times,
-                                     const std::function<void(size_t)>& on_start) {
-  return impl_->run(items, times, on_start);
+                                     const std::function<void(size_t)>& on_start, int batch_cap) {
+  return impl_->run(items, times, on_start, batch_cap);
 }
 struct RunHandle {
   std::shared_ptr<Engine::Impl::Job> job;
 };
-RunTicket Engine::submit(std::shared_ptr<const std::vector<WorkItem>> items, std::function<void(size_t)> on_start) {
-  return std::make_shared<RunHandle>(RunHandle{impl_->submit(std::move(items), std::move(on_start))});
+RunTicket Engine::submit(std::shared_ptr<const std::vector<WorkItem>> items, std::function<void(size_t)> on_start,
+                         int batch_cap) {
+  return std::make_shared<RunHandle>(RunHandle{impl_->submit(std::move(items), std::move(on_start), batch_cap)});
 }
 std::vector<SliceStatus> Engine::wait(const RunTicket& t, StageTimes* times) { return impl_->wait(t->job, times); }
 SingleResult Engine::run_single(const golden::SliceInput& s) { return impl_->run_single(s); }

@@ -1,6 +1,7 @@
-// Host NUMA placement (include/nm03/numa.h).
+// Host NUMA placement and per-rank CPU partitions (include/nm03/numa.h).
 #include "nm03/numa.h"
 
+#include <dirent.h>
 #include <hip/hip_runtime_api.h>
 #include <pthread.h>
 
@@ -8,6 +9,8 @@
 #include <cctype>
 #include <cstdlib>
 #include <fstream>
+#include <map>
+#include <set>
 #include <sstream>
 
 namespace nm03::numa {
@@ -33,14 +36,58 @@ std::vector<int> parse_cpulist(const std::string& s) {
   return out;
 }
 
-int device_node(int device) {
+std::string format_cpulist(const std::vector<int>& cpus) {
+  std::vector<int> v(cpus);
+  std::sort(v.begin(), v.end());
+  v.erase(std::unique(v.begin(), v.end()), v.end());
+  std::string out;
+  for (size_t i = 0; i < v.size();) {
+    size_t j = i;
+    while (j + 1 < v.size() && v[j + 1] == v[j] + 1) ++j;
+    if (!out.empty()) out += ",";
+    out += std::to_string(v[i]);
+    if (j > i) out += "-" + std::to_string(v[j]);
+    i = j + 1;
+  }
+  return out;
+}
+
+std::string device_bus_id(int device) {
   char bus[64] = {0};
-  if (hipDeviceGetPCIBusId(bus, sizeof(bus), device) != hipSuccess) return -1;
+  if (hipDeviceGetPCIBusId(bus, sizeof(bus), device) != hipSuccess) return "";
   std::string id(bus);
   for (auto& ch : id) ch = (char)std::tolower((unsigned char)ch);
+  return id;
+}
+
+int device_node(int device) {
+  const std::string id = device_bus_id(device);
+  if (id.empty()) return -1;
   const std::string v = read_line("/sys/bus/pci/devices/" + id + "/numa_node");
   if (v.empty()) return -1;
   return std::atoi(v.c_str());
+}
+
+std::vector<int> allowed_cpus() {
+  std::vector<int> out;
+  cpu_set_t set;
+  if (sched_getaffinity(0, sizeof(set), &set) != 0) return out;
+  for (int c = 0; c < CPU_SETSIZE; ++c)
+    if (CPU_ISSET(c, &set)) out.push_back(c);
+  return out;
+}
+
+int cpu_budget(const std::string& cgroup_root) {
+  int n = (int)allowed_cpus().size();
+  if (n < 1) n = 1;
+  std::istringstream in(read_line(cgroup_root + "/cpu.max"));
+  std::string quota;
+  long period = 0;
+  if (in >> quota >> period && quota != "max" && period > 0) {
+    const long q = std::atol(quota.c_str()) / period;
+    n = std::min<long>(n, std::max<long>(1, q));
+  }
+  return n;
 }
 
 std::vector<int> node_cpus(int node) {
@@ -52,26 +99,169 @@ std::vector<int> node_cpus(int node) {
   return cpus;
 }
 
-Placement::Placement(int device) {
+int Topology::node_index(int node) const {
+  for (size_t i = 0; i < nodes.size(); ++i)
+    if (nodes[i] == node) return (int)i;
+  return -1;
+}
+
+Topology read_topology(const std::string& sysfs, const std::vector<int>& allowed_in) {
+  const std::vector<int> allowed = allowed_in.empty() ? allowed_cpus() : allowed_in;
+  const std::set<int> ok(allowed.begin(), allowed.end());
+  Topology t;
+  std::vector<int> ids;
+  if (DIR* d = opendir((sysfs + "/devices/system/node").c_str())) {
+    while (dirent* e = readdir(d)) {
+      const std::string nm = e->d_name;
+      if (nm.size() > 4 && nm.compare(0, 4, "node") == 0 && std::isdigit((unsigned char)nm[4]))
+        ids.push_back(std::atoi(nm.c_str() + 4));
+    }
+    closedir(d);
+  }
+  std::sort(ids.begin(), ids.end());
+  for (int id : ids) {
+    std::vector<int> cpus = parse_cpulist(read_line(sysfs + "/devices/system/node/node" + std::to_string(id) + "/cpulist"));
+    cpus.erase(std::remove_if(cpus.begin(), cpus.end(), [&](int c) { return !ok.count(c); }), cpus.end());
+    std::sort(cpus.begin(), cpus.end());
+    if (cpus.empty()) continue;
+    t.nodes.push_back(id);
+    t.node_cpus.push_back(std::move(cpus));
+  }
+  if (t.nodes.empty()) {  // no NUMA information: one node with every allowed CPU
+    t.nodes.push_back(0);
+    t.node_cpus.push_back(std::vector<int>(ok.begin(), ok.end()));
+  }
+  const int maxc = ok.empty() ? 0 : *ok.rbegin() + 1;
+  t.core_of.assign((size_t)maxc, -1);
+  for (int c : allowed) {
+    const std::string base = sysfs + "/devices/system/cpu/cpu" + std::to_string(c) + "/topology/";
+    const std::string core = read_line(base + "core_id"), pkg = read_line(base + "physical_package_id");
+    if (!core.empty()) t.core_of[(size_t)c] = ((long)std::max(0, std::atoi(pkg.c_str())) << 20) | std::atol(core.c_str());
+  }
+  return t;
+}
+
+namespace {
+
+// Group `cpus` (ascending) by physical core, cores in order of their first CPU.
+std::vector<std::vector<int>> cores_of(const Topology& t, const std::vector<int>& cpus) {
+  std::vector<std::vector<int>> cores;
+  std::map<long, size_t> at;
+  for (int c : cpus) {
+    long key = (size_t)c < t.core_of.size() ? t.core_of[(size_t)c] : -1;
+    if (key < 0) key = (1L << 40) + c;  // unknown: every CPU is its own core
+    auto it = at.find(key);
+    if (it == at.end()) {
+      at.emplace(key, cores.size());
+      cores.push_back({c});
+    } else {
+      cores[it->second].push_back(c);
+    }
+  }
+  return cores;
+}
+
+}  // namespace
+
+RankCpus rank_partition(const Topology& t, const std::vector<int>& rank_nodes, int local_rank, int budget, int cap) {
+  RankCpus r;
+  const int n = (int)rank_nodes.size();
+  if (local_rank < 0 || local_rank >= n) return r;
+  // A rank's node counts only if the topology knows it; others share the leftover CPUs.
+  auto known = [&](int q) { return t.node_index(rank_nodes[(size_t)q]) >= 0; };
+  const bool mine_known = known(local_rank);
+  r.node = mine_known ? rank_nodes[(size_t)local_rank] : -1;
+  std::vector<int> pool;
+  if (mine_known) {
+    pool = t.node_cpus[(size_t)t.node_index(r.node)];
+  } else {
+    std::set<int> used;
+    for (int q = 0; q < n; ++q)
+      if (known(q))
+        for (int c : t.node_cpus[(size_t)t.node_index(rank_nodes[(size_t)q])]) used.insert(c);
+    for (const auto& cs : t.node_cpus)
+      for (int c : cs)
+        if (!used.count(c)) pool.push_back(c);
+    if (pool.empty())
+      for (const auto& cs : t.node_cpus) pool.insert(pool.end(), cs.begin(), cs.end());
+    std::sort(pool.begin(), pool.end());
+  }
+  // Ranks sharing this pool, in rank order.
+  r.count = 0;
+  r.index = 0;
+  for (int q = 0; q < n; ++q) {
+    const bool same = mine_known ? (known(q) && rank_nodes[(size_t)q] == r.node) : !known(q);
+    if (!same) continue;
+    if (q == local_rank) r.index = r.count;
+    ++r.count;
+  }
+  const int m = std::max(1, r.count), j = r.index;
+  if (!pool.empty()) {
+    const auto cores = cores_of(t, pool);
+    const size_t C = cores.size(), P = pool.size();
+    if (C >= (size_t)m) {
+      for (size_t k = C * j / m; k < C * (j + 1) / m; ++k) r.cpus.insert(r.cpus.end(), cores[k].begin(), cores[k].end());
+    } else if (P >= (size_t)m) {
+      // Fewer cores than ranks: split the logical CPUs, siblings adjacent.
+      std::vector<int> flat;
+      for (const auto& c : cores) flat.insert(flat.end(), c.begin(), c.end());
+      for (size_t k = P * j / m; k < P * (j + 1) / m; ++k) r.cpus.push_back(flat[k]);
+    } else {
+      r.cpus.push_back(pool[(size_t)j % P]);
+    }
+    std::sort(r.cpus.begin(), r.cpus.end());
+  }
+  const int share = std::max(1, budget / std::max(1, n));
+  r.threads = std::max(1, std::min({cap, (int)std::max<size_t>(1, r.cpus.size()), share}));
+  return r;
+}
+
+Placement::Placement(int device, const std::vector<int>& cpus) {
   const char* e = std::getenv("NM03_NUMA");
   if (e && *e == '0') return;
-  // Only worth it on multi-node hosts.
-  if (read_line("/sys/devices/system/node/node1/cpulist").empty()) return;
-  node_ = device_node(device);
-  cpus_ = node_cpus(node_);
+  const char* pin = std::getenv("NM03_PIN");
+  const bool per_core = pin && std::string(pin) == "core";
+  if (!cpus.empty()) {  // a rank partition: exactly these CPUs (within the affinity mask)
+    const std::vector<int> ok = allowed_cpus();
+    for (int c : cpus)
+      if (std::binary_search(ok.begin(), ok.end(), c)) cpus_.push_back(c);
+    node_ = device_node(device);
+  } else if (!read_line("/sys/devices/system/node/node1/cpulist").empty()) {  // multi-node host: the GPU's node
+    node_ = device_node(device);
+    cpus_ = node_cpus(node_);
+  } else if (per_core) {
+    cpus_ = allowed_cpus();
+  }
+  if (per_core && !cpus_.empty()) cores_ = cores_of(read_topology("/sys", cpus_), cpus_);
+}
+
+static void bind_cpus(const std::vector<int>& cpus) {
+  cpu_set_t set;
+  CPU_ZERO(&set);
+  for (int c : cpus) CPU_SET(c, &set);
+  (void)pthread_setaffinity_np(pthread_self(), sizeof(set), &set);
+}
+
+void Placement::bind_worker(int i, int n) const {
+  if (cpus_.empty()) return;
+  if (cores_.empty() || n < 1) {
+    bind_this_thread();
+    return;
+  }
+  const size_t C = cores_.size();
+  const size_t k = (size_t)n <= C ? (size_t)i * C / (size_t)n : (size_t)i % C;
+  bind_cpus(cores_[k]);
 }
 
 void Placement::bind_this_thread() const {
   if (cpus_.empty()) return;
-  cpu_set_t set;
-  CPU_ZERO(&set);
-  for (int c : cpus_) CPU_SET(c, &set);
-  (void)pthread_setaffinity_np(pthread_self(), sizeof(set), &set);
+  bind_cpus(cpus_);
 }
 
 std::string Placement::describe() const {
   if (cpus_.empty()) return "numa: off";
-  return "numa: node " + std::to_string(node_) + " (" + std::to_string(cpus_.size()) + " cpus)";
+  return "numa: node " + std::to_string(node_) + " (" + std::to_string(cpus_.size()) + " cpus: " +
+         format_cpulist(cpus_) + ")";
 }
 
 }  // namespace nm03::numa
