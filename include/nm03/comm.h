@@ -16,10 +16,12 @@
 //                   test-suite (no GPU needed).
 //
 // Failure model (the reference turns every failure into a message + continue or
-// exit 1, main_parallel.cpp:352-356, 377-380, 406-409): every blocking collective has a deadline
-// (NM03_COMM_TIMEOUT_S, default 120 s). The shared segment carries a job-wide abort flag; the
-// launcher raises it the moment a rank exits non-zero, so peers blocked in a collective fail
-// within milliseconds instead of hanging, and the job exits with "Rank k exited with status s".
+// exit 1, main_parallel.cpp:352-356, 377-380, 406-409): the shared segment carries a job-wide
+// abort flag; the launcher raises it the moment a rank exits non-zero, so peers blocked in a
+// collective fail within milliseconds instead of hanging, and the job exits with "Rank k exited
+// with status s". Blocking waits also have a deadline as a hang detector (a rank alive but stuck):
+// NM03_COMM_TIMEOUT_S, default 120 s for independently launched ranks (bench.py, torchrun), off
+// for the CLI launcher's supervised ranks unless the variable is set.
 #pragma once
 
 #include <cstddef>
@@ -73,8 +75,11 @@ class Comm {
   std::vector<std::vector<uint8_t>> allgather_bytes(const std::vector<uint8_t>& mine);  // variable sizes
 };
 
-// Deadline of one blocking collective wait: NM03_COMM_TIMEOUT_S (default 120 s).
+// Deadline of one blocking collective wait: NM03_COMM_TIMEOUT_S (default 120 s). A hang detector,
+// not a phase budget: ranks started by launch_ranks wait without a deadline unless the variable is
+// set (its supervisor turns a dead rank into the abort flag within milliseconds).
 double comm_timeout_s();
+constexpr double kNoDeadline = 1e9;  // ≈ 30 years
 
 // ---- process-shared control segment -------------------------------------------------------------
 // Host collectives, the RCCL unique-id hand-off and the job abort flag live here.

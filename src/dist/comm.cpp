@@ -397,6 +397,12 @@ LaunchOptions LaunchOptions::from_env() {
   LaunchOptions o;
   if (const char* e = std::getenv("NM03_COMM"); e && *e) o.comm = e;
   if (const char* e = std::getenv("NM03_DEVICE_OVERRIDE"); e && *e) o.device_override = std::atoi(e);
+  // Ranks under this launcher's supervisor: a dead rank raises the abort flag at once, so the
+  // collectives need no deadline for liveness. Rank 0 may plan (wipe, list, scan headers) while
+  // the others wait, and ranks wait for the slowest shard at the end — healthy phases of any
+  // length. The deadline stays a hang detector, on only when NM03_COMM_TIMEOUT_S asks for one.
+  const char* t = std::getenv("NM03_COMM_TIMEOUT_S");
+  o.timeout_s = (t && *t) ? comm_timeout_s() : kNoDeadline;
   return o;
 }
 

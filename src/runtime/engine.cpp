@@ -5,6 +5,7 @@
 #include <fcntl.h>
 #include <sys/mman.h>
 #include <sys/prctl.h>
+#include <sys/resource.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -147,8 +148,15 @@ struct Slot {
 // Directory fds of one run: every item's input series directory and output directory opened once
 // (O_PATH), so loads and writes use openat on the bare file name instead of walking the full path
 // per file. Opened per run, never cached across runs: a caller may wipe and re-create output
-// directories between runs (the CLIs do).
+// directories between runs (the CLIs do). At most max_fds() directories per run get an fd — a
+// fraction of RLIMIT_NOFILE, since several runs may be queued at once — the rest use full paths.
 struct IoDirs {
+  static size_t max_fds() {
+    rlimit rl{};
+    size_t lim = 1024;
+    if (getrlimit(RLIMIT_NOFILE, &rl) == 0 && rl.rlim_cur != RLIM_INFINITY) lim = (size_t)rl.rlim_cur;
+    return std::min<size_t>(256, lim / 8);
+  }
   std::vector<int> fds;
   // Per directory: 1 once a file was missing there (files are then created directly, see
   // jpeg::write_jpeg_at); 0 = try opening existing files without O_CREAT first.
@@ -157,10 +165,11 @@ struct IoDirs {
   std::vector<uint32_t> in_name;       // per item: offset of the file name in its path
   IoDirs(const std::vector<WorkItem>& items) {
     std::unordered_map<std::string, int32_t> idx;
+    const size_t cap = max_fds();
     auto dir_index = [&](const std::string& d) -> int32_t {
       auto it = idx.find(d);
       if (it != idx.end()) return it->second;
-      const int fd = ::open(d.empty() ? "/" : d.c_str(), O_PATH | O_DIRECTORY | O_CLOEXEC);
+      const int fd = fds.size() < cap ? ::open(d.empty() ? "/" : d.c_str(), O_PATH | O_DIRECTORY | O_CLOEXEC) : -1;
       int32_t k = -1;
       if (fd >= 0) {
         k = (int32_t)fds.size();

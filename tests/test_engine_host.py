@@ -1,0 +1,129 @@
+"""The engine's host path on the CPU (EngineConfig.host_only: every DICOM load, 12-bit pack and JPEG
+file write of a real run, the GPU stages replaced by fixed pre-encoded segments; no HIP call).
+Covers the scheduler, directory-fd handling, resume, batch caps and failure isolation without a GPU
+(the byte-level JPEG contract is tested against the golden model in test_gpu.py)."""
+import io
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _engine(native, **kw):
+    import nm03_capstone_project_amd as nm
+    cfg = nm.PipelineConfig(**{"batch_size": 4, "streams": 2, "threads": 3, **kw}).engine_config()
+    cfg.host_only = True
+    return native.Engine(cfg)
+
+
+def _items(native, root, out):
+    base = native.cohort_dir(root)
+    items = []
+    for pid in native.find_patient_dirs(base):
+        _, files = native.list_patient_series(base, pid)
+        d = os.path.join(out, pid)
+        os.makedirs(d, exist_ok=True)
+        items += [(f, d) for f in files]
+    return items
+
+
+def test_host_only_run_writes_every_file(native, cohort_root, tmp_path):
+    items = _items(native, cohort_root, str(tmp_path / "out"))
+    st, times = _engine(native).run(items)
+    assert [c for c, _ in st] == [0] * len(items)
+    assert times["kernels_s"] == 0.0 and times["batches"] == (len(items) + 3) // 4
+    from PIL import Image
+    for f, d in items:
+        stem = os.path.basename(f)[:-4]
+        for kind in ("original", "processed"):
+            b = open(os.path.join(d, f"{stem}_{kind}.jpg"), "rb").read()
+            assert b[:2] == b"\xff\xd8" and b[-2:] == b"\xff\xd9"
+            im = Image.open(io.BytesIO(b))
+            im.load()
+            assert im.size == (512, 512)
+
+
+def test_host_only_batch_cap(native, cohort_root, tmp_path):
+    items = _items(native, cohort_root, str(tmp_path / "out"))
+    wl = native.WorkList(items)
+    eng = _engine(native, batch_size=8)
+    codes, msgs, t = eng.run_list(wl, 3)
+    assert not msgs and t["batches"] == -(-len(items) // 3)
+    codes, msgs, t = eng.run_list(wl)
+    assert not msgs and t["batches"] == -(-len(items) // 8)
+
+
+def test_host_only_resume_skips_existing(native, cohort_root, tmp_path):
+    items = _items(native, cohort_root, str(tmp_path / "out"))
+    _engine(native).run(items)
+    st, _ = _engine(native, resume=True).run(items)
+    assert all(c == 0 and "resumed" in m for c, m in st)
+
+
+def test_host_only_too_small_and_corrupt(native, tmp_path):
+    """<100 guard (main_sequential.cpp:189-192) and an unreadable file: per-slice statuses."""
+    import numpy as np
+    d = tmp_path / "in"
+    d.mkdir()
+    good = native.phantom_slice(256, 256, 1, 3, 10, 7)
+    (d / "1-1.dcm").write_bytes(native.dicom_bytes(good, bits_stored=12))
+    (d / "1-2.dcm").write_bytes(native.dicom_bytes(np.zeros((64, 64), np.uint16)))
+    (d / "1-3.dcm").write_bytes(b"not a dicom file")
+    out = tmp_path / "out"
+    out.mkdir()
+    st, _ = _engine(native).run([(str(d / f"1-{k}.dcm"), str(out)) for k in (1, 2, 3)])
+    assert [c for c, _ in st] == [0, 2, 1]
+    assert "too small" in st[1][1]
+
+
+_FD_SCRIPT = r"""
+import os, resource, sys
+sys.path.insert(0, {root!r})
+resource.setrlimit(resource.RLIMIT_NOFILE, (64, resource.getrlimit(resource.RLIMIT_NOFILE)[1]))
+import nm03_capstone_project_amd as nm
+n = nm.native()
+src = {src!r}
+items = []
+for k in range(150):  # 150 distinct output directories, far more than 64 descriptors
+    d = os.path.join({out!r}, "d%03d" % k)
+    os.makedirs(d, exist_ok=True)
+    items.append((src[k % len(src)], d))
+cfg = nm.PipelineConfig(batch_size=16, streams=3, threads=4).engine_config()
+cfg.host_only = True
+eng = n.Engine(cfg)
+codes, msgs, t = eng.run_list(n.WorkList(items))
+ok = sum(1 for k in range(150) if os.path.exists(os.path.join({out!r}, "d%03d" % k)))
+print(len(msgs), ok)
+"""
+
+
+def test_host_only_many_directories_low_fd_limit(native, cohort_root, tmp_path):
+    """a run touching more directories than RLIMIT_NOFILE allows must not fail with
+    EMFILE — directory fds are capped per run, the rest use full paths."""
+    src = [f for f, _ in _items(native, cohort_root, str(tmp_path / "o0"))]
+    code = _FD_SCRIPT.format(root=ROOT, src=src, out=str(tmp_path / "many"))
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert r.stdout.split() == ["0", "150"], r.stdout
+    for k in range(150):
+        d = tmp_path / "many" / f"d{k:03d}"
+        assert len(os.listdir(d)) == 2
+
+
+@pytest.mark.parametrize("fault,code", [("corrupt_dicom:2", 1), ("fail_write:1", 4)])
+def test_host_only_fault_injection(native, cohort_root, tmp_path, fault, code):
+    """NM03_FAULT: the injected slice fails with its code, every other slice succeeds."""
+    items = _items(native, cohort_root, str(tmp_path / "out"))
+    script = (f"import sys, json; sys.path.insert(0, {ROOT!r}); import nm03_capstone_project_amd as nm; "
+              f"n = nm.native(); cfg = nm.PipelineConfig(batch_size=4, streams=2, threads=2).engine_config(); "
+              f"cfg.host_only = True; st, _ = n.Engine(cfg).run({items!r}); print(json.dumps([c for c, _ in st]))")
+    r = subprocess.run([sys.executable, "-c", script], capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, NM03_FAULT=fault))
+    assert r.returncode == 0, r.stderr[-2000:]
+    codes = json.loads(r.stdout.strip().splitlines()[-1])
+    bad = int(fault.split(":")[1])
+    assert codes[bad] == code and all(c == 0 for i, c in enumerate(codes) if i != bad)
