@@ -780,22 +780,28 @@ PYBIND11_MODULE(_nm03, m) {
     int32_t* d_seeds = nullptr;
     uint32_t* d_flag = nullptr;
     uint32_t* h_flag = nullptr;
+    uint64_t* scratch = nullptr;
     auto release = [&] {
       if (d_seeds) (void)hipFree(d_seeds);
       if (d_flag) (void)hipFree(d_flag);
       if (h_flag) (void)hipHostFree(h_flag);
+      if (scratch) (void)hipFree(scratch);
     };
     try {
-      gpu::check_hip(hipMalloc((void**)&d_flag, 2 * sizeof(uint32_t)), "hipMalloc flag");
-      gpu::check_hip(hipHostMalloc((void**)&h_flag, 2 * sizeof(uint32_t), hipHostMallocDefault), "hipHostMalloc flag");
+      gpu::check_hip(hipMalloc((void**)&d_flag, gpu::kSrg3dCtlWords * sizeof(uint32_t)), "hipMalloc flag");
+      gpu::check_hip(hipHostMalloc((void**)&h_flag, gpu::kSrg3dCtlWords * sizeof(uint32_t), hipHostMallocDefault),
+                     "hipHostMalloc flag");
+      if (const size_t sw = gpu::srg3d_scratch_words(w, h, d))
+        gpu::check_hip(hipMalloc((void**)&scratch, sw * 8), "hipMalloc srg3d scratch");
       if (!sx.empty()) {
         gpu::check_hip(hipMalloc((void**)&d_seeds, sx.size() * sizeof(int32_t)), "hipMalloc seeds");
         gpu::check_hip(hipMemcpyAsync(d_seeds, sx.data(), sx.size() * sizeof(int32_t), hipMemcpyHostToDevice, st),
                        "H2D seeds");
       }
-      const int sweeps = gpu::srg_volume((const uint64_t*)band, (uint64_t*)region, w, h, d, d_seeds,
-                                         (int)(sx.size() / 3), connectivity, d_flag, h_flag, st, reset);
+      gpu::srg_volume((const uint64_t*)band, (uint64_t*)region, w, h, d, d_seeds, (int)(sx.size() / 3), connectivity,
+                      d_flag, h_flag, scratch, st, reset);
       gpu::check_hip(hipStreamSynchronize(st), "k_srg3d");
+      const int sweeps = gpu::srg_volume_result(h_flag);
       release();
       return sweeps;
     } catch (...) {
@@ -807,8 +813,18 @@ PYBIND11_MODULE(_nm03, m) {
   m.def("k_dilate3d", [](uintptr_t src, uintptr_t dst, uintptr_t tmp, int w, int h, int d, int size, uintptr_t stream) {
     hipStream_t st = as_stream(stream);
     if (size < 1 || !(size & 1)) throw std::invalid_argument("dilation size must be odd and >= 1");
-    gpu::dilate_volume((const uint64_t*)src, (uint64_t*)dst, (uint64_t*)tmp, w, h, d, size, st);
-    gpu::check_hip(hipStreamSynchronize(st), "k_dilate3d");
+    void* scr = nullptr;
+    if (const size_t sw = gpu::morph3d_scratch_words(w, h, d))
+      gpu::check_hip(hipMalloc(&scr, sw * 8), "hipMalloc morph scratch");
+    try {
+      gpu::dilate_volume((const uint64_t*)src, (uint64_t*)dst, (uint64_t*)tmp, w, h, d, size, st, (uint64_t*)scr);
+      gpu::check_hip(hipStreamSynchronize(st), "k_dilate3d");
+    } catch (...) {
+      (void)hipStreamSynchronize(st);
+      if (scr) (void)hipFree(scr);
+      throw;
+    }
+    if (scr) (void)hipFree(scr);
   });
   m.def("k_jpeg", [](uintptr_t canvas, int n, int h, int w, int quality, uintptr_t stream) {
     hipStream_t st = as_stream(stream);

@@ -93,7 +93,8 @@ struct VolumeDevice {
   size_t words, ps;
   hipStream_t stream = nullptr;
   DevBuf raw, med, band, region, dil, tmp, desc, medt, shpt, stats, seeds, flag;
-  uint32_t* h_flag = nullptr;
+  DevBuf srg_scratch, morph_scratch;  // bit planes too large for LDS (a side > 512), else unused
+  uint32_t* h_flag = nullptr;         // the region growing's control words (sweep count, error)
   uint8_t* h_tables = nullptr;  // pinned staging: descriptors, tile lists, stats (reused per run)
   size_t n_medt, n_shpt;
   VolumeDevice(const VolumeInput& v)
@@ -103,11 +104,13 @@ struct VolumeDevice {
         tmp(words * v.d * 8), desc(sizeof(SliceDesc) * v.d),
         medt(sizeof(TileDesc) * v.d * ((v.w + 63) / 64) * ((v.h + 63) / 64)),
         shpt(sizeof(TileDesc) * v.d * ((v.w + 63) / 64) * ((v.h + kShpTileH - 1) / kShpTileH)), stats(sizeof(SliceStats) * v.d),
-        seeds(sizeof(int32_t) * 3 * kMaxSeeds), flag(16),
+        seeds(sizeof(int32_t) * 3 * kMaxSeeds), flag(sizeof(uint32_t) * kSrg3dCtlWords),
+        srg_scratch(8 * srg3d_scratch_words(v.w, v.h, v.d)), morph_scratch(8 * morph3d_scratch_words(v.w, v.h, v.d)),
         n_medt((size_t)v.d * ((v.w + 63) / 64) * ((v.h + 63) / 64)),
         n_shpt((size_t)v.d * ((v.w + 63) / 64) * ((v.h + kShpTileH - 1) / kShpTileH)) {
     check_hip(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking), "stream");
-    check_hip(hipHostMalloc((void**)&h_flag, 16, hipHostMallocDefault), "hipHostMalloc flag");
+    check_hip(hipHostMalloc((void**)&h_flag, sizeof(uint32_t) * kSrg3dCtlWords, hipHostMallocDefault),
+              "hipHostMalloc flag");
     check_hip(hipHostMalloc((void**)&h_tables, table_bytes(), hipHostMallocDefault), "hipHostMalloc tables");
   }
   size_t table_bytes() const {
@@ -167,7 +170,9 @@ static void volume_preprocess(VolumeDevice& V, const VolumeInput& v, const Pipel
                       V.shpt.as<TileDesc>(), (int)ns, pc, V.stats.as<SliceStats>(), V.stream);
 }
 
-static void volume_segment(VolumeDevice& V, const VolumeInput& v, const VolumeParams& p, int* sweeps) {
+// Enqueues seeding, region growing (convergence decided on the device) and the cube dilation; no
+// host synchronisation. The sweep count is read from V.h_flag after the caller's sync.
+static void volume_segment(VolumeDevice& V, const VolumeInput& v, const VolumeParams& p) {
   std::vector<int32_t> sx;
   std::vector<Seed> seeds = p.seeds;
   if (seeds.empty()) {
@@ -180,10 +185,11 @@ static void volume_segment(VolumeDevice& V, const VolumeInput& v, const VolumePa
     sx.push_back(seeds[i].z);
   }
   check_hip(hipMemcpyAsync(V.seeds.p, sx.data(), sx.size() * 4, hipMemcpyHostToDevice, V.stream), "H2D seeds");
-  *sweeps = srg_volume(V.band.as<uint64_t>(), V.region.as<uint64_t>(), v.w, v.h, v.d, V.seeds.as<int32_t>(),
-                       (int)(sx.size() / 3), p.connectivity == 26 ? 26 : 6, V.flag.as<uint32_t>(), V.h_flag, V.stream);
+  srg_volume(V.band.as<uint64_t>(), V.region.as<uint64_t>(), v.w, v.h, v.d, V.seeds.as<int32_t>(),
+             (int)(sx.size() / 3), p.connectivity == 26 ? 26 : 6, V.flag.as<uint32_t>(), V.h_flag,
+             V.srg_scratch.as<uint64_t>(), V.stream);
   dilate_volume(V.region.as<uint64_t>(), V.dil.as<uint64_t>(), V.tmp.as<uint64_t>(), v.w, v.h, v.d, p.dilation_size,
-                V.stream);
+                V.stream, V.morph_scratch.as<uint64_t>());
 }
 
 static void unpack_volume(const DevBuf& b, const VolumeDevice& V, std::vector<uint8_t>& out) {
@@ -286,9 +292,10 @@ VolumeResult VolumeRunner::run(const VolumeInput& v, const VolumeParams& p, bool
   r.h = v.h;
   r.d = v.d;
   volume_preprocess(V, v, p.pipe, pc);
-  volume_segment(V, v, p, &r.sweeps);
+  volume_segment(V, v, p);
   check_hip(hipEventRecord(I.e1, V.stream), "event");
   check_hip(hipEventSynchronize(I.e1), "sync");
+  r.sweeps = srg_volume_result(V.h_flag);
   float ms = 0;
   (void)hipEventElapsedTime(&ms, I.e0, I.e1);
   r.kernels_s = ms * 1e-3;
@@ -318,7 +325,7 @@ std::vector<std::vector<uint8_t>> VolumeRunner::export_jpegs(const VolumeInput& 
   uint64_t* bits = X.bits.as<uint64_t>();
   const size_t vol_words = V.words * V.d;
   check_hip(hipMemcpyAsync(bits, V.dil.p, vol_words * 8, hipMemcpyDeviceToDevice, V.stream), "D2D labels");
-  border_volume(bits, bits + vol_words, v.w, v.h, v.d, rp.border_radius, V.stream);
+  border_volume(bits, bits + vol_words, v.w, v.h, v.d, rp.border_radius, V.stream, V.morph_scratch.as<uint64_t>());
   const jpeg::Tables tables = jpeg::make_tables(rp.jpeg_quality);
   const std::vector<uint8_t> header = jpeg::make_header(cw, ch, tables);
   const RenderGeom g = make_render_geom(v.w, v.h, v.spacing_x, v.spacing_y, cw, ch);
