@@ -9,6 +9,7 @@
 #include <vector>
 
 #include "nm03/app.h"
+#include "nm03/comm.h"
 #include "nm03/engine.h"
 
 namespace nm03 {
@@ -60,6 +61,13 @@ class VolumeRunner {
   // the device — byte-identical to the golden host renderer + encoder.
   std::vector<std::vector<uint8_t>> export_jpegs(const VolumeInput& v, const VolumeParams& p, const RenderParams& rp,
                                                  struct VolumeExportStats* stats = nullptr);
+  // One rank's z-slab of a `depth`-deep volume (volume_slabs.h): `slab` holds planes
+  // [z0, z0 + slab.d); seeds (p.seeds, or the reference pattern on plane depth / 2) are in volume
+  // coordinates. Preprocesses the slab's planes, runs the global region-growing fixpoint and the
+  // halo cube dilation with the other ranks of `comm` (collective), leaving the slab on the device:
+  // export_jpegs(slab, ...) then exports its planes. Masks (when requested) are the slab's.
+  VolumeResult run_slab(Comm& comm, const VolumeInput& slab, int z0, int depth, const VolumeParams& p, bool want_masks,
+                        struct SlabStats* stats = nullptr);
 
  private:
   struct Impl;

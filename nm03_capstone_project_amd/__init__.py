@@ -8,7 +8,7 @@ Layers:
       img_processing_parallel)
   models/    the per-slice pipeline (2D) and the volume pipeline (3D) as Python objects
   ops/       torch-tensor entry points of every HIP kernel + plain-PyTorch fp32 references
-  parallel/  torch.distributed (RCCL over xGMI) sharding, collectives, and launch helpers
+  parallel/  native communicators (RCCL over xGMI / host), sharding, cohort plans, z-slab volumes
   utils/     DICOM/JPEG/cohort helpers and the synthetic T1+C cohort generator
 """
 from ._native import native, available  # noqa: F401

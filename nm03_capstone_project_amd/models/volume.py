@@ -33,13 +33,20 @@ class VolumePipeline:
         vol, _ = read_series(series_dir)
         return self.run(vol, seeds=seeds, device=device)
 
-    def run_slabs(self, volume=None, ctx=None, seeds=None, band=None, backend="auto", gather=True):
-        """The same pipeline on a volume split into z-slabs over the ranks of `ctx` (one process per
-        GPU, torch.distributed; parallel/volume_slabs.py). Returns the masks of the whole volume on
-        every rank with gather=True, else this rank's slab."""
+    def run_slabs(self, volume=None, comm=None, seeds=None, band=None, backend="gpu", gather=True, device=None):
+        """The same pipeline on a volume split into z-slabs over the ranks of the native `comm` (one
+        process per GPU; parallel/volume_slabs.py). Returns the whole volume's masks on every rank
+        with gather=True, else this rank's slab."""
         from ..parallel.volume_slabs import run_volume_slabs
-        return run_volume_slabs(volume=volume, ctx=ctx, config=self.config, connectivity=self.connectivity,
-                                dilation=self.dilation, seeds=seeds, band=band, backend=backend, gather=gather)
+        dev = self.config.device if device is None else device
+        runner = None
+        if backend == "gpu":
+            runner = self._runners.get(dev)
+            if runner is None:
+                runner = self._runners[dev] = native().VolumeRunner(dev)
+        return run_volume_slabs(volume=volume, comm=comm, config=self.config, connectivity=self.connectivity,
+                                dilation=self.dilation, seeds=seeds, band=band, backend=backend, gather=gather,
+                                device=dev, runner=runner)
 
     def golden(self, band, seeds):
         n = native()

@@ -1,6 +1,7 @@
-"""Data parallelism over MI355X ranks with torch.distributed (backend "nccl" = RCCL over xGMI on
-ROCm; "gloo" on CPU for tests): shard planning, byte collectives, and the distributed cohort run."""
-from .dist import (DistContext, allgather_bytes, allreduce_max, allreduce_sum, auto_threads,  # noqa: F401
-                   barrier, broadcast_bytes, cgroup_cpu_stat, cpu_budget, init_from_env, shard_bounds)
-from .cohort_runner import CohortPlan, plan_cohort, run_distributed_cohort  # noqa: F401
-from .volume_slabs import dilate_slabs, gather_slabs, grow_slabs, run_volume_slabs  # noqa: F401
+"""Data parallelism over MI355X ranks, one process per GPU, on the native communicators
+(native_comm.py → src/dist/: RCCL over xGMI, or the host comm when ranks share a GPU): rank
+environment, CPU budget and sharding, cohort planning, and the z-slab decomposition of one volume."""
+from .dist import auto_threads, cgroup_cpu_stat, cpu_budget, shard_bounds  # noqa: F401
+from .cohort_runner import CohortPlan, plan_cohort  # noqa: F401
+from .native_comm import make_native_comm, rank_device, rank_env  # noqa: F401
+from .volume_slabs import run_volume_slabs, slab_bounds  # noqa: F401

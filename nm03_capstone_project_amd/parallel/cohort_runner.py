@@ -1,13 +1,13 @@
-"""Distributed cohort processing with torch.distributed — the Python twin of the native
-`img_processing_parallel --gpus N` (src/app/processor.cpp): rank 0 plans (patients, series,
-output directories), broadcasts the work list, every rank runs its contiguous shard through its
-own native Engine, and rank 0 gathers per-slice statuses in the global order."""
+"""Cohort planning for the Python drivers (bench.py): rank 0 discovers the patients, series and
+slice order like the reference (main_sequential.cpp:93-168) and prepares the output directories;
+the plan travels as bytes over a native Comm (broadcast_bytes) and every rank takes its contiguous
+shard (dist.shard_bounds) — the same plan the native `img_processing_parallel` builds
+(src/app/processor.cpp)."""
 import json
 import os
 from dataclasses import dataclass, field
 
 from .._native import native
-from .dist import allgather_bytes, broadcast_bytes, shard_bounds
 
 
 @dataclass
@@ -43,19 +43,3 @@ def plan_cohort(data_root, out_root, wipe=True, replicas=1):
                 os.makedirs(od, exist_ok=True)
             pats.append((pid, od, series, list(files)))
     return CohortPlan(pats)
-
-
-def run_distributed_cohort(engine, plan, ctx):
-    """Run `plan` sharded over ranks. Returns (global statuses on rank 0 or None, local times)."""
-    data = broadcast_bytes(plan.to_bytes() if ctx.is_root else b"", ctx)
-    plan = CohortPlan.from_bytes(data)
-    items = plan.items
-    lo, hi = shard_bounds(len(items), ctx.rank, ctx.world)
-    statuses, times = engine.run(items[lo:hi])
-    gathered = allgather_bytes(json.dumps(statuses).encode(), ctx)
-    if not ctx.is_root:
-        return None, times
-    out = []
-    for g in gathered:
-        out.extend(tuple(s) for s in json.loads(g.decode()))
-    return out, times

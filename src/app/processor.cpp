@@ -50,6 +50,7 @@ void usage(const std::string& which) {
             << "  --dilation-size S      (default 3; 7 in --mode 3d)    --erosion-size S (default 3)\n"
             << "  --quality Q            JPEG quality (default 75)\n"
             << "  --mode 2d|3d           3d: whole series as a volume (SRG 6-conn + cube dilation)\n"
+            << "  --split-volume         3d: each volume split into z-slabs over all ranks (halo exchange)\n"
             << "  --input FILE           test_pipeline: slice to process\n"
             << "  --cpu                  test_pipeline / --mode 3d: golden CPU model instead of the GPU\n"
             << "  --no-montage           test_pipeline: skip the 5-view montage JPEG\n"
@@ -159,6 +160,7 @@ AppConfig parse_args(int argc, char** argv, const std::string& which) {
       c.max_dim_set = true;
     }
     else if (a == "--resume") c.engine.resume = true;
+    else if (a == "--split-volume") c.split_volume = true;
     else {
       std::cerr << "unknown option " << a << " (see --help)" << std::endl;
       std::exit(2);

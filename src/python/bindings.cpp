@@ -7,6 +7,7 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <sys/mman.h>
 #include <unistd.h>
 
 #include <chrono>
@@ -24,6 +25,7 @@
 #include "nm03/kernels.h"
 #include "nm03/synth.h"
 #include "nm03/volume.h"
+#include "nm03/volume_slabs.h"
 
 namespace py = pybind11;
 using namespace nm03;
@@ -714,7 +716,94 @@ PYBIND11_MODULE(_nm03, m) {
                                [&self](const VolumeInput& v, const VolumeParams& vp) { return self.run(v, vp, true); });
           },
           py::arg("volume"), py::arg("params") = PipelineParams(), py::arg("connectivity") = 6,
-          py::arg("dilation") = 7, py::arg("seeds") = std::vector<std::tuple<int, int, int>>{});
+          py::arg("dilation") = 7, py::arg("seeds") = std::vector<std::tuple<int, int, int>>{})
+      .def(
+          "run_slab",
+          // One rank's z-slab (planes [z0, z0 + slab depth) of a `depth`-deep volume) through the
+          // distributed 3D pipeline over `comm` (collective; volume_slabs.h). Seeds in volume
+          // coordinates. Returns the slab's masks plus rounds / exchanged bytes.
+          [](VolumeRunner& self, Comm& comm, py::array_t<uint16_t, py::array::c_style | py::array::forcecast> slab,
+             int z0, int depth, const PipelineParams& p, int connectivity, int dilation,
+             const std::vector<std::tuple<int, int, int>>& seeds) {
+            SlabStats st;
+            py::dict d = volume_call(slab, p, connectivity, dilation, seeds,
+                                     [&](const VolumeInput& v, const VolumeParams& vp) {
+                                       return self.run_slab(comm, v, z0, depth, vp, true, &st);
+                                     });
+            d["rounds"] = st.rounds;
+            d["exchanged_bytes"] = st.exchanged_bytes;
+            return d;
+          },
+          py::arg("comm"), py::arg("slab"), py::arg("z0"), py::arg("depth"), py::arg("params") = PipelineParams(),
+          py::arg("connectivity") = 6, py::arg("dilation") = 7,
+          py::arg("seeds") = std::vector<std::tuple<int, int, int>>{});
+
+  // The same decomposition on the golden model: this rank's slab of a band volume (0/1 uint8,
+  // planes [z0, z0 + d) of `depth`), seeds in volume coordinates. Collective over `comm`.
+  m.def(
+      "golden_volume_slab",
+      [](Comm& comm, py::array_t<uint8_t, py::array::c_style | py::array::forcecast> band, int z0, int depth,
+         const std::vector<std::tuple<int, int, int>>& seeds, int connectivity, int dilation) {
+        if (band.ndim() != 3) throw std::invalid_argument("band must be (depth, height, width)");
+        const int d = (int)band.shape(0), h = (int)band.shape(1), w = (int)band.shape(2);
+        GoldenSlabGrower g(from_np<uint8_t>(band), w, h, d, slab_seeds(seeds_from(seeds), w, h, depth, z0, d),
+                           connectivity);
+        SlabStats st;
+        {
+          py::gil_scoped_release nogil;
+          st = grow_and_dilate_slabs(comm, g, w, h, depth, z0, z0 + d, connectivity, dilation);
+        }
+        py::dict r;
+        r["region"] = to_np<uint8_t>(g.region(), {d, h, w});
+        r["dilated"] = to_np<uint8_t>(g.dilated(), {d, h, w});
+        r["rounds"] = st.rounds;
+        r["exchanged_bytes"] = st.exchanged_bytes;
+        return r;
+      },
+      py::arg("comm"), py::arg("band"), py::arg("z0"), py::arg("depth"), py::arg("seeds"), py::arg("connectivity") = 6,
+      py::arg("dilation") = 7);
+  // CPU self-test of the decomposition: `ranks` forked rank processes over the host comm (no HIP),
+  // each growing its slab of `band` on the golden model; returns the reassembled (region,
+  // dilated, rounds) — to compare with the single-volume golden result.
+  m.def(
+      "golden_slabs_selftest",
+      [](int ranks, py::array_t<uint8_t, py::array::c_style | py::array::forcecast> band,
+         const std::vector<std::tuple<int, int, int>>& seeds, int connectivity, int dilation) {
+        if (band.ndim() != 3) throw std::invalid_argument("band must be (depth, height, width)");
+        const int D = (int)band.shape(0), h = (int)band.shape(1), w = (int)band.shape(2);
+        const size_t vox = (size_t)D * h * w;
+        const std::vector<uint8_t> b = from_np<uint8_t>(band);
+        const std::vector<Seed> sd = seeds_from(seeds);
+        // Results come back through a shared anonymous mapping made before the fork.
+        void* map = mmap(nullptr, 2 * vox + 64, PROT_READ | PROT_WRITE, MAP_SHARED | MAP_ANONYMOUS, -1, 0);
+        if (map == MAP_FAILED) throw std::runtime_error("mmap failed");
+        auto* out = static_cast<uint8_t*>(map);
+        LaunchOptions o;
+        o.comm = "host";
+        o.timeout_s = 60;
+        int rc;
+        {
+          py::gil_scoped_release nogil;
+          rc = launch_ranks(ranks, [&](int rank, int size, Comm& c) {
+            const auto [z0, z1] = slab_bounds(D, rank, size);
+            const size_t plane = (size_t)w * h;
+            GoldenSlabGrower g(std::vector<uint8_t>(b.begin() + (long)(z0 * plane), b.begin() + (long)(z1 * plane)), w, h,
+                               z1 - z0, slab_seeds(sd, w, h, D, z0, z1 - z0), connectivity);
+            const SlabStats st = grow_and_dilate_slabs(c, g, w, h, D, z0, z1, connectivity, dilation);
+            std::memcpy(out + z0 * plane, g.region().data(), g.region().size());
+            std::memcpy(out + vox + z0 * plane, g.dilated().data(), g.dilated().size());
+            if (rank == 0) std::memcpy(out + 2 * vox, &st.rounds, sizeof(int));
+            return 0;
+          }, o);
+        }
+        std::vector<uint8_t> reg(out, out + vox), dil(out + vox, out + 2 * vox);
+        int rounds = 0;
+        std::memcpy(&rounds, out + 2 * vox, sizeof(int));
+        munmap(map, 2 * vox + 64);
+        if (rc != 0) throw std::runtime_error("golden_slabs_selftest: a rank failed with status " + std::to_string(rc));
+        return py::make_tuple(to_np<uint8_t>(reg, {D, h, w}), to_np<uint8_t>(dil, {D, h, w}), rounds);
+      },
+      py::arg("ranks"), py::arg("band"), py::arg("seeds"), py::arg("connectivity") = 6, py::arg("dilation") = 7);
 
   // ---- raw-pointer kernel entry points (torch interop; all synchronous on `stream`) ----------------
   m.def("k_threshold", [](uintptr_t in, uintptr_t out, size_t n, float lo, float hi, uintptr_t stream) {
@@ -900,6 +989,10 @@ PYBIND11_MODULE(_nm03, m) {
           double f = r * 1.5;
           c.allreduce_max_f64(&f, 1);
           if (f != (n - 1) * 1.5) errors[r] = "allreduce_max";
+          // ring neighbour exchange: send r+1 bytes up, receive r bytes from below (none at the ends)
+          std::vector<uint8_t> up((size_t)r + 1, (uint8_t)(10 + r)), got((size_t)std::max(r, 0));
+          c.sendrecv(up.data(), up.size(), r + 1 < n ? r + 1 : -1, got.data(), got.size(), r > 0 ? r - 1 : -1);
+          if (r > 0 && got != std::vector<uint8_t>((size_t)r, (uint8_t)(9 + r))) errors[r] = "sendrecv";
           c.barrier();
         } catch (const std::exception& e) {
           errors[r] = e.what();
@@ -940,6 +1033,13 @@ PYBIND11_MODULE(_nm03, m) {
               double f = rank * 1.5;
               c.allreduce_max_f64(&f, 1);
               if (f != (size - 1) * 1.5) return 15;
+              // neighbour exchange larger than a slot (chunked): rank r sends to r + 1
+              const size_t big = (2u << 20) + 777;
+              std::vector<uint8_t> snd(big), rcv(rank > 0 ? big : 0);
+              for (size_t i = 0; i < big; ++i) snd[i] = (uint8_t)(i * 13 + rank);
+              c.sendrecv(snd.data(), big, rank + 1 < size ? rank + 1 : -1, rcv.data(), rcv.size(), rank > 0 ? rank - 1 : -1);
+              for (size_t i = 0; i < rcv.size(); i += 4097)
+                if (rcv[i] != (uint8_t)(i * 13 + rank - 1)) return 16;
               const bool last = rank == size - 1;
               if (mode == "exit" && last && size > 2) return 7;
               if (mode == "die" && last) _exit(3);

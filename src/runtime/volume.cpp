@@ -16,6 +16,7 @@
 #include "nm03/comm.h"
 #include "nm03/golden.h"
 #include "nm03/thread_pool.h"
+#include "nm03/volume_slabs.h"
 #include "nm03/dicom.h"
 #include "nm03/gpu_types.h"
 #include "nm03/jpeg.h"
@@ -307,6 +308,111 @@ VolumeResult VolumeRunner::run(const VolumeInput& v, const VolumeParams& p, bool
   return r;
 }
 
+namespace {
+
+// GPU backend of the z-slab decomposition: the slab's planes on the device (VolumeDevice); plane
+// reads/writes are small synchronous copies (a boundary plane is 8 KiB for 256²).
+class GpuSlabGrower final : public SlabGrower {
+ public:
+  GpuSlabGrower(VolumeDevice& V, int nseeds, int connectivity) : V_(V), nseeds_(nseeds), conn_(connectivity) {}
+  int grow(bool first) override {
+    srg_volume(V_.band.as<uint64_t>(), V_.region.as<uint64_t>(), V_.w, V_.h, V_.d, V_.seeds.as<int32_t>(),
+               first ? nseeds_ : 0, conn_, V_.flag.as<uint32_t>(), V_.h_flag, V_.srg_scratch.as<uint64_t>(), V_.stream,
+               first);
+    check_hip(hipStreamSynchronize(V_.stream), "slab grow");
+    return srg_volume_result(V_.h_flag);
+  }
+  std::vector<uint64_t> band_plane(int zl) override { return plane(V_.band, zl); }
+  std::vector<uint64_t> region_plane(int zl) override { return plane(V_.region, zl); }
+  void or_region_plane(int zl, const std::vector<uint64_t>& bits) override {
+    std::vector<uint64_t> cur = plane(V_.region, zl);
+    for (size_t i = 0; i < cur.size(); ++i) cur[i] |= bits[i];
+    check_hip(hipMemcpy(V_.region.as<uint64_t>() + (size_t)zl * V_.words, cur.data(), V_.words * 8,
+                        hipMemcpyHostToDevice),
+              "H2D slab plane");
+  }
+  void dilate(int size, const std::vector<std::vector<uint64_t>>& below,
+              const std::vector<std::vector<uint64_t>>& above) override {
+    const int nb = (int)below.size(), na = (int)above.size(), de = nb + V_.d + na;
+    const size_t wds = V_.words;
+    DevBuf ext(wds * de * 8), dil(wds * de * 8), tmp(wds * de * 8), scr(8 * morph3d_scratch_words(V_.w, V_.h, de));
+    for (int k = 0; k < nb; ++k)
+      check_hip(hipMemcpy(ext.as<uint64_t>() + (size_t)k * wds, below[(size_t)k].data(), wds * 8, hipMemcpyHostToDevice),
+                "H2D halo");
+    for (int k = 0; k < na; ++k)
+      check_hip(hipMemcpy(ext.as<uint64_t>() + (size_t)(nb + V_.d + k) * wds, above[(size_t)k].data(), wds * 8,
+                          hipMemcpyHostToDevice),
+                "H2D halo");
+    check_hip(hipMemcpyAsync(ext.as<uint64_t>() + (size_t)nb * wds, V_.region.p, wds * V_.d * 8, hipMemcpyDeviceToDevice,
+                             V_.stream),
+              "D2D slab region");
+    dilate_volume(ext.as<uint64_t>(), dil.as<uint64_t>(), tmp.as<uint64_t>(), V_.w, V_.h, de, size, V_.stream,
+                  scr.as<uint64_t>());
+    check_hip(hipMemcpyAsync(V_.dil.p, dil.as<uint64_t>() + (size_t)nb * wds, wds * V_.d * 8, hipMemcpyDeviceToDevice,
+                             V_.stream),
+              "D2D slab dilation");
+    check_hip(hipStreamSynchronize(V_.stream), "slab dilation");
+  }
+
+ private:
+  std::vector<uint64_t> plane(const DevBuf& b, int zl) {
+    std::vector<uint64_t> v(V_.words);
+    check_hip(hipMemcpy(v.data(), b.as<uint64_t>() + (size_t)zl * V_.words, V_.words * 8, hipMemcpyDeviceToHost),
+              "D2H slab plane");
+    return v;
+  }
+  VolumeDevice& V_;
+  int nseeds_, conn_;
+};
+
+}  // namespace
+
+VolumeResult VolumeRunner::run_slab(Comm& comm, const VolumeInput& slab, int z0, int depth, const VolumeParams& p,
+                                    bool want_masks, SlabStats* stats) {
+  if (slab.d < 1 || slab.w < 1 || slab.h < 1) throw SliceError("empty slab");
+  Impl& I = *impl_;
+  check_hip(hipSetDevice(I.device), "hipSetDevice");
+  if (!I.V || I.V->w != slab.w || I.V->h != slab.h || I.V->d != slab.d) {
+    I.X.reset();
+    I.V.reset();
+    I.V = std::make_unique<VolumeDevice>(slab);
+  }
+  VolumeDevice& V = *I.V;
+  const PipeConsts pc = make_consts(p.pipe, 2);
+  check_hip(hipEventRecord(I.e0, V.stream), "event");
+  volume_preprocess(V, slab, p.pipe, pc);
+  // Seeds in volume coordinates → this slab's (the rest belong to other ranks).
+  std::vector<int32_t> sx;
+  for (const Seed& s : slab_seeds(p.seeds, slab.w, slab.h, depth, z0, slab.d))
+    if (sx.size() / 3 < (size_t)kMaxSeeds) {
+      sx.push_back(s.x);
+      sx.push_back(s.y);
+      sx.push_back(s.z);
+    }
+  if (!sx.empty())
+    check_hip(hipMemcpyAsync(V.seeds.p, sx.data(), sx.size() * 4, hipMemcpyHostToDevice, V.stream), "H2D seeds");
+  GpuSlabGrower g(V, (int)(sx.size() / 3), p.connectivity == 26 ? 26 : 6);
+  const SlabStats st = grow_and_dilate_slabs(comm, g, slab.w, slab.h, depth, z0, z0 + slab.d,
+                                             p.connectivity == 26 ? 26 : 6, p.dilation_size);
+  check_hip(hipEventRecord(I.e1, V.stream), "event");
+  check_hip(hipEventSynchronize(I.e1), "sync");
+  VolumeResult r;
+  r.w = slab.w;
+  r.h = slab.h;
+  r.d = slab.d;
+  r.sweeps = st.sweeps;
+  float ms = 0;
+  (void)hipEventElapsedTime(&ms, I.e0, I.e1);
+  r.kernels_s = ms * 1e-3;
+  if (stats) *stats = st;
+  if (want_masks) {
+    unpack_volume(V.band, V, r.band);
+    unpack_volume(V.region, V, r.region);
+    unpack_volume(V.dil, V, r.dilated);
+  }
+  return r;
+}
+
 std::vector<std::vector<uint8_t>> VolumeRunner::export_jpegs(const VolumeInput& v, const VolumeParams& p,
                                                              const RenderParams& rp, VolumeExportStats* st) {
   Impl& I = *impl_;
@@ -437,6 +543,8 @@ struct VolOutcome {
   int32_t sweeps = 0;
   double gpu_s = 0, export_s = 0, wall_s = 0;
   int64_t slices = 0, fallbacks = 0;
+  int32_t rounds = 0;         // --split-volume: grow/exchange rounds
+  int64_t exchanged = 0;      // --split-volume: boundary + halo bytes sent
 };
 
 std::vector<uint8_t> encode(const std::vector<VolPatient>& pl) {
@@ -478,44 +586,42 @@ void write_file(const std::string& path, const std::vector<uint8_t>& jpg) {
 
 // Golden 3D path (--cpu): per-plane preprocessing on a thread pool, 3D SRG + cube dilation, host
 // render + encoder — the oracle the GPU 3D export is checked against.
-std::vector<std::vector<uint8_t>> golden_volume_jpegs(const VolumeInput& v, const VolumeParams& vp,
-                                                      const RenderParams& rp) {
+struct GoldenPlanes {
+  std::vector<uint8_t> band;               // 0/1 voxels of every plane
+  std::vector<std::vector<float>> vals;    // rescaled values per plane (original render)
+};
+
+GoldenPlanes golden_preprocess(const VolumeInput& v, const VolumeParams& vp) {
   const size_t plane = (size_t)v.w * v.h;
-  std::vector<uint8_t> band(plane * v.d);
-  std::vector<std::vector<float>> vals((size_t)v.d);
-  auto slice = [&](int z) {
-    golden::SliceInput si;
-    si.w = v.w;
-    si.h = v.h;
-    si.type = v.type;
-    si.stored_bits = v.stored_bits;
-    si.slope = v.slope;
-    si.intercept = v.intercept;
-    si.spacing_x = v.spacing_x;
-    si.spacing_y = v.spacing_y;
-    si.raw.assign(v.raw.begin() + z * plane, v.raw.begin() + (z + 1) * plane);
-    return si;
-  };
-  {
-    ThreadPool pool(16);
-    TaskGroup tg(pool);
-    for (int z = 0; z < v.d; ++z)
-      tg.run([&, z] {
-        golden::SliceInput si = slice(z);
-        golden::SliceResult r = golden::run(si, vp.pipe, false);
-        std::copy(r.band.begin(), r.band.end(), band.begin() + z * plane);
-        vals[z] = golden::rescaled(si, vp.pipe);
-      });
-    tg.wait();
-  }
-  std::vector<Seed> seeds = vp.seeds;
-  if (seeds.empty()) {
-    seeds = reference_seeds(v.w, v.h);
-    for (auto& sd : seeds) sd.z = v.d / 2;
-  }
-  const auto region = golden::region_grow3d(band, v.w, v.h, v.d, seeds, vp.connectivity);
-  const auto dil = golden::dilate3d(region, v.w, v.h, v.d, vp.dilation_size);
-  const jpeg::Tables t = jpeg::make_tables(rp.jpeg_quality);
+  GoldenPlanes g;
+  g.band.assign(plane * v.d, 0);
+  g.vals.resize((size_t)v.d);
+  ThreadPool pool(16);
+  TaskGroup tg(pool);
+  for (int z = 0; z < v.d; ++z)
+    tg.run([&, z] {
+      golden::SliceInput si;
+      si.w = v.w;
+      si.h = v.h;
+      si.type = v.type;
+      si.stored_bits = v.stored_bits;
+      si.slope = v.slope;
+      si.intercept = v.intercept;
+      si.spacing_x = v.spacing_x;
+      si.spacing_y = v.spacing_y;
+      si.raw.assign(v.raw.begin() + z * plane, v.raw.begin() + (z + 1) * plane);
+      golden::SliceResult r = golden::run(si, vp.pipe, false);
+      std::copy(r.band.begin(), r.band.end(), g.band.begin() + z * plane);
+      g.vals[z] = golden::rescaled(si, vp.pipe);
+    });
+  tg.wait();
+  return g;
+}
+
+// The 2·d files (original, processed per plane) of the dilated mask `dil` of volume `v`.
+std::vector<std::vector<uint8_t>> golden_export(const VolumeInput& v, const std::vector<std::vector<float>>& vals,
+                                                const std::vector<uint8_t>& dil, const RenderParams& rp) {
+  const size_t plane = (size_t)v.w * v.h;
   const RenderGeom g = make_render_geom(v.w, v.h, v.spacing_x, v.spacing_y, rp.out_width, rp.out_height);
   std::vector<std::vector<uint8_t>> files((size_t)2 * v.d);
   for (int z = 0; z < v.d; ++z) {
@@ -528,6 +634,30 @@ std::vector<std::vector<uint8_t>> golden_volume_jpegs(const VolumeInput& v, cons
     files[2 * z + 1] = jpeg::encode_gray420(c1.data(), rp.out_width, rp.out_height, rp.out_width, rp.jpeg_quality);
   }
   return files;
+}
+
+std::vector<std::vector<uint8_t>> golden_volume_jpegs(const VolumeInput& v, const VolumeParams& vp,
+                                                      const RenderParams& rp) {
+  const GoldenPlanes gp = golden_preprocess(v, vp);
+  std::vector<Seed> seeds = vp.seeds;
+  if (seeds.empty()) {
+    seeds = reference_seeds(v.w, v.h);
+    for (auto& sd : seeds) sd.z = v.d / 2;
+  }
+  const auto region = golden::region_grow3d(gp.band, v.w, v.h, v.d, seeds, vp.connectivity);
+  const auto dil = golden::dilate3d(region, v.w, v.h, v.d, vp.dilation_size);
+  return golden_export(v, gp.vals, dil, rp);
+}
+
+// One rank's z-slab of a volume on the golden model (--cpu --split-volume): the same
+// decomposition and exchanges as the GPU slab path (volume_slabs.h), host arithmetic.
+std::vector<std::vector<uint8_t>> golden_slab_jpegs(Comm& comm, const VolumeInput& slab, int z0, int depth,
+                                                    const VolumeParams& vp, const RenderParams& rp, SlabStats* st) {
+  GoldenPlanes gp = golden_preprocess(slab, vp);
+  GoldenSlabGrower g(std::move(gp.band), slab.w, slab.h, slab.d, slab_seeds(vp.seeds, slab.w, slab.h, depth, z0, slab.d),
+                     vp.connectivity);
+  *st = grow_and_dilate_slabs(comm, g, slab.w, slab.h, depth, z0, z0 + slab.d, vp.connectivity, vp.dilation_size);
+  return golden_export(slab, gp.vals, g.dilated(), rp);
 }
 
 int volume_rank(const AppConfig& cfg, int rank, int size, Comm& comm, int device) {
@@ -591,7 +721,74 @@ int volume_rank(const AppConfig& cfg, int rank, int size, Comm& comm, int device
   }
   std::vector<VolOutcome> mine;
   double my_wall = 0;
-  for (size_t i = lo; i < hi; ++i) {
+  auto write_planes = [&](const VolPatient& pp, int z0, int d, const std::vector<std::vector<uint8_t>>& files) {
+    for (int z = 0; z < d; ++z) {
+      const std::string stem = pp.out_dir + "/" + cohort::stem(pp.files[(size_t)(z0 + z)]);
+      write_file(stem + "_original.jpg", files[2 * z]);
+      write_file(stem + "_processed.jpg", files[2 * z + 1]);
+    }
+  };
+  if (cfg.split_volume) {
+    // Every patient's volume over ALL ranks, one z-slab each (volume_slabs.h). Failures before the
+    // collective part are agreed on first; a failure inside it is fatal for the rank, and the
+    // launcher's abort flag then ends the others' collectives.
+    for (const VolPatient& pp : plan) {
+      VolOutcome o;
+      const double t0 = wall_now();
+      const int depth = (int)pp.files.size();
+      int z0 = 0, z1 = 0;
+      VolumeInput slab;
+      int64_t bad = 0;
+      try {
+        if (!setup_error.empty()) throw std::runtime_error(setup_error);
+        if (!pp.listed) throw std::runtime_error(pp.error);
+        if (depth < size)
+          throw std::runtime_error("--split-volume: " + std::to_string(depth) + " planes cannot be split over " +
+                                   std::to_string(size) + " ranks");
+        std::tie(z0, z1) = slab_bounds(depth, rank, size);
+        slab = load_volume(std::vector<std::string>(pp.files.begin() + z0, pp.files.begin() + z1));
+      } catch (const std::exception& e) {
+        o.message = e.what();
+        bad = 1;
+      }
+      // Agree on failures and on the plane shape before any exchange.
+      double shape[2] = {bad ? -1.0 : (double)slab.w, bad ? -1.0 : (double)slab.h};
+      double nshape[2] = {-shape[0], -shape[1]};
+      comm.allreduce_sum_i64(&bad, 1);
+      comm.allreduce_max_f64(shape, 2);
+      comm.allreduce_max_f64(nshape, 2);
+      if (!bad && (shape[0] != -nshape[0] || shape[1] != -nshape[1])) {
+        bad = 1;
+        o.message = "volume slices differ in size across slabs";
+      }
+      if (!bad) {
+        SlabStats st;
+        std::vector<std::vector<uint8_t>> files;
+        if (cfg.cpu) {
+          files = golden_slab_jpegs(comm, slab, z0, depth, vp, rp, &st);
+        } else {
+          VolumeResult r = runner->run_slab(comm, slab, z0, depth, vp, false, &st);
+          o.gpu_s = r.kernels_s;
+          VolumeExportStats xs;
+          files = runner->export_jpegs(slab, vp, rp, &xs);
+          o.export_s = xs.export_s;
+          o.fallbacks = xs.jpeg_fallbacks;
+        }
+        o.sweeps = st.sweeps;
+        o.rounds = st.rounds;
+        o.exchanged = st.exchanged_bytes;
+        o.slices = slab.d;
+        write_planes(pp, z0, slab.d, files);
+        o.ok = 1;
+      } else if (o.message.empty()) {
+        o.message = "failed on another rank";
+      }
+      o.wall_s = wall_now() - t0;
+      my_wall += o.wall_s;
+      mine.push_back(std::move(o));
+    }
+  }
+  for (size_t i = lo; i < hi && !cfg.split_volume; ++i) {
     const VolPatient& pp = plan[i];
     VolOutcome o;
     const double t0 = wall_now();
@@ -612,11 +809,7 @@ int volume_rank(const AppConfig& cfg, int rank, int size, Comm& comm, int device
         o.export_s = xs.export_s;
         o.fallbacks = xs.jpeg_fallbacks;
       }
-      for (int z = 0; z < v.d; ++z) {
-        const std::string stem = pp.out_dir + "/" + cohort::stem(pp.files[z]);
-        write_file(stem + "_original.jpg", files[2 * z]);
-        write_file(stem + "_processed.jpg", files[2 * z + 1]);
-      }
+      write_planes(pp, 0, v.d, files);
       o.ok = 1;
     } catch (const std::exception& e) {
       o.message = e.what();
@@ -637,6 +830,8 @@ int volume_rank(const AppConfig& cfg, int rank, int size, Comm& comm, int device
     w.f64(o.wall_s);
     w.u64((uint64_t)o.slices);
     w.u64((uint64_t)o.fallbacks);
+    w.i32(o.rounds);
+    w.u64((uint64_t)o.exchanged);
   }
   auto all = comm.allgather_bytes(w.b);
   double tot = wall_now() - t_start;
@@ -658,8 +853,35 @@ int volume_rank(const AppConfig& cfg, int rank, int size, Comm& comm, int device
       o.wall_s = r.f64();
       o.slices = (int64_t)r.u64();
       o.fallbacks = (int64_t)r.u64();
+      o.rounds = r.i32();
+      o.exchanged = (int64_t)r.u64();
       outs.push_back(std::move(o));
     }
+  }
+  if (cfg.split_volume) {
+    // Rank-major per-patient outcomes → one per patient: ok if every slab was, the first failure's
+    // message, the slowest slab's times, the sum of planes and exchanged bytes.
+    std::vector<VolOutcome> merged(plan.size());
+    for (size_t i = 0; i < plan.size(); ++i) {
+      VolOutcome& m = merged[i];
+      m.ok = 1;
+      for (int q = 0; q < size; ++q) {
+        const VolOutcome& o = outs[(size_t)q * plan.size() + i];
+        if (!o.ok) {
+          if (m.ok || m.message == "failed on another rank") m.message = o.message;
+          m.ok = 0;
+        }
+        m.sweeps = std::max(m.sweeps, o.sweeps);
+        m.rounds = std::max(m.rounds, o.rounds);
+        m.gpu_s = std::max(m.gpu_s, o.gpu_s);
+        m.export_s = std::max(m.export_s, o.export_s);
+        m.wall_s = std::max(m.wall_s, o.wall_s);
+        m.slices += o.slices;
+        m.fallbacks += o.fallbacks;
+        m.exchanged += o.exchanged;
+      }
+    }
+    outs = std::move(merged);
   }
   int successful = 0;
   int64_t slices = 0, fallbacks = 0;
@@ -682,12 +904,16 @@ int volume_rank(const AppConfig& cfg, int rank, int size, Comm& comm, int device
       else
         std::cout << "\nPatient " << pp.id << " completed. 3D region growing converged in " << o.sweeps
                   << " sweeps; GPU time " << o.gpu_s * 1e3 << " ms." << std::endl;
+      if (cfg.split_volume)
+        std::cout << "Split over " << size << " ranks: " << o.rounds << " exchange rounds, " << o.exchanged
+                  << " bytes exchanged." << std::endl;
     } else {
       std::cerr << "Error processing patient " << pp.id << ": " << o.message << std::endl;
     }
     pj << (i ? ", " : "") << "{\"id\": \"" << pp.id << "\", \"ok\": " << (o.ok ? "true" : "false")
        << ", \"slices\": " << o.slices << ", \"sweeps\": " << o.sweeps << ", \"gpu_s\": " << o.gpu_s
-       << ", \"export_s\": " << o.export_s << ", \"wall_s\": " << o.wall_s << "}";
+       << ", \"export_s\": " << o.export_s << ", \"wall_s\": " << o.wall_s << ", \"rounds\": " << o.rounds
+       << ", \"exchanged_bytes\": " << o.exchanged << "}";
   }
   std::cout << "\n=== All Processing Completed ===\n" << std::endl;
   std::cout << "Successfully processed " << successful << "/" << plan.size() << " patients." << std::endl;
@@ -695,7 +921,8 @@ int volume_rank(const AppConfig& cfg, int rank, int size, Comm& comm, int device
     std::ofstream f(cfg.json, std::ios::trunc);
     f << "{\"mode\": \"3d\", \"backend\": \"" << (cfg.cpu ? "cpu" : "gpu") << "\", \"gpus\": " << size
       << ", \"comm\": \"" << comm.backend() << "\", \"dilation_size\": " << vp.dilation_size
-      << ", \"connectivity\": " << vp.connectivity << ", \"wall_s\": " << tot << ", \"slices\": " << slices
+      << ", \"connectivity\": " << vp.connectivity << ", \"split_volume\": " << (cfg.split_volume ? "true" : "false")
+      << ", \"wall_s\": " << tot << ", \"slices\": " << slices
       << ", \"jpeg_fallbacks\": " << fallbacks << ", \"per_rank_wall_s\": [";
     for (int r = 0; r < size; ++r) f << (r ? ", " : "") << walls[r];
     f << "], \"patients\": [" << pj.str() << "]}\n";
@@ -710,7 +937,13 @@ int run_volume_cohort(const AppConfig& cfg) {
   // (3D SRG + cube dilation on the GPU), exported per plane like the 2D run; patients are sharded
   // over the ranks (one process per MI355X) like the 2D work list.
   LaunchOptions lo = LaunchOptions::from_env();
-  const int n = cfg.cpu ? 1 : resolve_gpus(cfg, lo);
+  int n = 1;
+  if (cfg.cpu) {  // golden model: the ranks are CPU processes over the host comm (default 1)
+    n = std::max(1, cfg.gpus);
+    lo.comm = "host";
+  } else {
+    n = resolve_gpus(cfg, lo);
+  }
   return launch_ranks(n, [&](int rank, int size, Comm& comm) {
     const int dev = size > 1 ? lo.device_of(rank) : lo.device_override >= 0 ? lo.device_override : cfg.engine.device;
     return volume_rank(cfg, rank, size, comm, dev);

@@ -108,6 +108,37 @@ def test_volume_cli_cpu_golden(native, cohort_root, tmp_path):
     assert r.returncode == 0 and json.load(open(js))["dilation_size"] == 3
 
 
+def _tree(root):
+    return {str(p.relative_to(root)): p.read_bytes() for p in sorted(root.rglob("*.jpg"))}
+
+
+@pytest.mark.parametrize("ranks,conn", [(2, "6"), (3, "26"), (4, "6")])
+def test_volume_cli_cpu_split_volume_identical(native, cohort_root, tmp_path, ranks, conn):
+    """--mode 3d --cpu --split-volume --gpus N: every volume cut into z-slabs over N rank processes
+    (host comm), boundary planes and dilation halos exchanged (volume_slabs.h) — byte-identical to
+    the single-process golden 3D output (thin slabs included: 3–5 planes, dilation radius 3)."""
+    import json
+    ref, out = tmp_path / "ref", tmp_path / "split"
+    r = run_bin("img_processing_parallel", "--mode", "3d", "--cpu", "--srg-connectivity", conn, "--data-root",
+                cohort_root, "--out", str(ref), "--quiet")
+    assert r.returncode == 0, r.stderr
+    r = run_bin("img_processing_parallel", "--mode", "3d", "--cpu", "--split-volume", "--gpus", str(ranks),
+                "--srg-connectivity", conn, "--data-root", cohort_root, "--out", str(out), "--quiet", "--json",
+                str(tmp_path / "s.json"))
+    if ranks > 3:  # the cohort has 3–5 planes per patient: a too-thin volume fails, the rest succeed
+        assert r.returncode == 0, r.stderr
+        j = json.load(open(tmp_path / "s.json"))
+        bad = [p for p in j["patients"] if not p["ok"]]
+        assert bad and all(p["slices"] == 0 for p in bad)
+        assert "cannot be split over 4 ranks" in r.stderr
+        return
+    assert r.returncode == 0, r.stderr
+    t = _tree(ref)
+    assert len(t) > 0 and _tree(out) == t
+    j = json.load(open(tmp_path / "s.json"))
+    assert j["split_volume"] and j["gpus"] == ranks and all(p["ok"] for p in j["patients"])
+
+
 @pytest.mark.parametrize("cli,args", [
     ("test_pipeline", ["--cpu"]),
     ("img_processing_parallel", ["--mode", "3d", "--cpu"]),

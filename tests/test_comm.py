@@ -1,11 +1,8 @@
-"""Distributed layer on CPU: loopback Comm, fork launcher, torch.distributed (gloo) helpers,
+"""Distributed layer on CPU: loopback Comm, fork launcher, native host comm across processes,
 sharding coverage."""
 import os
-import socket
 
 import pytest
-import torch
-import torch.multiprocessing as mp
 
 from nm03_capstone_project_amd.parallel import dist as D
 
@@ -88,75 +85,31 @@ def test_shard_bounds_cover_once(n, world):
     assert seen == list(range(n))
 
 
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
-
-
-def _worker(rank, world, port, q):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
-                      LOCAL_RANK=str(rank))
-    ctx = D.init_from_env(backend="gloo", use_gpu=False)
-    try:
-        b = D.broadcast_bytes(b"work-list" if rank == 0 else b"", ctx)
-        g = D.allgather_bytes(bytes([rank]) * (rank + 1), ctx)
-        mx = D.allreduce_max(rank * 2.5, ctx)
-        sm = D.allreduce_sum(rank + 1, ctx)
-        D.barrier(ctx)
-        q.put((rank, b, g, mx, sm))
-    finally:
-        torch.distributed.destroy_process_group()
-
-
-def test_torch_gloo_collectives():
-    world, port = 2, _free_port()
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    ps = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
-    for p in ps:
-        p.start()
-    res = sorted(q.get(timeout=120) for _ in range(world))
-    for p in ps:
-        p.join(60)
-        assert p.exitcode == 0
-    for rank, b, g, mx, sm in res:
-        assert b == b"work-list"
-        assert g == [b"\x00", b"\x01\x01"]
-        assert mx == 2.5 and sm == 3
-
-
-def _cohort_worker(rank, world, port, data_root, out_root, q):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
-                      LOCAL_RANK=str(rank))
+def test_plan_broadcast_over_native_host_comm(cohort_root, tmp_path, native):
+    """bench.py's planning path without torch: rank 0 plans the cohort, the plan travels over the
+    native host comm (forked rank), every rank takes its contiguous shard."""
     from nm03_capstone_project_amd.parallel import cohort_runner as C
-    ctx = D.init_from_env(backend="gloo", use_gpu=False)
-    try:
-        plan = C.plan_cohort(data_root, out_root) if rank == 0 else C.CohortPlan()
-        data = D.broadcast_bytes(plan.to_bytes() if rank == 0 else b"", ctx)
-        plan = C.CohortPlan.from_bytes(data)
-        lo, hi = D.shard_bounds(len(plan.items), rank, world)
-        q.put((rank, len(plan.items), lo, hi))
-    finally:
-        torch.distributed.destroy_process_group()
-
-
-def test_distributed_plan_broadcast(cohort_root, tmp_path):
-    world, port = 2, _free_port()
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    ps = [ctx.Process(target=_cohort_worker, args=(r, world, port, cohort_root, str(tmp_path / "out"), q))
-          for r in range(world)]
-    for p in ps:
-        p.start()
-    res = sorted(q.get(timeout=120) for _ in range(world))
-    for p in ps:
-        p.join(60)
-    n = res[0][1]
-    assert all(r[1] == n for r in res) and n > 0
-    assert res[0][2] == 0 and res[-1][3] == n and res[0][3] == res[1][2]
+    seg, name = native.shm_create(2)
+    r_out, w_out = os.pipe()
+    pid = os.fork()
+    if pid == 0:  # rank 1
+        code = 1
+        try:
+            c1 = native.host_comm(native.shm_attach(name, 2, 10.0), 1, 10.0)
+            plan = C.CohortPlan.from_bytes(c1.broadcast_bytes(b"", 0))
+            lo, hi = D.shard_bounds(len(plan.items), 1, 2)
+            os.write(w_out, f"{len(plan.items)} {lo} {hi}".encode())
+            code = 0
+        finally:
+            os._exit(code)
+    seg.wait_attached_and_unlink(10.0)
+    c0 = native.host_comm(seg, 0, 10.0)
+    plan = C.plan_cohort(cohort_root, str(tmp_path / "out"))
+    assert C.CohortPlan.from_bytes(c0.broadcast_bytes(plan.to_bytes(), 0)).items == plan.items
+    _, st = os.waitpid(pid, 0)
+    assert os.WEXITSTATUS(st) == 0
+    n, lo, hi = map(int, os.read(r_out, 100).decode().split())
+    assert n == len(plan.items) > 0 and lo == D.shard_bounds(n, 0, 2)[1] and hi == n
 
 
 def test_auto_threads_respects_budget(monkeypatch):

@@ -755,7 +755,7 @@ def test_test_pipeline_dump_mhd_gpu_equals_cpu(native, cohort_root, tmp_path):
 
 
 # ---------------------------------------------------------------------------------------------
-# 3D torch ops and the z-slab decomposition (parallel/volume_slabs.py) on the GPU
+# 3D torch ops and the z-slab decomposition (volume_slabs.h, parallel/volume_slabs.py) on the GPU
 # ---------------------------------------------------------------------------------------------
 def test_region_grow3d_and_dilate3d_ops_vs_golden(native):
     from nm03_capstone_project_amd import ops
@@ -797,56 +797,30 @@ def test_volume_slabs_single_rank_equals_volume_pipeline(native):
     vol = np.stack([native.phantom_slice(h, w, 2, z, d, 5) for z in range(d)])
     vp = nm.VolumePipeline(connectivity=6, dilation=7)
     ref = vp.run(vol)
-    ctx = nm.parallel.DistContext(0, 1, 0, "none", torch.device("cuda", 0))
-    r = run_volume_slabs(volume=vol, ctx=ctx, connectivity=6, dilation=7, backend="gpu")
-    assert ref["region"].sum() > 0
-    assert np.array_equal(r["band"].cpu().numpy().astype(np.uint8), ref["band"])
-    assert np.array_equal(r["region"].cpu().numpy().astype(np.uint8), ref["region"])
-    assert np.array_equal(r["dilated"].cpu().numpy().astype(np.uint8), ref["dilated"])
+    r = run_volume_slabs(volume=vol, connectivity=6, dilation=7, backend="gpu")
+    assert ref["region"].sum() > 0 and (r["z0"], r["z1"]) == (0, d) and r["rounds"] == 1
+    for k in ("band", "region", "dilated"):
+        assert np.array_equal(r[k], ref[k]), k
 
 
-def _slab_gpu_worker(rank, world, port, q):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
-                      LOCAL_RANK=str(rank), NM03_DEVICE_OVERRIDE="0")
-    import nm03_capstone_project_amd as nmx
-    from nm03_capstone_project_amd.parallel.volume_slabs import run_volume_slabs
-    ctx = nmx.parallel.init_from_env(backend="gloo")
-    try:
-        n = nmx.native()
-        d, h, w = 24, 96, 128
-        vol = np.stack([n.phantom_slice(h, w, 2, z, d, 5) for z in range(d)])
-        r = run_volume_slabs(volume=vol, ctx=ctx, connectivity=26, dilation=7, backend="gpu", gather=True)
-        q.put((rank, r["region"].cpu().numpy().astype(np.uint8), r["dilated"].cpu().numpy().astype(np.uint8),
-               r["rounds"]))
-    finally:
-        torch.distributed.destroy_process_group()
-
-
-def test_volume_slabs_two_ranks_on_one_gpu(native):
-    """Two ranks (spawned, gloo collectives, both on device 0) decompose one volume into z-slabs:
-    the gathered masks equal the single-GPU VolumePipeline result."""
-    import socket
-    import torch.multiprocessing as mp
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    d, h, w = 24, 96, 128
-    vol = np.stack([native.phantom_slice(h, w, 2, z, d, 5) for z in range(d)])
-    ref = nm.VolumePipeline(connectivity=26, dilation=7).run(vol)
-    mctx = mp.get_context("spawn")
-    q = mctx.Queue()
-    ps = [mctx.Process(target=_slab_gpu_worker, args=(r, 2, port, q)) for r in range(2)]
-    for p in ps:
-        p.start()
-    res = [q.get(timeout=100) for _ in range(2)]
-    for p in ps:
-        p.join(30)
-        assert p.exitcode == 0
-    for rank, region, dil, rounds in res:
-        assert np.array_equal(region, ref["region"]), rank
-        assert np.array_equal(dil, ref["dilated"]), rank
-        assert rounds >= 2  # the lesion spans the slab boundary: at least one exchange added voxels
+@pytest.mark.parametrize("ranks", [2, 3])
+def test_volume_cli_split_volume_identical(native, cohort_root, tmp_path, ranks):
+    """img_processing_parallel --mode 3d --split-volume: every volume cut into z-slabs over N ranks
+    (host comm, all on GPU 0), boundary planes and dilation halos exchanged natively — the output
+    tree is byte-identical to the single-GPU 3D run."""
+    import json
+    ref, out = tmp_path / "ref", tmp_path / "split"
+    r = run_bin("img_processing_parallel", "--mode", "3d", "--data-root", cohort_root, "--out", str(ref), "--quiet")
+    assert r.returncode == 0, r.stderr
+    r = run_bin("img_processing_parallel", "--mode", "3d", "--split-volume", "--gpus", str(ranks), "--data-root",
+                cohort_root, "--out", str(out), "--quiet", "--json", str(tmp_path / "s.json"),
+                env={"NM03_DEVICE_OVERRIDE": "0", "NM03_COMM_TIMEOUT_S": "60"})
+    assert r.returncode == 0, r.stderr
+    assert f"Split over {ranks} ranks" in r.stdout
+    t = _tree(str(ref))
+    assert len(t) > 0 and _tree(str(out)) == t
+    j = json.load(open(tmp_path / "s.json"))
+    assert j["split_volume"] and j["gpus"] == ranks and all(p["ok"] and p["rounds"] >= 1 for p in j["patients"])
 
 
 def test_cli_parallel_sizes_buffers_from_headers(native, cohort_root, tmp_path):

@@ -1,22 +1,12 @@
-"""Z-slab decomposition of one 3D volume over ranks (parallel/volume_slabs.py) on the
-CPU: gloo process groups of 2 and 3 ranks, golden backend. The reassembled region and dilation must
-equal the single-volume golden 3D region growing + cube dilation exactly, including a serpentine
-band that crosses every slab boundary many times (many exchange rounds)."""
+"""Z-slab decomposition of one 3D volume over ranks (include/nm03/volume_slabs.h,
+parallel/volume_slabs.py) on the CPU: forked rank processes over the native host comm, golden
+backend. The reassembled region and dilation must equal the single-volume golden 3D region growing
++ cube dilation exactly, including a serpentine band that crosses every slab boundary many times
+(many exchange rounds) and slabs thinner than the dilation radius (halo from several ranks)."""
 import os
-import socket
 
 import numpy as np
 import pytest
-import torch
-import torch.multiprocessing as mp
-
-
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
 
 
 def _serpentine(d, h, w):
@@ -40,102 +30,51 @@ def _volumes():
     return {"random": (rand, seeds_rand), "snake": (snake, [(0, 2, 0)])}
 
 
-def _worker(rank, world, port, conn, dilation, q):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
-                      LOCAL_RANK=str(rank))
-    from nm03_capstone_project_amd.parallel import dist as D
-    from nm03_capstone_project_amd.parallel.volume_slabs import run_volume_slabs
-    ctx = D.init_from_env(backend="gloo", use_gpu=False)
-    try:
-        out = {}
-        for name, (band, seeds) in _volumes().items():
-            r = run_volume_slabs(band=band, ctx=ctx, connectivity=conn, dilation=dilation, seeds=seeds,
-                                 backend="cpu", gather=True)
-            out[name] = (r["region"].numpy().astype(np.uint8), r["dilated"].numpy().astype(np.uint8), r["rounds"])
-        q.put((rank, out))
-    finally:
-        torch.distributed.destroy_process_group()
-
-
-@pytest.mark.parametrize("world,conn,dilation", [(2, 6, 7), (3, 26, 3), (3, 6, 5)])
+@pytest.mark.parametrize("world,conn,dilation", [(2, 6, 7), (3, 26, 3), (3, 6, 5), (5, 26, 7)])
 def test_slabs_equal_single_volume(native, world, conn, dilation):
-    port = _free_port()
-    mctx = mp.get_context("spawn")
-    q = mctx.Queue()
-    ps = [mctx.Process(target=_worker, args=(r, world, port, conn, dilation, q)) for r in range(world)]
-    for p in ps:
-        p.start()
-    res = sorted((q.get(timeout=180) for _ in range(world)), key=lambda t: t[0])
-    for p in ps:
-        p.join(60)
-        assert p.exitcode == 0
     for name, (band, seeds) in _volumes().items():
-        ref_r = native.golden_region_grow3d(band, seeds, conn)
-        ref_d = native.golden_dilate3d(ref_r, dilation)
-        assert ref_r.sum() > 0
-        for rank, out in res:
-            region, dil, rounds = out[name]
-            assert np.array_equal(region, ref_r), (name, rank)
-            assert np.array_equal(dil, ref_d), (name, rank)
-        if name == "snake" and conn == 6:
-            assert res[0][1][name][2] > 4  # growth hopped across slab boundaries several times
+        region, dil, rounds = native.golden_slabs_selftest(world, band, seeds, conn, dilation)
+        ref = native.golden_region_grow3d(band, seeds, conn)
+        assert np.array_equal(region, ref), name
+        assert np.array_equal(dil, native.golden_dilate3d(ref, dilation)), name
+        if name == "snake":
+            assert rounds > world  # growth hops between slabs round after round
 
 
-def test_single_rank_matches_golden(native):
+def test_run_volume_slabs_api_two_processes(native):
+    """parallel.run_volume_slabs (cpu backend, gather=True) in two forked processes over a named
+    native segment: both ranks return the whole volume's masks, equal to the golden model."""
     from nm03_capstone_project_amd.parallel.volume_slabs import run_volume_slabs
     band, seeds = _volumes()["random"]
-    r = run_volume_slabs(band=band, connectivity=6, dilation=7, seeds=seeds, backend="cpu")
-    ref = native.golden_region_grow3d(band, seeds, 6)
-    assert np.array_equal(r["region"].numpy().astype(np.uint8), ref)
-    assert np.array_equal(r["dilated"].numpy().astype(np.uint8), native.golden_dilate3d(ref, 7))
-    assert r["rounds"] == 1 and r["z0"] == 0
-
-
-def test_volume_pipeline_run_slabs_cpu(native):
-    """VolumePipeline.run_slabs (single process, golden backend) == golden 3D region growing + dilation."""
-    import nm03_capstone_project_amd as nm
-    band, seeds = _volumes()["random"]
-    vp = nm.VolumePipeline(connectivity=26, dilation=5)
-    r = vp.run_slabs(band=band, seeds=seeds, backend="cpu")
     ref = native.golden_region_grow3d(band, seeds, 26)
-    assert np.array_equal(r["region"].numpy().astype(np.uint8), ref)
-    assert np.array_equal(r["dilated"].numpy().astype(np.uint8), native.golden_dilate3d(ref, 5))
+    refd = native.golden_dilate3d(ref, 5)
+    seg, name = native.shm_create(2)
+    pid = os.fork()
+    if pid == 0:
+        code = 1
+        try:
+            c1 = native.host_comm(native.shm_attach(name, 2, 10.0), 1, 20.0)
+            r = run_volume_slabs(band=band, comm=c1, connectivity=26, dilation=5, seeds=seeds, backend="cpu",
+                                 gather=True)
+            code = 0 if (np.array_equal(r["region"], ref) and np.array_equal(r["dilated"], refd)) else 2
+        finally:
+            os._exit(code)
+    seg.wait_attached_and_unlink(10.0)
+    c0 = native.host_comm(seg, 0, 20.0)
+    r = run_volume_slabs(band=band, comm=c0, connectivity=26, dilation=5, seeds=seeds, backend="cpu", gather=True)
+    assert (r["z0"], r["z1"]) == (0, 6)
+    assert np.array_equal(r["region"], ref) and np.array_equal(r["dilated"], refd)
+    _, st = os.waitpid(pid, 0)
+    assert os.WEXITSTATUS(st) == 0
 
 
-def _empty_slab_worker(rank, world, port, q):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
-                      LOCAL_RANK=str(rank))
-    from nm03_capstone_project_amd.parallel import dist as D
-    from nm03_capstone_project_amd.parallel.volume_slabs import grow_slabs, run_volume_slabs
-    ctx = D.init_from_env(backend="gloo", use_gpu=False)
-    errs = []
-    try:
-        band = np.ones((2, 8, 8), dtype=bool)  # depth 2 < 3 ranks
-        for call in (lambda: run_volume_slabs(band=band, ctx=ctx, backend="cpu"),
-                     # a caller-built decomposition with an empty slab on the last rank
-                     lambda: grow_slabs(torch.from_numpy(band[:1] if rank < 2 else band[:0]), rank, [(1, 1, 0)], ctx)):
-            try:
-                call()
-                errs.append("no error")
-            except ValueError as e:
-                errs.append(str(e))
-        q.put((rank, errs))
-    finally:
-        torch.distributed.destroy_process_group()
-
-
-def test_empty_slabs_fail_on_every_rank(native):
-    """depth < world: every rank raises (no rank left waiting in a collective) — ADVICE r1."""
-    world, port = 3, _free_port()
-    mctx = mp.get_context("spawn")
-    q = mctx.Queue()
-    ps = [mctx.Process(target=_empty_slab_worker, args=(r, world, port, q)) for r in range(world)]
-    for p in ps:
-        p.start()
-    res = sorted((q.get(timeout=180) for _ in range(world)), key=lambda t: t[0])
-    for p in ps:
-        p.join(60)
-        assert p.exitcode == 0
-    for rank, errs in res:
-        assert "leaves empty slabs" in errs[0], (rank, errs)
-        assert "at least one plane" in errs[1], (rank, errs)
+def test_single_rank_and_errors(native):
+    from nm03_capstone_project_amd.parallel.volume_slabs import run_volume_slabs
+    band, seeds = _volumes()["snake"]
+    r = run_volume_slabs(band=band, seeds=seeds, connectivity=6, dilation=3, backend="cpu")
+    ref = native.golden_region_grow3d(band, seeds, 6)
+    assert np.array_equal(r["region"], ref) and r["rounds"] == 1
+    with pytest.raises(ValueError):
+        run_volume_slabs(backend="cpu")
+    with pytest.raises(RuntimeError, match="a rank failed"):  # stderr: "... leaves empty slabs"
+        native.golden_slabs_selftest(4, band[:3], seeds, 6, 3)
