@@ -36,6 +36,7 @@ struct Topology {
   std::vector<int> nodes;                    // NUMA node ids with allowed CPUs, ascending
   std::vector<std::vector<int>> node_cpus;   // per entry of `nodes`: allowed CPUs, ascending
   std::vector<long> core_of;                 // cpu -> physical core key (package << 20 | core id); -1 unknown
+  std::vector<long> l3_of;                   // cpu -> L3 domain key (package << 20 | cache id); -1 unknown
   int node_index(int node) const;            // index into `nodes`, -1 if absent
 };
 // `allowed` empty: the calling process's affinity mask.
@@ -71,8 +72,14 @@ class Placement {
   void bind_this_thread() const;
   // Pins pool worker `i` of `n`. NM03_PIN=set (default): the whole CPU set, like bind_this_thread;
   // NM03_PIN=core: one physical core of the set per worker (cores spread evenly over the set), so
-  // a worker never migrates and its staging buffers stay in that core's L2.
+  // a worker never migrates and its staging buffers stay in that core's L2;
+  // NM03_PIN=l3: worker i floats within L3 domain (CCD) i mod groups() of the set.
   void bind_worker(int i, int n) const;
+  // NM03_PIN=l3: the L3 domains (CCDs) of the set; work keyed to a domain (engine.cpp: slice
+  // i's load and export run on domain i mod groups()) keeps a file's page-cache lines in one L3
+  // across passes instead of bouncing them between CCDs. 1 otherwise.
+  int groups() const { return l3_groups_.empty() ? 1 : (int)l3_groups_.size(); }
+  int worker_group(int i) const { return l3_groups_.empty() ? 0 : i % (int)l3_groups_.size(); }
   // Runs `f` with the calling thread temporarily pinned (first-touch / pinned allocations land on
   // the node), restoring the previous affinity afterwards.
   template <class F>
@@ -88,7 +95,8 @@ class Placement {
  private:
   int node_ = -1;
   std::vector<int> cpus_;
-  std::vector<std::vector<int>> cores_;  // cpus_ grouped by physical core (NM03_PIN=core)
+  std::vector<std::vector<int>> cores_;      // cpus_ grouped by physical core (NM03_PIN=core)
+  std::vector<std::vector<int>> l3_groups_;  // cpus_ grouped by L3 domain (NM03_PIN=l3)
 };
 
 }  // namespace nm03::numa

@@ -32,6 +32,7 @@ class ThreadPool {
     for (int i = 0; i < n; ++i)
       workers_.emplace_back([this, on_start, i] {
         pthread_setname_np(pthread_self(), "nm03-pool");  // per-thread CPU accounting (bench.py)
+        worker_index_ref() = i;
         if (on_start) on_start(i);
         loop();
       });
@@ -66,12 +67,18 @@ class ThreadPool {
       cv_.notify_all();
   }
   int size() const { return (int)workers_.size(); }
+  // Index of the calling pool worker thread (-1 outside any pool).
+  static int current_worker() { return worker_index_ref(); }
 
  private:
   struct Task {
     uint64_t prio, seq;
     std::function<void()> f;
   };
+  static int& worker_index_ref() {
+    static thread_local int idx = -1;
+    return idx;
+  }
   static bool later(const Task& a, const Task& b) { return a.prio != b.prio ? a.prio > b.prio : a.seq > b.seq; }
   void push(std::function<void()> f, uint64_t prio) {
     q_.push_back(Task{prio, seq_++, std::move(f)});
@@ -144,6 +151,46 @@ class TaskGroup {
         },
         prio);
   }
+  // for_each with affinity: item i belongs to group group_of(i) ∈ [0, groups); a runner on a pool
+  // worker of group worker_group(ThreadPool::current_worker()) takes its own group's items first
+  // (in index order), then steals from the other groups — so work keyed to a group runs on that
+  // group's CPUs whenever they keep up, and no runner idles while items remain.
+  void for_each_grouped(size_t n, std::function<void(size_t)> fn, int groups, const std::function<int(size_t)>& group_of,
+                        std::function<int(int)> worker_group, uint64_t prio = 0,
+                        std::atomic<int64_t>* cpu_ns = nullptr) {
+    if (n == 0) return;
+    if (groups <= 1) {
+      for_each(n, std::move(fn), prio, cpu_ns);
+      return;
+    }
+    auto st = std::make_shared<Grouped>();
+    st->lists.resize((size_t)groups);
+    for (size_t i = 0; i < n; ++i) st->lists[(size_t)(group_of(i) % groups)].push_back(i);
+    st->next = std::make_unique<std::atomic<size_t>[]>((size_t)groups);
+    for (int g = 0; g < groups; ++g) st->next[g].store(0, std::memory_order_relaxed);
+    st->fn = std::move(fn);
+    st->worker_group = std::move(worker_group);
+    const int runners = (int)std::min<size_t>(n, (size_t)pool_.size());
+    {
+      std::lock_guard<std::mutex> g(m_);
+      pending_ += (size_t)runners;
+    }
+    pool_.submit_n(
+        runners,
+        [this, st, cpu_ns, groups] {
+          const int64_t c0 = cpu_ns ? thread_cpu_now_ns() : 0;
+          const int w = ThreadPool::current_worker();
+          const int home = w >= 0 ? st->worker_group(w) % groups : 0;
+          for (int k = 0; k < groups; ++k) {
+            const size_t g = (size_t)((home + k) % groups);
+            const auto& list = st->lists[g];
+            for (size_t j; (j = st->next[g].fetch_add(1)) < list.size();) st->fn(list[j]);
+          }
+          if (cpu_ns) cpu_ns->fetch_add(thread_cpu_now_ns() - c0, std::memory_order_relaxed);
+          done(1);
+        },
+        prio);
+  }
   void wait() {
     std::unique_lock<std::mutex> g(m_);
     cv_.wait(g, [this] { return pending_ == 0; });
@@ -155,6 +202,12 @@ class TaskGroup {
     std::atomic<size_t> next{0};
     size_t n = 0;
     std::function<void(size_t)> fn;
+  };
+  struct Grouped {
+    std::vector<std::vector<size_t>> lists;
+    std::unique_ptr<std::atomic<size_t>[]> next;
+    std::function<void(size_t)> fn;
+    std::function<int(int)> worker_group;
   };
   void done(size_t k) {
     std::lock_guard<std::mutex> g(m_);

@@ -1019,10 +1019,22 @@ struct Engine::Impl {
     }
     std::atomic<int64_t> load_ns{0}, bytes_in{0}, write_ns{0}, bytes_out{0}, load_cpu_ns{0}, write_cpu_ns{0};
     std::string upload_error;
+    // NM03_PIN=l3: slice (first + i)'s load and export run on L3 domain (first + i) mod G, so the
+    // same files' page-cache lines meet the same CCD every pass (numa.h Placement::groups()).
+    const int G = place.groups();
+    auto worker_group = [this](int w) { return place.worker_group(w); };
+    auto for_items = [&](TaskGroup& tg, size_t n, const std::function<size_t(size_t)>& item_of,
+                         std::function<void(size_t)> fn, uint64_t pr, std::atomic<int64_t>* cpu) {
+      if (G > 1)
+        tg.for_each_grouped(n, std::move(fn), G, [&](size_t k) { return (int)(item_of(k) % (size_t)G); }, worker_group,
+                            pr, cpu);
+      else
+        tg.for_each(n, std::move(fn), pr, cpu);
+    };
     {
       TaskGroup tg(*pool);
-      tg.for_each(
-          count,
+      for_items(
+          tg, count, [&](size_t i) { return first + i; },
           [&](size_t i) {
             if (on_start) on_start(first + i);
             if (cfg.resume && outputs_exist(items[first + i])) {
@@ -1114,8 +1126,8 @@ struct Engine::Impl {
         for (size_t c = 0; c < order.size(); ++c) order[c] = (int)c;
       }
       TaskGroup tg(*pool);
-      tg.for_each(
-          s.live.size(),
+      for_items(
+          tg, s.live.size(), [&](size_t oc) { return first + (size_t)s.live[(size_t)order[oc]]; },
           [&](size_t oc) {
             const size_t c = (size_t)order[oc];
             const size_t item = first + s.live[c];

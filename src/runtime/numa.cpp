@@ -133,10 +133,16 @@ Topology read_topology(const std::string& sysfs, const std::vector<int>& allowed
   }
   const int maxc = ok.empty() ? 0 : *ok.rbegin() + 1;
   t.core_of.assign((size_t)maxc, -1);
+  t.l3_of.assign((size_t)maxc, -1);
   for (int c : allowed) {
-    const std::string base = sysfs + "/devices/system/cpu/cpu" + std::to_string(c) + "/topology/";
-    const std::string core = read_line(base + "core_id"), pkg = read_line(base + "physical_package_id");
-    if (!core.empty()) t.core_of[(size_t)c] = ((long)std::max(0, std::atoi(pkg.c_str())) << 20) | std::atol(core.c_str());
+    const std::string cpu = sysfs + "/devices/system/cpu/cpu" + std::to_string(c);
+    const std::string core = read_line(cpu + "/topology/core_id"), pkg = read_line(cpu + "/topology/physical_package_id");
+    const long pk = (long)std::max(0, std::atoi(pkg.c_str())) << 20;
+    if (!core.empty()) t.core_of[(size_t)c] = pk | std::atol(core.c_str());
+    if (read_line(cpu + "/cache/index3/level") == "3") {
+      const std::string id = read_line(cpu + "/cache/index3/id");
+      if (!id.empty()) t.l3_of[(size_t)c] = pk | std::atol(id.c_str());
+    }
   }
   return t;
 }
@@ -233,6 +239,21 @@ Placement::Placement(int device, const std::vector<int>& cpus) {
     cpus_ = allowed_cpus();
   }
   if (per_core && !cpus_.empty()) cores_ = cores_of(read_topology("/sys", cpus_), cpus_);
+  if (pin && std::string(pin) == "l3" && !cpus_.empty()) {
+    const Topology t = read_topology("/sys", cpus_);
+    std::map<long, size_t> at;
+    for (int c : cpus_) {
+      const long key = (size_t)c < t.l3_of.size() ? t.l3_of[(size_t)c] : -1;
+      auto it = at.find(key);
+      if (it == at.end()) {
+        at.emplace(key, l3_groups_.size());
+        l3_groups_.push_back({c});
+      } else {
+        l3_groups_[it->second].push_back(c);
+      }
+    }
+    if (l3_groups_.size() < 2) l3_groups_.clear();  // one domain: nothing to key work to
+  }
 }
 
 static void bind_cpus(const std::vector<int>& cpus) {
@@ -244,6 +265,10 @@ static void bind_cpus(const std::vector<int>& cpus) {
 
 void Placement::bind_worker(int i, int n) const {
   if (cpus_.empty()) return;
+  if (!l3_groups_.empty()) {
+    bind_cpus(l3_groups_[(size_t)worker_group(i)]);
+    return;
+  }
   if (cores_.empty() || n < 1) {
     bind_this_thread();
     return;
@@ -261,7 +286,7 @@ void Placement::bind_this_thread() const {
 std::string Placement::describe() const {
   if (cpus_.empty()) return "numa: off";
   return "numa: node " + std::to_string(node_) + " (" + std::to_string(cpus_.size()) + " cpus: " +
-         format_cpulist(cpus_) + ")";
+         format_cpulist(cpus_) + (l3_groups_.empty() ? "" : ", " + std::to_string(l3_groups_.size()) + " L3 groups") + ")";
 }
 
 }  // namespace nm03::numa

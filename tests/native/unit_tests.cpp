@@ -430,6 +430,31 @@ TEST(thread_pool_for_each_exactly_once) {
   }
 }
 
+TEST(thread_pool_for_each_grouped_exactly_once_and_affine) {
+  nm03::ThreadPool pool(6);
+  for (int groups : {1, 3, 4}) {
+    for (size_t n : {0u, 1u, 7u, 500u}) {
+      std::vector<std::atomic<int>> hits(n);
+      std::atomic<int> home{0}, away{0};
+      nm03::TaskGroup tg(pool);
+      tg.for_each_grouped(
+          n,
+          [&](size_t i) {
+            hits[i].fetch_add(1);
+            const int w = nm03::ThreadPool::current_worker();
+            ((int)(i % (size_t)groups) == w % groups ? home : away).fetch_add(1);
+          },
+          groups, [&](size_t i) { return (int)(i % (size_t)groups); }, [](int w) { return w; }, 3);
+      tg.wait();
+      bool ok = true;
+      for (auto& h : hits) ok &= h.load() == 1;
+      CHECK(ok);
+      CHECK(home.load() + away.load() == (int)n);
+    }
+  }
+  CHECK(nm03::ThreadPool::current_worker() == -1);
+}
+
 TEST(thread_pool_priorities_order_a_single_worker) {
   nm03::ThreadPool pool(1);
   std::vector<int> order;
