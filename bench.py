@@ -398,13 +398,17 @@ def run_rank(args):
                                        for k in ("usage_usec", "throttled_usec") if k in cg1},
         }
 
-    def single_pass(out_root, passes, capped):
+    def single_pass(out_root, passes, capped, ranks_like=0):
         """BASELINE config 3 as written, as a latency: ONE cohort sharded over the ranks, one engine
         pass per rank, nothing else in flight; each pass bracketed by barriers, max over ranks.
         `capped`: the shard cut into ⌈shard / streams⌉-slice batches, so its loads, uploads,
         kernels and writes overlap across the slots (a 58-slice shard at 8 ranks is otherwise one
-        batch run stage after stage). Returns (median ms, min ms)."""
+        batch run stage after stage). `ranks_like` > 0 (one rank only): time the shard rank 0 would
+        get with that many ranks (465 / 8 = 58 slices) — the 8-GPU strong-scaling latency of one
+        GPU's share. Returns (median ms, min ms)."""
         mine, _ = shard("strong", out_root)
+        if ranks_like > 0:
+            mine = mine[:len(mine) // ranks_like]
         work = n.WorkList(mine)
         cap = -(-len(mine) // args.streams) if capped else 0
         times = []
@@ -443,6 +447,12 @@ def run_rank(args):
         sp = {"single_pass_ms": med, "single_pass_min_ms": best, "single_pass_batch_cap": "ceil(shard/streams)",
               "single_pass_uncapped_ms": med_u, "single_pass_uncapped_min_ms": best_u,
               "single_pass_passes": args.single_passes}
+        if world == 1:
+            # One GPU's share of the 8-GPU config-3 run (58 of 465 slices), capped vs one batch.
+            m8, b8 = single_pass(sp_root, args.single_passes, capped=True, ranks_like=8)
+            m8u, b8u = single_pass(sp_root, args.single_passes, capped=False, ranks_like=8)
+            sp.update({"single_pass_shard8_ms": m8, "single_pass_shard8_min_ms": b8,
+                       "single_pass_shard8_uncapped_ms": m8u, "single_pass_shard8_uncapped_min_ms": b8u})
 
     if is_root:
         value = primary["value"]
