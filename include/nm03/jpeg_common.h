@@ -125,13 +125,14 @@ NM03_HD int32_t fdct_mul(int32_t a, int32_t b) {
 
 // LL&M integer forward DCT, libjpeg jfdctint "islow" arithmetic.  `d` holds 64 level-shifted
 // samples (x-128) in natural order; on return it holds coefficients scaled up by 8.
-NM03_HD void fdct_islow(int32_t* d) {
-  constexpr int CB = 13, P1 = 2;
-  constexpr int32_t F0_298 = 2446, F0_390 = 3196, F0_541 = 4433, F0_765 = 6270, F0_899 = 7373,
-                    F1_175 = 9633, F1_501 = 12299, F1_847 = 15137, F1_961 = 16069,
-                    F2_053 = 16819, F2_562 = 20995, F3_072 = 25172;
+// libjpeg's jfdctint.c islow forward DCT, in two passes (rows, then columns); fdct_islow = both.
 #define NM03_DESCALE(x, n) (((x) + (1 << ((n)-1))) >> (n))
-  // Pass 1: rows.
+constexpr int kFdctCB = 13, kFdctP1 = 2;
+constexpr int32_t kF0_298 = 2446, kF0_390 = 3196, kF0_541 = 4433, kF0_765 = 6270, kF0_899 = 7373, kF1_175 = 9633,
+                  kF1_501 = 12299, kF1_847 = 15137, kF1_961 = 16069, kF2_053 = 16819, kF2_562 = 20995, kF3_072 = 25172;
+
+NM03_HD void fdct_islow_pass1(int32_t* d) {
+  constexpr int CB = kFdctCB, P1 = kFdctP1;
   for (int r = 0; r < 8; ++r) {
     int32_t* p = d + r * 8;
     int32_t t0 = p[0] + p[7], t7 = p[0] - p[7];
@@ -141,20 +142,20 @@ NM03_HD void fdct_islow(int32_t* d) {
     int32_t t10 = t0 + t3, t13 = t0 - t3, t11 = t1 + t2, t12 = t1 - t2;
     p[0] = (t10 + t11) * (1 << P1);
     p[4] = (t10 - t11) * (1 << P1);
-    int32_t z1 = fdct_mul(t12 + t13, F0_541);
-    p[2] = NM03_DESCALE(z1 + fdct_mul(t13, F0_765), CB - P1);
-    p[6] = NM03_DESCALE(z1 + fdct_mul(t12, -F1_847), CB - P1);
+    int32_t z1 = fdct_mul(t12 + t13, kF0_541);
+    p[2] = NM03_DESCALE(z1 + fdct_mul(t13, kF0_765), CB - P1);
+    p[6] = NM03_DESCALE(z1 + fdct_mul(t12, -kF1_847), CB - P1);
     z1 = t4 + t7;
     int32_t z2 = t5 + t6, z3 = t4 + t6, z4 = t5 + t7;
-    int32_t z5 = fdct_mul(z3 + z4, F1_175);
-    t4 = fdct_mul(t4, F0_298);
-    t5 = fdct_mul(t5, F2_053);
-    t6 = fdct_mul(t6, F3_072);
-    t7 = fdct_mul(t7, F1_501);
-    z1 = fdct_mul(z1, -F0_899);
-    z2 = fdct_mul(z2, -F2_562);
-    z3 = fdct_mul(z3, -F1_961);
-    z4 = fdct_mul(z4, -F0_390);
+    int32_t z5 = fdct_mul(z3 + z4, kF1_175);
+    t4 = fdct_mul(t4, kF0_298);
+    t5 = fdct_mul(t5, kF2_053);
+    t6 = fdct_mul(t6, kF3_072);
+    t7 = fdct_mul(t7, kF1_501);
+    z1 = fdct_mul(z1, -kF0_899);
+    z2 = fdct_mul(z2, -kF2_562);
+    z3 = fdct_mul(z3, -kF1_961);
+    z4 = fdct_mul(z4, -kF0_390);
     z3 += z5;
     z4 += z5;
     p[7] = NM03_DESCALE(t4 + z1 + z3, CB - P1);
@@ -162,7 +163,10 @@ NM03_HD void fdct_islow(int32_t* d) {
     p[3] = NM03_DESCALE(t6 + z2 + z3, CB - P1);
     p[1] = NM03_DESCALE(t7 + z1 + z4, CB - P1);
   }
-  // Pass 2: columns.
+}
+
+NM03_HD void fdct_islow_pass2(int32_t* d) {
+  constexpr int CB = kFdctCB, P1 = kFdctP1;
   for (int c = 0; c < 8; ++c) {
     int32_t* p = d + c;
     int32_t t0 = p[0] + p[56], t7 = p[0] - p[56];
@@ -172,20 +176,20 @@ NM03_HD void fdct_islow(int32_t* d) {
     int32_t t10 = t0 + t3, t13 = t0 - t3, t11 = t1 + t2, t12 = t1 - t2;
     p[0] = NM03_DESCALE(t10 + t11, P1);
     p[32] = NM03_DESCALE(t10 - t11, P1);
-    int32_t z1 = fdct_mul(t12 + t13, F0_541);
-    p[16] = NM03_DESCALE(z1 + fdct_mul(t13, F0_765), CB + P1);
-    p[48] = NM03_DESCALE(z1 + fdct_mul(t12, -F1_847), CB + P1);
+    int32_t z1 = fdct_mul(t12 + t13, kF0_541);
+    p[16] = NM03_DESCALE(z1 + fdct_mul(t13, kF0_765), CB + P1);
+    p[48] = NM03_DESCALE(z1 + fdct_mul(t12, -kF1_847), CB + P1);
     z1 = t4 + t7;
     int32_t z2 = t5 + t6, z3 = t4 + t6, z4 = t5 + t7;
-    int32_t z5 = fdct_mul(z3 + z4, F1_175);
-    t4 = fdct_mul(t4, F0_298);
-    t5 = fdct_mul(t5, F2_053);
-    t6 = fdct_mul(t6, F3_072);
-    t7 = fdct_mul(t7, F1_501);
-    z1 = fdct_mul(z1, -F0_899);
-    z2 = fdct_mul(z2, -F2_562);
-    z3 = fdct_mul(z3, -F1_961);
-    z4 = fdct_mul(z4, -F0_390);
+    int32_t z5 = fdct_mul(z3 + z4, kF1_175);
+    t4 = fdct_mul(t4, kF0_298);
+    t5 = fdct_mul(t5, kF2_053);
+    t6 = fdct_mul(t6, kF3_072);
+    t7 = fdct_mul(t7, kF1_501);
+    z1 = fdct_mul(z1, -kF0_899);
+    z2 = fdct_mul(z2, -kF2_562);
+    z3 = fdct_mul(z3, -kF1_961);
+    z4 = fdct_mul(z4, -kF0_390);
     z3 += z5;
     z4 += z5;
     p[56] = NM03_DESCALE(t4 + z1 + z3, CB + P1);
@@ -193,7 +197,12 @@ NM03_HD void fdct_islow(int32_t* d) {
     p[24] = NM03_DESCALE(t6 + z2 + z3, CB + P1);
     p[8] = NM03_DESCALE(t7 + z1 + z4, CB + P1);
   }
+}
 #undef NM03_DESCALE
+
+NM03_HD void fdct_islow(int32_t* d) {
+  fdct_islow_pass1(d);
+  fdct_islow_pass2(d);
 }
 
 // Rounding division by the islow divisor (8·Q), sign-symmetric (libjpeg forward_DCT).

@@ -297,9 +297,9 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(kOcc)))
     if (dbg == 6) {  // profiling variant: no render
 #pragma unroll
       for (int i = 0; i < 64; ++i) blk[i] = (i * 7 + bx + by) & 255;
-    } else if (lstaged) {
+    } else if (lstaged) {  // d.render ≥ 0: the fit is exactly 2× (render_is_exact_2x)
       const int wpr = rd.wpr;
-      render_labels_2x(rd, [&](int y, int k, uint64_t& lab, uint64_t& brd) {
+      render_labels_exact2x(rd, [&](int y, int k, uint64_t& lab, uint64_t& brd) {
         const int i = (y - ys0) * wpr + k;
         lab = slab[i];
         brd = slab[pcols + i];

@@ -152,6 +152,29 @@ __device__ __forceinline__ void render_labels_2x(const RenderDesc& d, Words&& wo
   }
 }
 
+// render_labels_2x for a fit known to be exactly 2× (render_is_exact_2x: origin 0, scale 1/2):
+// canvas (8bx + c, 8by + r) samples source (4bx + c/2, 4by + r/2), so the block is 4 × 4 cells of
+// 2 × 2 equal pixels, one nibble of one word per source row — 16 bit tests instead of 64 (the
+// generic form evaluates every pixel's source coordinate). Same values as render_labels_2x.
+template <class Words>
+__device__ __forceinline__ void render_labels_exact2x(const RenderDesc& d, Words&& words, int bx, int by, int32_t* px) {
+  const int sh = (4 * bx) & 63;
+#pragma unroll
+  for (int r2 = 0; r2 < 4; ++r2) {
+    uint64_t lab, brd;
+    words(4 * by + r2, (4 * bx) >> 6, lab, brd);
+    const uint32_t nl = (uint32_t)(lab >> sh), nb = (uint32_t)(brd >> sh);
+#pragma unroll
+    for (int c2 = 0; c2 < 4; ++c2) {
+      const int32_t v = ((nb >> c2) & 1u) ? (int32_t)d.border_value : (((nl >> c2) & 1u) ? (int32_t)d.fill : 0);
+      px[(2 * r2) * 8 + 2 * c2] = v;
+      px[(2 * r2) * 8 + 2 * c2 + 1] = v;
+      px[(2 * r2 + 1) * 8 + 2 * c2] = v;
+      px[(2 * r2 + 1) * 8 + 2 * c2 + 1] = v;
+    }
+  }
+}
+
 // Fused 2× render of the 8×8 canvas block (bx, by) into px[64] (row-major), for a RenderDesc
 // with render_is_exact_2x(): the block's source footprint is a 6×6 patch (gray) or 4×4 (labels).
 __device__ __forceinline__ void render_block_2x(const RenderDesc& d, const uint16_t* raw, const float* f32,
