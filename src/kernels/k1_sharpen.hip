@@ -97,6 +97,11 @@ __global__ __launch_bounds__(256) void sharpen_band_kernel(const uint16_t* __res
       const int xs = x0 - 4 * RA + 4 * g;
       v[t] = *reinterpret_cast<const uint2*>(row + clampi(xs, 0, W - 4));
     }
+    // Store order rotated per 8-lane group: store j of lane l writes key q = (j + l/8) mod 4. In
+    // natural order the 32 lanes of a ds_write_b32 group write addresses 4 dwords apart (8 banks,
+    // 4-way conflicts: 2.49 conflict cycles per LDS instruction, profiles/r2/pmc); rotated, lanes
+    // 8k..8k+7 take banks ≡ k (mod 4) and the group covers all 32 banks.
+    const int rot = (threadIdx.x >> 3) & 3;
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
       const int i = threadIdx.x + 256 * t;
@@ -107,9 +112,11 @@ __global__ __launch_bounds__(256) void sharpen_band_kernel(const uint16_t* __res
       if (xs < 0) px[1] = px[2] = px[3] = px[0];
       if (xs >= W) px[0] = px[1] = px[2] = px[3];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
+      for (int j = 0; j < 4; ++j) {
+        const int q = (j + rot) & 3;
+        const uint16_t key = q == 0 ? px[0] : q == 1 ? px[1] : q == 2 ? px[2] : px[3];  // selects, no scratch
         const int c = 4 * g + q - (4 * RA - R);
-        if (c >= 0 && c < CW) C[r * CS + c] = norm_clip_key(px[q], d.type, nc);
+        if (c >= 0 && c < CW) C[r * CS + c] = norm_clip_key(key, d.type, nc);
       }
     }
   } else {

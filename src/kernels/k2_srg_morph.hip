@@ -42,7 +42,7 @@ __global__ __launch_bounds__(kSrgThreads) void srg_morph_kernel(const uint64_t* 
                                                         const SeedXY* __restrict__ seeds, PipeConsts pc,
                                                         SrgOutputs out, int plane_words) {
   extern __shared__ __attribute__((aligned(16))) uint64_t lds_planes[];
-  __shared__ int flag;
+  __shared__ int flag[2];  // srg_fixpoint's two alternating change words
   uint64_t* const smem = kGlobal ? out.scratch + (size_t)blockIdx.x * 4 * plane_words : lds_planes;
   const SliceDesc d = descs[blockIdx.x];
   const int W = d.w, H = d.h, n = d.wpr, hb = (H + 63) >> 6;
@@ -72,7 +72,7 @@ __global__ __launch_bounds__(kSrgThreads) void srg_morph_kernel(const uint64_t* 
   transpose_plane(M, H, n, Mt, W, false, nullptr, sn, st);
   __syncthreads();
 
-  const int iters = srg_fixpoint(M, Rg, Mt, Rt, W, H, n, pc.connectivity, &flag, sn, st);
+  const int iters = srg_fixpoint(M, Rg, Mt, Rt, W, H, n, pc.connectivity, flag, sn, st);
   // An iteration in which no step changed anything ⇒ Rg is the fixpoint region.
   if (out.iterations && threadIdx.x == 0) out.iterations[blockIdx.x] = iters;
   const size_t off = d.mask_off;

@@ -137,7 +137,7 @@ __global__ __launch_bounds__(kSrg3dThreads) void srg3d_kernel(const uint64_t* __
                                                               int w, int h, int d, int connectivity, int plane_words,
                                                               uint32_t* ctl, int max_sweeps, uint64_t* scratch) {
   extern __shared__ __attribute__((aligned(16))) uint64_t lds_planes[];
-  __shared__ int flag;
+  __shared__ int flag[2];  // srg_fixpoint's two alternating change words
   uint64_t* const planes = kGlobal ? scratch + (size_t)blockIdx.x * 4 * plane_words : lds_planes;
   int sweep = 0;
   for (; sweep < max_sweeps; ++sweep) {
@@ -149,7 +149,7 @@ __global__ __launch_bounds__(kSrg3dThreads) void srg3d_kernel(const uint64_t* __
       __hip_atomic_store(&ctl[kCtlChanged + (sweep + 1) % 3], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     bool changed = false;
     for (int p = blockIdx.x; p < nplanes; p += gridDim.x)
-      changed |= sweep_plane(band, region, w, h, d, axis, p, connectivity, plane_words, planes, &flag);
+      changed |= sweep_plane(band, region, w, h, d, axis, p, connectivity, plane_words, planes, flag);
     if (__syncthreads_or(changed) && threadIdx.x == 0) atomicOr(&ctl[kCtlChanged + sweep % 3], 1u);
     if (!grid_barrier(ctl, gridDim.x)) return;
     const uint32_t c = __hip_atomic_load(&ctl[kCtlChanged + sweep % 3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

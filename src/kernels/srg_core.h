@@ -128,22 +128,26 @@ __device__ inline void store_plane(const uint64_t* src, uint64_t* dst, int h, in
 // scratch. All planes in LDS; M/Rg rows are sn words apart, Mt/Rt rows st words apart (0 = dense;
 // odd strides keep the thread-per-row sweeps and transposes free of LDS bank conflicts). `flag` is
 // an LDS int. Returns the iteration count.
+// `flagp` points at TWO LDS ints: iteration k reports changes in flag[k & 1] and clears
+// flag[(k + 1) & 1] after its first barrier (every thread read that word at the end of iteration
+// k − 1 before reaching it), so the end of an iteration needs one barrier, not three.
 __device__ inline int srg_fixpoint(uint64_t* M, uint64_t* Rg, const uint64_t* Mt, uint64_t* Rt, int W, int H, int n,
                             int connectivity, int* flagp, int sn = 0, int st = 0) {
-  int& flag = *flagp;
   const int hb = (H + 63) >> 6, words = H * n;
   if (sn == 0) sn = n;
   if (st == 0) st = hb;
   int iters = 0;
   const int max_iters = W * H + 4;  // monotone growth ⇒ always terminates earlier
-  if (threadIdx.x == 0) flag = 0;
+  if (threadIdx.x == 0) flagp[0] = flagp[1] = 0;
   __syncthreads();
   for (;;) {
+    int& flag = flagp[iters & 1];
     ++iters;
     bool ch = false;
     for (int y = threadIdx.x; y < H; y += blockDim.x) ch |= fill_row(Rg + y * sn, M + y * sn, n);
     if (ch) flag = 1;
     __syncthreads();
+    if (threadIdx.x == 0) flagp[iters & 1] = 0;  // the next iteration's word
     if (connectivity == 8) {
       // Diagonal seeding from a snapshot of the horizontally dilated rows (Rt as scratch).
       for (int y = threadIdx.x; y < H; y += blockDim.x) morph_row_h(Rg + y * sn, Rt + y * sn, n, W, 1, true);
@@ -169,11 +173,7 @@ __device__ inline int srg_fixpoint(uint64_t* M, uint64_t* Rg, const uint64_t* Mt
     __syncthreads();
     transpose_plane(Rt, W, hb, Rg, H, true, &flag, st, sn);
     __syncthreads();
-    const int f = flag;
-    __syncthreads();
-    if (threadIdx.x == 0) flag = 0;
-    __syncthreads();
-    if (f == 0 || iters >= max_iters) break;
+    if (flag == 0 || iters >= max_iters) break;
   }
   return iters;
 }
