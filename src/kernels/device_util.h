@@ -66,24 +66,58 @@ __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t* s
   return res;
 }
 
-// 64×64 bit-matrix transpose across a wave: lane l holds row l (bit c = column c) and receives
-// column l. Six butterfly stages of off-diagonal block swaps.
-__device__ __forceinline__ uint64_t wave_transpose64(uint64_t x, int lane) {
-  const uint64_t masks[6] = {0x00000000FFFFFFFFull, 0x0000FFFF0000FFFFull, 0x00FF00FF00FF00FFull,
-                             0x0F0F0F0F0F0F0F0Full, 0x3333333333333333ull, 0x5555555555555555ull};
-#pragma unroll
-  for (int s = 0; s < 6; ++s) {
-    const int j = 32 >> s;
-    const uint64_t m = masks[s];
-    const uint64_t other = __shfl_xor(x, j, 64);
-    if ((lane & j) == 0) {
-      const uint64_t t = ((x >> j) ^ other) & m;
-      x ^= t << j;
-    } else {
-      const uint64_t t = ((other >> j) ^ x) & m;
-      x ^= t;
-    }
+// x of lane (lane ^ J), without the LDS crossbar: v_permlane32_swap / v_permlane16_swap (gfx950)
+// for J = 32 / 16, DPP row rotates for J = 8 / 4 (row_ror:N = from lane − N within a 16-lane
+// row) and DPP quad permutes for J = 2 / 1. Each is 1–3 VALU ops; a ds_bpermute_b32 round trip
+// costs ~100 cycles, and the bit transposes below chain six of them.
+template <int J>
+__device__ __forceinline__ uint32_t lane_xor(uint32_t x, int lane) {
+  if constexpr (J == 32) {
+    const auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);  // {dst', src'}
+    return (lane & 32) ? r[0] : r[1];
+  } else if constexpr (J == 16) {
+    const auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);
+    return (lane & 16) ? r[0] : r[1];
+  } else if constexpr (J == 8) {
+    return __builtin_amdgcn_update_dpp(0u, x, 0x128, 0xF, 0xF, true);  // row_ror:8
+  } else if constexpr (J == 4) {
+    const uint32_t from_lo = __builtin_amdgcn_update_dpp(0u, x, 0x124, 0xF, 0xF, true);  // row_ror:4  (lane − 4)
+    const uint32_t from_hi = __builtin_amdgcn_update_dpp(0u, x, 0x12C, 0xF, 0xF, true);  // row_ror:12 (lane + 4)
+    return (lane & 4) ? from_lo : from_hi;
+  } else if constexpr (J == 2) {
+    return __builtin_amdgcn_update_dpp(0u, x, 0x4E, 0xF, 0xF, true);  // quad_perm [2,3,0,1]
+  } else {
+    static_assert(J == 1, "lane_xor: J in {1,2,4,8,16,32}");
+    return __builtin_amdgcn_update_dpp(0u, x, 0xB1, 0xF, 0xF, true);  // quad_perm [1,0,3,2]
   }
+}
+
+template <int J>
+__device__ __forceinline__ void transpose_stage(uint64_t& x, int lane, uint64_t m) {
+  const uint64_t other = ((uint64_t)lane_xor<J>((uint32_t)(x >> 32), lane) << 32) | lane_xor<J>((uint32_t)x, lane);
+  if ((lane & J) == 0) {
+    const uint64_t t = ((x >> J) ^ other) & m;
+    x ^= t << J;
+  } else {
+    const uint64_t t = ((other >> J) ^ x) & m;
+    x ^= t;
+  }
+}
+
+// 64×64 bit-matrix transpose across a wave: lane l holds row l (bit c = column c) and receives
+// column l. Six butterfly stages of off-diagonal block swaps; the 32-block stage (lanes < 32 take
+// the partner's low half into their high half and vice versa) is exactly one v_permlane32_swap of
+// (lo, hi). All stages stay in VALU (the r2 form was 12 dependent ds_bpermute_b32).
+__device__ __forceinline__ uint64_t wave_transpose64(uint64_t x, int lane) {
+  {
+    const auto r = __builtin_amdgcn_permlane32_swap((uint32_t)x, (uint32_t)(x >> 32), false, false);
+    x = ((uint64_t)r[1] << 32) | r[0];
+  }
+  transpose_stage<16>(x, lane, 0x0000FFFF0000FFFFull);
+  transpose_stage<8>(x, lane, 0x00FF00FF00FF00FFull);
+  transpose_stage<4>(x, lane, 0x0F0F0F0F0F0F0F0Full);
+  transpose_stage<2>(x, lane, 0x3333333333333333ull);
+  transpose_stage<1>(x, lane, 0x5555555555555555ull);
   return x;
 }
 

@@ -27,10 +27,18 @@ namespace nm03::gpu {
 constexpr int kMaxR = 7;
 
 // Two adjacent f32 in one register pair: the stencil passes run on packed f32 (v_pk_mul_f32 /
-// v_pk_add_f32, per-lane IEEE rounding, so results are those of the scalar ops). The LDS row
-// stride is odd, so a pair is read with ds_read2_b32 (4-byte alignment) rather than a b64 load.
+// v_pk_add_f32, per-lane IEEE rounding, so results are those of the scalar ops).
+//
+// LDS layout: row stride CS ≡ 2 (mod 4) dwords, so every even column pair is 8-byte aligned and
+// moves with one ds_read_b64 / ds_write_b64. A b64 access is served 16 lanes at a time; 16 lanes
+// on consecutive pairs of one row cover all 32 banks (vertical pass), and 16 lanes on 16
+// consecutive rows hit banks (CS·r + {0,1}) mod 32 — distinct for r < 16 because CS/2 is odd
+// (horizontal pass). The r2 layout (odd stride, pairs as ds_read2_b32 at stride 2 across lanes)
+// ran at 2.49 bank-conflict cycles per LDS instruction (profiles/r2/pmc).
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ f32x2 lds_pair(const float* p) { return f32x2{p[0], p[1]}; }
+__device__ __forceinline__ f32x2 lds_pair_a(const float* p) { return *reinterpret_cast<const f32x2*>(p); }
+__device__ __forceinline__ void lds_store_pair(float* p, f32x2 v) { *reinterpret_cast<f32x2*>(p) = v; }
 static_assert(kShpTileW == 64 && kShpTileH == 64, "sharpen tile is 64x64");
 
 template <int R>
@@ -41,12 +49,16 @@ __global__ __launch_bounds__(256) void sharpen_band_kernel(const uint16_t* __res
                                                            SliceStats* stats, const uint32_t* __restrict__ tile_mm) {
   constexpr int TW = kShpTileW, TH = kShpTileH;
   constexpr int CW = TW + 2 * R, CH = TH + 2 * R;
-  constexpr int CS = CW | 1;          // odd LDS row stride
-  constexpr int RA = (R + 3) / 4;     // 4-key groups of halo on each side
-  constexpr int G = TW / 4 + 2 * RA;  // groups per input row
-  constexpr int RB = 16;              // rows per vertical-pass task
-  __shared__ float C[CH * CS];
-  __shared__ float T[TH * CS];
+  constexpr int CS = CW % 4 == 0 ? CW + 2 : CW;  // LDS row stride ≡ 2 (mod 4)
+  constexpr int RA = (R + 3) / 4;                 // 4-key groups of halo on each side
+  constexpr int G = TW / 4 + 2 * RA;              // groups per input row
+  constexpr int OFS = 4 * RA - R;                 // window column of tile column 0
+  // Vertical pass: 7 row blocks of RB rows (the last one starts at TH - RB and recomputes 6 rows),
+  // so (32 + R)·7 tasks keep all 256 threads busy for R ≤ 4 (16-row blocks left 112 idle).
+  constexpr int RB = 10, NB = (TH + RB - 1) / RB;
+  static_assert(CS % 4 == 2, "pair alignment");
+  __shared__ __attribute__((aligned(16))) float C[CH * CS];
+  __shared__ __attribute__((aligned(16))) float T[TH * CS];
   const TileDesc t = tiles[blockIdx.x];
   const SliceDesc d = descs[t.slice];
   const int x0 = t.tx * TW, y0 = t.ty * TH;
@@ -84,12 +96,31 @@ __global__ __launch_bounds__(256) void sharpen_band_kernel(const uint16_t* __res
     // loads are issued before any is consumed: every wave of the launch is in this phase at the
     // same time, so a load → use → load chain would expose the memory latency once per task.
     constexpr int NT = (CH * G + 255) / 256;  // tasks per thread
+    // Task i → (row r, group g): the first CH·16 tasks are the 16 interior groups of each row, so a
+    // 16-lane store group stays on one row (with the rotation below: all 32 banks); the 2·RA halo
+    // groups per row follow.
+    auto task_rg = [](int i, int& r, int& g) {
+      if (i < CH * 16) {
+        r = i >> 4;
+        g = (i & 15) + RA;
+      } else {
+        const int k = i - CH * 16;
+        if constexpr (RA > 0) {
+          r = k / (2 * RA);
+          const int hg = k - r * (2 * RA);
+          g = hg < RA ? hg : 16 + hg;
+        } else {
+          r = g = 0;
+        }
+      }
+    };
     uint2 v[NT];
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
       const int i = threadIdx.x + 256 * t;
       if (i >= CH * G) break;
-      const int r = i / G, g = i - r * G;
+      int r, g;
+      task_rg(i, r, g);
       const int y = clampi(y0 - R + r, 0, H - 1);
       const uint16_t* row = src + (size_t)y * W;
       // W % 4 == 0 and xs ≡ x0 (mod 4): a group is wholly inside or wholly outside the image, and
@@ -97,26 +128,37 @@ __global__ __launch_bounds__(256) void sharpen_band_kernel(const uint16_t* __res
       const int xs = x0 - 4 * RA + 4 * g;
       v[t] = *reinterpret_cast<const uint2*>(row + clampi(xs, 0, W - 4));
     }
-    // Store order rotated per 8-lane group: store j of lane l writes key q = (j + l/8) mod 4. In
-    // natural order the 32 lanes of a ds_write_b32 group write addresses 4 dwords apart (8 banks,
-    // 4-way conflicts: 2.49 conflict cycles per LDS instruction, profiles/r2/pmc); rotated, lanes
-    // 8k..8k+7 take banks ≡ k (mod 4) and the group covers all 32 banks.
+    // Store order rotated per 8-lane group so the lanes of one store instruction spread over the
+    // banks: a ds_write_b64 is served 16 lanes at a time, bank (a/4) mod 32; lanes 0–7 write pair
+    // h at dwords 4g + 2h, lanes 8–15 pair 1 − h at 4(g + 8) + 2(1 − h) ≡ the other 16 banks.
     const int rot = (threadIdx.x >> 3) & 3;
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
       const int i = threadIdx.x + 256 * t;
       if (i >= CH * G) break;
-      const int r = i / G, g = i - r * G;
+      int r, g;
+      task_rg(i, r, g);
       const int xs = x0 - 4 * RA + 4 * g;
       uint16_t px[4] = {(uint16_t)v[t].x, (uint16_t)(v[t].x >> 16), (uint16_t)v[t].y, (uint16_t)(v[t].y >> 16)};
       if (xs < 0) px[1] = px[2] = px[3] = px[0];
       if (xs >= W) px[0] = px[1] = px[2] = px[3];
+      if constexpr (OFS % 2 == 0) {
+        // Keys (0,1) and (2,3) land on even window columns: two aligned pair stores.
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int q = (j + rot) & 3;
-        const uint16_t key = q == 0 ? px[0] : q == 1 ? px[1] : q == 2 ? px[2] : px[3];  // selects, no scratch
-        const int c = 4 * g + q - (4 * RA - R);
-        if (c >= 0 && c < CW) C[r * CS + c] = norm_clip_key(key, d.type, nc);
+        for (int j = 0; j < 2; ++j) {
+          const int h = (j + rot) & 1;
+          const int c = 4 * g + 2 * h - OFS;
+          const f32x2 kv{norm_clip_key(h ? px[2] : px[0], d.type, nc), norm_clip_key(h ? px[3] : px[1], d.type, nc)};
+          if (c >= 0 && c < CW) lds_store_pair(C + r * CS + c, kv);
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int q = (j + rot) & 3;
+          const uint16_t key = q == 0 ? px[0] : q == 1 ? px[1] : q == 2 ? px[2] : px[3];  // selects, no scratch
+          const int c = 4 * g + q - OFS;
+          if (c >= 0 && c < CW) C[r * CS + c] = norm_clip_key(key, d.type, nc);
+        }
       }
     }
   } else {
@@ -128,14 +170,15 @@ __global__ __launch_bounds__(256) void sharpen_band_kernel(const uint16_t* __res
   }
   __syncthreads();
 
-  // ---- 2. vertical pass: columns (c, c+1), rows [RB·rb, RB·rb + RB) from a register window of
+  // ---- 2. vertical pass: columns (c, c+1), rows [r0, r0 + RB) from a register window of
   //         column pairs; every tap is one v_pk_mul_f32 + one v_pk_add_f32 for two outputs --------
   constexpr int CP = CW / 2;  // CW = 64 + 2R is even
-  for (int task = threadIdx.x; task < CP * (TH / RB); task += 256) {
+  for (int task = threadIdx.x; task < CP * NB; task += 256) {
     const int rb = task / CP, c = 2 * (task - rb * CP);
+    const int r0 = min(rb * RB, TH - RB);
     f32x2 win[RB + 2 * R];
 #pragma unroll
-    for (int k = 0; k < RB + 2 * R; ++k) win[k] = lds_pair(C + (rb * RB + k) * CS + c);
+    for (int k = 0; k < RB + 2 * R; ++k) win[k] = lds_pair_a(C + (r0 + k) * CS + c);
 #pragma unroll
     for (int rr = 0; rr < RB; ++rr) {
       f32x2 acc = 0.0f;
@@ -144,8 +187,7 @@ __global__ __launch_bounds__(256) void sharpen_band_kernel(const uint16_t* __res
         const f32x2 p = pc.taps[k] * win[rr + k];
         acc = acc + p;
       }
-      T[(rb * RB + rr) * CS + c] = acc.x;
-      T[(rb * RB + rr) * CS + c + 1] = acc.y;
+      lds_store_pair(T + (r0 + rr) * CS + c, acc);
     }
   }
   __syncthreads();
@@ -153,16 +195,19 @@ __global__ __launch_bounds__(256) void sharpen_band_kernel(const uint16_t* __res
   // ---- 3. horizontal pass + combine + band: a thread owns row r, columns [16·seg, 16·seg + 16)
   //         and keeps the overlapping column pairs (a, a+1) of its (16+2R)-value window in
   //         registers, so output pairs (j, j+1) take packed f32 ops as in the vertical pass; band
-  //         bits go through LDS to form the 64-bit row words. Wave = segment, lane = row: a
-  //         half-wave reads 32 rows at the odd stride CS, i.e. 32 distinct banks.
+  //         bits go through LDS to form the 64-bit row words. Wave = segment, lane = row: the
+  //         window is read as 8 + R aligned pairs (the odd-offset pairs are register moves).
   __shared__ uint16_t bm[4 * TH];
   const int r = threadIdx.x & (TH - 1), seg = threadIdx.x / TH;
   const int y = y0 + r;
   float smin = INFINITY, smax = -INFINITY;
   {
+    f32x2 ev[8 + R];
+#pragma unroll
+    for (int b = 0; b < 8 + R; ++b) ev[b] = lds_pair_a(T + r * CS + 16 * seg + 2 * b);
     f32x2 pw[16 + 2 * R - 1];
 #pragma unroll
-    for (int a = 0; a < 16 + 2 * R - 1; ++a) pw[a] = lds_pair(T + r * CS + 16 * seg + a);
+    for (int a = 0; a < 16 + 2 * R - 1; ++a) pw[a] = (a & 1) ? f32x2{ev[a >> 1].y, ev[(a >> 1) + 1].x} : ev[a >> 1];
     uint32_t bits = 0;
 #pragma unroll
     for (int j = 0; j < 16; j += 2) {
@@ -173,7 +218,10 @@ __global__ __launch_bounds__(256) void sharpen_band_kernel(const uint16_t* __res
         acc = acc + p;
       }
       // sharpen_combine (pixel_math.h) on both lanes: s = c + gain·(c − b), same rounding steps.
-      const f32x2 cv = lds_pair(C + (r + R) * CS + 16 * seg + j + R);
+      const float* cp = C + (r + R) * CS + 16 * seg + j + R;
+      f32x2 cv;
+      if constexpr (R % 2 == 0) cv = lds_pair_a(cp);
+      else cv = lds_pair(cp);
       const f32x2 dd = cv - acc;
       const f32x2 gg = pc.gain * dd;
       const f32x2 sv = cv + gg;

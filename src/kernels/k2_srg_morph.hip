@@ -34,18 +34,13 @@ namespace nm03::gpu {
 constexpr int kSrgThreads = NM03_SRG_THREADS;
 
 
-// kGlobal: slices above kSrgMaxDim — the same algorithm on bit planes in a per-slice global scratch
-// (L2-resident for a 1024² slice: 4 × 128 KiB), for capability rather than speed.
-template <bool kGlobal>
-__global__ __launch_bounds__(kSrgThreads) void srg_morph_kernel(const uint64_t* __restrict__ band,
-                                                        const SliceDesc* __restrict__ descs,
-                                                        const SeedXY* __restrict__ seeds, PipeConsts pc,
-                                                        SrgOutputs out, int plane_words) {
-  extern __shared__ __attribute__((aligned(16))) uint64_t lds_planes[];
-  __shared__ int flag[2];  // srg_fixpoint's two alternating change words
-  uint64_t* const smem = kGlobal ? out.scratch + (size_t)blockIdx.x * 4 * plane_words : lds_planes;
-  const SliceDesc d = descs[blockIdx.x];
-  const int W = d.w, H = d.h, n = d.wpr, hb = (H + 63) >> 6;
+// One slice's region growing + morphology, on four bit planes at `smem` (LDS or global scratch).
+// NW > 0: every row has NW words and every column HB words (compile time: unrolled register fills).
+template <int NW, int HB>
+__device__ __forceinline__ void srg_slice(uint64_t* const smem, int* flag, const uint64_t* __restrict__ band,
+                                          const SliceDesc& d, const SeedXY* __restrict__ seeds, const PipeConsts& pc,
+                                          const SrgOutputs& out, int plane_words) {
+  const int W = d.w, H = d.h, n = NW > 0 ? NW : d.wpr, hb = HB > 0 ? HB : (H + 63) >> 6;
   const int words = H * n;
   // LDS row strides: odd word counts, so the thread-per-row sweeps and the 64-row transposes (lane
   // = row) hit 32 distinct 8-byte bank pairs per half-wave instead of 4-way conflicts at stride 4.
@@ -72,34 +67,52 @@ __global__ __launch_bounds__(kSrgThreads) void srg_morph_kernel(const uint64_t* 
   transpose_plane(M, H, n, Mt, W, false, nullptr, sn, st);
   __syncthreads();
 
-  const int iters = srg_fixpoint(M, Rg, Mt, Rt, W, H, n, pc.connectivity, flag, sn, st);
+  const int iters = srg_fixpoint<NW, HB>(M, Rg, Mt, Rt, W, H, n, pc.connectivity, flag, sn, st);
   // An iteration in which no step changed anything ⇒ Rg is the fixpoint region.
   if (out.iterations && threadIdx.x == 0) out.iterations[blockIdx.x] = iters;
   const size_t off = d.mask_off;
   if (out.region) store_plane(Rg, out.region + off, H, n, sn);
   // Scratch planes now: M, Mt, Rt (all used in row layout, stride sn, from here on).
   if (out.dilated || out.border_dilated) {
-    morph(Rg, Mt, M, W, H, n, pc.dilation_size, true, sn);  // Mt = D
+    morph<NW>(Rg, Mt, M, W, H, n, pc.dilation_size, true, sn);  // Mt = D
     if (out.dilated) store_plane(Mt, out.dilated + off, H, n, sn);
     if (out.border_dilated) {
-      morph(Mt, Rt, M, W, H, n, 2 * pc.border_radius + 1, false, sn);  // Rt = erode(D)
+      morph<NW>(Mt, Rt, M, W, H, n, 2 * pc.border_radius + 1, false, sn);  // Rt = erode(D)
       for (int i = threadIdx.x; i < words; i += blockDim.x) out.border_dilated[off + i] = Mt[at(i)] & ~Rt[at(i)];
     }
     __syncthreads();
   }
   if (out.border_region) {
-    morph(Rg, Rt, M, W, H, n, 2 * pc.border_radius + 1, false, sn);
+    morph<NW>(Rg, Rt, M, W, H, n, 2 * pc.border_radius + 1, false, sn);
     for (int i = threadIdx.x; i < words; i += blockDim.x) out.border_region[off + i] = Rg[at(i)] & ~Rt[at(i)];
     __syncthreads();
   }
   if (out.eroded || out.border_eroded) {
-    morph(Rg, Mt, M, W, H, n, pc.erosion_size, false, sn);  // Mt = E
+    morph<NW>(Rg, Mt, M, W, H, n, pc.erosion_size, false, sn);  // Mt = E
     if (out.eroded) store_plane(Mt, out.eroded + off, H, n, sn);
     if (out.border_eroded) {
-      morph(Mt, Rt, M, W, H, n, 2 * pc.border_radius + 1, false, sn);
+      morph<NW>(Mt, Rt, M, W, H, n, 2 * pc.border_radius + 1, false, sn);
       for (int i = threadIdx.x; i < words; i += blockDim.x) out.border_eroded[off + i] = Mt[at(i)] & ~Rt[at(i)];
     }
   }
+}
+
+// kGlobal: slices above kSrgMaxDim — the same algorithm on bit planes in a per-slice global scratch
+// (L2-resident for a 1024² slice: 4 × 128 KiB), for capability rather than speed. 256×256 slices
+// (the cohort shape) take the 4-word specialisation.
+template <bool kGlobal>
+__global__ __launch_bounds__(kSrgThreads) void srg_morph_kernel(const uint64_t* __restrict__ band,
+                                                        const SliceDesc* __restrict__ descs,
+                                                        const SeedXY* __restrict__ seeds, PipeConsts pc,
+                                                        SrgOutputs out, int plane_words) {
+  extern __shared__ __attribute__((aligned(16))) uint64_t lds_planes[];
+  __shared__ int flag[2];  // srg_fixpoint's two alternating change words
+  uint64_t* const smem = kGlobal ? out.scratch + (size_t)blockIdx.x * 4 * plane_words : lds_planes;
+  const SliceDesc d = descs[blockIdx.x];
+  if (!kGlobal && d.wpr == 4 && d.h > 192 && d.h <= 256)
+    srg_slice<4, 4>(smem, flag, band, d, seeds, pc, out, plane_words);
+  else
+    srg_slice<0, 0>(smem, flag, band, d, seeds, pc, out, plane_words);
 }
 
 size_t srg_plane_words(int max_w, int max_h) {

@@ -38,6 +38,45 @@ __device__ __forceinline__ bool fill_row(uint64_t* R, const uint64_t* M, int n) 
   return changed;
 }
 
+// fill_row for a compile-time word count: all loads issued up front, both sweeps in registers,
+// one store per word (the runtime-n loop above serialises an LDS round trip per word and sweep).
+template <int NW>
+__device__ __forceinline__ bool fill_row_n(uint64_t* R, const uint64_t* M) {
+  uint64_t m[NW], r[NW], o[NW];
+#pragma unroll
+  for (int i = 0; i < NW; ++i) {
+    m[i] = M[i];
+    r[i] = R[i];
+  }
+  uint64_t carry = 0;
+#pragma unroll
+  for (int i = 0; i < NW; ++i) {
+    const uint64_t s = (r[i] & m[i]) | (carry & m[i] & 1ull);
+    const uint64_t f = fill_up(m[i], s);
+    o[i] = r[i] | f;
+    carry = f >> 63;
+  }
+  carry = 0;
+  bool changed = false;
+#pragma unroll
+  for (int i = NW - 1; i >= 0; --i) {
+    const uint64_t mb = brev64(m[i]), rb = brev64(o[i]);
+    const uint64_t s = (rb & mb) | (carry & mb & 1ull);
+    const uint64_t f = fill_up(mb, s);
+    o[i] = brev64(rb | f);
+    carry = f >> 63;
+    changed |= o[i] != r[i];
+    R[i] = o[i];
+  }
+  return changed;
+}
+
+template <int NW>
+__device__ __forceinline__ bool fill_row_any(uint64_t* R, const uint64_t* M, int n) {
+  if constexpr (NW > 0) return fill_row_n<NW>(R, M);
+  else return fill_row(R, M, n);
+}
+
 // Transpose a [rows][wpr] bit-plane (row stride ss words) into [cols][ceil(rows/64)] (row stride
 // ds words; 0 = dense). Returns (via flag) whether any destination word changed when `cmp` is set.
 __device__ inline void transpose_plane(const uint64_t* src, int rows, int wpr, uint64_t* dst, int cols, bool cmp, int* flag,
@@ -69,12 +108,26 @@ __device__ __forceinline__ uint64_t last_mask(int w) {
 }
 
 // Horizontal morphology of one row: OR (dilate) or AND (erode, outside = 1) of shifts by ±1..±r.
+// NW > 0: compile-time word count (n ignored), the row is loaded into registers once.
+template <int NW = 0>
 __device__ __forceinline__ void morph_row_h(const uint64_t* src, uint64_t* dst, int n, int w, int r, bool dil) {
   const uint64_t lm = last_mask(w);
+  constexpr int NR = NW > 0 ? NW : 1;
+  uint64_t row[NR];
+  if constexpr (NW > 0) {
+    n = NW;
+#pragma unroll
+    for (int i = 0; i < NW; ++i) row[i] = src[i];
+  }
+  auto word = [&](int i) -> uint64_t {
+    if constexpr (NW > 0) return row[i];
+    else return src[i];
+  };
+#pragma unroll
   for (int i = 0; i < n; ++i) {
-    uint64_t v = src[i];
-    uint64_t prev = i > 0 ? src[i - 1] : (dil ? 0ull : ~0ull);
-    uint64_t next = i + 1 < n ? src[i + 1] : (dil ? 0ull : ~0ull);
+    uint64_t v = word(i);
+    uint64_t prev = i > 0 ? word(i - 1) : (dil ? 0ull : ~0ull);
+    uint64_t next = i + 1 < n ? word(i + 1) : (dil ? 0ull : ~0ull);
     if (!dil) {
       if (i == n - 1) v |= ~lm;          // bits past the right edge count as "ignored" (=1)
       if (i + 1 == n - 1) next |= ~lm;
@@ -104,11 +157,12 @@ __device__ __forceinline__ void morph_rows_v(const uint64_t* src, uint64_t* dst,
   }
 }
 
+template <int NW = 0>
 __device__ inline void morph(const uint64_t* src, uint64_t* dst, uint64_t* tmp, int w, int h, int n, int size, bool dil,
                              int s = 0) {
   if (s == 0) s = n;
   const int r = size / 2;
-  for (int y = threadIdx.x; y < h; y += blockDim.x) morph_row_h(src + y * s, tmp + y * s, n, w, r, dil);
+  for (int y = threadIdx.x; y < h; y += blockDim.x) morph_row_h<NW>(src + y * s, tmp + y * s, n, w, r, dil);
   __syncthreads();
   morph_rows_v(tmp, dst, h, n, r, dil, s);
   __syncthreads();
@@ -128,9 +182,11 @@ __device__ inline void store_plane(const uint64_t* src, uint64_t* dst, int h, in
 // scratch. All planes in LDS; M/Rg rows are sn words apart, Mt/Rt rows st words apart (0 = dense;
 // odd strides keep the thread-per-row sweeps and transposes free of LDS bank conflicts). `flag` is
 // an LDS int. Returns the iteration count.
+// NW / HB > 0: compile-time words per row of the row / transposed planes (n / ceil(H/64)).
 // `flagp` points at TWO LDS ints: iteration k reports changes in flag[k & 1] and clears
 // flag[(k + 1) & 1] after its first barrier (every thread read that word at the end of iteration
 // k − 1 before reaching it), so the end of an iteration needs one barrier, not three.
+template <int NW = 0, int HB = 0>
 __device__ inline int srg_fixpoint(uint64_t* M, uint64_t* Rg, const uint64_t* Mt, uint64_t* Rt, int W, int H, int n,
                             int connectivity, int* flagp, int sn = 0, int st = 0) {
   const int hb = (H + 63) >> 6, words = H * n;
@@ -144,13 +200,13 @@ __device__ inline int srg_fixpoint(uint64_t* M, uint64_t* Rg, const uint64_t* Mt
     int& flag = flagp[iters & 1];
     ++iters;
     bool ch = false;
-    for (int y = threadIdx.x; y < H; y += blockDim.x) ch |= fill_row(Rg + y * sn, M + y * sn, n);
+    for (int y = threadIdx.x; y < H; y += blockDim.x) ch |= fill_row_any<NW>(Rg + y * sn, M + y * sn, n);
     if (ch) flag = 1;
     __syncthreads();
     if (threadIdx.x == 0) flagp[iters & 1] = 0;  // the next iteration's word
     if (connectivity == 8) {
       // Diagonal seeding from a snapshot of the horizontally dilated rows (Rt as scratch).
-      for (int y = threadIdx.x; y < H; y += blockDim.x) morph_row_h(Rg + y * sn, Rt + y * sn, n, W, 1, true);
+      for (int y = threadIdx.x; y < H; y += blockDim.x) morph_row_h<NW>(Rg + y * sn, Rt + y * sn, n, W, 1, true);
       __syncthreads();
       bool dch = false;
       for (int q = threadIdx.x; q < words; q += blockDim.x) {
@@ -169,7 +225,7 @@ __device__ inline int srg_fixpoint(uint64_t* M, uint64_t* Rg, const uint64_t* Mt
     }
     transpose_plane(Rg, H, n, Rt, W, false, nullptr, sn, st);
     __syncthreads();
-    for (int x = threadIdx.x; x < W; x += blockDim.x) fill_row(Rt + x * st, Mt + x * st, hb);
+    for (int x = threadIdx.x; x < W; x += blockDim.x) fill_row_any<HB>(Rt + x * st, Mt + x * st, hb);
     __syncthreads();
     transpose_plane(Rt, W, hb, Rg, H, true, &flag, st, sn);
     __syncthreads();

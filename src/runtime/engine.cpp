@@ -482,7 +482,14 @@ struct Engine::Impl {
         s.d_jsizes = dmalloc<int32_t>(s.cap_canvases, "hipMalloc jpeg sizes");
         s.jofs.assign(s.cap_canvases, 0);
       } else {
-        check_hip(hipHostMalloc((void**)&s.h_out, out_bytes, hipHostMallocMapped), "hipHostMalloc out");
+        // NM03_JPEG_OUT_MEM=coherent|noncoherent overrides HIP's default coherence of the
+        // host-mapped JPEG output (A/B of where the encoder's PCIe writes are paid).
+        static const unsigned out_flags = [] {
+          const char* e = std::getenv("NM03_JPEG_OUT_MEM");
+          const std::string v = e ? e : "";
+          return hipHostMallocMapped | (v == "coherent" ? hipHostMallocCoherent : v == "noncoherent" ? hipHostMallocNonCoherent : 0u);
+        }();
+        check_hip(hipHostMalloc((void**)&s.h_out, out_bytes, out_flags), "hipHostMalloc out");
         check_hip(hipHostGetDevicePointer((void**)&s.d_out, s.h_out, 0), "hipHostGetDevicePointer out");
       }
       check_hip(hipHostMalloc((void**)&s.h_sizes, sizeof(int32_t) * s.cap_canvases, hipHostMallocMapped),
