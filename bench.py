@@ -417,7 +417,8 @@ def run_rank(args):
             if gpu:
                 torch.cuda.synchronize()
             t0 = time.perf_counter()
-            codes, msgs, _ = engine.run_list(work, cap)
+            with _roctx_range("bench.step"):
+                codes, msgs, _ = engine.run_list(work, cap)
             dt = time.perf_counter() - t0
             if msgs:
                 raise SystemExit(f"rank {rank}: {len(msgs)} slices failed in the single pass")

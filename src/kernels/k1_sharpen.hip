@@ -173,8 +173,20 @@ __global__ __launch_bounds__(256) void sharpen_band_kernel(const uint16_t* __res
   // ---- 2. vertical pass: columns (c, c+1), rows [r0, r0 + RB) from a register window of
   //         column pairs; every tap is one v_pk_mul_f32 + one v_pk_add_f32 for two outputs --------
   constexpr int CP = CW / 2;  // CW = 64 + 2R is even
+  // Task → (block, pair): the first 32·NB tasks take pairs 0..31 (a 16-lane group of a b64 access
+  // stays inside one row block: conflict-free), the (CP − 32)·NB remaining pairs follow.
   for (int task = threadIdx.x; task < CP * NB; task += 256) {
-    const int rb = task / CP, c = 2 * (task - rb * CP);
+    int rb, cp;
+    if (task < 32 * NB) {
+      rb = task >> 5;
+      cp = task & 31;
+    } else {
+      constexpr int X = CP > 32 ? CP - 32 : 1;  // (CP = 32 never gets here)
+      const int k = task - 32 * NB;
+      rb = k / X;
+      cp = 32 + (k - rb * X);
+    }
+    const int c = 2 * cp;
     const int r0 = min(rb * RB, TH - RB);
     f32x2 win[RB + 2 * R];
 #pragma unroll

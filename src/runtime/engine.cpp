@@ -132,7 +132,7 @@ struct Slot {
   int ncanvas = 0;
   bool any_canvas = false;  // some image of the batch needs the generic render → canvas path
   int max_w = 0, max_h = 0;
-  double batch_ema_s = 0;  // enqueue → completion time of recent batches (wait_batch)
+  double batch_ema_s = 0;  // enqueue → completion time per slice of recent batches (wait_batch)
   // NM03_LOAD_MODE=mapped: per-slot reserved address range; slice i of a batch maps its file at
   // map_region + i * map_stride and the whole range is unmapped once after the batch's loads.
   uint8_t* map_region = nullptr;
@@ -574,9 +574,13 @@ struct Engine::Impl {
     return us;
   }
   // The slot first sleeps through most of the time its recent batches took from enqueue to
-  // completion (EMA), then polls: ~10 wake-ups per batch instead of one per poll interval over
-  // the whole batch (each wake-up is a context switch of host CPU the loaders/writers need).
-  void wait_batch(Slot& s, hipEvent_t ev, double t_enq) {
+  // completion (EMA, per slice × this batch's slices), then polls: ~10 wake-ups per batch instead of
+  // one per poll interval over the whole batch (each wake-up is a context switch of host CPU the
+  // loaders/writers need). Per slice, so a short batch after full ones (a strong-scaling shard cut
+  // into ⌈shard / streams⌉-slice batches) is not slept through at the full batches' time: fixed
+  // per-batch costs make small batches slower per slice, so the scaled estimate errs short (more
+  // polls), never long. NM03_EVENT_EMA=batch restores the per-batch EMA (A/B).
+  void wait_batch(Slot& s, hipEvent_t ev, double t_enq, int nslices) {
     if (wait_mode() != WaitMode::kPoll) {
       check_hip(hipEventSynchronize(ev), "batch sync");
       return;
@@ -585,13 +589,18 @@ struct Engine::Impl {
       const char* e = std::getenv("NM03_EVENT_ADAPT");  // 0: plain polling (A/B)
       return !(e && *e == '0');
     }();
+    static const bool per_batch = [] {
+      const char* e = std::getenv("NM03_EVENT_EMA");
+      return e && std::string(e) == "batch";
+    }();
+    const double scale = per_batch ? 1.0 : (double)std::max(1, nslices);
     // Sleep through most of the batch's expected time (0.8 × the recent mean), in chunks of at
     // most 250 µs with an event check between them, then poll. One long sleep would feed itself:
     // a slow batch (GPU shared with another process, host CPU stolen) raises the mean, the next
     // batches oversleep by the same amount, and the mean — measured from these overslept waits —
     // decays by only ≈5% per batch. Chunked, a wait ends within one chunk of the batch's real
     // completion, so the mean tracks the GPU again after a few batches.
-    const double target = adapt ? 0.8 * s.batch_ema_s : 0.0;
+    const double target = adapt ? 0.8 * s.batch_ema_s * scale : 0.0;
     for (;;) {
       const hipError_t e = hipEventQuery(ev);
       if (e == hipSuccess) break;
@@ -602,7 +611,7 @@ struct Engine::Impl {
       else
         std::this_thread::sleep_for(std::chrono::microseconds(poll_us()));
     }
-    const double took = now_s() - t_enq;
+    const double took = (now_s() - t_enq) / scale;
     s.batch_ema_s = s.batch_ema_s > 0 ? 0.75 * s.batch_ema_s + 0.25 * took : took;
   }
 
@@ -866,12 +875,19 @@ struct Engine::Impl {
     const double t_enq = now_s();
     if (!s.upload_started) check_hip(hipEventRecord(s.ev0, s.stream), "event");
     // Tables, then the raw pixels not already queued by upload_progress (all of them without it).
-    check_hip(hipMemcpyAsync(s.d_blob, s.h_blob, s.raw_base, hipMemcpyHostToDevice, s.stream), "H2D tables");
+    // The tables sit right before the raw region: with nothing uploaded early (a small batch) both
+    // go as one copy — one SDMA command and one completion on the batch's critical path, not two.
     const size_t raw_end = s.raw_used.load();
-    if (raw_end > s.uploaded)
-      check_hip(hipMemcpyAsync(s.d_blob + s.raw_base + s.uploaded * 2, s.h_blob + s.raw_base + s.uploaded * 2,
-                               (raw_end - s.uploaded) * 2, hipMemcpyHostToDevice, s.stream),
-                "H2D pixels");
+    if (s.uploaded == 0) {
+      check_hip(hipMemcpyAsync(s.d_blob, s.h_blob, s.raw_base + raw_end * 2, hipMemcpyHostToDevice, s.stream),
+                "H2D tables + pixels");
+    } else {
+      check_hip(hipMemcpyAsync(s.d_blob, s.h_blob, s.raw_base, hipMemcpyHostToDevice, s.stream), "H2D tables");
+      if (raw_end > s.uploaded)
+        check_hip(hipMemcpyAsync(s.d_blob + s.raw_base + s.uploaded * 2, s.h_blob + s.raw_base + s.uploaded * 2,
+                                 (raw_end - s.uploaded) * 2, hipMemcpyHostToDevice, s.stream),
+                  "H2D pixels");
+    }
     s.uploaded = raw_end;
     check_hip(hipEventRecord(s.ev1, s.stream), "event");
     auto chain = [&] {
@@ -947,7 +963,7 @@ struct Engine::Impl {
       check_hip(hipMemcpyAsync(s.h_out, s.d_jcomp, s.jcopied, hipMemcpyDeviceToHost, s.stream), "jpeg D2H");
     }
     check_hip(hipEventRecord(s.ev2, s.stream), "event");
-    wait_batch(s, s.ev2, t_enq);
+    wait_batch(s, s.ev2, t_enq, nl);
     if (jpeg_d2h_ && ncanv > 0) finish_jpeg_d2h(s, ncanv);
     if (acc) {
       float a = 0, b = 0;

@@ -5,7 +5,7 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"; export TMPDIR=/tmp; O=gpurun_out/r3o; mkdir -p $O
 timeout -k 10 300 python -u -m pytest tests/test_gpu.py -x -q --timeout 120 --timeout-method thread \
-  -k "jpeg or engine or cli_sequential_equals" > $O/pytest.log 2>&1 || exit 31
+  -k "jpeg or engine or cli_sequential_equals or sharpen" > $O/pytest.log 2>&1 || exit 31
 D=/tmp/r3o_data
 build/bin/nm03_synth --data-root $D/ --threads 16 > /dev/null || exit 41
 run() {  # name, env...
@@ -22,4 +22,8 @@ for rep in 1 2; do
   run coh_$rep NM03_JPEG_OUT_MEM=coherent || exit 45
   run noncoh_$rep NM03_JPEG_OUT_MEM=noncoherent || exit 46
 done
+mkdir -p $O/pmc
+timeout -s KILL 90 rocprofv3 --pmc SQ_WAVES SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_INSTS_VALU SQ_WAVE_CYCLES --output-format csv -d $O/pmc/p1 -o run \
+  -- build/bin/nm03_bench --config cohort --data-root $D/ --steps 2 --warmup 1 --batch-size 96 --streams 1 > $O/pmc/p1.log 2>&1 || exit 71
+python3 tools/pmc_summary.py $O/pmc $O/s16_1/run_kernel_stats.csv > $O/pmc_summary.txt 2>&1 || exit 69
 rm -rf $D
