@@ -125,6 +125,9 @@ struct Slot {
   std::mutex prog_m;
   std::condition_variable prog_cv;
   size_t loads_finished = 0;  // guarded by prog_m
+  // Set by upload_progress when the whole batch fits in one upload chunk: loaders stop notifying
+  // (a wake-up of the slot thread per load, on CPUs the loaders need, for nothing to upload early).
+  std::atomic<bool> progress_quiet{false};
   size_t uploaded = 0;        // u16 elements of the raw region already queued for upload
   bool upload_started = false;
   // built per batch
@@ -533,7 +536,13 @@ struct Engine::Impl {
         ++next;
       }
       if (all) return;  // the remainder goes with the tables in build_and_run
-      if (!chunk && next > 0) chunk = std::max(upload_chunk_, count * s.allocs[0].len * 2 / 4);
+      if (!chunk && next > 0) {
+        chunk = std::max(upload_chunk_, count * s.allocs[0].len * 2 / 4);
+        if (chunk >= count * s.allocs[0].len * 2) {  // a small batch: one upload with the tables
+          s.progress_quiet.store(true, std::memory_order_relaxed);
+          return;
+        }
+      }
       if (chunk && (end - s.uploaded) * 2 >= chunk) {
         if (!s.upload_started) {
           check_hip(hipEventRecord(s.ev0, s.stream), "event");
@@ -1040,6 +1049,7 @@ struct Engine::Impl {
       std::lock_guard<std::mutex> g(s.prog_m);
       s.loads_finished = 0;
     }
+    s.progress_quiet.store(false, std::memory_order_relaxed);
     std::atomic<int64_t> load_ns{0}, bytes_in{0}, write_ns{0}, bytes_out{0}, load_cpu_ns{0}, write_cpu_ns{0};
     std::string upload_error;
     // NM03_PIN=l3: slice (first + i)'s load and export run on L3 domain (first + i) mod G, so the
@@ -1073,7 +1083,7 @@ struct Engine::Impl {
                 std::lock_guard<std::mutex> g(s.prog_m);
                 ++s.loads_finished;
               }
-              s.prog_cv.notify_one();
+              if (!s.progress_quiet.load(std::memory_order_relaxed)) s.prog_cv.notify_one();
             }
           },
           2 * prio, &load_cpu_ns);
