@@ -96,6 +96,8 @@ def parse_args(argv=None):
     ap.add_argument("--streams", type=int, default=4)
     ap.add_argument("--threads", type=int, default=0,
                     help="host I/O threads per rank (0 = the rank's CPU partition and budget share, ≤16)")
+    ap.add_argument("--single-pass-cap", type=int, default=0,
+                    help="batch cap of the capped single passes (0 = ceil(shard / streams))")
     ap.add_argument("--single-passes", type=int, default=10,
                     help="also time this many single strong-scaling passes (one cohort sharded over the "
                          "ranks, nothing else in flight; config.strong.single_pass_ms; 0 = skip)")
@@ -410,7 +412,7 @@ def run_rank(args):
         if ranks_like > 0:
             mine = mine[:len(mine) // ranks_like]
         work = n.WorkList(mine)
-        cap = -(-len(mine) // args.streams) if capped else 0
+        cap = (args.single_pass_cap or -(-len(mine) // args.streams)) if capped else 0
         times = []
         for k in range(passes + 1):  # pass 0 warms the output files
             comm.barrier()
@@ -445,7 +447,7 @@ def run_rank(args):
         sp_root = os.path.join(args.out_root, "single")
         med, best = single_pass(sp_root, args.single_passes, capped=True)
         med_u, best_u = single_pass(sp_root, args.single_passes, capped=False)
-        sp = {"single_pass_ms": med, "single_pass_min_ms": best, "single_pass_batch_cap": "ceil(shard/streams)",
+        sp = {"single_pass_ms": med, "single_pass_min_ms": best, "single_pass_batch_cap": args.single_pass_cap or "ceil(shard/streams)",
               "single_pass_uncapped_ms": med_u, "single_pass_uncapped_min_ms": best_u,
               "single_pass_passes": args.single_passes}
         if world == 1:

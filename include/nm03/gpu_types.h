@@ -99,7 +99,8 @@ struct JpegDesc {
   uint32_t stage_words;
   uint64_t out_off;     // byte offset in the output buffer (host-mapped)
   uint32_t out_cap;     // capacity in bytes
-  int32_t render;       // ≥0: fused 2× render from RenderDesc[render] (no canvas); -1: read canvas
+  int32_t render;       // -1: read canvas; else the fused 2× render from RenderDesc[render], where
+                        // render is this descriptor's own index (the encoder loads both at once)
 };
 
 // Byte-stuffing chunk (bytes of entropy-coded data per workgroup in the stuffing kernels).

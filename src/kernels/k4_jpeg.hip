@@ -170,20 +170,31 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(kOcc)))
     if (tid == 999) out_sizes[0] = 1;
     return;
   }
-  actab[tid] = kHuffAcLuma.e[tid];
-  if (tid < 16) dctab[tid] = tid < 12 ? kHuffDcLuma.e[tid] : 0u;
   const int bpi = (out_w >> 3) * (out_h >> 3);
   const int parts = (bpi + kJpegWG - 1) / kJpegWG;
-  // The image is fixed by the dispatch index; only the part comes from the ticket, so the
-  // descriptor loads below overlap the ticket's round trip.
+  // The image is fixed by the dispatch index; only the part comes from the ticket. The ticket's
+  // device-scope atomic is issued first, so its round trip overlaps the table and descriptor
+  // loads below (issued after them it waited behind three dependent descriptor loads).
   const int img = (int)(blockIdx.x / (uint32_t)parts);
+  uint32_t ticket = 0;
+  if (tid == 0 && dbg != 9) {
+    // The address goes through a VGPR the compiler cannot prove uniform: a uniform-address atomic
+    // is rewritten into a wave-aggregated one whose result is waited for on the spot.
+    // (Kept in the global address space: a flat atomic would also count in lgkmcnt and hold up
+    // the LDS waits behind it.)
+    auto* tp = (__attribute__((address_space(1))) uint32_t*)&w.ticket[img];
+    asm volatile("" : "+v"(tp));
+    ticket = __hip_atomic_fetch_add(tp, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  actab[tid] = kHuffAcLuma.e[tid];
+  if (tid < 16) dctab[tid] = tid < 12 ? kHuffDcLuma.e[tid] : 0u;
+  // JpegDesc::render is -1 or img itself, so the render descriptor loads alongside the JPEG one
+  // (no dependent round trip); the render window (stats of the slice) is computed where the render
+  // first needs it, so its load overlaps the staging below.
   const JpegDesc d = jd[img];
   RenderDesc rd;
+  if (rs.rd) rd = rs.rd[img];
   RWindow win{0.f, 0.f};
-  if (d.render >= 0) {
-    rd = rs.rd[d.render];
-    if (rd.kind != kRenderLabels) win = render_window(rd, rs.stats);
-  }
   if (tid == 0) {
     // Ordered tickets per image: workgroup b encodes image b / parts and takes the next part of
     // that image from the image's counter, so it only ever waits on parts whose workgroups have
@@ -194,7 +205,7 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(kOcc)))
     // GPU.) One counter per image keeps the serialised atomics per address at `parts`.
     uint32_t p = blockIdx.x - (uint32_t)img * (uint32_t)parts;
     if (dbg != 9) {
-      p = atomicAdd(&w.ticket[img], 1u);
+      p = ticket;
       if (p == (uint32_t)parts - 1) atomicExch(&w.ticket[img], 0u);  // the image's last ticket
     }
     s_ticket = p;
@@ -286,6 +297,7 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(kOcc)))
   // quantised and — if non-zero in some lane of the wave (else the position is skipped) — coded
   // straight into the block's private bit buffer. The DC code depends on the previous block's DC,
   // so the AC stream is coded first and the DC code is prepended at assembly time.
+  if (d.render >= 0 && rd.kind != kRenderLabels) win = render_window(rd, rs.stats);
   uint32_t* const pbuf = spriv + tid * kPrivWords;
   uint32_t* const pspill = w.spill + ((size_t)blockIdx.x * kJpegWG + tid) * kSpillWords;
   int dc0 = 0;
