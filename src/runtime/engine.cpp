@@ -6,6 +6,7 @@
 #include <sys/mman.h>
 #include <sys/prctl.h>
 #include <sys/resource.h>
+#include <sys/syscall.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -148,6 +149,30 @@ struct Slot {
   std::map<std::array<int, 11>, hipGraphExec_t> graphs;
 };
 
+// Private fd tables for the host pool's workers (NM03_PRIVATE_FDS, default on). Every open and
+// close takes the process's fd-table lock; with 16 loader/writer threads doing three opens and
+// three closes per slice that lock (and its cache line crossing CCDs) doubled the per-file cost:
+// 23–24 µs per load and 31.7 µs per JPEG pair in 16 threads of one process vs 14.7–16.5 and
+// 10.0–10.6 µs in 16 processes (tools/io_contention.cpp, profiles/r3/io_contention/). Each worker
+// therefore starts with close_range(3, ~0U, CLOSE_RANGE_UNSHARE): its own table, holding only
+// stdin/out/err (no duplicates of the process's other fds, so a pipe or file the process closes is
+// not kept open by a worker). Directory fds are then per worker too (IoDirs::dir_fd).
+static bool private_fds_wanted() {
+  static const bool on = [] {
+    const char* e = std::getenv("NM03_PRIVATE_FDS");
+    return !(e && *e == '0');
+  }();
+  return on;
+}
+static thread_local bool tl_private_fds = false;
+
+static void make_fd_table_private() {
+#ifndef CLOSE_RANGE_UNSHARE
+#define CLOSE_RANGE_UNSHARE (1U << 1)
+#endif
+  if (private_fds_wanted() && ::syscall(SYS_close_range, 3u, ~0u, CLOSE_RANGE_UNSHARE) == 0) tl_private_fds = true;
+}
+
 // Directory fds of one run: every item's input series directory and output directory opened once
 // (O_PATH), so loads and writes use openat on the bare file name instead of walking the full path
 // per file. Opened per run, never cached across runs: a caller may wipe and re-create output
@@ -161,12 +186,16 @@ struct IoDirs {
     return std::min<size_t>(256, lim / 8);
   }
   std::vector<int> fds;
+  std::vector<std::string> paths;  // per fd index
+  uint64_t id;                     // unique per run (keys the workers' private directory fds)
   // Per directory: 1 once a file was missing there (files are then created directly, see
   // jpeg::write_jpeg_at); 0 = try opening existing files without O_CREAT first.
   std::unique_ptr<std::atomic<uint8_t>[]> creating;
   std::vector<int32_t> in_fd, out_fd;  // per item: fd index, -1 = fall back to the full path
   std::vector<uint32_t> in_name;       // per item: offset of the file name in its path
   IoDirs(const std::vector<WorkItem>& items) {
+    static std::atomic<uint64_t> next_id{1};
+    id = next_id.fetch_add(1, std::memory_order_relaxed);
     std::unordered_map<std::string, int32_t> idx;
     const size_t cap = max_fds();
     auto dir_index = [&](const std::string& d) -> int32_t {
@@ -177,6 +206,7 @@ struct IoDirs {
       if (fd >= 0) {
         k = (int32_t)fds.size();
         fds.push_back(fd);
+        paths.push_back(d.empty() ? "/" : d);
       }
       idx.emplace(d, k);
       return k;
@@ -201,6 +231,36 @@ struct IoDirs {
   }
   ~IoDirs() {
     for (int fd : fds) ::close(fd);
+  }
+  // fd of directory k usable on the calling thread, -1 if none (the caller then uses the full
+  // path). A worker with a private fd table opens its own O_PATH fds lazily, cached for the two most
+  // recent runs it served (runs are pipelined, so a worker alternates between two).
+  int dir_fd(int32_t k) const {
+    if (k < 0) return -1;
+    if (!tl_private_fds) return fds[(size_t)k];
+    struct Cache {
+      uint64_t id[2] = {0, 0};
+      std::vector<int> fds[2];
+      int victim = 0;
+      ~Cache() {
+        for (auto& v : fds)
+          for (int fd : v)
+            if (fd >= 0) ::close(fd);
+      }
+    };
+    static thread_local Cache c;
+    int slot = c.id[0] == id ? 0 : c.id[1] == id ? 1 : -1;
+    if (slot < 0) {
+      slot = c.victim;
+      c.victim ^= 1;
+      for (int fd : c.fds[slot])
+        if (fd >= 0) ::close(fd);
+      c.fds[slot].assign(fds.size(), -2);  // -2: not opened yet
+      c.id[slot] = id;
+    }
+    int& fd = c.fds[slot][(size_t)k];
+    if (fd == -2) fd = ::open(paths[(size_t)k].c_str(), O_PATH | O_DIRECTORY | O_CLOEXEC);
+    return fd;
   }
   IoDirs(const IoDirs&) = delete;
   IoDirs& operator=(const IoDirs&) = delete;
@@ -340,7 +400,10 @@ struct Engine::Impl {
     if (!host_only_) check_hip(hipSetDevice(cfg.device), "hipSetDevice");
     const double t1 = now_s();
     // Host threads and pinned buffers on the GPU's socket (numa.h).
-    pool = std::make_unique<ThreadPool>(cfg.threads, [this](int i) { place.bind_worker(i, cfg.threads); });
+    pool = std::make_unique<ThreadPool>(cfg.threads, [this](int i) {
+      place.bind_worker(i, cfg.threads);
+      make_fd_table_private();
+    });
     const double t2 = now_s();
     // Slot 0 is built here (its failure fails the constructor); the others are built by their own
     // worker threads while slot 0 already runs batches — a slot costs ≈11–18 ms of pinned and
@@ -1074,8 +1137,9 @@ struct Engine::Impl {
               status[first + i] = SliceStatus{kSliceOk, "resumed: outputs already present"};
             } else {
               const size_t it = first + i;
-              const int dfd = dirs.in_fd[it] >= 0 ? dirs.fds[dirs.in_fd[it]] : AT_FDCWD;
-              const char* nm = items[it].path.c_str() + (dirs.in_fd[it] >= 0 ? dirs.in_name[it] : 0);
+              const int dk = dirs.dir_fd(dirs.in_fd[it]);
+              const int dfd = dk >= 0 ? dk : AT_FDCWD;
+              const char* nm = items[it].path.c_str() + (dk >= 0 ? dirs.in_name[it] : 0);
               load_into(s, (int)i, it, items[it].path, dfd, nm, status[it], load_ns, bytes_in);
             }
             if (upload_chunk_) {
@@ -1169,8 +1233,9 @@ struct Engine::Impl {
             TraceRange tr("nm03.export");
             try {
               if (fault_plan().fail_write == (int64_t)item) throw std::runtime_error("injected fault: export failure");
-              const bool rel = dirs.out_fd[item] >= 0;
-              const int dfd = rel ? dirs.fds[dirs.out_fd[item]] : AT_FDCWD;
+              const int dk = dirs.dir_fd(dirs.out_fd[item]);
+              const bool rel = dk >= 0;
+              const int dfd = rel ? dk : AT_FDCWD;
               const std::string base = (rel ? std::string() : cohort::with_slash(items[item].out_dir)) +
                                        cohort::stem(items[item].path);
               for (int k = 0; k < 2; ++k) {
