@@ -118,6 +118,9 @@ void launch_threshold(const float* in, uint8_t* out, size_t n, float lo, float h
 
 // K0: expand a batch's uploaded raw region (12-bit packed or plain 16-bit slices, SliceDesc::blob_off
 // and flags) into the 16-bit sample buffer at SliceDesc::raw_off.
+// Shader copy of `bytes` from host-mapped pinned memory (device view) into device memory; 16-byte
+// aligned pointers.
+void launch_copy_from_host(const void* src, void* dst, size_t bytes, hipStream_t stream);
 void launch_unpack(const uint16_t* blob_raw, uint16_t* raw, const SliceDesc* descs, int nslices, int max_pixels,
                    hipStream_t stream);
 // True when RenderDesc r is an exact 2× fit onto the canvas (the fused fast path applies).

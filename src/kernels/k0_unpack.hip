@@ -4,6 +4,8 @@
 // HBM-bound and tiny next to the upload it shortens (≈6 MB read, 8 MB written per 64-slice batch).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "nm03/gpu_types.h"
 #include "nm03/kernels.h"
 
@@ -59,6 +61,30 @@ void launch_unpack(const uint16_t* blob_raw, uint16_t* raw, const SliceDesc* des
   dim3 grid((unsigned)((groups + 255) / 256), (unsigned)nslices), block(256);
   unpack_kernel<<<grid, block, 0, stream>>>(blob_raw, raw, descs);
   check_launch("unpack_kernel");
+}
+
+// Upload of a small batch as a shader copy from host-mapped pinned memory (engine: batches up to
+// NM03_SHADER_UPLOAD_KB). The copy runs on the batch's compute queue, so the median starts without
+// an SDMA → compute dependency and does not queue behind other slots' SDMA uploads (a 15-slice
+// batch's copy measured 36 µs when alone and up to ≈180 µs beside three others, plus ≈12 µs from
+// its end to the first kernel: profiles/r3/single_pass/).
+__global__ __launch_bounds__(256) void copy_from_host_kernel(const uint4* __restrict__ src, uint4* __restrict__ dst,
+                                                             size_t n16, const uint8_t* __restrict__ src_tail,
+                                                             uint8_t* __restrict__ dst_tail, int tail) {
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n16; i += (size_t)gridDim.x * 256) dst[i] = src[i];
+  if (blockIdx.x == 0 && (int)threadIdx.x < tail) dst_tail[threadIdx.x] = src_tail[threadIdx.x];
+}
+
+void launch_copy_from_host(const void* src, void* dst, size_t bytes, hipStream_t stream) {
+  if (bytes == 0) return;
+  if (((uintptr_t)src | (uintptr_t)dst) & 15) throw DeviceError("launch_copy_from_host: pointers must be 16-byte aligned");
+  const size_t n16 = bytes / 16;
+  const int tail = (int)(bytes % 16);
+  const size_t groups = std::max<size_t>(1, std::min<size_t>((n16 + 255) / 256, 2048));
+  copy_from_host_kernel<<<(unsigned)groups, 256, 0, stream>>>(
+      static_cast<const uint4*>(src), static_cast<uint4*>(dst), n16, static_cast<const uint8_t*>(src) + n16 * 16,
+      static_cast<uint8_t*>(dst) + n16 * 16, tail);
+  check_launch("copy_from_host_kernel");
 }
 
 }  // namespace nm03::gpu

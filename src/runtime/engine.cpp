@@ -89,6 +89,7 @@ struct Slot {
          raw_base = 0, blob_bytes = 0;
   size_t max_medt = 0, max_shpt = 0;
   uint8_t* h_blob = nullptr;
+  uint8_t* d_hblob = nullptr;  // device view of h_blob (shader uploads of small batches), or null
   uint8_t* d_blob = nullptr;
   uint16_t* d_raw_x = nullptr;  // expanded 16-bit samples of the batch (K0 output, every kernel's input)
   uint16_t* d_med = nullptr;
@@ -519,6 +520,10 @@ struct Engine::Impl {
       const bool spin = wait_mode() == WaitMode::kSpin;
       check_hip(hipEventCreateWithFlags(&s.ev2, spin ? hipEventDefault : hipEventBlockingSync), "hipEventCreate");
       check_hip(hipHostMalloc((void**)&s.h_blob, s.blob_bytes, hipHostMallocDefault), "hipHostMalloc blob");
+      if (hipHostGetDevicePointer((void**)&s.d_hblob, s.h_blob, 0) != hipSuccess) {
+        (void)hipGetLastError();
+        s.d_hblob = nullptr;
+      }
       // +64 B tail slack: the median's packed-group loads read whole dwords (k1_median.hip).
       s.d_blob = dmalloc<uint8_t>(s.blob_bytes + 64, "hipMalloc blob");
       s.d_raw_x = dmalloc<uint16_t>(s.cap_pixels, "hipMalloc raw");
@@ -576,6 +581,12 @@ struct Engine::Impl {
   // batches of large slices use a quarter of the batch (512² × 64: 8 MiB — many concurrent small
   // copies cost 10% of the upload rate there, profiles/iter5/c4_sweep.txt).
   size_t upload_chunk_ = 2u << 20;
+  // Batches whose whole upload (tables + pixels) is at most this many bytes are copied by a shader
+  // on the compute queue (launch_copy_from_host) instead of SDMA; NM03_SHADER_UPLOAD_KB, 0 = never.
+  size_t shader_upload_bytes_ = [] {
+    const char* e = std::getenv("NM03_SHADER_UPLOAD_KB");
+    return (size_t)(e && *e ? std::atoll(e) : 0) * 1024;
+  }();
 
   void upload_progress(Slot& s, size_t count) {
     size_t next = 0, seen = 0;
@@ -950,7 +961,9 @@ struct Engine::Impl {
     // The tables sit right before the raw region: with nothing uploaded early (a small batch) both
     // go as one copy — one SDMA command and one completion on the batch's critical path, not two.
     const size_t raw_end = s.raw_used.load();
-    if (s.uploaded == 0) {
+    if (s.uploaded == 0 && s.d_hblob && s.raw_base + raw_end * 2 <= shader_upload_bytes_) {
+      launch_copy_from_host(s.d_hblob, s.d_blob, s.raw_base + raw_end * 2, s.stream);  // small batch: no SDMA
+    } else if (s.uploaded == 0) {
       check_hip(hipMemcpyAsync(s.d_blob, s.h_blob, s.raw_base + raw_end * 2, hipMemcpyHostToDevice, s.stream),
                 "H2D tables + pixels");
     } else {
@@ -1143,11 +1156,16 @@ struct Engine::Impl {
               load_into(s, (int)i, it, items[it].path, dfd, nm, status[it], load_ns, bytes_in);
             }
             if (upload_chunk_) {
+              size_t lf;
               {
                 std::lock_guard<std::mutex> g(s.prog_m);
-                ++s.loads_finished;
+                lf = ++s.loads_finished;
               }
-              if (!s.progress_quiet.load(std::memory_order_relaxed)) s.prog_cv.notify_one();
+              // Every 4th load (and the last) wakes the slot thread: an upload chunk is ≥ 2 MiB
+              // (≥ 20 slices of 256²), so finer wake-ups only cost context switches on the CPUs
+              // the loaders run on.
+              if (!s.progress_quiet.load(std::memory_order_relaxed) && ((lf & 3) == 0 || lf == count))
+                s.prog_cv.notify_one();
             }
           },
           2 * prio, &load_cpu_ns);
