@@ -127,3 +127,49 @@ def test_host_only_fault_injection(native, cohort_root, tmp_path, fault, code):
     codes = json.loads(r.stdout.strip().splitlines()[-1])
     bad = int(fault.split(":")[1])
     assert codes[bad] == code and all(c == 0 for i, c in enumerate(codes) if i != bad)
+
+
+def _tree_bytes(items):
+    out = {}
+    for f, d in items:
+        stem = os.path.basename(f)[:-4]
+        for kind in ("original", "processed"):
+            p = os.path.join(d, f"{stem}_{kind}.jpg")
+            out[p] = open(p, "rb").read()
+    return out
+
+
+@pytest.mark.parametrize("private", ["1", "0"])
+def test_host_only_private_fd_tables_identical(native, cohort_root, tmp_path, monkeypatch, private):
+    """Pool workers with private fd tables (close_range UNSHARE, per-worker directory fds) write
+    the same files as with the shared table, across several queued runs (the per-worker directory
+    cache alternates between runs) and fresh vs existing output trees."""
+    monkeypatch.setenv("NM03_PRIVATE_FDS", private)
+    items = _items(native, cohort_root, str(tmp_path / "a"))
+    items_b = _items(native, cohort_root, str(tmp_path / "b"))
+    eng = _engine(native, threads=4)
+    wa, wb = native.WorkList(items), native.WorkList(items_b)
+    for _ in range(2):  # first pass creates, second rewrites in place
+        ta, tb = eng.submit(wa), eng.submit(wb)
+        for t in (ta, tb):
+            codes, msgs, _ = eng.wait(t)
+            assert not msgs
+    a, b = _tree_bytes(items), _tree_bytes(items_b)
+    assert len(a) == 2 * len(items) and sorted(a.values()) == sorted(b.values())
+
+
+def test_private_fd_tables_do_not_hold_process_fds(native, cohort_root, tmp_path, monkeypatch):
+    """A worker's private table starts with stdin/out/err only: a pipe the process creates before
+    the engine and closes afterwards must reach EOF while the engine (and its pool) is alive."""
+    monkeypatch.setenv("NM03_PRIVATE_FDS", "1")
+    r, w = os.pipe()
+    eng = _engine(native, threads=4)
+    items = _items(native, cohort_root, str(tmp_path / "o"))
+    codes, msgs, _ = eng.run_list(native.WorkList(items))
+    assert not msgs
+    os.close(w)
+    import select
+    ready, _, _ = select.select([r], [], [], 5.0)
+    assert ready and os.read(r, 1) == b""  # EOF: no worker kept a duplicate of the write end
+    os.close(r)
+    del eng

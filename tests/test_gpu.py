@@ -492,6 +492,26 @@ def test_engine_progressive_upload_identical(native, cohort_root, tmp_path, monk
         assert tree == runs[0][1]
 
 
+def test_engine_shader_upload_and_batch_cap_identical(native, cohort_root, tmp_path, monkeypatch):
+    """Small batches uploaded by the shader copy from host-mapped memory (NM03_SHADER_UPLOAD_KB)
+    vs SDMA, with the batch cap of the single-pass measurement (run_list(items, cap)) and with the
+    private worker fd tables off: same statuses, byte-identical trees."""
+    runs = []
+    for i, (kb, cap, pfd) in enumerate([("0", 0, "1"), ("4096", 5, "1"), ("0", 5, "0"), ("4096", 0, "1")]):
+        out = str(tmp_path / f"o{i}")
+        items = _items(native, cohort_root, out)[:37]
+        monkeypatch.setenv("NM03_SHADER_UPLOAD_KB", kb)
+        monkeypatch.setenv("NM03_PRIVATE_FDS", pfd)
+        eng = native.Engine(nm.PipelineConfig(batch_size=16, streams=3, threads=4).engine_config())
+        codes, msgs, _ = eng.run_list(native.WorkList(items), cap)
+        del eng
+        runs.append((list(codes), _tree(out)))
+    assert runs[0][0].count(0) == len(runs[0][0])
+    for codes, tree in runs[1:]:
+        assert codes == runs[0][0]
+        assert tree == runs[0][1]
+
+
 # ---------------------------------------------------------------------------------------------
 # CLIs on the GPU: sequential ≡ parallel byte-for-byte, reference message catalogue
 # ---------------------------------------------------------------------------------------------
