@@ -78,6 +78,7 @@ struct LoadedSlice {
 struct Slot {
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
+  hipStream_t up = nullptr;  // stream of this slot's H2D copies: its own stream, or the engine's shared one
   int cap_slices = 0, cap_canvases = 0;
   size_t cap_pixels = 0;  // u16 elements of expanded samples per batch (device raw/median buffers)
   // The blob's raw region also holds `hole_slack` u16 of slack for abandoned 12-bit reservations
@@ -439,6 +440,30 @@ struct Engine::Impl {
     if (!host_only_) (void)hipSetDevice(cfg.device);
     for (auto& s : slots)
       if (s) hip_free_all(*s);
+    if (shared_up_) (void)hipStreamDestroy(shared_up_);
+  }
+
+  // Every slot's H2D copies go through one engine-wide stream (default; NM03_UPLOAD_STREAM=own: each
+  // slot's own stream), so at most one SDMA upload runs at a time: two or more concurrent copies
+  // from different streams drop the copy engine's aggregate rate on the MI355X boxes
+  // (tools/h2d_probe.hip: 28 vs 53-57 GB/s), and in the bench 20-40% of the upload time had two or
+  // more in flight (profiles/r3/timeline/). The slot's kernels wait on an event after its last copy.
+  // Measured: rank-0 H2D time per 50 steps 0.056 vs 0.080-0.107 s, 377-399k vs 310-334k slices/s
+  // (4 interleaved pairs, profiles/r3/upload_stream/).
+  hipStream_t shared_up_ = nullptr;
+  std::mutex shared_up_m_;
+  static bool shared_upload_stream() {
+    static const bool on = [] {
+      const char* e = std::getenv("NM03_UPLOAD_STREAM");
+      return !(e && std::string(e) == "own");
+    }();
+    return on;
+  }
+  hipStream_t upload_stream_for(hipStream_t own) {
+    if (!shared_upload_stream()) return own;
+    std::lock_guard<std::mutex> g(shared_up_m_);
+    if (!shared_up_) check_hip(hipStreamCreateWithFlags(&shared_up_, hipStreamNonBlocking), "hipStreamCreate upload");
+    return shared_up_;
   }
 
   void make_templates() {
@@ -514,6 +539,7 @@ struct Engine::Impl {
         s.map_region = static_cast<uint8_t*>(r);
       }
       check_hip(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking), "hipStreamCreate");
+      s.up = upload_stream_for(s.stream);
       check_hip(hipEventCreate(&s.ev0), "hipEventCreate");
       check_hip(hipEventCreate(&s.ev1), "hipEventCreate");
       // Batch completion is waited on by the slot thread (wait_batch).
@@ -619,11 +645,11 @@ struct Engine::Impl {
       }
       if (chunk && (end - s.uploaded) * 2 >= chunk) {
         if (!s.upload_started) {
-          check_hip(hipEventRecord(s.ev0, s.stream), "event");
+          check_hip(hipEventRecord(s.ev0, s.up), "event");
           s.upload_started = true;
         }
         check_hip(hipMemcpyAsync(s.d_blob + s.raw_base + s.uploaded * 2, s.h_blob + s.raw_base + s.uploaded * 2,
-                                 (end - s.uploaded) * 2, hipMemcpyHostToDevice, s.stream),
+                                 (end - s.uploaded) * 2, hipMemcpyHostToDevice, s.up),
                   "H2D pixels");
         s.uploaded = end;
       }
@@ -956,25 +982,28 @@ struct Engine::Impl {
     auto plane = [&](Plane p) { return s.d_bits + p * s.plane_words; };
 
     const double t_enq = now_s();
-    if (!s.upload_started) check_hip(hipEventRecord(s.ev0, s.stream), "event");
     // Tables, then the raw pixels not already queued by upload_progress (all of them without it).
     // The tables sit right before the raw region: with nothing uploaded early (a small batch) both
     // go as one copy — one SDMA command and one completion on the batch's critical path, not two.
     const size_t raw_end = s.raw_used.load();
-    if (s.uploaded == 0 && s.d_hblob && s.raw_base + raw_end * 2 <= shader_upload_bytes_) {
+    const bool shader = s.uploaded == 0 && s.d_hblob && s.raw_base + raw_end * 2 <= shader_upload_bytes_;
+    hipStream_t up = shader ? s.stream : s.up;
+    if (!s.upload_started) check_hip(hipEventRecord(s.ev0, up), "event");
+    if (shader) {
       launch_copy_from_host(s.d_hblob, s.d_blob, s.raw_base + raw_end * 2, s.stream);  // small batch: no SDMA
     } else if (s.uploaded == 0) {
-      check_hip(hipMemcpyAsync(s.d_blob, s.h_blob, s.raw_base + raw_end * 2, hipMemcpyHostToDevice, s.stream),
+      check_hip(hipMemcpyAsync(s.d_blob, s.h_blob, s.raw_base + raw_end * 2, hipMemcpyHostToDevice, up),
                 "H2D tables + pixels");
     } else {
-      check_hip(hipMemcpyAsync(s.d_blob, s.h_blob, s.raw_base, hipMemcpyHostToDevice, s.stream), "H2D tables");
+      check_hip(hipMemcpyAsync(s.d_blob, s.h_blob, s.raw_base, hipMemcpyHostToDevice, up), "H2D tables");
       if (raw_end > s.uploaded)
         check_hip(hipMemcpyAsync(s.d_blob + s.raw_base + s.uploaded * 2, s.h_blob + s.raw_base + s.uploaded * 2,
-                                 (raw_end - s.uploaded) * 2, hipMemcpyHostToDevice, s.stream),
+                                 (raw_end - s.uploaded) * 2, hipMemcpyHostToDevice, up),
                   "H2D pixels");
     }
     s.uploaded = raw_end;
-    check_hip(hipEventRecord(s.ev1, s.stream), "event");
+    check_hip(hipEventRecord(s.ev1, up), "event");
+    if (up != s.stream) check_hip(hipStreamWaitEvent(s.stream, s.ev1, 0), "wait upload");
     auto chain = [&] {
       const auto* blob_raw = reinterpret_cast<const uint16_t*>(db + s.raw_base);
       if (separate_unpack()) {  // A/B: the standalone K0 expansion pass before the median
@@ -1190,7 +1219,7 @@ struct Engine::Impl {
     for (size_t i = 0; i < count; ++i)
       if (s.loaded[i].ok) s.live.push_back((int)i);
     // Nothing to run, but early chunks may be in flight: the next batch reuses the pinned blob.
-    if (s.live.empty() && s.upload_started) check_hip(hipStreamSynchronize(s.stream), "upload drain");
+    if (s.live.empty() && s.upload_started) check_hip(hipStreamSynchronize(s.up), "upload drain");
     StageTimes local;
     int64_t fallbacks = 0;
     if (!s.live.empty()) {
@@ -1203,7 +1232,7 @@ struct Engine::Impl {
       } catch (const std::exception& e) {
         for (int i : s.live) status[first + i] = SliceStatus{kSliceDeviceError, e.what()};
         s.live.clear();
-        if (s.upload_started) (void)hipStreamSynchronize(s.stream);  // blob is reused next batch
+        if (s.upload_started) (void)hipStreamSynchronize(s.up);  // blob is reused next batch
       }
     }
     if (cfg.export_jpeg && !s.live.empty()) {
