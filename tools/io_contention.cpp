@@ -22,7 +22,8 @@
 static double now(){return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();}
 static long long tcpu(){timespec t;clock_gettime(CLOCK_THREAD_CPUTIME_ID,&t);return t.tv_sec*1000000000LL+t.tv_nsec;}
 int main(int argc,char**argv){
-  if(argc<6){fprintf(stderr,"usage: io_contention root T nfiles reps mode(0 threads|1 procs|2 threads+unshare)\n");return 2;}
+  if(argc<6){fprintf(stderr,"usage: io_contention root T nfiles reps mode(0 threads|1 procs|2 threads+unshare) [mmap]\n");return 2;}
+  const bool use_mmap = argc > 6 && atoi(argv[6]) != 0;  // loads: mmap(MAP_POPULATE) + sum + munmap instead of pread
   const char* root=argv[1]; int T=atoi(argv[2]); int nfiles=atoi(argv[3]); int reps=atoi(argv[4]); int procs=atoi(argv[5]);
   const size_t seg=12000, rsz=131*1024;
   std::vector<uint8_t> src((size_t)nfiles*seg*2+4096); for(size_t i=0;i<src.size();++i) src[i]=(uint8_t)(i*131);
@@ -41,7 +42,11 @@ int main(int argc,char**argv){
         for(int d=0;d<nd;++d) my[d]=open((std::string(root)+"/d"+std::to_string(d)).c_str(),O_PATH|O_DIRECTORY); }
       for(int i=t;i<nfiles;i+=T){
         long long c0=tcpu();
-        int fd=openat(my[i%nd],name(i,2).c_str(),O_RDONLY); if(pread(fd,buf.data(),rsz,0)<0) abort(); close(fd);
+        int fd=openat(my[i%nd],name(i,2).c_str(),O_RDONLY);
+        if(use_mmap){ void* m=mmap(nullptr,rsz,PROT_READ,MAP_PRIVATE|MAP_POPULATE,fd,0); if(m==MAP_FAILED) abort();
+          const uint64_t* q=(const uint64_t*)m; uint64_t acc=0; for(size_t k=0;k<rsz/8;k+=8) acc+=q[k]; buf[0]=(uint8_t)acc; munmap(m,rsz); }
+        else if(pread(fd,buf.data(),rsz,0)<0) abort();
+        close(fd);
         long long c1=tcpu(); cr+=c1-c0;
         for(int k=0;k<2;++k){ const uint8_t* s=src.data()+((size_t)i*2+k)*seg;
           int f2=openat(my[i%nd],name(i,k).c_str(),O_WRONLY); iovec v[1]={{(void*)s,seg}}; if(pwritev(f2,v,1,0)<0) abort(); close(f2);}
@@ -51,6 +56,6 @@ int main(int argc,char**argv){
     if(procs==1){ std::vector<pid_t> ps; for(int t=0;t<T;++t){pid_t p=fork(); if(p==0){work(t); _exit(0);} ps.push_back(p);} for(auto p:ps) waitpid(p,nullptr,0); }
     else { std::vector<std::thread> th; for(int t=0;t<T;++t) th.emplace_back(work,t); for(auto&x:th) x.join(); }
     double dt=now()-t0;
-    printf("T=%2d %s  read %.2f us/file  write %.2f us/pair  wall %.1f ms\n",T,procs==1?"procs  ":procs==2?"unshare":"threads",shared[0].load()/1e3/nfiles,shared[1].load()/1e3/nfiles,dt*1e3);
+    printf("T=%2d %s%s  read %.2f us/file  write %.2f us/pair  wall %.1f ms\n",T,procs==1?"procs  ":procs==2?"unshare":"threads",use_mmap?"+mmap":"",shared[0].load()/1e3/nfiles,shared[1].load()/1e3/nfiles,dt*1e3);
   }
 }
