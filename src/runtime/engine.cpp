@@ -187,29 +187,24 @@ struct IoDirs {
     if (getrlimit(RLIMIT_NOFILE, &rl) == 0 && rl.rlim_cur != RLIM_INFINITY) lim = (size_t)rl.rlim_cur;
     return std::min<size_t>(256, lim / 8);
   }
-  std::vector<int> fds;
-  std::vector<std::string> paths;  // per fd index
-  uint64_t id;                     // unique per run (keys the workers' private directory fds)
+  std::vector<int> fds;  // per directory index: O_PATH fd, or -1 (full paths)
   // Per directory: 1 once a file was missing there (files are then created directly, see
   // jpeg::write_jpeg_at); 0 = try opening existing files without O_CREAT first.
   std::unique_ptr<std::atomic<uint8_t>[]> creating;
-  std::vector<int32_t> in_fd, out_fd;  // per item: fd index, -1 = fall back to the full path
+  std::vector<int32_t> in_fd, out_fd;  // per item: directory index, -1 = none (bare file name)
   std::vector<uint32_t> in_name;       // per item: offset of the file name in its path
-  IoDirs(const std::vector<WorkItem>& items) {
-    static std::atomic<uint64_t> next_id{1};
-    id = next_id.fetch_add(1, std::memory_order_relaxed);
+  // `open_fds`: false when the pool workers have private fd tables and could not use them.
+  explicit IoDirs(const std::vector<WorkItem>& items, bool open_fds = true) {
     std::unordered_map<std::string, int32_t> idx;
-    const size_t cap = max_fds();
+    const size_t cap = open_fds ? max_fds() : 0;
+    size_t opened = 0;
     auto dir_index = [&](const std::string& d) -> int32_t {
       auto it = idx.find(d);
       if (it != idx.end()) return it->second;
-      const int fd = fds.size() < cap ? ::open(d.empty() ? "/" : d.c_str(), O_PATH | O_DIRECTORY | O_CLOEXEC) : -1;
-      int32_t k = -1;
-      if (fd >= 0) {
-        k = (int32_t)fds.size();
-        fds.push_back(fd);
-        paths.push_back(d.empty() ? "/" : d);
-      }
+      const int fd = opened < cap ? ::open(d.empty() ? "/" : d.c_str(), O_PATH | O_DIRECTORY | O_CLOEXEC) : -1;
+      opened += fd >= 0;
+      const int32_t k = (int32_t)fds.size();
+      fds.push_back(fd);
       idx.emplace(d, k);
       return k;
     };
@@ -232,38 +227,16 @@ struct IoDirs {
     for (size_t k = 0; k < fds.size(); ++k) creating[k].store(0, std::memory_order_relaxed);
   }
   ~IoDirs() {
-    for (int fd : fds) ::close(fd);
+    for (int fd : fds)
+      if (fd >= 0) ::close(fd);
   }
   // fd of directory k usable on the calling thread, -1 if none (the caller then uses the full
-  // path). A worker with a private fd table opens its own O_PATH fds lazily, cached for the two most
-  // recent runs it served (runs are pipelined, so a worker alternates between two).
-  int dir_fd(int32_t k) const {
-    if (k < 0) return -1;
-    if (!tl_private_fds) return fds[(size_t)k];
-    struct Cache {
-      uint64_t id[2] = {0, 0};
-      std::vector<int> fds[2];
-      int victim = 0;
-      ~Cache() {
-        for (auto& v : fds)
-          for (int fd : v)
-            if (fd >= 0) ::close(fd);
-      }
-    };
-    static thread_local Cache c;
-    int slot = c.id[0] == id ? 0 : c.id[1] == id ? 1 : -1;
-    if (slot < 0) {
-      slot = c.victim;
-      c.victim ^= 1;
-      for (int fd : c.fds[slot])
-        if (fd >= 0) ::close(fd);
-      c.fds[slot].assign(fds.size(), -2);  // -2: not opened yet
-      c.id[slot] = id;
-    }
-    int& fd = c.fds[slot][(size_t)k];
-    if (fd == -2) fd = ::open(paths[(size_t)k].c_str(), O_PATH | O_DIRECTORY | O_CLOEXEC);
-    return fd;
-  }
+  // path). A pool worker with a private fd table cannot use these fds and takes the full path: a
+  // per-worker cache of directory fds had to be rebuilt for every run (each pass is a new run),
+  // 16 workers × ~40 directories × open + close per pass, which cost more than the path walks
+  // (loads 28–32 vs 22–23 µs per slice, profiles/r3/depth/).
+  int dir_fd(int32_t k) const { return k < 0 || tl_private_fds ? -1 : fds[(size_t)k]; }
+  size_t ndirs() const { return fds.size(); }
   IoDirs(const IoDirs&) = delete;
   IoDirs& operator=(const IoDirs&) = delete;
 };
@@ -1291,7 +1264,7 @@ struct Engine::Impl {
                 const uint8_t* seg = use_fb[cv] ? fb[cv].data() : jpeg_bytes(s, cv);
                 const size_t len = use_fb[cv] ? fb[cv].size() : (size_t)s.h_sizes[cv];
                 jpeg::write_jpeg_at(dfd, rel ? items[item].out_dir : std::string(), name, jpeg_header, seg, len,
-                                    rel ? &dirs.creating[dirs.out_fd[item]] : nullptr);
+                                    dirs.out_fd[item] >= 0 ? &dirs.creating[dirs.out_fd[item]] : nullptr);
                 bytes_out += (int64_t)(jpeg_header.size() + len + 2);
               }
             } catch (const std::exception& e) {
@@ -1461,7 +1434,7 @@ struct Engine::Impl {
     auto j = std::make_shared<Job>();
     j->t0 = now_s();
     j->items = std::move(items);
-    j->dirs = std::make_unique<IoDirs>(*j->items);
+    j->dirs = std::make_unique<IoDirs>(*j->items, !private_fds_wanted());
     j->on_start = std::move(on_start);
     j->status.resize(j->items->size());
     const size_t B = batch_cap > 0 ? std::min<size_t>((size_t)batch_cap, (size_t)cfg.batch_size) : (size_t)cfg.batch_size;

@@ -173,3 +173,17 @@ def test_private_fd_tables_do_not_hold_process_fds(native, cohort_root, tmp_path
     assert ready and os.read(r, 1) == b""  # EOF: no worker kept a duplicate of the write end
     os.close(r)
     del eng
+
+
+def test_host_only_many_queued_runs_private_fds(native, cohort_root, tmp_path, monkeypatch):
+    """More runs in flight than a worker's directory-fd cache holds (LRU eviction of whole runs):
+    every run still writes every file."""
+    monkeypatch.setenv("NM03_PRIVATE_FDS", "1")
+    eng = _engine(native, threads=4, batch_size=8, streams=3)
+    trees = [_items(native, cohort_root, str(tmp_path / f"t{k}"))[:24] for k in range(11)]
+    tickets = [eng.submit(native.WorkList(t)) for t in trees]
+    for t in tickets:
+        codes, msgs, _ = eng.wait(t)
+        assert not msgs
+    for t in trees:
+        assert len(_tree_bytes(t)) == 2 * len(t)
