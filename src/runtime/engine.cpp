@@ -158,7 +158,7 @@ struct Slot {
 // 10.0–10.6 µs in 16 processes (tools/io_contention.cpp, profiles/r3/io_contention/). Each worker
 // therefore starts with close_range(3, ~0U, CLOSE_RANGE_UNSHARE): its own table, holding only
 // stdin/out/err (no duplicates of the process's other fds, so a pipe or file the process closes is
-// not kept open by a worker). Directory fds are then per worker too (IoDirs::dir_fd).
+// not kept open by a worker). Such workers open files by full path (IoDirs::dir_fd).
 static bool private_fds_wanted() {
   static const bool on = [] {
     const char* e = std::getenv("NM03_PRIVATE_FDS");
@@ -236,7 +236,6 @@ struct IoDirs {
   // 16 workers × ~40 directories × open + close per pass, which cost more than the path walks
   // (loads 28–32 vs 22–23 µs per slice, profiles/r3/depth/).
   int dir_fd(int32_t k) const { return k < 0 || tl_private_fds ? -1 : fds[(size_t)k]; }
-  size_t ndirs() const { return fds.size(); }
   IoDirs(const IoDirs&) = delete;
   IoDirs& operator=(const IoDirs&) = delete;
 };

@@ -1,7 +1,8 @@
 #!/bin/bash
 # (gpurun; host-only engine, no GPU use) Deep pipelining diagnosis: per-run latency and stage times
 # at depth 2 / 4 with private worker fd tables (default), shared tables, and private tables without
-# worker directory fds. gpurun_out/r3dq/.
+# worker directory fds. gpurun_out/r3dq/. (Historical: NM03_WORKER_DIRFDS selected the per-worker
+# directory-fd cache this probe measured; the cache was removed, workers with private tables use full paths.)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"; O=gpurun_out/r3dq; mkdir -p $O
 export DP_ROOT=/dev/shm/r3dq_data/ DP_THREADS=16
