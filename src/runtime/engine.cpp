@@ -823,6 +823,9 @@ struct Engine::Impl {
 
   // ---- descriptor build + GPU enqueue --------------------------------------------------------
   // mode 0: export pair (original, processed); mode 1: test_pipeline (5 canvases, all planes).
+  // (seeds_*: per-thread cache of reference_seeds for build_and_run; slot threads run concurrently.)
+  static inline thread_local std::vector<Seed> seeds_cache_;
+  static inline thread_local int seeds_w_ = 0, seeds_h_ = 0;
   void build_and_run(Slot& s, int mode, StageTimes* acc) {
     const int nl = (int)s.live.size();
     uint8_t* hb = s.h_blob;
@@ -861,7 +864,14 @@ struct Engine::Impl {
       d.slope = L.slope;
       d.intercept = L.intercept;
       d.f32_off = raw_off;
-      auto sv = reference_seeds(L.w, L.h);
+      // Seeds depend on the slice size only: reuse the last size's list (a batch is nearly always
+      // one size) instead of building a vector per slice on the slot thread.
+      if (L.w != seeds_w_ || L.h != seeds_h_) {
+        seeds_cache_ = reference_seeds(L.w, L.h);
+        seeds_w_ = L.w;
+        seeds_h_ = L.h;
+      }
+      const auto& sv = seeds_cache_;
       d.seed_off = (uint32_t)nseed;
       d.seed_count = (uint16_t)std::min<size_t>(sv.size(), kMaxSeeds);
       for (int k = 0; k < d.seed_count; ++k) seeds[nseed++] = SeedXY{(int16_t)sv[k].x, (int16_t)sv[k].y};
