@@ -74,6 +74,7 @@ class SliceFile {
   ~SliceFile();
   SliceFile(const SliceFile&) = delete;
   SliceFile& operator=(const SliceFile&) = delete;
+  // File size; for kStaged known only after header() (the whole-file read replaces the fstat).
   size_t size() const { return size_; }
   // kMapped only: map the file at `addr` (MAP_FIXED inside a caller-reserved region of `cap`
   // bytes) instead of a fresh address, and leave it mapped: the caller unmaps the whole region in
@@ -95,6 +96,8 @@ class SliceFile {
 
  private:
   void pread_all(void* dst, size_t n, size_t off);
+  void stat_size();
+  bool size_known_ = false;
   const uint8_t* data() const { return map_ ? map_ : buf_->data(); }
   std::string path_;
   const uint8_t* map_ = nullptr;  // kMapped: the whole file

@@ -340,13 +340,19 @@ SliceFile::SliceFile(int dirfd, const char* name, const std::string& path, ReadM
     : path_(path), mode_(mode), prefix_(prefix < 1024 ? 1024 : prefix) {
   fd_ = ::openat(dirfd, name, O_RDONLY | O_CLOEXEC);
   if (fd_ < 0) throw SliceError("Cannot open file: " + path + " (" + std::strerror(errno) + ")");
+  if (mode_ == ReadMode::kStaged) return;  // size from the whole-file read (header): no fstat
+  stat_size();
+}
+
+void SliceFile::stat_size() {
   struct stat st;
   if (fstat(fd_, &st) != 0) {
     ::close(fd_);
     fd_ = -1;
-    throw SliceError("Cannot stat file: " + path);
+    throw SliceError("Cannot stat file: " + path_);
   }
   size_ = (size_t)st.st_size;
+  size_known_ = true;
 }
 
 SliceFile::~SliceFile() {
@@ -366,6 +372,29 @@ void SliceFile::pread_all(void* dst, size_t n, size_t off) {
 
 const Header& SliceFile::header(std::vector<uint8_t>& buf) {
   buf_ = &buf;
+  if (mode_ == ReadMode::kStaged && !size_known_) {
+    // One read of up to the buffer's size (≥ 256 KiB): a short read of a regular file is its end
+    // (pool threads block signals, so no read is cut short by one); a full buffer may mean more,
+    // then the size comes from fstat.
+    if (buf.size() < (256u << 10)) buf.resize(256u << 10);
+    size_t got = 0;
+    for (;;) {
+      const ssize_t r = ::pread(fd_, buf.data() + got, buf.size() - got, (off_t)got);
+      if (r < 0 && errno == EINTR) continue;
+      if (r < 0) throw SliceError("Read error on file: " + path_);
+      got += (size_t)r;
+      if (got < buf.size() || r == 0) break;
+      stat_size();
+      if (size_ <= got) break;
+      buf.resize(size_);
+    }
+    size_ = got;
+    size_known_ = true;
+    have_ = size_;
+    h_ = parse(buf.data(), size_);
+    whole_ = true;
+    return h_;
+  }
   if (mode_ == ReadMode::kMapped && size_ > 0) {
     const bool fixed = map_at_ && size_ <= map_cap_;
     void* m = ::mmap(fixed ? map_at_ : nullptr, size_, PROT_READ, MAP_PRIVATE | MAP_POPULATE | (fixed ? MAP_FIXED : 0),

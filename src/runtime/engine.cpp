@@ -3,6 +3,7 @@
 
 #include <hip/hip_runtime_api.h>
 #include <fcntl.h>
+#include <signal.h>
 #include <sys/mman.h>
 #include <sys/prctl.h>
 #include <sys/resource.h>
@@ -377,6 +378,11 @@ struct Engine::Impl {
     pool = std::make_unique<ThreadPool>(cfg.threads, [this](int i) {
       place.bind_worker(i, cfg.threads);
       make_fd_table_private();
+      // Signals go to other threads: a pool worker's reads are never cut short (SliceFile's
+      // staged read takes a short read as the end of the file).
+      sigset_t all;
+      sigfillset(&all);
+      pthread_sigmask(SIG_BLOCK, &all, nullptr);
     });
     const double t2 = now_s();
     // Slot 0 is built here (its failure fails the constructor); the others are built by their own
@@ -706,8 +712,8 @@ struct Engine::Impl {
       if (fault_plan().corrupt_dicom == (int64_t)item) throw SliceError("injected fault: corrupt DICOM data");
       dicom::SliceFile file(dirfd, name, path, read_mode_, read_prefix_);
       if (s.map_region) file.map_at(s.map_region + (size_t)i * s.map_stride, s.map_stride);
-      const size_t n = file.size();
       const dicom::Header& h = file.header(buf);
+      const size_t n = file.size();  // after header(): staged reads learn the size from the read
       const int md = cfg.pipe.min_dim;
       if (md > 0 && (h.cols < md || h.rows < md)) {
         st.code = kSliceTooSmall;
