@@ -175,6 +175,47 @@ TEST(slice_file_modes_agree) {
   }
 }
 
+TEST(slice_file_staged_sizes) {
+  // Staged reads take the file size from the whole-file read (no fstat): files below, at and above
+  // the 256 KiB first read, with a caller buffer that starts empty, small and already large.
+  using namespace nm03::dicom;
+  for (int rows : {64, 360, 512}) {  // 8 KiB, ≈253 KiB (just below 256 KiB with the header), 512 KiB
+    const int cols = rows == 360 ? 360 : rows;
+    auto px = ramp(rows * cols, 4242 + rows);
+    WriteSpec ws;
+    ws.rows = rows;
+    ws.cols = cols;
+    ws.pixels = px.data();
+    const std::string path = tmpdir() + "/staged_" + std::to_string(rows) + ".dcm";
+    write_file(path, ws);
+    for (size_t start : {(size_t)0, (size_t)1000, (size_t)(1u << 20)}) {
+      std::vector<uint8_t> scratch(start);
+      SliceFile f(path, ReadMode::kStaged, 0);
+      const Header& h = f.header(scratch);
+      CHECK(h.rows == rows && h.cols == cols);
+      CHECK(f.size() > (size_t)rows * cols * 2);
+      const uint16_t* sm = f.staged_samples();
+      CHECK(sm != nullptr && std::equal(px.begin(), px.end(), sm));
+    }
+  }
+}
+
+TEST(duplicate_device_detection) {
+  using nm03::RankDevice;
+  auto mk = [](const char* bus) {
+    RankDevice d;
+    d.bus_id = bus;
+    return d;
+  };
+  CHECK(nm03::duplicate_device({mk("0000:0d:00.0"), mk("0000:26:00.0"), mk("0000:f1:00.0")}).empty());
+  const std::string m = nm03::duplicate_device({mk("0000:0d:00.0"), mk("0000:26:00.0"), mk("0000:0d:00.0")});
+  CHECK(m.find("ranks 0 and 2") != std::string::npos && m.find("0000:0d:00.0") != std::string::npos);
+  CHECK(nm03::duplicate_device({mk(""), mk("")}).empty());  // no GPU: nothing to compare
+  const std::string j = nm03::rank_devices_json({mk("0000:0d:00.0"), mk("0000:26:00.0")});
+  CHECK(j.find("\"bus_id\": [\"0000:0d:00.0\", \"0000:26:00.0\"]") != std::string::npos ||
+        j.find("\"bus_id\":[\"0000:0d:00.0\",\"0000:26:00.0\"]") != std::string::npos);
+}
+
 TEST(stream_copy_edges) {
   std::vector<uint8_t> src(5000), dst(5100);
   for (size_t i = 0; i < src.size(); ++i) src[i] = (uint8_t)(i * 7 + 1);
