@@ -500,7 +500,9 @@ def run_rank(args):
         if wiped is not None:
             rec["config"]["wipe_each_pass"] = {"value": round(wiped["value"], 2),
                                                "ms_per_step": round(wiped["ms_per_step"], 3),
-                                               "steps": args.wipe_passes}
+                                               "steps": args.wipe_passes,
+                                               "rank0_process_cpu_ms_per_step": wiped["rank0_process_cpu_ms_per_step"],
+                                               "rank0_stage_s": wiped["rank0_stage_s"]}
         if secondary is not None:
             rec["config"][other] = {k: (round(v, 3) if isinstance(v, float) else v) for k, v in secondary.items()
                                     if k in ("value", "ms_per_step", "global_batch", "per_rank", "note",
