@@ -92,6 +92,8 @@ struct Slot {
   size_t max_medt = 0, max_shpt = 0;
   uint8_t* h_blob = nullptr;
   uint8_t* d_hblob = nullptr;  // device view of h_blob (shader uploads of small batches), or null
+  uint8_t* h_single = nullptr;  // run_single's pinned read-back area (allocated on first use)
+  size_t single_bytes = 0;
   uint8_t* d_blob = nullptr;
   uint16_t* d_raw_x = nullptr;  // expanded 16-bit samples of the batch (K0 output, every kernel's input)
   uint16_t* d_med = nullptr;
@@ -252,6 +254,7 @@ void hip_free_all(Slot& s) {
   if (s.h_blob) (void)hipHostFree(s.h_blob);
   if (s.h_out) (void)hipHostFree(s.h_out);
   if (s.h_sizes) (void)hipHostFree(s.h_sizes);
+  if (s.h_single) (void)hipHostFree(s.h_single);
   for (void* p : {(void*)s.d_blob, (void*)s.d_raw_x, (void*)s.d_med, (void*)s.d_tile_mm, (void*)s.d_f32, (void*)s.d_bits, (void*)s.d_srg_scratch, (void*)s.d_canvas,
                   (void*)s.jw.look, (void*)s.jw.ticket, (void*)s.jw.spill, (void*)s.d_jraw,
                   (void*)s.d_jcomp, (void*)s.d_jsizes})
@@ -1521,18 +1524,53 @@ struct Engine::Impl {
     r.w = in.w;
     r.h = in.h;
     const size_t npix = (size_t)in.w * in.h;
-    r.median_keys.resize(npix);
-    r.sharpened.resize(npix);
-    check_hip(hipMemcpy(r.median_keys.data(), s.d_med, npix * 2, hipMemcpyDeviceToHost), "D2H median");
-    check_hip(hipMemcpy(r.sharpened.data(), s.d_f32, npix * 4, hipMemcpyDeviceToHost), "D2H sharpened");
     const int wpr = (in.w + 63) / 64;
-    std::vector<uint64_t> words((size_t)in.h * wpr);
-    auto unpack = [&](Plane p, std::vector<uint8_t>& dst) {
-      check_hip(hipMemcpy(words.data(), s.d_bits + p * s.plane_words, words.size() * 8, hipMemcpyDeviceToHost),
+    const size_t pw = (size_t)in.h * wpr;  // words of one plane of this slice
+    const int cw = cfg.render.out_width, ch = cfg.render.out_height;
+    const size_t cvb = (size_t)cw * ch;
+    // Every read-back as an async copy into one pinned area and a single synchronisation (was 14
+    // synchronous copies into pageable vectors, each staged by the runtime).
+    auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+    const size_t o_med = 0, o_f32 = al(npix * 2), o_bits = o_f32 + al(npix * 4),
+                 o_cv = o_bits + al(kNumPlanes * pw * 8), need = o_cv + (size_t)s.ncanvas * cvb;
+    if (s.single_bytes < need) {
+      if (s.h_single) (void)hipHostFree(s.h_single);
+      s.h_single = nullptr;
+      s.single_bytes = 0;
+      check_hip(hipHostMalloc((void**)&s.h_single, need, hipHostMallocDefault), "hipHostMalloc single");
+      s.single_bytes = need;
+    }
+    uint8_t* hs = s.h_single;
+    check_hip(hipMemcpyAsync(hs + o_med, s.d_med, npix * 2, hipMemcpyDeviceToHost, s.stream), "D2H median");
+    check_hip(hipMemcpyAsync(hs + o_f32, s.d_f32, npix * 4, hipMemcpyDeviceToHost, s.stream), "D2H sharpened");
+    for (int p = 0; p < kNumPlanes; ++p)
+      check_hip(hipMemcpyAsync(hs + o_bits + (size_t)p * pw * 8, s.d_bits + (size_t)p * s.plane_words, pw * 8,
+                               hipMemcpyDeviceToHost, s.stream),
                 "D2H plane");
-      dst.assign(npix, 0);
-      for (int y = 0; y < in.h; ++y)
-        for (int x = 0; x < in.w; ++x) dst[(size_t)y * in.w + x] = (words[(size_t)y * wpr + x / 64] >> (x % 64)) & 1;
+    if (s.ncanvas > 0)
+      check_hip(hipMemcpyAsync(hs + o_cv, s.d_canvas, (size_t)s.ncanvas * cvb, hipMemcpyDeviceToHost, s.stream),
+                "D2H canvases");
+    check_hip(hipStreamSynchronize(s.stream), "single read-back");
+    r.median_keys.assign(reinterpret_cast<const uint16_t*>(hs + o_med), reinterpret_cast<const uint16_t*>(hs + o_med) + npix);
+    r.sharpened.assign(reinterpret_cast<const float*>(hs + o_f32), reinterpret_cast<const float*>(hs + o_f32) + npix);
+    // Bits → bytes eight at a time (x86 little-endian: byte i of the table entry is bit i).
+    static const auto expand = [] {
+      std::array<uint64_t, 256> t{};
+      for (int v = 0; v < 256; ++v)
+        for (int i = 0; i < 8; ++i) t[v] |= (uint64_t)((v >> i) & 1) << (8 * i);
+      return t;
+    }();
+    auto unpack = [&](Plane p, std::vector<uint8_t>& dst) {
+      const uint64_t* words = reinterpret_cast<const uint64_t*>(hs + o_bits + (size_t)p * pw * 8);
+      dst.resize(npix + 8);
+      for (int y = 0; y < in.h; ++y) {
+        uint8_t* row = dst.data() + (size_t)y * in.w;
+        for (int x = 0; x < in.w; x += 8) {
+          const uint64_t v = expand[(words[(size_t)y * wpr + x / 64] >> (x % 64)) & 0xFF];
+          std::memcpy(row + x, &v, 8);  // the row's last group may spill into the next row: rewritten there
+        }
+      }
+      dst.resize(npix);
     };
     unpack(kPBand, r.band);
     unpack(kPRegion, r.region);
@@ -1541,11 +1579,8 @@ struct Engine::Impl {
     unpack(kPBorderR, r.border_region);
     unpack(kPBorderE, r.border_eroded);
     unpack(kPBorderD, r.border_dilated);
-    const int cw = cfg.render.out_width, ch = cfg.render.out_height;
     for (int k = 0; k < s.ncanvas; ++k) {
-      std::vector<uint8_t> cv((size_t)cw * ch);
-      check_hip(hipMemcpy(cv.data(), s.d_canvas + (size_t)k * cw * ch, cv.size(), hipMemcpyDeviceToHost), "D2H canvas");
-      r.canvases.push_back(std::move(cv));
+      r.canvases.emplace_back(hs + o_cv + (size_t)k * cvb, hs + o_cv + (size_t)(k + 1) * cvb);
       std::vector<uint8_t> fb;
       const bool gpu_ok = jpeg_segment(s, k, fb, nullptr);
       std::vector<uint8_t> f = jpeg_header;
