@@ -524,8 +524,15 @@ struct Engine::Impl {
       check_hip(hipEventCreate(&s.ev0), "hipEventCreate");
       check_hip(hipEventCreate(&s.ev1), "hipEventCreate");
       // Batch completion is waited on by the slot thread (wait_batch).
-      const bool spin = wait_mode() == WaitMode::kSpin;
-      check_hip(hipEventCreateWithFlags(&s.ev2, spin ? hipEventDefault : hipEventBlockingSync), "hipEventCreate");
+      // Only the blocking wait mode sleeps in hipEventSynchronize and needs a blocking-sync event;
+      // the default polling wait queries it (NM03_EV2_BLOCKING=1 restores the blocking-sync event for
+      // polling too: A/B of the runtime's interrupt handling cost).
+      static const bool ev2_blocking = [] {
+        const char* e = std::getenv("NM03_EV2_BLOCKING");
+        return e && *e == '1';
+      }();
+      const bool blocking = wait_mode() == WaitMode::kBlock || (wait_mode() == WaitMode::kPoll && ev2_blocking);
+      check_hip(hipEventCreateWithFlags(&s.ev2, blocking ? hipEventBlockingSync : hipEventDefault), "hipEventCreate");
       check_hip(hipHostMalloc((void**)&s.h_blob, s.blob_bytes, hipHostMallocDefault), "hipHostMalloc blob");
       if (hipHostGetDevicePointer((void**)&s.d_hblob, s.h_blob, 0) != hipSuccess) {
         (void)hipGetLastError();
