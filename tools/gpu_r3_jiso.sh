@@ -7,8 +7,8 @@ timeout -k 10 300 python -u -m pytest tests/test_gpu.py -x -q --timeout 120 --ti
   -k "jpeg_kernel" > $O/pytest.log 2>&1 || exit 31
 D=/tmp/r3ji_data
 build/bin/nm03_synth --data-root $D/ --threads 16 > /dev/null || exit 41
-for rep in 1; do
-  for v in 1 16 2; do
+for rep in 1 2; do
+  for v in 0 17; do
     NM03_JPEG_DBG=$v timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $O/d${v}_$rep -o run \
       -- build/bin/nm03_bench --config cohort --data-root $D/ --steps 4 --warmup 1 --streams 1 --batch-size 96 ${EXTRA} \
       > $O/d${v}_$rep.log 2>&1 || exit 42
