@@ -146,6 +146,7 @@ class TaskGroup {
     {
       std::lock_guard<std::mutex> g(m_);
       ++pending_;
+      pending_a_.store(pending_, std::memory_order_release);
     }
     pool_.submit(
         [this, f = std::move(f)] {
@@ -166,6 +167,7 @@ class TaskGroup {
     {
       std::lock_guard<std::mutex> g(m_);
       pending_ += (size_t)runners;
+      pending_a_.store(pending_, std::memory_order_release);
     }
     pool_.submit_n(
         runners,
@@ -200,6 +202,7 @@ class TaskGroup {
     {
       std::lock_guard<std::mutex> g(m_);
       pending_ += (size_t)runners;
+      pending_a_.store(pending_, std::memory_order_release);
     }
     pool_.submit_n(
         runners,
@@ -217,7 +220,19 @@ class TaskGroup {
         },
         prio);
   }
-  void wait() {
+  // With spin_us > 0, spins that long on the pending count before sleeping: the waiter then
+  // continues without a wake-up (NM03_WAIT_SPIN_US overrides).
+  void wait(int spin_us = 0) {
+    static const int env = [] {
+      const char* e = std::getenv("NM03_WAIT_SPIN_US");
+      return e && *e ? std::max(0, std::atoi(e)) : -1;
+    }();
+    const int spin = env >= 0 ? env : spin_us;
+    if (spin > 0 && pending_a_.load(std::memory_order_acquire) != 0) {
+      const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(spin);
+      while (pending_a_.load(std::memory_order_acquire) != 0 && std::chrono::steady_clock::now() < until)
+        __builtin_ia32_pause();
+    }
     std::unique_lock<std::mutex> g(m_);
     cv_.wait(g, [this] { return pending_ == 0; });
   }
@@ -238,12 +253,14 @@ class TaskGroup {
   void done(size_t k) {
     std::lock_guard<std::mutex> g(m_);
     pending_ -= k;
+    pending_a_.store(pending_, std::memory_order_release);
     if (pending_ == 0) cv_.notify_all();
   }
   ThreadPool& pool_;
   std::mutex m_;
   std::condition_variable cv_;
   size_t pending_ = 0;
+  std::atomic<size_t> pending_a_{0};  // pending_, readable without the lock (wait's spin phase)
 };
 
 }  // namespace nm03

@@ -1136,6 +1136,12 @@ struct Engine::Impl {
     return false;
   }
 
+  // A slot thread waiting for a small batch's loads or exports spins up to 200 µs before sleeping:
+  // such batches are latency-bound (a strong-scaling shard cut into ⌈shard / streams⌉ batches), and
+  // the wake-up is on their critical path. Full batches sleep at once (the spin would take CPU the
+  // pool needs: 96-slice batches measured 374–388k with it vs 379–401k without, profiles/r3/wait_spin/).
+  static int small_batch_spin(size_t count) { return count <= 16 ? 200 : 0; }
+
   // `batch`: index within its run (fault injection); `prio`: engine-wide batch sequence number,
   // the host-pool priority (earlier batches first, also across queued runs).
   void process_batch(Slot& s, const std::vector<WorkItem>& items, const IoDirs& dirs, size_t batch, uint64_t prio,
@@ -1205,7 +1211,7 @@ struct Engine::Impl {
           upload_error = e.what();
         }
       }
-      tg.wait();
+      tg.wait(small_batch_spin(count));
     }
     if (s.map_region) {
       // One unmap for the batch's file mappings (they were only read by the loads above).
@@ -1298,7 +1304,7 @@ struct Engine::Impl {
             write_ns += (int64_t)((now_s() - t0) * 1e9);
           },
           2 * prio + 1, &write_cpu_ns);
-      tg.wait();
+      tg.wait(small_batch_spin(count));
     }
     std::lock_guard<std::mutex> g(acc_m);
     acc.load_s += load_ns.load() * 1e-9;
