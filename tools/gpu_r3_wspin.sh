@@ -5,7 +5,7 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT"; export TMPDIR=/tmp; O=gpurun_out/r3ws; mkdir -p $O
 for rep in 1 2 3 4; do
   for v in def 0; do
-    E=""; [ "$v" = "0" ] && E="NM03_WAIT_SPIN_US=0"; env $E timeout -k 10 300 python3 bench.py --steps 50 --warmup 3 --wipe-passes 0 --single-passes 10 > $O/w${v}_$rep.log 2>&1 || exit 40
+    E="NM03_X=1"; [ "$v" = "0" ] && E="NM03_WAIT_SPIN_US=0"; env $E timeout -k 10 300 python3 bench.py --steps 50 --warmup 3 --wipe-passes 0 --single-passes 10 > $O/w${v}_$rep.log 2>&1 || exit 40
     python3 - $O/w${v}_$rep.log wspin$v >> $O/summary.txt <<'PY'
 import json, sys
 for l in open(sys.argv[1]):
