@@ -1386,6 +1386,14 @@ struct Engine::Impl {
   std::mutex job_m, single_m;
   std::condition_variable job_cv, done_cv;
   std::deque<std::shared_ptr<Job>> queue;  // runs with unclaimed batches, oldest first
+  std::atomic<size_t> queued_jobs_{0};      // queue.size() for the idle slots' spin (no lock)
+  static int slot_spin_us() {
+    static const int us = [] {
+      const char* e = std::getenv("NM03_SLOT_SPIN_US");
+      return e && *e ? std::max(0, std::atoi(e)) : 500;
+    }();
+    return us;
+  }
   uint64_t seq_next = 0;
   size_t inflight = 0;  // submitted runs not finished yet
   bool quit = false;
@@ -1435,6 +1443,13 @@ struct Engine::Impl {
     for (;;) {
       std::shared_ptr<Job> j;
       size_t b;
+      // An idle slot spins up to NM03_SLOT_SPIN_US (default 500) for the next run before sleeping:
+      // +2.5-3% headline in 6/8 A/B pairs (profiles/r3/slot_spin), single pass unchanged.
+      if (const int us = slot_spin_us(); us > 0 && queued_jobs_.load(std::memory_order_acquire) == 0) {
+        const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(us);
+        while (queued_jobs_.load(std::memory_order_acquire) == 0 && std::chrono::steady_clock::now() < until)
+          __builtin_ia32_pause();
+      }
       {
         std::unique_lock<std::mutex> g(job_m);
         job_cv.wait(g, [&] { return quit || !queue.empty(); });
@@ -1442,6 +1457,7 @@ struct Engine::Impl {
         j = queue.front();
         b = j->next++;
         if (j->next == j->batches.size()) queue.pop_front();
+        queued_jobs_.store(queue.size(), std::memory_order_release);
       }
       const int64_t c0 = thread_cpu_ns();
       try {
@@ -1478,6 +1494,7 @@ struct Engine::Impl {
       seq_next += j->batches.size();
       ++inflight;
       if (!j->batches.empty()) queue.push_back(j);
+      queued_jobs_.store(queue.size(), std::memory_order_release);
     }
     if (j->batches.empty())
       finish(*j);
