@@ -98,7 +98,7 @@ def parse_args(argv=None):
                     help="host I/O threads per rank (0 = the rank's CPU partition and budget share, ≤16)")
     ap.add_argument("--single-pass-cap", type=int, default=0,
                     help="batch cap of the capped single passes (0 = ceil(shard / streams))")
-    ap.add_argument("--single-passes", type=int, default=10,
+    ap.add_argument("--single-passes", type=int, default=100,
                     help="also time this many single strong-scaling passes (one cohort sharded over the "
                          "ranks, nothing else in flight; config.strong.single_pass_ms; 0 = skip)")
     ap.add_argument("--comm", choices=("auto", "rccl", "host"), default=os.environ.get("NM03_COMM", "auto"))

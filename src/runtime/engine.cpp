@@ -690,6 +690,24 @@ struct Engine::Impl {
       const char* e = std::getenv("NM03_EVENT_EMA");
       return e && std::string(e) == "batch";
     }();
+    // A small batch (≤ 16 slices: a strong-scaling shard's, latency-bound) spin-polls its event for
+    // up to 1 ms instead of sleeping through the slot's recent per-slice mean: that mean comes from
+    // full, queued batches, and scaled to 15 slices it overslept completed batches by 80–190 µs in
+    // the single-pass trace (profiles/r3/small_upload/hip_trace_inline.txt). NM03_SMALL_POLL=0: A/B.
+    static const bool small_poll = [] {
+      const char* e = std::getenv("NM03_SMALL_POLL");
+      return !(e && *e == '0');
+    }();
+    if (small_poll && nslices <= 16) {
+      const double until = t_enq + 1e-3;
+      for (;;) {
+        const hipError_t e = hipEventQuery(ev);
+        if (e == hipSuccess) return;
+        if (e != hipErrorNotReady) check_hip(e, "batch sync");
+        if (now_s() > until) break;
+        for (int k = 0; k < 32; ++k) __builtin_ia32_pause();
+      }
+    }
     const double scale = per_batch ? 1.0 : (double)std::max(1, nslices);
     // Sleep through most of the batch's expected time (0.8 × the recent mean), in chunks of at
     // most 250 µs with an event check between them, then poll. One long sleep would feed itself:
@@ -985,8 +1003,9 @@ struct Engine::Impl {
     // go as one copy — one SDMA command and one completion on the batch's critical path, not two.
     const size_t raw_end = s.raw_used.load();
     const bool shader = s.uploaded == 0 && s.d_hblob && s.raw_base + raw_end * 2 <= shader_upload_bytes_;
-    hipStream_t up = shader ? s.stream : s.up;
-    if (!s.upload_started) check_hip(hipEventRecord(s.ev0, up), "event");
+    const bool inline_up = !shader && s.uploaded == 0 && !s.upload_started && nl <= 16 && small_inline_upload();
+    hipStream_t up = shader || inline_up ? s.stream : s.up;
+    if (!s.upload_started && !inline_up) check_hip(hipEventRecord(s.ev0, up), "event");
     if (shader) {
       launch_copy_from_host(s.d_hblob, s.d_blob, s.raw_base + raw_end * 2, s.stream);  // small batch: no SDMA
     } else if (s.uploaded == 0) {
@@ -1000,7 +1019,7 @@ struct Engine::Impl {
                   "H2D pixels");
     }
     s.uploaded = raw_end;
-    check_hip(hipEventRecord(s.ev1, up), "event");
+    if (!inline_up) check_hip(hipEventRecord(s.ev1, up), "event");
     if (up != s.stream) check_hip(hipStreamWaitEvent(s.stream, s.ev1, 0), "wait upload");
     auto chain = [&] {
       const auto* blob_raw = reinterpret_cast<const uint16_t*>(db + s.raw_base);
@@ -1077,7 +1096,7 @@ struct Engine::Impl {
     check_hip(hipEventRecord(s.ev2, s.stream), "event");
     wait_batch(s, s.ev2, t_enq, nl);
     if (jpeg_d2h_ && ncanv > 0) finish_jpeg_d2h(s, ncanv);
-    if (acc) {
+    if (acc && !inline_up) {  // an inline small upload records no split events
       float a = 0, b = 0;
       (void)hipEventElapsedTime(&a, s.ev0, s.ev1);
       (void)hipEventElapsedTime(&b, s.ev1, s.ev2);
@@ -1141,6 +1160,18 @@ struct Engine::Impl {
   // the wake-up is on their critical path. Full batches sleep at once (the spin would take CPU the
   // pool needs: 96-slice batches measured 374–388k with it vs 379–401k without, profiles/r3/wait_spin/).
   static int small_batch_spin(size_t count) { return count <= 16 ? 200 : 0; }
+  // A small batch (≤ 16 slices) with nothing uploaded early copies on its own stream, without the
+  // upload stream's events: on the shared stream every copy sat ≈ 20 µs behind the previous one
+  // (SDMA → event marker → SDMA hand-offs) and its first kernel ≈ 16–20 µs behind the copy (the
+  // cross-stream wait). 58-slice single pass 0.373–0.399 vs 0.435–0.447 ms median over 200 passes
+  // in 3 of 3 rounds (profiles/r3/small_upload/). NM03_SMALL_UPLOAD=shared restores the old path.
+  static bool small_inline_upload() {
+    static const bool on = [] {
+      const char* e = std::getenv("NM03_SMALL_UPLOAD");
+      return !(e && std::string(e) == "shared");
+    }();
+    return on;
+  }
 
   // `batch`: index within its run (fault injection); `prio`: engine-wide batch sequence number,
   // the host-pool priority (earlier batches first, also across queued runs).
