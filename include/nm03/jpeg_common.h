@@ -198,12 +198,70 @@ NM03_HD void fdct_islow_pass2(int32_t* d) {
     p[8] = NM03_DESCALE(t7 + z1 + z4, CB + P1);
   }
 }
-#undef NM03_DESCALE
-
 NM03_HD void fdct_islow(int32_t* d) {
   fdct_islow_pass1(d);
   fdct_islow_pass2(d);
 }
+
+// The same islow FDCT in dot-product form. With the z-terms distributed out, each odd output is a
+// fixed integer combination of t4..t7 and the even pair (2, 6) one of t12, t13 — the very same
+// integers (distributivity; no intermediate leaves int32). Every butterfly term fits int16 (pass 1:
+// |t| ≤ 510 for 8-bit samples; pass 2: |t| ≤ 16320, pass-1 outputs being ≤ 8160) and so does every
+// combined constant (≤ 11363), so on gfx950 an output is one or two v_dot2_i32_i16 (16-bit pairs,
+// 32-bit accumulate, the rounding bias as the accumulator seed) instead of the multiply/add chain.
+// Host builds evaluate the identical sums with plain int32 arithmetic (tests/native: bit-equal to
+// fdct_islow over random and extreme blocks).
+NM03_HD int32_t fdct_dot2(int32_t a, int32_t b, int32_t ca, int32_t cb, int32_t acc) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  typedef short s2 __attribute__((ext_vector_type(2)));
+  const s2 x = {(short)a, (short)b}, c = {(short)ca, (short)cb};
+  return __builtin_amdgcn_sdot2(x, c, acc, false);
+#else
+  return a * ca + b * cb + acc;
+#endif
+}
+namespace fdct_dot {
+constexpr int32_t kE2[2] = {kF0_541, kF0_541 + kF0_765}, kE6[2] = {kF0_541 - kF1_847, kF0_541};
+// Odd outputs 1, 3, 5, 7 as coefficients of (t4, t5, t6, t7).
+constexpr int32_t kO1[4] = {kF1_175 - kF0_899, kF1_175 - kF0_390, kF1_175, kF1_501 - kF0_899 - kF0_390 + kF1_175};
+constexpr int32_t kO3[4] = {kF1_175 - kF1_961, kF1_175 - kF2_562, kF3_072 - kF2_562 - kF1_961 + kF1_175, kF1_175};
+constexpr int32_t kO5[4] = {kF1_175, kF2_053 - kF2_562 - kF0_390 + kF1_175, kF1_175 - kF2_562, kF1_175 - kF0_390};
+constexpr int32_t kO7[4] = {kF0_298 - kF0_899 - kF1_961 + kF1_175, kF1_175, kF1_175 - kF1_961, kF1_175 - kF0_899};
+static_assert(kO7[0] == -11363 && kO1[3] == 11363 && kE6[0] == -10704, "combined FDCT constants");
+
+// One 1-D transform of p[0], p[s], ..., p[7s]; pass 2 descales the even outputs by P1 and the
+// rotated ones by CB + P1, pass 1 scales the even ones up by P1 and the rotated ones down by CB − P1.
+template <bool kPass2>
+NM03_HD void fdct_1d(int32_t* p, int s) {
+  constexpr int sh = kPass2 ? kFdctCB + kFdctP1 : kFdctCB - kFdctP1;
+  constexpr int32_t R = 1 << (sh - 1);
+  const int32_t t0 = p[0] + p[7 * s], t7 = p[0] - p[7 * s];
+  const int32_t t1 = p[s] + p[6 * s], t6 = p[s] - p[6 * s];
+  const int32_t t2 = p[2 * s] + p[5 * s], t5 = p[2 * s] - p[5 * s];
+  const int32_t t3 = p[3 * s] + p[4 * s], t4 = p[3 * s] - p[4 * s];
+  const int32_t t10 = t0 + t3, t13 = t0 - t3, t11 = t1 + t2, t12 = t1 - t2;
+  if (kPass2) {
+    p[0] = NM03_DESCALE(t10 + t11, kFdctP1);
+    p[4 * s] = NM03_DESCALE(t10 - t11, kFdctP1);
+  } else {
+    p[0] = (t10 + t11) * (1 << kFdctP1);
+    p[4 * s] = (t10 - t11) * (1 << kFdctP1);
+  }
+  p[2 * s] = fdct_dot2(t12, t13, kE2[0], kE2[1], R) >> sh;
+  p[6 * s] = fdct_dot2(t12, t13, kE6[0], kE6[1], R) >> sh;
+  p[1 * s] = fdct_dot2(t6, t7, kO1[2], kO1[3], fdct_dot2(t4, t5, kO1[0], kO1[1], R)) >> sh;
+  p[3 * s] = fdct_dot2(t6, t7, kO3[2], kO3[3], fdct_dot2(t4, t5, kO3[0], kO3[1], R)) >> sh;
+  p[5 * s] = fdct_dot2(t6, t7, kO5[2], kO5[3], fdct_dot2(t4, t5, kO5[0], kO5[1], R)) >> sh;
+  p[7 * s] = fdct_dot2(t6, t7, kO7[2], kO7[3], fdct_dot2(t4, t5, kO7[0], kO7[1], R)) >> sh;
+}
+}  // namespace fdct_dot
+
+// `d` holds 64 unshifted 8-bit samples (0..255; the int16 bounds above assume it).
+NM03_HD void fdct_islow_dot(int32_t* d) {
+  for (int r = 0; r < 8; ++r) fdct_dot::fdct_1d<false>(d + 8 * r, 1);
+  for (int c = 0; c < 8; ++c) fdct_dot::fdct_1d<true>(d + c, 8);
+}
+#undef NM03_DESCALE
 
 // Rounding division by the islow divisor (8·Q), sign-symmetric (libjpeg forward_DCT).
 NM03_HD int16_t quantize(int32_t v, int32_t divisor) {

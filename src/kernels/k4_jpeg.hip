@@ -147,7 +147,10 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(kOcc)))
                                                              const JpegDesc* __restrict__ jd, int ncanvas, int out_w,
                                                              int out_h, QuantRecip q, JpegWork w, JpegRenderSrc rs,
                                                              uint8_t* __restrict__ out, int32_t* __restrict__ out_sizes,
-                                                             int dbg) {
+                                                             int dbgw) {
+  // dbgw: profiling variant in the low byte (NM03_JPEG_DBG), bit 8 = flat-wave path off (NM03_JPEG_FLAT=0).
+  const int dbg = dbgw & 0xFF;
+  const bool flat_ok = !(dbgw & 0x100);
   __shared__ uint32_t actab[256];
   __shared__ uint32_t dctab[16];
   __shared__ int32_t sdc[kJpegWG];
@@ -306,6 +309,11 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(kOcc)))
     const int mcu = b >> 2, sub = b & 3;
     const int bx = 2 * (mcu % mcux) + (sub & 1), by = 2 * (mcu / mcux) + (sub >> 1);
     int32_t blk[64];
+    // Label images are mostly background: when every block of the wave is one flat colour (76% of
+    // the phantom cohort's label waves, 97.5% of its blocks) the islow FDCT of a constant block is
+    // exactly DC = 64·x with every AC coefficient 0 (all butterfly differences vanish), so the
+    // wave skips the FDCT, the quantisation and the zig-zag walk (wave-uniform branch).
+    bool flat = false;
     if (dbg == 6) {  // profiling variant: no render
 #pragma unroll
       for (int i = 0; i < 64; ++i) blk[i] = (i * 7 + bx + by) & 255;
@@ -316,6 +324,10 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(kOcc)))
         lab = slab[i];
         brd = slab[pcols + i];
       }, bx, by, blk);
+      bool same = true;
+#pragma unroll
+      for (int i = 1; i < 64; ++i) same = same && blk[i] == blk[0];  // 15 distinct cells after CSE
+      flat = flat_ok && __ballot(!same) == 0;
     } else if (staged) {
       // Patch element (j, i) = source (4by-1+j, 4bx-1+i) = LDS (4by-1+j-ys0, 4bx+i).
       const float* pp = spatch + (4 * by - 1 - ys0) * pcols + 4 * bx;
@@ -341,51 +353,57 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(kOcc)))
       if (acc == 0x7FFFFFF1) out_sizes[0] = 1;
       return;
     }
-    // Level shift (x − 128) folded into the DC term: the islow FDCT is linear and its only
-    // rounding of the DC is a shift that divides the constant exactly, so fdct(x − 128) ==
-    // fdct(x) with DC − 64·128 (checked for all-extreme and random blocks). Saves 64 VALU ops.
-    fdct_islow(blk);
-    blk[0] -= 64 * 128;
-    // Quantise into packed int16 pairs first (frees the 64 int32 DCT registers), then walk the
-    // zig-zag order from those registers.
-    uint32_t zp[32];
-#pragma unroll
-    for (int k = 0; k < 64; k += 2) {
-      const int16_t a = quant_recip(blk[kNatural[k]], q, kNatural[k]);
-      const int16_t c = quant_recip(blk[kNatural[k + 1]], q, kNatural[k + 1]);
-      zp[k >> 1] = (uint32_t)(uint16_t)a | ((uint32_t)(uint16_t)c << 16);
-    }
-    dc0 = (int16_t)(zp[0] & 0xFFFFu);
-    if (dbg == 16) {  // profiling variant: stop after the FDCT and quantisation
-      uint32_t acc = 0;
-#pragma unroll
-      for (int i = 0; i < 32; ++i) acc ^= zp[i] * (uint32_t)(2 * i + 1);
-      if (acc == 0x7FFFFFF1u) out_sizes[0] = 1;
-      return;
-    }
     LBitWriter lw(pbuf, pspill);
     int last = 0;
-    // Outer loop not unrolled: zp[j] is indexed by a wave-uniform counter (register indexing, no
-    // scratch), keeping the code compact.
-#pragma unroll 1
-    for (int j = 0; j < 32; ++j) {
-      const uint32_t word = zp[j];
+    if (flat) {
+      dc0 = quant_recip(64 * (blk[0] - 128), q, 0);  // == fdct_islow's DC − 64·128 for a flat block
+    } else {
+      // Level shift (x − 128) folded into the DC term: the islow FDCT is linear and its only
+      // rounding of the DC is a shift that divides the constant exactly, so fdct(x − 128) ==
+      // fdct(x) with DC − 64·128 (checked for all-extreme and random blocks). Saves 64 VALU ops.
+      // islow FDCT as 16-bit dot products (jpeg_common.h fdct_islow_dot): 63 fewer static VALU
+      // instructions than the multiply/add form and no scratch spills (20 scratch instructions).
+      fdct_islow_dot(blk);
+      blk[0] -= 64 * 128;
+      // Quantise into packed int16 pairs first (frees the 64 int32 DCT registers), then walk the
+      // zig-zag order from those registers.
+      uint32_t zp[32];
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int k = 2 * j + h;
-        const int v = (int16_t)(word >> (16 * h));
-        if (k > 0 && __ballot(v != 0)) {
-          if (v != 0) {
-            int run = k - last - 1;
-            while (run > 15) {
-              lw.put_sym(actab[0xF0]);
-              run -= 16;
+      for (int k = 0; k < 64; k += 2) {
+        const int16_t a = quant_recip(blk[kNatural[k]], q, kNatural[k]);
+        const int16_t c = quant_recip(blk[kNatural[k + 1]], q, kNatural[k + 1]);
+        zp[k >> 1] = (uint32_t)(uint16_t)a | ((uint32_t)(uint16_t)c << 16);
+      }
+      dc0 = (int16_t)(zp[0] & 0xFFFFu);
+      if (dbg == 16) {  // profiling variant: stop after the FDCT and quantisation
+        uint32_t acc = 0;
+#pragma unroll
+        for (int i = 0; i < 32; ++i) acc ^= zp[i] * (uint32_t)(2 * i + 1);
+        if (acc == 0x7FFFFFF1u) out_sizes[0] = 1;
+        return;
+      }
+      // Outer loop not unrolled: zp[j] is indexed by a wave-uniform counter (register indexing, no
+      // scratch), keeping the code compact.
+#pragma unroll 1
+      for (int j = 0; j < 32; ++j) {
+        const uint32_t word = zp[j];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int k = 2 * j + h;
+          const int v = (int16_t)(word >> (16 * h));
+          if (k > 0 && __ballot(v != 0)) {
+            if (v != 0) {
+              int run = k - last - 1;
+              while (run > 15) {
+                lw.put_sym(actab[0xF0]);
+                run -= 16;
+              }
+              const int nb = mag_bits_fast(v);
+              const uint32_t e = actab[(run << 4) + nb];  // symbol and magnitude in one put (≤ 27 bits)
+              const uint32_t mag = (uint32_t)(v < 0 ? v - 1 : v) & ((1u << nb) - 1u);
+              lw.put(((e & 0xFFFFu) << nb) | mag, (int)(e >> 16) + nb);
+              last = k;
             }
-            const int nb = mag_bits_fast(v);
-            const uint32_t e = actab[(run << 4) + nb];  // symbol and magnitude in one put (≤ 27 bits)
-            const uint32_t mag = (uint32_t)(v < 0 ? v - 1 : v) & ((1u << nb) - 1u);
-            lw.put(((e & 0xFFFFu) << nb) | mag, (int)(e >> 16) + nb);
-            last = k;
           }
         }
       }
@@ -726,7 +744,8 @@ void launch_jpeg(const uint8_t* canvas, const JpegDesc* jd, int ncanvas, int out
   // NM03_JPEG_DBG selects truncated profiling variants (output invalid; tools/gpu_jpeg_split.sh).
   static const int dbg = [] {
     const char* e = std::getenv("NM03_JPEG_DBG");
-    return e ? std::atoi(e) : 0;
+    const char* f = std::getenv("NM03_JPEG_FLAT");  // 0: no flat-wave path (A/B)
+    return (e ? std::atoi(e) & 0xFF : 0) | (f && std::atoi(f) == 0 ? 0x100 : 0);
   }();
   // NM03_JPEG_LDS_PAD: extra dynamic LDS per workgroup (caps the encoder's residency per CU so
   // other streams' kernels keep LDS to run alongside it).

@@ -27,6 +27,7 @@
 #include "nm03/dicom.h"
 #include "nm03/golden.h"
 #include "nm03/jpeg.h"
+#include "nm03/jpeg_common.h"
 #include "nm03/numa.h"
 #include "nm03/pack12.h"
 #include "nm03/params.h"
@@ -312,6 +313,47 @@ TEST(jpeg_container) {
   bool ok = true;
   for (size_t i = hdr.size(); i + 2 < j.size(); ++i)
     if (j[i] == 0xFF && j[i + 1] != 0x00) ok = false;
+  CHECK(ok);
+}
+
+TEST(fdct_dot_form_bit_equal) {
+  // fdct_islow_dot (the kernel's v_dot2 form) against the multiply/add islow FDCT: random blocks,
+  // extremes, flat blocks, 2x2-duplicated label blocks and single impulses.
+  std::mt19937 rng(17);
+  auto check = [&](const int32_t* blk) {
+    int32_t a[64], b[64];
+    std::copy(blk, blk + 64, a);
+    std::copy(blk, blk + 64, b);
+    nm03::jpeg::fdct_islow(a);
+    nm03::jpeg::fdct_islow_dot(b);
+    return std::equal(a, a + 64, b);
+  };
+  int32_t blk[64];
+  bool ok = true;
+  for (int it = 0; it < 200000 && ok; ++it) {
+    const int kind = it % 5;
+    for (int i = 0; i < 64; ++i) {
+      switch (kind) {
+        case 0: blk[i] = (int32_t)(rng() & 255); break;
+        case 1: blk[i] = (rng() & 1) ? 255 : 0; break;
+        case 2: blk[i] = (int32_t)(it & 255); break;
+        case 3: blk[i] = ((i >> 3) + (i & 7)) * 17 % 256; break;
+        default: blk[i] = i == (it % 64) ? 255 : 0; break;
+      }
+    }
+    ok = check(blk);
+  }
+  CHECK(ok);
+  for (int v : {0, 255}) {  // checkerboards and stripes at both extremes
+    for (int pat = 0; pat < 4 && ok; ++pat) {
+      for (int i = 0; i < 64; ++i) {
+        const int r = i >> 3, c = i & 7;
+        const bool on = pat == 0 ? ((r + c) & 1) : pat == 1 ? (r & 1) : pat == 2 ? (c & 1) : (c < 4) != (r < 4);
+        blk[i] = on ? v : 255 - v;
+      }
+      ok = check(blk);
+    }
+  }
   CHECK(ok);
 }
 
