@@ -10,6 +10,8 @@
 #include <unistd.h>
 #include <sys/stat.h>
 #include <sched.h>
+#include <linux/capability.h>
+#include <sys/syscall.h>
 #include <atomic>
 #include <chrono>
 #include <cstdio>
@@ -22,7 +24,7 @@
 static double now(){return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();}
 static long long tcpu(){timespec t;clock_gettime(CLOCK_THREAD_CPUTIME_ID,&t);return t.tv_sec*1000000000LL+t.tv_nsec;}
 int main(int argc,char**argv){
-  if(argc<6){fprintf(stderr,"usage: io_contention root T nfiles reps mode(0 threads|1 procs|2 threads+unshare files|3 +fs) [mmap]\n");return 2;}
+  if(argc<6){fprintf(stderr,"usage: io_contention root T nfiles reps mode(0 threads|1 procs|2 threads+unshare files|3 +fs|4 unshare files+private cred) [mmap]\n");return 2;}
   const bool use_mmap = argc > 6 && atoi(argv[6]) != 0;  // loads: mmap(MAP_POPULATE) + sum + munmap instead of pread
   const char* root=argv[1]; int T=atoi(argv[2]); int nfiles=atoi(argv[3]); int reps=atoi(argv[4]); int procs=atoi(argv[5]);
   const size_t seg=12000, rsz=131*1024;
@@ -38,7 +40,11 @@ int main(int argc,char**argv){
     new(&shared[0]) std::atomic<long long>(0); new(&shared[1]) std::atomic<long long>(0); new(&shared[2]) std::atomic<long long>(0);
     auto work=[&](int t){ std::vector<uint8_t> buf(rsz); long long cw=0, cr=0;
       std::vector<int> my=dfd;
-      if(procs==2||procs==3){ if(unshare(procs==3?(CLONE_FILES|CLONE_FS):CLONE_FILES)!=0) abort();  // private fd table (+fs_struct)
+      if(procs==4){  // private struct cred: capset(current caps) commits a fresh cred for this thread only,
+        // so every open/close's get_cred/put_cred (file->f_cred) hits a per-thread refcount line
+        __user_cap_header_struct h{_LINUX_CAPABILITY_VERSION_3, 0}; __user_cap_data_struct c[2]{};
+        if(syscall(SYS_capget,&h,c)!=0||syscall(SYS_capset,&h,c)!=0) abort(); }
+      if(procs==2||procs==3||procs==4){ if(unshare(procs==3?(CLONE_FILES|CLONE_FS):CLONE_FILES)!=0) abort();  // private fd table (+fs_struct)
         for(int d=0;d<nd;++d) my[d]=open((std::string(root)+"/d"+std::to_string(d)).c_str(),O_PATH|O_DIRECTORY); }
       for(int i=t;i<nfiles;i+=T){
         long long c0=tcpu();
@@ -56,6 +62,6 @@ int main(int argc,char**argv){
     if(procs==1){ std::vector<pid_t> ps; for(int t=0;t<T;++t){pid_t p=fork(); if(p==0){work(t); _exit(0);} ps.push_back(p);} for(auto p:ps) waitpid(p,nullptr,0); }
     else { std::vector<std::thread> th; for(int t=0;t<T;++t) th.emplace_back(work,t); for(auto&x:th) x.join(); }
     double dt=now()-t0;
-    printf("T=%2d %s%s  read %.2f us/file  write %.2f us/pair  wall %.1f ms\n",T,procs==1?"procs  ":procs==2?"unshare":procs==3?"unsh+fs":"threads",use_mmap?"+mmap":"",shared[0].load()/1e3/nfiles,shared[1].load()/1e3/nfiles,dt*1e3);
+    printf("T=%2d %s%s  read %.2f us/file  write %.2f us/pair  wall %.1f ms\n",T,procs==1?"procs  ":procs==2?"unshare":procs==3?"unsh+fs":procs==4?"unsh+cr":"threads",use_mmap?"+mmap":"",shared[0].load()/1e3/nfiles,shared[1].load()/1e3/nfiles,dt*1e3);
   }
 }
