@@ -12,3 +12,4 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/pro
 python3 tools/kstats.py $O/prof/bench_kernel_stats.csv > $O/bench_kernels.txt || exit 52
 lscpu > $O/lscpu.txt 2>&1
 for i in 1 2 3; do timeout -k 5 60 build/bin/pack_probe >> $O/pack_probe.txt 2>&1 || exit 60; done
+timeout -k 5 30 build/bin/uring_probe > $O/uring_probe.txt 2>&1 || true
