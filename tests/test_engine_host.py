@@ -187,3 +187,25 @@ def test_host_only_many_queued_runs_private_fds(native, cohort_root, tmp_path, m
         assert not msgs
     for t in trees:
         assert len(_tree_bytes(t)) == 2 * len(t)
+
+
+@pytest.mark.parametrize("cred", ["1", "0"])
+def test_host_only_private_cred_identical(native, cohort_root, tmp_path, cred):
+    """Pool workers with their own struct cred (NM03_PRIVATE_CRED, the default) or the process's
+    shared one write the same bytes, twice over (create, then rewrite in place). Each setting runs in
+    a fresh process: the engine reads the variable once per process."""
+    items = _items(native, cohort_root, str(tmp_path / "o"))
+    script = (f"import sys; sys.path.insert(0, {ROOT!r}); import nm03_capstone_project_amd as nm; "
+              f"n = nm.native(); cfg = nm.PipelineConfig(batch_size=4, streams=2, threads=4).engine_config(); "
+              f"cfg.host_only = True; e = n.Engine(cfg); w = n.WorkList({items!r}); "
+              f"bad = [len(e.run_list(w)[1]) for _ in range(2)]; print(sum(bad))")
+    r = subprocess.run([sys.executable, "-c", script], capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, NM03_PRIVATE_CRED=cred))
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert r.stdout.strip().splitlines()[-1] == "0"
+    ref = tmp_path / "ref"
+    ref_items = _items(native, cohort_root, str(ref))
+    st, _ = _engine(native, threads=2).run(ref_items)
+    assert all(c == 0 for c, _ in st)
+    got, want = _tree_bytes(items), _tree_bytes(ref_items)
+    assert sorted(got.values()) == sorted(want.values()) and len(got) == 2 * len(items)
