@@ -140,20 +140,24 @@ def _tree_bytes(items):
 
 
 @pytest.mark.parametrize("private", ["1", "0"])
-def test_host_only_private_fd_tables_identical(native, cohort_root, tmp_path, monkeypatch, private):
-    """Pool workers with private fd tables (close_range UNSHARE, per-worker directory fds) write
-    the same files as with the shared table, across several queued runs (the per-worker directory
-    cache alternates between runs) and fresh vs existing output trees."""
-    monkeypatch.setenv("NM03_PRIVATE_FDS", private)
+def test_host_only_private_fd_tables_identical(native, cohort_root, tmp_path, private):
+    """Pool workers with private fd tables (close_range UNSHARE) write the same files as with the
+    shared table, across two queued runs and fresh vs existing output trees. Each setting runs in a
+    fresh process: the engine reads NM03_PRIVATE_FDS once per process."""
     items = _items(native, cohort_root, str(tmp_path / "a"))
     items_b = _items(native, cohort_root, str(tmp_path / "b"))
-    eng = _engine(native, threads=4)
-    wa, wb = native.WorkList(items), native.WorkList(items_b)
-    for _ in range(2):  # first pass creates, second rewrites in place
-        ta, tb = eng.submit(wa), eng.submit(wb)
-        for t in (ta, tb):
-            codes, msgs, _ = eng.wait(t)
-            assert not msgs
+    script = (f"import sys; sys.path.insert(0, {ROOT!r}); import nm03_capstone_project_amd as nm; "
+              f"n = nm.native(); cfg = nm.PipelineConfig(batch_size=4, streams=2, threads=4).engine_config(); "
+              f"cfg.host_only = True; e = n.Engine(cfg); wa, wb = n.WorkList({items!r}), n.WorkList({items_b!r}); "
+              f"bad = 0\n"
+              f"for _ in range(2):\n"
+              f"    ta, tb = e.submit(wa), e.submit(wb)\n"
+              f"    bad += sum(len(e.wait(t)[1]) for t in (ta, tb))\n"
+              f"print(bad)")
+    r = subprocess.run([sys.executable, "-c", script], capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, NM03_PRIVATE_FDS=private))
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert r.stdout.strip().splitlines()[-1] == "0"
     a, b = _tree_bytes(items), _tree_bytes(items_b)
     assert len(a) == 2 * len(items) and sorted(a.values()) == sorted(b.values())
 
