@@ -163,20 +163,18 @@ struct Slot {
 // therefore starts with close_range(3, ~0U, CLOSE_RANGE_UNSHARE): its own table, holding only
 // stdin/out/err (no duplicates of the process's other fds, so a pipe or file the process closes is
 // not kept open by a worker). Such workers open files by full path (IoDirs::dir_fd).
-static bool private_fds_wanted() {
-  static const bool on = [] {
-    const char* e = std::getenv("NM03_PRIVATE_FDS");
-    return !(e && *e == '0');
-  }();
-  return on;
+// NM03_PRIVATE_FDS=0 keeps the shared table; read when an engine is built (tests flip it in-process).
+static bool env_flag_on(const char* name) {
+  const char* e = std::getenv(name);
+  return !(e && *e == '0');
 }
 static thread_local bool tl_private_fds = false;
 
-static void make_fd_table_private() {
+static void make_fd_table_private(bool on) {
 #ifndef CLOSE_RANGE_UNSHARE
 #define CLOSE_RANGE_UNSHARE (1U << 1)
 #endif
-  if (private_fds_wanted() && ::syscall(SYS_close_range, 3u, ~0u, CLOSE_RANGE_UNSHARE) == 0) tl_private_fds = true;
+  if (on && ::syscall(SYS_close_range, 3u, ~0u, CLOSE_RANGE_UNSHARE) == 0) tl_private_fds = true;
 }
 
 // Every open() stores the opener's struct cred in the file (get_cred) and close() drops it (put_cred):
@@ -185,11 +183,7 @@ static void make_fd_table_private() {
 // commits a fresh, identical cred for the calling thread only (no privilege change). Bench, 5
 // interleaved pairs: 385–402k vs 327–398k slices/s, JPEG-pair write CPU 0.17–0.22 vs 0.19–0.26 s
 // per 40 steps (profiles/r3/private_cred/). NM03_PRIVATE_CRED=0 keeps the shared cred.
-static void make_cred_private() {
-  static const bool on = [] {
-    const char* e = std::getenv("NM03_PRIVATE_CRED");
-    return !(e && *e == '0');
-  }();
+static void make_cred_private(bool on) {
   if (!on) return;
   __user_cap_header_struct h{_LINUX_CAPABILITY_VERSION_3, 0};
   __user_cap_data_struct c[2]{};
@@ -311,6 +305,9 @@ struct Engine::Impl {
   size_t read_prefix_ = 16384;
   // 12-bit transfer packing of slices whose samples fit (nm03/pack12.h); NM03_PACK12=0 disables.
   bool pack12_ = pack12::available();
+  // Pool workers' private fd tables and creds (NM03_PRIVATE_FDS / NM03_PRIVATE_CRED, default on).
+  const bool private_fds_ = env_flag_on("NM03_PRIVATE_FDS");
+  const bool private_cred_ = env_flag_on("NM03_PRIVATE_CRED");
   // Host-mapped bytes per image for the GPU encoder's stuffed output: half the canvas (128 KiB for
   // 512², ~5× a typical medical render; anything larger is CPU re-encoded, counted in StageTimes).
   // NM03_JPEG_OUT_CAP=<bytes> overrides (tests force the fallback with a tiny cap).
@@ -398,8 +395,8 @@ struct Engine::Impl {
     // Host threads and pinned buffers on the GPU's socket (numa.h).
     pool = std::make_unique<ThreadPool>(cfg.threads, [this](int i) {
       place.bind_worker(i, cfg.threads);
-      make_fd_table_private();
-      make_cred_private();
+      make_fd_table_private(private_fds_);
+      make_cred_private(private_cred_);
       // Signals go to other threads: a pool worker's reads are never cut short (SliceFile's
       // staged read takes a short read as the end of the file).
       sigset_t all;
@@ -1531,7 +1528,7 @@ struct Engine::Impl {
     auto j = std::make_shared<Job>();
     j->t0 = now_s();
     j->items = std::move(items);
-    j->dirs = std::make_unique<IoDirs>(*j->items, !private_fds_wanted());
+    j->dirs = std::make_unique<IoDirs>(*j->items, !private_fds_);
     j->on_start = std::move(on_start);
     j->status.resize(j->items->size());
     const size_t B = batch_cap > 0 ? std::min<size_t>((size_t)batch_cap, (size_t)cfg.batch_size) : (size_t)cfg.batch_size;
