@@ -1,6 +1,7 @@
 // nm03_bench — native benchmark driver: the BASELINE configs on the engine without the CLI's
 // message catalogue. Prints one JSON line.
-//   --config cohort  (2/3)   full synthetic T1+C cohort, end-to-end (read → GPU → JPEG files)
+//   --config cohort  (2/3)   full synthetic T1+C cohort, end-to-end (read → GPU → JPEG files);
+//                            with --host-only every load, pack and file write but no GPU
 //   --config volume  (5)     one patient series as a volume, 3D SRG + cube dilation
 //   --config cpu-reference   BASELINE.md protocol: the golden CPU model in the reference's
 //                            structure — per patient, batches of ≤25 slices over 16 threads
@@ -48,6 +49,7 @@ int main(int argc, char** argv) {
     else if (a == "--max-dim") ec.max_dim = std::atoi(v().c_str());
     else if (a == "--dilation-3d") dil3d = std::atoi(v().c_str());
     else if (a == "--device") ec.device = std::atoi(v().c_str());
+    else if (a == "--host-only") ec.host_only = true;  // cohort: every load/pack/write, no GPU (sanitizer sweeps)
     else {
       std::cerr << "unknown option " << a << std::endl;
       return 2;

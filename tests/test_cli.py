@@ -160,3 +160,18 @@ def test_fast_exit_same_output(native, cohort_root, tmp_path, cli, args):
         res.append((r.returncode, norm(r.stdout), norm(r.stderr), tree))
     assert res[0] == res[1]
     assert res[0][1] or res[0][2]  # something was printed and survived the fast exit
+
+
+def test_native_bench_cohort_host_only(native, cohort_root, tmp_path):
+    """nm03_bench --config cohort --host-only (the sanitizer sweep's engine run): every slice loaded
+    and both JPEGs written per slice, no GPU."""
+    import json
+    out = tmp_path / "o"
+    r = run_bin("nm03_bench", "--config", "cohort", "--host-only", "--data-root", cohort_root, "--out", str(out),
+                "--steps", "2", "--warmup", "1", "--threads", "4", "--streams", "2", "--batch-size", "8")
+    assert r.returncode == 0, r.stderr
+    rec = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert rec["slices_per_s"] > 0 and rec["kernels_s"] == 0
+    n = rec["slices_per_step"]
+    files = [p for d in out.iterdir() for p in d.iterdir()]
+    assert len(files) == 2 * n and all(p.read_bytes()[:2] == b"\xff\xd8" for p in files)
