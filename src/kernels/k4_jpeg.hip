@@ -10,7 +10,8 @@
 //                        256 KiB canvas never exists. The workgroup first stages its source rows
 //                        in LDS (gray: rescaled f32, 18 × 258 for a 256² slice; labels: the label
 //                        and border bit rows) with coalesced loads: 76 → 67 µs per 64-slice batch.
-//                        islow FDCT (24-bit multiplies), quantisation by exact reciprocal (umulhi
+//                        islow FDCT as v_dot2_i32_i16 dot products (label waves of one flat colour
+//                        skip FDCT, quantisation and coding), quantisation by exact reciprocal (umulhi
 //                        by ceil(2^32/d): exact for |x|, d < 2^16),
 //                        Huffman cost, workgroup scan, the workgroup's bit range assembled in LDS,
 //                        its 0xFF-byte counts for all 8 byte alignments, a decoupled look-back
