@@ -51,6 +51,23 @@ __attribute__((target("avx2"))) inline void pack16(const uint16_t* src, uint8_t*
   _mm_storeu_si128(reinterpret_cast<__m128i*>(d + 12), _mm256_extracti128_si256(c, 1));
 }
 
+// Bounce → destination copy: streaming (non-temporal) stores by default; NM03_PACK_NT=0 uses
+// regular cached stores (A/B: the DMA upload may then read recently packed lines from the CPU
+// caches instead of DRAM).
+inline bool pack_nt() {
+  static const bool on = [] {
+    const char* e = std::getenv("NM03_PACK_NT");
+    return !(e && *e == '0');
+  }();
+  return on;
+}
+inline void bounce_out(uint8_t* dst, const uint8_t* src, size_t bytes) {
+  if (pack_nt())
+    dicom::stream_copy_unfenced(dst, src, bytes);
+  else
+    std::memcpy(dst, src, bytes);
+}
+
 // Packs and range-checks in the same pass (one read of the samples): returns false — dst then
 // holds garbage the caller must not use — when some sample needs more than 12 bits.
 __attribute__((target("avx2"))) bool pack_stream_avx2(const uint16_t* src, size_t n, uint8_t* dst) {
@@ -63,7 +80,7 @@ __attribute__((target("avx2"))) bool pack_stream_avx2(const uint16_t* src, size_
       acc = _mm256_or_si256(acc, _mm256_loadu_si256(reinterpret_cast<const __m256i*>(src + i + k)));
       pack16(src + i + k, bounce + k / 2 * 3);
     }
-    dicom::stream_copy_unfenced(dst + i / 2 * 3, bounce, m / 2 * 3);
+    bounce_out(dst + i / 2 * 3, bounce, m / 2 * 3);
   }
   _mm_sfence();  // one fence for the whole slice
   return _mm256_testz_si256(acc, _mm256_set1_epi16((short)0xF000));
@@ -97,7 +114,7 @@ __attribute__((target("avx2,avx512f,avx512bw,avx512vbmi"))) bool pack_stream_avx
       acc = _mm512_or_si512(acc, _mm512_zextsi256_si512(_mm256_loadu_si256(reinterpret_cast<const __m256i*>(src + i + m32))));
       pack16(src + i + m32, bounce + m32 / 2 * 3);
     }
-    dicom::stream_copy_unfenced(dst + i / 2 * 3, bounce, m / 2 * 3);
+    bounce_out(dst + i / 2 * 3, bounce, m / 2 * 3);
   }
   _mm_sfence();
   return _mm512_test_epi16_mask(acc, _mm512_set1_epi16((short)0xF000)) == 0;
