@@ -342,6 +342,37 @@ def test_engine_fault_isolation(native, tmp_path):
     assert t2["slices_ok"] == 2 and t2["slices_failed"] == 2
 
 
+def test_engine_flat_label_waves_vs_golden(native, tmp_path):
+    """Label images whose waves are one flat colour skip the FDCT, quantisation and zig-zag walk
+    (k4_jpeg.hip, NM03_JPEG_FLAT): every exported JPEG — all-background label images (uniform and
+    noise-only slices: no region grows), phantom slices with a partial region, and a slice whose
+    region fills most of the canvas — is byte-identical to the golden encoder's."""
+    d = tmp_path / "series"
+    d.mkdir()
+    rng = np.random.default_rng(5)
+    slices = [np.zeros((256, 256), np.uint16), np.full((256, 256), 1000, np.uint16),
+              rng.integers(0, 40, (256, 256), dtype=np.uint16)]
+    slices += [native.phantom_slice(256, 256, p, s, 23, 7) for p, s in ((0, 3), (1, 11), (2, 20))]
+    bright = native.phantom_slice(256, 256, 3, 11, 23, 7).astype(np.float64)
+    slices.append(np.clip(bright * 1.6, 0, 4095).astype(np.uint16))  # most of the head in the SRG band
+    out = tmp_path / "out"
+    out.mkdir()
+    items = []
+    for i, a in enumerate(slices, start=1):
+        (d / f"1-{i}.dcm").write_bytes(native.dicom_bytes(a))
+        items.append((str(d / f"1-{i}.dcm"), str(out)))
+    st, times = native.Engine(nm.PipelineConfig(batch_size=8, streams=1, threads=2).engine_config()).run(items)
+    assert all(c == 0 for c, _ in st), st
+    assert times["jpeg_fallbacks"] == 0
+    for f, _ in items:
+        raw, meta = native.read_slice(f)
+        g = native.golden_run(raw, meta["type"], meta["stored_bits"], meta["slope"], meta["intercept"],
+                              native.PipelineParams(), native.RenderParams(), meta["spacing_x"], meta["spacing_y"])
+        stem = os.path.splitext(os.path.basename(f))[0]
+        assert (out / f"{stem}_original.jpg").read_bytes() == g["jpeg_original"], stem
+        assert (out / f"{stem}_processed.jpg").read_bytes() == g["jpeg_processed"], stem
+
+
 def test_engine_pack12_identical(native, cohort_root, tmp_path, monkeypatch):
     """12-bit transfer packing (nm03/pack12.h + K0 unpack) on vs off: byte-identical JPEGs and the
     same statuses, on batches mixing packable 12-bit slices, a slice with 13-bit samples (shipped as
