@@ -149,7 +149,8 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(kOcc)))
                                                              int out_h, QuantRecip q, JpegWork w, JpegRenderSrc rs,
                                                              uint8_t* __restrict__ out, int32_t* __restrict__ out_sizes,
                                                              int dbgw) {
-  // dbgw: profiling variant in the low byte (NM03_JPEG_DBG), bit 8 = flat-wave path off (NM03_JPEG_FLAT=0).
+  // dbgw: profiling variant in the low byte (NM03_JPEG_DBG), bit 8 = flat-wave path off (NM03_JPEG_FLAT=0),
+  // bit 10 = blocked image order (NM03_JPEG_SPREAD=0).
   const int dbg = dbgw & 0xFF;
   const bool flat_ok = !(dbgw & 0x100);
   __shared__ uint32_t actab[256];
@@ -179,7 +180,13 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(kOcc)))
   // The image is fixed by the dispatch index; only the part comes from the ticket. The ticket's
   // device-scope atomic is issued first, so its round trip overlaps the table and descriptor
   // loads below (issued after them it waited behind three dependent descriptor loads).
-  const int img = (int)(blockIdx.x / (uint32_t)parts);
+  // Images are dealt round-robin over the dispatch order (workgroup b encodes image b mod
+  // ncanvas): consecutive workgroups hit different ticket counters instead of `parts` of them
+  // queueing on one address, and an image's parts start one `ncanvas` stride apart, so a part's
+  // predecessors have mostly finished encoding when it looks back (dbgw bit 10 / NM03_JPEG_SPREAD=0:
+  // the blocked order, A/B).
+  const bool spread = !(dbgw & 0x400);
+  const int img = spread ? (int)(blockIdx.x % (uint32_t)ncanvas) : (int)(blockIdx.x / (uint32_t)parts);
   uint32_t ticket = 0;
   if (tid == 0 && dbg != 9) {
     // The address goes through a VGPR the compiler cannot prove uniform: a uniform-address atomic
@@ -207,7 +214,7 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(kOcc)))
     // index as the part is ~5% faster, NM03_JPEG_DBG=9, but two encoders interleaving on the same
     // XCDs can starve each other's predecessors: measured 2.3 s/step stalls with two ranks per
     // GPU.) One counter per image keeps the serialised atomics per address at `parts`.
-    uint32_t p = blockIdx.x - (uint32_t)img * (uint32_t)parts;
+    uint32_t p = spread ? blockIdx.x / (uint32_t)ncanvas : blockIdx.x - (uint32_t)img * (uint32_t)parts;
     if (dbg != 9) {
       p = ticket;
       if (p == (uint32_t)parts - 1) atomicExch(&w.ticket[img], 0u);  // the image's last ticket
@@ -745,8 +752,9 @@ void launch_jpeg(const uint8_t* canvas, const JpegDesc* jd, int ncanvas, int out
   // NM03_JPEG_DBG selects truncated profiling variants (output invalid; tools/gpu_jpeg_split.sh).
   static const int dbg = [] {
     const char* e = std::getenv("NM03_JPEG_DBG");
-    const char* f = std::getenv("NM03_JPEG_FLAT");  // 0: no flat-wave path (A/B)
-    return (e ? std::atoi(e) & 0xFF : 0) | (f && std::atoi(f) == 0 ? 0x100 : 0);
+    const char* f = std::getenv("NM03_JPEG_FLAT");      // 0: no flat-wave path (A/B)
+    const char* sp = std::getenv("NM03_JPEG_SPREAD");   // 0: blocked image order (A/B)
+    return (e ? std::atoi(e) & 0xFF : 0) | (f && std::atoi(f) == 0 ? 0x100 : 0) | (sp && std::atoi(sp) == 0 ? 0x400 : 0);
   }();
   // NM03_JPEG_LDS_PAD: extra dynamic LDS per workgroup (caps the encoder's residency per CU so
   // other streams' kernels keep LDS to run alongside it).
