@@ -87,10 +87,15 @@ constexpr int kJpegWG = 256;     // luma blocks (threads) per workgroup = 64 MCU
 // side, full width + 1-column halos, edge-clamped) are loaded once, coalesced, into LDS; the 6×6
 // patches of the exact-2× render then come from LDS instead of 36 scattered global loads per
 // block. Pixels are converted to f32 (rescale) once while staging, not once per patch use (2.25×).
-constexpr int kPatchLds = 4864;  // f32 elements (19 KiB; 256²: 18 × 258 = 4644); larger footprints use global loads
+// Staged gray rows are swizzled: source column c (0..W+1 with the halos) sits at c + c/4 of a row of
+// stride ≡ 4 (mod 8) words. A half-wave's patch reads then hit distinct banks: its 16 blocks step
+// 5 words apart (16 distinct banks mod 32) and its two block rows, 4 source rows apart, are offset
+// by 16 banks (disjoint sets) — the plain layout's 4-byte stride put 4 addresses on each bank.
+constexpr int kPatchLds = 5832;  // f32 elements (22.8 KiB; 256²: 18 × 324); larger footprints use global loads
+__device__ __forceinline__ int swz_col(int c, bool on) { return on ? c + (c >> 2) : c; }
 // One LDS region serves the render (source patch above) and then, once every block is rendered,
 // the workgroup's assembled bit range followed by its staged stuffed output bytes.
-constexpr int kUnionWords = kPatchLds + 2048;  // 27 KiB: bit ranges up to ~220 Kbit
+constexpr int kUnionWords = kPatchLds + 1080;  // 27 KiB as before (4 workgroups per CU): bit ranges up to ~220 Kbit
 
 constexpr int kPrivWords = 5;    // per-block Huffman bits kept in LDS (160 bits, odd stride) ...
 constexpr int kSpillWords = 56;  // ... the rest in the block's global spill slot (a block needs ≤ 1700)
@@ -141,7 +146,7 @@ __device__ __forceinline__ uint32_t priv_word(const uint32_t* pb, const uint32_t
 //  4. each thread writes its block's codes at its bit offset (atomicOr into the zeroed stage).
 // The last workgroup of an image publishes the total (or the overflow marker).
 // kOcc: target waves per SIMD (= workgroups per CU); kUnion: LDS words of the patch / bit-range
-// union. <4, kUnionWords> is the default; <5, kPatchLds + 1200> fits 5 workgroups per CU (31.7 KiB)
+// union. <4, kUnionWords> is the default; <5, kPatchLds + 232> fits 5 workgroups per CU (31.7 KiB)
 // at ≤ 96 VGPRs (NM03_JPEG_OCC=5, A/B).
 template <int kOcc, int kUnion>
 __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(kOcc))) void jpeg_fused_kernel(const uint8_t* __restrict__ canvas,
@@ -150,7 +155,7 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(kOcc)))
                                                              uint8_t* __restrict__ out, int32_t* __restrict__ out_sizes,
                                                              int dbgw) {
   // dbgw: profiling variant in the low byte (NM03_JPEG_DBG), bit 8 = flat-wave path off (NM03_JPEG_FLAT=0),
-  // bit 10 = blocked image order (NM03_JPEG_SPREAD=0).
+  // bit 10 = blocked image order (NM03_JPEG_SPREAD=0), bit 11 = plain staged rows (NM03_JPEG_SWIZZLE=0).
   const int dbg = dbgw & 0xFF;
   const bool flat_ok = !(dbgw & 0x100);
   __shared__ uint32_t actab[256];
@@ -186,6 +191,7 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(kOcc)))
   // predecessors have mostly finished encoding when it looks back (dbgw bit 10 / NM03_JPEG_SPREAD=0:
   // the blocked order, A/B).
   const bool spread = !(dbgw & 0x400);
+  const bool swz = !(dbgw & 0x800);  // swizzled gray staging (NM03_JPEG_SWIZZLE=0: plain rows, A/B)
   const int img = spread ? (int)(blockIdx.x % (uint32_t)ncanvas) : (int)(blockIdx.x / (uint32_t)parts);
   uint32_t ticket = 0;
   if (tid == 0 && dbg != 9) {
@@ -257,7 +263,8 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(kOcc)))
     const int m0 = part * (kJpegWG / 4), m1 = min(m0 + kJpegWG / 4, bpi >> 2) - 1;
     const int r0 = m0 / mcux, r1 = m1 / mcux;
     const int nrows = 8 * (r1 - r0) + 10;
-    pcols = rd.src_w + 2;
+    pcols = swz_col(rd.src_w + 1, swz) + 1;
+    if (swz) pcols += (4 - pcols % 8 + 8) % 8;  // row stride ≡ 4 (mod 8)
     if (nrows * pcols <= kPatchLds && !(rd.src_off & 1)) {
       staged = true;
       ys0 = 8 * r0 - 1;
@@ -284,20 +291,20 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(kOcc)))
         const int i = tid + t * kJpegWG;
         if (i < nw) {
           const int j = i / hw, k = i - j * hw;
-          spatch[j * pcols + 2 * k + 1] = value((uint16_t)(v[t] & 0xFFFFu));
-          spatch[j * pcols + 2 * k + 2] = value((uint16_t)(v[t] >> 16));
+          spatch[j * pcols + swz_col(2 * k + 1, swz)] = value((uint16_t)(v[t] & 0xFFFFu));
+          spatch[j * pcols + swz_col(2 * k + 2, swz)] = value((uint16_t)(v[t] >> 16));
         }
       }
       for (int i = tid + kU * kJpegWG; i < nw; i += kJpegWG) {  // larger footprints
         const int j = i / hw, k = i - j * hw;
         const uint32_t u = *reinterpret_cast<const uint32_t*>(src + (size_t)clampi(ys0 + j, 0, H - 1) * W + 2 * k);
-        spatch[j * pcols + 2 * k + 1] = value((uint16_t)(u & 0xFFFFu));
-        spatch[j * pcols + 2 * k + 2] = value((uint16_t)(u >> 16));
+        spatch[j * pcols + swz_col(2 * k + 1, swz)] = value((uint16_t)(u & 0xFFFFu));
+        spatch[j * pcols + swz_col(2 * k + 2, swz)] = value((uint16_t)(u >> 16));
       }
       // Clamped halo columns 0 and W+1.
       for (int i = tid; i < 2 * nrows; i += kJpegWG) {
         const int j = i >> 1, right = i & 1;
-        spatch[j * pcols + (right ? W + 1 : 0)] =
+        spatch[j * pcols + (right ? swz_col(W + 1, swz) : 0)] =
             value(src[(size_t)clampi(ys0 + j, 0, H - 1) * W + (right ? W - 1 : 0)]);
       }
       __syncthreads();
@@ -337,9 +344,10 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(kOcc)))
       for (int i = 1; i < 64; ++i) same = same && blk[i] == blk[0];  // 15 distinct cells after CSE
       flat = flat_ok && __ballot(!same) == 0;
     } else if (staged) {
-      // Patch element (j, i) = source (4by-1+j, 4bx-1+i) = LDS (4by-1+j-ys0, 4bx+i).
-      const float* pp = spatch + (4 * by - 1 - ys0) * pcols + 4 * bx;
-      render_patch_2x([&](int j, int i) { return pp[j * pcols + i]; }, win, blk);
+      // Patch element (j, i) = source (4by-1+j, 4bx-1+i) = staged row 4by-1+j-ys0, column 4bx+i.
+      // Patch column i = source column 4bx-1+i = staged column 4bx+i → swizzled 5bx + i + (i ≥ 4).
+      const float* pp = spatch + (4 * by - 1 - ys0) * pcols + (swz ? 5 : 4) * bx;
+      render_patch_2x([&](int j, int i) { return pp[j * pcols + i + (swz && i >= 4 ? 1 : 0)]; }, win, blk);
     } else if (d.render >= 0) {
       render_block_2x(rd, rs.raw, rs.f32, rs.bits, win, bx, by, blk, dbg == 11);
     } else {
@@ -754,7 +762,9 @@ void launch_jpeg(const uint8_t* canvas, const JpegDesc* jd, int ncanvas, int out
     const char* e = std::getenv("NM03_JPEG_DBG");
     const char* f = std::getenv("NM03_JPEG_FLAT");      // 0: no flat-wave path (A/B)
     const char* sp = std::getenv("NM03_JPEG_SPREAD");   // 0: blocked image order (A/B)
-    return (e ? std::atoi(e) & 0xFF : 0) | (f && std::atoi(f) == 0 ? 0x100 : 0) | (sp && std::atoi(sp) == 0 ? 0x400 : 0);
+    const char* sw = std::getenv("NM03_JPEG_SWIZZLE");  // 0: plain staged rows (A/B)
+    return (e ? std::atoi(e) & 0xFF : 0) | (f && std::atoi(f) == 0 ? 0x100 : 0) | (sp && std::atoi(sp) == 0 ? 0x400 : 0) |
+           (sw && std::atoi(sw) == 0 ? 0x800 : 0);
   }();
   // NM03_JPEG_LDS_PAD: extra dynamic LDS per workgroup (caps the encoder's residency per CU so
   // other streams' kernels keep LDS to run alongside it).
@@ -785,7 +795,7 @@ void launch_jpeg(const uint8_t* canvas, const JpegDesc* jd, int ncanvas, int out
     return e && std::atoi(e) == 5 ? 5 : 4;
   }();
   if (occ == 5)
-    jpeg_fused_kernel<5, kPatchLds + 1200><<<parts * ncanvas, kJpegWG, pad, stream>>>(
+    jpeg_fused_kernel<5, kPatchLds + 232><<<parts * ncanvas, kJpegWG, pad, stream>>>(
         canvas, jd, ncanvas, out_w, out_h, q, w, rs, out, out_sizes, dbg);
   else
     jpeg_fused_kernel<4, kUnionWords><<<parts * ncanvas, kJpegWG, pad, stream>>>(canvas, jd, ncanvas, out_w, out_h, q, w,
