@@ -92,6 +92,13 @@ def parse_args(argv=None):
     # 96 slices × 4 slots: 5 batches per 465-slice pass instead of 8 at 64 × 6; won 10 of 11
     # interleaved pairs on two boxes (median 324k vs 297k and 354k vs 324k slices/s) with less host
     # CPU per step (profiles/r2/batch_streams/).
+    ap.add_argument("--wipe-mode", choices=("reaper", "inline"), default="reaper",
+                    help="wipe passes: rename each output directory aside and delete it on 2 background "
+                         "reaper threads (cohort.h OutputReaper; the final drain is inside the clock), or "
+                         "unlink everything before the pass on 8 threads (round 3)")
+    ap.add_argument("--create-writers", type=int, default=-1,
+                    help="EngineConfig.create_writers: pool workers writing a batch's JPEGs at once while "
+                         "its directories are being filled (-1 = engine default, 0 = no limit)")
     ap.add_argument("--batch-size", type=int, default=96)
     ap.add_argument("--streams", type=int, default=4)
     ap.add_argument("--threads", type=int, default=0,
@@ -102,12 +109,11 @@ def parse_args(argv=None):
                     help="also time this many single strong-scaling passes (one cohort sharded over the "
                          "ranks, nothing else in flight; config.strong.single_pass_ms; 0 = skip)")
     ap.add_argument("--comm", choices=("auto", "rccl", "host"), default=os.environ.get("NM03_COMM", "auto"))
-    ap.add_argument("--data-root", default=os.environ.get("NM03_BENCH_DATA", os.path.join(_scratch(), "nm03_bench_data")))
-    ap.add_argument("--out-root", default=os.environ.get("NM03_BENCH_OUT", os.path.join(_scratch(), "nm03_bench_out")))
+    ap.add_argument("--data-root", default=os.path.join(_scratch(), "nm03_bench_data"))
+    ap.add_argument("--out-root", default=os.path.join(_scratch(), "nm03_bench_out"))
     ap.add_argument("--keep-data", action="store_true", help="keep a generated dataset in tmpfs after the run")
     ap.add_argument("--keep-output", action="store_true")
-    ap.add_argument("--graphs", action="store_true", help="hipGraph replay of the per-batch kernel chain")
-    ap.add_argument("--pipeline-depth", type=int, default=int(os.environ.get("NM03_BENCH_DEPTH", "0")),
+    ap.add_argument("--pipeline-depth", type=int, default=0,
                     help="passes in flight (each with its own output tree); 0 = auto: 2, or 4 when the rank's "
                          "shard is smaller than one batch per slot (strong scaling: a pass is then mostly "
                          "latency, and more passes in flight overlap it)")
@@ -125,7 +131,11 @@ def parse_args(argv=None):
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU rehearsal of the launcher, rendezvous, comm, sharding and aggregation: every step "
                          "of a real run except the engine (no GPU); the JSON value is meaningless")
-    ap.add_argument("--numa-data", choices=("auto", "off"), default=os.environ.get("NM03_BENCH_NUMA_DATA", "auto"),
+    ap.add_argument("--cli-runs", type=int, default=10,
+                    help="also time this many whole invocations of the unmodified img_processing_parallel --gpus N "
+                         "on the bench cohort, as the reference measured its binaries (hyperfine, README.md:92-96); "
+                         "reported as config.cli_wall (0 = skip)")
+    ap.add_argument("--numa-data", choices=("auto", "off"), default="auto",
                     help="auto: one input copy per NUMA node, each rank reads the copy on its GPU's node")
     return ap.parse_args(argv)
 
@@ -275,15 +285,19 @@ def run_rank(args):
     dev_node = n.numa_device_node(device) if nodes else -1
     local_root = replica_root(args.data_root, dev_node) if dev_node in nodes else roots[0]
 
-    fail_rank = os.environ.get("NM03_BENCH_FAIL_RANK", "")  # fault injection (tests): this rank dies here
+    # Fault injection (tests): NM03_FAULT=rank_exit:<r> makes rank r die here (log.h FaultPlan).
+    fail_rank = next((f.split(":", 1)[1] for f in os.environ.get("NM03_FAULT", "").split(",")
+                      if f.startswith("rank_exit:")), "")
     if fail_rank != "" and int(fail_rank) == rank:
         print(f"bench: rank {rank}: injected failure", file=sys.stderr, flush=True)
         os._exit(5)
     cfg = nm.PipelineConfig(batch_size=args.batch_size, streams=args.streams, threads=args.threads,
-                            device=device, graphs=args.graphs)
+                            device=device)
     ecfg = cfg.engine_config()
     ecfg.cpus = part["cpus"]
     ecfg.host_only = args.host_only
+    if args.create_writers >= 0:
+        ecfg.create_writers = args.create_writers
     engine = _DryEngine() if args.dry_run else n.Engine(ecfg)
 
     def pipeline_depth(shard_len):
@@ -323,11 +337,15 @@ def run_rank(args):
         if rediscover and discover() != mine:
             raise SystemExit(f"rank {rank}: rediscovered cohort differs from the planned shard")
 
+        reaper = n.OutputReaper(2) if wipe and args.wipe_mode == "reaper" else None
+
         def pass_work(k):
             """Native work list of pass k; wipe passes first empty the pass's output tree (the
             reference's per-run rm -rf + mkdir)."""
             j = k % depth
-            if wipe:
+            if reaper is not None:
+                reaper.wipe(tree_dirs[j])
+            elif wipe:
                 n.setup_output_dirs(tree_dirs[j], 8)
             if not rediscover:
                 return works[j]
@@ -383,6 +401,8 @@ def run_rank(args):
                     stage[k] += times[k]
             with _roctx_range("bench.steps"):
                 passes(steps, sink)
+        if reaper is not None:
+            reaper.drain()  # the timed passes' deletions are part of their cost
         t_own = time.perf_counter() - t0  # this rank's own time, before waiting for the others
         if torch.cuda.is_available():
             torch.cuda.synchronize()
@@ -477,6 +497,16 @@ def run_rank(args):
             sp.update({"single_pass_shard8_ms": m8, "single_pass_shard8_min_ms": b8,
                        "single_pass_shard8_uncapped_ms": m8u, "single_pass_shard8_uncapped_min_ms": b8u})
 
+    cli = None
+    if args.cli_runs > 0 and not args.dry_run:
+        # After the engine is gone (its pool threads would compete with the CLI's): rank 0 runs the
+        # whole CLI --gpus N, reaped with wait4 (exact wall + rusage); the other ranks wait.
+        del engine
+        engine = None
+        if is_root:
+            cli = cli_wall(args, world, local_root)
+        comm.barrier()
+
     if is_root:
         value = primary["value"]
         rec = {
@@ -501,6 +531,7 @@ def run_rank(args):
                 "batch_size": args.batch_size,
                 "streams": args.streams,
                 "threads": args.threads,
+                "create_writers": ecfg.create_writers,
                 "stream_steps": bool(args.stream_steps),
                 "pipelined_passes": not args.no_pipeline and not args.stream_steps,
                 "pipeline_depth": primary["pipeline_depth"],
@@ -522,6 +553,8 @@ def run_rank(args):
                                                "ms_per_step": round(wiped["ms_per_step"], 3),
                                                "steps": args.wipe_passes,
                                                "rank0_process_cpu_ms_per_step": wiped["rank0_process_cpu_ms_per_step"],
+                                               "cgroup_cpu_ms_per_step": wiped["cgroup_cpu_ms_per_step"],
+                                               "wipe_mode": args.wipe_mode,
                                                "rank0_stage_s": wiped["rank0_stage_s"]}
         if secondary is not None:
             rec["config"][other] = {k: (round(v, 3) if isinstance(v, float) else v) for k, v in secondary.items()
@@ -529,6 +562,8 @@ def run_rank(args):
                                              "own_time_imbalance", "pipeline_depth")}
         if sp is not None:
             rec["config"].setdefault("strong", {}).update(sp)
+        if cli is not None:
+            rec["config"]["cli_wall"] = cli
         if args.host_only:
             rec["metric"] = "host path only: DICOM loads + JPEG writes per s (GPU stages replaced by fixed segments)"
             rec["vs_baseline"] = None
@@ -557,6 +592,35 @@ def run_rank(args):
         for r in roots:
             shutil.rmtree(r, ignore_errors=True)
     return 0
+
+
+def cli_wall(args, world, data_root):
+    """config.cli_wall: `img_processing_parallel --gpus N --quiet --json` on the bench cohort, run
+    args.cli_runs times. Every invocation is a cold reference-style run: process start, HIP
+    initialisation, cohort discovery, per-patient output wipe (main_parallel.cpp:49-64), every
+    slice, exit. Median/min wall and the CLI's own phase split (hip_init_s, engine_ctor_s,
+    processing_wall_s)."""
+    from nm03_capstone_project_amd.utils.cli_wall import time_cli
+    exe = os.path.join(ROOT, "build", "bin", "img_processing_parallel")
+    if not os.path.exists(exe):
+        return {"skipped": f"{exe} not built"}
+    out = os.path.join(args.out_root, "cli")
+    js = os.path.join(args.out_root, "cli.json")
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK", "NM03_COMM_JOB")}
+    argv = [exe, "--gpus", str(world), "--data-root", data_root, "--out", out, "--quiet", "--json", js]
+    res = time_cli(argv, runs=args.cli_runs, json_path=js, env=env)
+    slices = None
+    try:
+        with open(js) as f:
+            slices = json.load(f).get("slices")
+    except (OSError, ValueError):
+        pass
+    res["cmd"] = f"img_processing_parallel --gpus {world} --quiet --json (cohort of {slices} slices)"
+    res["slices"] = slices
+    if slices and res["wall_median_s"] > 0:
+        res["slices_per_s_median"] = round(slices / res["wall_median_s"], 1)
+    return res
 
 
 def main(argv=None):

@@ -6,6 +6,8 @@
 //   loadDICOMFilesForPatient main_sequential.cpp:121-168 (main_parallel.cpp:261-308)
 #pragma once
 
+#include <cstdint>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -39,6 +41,34 @@ void setup_output_dir(const std::string& dir);
 // setup_output_dir for several directories on up to `threads` threads (first error rethrown).
 void setup_output_dirs(const std::vector<std::string>& dirs, int threads);
 void make_dirs(const std::string& dir);
+
+// The same wipe with the deletion taken off the caller's path. An existing directory is renamed to
+// a trash name beside it (".nm03-trash-<pid>-<n>", one rename under the parent's lock) and
+// re-created empty at once; `threads` background reaper threads delete the trash while the caller
+// goes on (drain() waits for them; the destructor drains too). Trash left behind by a killed run in
+// a parent directory is queued as well the first time that parent is seen.
+//
+// Why (tools/create_probe.cpp on the MI355X box, profiles/r4/create_probe/): creating and deleting
+// tmpfs files serialise on per-filesystem locks (inode accounting and the superblock's inode list),
+// not on the directory — one-directory-per-thread layouts measure the same. Deleting a JPEG pair
+// costs 5–12 µs of CPU on one thread and 23–35 µs with 16 threads deleting at once; done by 2
+// reaper threads beside the engine, the wipe costs a fraction of the CPU and no wall time.
+class OutputReaper {
+ public:
+  explicit OutputReaper(int threads = 2);
+  ~OutputReaper();
+  OutputReaper(const OutputReaper&) = delete;
+  OutputReaper& operator=(const OutputReaper&) = delete;
+  void wipe(const std::string& dir);  // throws like setup_output_dir
+  void wipe(const std::vector<std::string>& dirs);
+  void drain();                       // returns when every queued trash directory is gone
+  int64_t files_reaped() const;
+
+  struct Impl;
+
+ private:
+  std::unique_ptr<Impl> impl_;
+};
 
 // File stem ("…/1-14.dcm" → "1-14") and file name.
 std::string stem(const std::string& path);

@@ -68,22 +68,25 @@ struct EngineConfig {
   RenderParams render;
   bool export_jpeg = true;
   bool resume = false;  // skip items whose two JPEGs already exist (SURVEY §5.4 --resume)
-  // Replay each slot's per-batch kernel chain from a captured hipGraph (one graph per launch
-  // signature). Ignored (eager launches) when NM03_SYNC_LAUNCHES debugging is on. Off by default:
-  // measured on MI355X/ROCm 7.2 with 6 slots, replay ran at 85k slices/s vs 110k eager
-  // (profiles/graphs_ab.txt) — the chain is only 8 launches per 64 slices, so there is no launch
-  // overhead to win and graph launches lose cross-stream overlap.
-  bool graphs = false;
-  // Tapered batch schedule (small first and last batches; engine.cpp plan_batches). Off by default:
-  // measured 209k vs 220k slices/s (4 interleaved runs each) — the extra batches cost more than the
-  // shorter fill/drain gains. NM03_BATCH_TAPER=1 turns it on.
-  bool taper = false;
-  // Host path only (NM03_HOST_ONLY=1 also turns it on): no HIP call at all. Every load, parse,
+  // Host path only: no HIP call at all. Every load, parse,
   // 12-bit pack into the (pageable) upload blob and every JPEG file write runs exactly as in a
   // GPU run; the GPU stages are replaced by streaming a fixed pair of pre-encoded JPEG segments
   // into the output buffer (what the encoder's PCIe stores would leave in memory). Measures the
   // host side's CPU per slice on its own, on any machine (bench.py --host-only).
   bool host_only = false;
+  // Host-mapped bytes per image for the GPU encoder's stuffed output (0 = half the canvas: 128 KiB
+  // for 512², ~5x a typical medical render). Larger images are CPU re-encoded (StageTimes counts
+  // them); tests force that path with a tiny capacity.
+  uint32_t jpeg_out_cap = 0;
+  // Progressive upload: a batch's finished prefix of raw pixels is queued for H2D once it has grown
+  // by this many KiB while its loads still run (-1 = 2048; 0 = one upload per batch after all loads).
+  int upload_chunk_kb = -1;
+  // At most this many pool workers write a batch's JPEGs at once when its output directories are
+  // being filled (files created, not rewritten; 0 = no limit). tmpfs inode allocation serialises on
+  // per-filesystem locks: a JPEG pair costs ≈10 µs of CPU to create on one thread, ≈13–15 µs with
+  // 4 creating at once and 35–44 µs with 16 (tools/create_probe.cpp, profiles/r4/create_probe/);
+  // the other workers take the next batches' loads meanwhile.
+  int create_writers = 4;
 };
 
 // Everything test_pipeline exports / tests inspect for one slice (host copies).

@@ -40,7 +40,9 @@ std::vector<uint8_t> encode_scan_gray420(const uint8_t* gray, int width, int hei
 void write_jpeg_file(const std::string& path, const std::vector<uint8_t>& header, const uint8_t* scan,
                      size_t scan_len);
 // Same, `name` relative to the directory fd `dirfd` (openat: no path walk per file); `dir` only
-// names the file in error messages.
+// names the file in error messages. `creating`: the directory's creation hint (0 unknown, 1 the
+// directory is being filled — create with O_EXCL directly, 2 its files exist — open without O_CREAT
+// first); a missing file sets it to 1.
 void write_jpeg_at(int dirfd, const std::string& dir, const std::string& name, const std::vector<uint8_t>& header,
                    const uint8_t* scan, size_t scan_len,
                    std::atomic<uint8_t>* creating = nullptr);

@@ -15,6 +15,9 @@ void check_hip(hipError_t e, const char* what);
 void check_launch(const char* what);
 // NM03_SYNC_LAUNCHES=1: synchronise after every launch (debugging; disables graph capture).
 bool sync_launches();
+// Profiling variant of `kernel` ("jpeg", "median") from NM03_PROFILE_VARIANT="jpeg=12,median=1"; 0 = the
+// real kernel. Variants truncate the kernel for time splits; their output is invalid.
+int profile_variant(const char* kernel);
 
 // K1a: k×k median of raw keys → `med` (u16 keys, same layout as raw). k ∈ {3,5,7,9}.
 // Per-slice key range: with `tile_mm` (2 u32 per tile) each tile stores its (min, max) and
@@ -102,27 +105,18 @@ struct JpegRenderSrc {
   const float* f32 = nullptr;
   const uint64_t* bits = nullptr;
   const SliceStats* stats = nullptr;
+  // Render descriptors, one per canvas: JpegDesc k's `render` is either -1 (encode canvas k from
+  // `canvas`) or k itself (render descriptor k fused into the encoder). launch_jpeg checks that
+  // `nrd` covers every canvas when rd is set.
   const RenderDesc* rd = nullptr;
+  int nrd = 0;
 };
 void launch_jpeg(const uint8_t* canvas, const JpegDesc* jd, int ncanvas, int out_w, int out_h, const int32_t* div_luma,
                  JpegWork& w, uint8_t* out, int32_t* out_sizes, hipStream_t stream,
                  const JpegRenderSrc* fused = nullptr);
-// Compacts the encoder's per-canvas HBM segments (canvas k at k × stride) to 16-byte-aligned prefix
-// offsets in dst and mirrors the sizes into host_sizes (host-mapped); see jpeg_compact_offset.
-void launch_jpeg_gather(const uint8_t* src, uint32_t stride, const int32_t* sizes, int ncanvas, uint8_t* dst,
-                        int32_t* host_sizes, hipStream_t stream);
-// Host side of the same layout: offset of canvas k = Σ_{i<k} align16(max(size_i, 0)).
-inline size_t jpeg_compact_bytes(int32_t size) { return size > 0 ? ((size_t)size + 15) & ~(size_t)15 : 0; }
 // K6: binary threshold lo ≤ x ≤ hi → u8 0/1 (in 16-byte aligned, out 4-byte aligned).
 void launch_threshold(const float* in, uint8_t* out, size_t n, float lo, float hi, hipStream_t stream);
 
-// K0: expand a batch's uploaded raw region (12-bit packed or plain 16-bit slices, SliceDesc::blob_off
-// and flags) into the 16-bit sample buffer at SliceDesc::raw_off.
-// Shader copy of `bytes` from host-mapped pinned memory (device view) into device memory; 16-byte
-// aligned pointers.
-void launch_copy_from_host(const void* src, void* dst, size_t bytes, hipStream_t stream);
-void launch_unpack(const uint16_t* blob_raw, uint16_t* raw, const SliceDesc* descs, int nslices, int max_pixels,
-                   hipStream_t stream);
 // True when RenderDesc r is an exact 2× fit onto the canvas (the fused fast path applies).
 bool render_is_exact_2x(const RenderDesc& r, int out_w, int out_h);
 

@@ -44,4 +44,10 @@ struct FaultPlan {
 };
 const FaultPlan& fault_plan();  // parsed once from NM03_FAULT
 
+// Fatal-signal reporter for the native executables: on SIGSEGV/SIGBUS/SIGFPE/SIGILL/SIGABRT it
+// writes the signal, the faulting address and a symbolised backtrace (backtrace_symbols_fd, no
+// allocation) to stderr, then re-raises with the default action so the exit status is unchanged.
+// Runs on an alternate stack (a stack overflow still reports). Idempotent.
+void install_crash_handler();
+
 }  // namespace nm03

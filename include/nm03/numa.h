@@ -70,16 +70,10 @@ class Placement {
   const std::vector<int>& cpus() const { return cpus_; }
   // Pins the calling thread to the placement's CPUs (no-op when inactive).
   void bind_this_thread() const;
-  // Pins pool worker `i` of `n`. NM03_PIN=set (default): the whole CPU set, like bind_this_thread;
-  // NM03_PIN=core: one physical core of the set per worker (cores spread evenly over the set), so
-  // a worker never migrates and its staging buffers stay in that core's L2;
-  // NM03_PIN=l3: worker i floats within L3 domain (CCD) i mod groups() of the set.
-  void bind_worker(int i, int n) const;
-  // NM03_PIN=l3: the L3 domains (CCDs) of the set; work keyed to a domain (engine.cpp: slice
-  // i's load and export run on domain i mod groups()) keeps a file's page-cache lines in one L3
-  // across passes instead of bouncing them between CCDs. 1 otherwise.
-  int groups() const { return l3_groups_.empty() ? 1 : (int)l3_groups_.size(); }
-  int worker_group(int i) const { return l3_groups_.empty() ? 0 : i % (int)l3_groups_.size(); }
+  // Pool workers float over the whole set (bind_this_thread). Measured and removed in round 4:
+  // one physical core per worker (NM03_PIN=core: host-only 283–304k vs 365–392k slices/s) and
+  // workers + work keyed to L3 domains (NM03_PIN=l3: writes get slower when the threads spread
+  // over more L3 domains, 17 → 29 µs per JPEG pair; profiles/r3/host_pin/, profiles/r3/pin_l3/).
   // Runs `f` with the calling thread temporarily pinned (first-touch / pinned allocations land on
   // the node), restoring the previous affinity afterwards.
   template <class F>
@@ -95,8 +89,6 @@ class Placement {
  private:
   int node_ = -1;
   std::vector<int> cpus_;
-  std::vector<std::vector<int>> cores_;      // cpus_ grouped by physical core (NM03_PIN=core)
-  std::vector<std::vector<int>> l3_groups_;  // cpus_ grouped by L3 domain (NM03_PIN=l3)
 };
 
 }  // namespace nm03::numa

@@ -90,22 +90,16 @@ class ThreadPool {
   }
   // Spin (polling the queue size without the lock) for up to spin_us before sleeping on the
   // condition variable: a task submitted shortly after the queue ran dry starts without a futex
-  // wake-up and the scheduler's wake-up latency (NM03_POOL_SPIN_US, default 200; 0 = sleep at once).
+  // wake-up and the scheduler's wake-up latency.
   // Measured on the shared boxes (profiles/r3/pool_spin/): 0 / 50 / 200 µs gave 329–398k /
   // 345–398k / 357–398k slices/s over 4 interleaved rounds at equal host CPU per step — equal on
   // quiet boxes, up to +20% when other tenants load the host (delayed wake-ups).
-  static int spin_us() {
-    static const int us = [] {
-      const char* e = std::getenv("NM03_POOL_SPIN_US");
-      return e && *e ? std::max(0, std::atoi(e)) : 200;
-    }();
-    return us;
-  }
+  static constexpr int kSpinUs = 200;
   void loop() {
     for (;;) {
       std::function<void()> f;
-      if (const int us = spin_us(); us > 0 && queued_.load(std::memory_order_relaxed) == 0) {
-        const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(us);
+      if (queued_.load(std::memory_order_relaxed) == 0) {
+        const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(kSpinUs);
         while (queued_.load(std::memory_order_relaxed) == 0 && !stop_flag_.load(std::memory_order_relaxed) &&
                std::chrono::steady_clock::now() < until)
           __builtin_ia32_pause();
@@ -155,12 +149,18 @@ class TaskGroup {
         },
         prio);
   }
-  // fn(i) for i in [0, n): min(n, pool size) runners pull indices from a shared counter. With
-  // `cpu_ns`, each runner adds the thread CPU time of its whole share (two clock reads per runner
-  // instead of two per item: a thread-CPU clock read is a system call, ≈0.3 µs).
-  void for_each(size_t n, std::function<void(size_t)> fn, uint64_t prio = 0, std::atomic<int64_t>* cpu_ns = nullptr) {
+  // fn(i) for i in [0, n): min(n, pool size, max_runners) runners pull indices from a shared
+  // counter. `max_runners` > 0 bounds how many items run concurrently (file creation on tmpfs: the
+  // inode allocation and release serialise on per-filesystem locks, so 16 concurrent creators
+  // cost 3.7x the CPU per file of one, tools/create_probe.cpp); the other workers take other
+  // tasks meanwhile. With `cpu_ns`, each runner adds the thread CPU time of its whole share (two
+  // clock reads per runner instead of two per item: a thread-CPU clock read is a system call).
+  void for_each(size_t n, std::function<void(size_t)> fn, uint64_t prio = 0, std::atomic<int64_t>* cpu_ns = nullptr,
+                int max_runners = 0) {
     if (n == 0) return;
-    const int runners = (int)std::min<size_t>(n, (size_t)pool_.size());
+    size_t cap = (size_t)pool_.size();
+    if (max_runners > 0) cap = std::min(cap, (size_t)max_runners);
+    const int runners = (int)std::min<size_t>(n, cap);
     auto st = std::make_shared<ForEach>();
     st->n = n;
     st->fn = std::move(fn);
@@ -179,55 +179,10 @@ class TaskGroup {
         },
         prio);
   }
-  // for_each with affinity: item i belongs to group group_of(i) ∈ [0, groups); a runner on a pool
-  // worker of group worker_group(ThreadPool::current_worker()) takes its own group's items first
-  // (in index order), then steals from the other groups — so work keyed to a group runs on that
-  // group's CPUs whenever they keep up, and no runner idles while items remain.
-  void for_each_grouped(size_t n, std::function<void(size_t)> fn, int groups, const std::function<int(size_t)>& group_of,
-                        std::function<int(int)> worker_group, uint64_t prio = 0,
-                        std::atomic<int64_t>* cpu_ns = nullptr) {
-    if (n == 0) return;
-    if (groups <= 1) {
-      for_each(n, std::move(fn), prio, cpu_ns);
-      return;
-    }
-    auto st = std::make_shared<Grouped>();
-    st->lists.resize((size_t)groups);
-    for (size_t i = 0; i < n; ++i) st->lists[(size_t)(group_of(i) % groups)].push_back(i);
-    st->next = std::make_unique<std::atomic<size_t>[]>((size_t)groups);
-    for (int g = 0; g < groups; ++g) st->next[g].store(0, std::memory_order_relaxed);
-    st->fn = std::move(fn);
-    st->worker_group = std::move(worker_group);
-    const int runners = (int)std::min<size_t>(n, (size_t)pool_.size());
-    {
-      std::lock_guard<std::mutex> g(m_);
-      pending_ += (size_t)runners;
-      pending_a_.store(pending_, std::memory_order_release);
-    }
-    pool_.submit_n(
-        runners,
-        [this, st, cpu_ns, groups] {
-          const int64_t c0 = cpu_ns ? thread_cpu_now_ns() : 0;
-          const int w = ThreadPool::current_worker();
-          const int home = w >= 0 ? st->worker_group(w) % groups : 0;
-          for (int k = 0; k < groups; ++k) {
-            const size_t g = (size_t)((home + k) % groups);
-            const auto& list = st->lists[g];
-            for (size_t j; (j = st->next[g].fetch_add(1)) < list.size();) st->fn(list[j]);
-          }
-          if (cpu_ns) cpu_ns->fetch_add(thread_cpu_now_ns() - c0, std::memory_order_relaxed);
-          done(1);
-        },
-        prio);
-  }
   // With spin_us > 0, spins that long on the pending count before sleeping: the waiter then
-  // continues without a wake-up (NM03_WAIT_SPIN_US overrides).
+  // continues without a wake-up.
   void wait(int spin_us = 0) {
-    static const int env = [] {
-      const char* e = std::getenv("NM03_WAIT_SPIN_US");
-      return e && *e ? std::max(0, std::atoi(e)) : -1;
-    }();
-    const int spin = env >= 0 ? env : spin_us;
+    const int spin = spin_us;
     if (spin > 0 && pending_a_.load(std::memory_order_acquire) != 0) {
       const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(spin);
       while (pending_a_.load(std::memory_order_acquire) != 0 && std::chrono::steady_clock::now() < until)
@@ -243,12 +198,6 @@ class TaskGroup {
     std::atomic<size_t> next{0};
     size_t n = 0;
     std::function<void(size_t)> fn;
-  };
-  struct Grouped {
-    std::vector<std::vector<size_t>> lists;
-    std::unique_ptr<std::atomic<size_t>[]> next;
-    std::function<void(size_t)> fn;
-    std::function<int(int)> worker_group;
   };
   void done(size_t k) {
     std::lock_guard<std::mutex> g(m_);

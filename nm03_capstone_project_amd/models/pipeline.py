@@ -49,8 +49,6 @@ class PipelineConfig:
     device: int = 0
     export_jpeg: bool = True
     resume: bool = False
-    graphs: bool = False  # replay per-batch kernel chains from captured hipGraphs (slower, see engine.h)
-    taper: bool = False  # small first/last batches (measured slower, see engine.h)
     host_only: bool = False  # host path only, no GPU (loads + JPEG writes with fixed segments, engine.h)
 
     _PIPE = ("norm_low", "norm_high", "norm_min", "norm_max", "clip_min", "clip_max", "median_window",
@@ -81,8 +79,6 @@ class PipelineConfig:
         c.render = self.render_params()
         c.export_jpeg = self.export_jpeg
         c.resume = self.resume
-        c.graphs = self.graphs
-        c.taper = self.taper
         c.host_only = self.host_only
         return c
 

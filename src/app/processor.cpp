@@ -107,6 +107,7 @@ int visible_gpu_count() {
 }
 
 AppConfig parse_args(int argc, char** argv, const std::string& which) {
+  install_crash_handler();
   AppConfig c;
   c.data_root = cohort::default_data_root();
   c.out_dir = which == "test_pipeline" ? "../out-test" : which == "img_processing_sequential" ? "../out-sequential" : "../out-parallel";
@@ -186,6 +187,9 @@ int run_sequential(const AppConfig& cfg) {
         if (fast_exit_enabled()) (void)e.release();
       }
     } leak{engine_p};
+    // Patient directories are wiped by renaming them aside; the deletions run on background threads
+    // while the engine works (cohort.h OutputReaper) and are waited for before the run ends.
+    cohort::OutputReaper reaper(2);
     const double t0 = now_s();
     StageTimes total;
     int64_t slices = 0, slices_ok = 0;
@@ -213,7 +217,7 @@ int run_sequential(const AppConfig& cfg) {
               if (cfg.engine.resume)
                 cohort::make_dirs(out);
               else
-                cohort::setup_output_dir(out);
+                reaper.wipe(out);
             } catch (const std::exception& e) {
               throw std::runtime_error(std::string("Error setting up output directory: ") + e.what());
             }
@@ -278,6 +282,7 @@ int run_sequential(const AppConfig& cfg) {
       std::cout << "\n=== All Processing Completed ===\n" << std::endl;                              // :340
       std::cout << "Successfully processed " << successful << "/" << patients.size() << " patients." << std::endl;  // :341
     }
+    reaper.drain();
     const double wall = now_s() - t0;
     write_json(cfg.json, std::string("{\"mode\": \"sequential\", \"gpus\": 1, \"wall_s\": ") + fmt(wall) +
                              ", \"slices\": " + std::to_string(slices) + ", \"slices_ok\": " + std::to_string(slices_ok) +
@@ -426,6 +431,10 @@ int parallel_rank(const AppConfig& cfg, int rank, int size, Comm& comm, int devi
   double proc_wall = 0, my_wall = 0;
   int64_t total_ok = 0, total_slices = 0, my_slices = 0, my_ok = 0;
   StageTimes agg;
+  // Rank 0 wipes the patient directories by renaming them aside; 2 background threads delete the
+  // old files while the ranks process (cohort.h OutputReaper), waited for before the run ends.
+  std::unique_ptr<cohort::OutputReaper> reaper;
+  if (rank == 0 && !cfg.engine.resume) reaper = std::make_unique<cohort::OutputReaper>(2);
   for (int rep = 0; rep < cfg.repeat; ++rep) {
     // ---- plan on rank 0 --------------------------------------------------------------------
     std::vector<uint8_t> plan_bytes;
@@ -451,7 +460,7 @@ int parallel_rank(const AppConfig& cfg, int rank, int size, Comm& comm, int devi
             if (cfg.engine.resume)
               cohort::make_dirs(p.out_dir);
             else
-              cohort::setup_output_dir(p.out_dir);
+              reaper->wipe(p.out_dir);
             p.setup_ok = true;
             cohort::Series s = cohort::list_patient_series(base, pid);
             p.series_dir = s.series_dir;
@@ -635,6 +644,7 @@ int parallel_rank(const AppConfig& cfg, int rank, int size, Comm& comm, int devi
       }
     }
   }
+  if (reaper) reaper->drain();
   double tot = now_s() - t_start;
   comm.allreduce_max_f64(&tot, 1);
   // Per-rank stage figures, all-gathered (fields: kRankFields).

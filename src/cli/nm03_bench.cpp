@@ -18,10 +18,12 @@
 #include <memory>
 #include <string>
 
+#include "nm03/app.h"
 #include "nm03/cohort.h"
 #include "nm03/engine.h"
 #include "nm03/golden.h"
 #include "nm03/jpeg.h"
+#include "nm03/log.h"
 #include "nm03/thread_pool.h"
 #include "nm03/volume.h"
 
@@ -30,6 +32,7 @@ static double now_s() {
 }
 
 int main(int argc, char** argv) {
+  nm03::install_crash_handler();
   std::string config = "cohort", root = nm03::cohort::default_data_root(), out = "/tmp/nm03_bench_out";
   int steps = 10, warmup = 2;
   nm03::EngineConfig ec;
@@ -242,7 +245,13 @@ int main(int argc, char** argv) {
     }
   } catch (const std::exception& e) {
     std::cerr << "Fatal error: " << e.what() << std::endl;
-    return 1;
+    return nm03::app::cli_exit(1);
   }
-  return 0;
+  // Like the CLIs: flush and _exit, no static destructors. Under rocprofv3 the process used to die
+  // with SIGSEGV after main returned (exit 139): the crash handler's backtrace shows the fault in
+  // libamdhip64's own static destructor (__cxa_finalize → libamdhip64 → libhsa-runtime64), after
+  // rocprofv3's "tool finalization" — HIP's exit-time teardown calls into an HSA runtime the
+  // profiler's tool has already finalised. No nm03 frame is on that stack; the results were
+  // complete. Skipping the exit-time teardown removes the fault (gpurun_out r4, profiles/r4/).
+  return nm03::app::cli_exit(0);
 }

@@ -2,14 +2,22 @@
 
 #include <dirent.h>
 #include <fcntl.h>
+#include <linux/capability.h>
+#include <pthread.h>
+#include <sys/stat.h>
+#include <sys/syscall.h>
 #include <unistd.h>
 
 #include <algorithm>
 #include <atomic>
 #include <cerrno>
+#include <condition_variable>
+#include <deque>
 #include <mutex>
+#include <set>
 #include <thread>
 #include <cstdlib>
+#include <cstring>
 #include <filesystem>
 #include <stdexcept>
 #include <system_error>
@@ -146,6 +154,147 @@ void setup_output_dirs(const std::vector<std::string>& dirs, int threads) {
   for (auto& t : th) t.join();
   if (!err.empty()) throw std::runtime_error(err);
 }
+
+namespace {
+
+// Deletes everything under `dir` and `dir` itself; returns the number of files unlinked.
+int64_t remove_tree(const std::string& dir) {
+  const int dfd = ::open(dir.c_str(), O_RDONLY | O_DIRECTORY | O_CLOEXEC);
+  if (dfd < 0) return 0;
+  DIR* d = ::fdopendir(dfd);
+  if (!d) {
+    ::close(dfd);
+    return 0;
+  }
+  std::vector<std::string> files, subdirs;
+  while (dirent* e = ::readdir(d)) {
+    const char* nm = e->d_name;
+    if (nm[0] == '.' && (nm[1] == 0 || (nm[1] == '.' && nm[2] == 0))) continue;
+    (e->d_type == DT_DIR ? subdirs : files).push_back(nm);
+  }
+  int64_t n = 0;
+  for (const auto& f : files) {
+    if (::unlinkat(dfd, f.c_str(), 0) == 0)
+      ++n;
+    else if (errno == EISDIR)
+      subdirs.push_back(f);
+  }
+  ::closedir(d);
+  for (const auto& sd : subdirs) n += remove_tree(dir + "/" + sd);
+  ::rmdir(dir.c_str());
+  return n;
+}
+
+constexpr const char* kTrashPrefix = ".nm03-trash-";
+
+}  // namespace
+
+struct OutputReaper::Impl {
+  std::mutex m;
+  std::condition_variable cv, idle_cv;
+  std::deque<std::string> q;
+  size_t busy = 0;
+  bool stop = false;
+  std::atomic<int64_t> files{0};
+  std::atomic<uint64_t> seq{0};
+  std::set<std::string> parents_seen;  // guarded by m
+  std::vector<std::thread> threads;
+
+  void push(std::string p) {
+    {
+      std::lock_guard<std::mutex> g(m);
+      q.push_back(std::move(p));
+    }
+    cv.notify_one();
+  }
+  void run() {
+    pthread_setname_np(pthread_self(), "nm03-reaper");
+    // Own fd table and cred, like the engine's pool workers (engine.cpp): no shared fd-table lock
+    // or cred refcount line with the writers.
+#ifndef CLOSE_RANGE_UNSHARE
+#define CLOSE_RANGE_UNSHARE (1U << 1)
+#endif
+    (void)::syscall(SYS_close_range, 3u, ~0u, CLOSE_RANGE_UNSHARE);
+    __user_cap_header_struct h{_LINUX_CAPABILITY_VERSION_3, 0};
+    __user_cap_data_struct c[2]{};
+    if (::syscall(SYS_capget, &h, c) == 0) (void)::syscall(SYS_capset, &h, c);
+    for (;;) {
+      std::string p;
+      {
+        std::unique_lock<std::mutex> g(m);
+        cv.wait(g, [&] { return stop || !q.empty(); });
+        if (q.empty()) return;
+        p = std::move(q.front());
+        q.pop_front();
+        ++busy;
+      }
+      files += remove_tree(p);
+      {
+        std::lock_guard<std::mutex> g(m);
+        --busy;
+        if (q.empty() && busy == 0) idle_cv.notify_all();
+      }
+    }
+  }
+  // Stale trash of killed runs in `parent` (first time the parent is seen).
+  void sweep_parent(const std::string& parent) {
+    {
+      std::lock_guard<std::mutex> g(m);
+      if (!parents_seen.insert(parent).second) return;
+    }
+    DIR* d = ::opendir(parent.c_str());
+    if (!d) return;
+    std::vector<std::string> stale;
+    while (dirent* e = ::readdir(d))
+      if (std::strncmp(e->d_name, kTrashPrefix, std::strlen(kTrashPrefix)) == 0) stale.push_back(e->d_name);
+    ::closedir(d);
+    for (auto& n : stale) push(parent + "/" + n);
+  }
+};
+
+OutputReaper::OutputReaper(int threads) : impl_(std::make_unique<Impl>()) {
+  for (int t = 0; t < std::max(1, threads); ++t) impl_->threads.emplace_back([this] { impl_->run(); });
+}
+
+OutputReaper::~OutputReaper() {
+  drain();
+  {
+    std::lock_guard<std::mutex> g(impl_->m);
+    impl_->stop = true;
+  }
+  impl_->cv.notify_all();
+  for (auto& t : impl_->threads) t.join();
+}
+
+void OutputReaper::wipe(const std::string& dir_in) {
+  std::string dir = dir_in;
+  while (dir.size() > 1 && dir.back() == '/') dir.pop_back();
+  const size_t slash = dir.rfind('/');
+  const std::string parent = slash == std::string::npos ? "." : slash == 0 ? "/" : dir.substr(0, slash);
+  make_dirs(parent);
+  impl_->sweep_parent(parent);
+  const std::string trash = parent + "/" + kTrashPrefix + std::to_string(::getpid()) + "-" +
+                            std::to_string(impl_->seq.fetch_add(1));
+  if (::rename(dir.c_str(), trash.c_str()) == 0) {
+    impl_->push(trash);
+  } else if (errno != ENOENT) {
+    setup_output_dir(dir);  // not renamable (a mount point, another file system): wipe in place
+    return;
+  }
+  if (::mkdir(dir.c_str(), 0755) != 0 && errno != EEXIST)
+    throw std::runtime_error("Failed to setup output directory: " + dir + " (" + std::strerror(errno) + ")");
+}
+
+void OutputReaper::wipe(const std::vector<std::string>& dirs) {
+  for (const auto& d : dirs) wipe(d);
+}
+
+void OutputReaper::drain() {
+  std::unique_lock<std::mutex> g(impl_->m);
+  impl_->idle_cv.wait(g, [&] { return impl_->q.empty() && impl_->busy == 0; });
+}
+
+int64_t OutputReaper::files_reaped() const { return impl_->files.load(); }
 
 std::string stem(const std::string& path) { return fs::path(path).stem().string(); }
 std::string filename(const std::string& path) { return fs::path(path).filename().string(); }

@@ -391,7 +391,19 @@ const Header& SliceFile::header(std::vector<uint8_t>& buf) {
     size_ = got;
     size_known_ = true;
     have_ = size_;
-    h_ = parse(buf.data(), size_);
+    try {
+      h_ = parse(buf.data(), size_);
+    } catch (const SliceError&) {
+      // A short read is normally the end of the file, but a read can also come back short
+      // without reaching it (a signal on a thread that does not block them, NFS/FUSE): before
+      // reporting a truncated file, check the size and finish the read.
+      stat_size();
+      if (size_ <= got) throw;
+      if (buf.size() < size_) buf.resize(size_);
+      pread_all(buf.data() + got, size_ - got, got);
+      have_ = size_;
+      h_ = parse(buf.data(), size_);
+    }
     whole_ = true;
     return h_;
   }

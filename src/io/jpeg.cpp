@@ -212,7 +212,7 @@ void write_jpeg_at(int dirfd, const std::string& dir, const std::string& name, c
   // A file this call creates (O_EXCL) is empty, so its size needs no fstat afterwards.
   int fd = -1;
   bool fresh = false;
-  if (creating && !creating->load(std::memory_order_relaxed)) {
+  if (creating && creating->load(std::memory_order_relaxed) != 1) {
     fd = ::openat(dirfd, name.c_str(), O_WRONLY | O_CLOEXEC);
     if (fd < 0 && errno == ENOENT) creating->store(1, std::memory_order_relaxed);
   }

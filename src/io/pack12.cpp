@@ -51,22 +51,11 @@ __attribute__((target("avx2"))) inline void pack16(const uint16_t* src, uint8_t*
   _mm_storeu_si128(reinterpret_cast<__m128i*>(d + 12), _mm256_extracti128_si256(c, 1));
 }
 
-// Bounce → destination copy: streaming (non-temporal) stores by default; NM03_PACK_NT=0 uses
-// regular cached stores (A/B: the DMA upload may then read recently packed lines from the CPU
-// caches instead of DRAM).
-inline bool pack_nt() {
-  static const bool on = [] {
-    const char* e = std::getenv("NM03_PACK_NT");
-    return !(e && *e == '0');
-  }();
-  return on;
-}
-inline void bounce_out(uint8_t* dst, const uint8_t* src, size_t bytes) {
-  if (pack_nt())
-    dicom::stream_copy_unfenced(dst, src, bytes);
-  else
-    std::memcpy(dst, src, bytes);
-}
+// Bounce → destination copy with streaming (non-temporal) stores. Cached stores were measured in
+// round 3 (would the DMA upload read recently packed lines from the CPU caches instead of DRAM?):
+// 292–314k vs 369–389k slices/s — they read every destination line for ownership and evict the
+// loaders' working set (profiles/r3/pack_nt/ab.txt).
+inline void bounce_out(uint8_t* dst, const uint8_t* src, size_t bytes) { dicom::stream_copy_unfenced(dst, src, bytes); }
 
 // Packs and range-checks in the same pass (one read of the samples): returns false — dst then
 // holds garbage the caller must not use — when some sample needs more than 12 bits.
@@ -122,7 +111,6 @@ __attribute__((target("avx2,avx512f,avx512bw,avx512vbmi"))) bool pack_stream_avx
 
 bool use_avx512() {
   static const bool ok = [] {
-    if (const char* e = std::getenv("NM03_PACK_AVX512"); e && *e == '0') return false;
     return __builtin_cpu_supports("avx512f") && __builtin_cpu_supports("avx512bw") &&
            __builtin_cpu_supports("avx512vbmi");
   }();

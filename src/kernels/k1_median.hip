@@ -235,10 +235,7 @@ void launch_median(const uint16_t* raw, uint16_t* med, const SliceDesc* descs, c
   if (blob && !raw_out) throw DeviceError("launch_median: blob input needs a raw_out buffer");
   if (ntiles <= 0) return;
   dim3 grid(ntiles), block(256);
-  static const int dbg = [] {  // NM03_MEDIAN_DBG=1: profiling variant (output invalid)
-    const char* e = std::getenv("NM03_MEDIAN_DBG");
-    return e ? std::atoi(e) : 0;
-  }();
+  static const int dbg = profile_variant("median");  // 1: tile load + store only (output invalid)
   switch (k) {
     case 3: median_kernel<3><<<grid, block, 0, stream>>>(raw, med, descs, tiles, stats, tile_mm, dbg, blob, raw_out); break;
     case 5: median_kernel<5><<<grid, block, 0, stream>>>(raw, med, descs, tiles, stats, tile_mm, dbg, blob, raw_out); break;

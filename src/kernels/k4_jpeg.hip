@@ -762,21 +762,10 @@ void launch_jpeg(const uint8_t* canvas, const JpegDesc* jd, int ncanvas, int out
   const int parts = (bpi + kJpegWG - 1) / kJpegWG;
   if ((size_t)parts * ncanvas > w.look_cap) throw DeviceError("launch_jpeg: look-back capacity exceeded");
   w.look_used = (size_t)parts * ncanvas;
-  // NM03_JPEG_DBG selects truncated profiling variants (output invalid; tools/gpu_jpeg_split.sh).
-  static const int dbg = [] {
-    const char* e = std::getenv("NM03_JPEG_DBG");
-    const char* f = std::getenv("NM03_JPEG_FLAT");      // 0: no flat-wave path (A/B)
-    const char* sp = std::getenv("NM03_JPEG_SPREAD");   // 0: blocked image order (A/B)
-    const char* sw = std::getenv("NM03_JPEG_SWIZZLE");  // 0: plain staged rows (A/B)
-    return (e ? std::atoi(e) & 0xFF : 0) | (f && std::atoi(f) == 0 ? 0x100 : 0) | (sp && std::atoi(sp) == 0 ? 0x400 : 0) |
-           (sw && std::atoi(sw) == 0 ? 0x800 : 0);
-  }();
-  // NM03_JPEG_LDS_PAD: extra dynamic LDS per workgroup (caps the encoder's residency per CU so
-  // other streams' kernels keep LDS to run alongside it).
-  static const int pad = [] {
-    const char* e = std::getenv("NM03_JPEG_LDS_PAD");
-    return e ? std::atoi(e) : 0;
-  }();
+  // NM03_PROFILE_VARIANT=jpeg=N selects truncated profiling variants (output invalid;
+  // tools/gpu_jpeg_split.sh).
+  static const int dbg = profile_variant("jpeg") & 0xFF;
+  if (rs.rd && rs.nrd < ncanvas) throw DeviceError("launch_jpeg: fewer render descriptors than canvases");
   // The look-back records (3 words per workgroup) start unpublished. Eager launches alternate
   // between two halves of the look area, each launch clearing the half the previous one used
   // (stream order makes that safe); captured launches (hipGraph replay repeats the arguments)
@@ -795,57 +784,9 @@ void launch_jpeg(const uint8_t* canvas, const JpegDesc* jd, int ncanvas, int out
     w.look_base = w.look_base ? 0 : half;
     w.prev_words = words;
   }
-  static const int occ = [] {
-    const char* e = std::getenv("NM03_JPEG_OCC");
-    return e && std::atoi(e) == 5 ? 5 : 4;
-  }();
-  if (occ == 5)
-    jpeg_fused_kernel<5, kPatchLds + 232><<<parts * ncanvas, kJpegWG, pad, stream>>>(
-        canvas, jd, ncanvas, out_w, out_h, q, w, rs, out, out_sizes, dbg);
-  else
-    jpeg_fused_kernel<4, kUnionWords><<<parts * ncanvas, kJpegWG, pad, stream>>>(canvas, jd, ncanvas, out_w, out_h, q, w,
-                                                                                  rs, out, out_sizes, dbg);
+  jpeg_fused_kernel<4, kUnionWords><<<parts * ncanvas, kJpegWG, 0, stream>>>(canvas, jd, ncanvas, out_w, out_h, q, w,
+                                                                              rs, out, out_sizes, dbg);
   check_launch("jpeg_fused_kernel");
-}
-
-// Compaction of the encoder's HBM output for one SDMA copy to the host (engine NM03_JPEG_D2H=1/2, opt-in): canvas k's
-// segment moves from k × stride to the 16-byte-aligned prefix sum of the earlier segments' sizes
-// (a negative size — capacity overflow, re-encoded on the CPU — counts as 0). One workgroup per
-// (16 KiB column, canvas); wave 0 of every workgroup sums the ≤ cap earlier sizes from HBM, which is
-// cheaper than a separate scan launch. The sizes are mirrored into host-mapped memory for the host,
-// which derives the same offsets (jpeg_compact_bytes). Motivation: the encoder takes 96 µs per
-// 64-slice batch storing into host-mapped memory and 75 µs storing into HBM (profiles/r2/jpeg_devout/);
-// the copy that then has to follow costs more than it saves (engine.cpp, jpeg_d2h_).
-__global__ __launch_bounds__(256) void jpeg_gather_kernel(const uint8_t* __restrict__ src, uint32_t stride,
-                                                          const int32_t* __restrict__ sizes,
-                                                          uint8_t* __restrict__ dst, int32_t* __restrict__ host_sizes) {
-  const int k = blockIdx.y;
-  __shared__ uint32_t s_off;
-  if (threadIdx.x < 64) {
-    uint32_t acc = 0;
-    for (int i = threadIdx.x; i < k; i += 64) {
-      const int32_t z = sizes[i];
-      acc += z > 0 ? ((uint32_t)z + 15u) & ~15u : 0u;
-    }
-    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
-    if (threadIdx.x == 0) s_off = acc;
-  }
-  const int32_t z = sizes[k];
-  if (blockIdx.x == 0 && threadIdx.x == 0) host_sizes[k] = z;
-  __syncthreads();
-  if (z <= 0) return;
-  const uint32_t n16 = ((uint32_t)z + 15u) >> 4;
-  const uint4* s4 = reinterpret_cast<const uint4*>(src + (size_t)k * stride);
-  uint4* d4 = reinterpret_cast<uint4*>(dst + s_off);
-  for (uint32_t w = blockIdx.x * 256 + threadIdx.x; w < n16; w += gridDim.x * 256) d4[w] = s4[w];
-}
-
-void launch_jpeg_gather(const uint8_t* src, uint32_t stride, const int32_t* sizes, int ncanvas, uint8_t* dst,
-                        int32_t* host_sizes, hipStream_t stream) {
-  if (ncanvas <= 0) return;
-  if (stride % 16) throw DeviceError("launch_jpeg_gather: canvas stride must be a multiple of 16");
-  jpeg_gather_kernel<<<dim3(4, ncanvas), 256, 0, stream>>>(src, stride, sizes, dst, host_sizes);
-  check_launch("jpeg_gather_kernel");
 }
 
 }  // namespace nm03::gpu

@@ -272,8 +272,9 @@ PYBIND11_MODULE(_nm03, m) {
       .def_readwrite("render", &EngineConfig::render)
       .def_readwrite("export_jpeg", &EngineConfig::export_jpeg)
       .def_readwrite("resume", &EngineConfig::resume)
-      .def_readwrite("graphs", &EngineConfig::graphs)
-      .def_readwrite("taper", &EngineConfig::taper)
+      .def_readwrite("jpeg_out_cap", &EngineConfig::jpeg_out_cap)
+      .def_readwrite("upload_chunk_kb", &EngineConfig::upload_chunk_kb)
+      .def_readwrite("create_writers", &EngineConfig::create_writers)
       .def_readwrite("host_only", &EngineConfig::host_only);
 
   m.def("reference_seeds", [](int w, int h) {
@@ -430,6 +431,17 @@ PYBIND11_MODULE(_nm03, m) {
     py::gil_scoped_release nogil;
     cohort::setup_output_dirs(dirs, threads);
   }, py::arg("dirs"), py::arg("threads") = 8);
+  py::class_<cohort::OutputReaper>(m, "OutputReaper")
+      .def(py::init<int>(), py::arg("threads") = 2)
+      .def("wipe", [](cohort::OutputReaper& r, const std::vector<std::string>& dirs) {
+        py::gil_scoped_release nogil;
+        r.wipe(dirs);
+      })
+      .def("drain", [](cohort::OutputReaper& r) {
+        py::gil_scoped_release nogil;
+        r.drain();
+      })
+      .def_property_readonly("files_reaped", &cohort::OutputReaper::files_reaped);
   m.def(
       "synth_cohort",
       [](const std::string& root, int patients, int min_slices, int max_slices, int rows, int cols, uint64_t seed,

@@ -21,7 +21,6 @@
 #include <cstring>
 #include <deque>
 #include <unordered_map>
-#include <map>
 #include <mutex>
 #include <thread>
 
@@ -45,12 +44,6 @@ namespace {
 
 constexpr size_t kAlign = 256;
 inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
-// NM03_SEPARATE_UNPACK=1: expand the upload with the standalone K0 pass instead of inside the
-// median's tile load (A/B switch; both produce identical buffers).
-bool separate_unpack() {
-  const char* e = std::getenv("NM03_SEPARATE_UNPACK");  // read per batch: tests flip it in-process
-  return e && e[0] && e[0] != '0';
-}
 // CPU time of the calling thread (ns): loader/writer tasks report it next to their wall time, so a
 // CPU-quota stall or preemption (wall ≫ cpu) can be told apart from work (wall ≈ cpu).
 inline int64_t thread_cpu_ns() {
@@ -92,7 +85,6 @@ struct Slot {
          raw_base = 0, blob_bytes = 0;
   size_t max_medt = 0, max_shpt = 0;
   uint8_t* h_blob = nullptr;
-  uint8_t* d_hblob = nullptr;  // device view of h_blob (shader uploads of small batches), or null
   uint8_t* h_single = nullptr;  // run_single's pinned read-back area (allocated on first use)
   size_t single_bytes = 0;
   uint8_t* d_blob = nullptr;
@@ -105,17 +97,12 @@ struct Slot {
   size_t plane_words = 0;
   uint8_t* d_canvas = nullptr;
   JpegWork jw;
+  // The encoder stores each canvas's stuffed bytes straight into host-mapped h_out over PCIe
+  // (canvas k at k × out_cap). Measured alternatives, removed in round 4 (docs/ARCHITECTURE.md §6):
+  // HBM + gather kernel + one SDMA copy (the D2H copies share the copy engines with the uploads:
+  // 138-242k vs 286-340k slices/s) and HBM + a gather kernel storing into host memory (no gain).
   uint8_t* h_out = nullptr;
   uint8_t* d_out = nullptr;
-  // JPEG D2H modes (opt-in, NM03_JPEG_D2H=1/2, see jpeg_d2h_): the encoder writes its segments to
-  // d_jraw (HBM, canvas k at k × out_cap) and jpeg_gather_kernel packs them — into d_jcomp for one
-  // SDMA copy into h_out (plain pinned memory), or straight into host-mapped h_out; h_sizes stays
-  // host-mapped. Default (0): the encoder stores straight into host-mapped h_out over PCIe.
-  uint8_t* d_jraw = nullptr;
-  uint8_t* d_jcomp = nullptr;
-  int32_t* d_jsizes = nullptr;
-  size_t jcopied = 0;              // bytes of d_jcomp copied by the batch's first D2H
-  std::vector<size_t> jofs;        // per-canvas offsets into h_out (D2H mode)
   int32_t* h_sizes = nullptr;
   int32_t* d_sizes = nullptr;
   std::atomic<size_t> raw_used{0};
@@ -143,16 +130,9 @@ struct Slot {
   bool any_canvas = false;  // some image of the batch needs the generic render → canvas path
   int max_w = 0, max_h = 0;
   double batch_ema_s = 0;  // enqueue → completion time per slice of recent batches (wait_batch)
-  // NM03_LOAD_MODE=mapped: per-slot reserved address range; slice i of a batch maps its file at
-  // map_region + i * map_stride and the whole range is unmapped once after the batch's loads.
-  uint8_t* map_region = nullptr;
-  size_t map_stride = 0;
   // Host-only engine (EngineConfig::host_only): h_blob / h_out are plain mappings, no device side.
   bool host_only = false;
   size_t out_bytes = 0;
-  // Captured kernel chains keyed by launch signature (see GraphKey in build_and_run). Every
-  // pointer in the chain is fixed per slot, so a signature fully determines the launches.
-  std::map<std::array<int, 11>, hipGraphExec_t> graphs;
 };
 
 // Private fd tables for the host pool's workers (NM03_PRIVATE_FDS, default on). Every open and
@@ -162,19 +142,12 @@ struct Slot {
 // 10.0–10.6 µs in 16 processes (tools/io_contention.cpp, profiles/r3/io_contention/). Each worker
 // therefore starts with close_range(3, ~0U, CLOSE_RANGE_UNSHARE): its own table, holding only
 // stdin/out/err (no duplicates of the process's other fds, so a pipe or file the process closes is
-// not kept open by a worker). Such workers open files by full path (IoDirs::dir_fd).
-// NM03_PRIVATE_FDS=0 keeps the shared table; read when an engine is built (tests flip it in-process).
-static bool env_flag_on(const char* name) {
-  const char* e = std::getenv(name);
-  return !(e && *e == '0');
-}
-static thread_local bool tl_private_fds = false;
-
-static void make_fd_table_private(bool on) {
+// not kept open by a worker). Such workers open files by full path.
+static void make_fd_table_private() {
 #ifndef CLOSE_RANGE_UNSHARE
 #define CLOSE_RANGE_UNSHARE (1U << 1)
 #endif
-  if (on && ::syscall(SYS_close_range, 3u, ~0u, CLOSE_RANGE_UNSHARE) == 0) tl_private_fds = true;
+  (void)::syscall(SYS_close_range, 3u, ~0u, CLOSE_RANGE_UNSHARE);
 }
 
 // Every open() stores the opener's struct cred in the file (get_cred) and close() drops it (put_cred):
@@ -182,75 +155,35 @@ static void make_fd_table_private(bool on) {
 // their own). Each pool worker therefore gets its own copy: capset() with the current capabilities
 // commits a fresh, identical cred for the calling thread only (no privilege change). Bench, 5
 // interleaved pairs: 385–402k vs 327–398k slices/s, JPEG-pair write CPU 0.17–0.22 vs 0.19–0.26 s
-// per 40 steps (profiles/r3/private_cred/). NM03_PRIVATE_CRED=0 keeps the shared cred.
-static void make_cred_private(bool on) {
-  if (!on) return;
+// per 40 steps (profiles/r3/private_cred/).
+static void make_cred_private() {
   __user_cap_header_struct h{_LINUX_CAPABILITY_VERSION_3, 0};
   __user_cap_data_struct c[2]{};
   if (::syscall(SYS_capget, &h, c) == 0) (void)::syscall(SYS_capset, &h, c);
 }
 
-// Directory fds of one run: every item's input series directory and output directory opened once
-// (O_PATH), so loads and writes use openat on the bare file name instead of walking the full path
-// per file. Opened per run, never cached across runs: a caller may wipe and re-create output
-// directories between runs (the CLIs do). At most max_fds() directories per run get an fd — a
-// fraction of RLIMIT_NOFILE, since several runs may be queued at once — the rest use full paths.
+// Output directories of one run: an index per item and a creation hint per directory. Pool
+// workers have private fd tables (above), so loads and writes take full paths: a per-worker cache
+// of O_PATH directory fds had to be rebuilt for every run (each bench pass is a run), 16 workers ×
+// ≈40 directories × open + close per pass, which cost more than the path walks (loads 28–32 vs
+// 22–23 µs per slice, profiles/r3/depth/).
 struct IoDirs {
-  static size_t max_fds() {
-    rlimit rl{};
-    size_t lim = 1024;
-    if (getrlimit(RLIMIT_NOFILE, &rl) == 0 && rl.rlim_cur != RLIM_INFINITY) lim = (size_t)rl.rlim_cur;
-    return std::min<size_t>(256, lim / 8);
-  }
-  std::vector<int> fds;  // per directory index: O_PATH fd, or -1 (full paths)
-  // Per directory: 1 once a file was missing there (files are then created directly, see
-  // jpeg::write_jpeg_at); 0 = try opening existing files without O_CREAT first.
+  size_t ndirs = 0;
+  // Per directory: 0 unknown, 1 being filled (files are created directly, see jpeg::write_jpeg_at),
+  // 2 its files exist (opened without O_CREAT first).
   std::unique_ptr<std::atomic<uint8_t>[]> creating;
-  std::vector<int32_t> in_fd, out_fd;  // per item: directory index, -1 = none (bare file name)
-  std::vector<uint32_t> in_name;       // per item: offset of the file name in its path
-  // `open_fds`: false when the pool workers have private fd tables and could not use them.
-  explicit IoDirs(const std::vector<WorkItem>& items, bool open_fds = true) {
+  std::vector<int32_t> out_dir;  // per item: its output directory's index
+  explicit IoDirs(const std::vector<WorkItem>& items) {
     std::unordered_map<std::string, int32_t> idx;
-    const size_t cap = open_fds ? max_fds() : 0;
-    size_t opened = 0;
-    auto dir_index = [&](const std::string& d) -> int32_t {
-      auto it = idx.find(d);
-      if (it != idx.end()) return it->second;
-      const int fd = opened < cap ? ::open(d.empty() ? "/" : d.c_str(), O_PATH | O_DIRECTORY | O_CLOEXEC) : -1;
-      opened += fd >= 0;
-      const int32_t k = (int32_t)fds.size();
-      fds.push_back(fd);
-      idx.emplace(d, k);
-      return k;
-    };
-    in_fd.resize(items.size());
-    out_fd.resize(items.size());
-    in_name.resize(items.size());
+    out_dir.resize(items.size());
     for (size_t i = 0; i < items.size(); ++i) {
-      const std::string& p = items[i].path;
-      const size_t slash = p.rfind('/');
-      if (slash == std::string::npos) {
-        in_fd[i] = -1;
-        in_name[i] = 0;
-      } else {
-        in_fd[i] = dir_index(p.substr(0, slash));
-        in_name[i] = (uint32_t)(slash + 1);
-      }
-      out_fd[i] = dir_index(items[i].out_dir);
+      auto it = idx.emplace(items[i].out_dir, (int32_t)idx.size()).first;
+      out_dir[i] = it->second;
     }
-    creating.reset(new std::atomic<uint8_t>[std::max<size_t>(fds.size(), 1)]);
-    for (size_t k = 0; k < fds.size(); ++k) creating[k].store(0, std::memory_order_relaxed);
+    ndirs = idx.size();
+    creating.reset(new std::atomic<uint8_t>[std::max<size_t>(ndirs, 1)]);
+    for (size_t k = 0; k < ndirs; ++k) creating[k].store(0, std::memory_order_relaxed);
   }
-  ~IoDirs() {
-    for (int fd : fds)
-      if (fd >= 0) ::close(fd);
-  }
-  // fd of directory k usable on the calling thread, -1 if none (the caller then uses the full
-  // path). A pool worker with a private fd table cannot use these fds and takes the full path: a
-  // per-worker cache of directory fds had to be rebuilt for every run (each pass is a new run),
-  // 16 workers × ~40 directories × open + close per pass, which cost more than the path walks
-  // (loads 28–32 vs 22–23 µs per slice, profiles/r3/depth/).
-  int dir_fd(int32_t k) const { return k < 0 || tl_private_fds ? -1 : fds[(size_t)k]; }
   IoDirs(const IoDirs&) = delete;
   IoDirs& operator=(const IoDirs&) = delete;
 };
@@ -260,7 +193,6 @@ void hip_free_all(Slot& s) {
     if (s.h_blob) munmap(s.h_blob, s.blob_bytes);
     if (s.h_out) munmap(s.h_out, s.out_bytes);
     delete[] s.h_sizes;
-    if (s.map_region) munmap(s.map_region, (size_t)s.cap_slices * s.map_stride);
     return;
   }
   if (s.h_blob) (void)hipHostFree(s.h_blob);
@@ -268,12 +200,8 @@ void hip_free_all(Slot& s) {
   if (s.h_sizes) (void)hipHostFree(s.h_sizes);
   if (s.h_single) (void)hipHostFree(s.h_single);
   for (void* p : {(void*)s.d_blob, (void*)s.d_raw_x, (void*)s.d_med, (void*)s.d_tile_mm, (void*)s.d_f32, (void*)s.d_bits, (void*)s.d_srg_scratch, (void*)s.d_canvas,
-                  (void*)s.jw.look, (void*)s.jw.ticket, (void*)s.jw.spill, (void*)s.d_jraw,
-                  (void*)s.d_jcomp, (void*)s.d_jsizes})
+                  (void*)s.jw.look, (void*)s.jw.ticket, (void*)s.jw.spill})
     if (p) (void)hipFree(p);
-  if (s.map_region) munmap(s.map_region, (size_t)s.cap_slices * s.map_stride);
-  for (auto& kv : s.graphs) (void)hipGraphExecDestroy(kv.second);
-  s.graphs.clear();
   if (s.ev0) (void)hipEventDestroy(s.ev0);
   if (s.ev1) (void)hipEventDestroy(s.ev1);
   if (s.ev2) (void)hipEventDestroy(s.ev2);
@@ -297,65 +225,23 @@ struct Engine::Impl {
   std::vector<uint8_t> jpeg_header;
   int32_t divs[64];
   PipeConsts pc{};
-  // Loader read path (dicom::ReadMode); NM03_LOAD_MODE=direct|staged|mapped, NM03_LOAD_PREFIX=<bytes>.
-  // Staged is the default: 231k/232k/224k vs 221k/205k/223k slices/s for direct (interleaved,
-  // tools/gpu_load_ab.sh); a 4 KiB direct prefix misaligns the pixel pread's destination and is
-  // slower still (198k/187k/200k).
-  dicom::ReadMode read_mode_ = dicom::ReadMode::kStaged;
-  size_t read_prefix_ = 16384;
   // 12-bit transfer packing of slices whose samples fit (nm03/pack12.h); NM03_PACK12=0 disables.
   bool pack12_ = pack12::available();
-  // Pool workers' private fd tables and creds (NM03_PRIVATE_FDS / NM03_PRIVATE_CRED, default on).
-  const bool private_fds_ = env_flag_on("NM03_PRIVATE_FDS");
-  const bool private_cred_ = env_flag_on("NM03_PRIVATE_CRED");
-  // Host-mapped bytes per image for the GPU encoder's stuffed output: half the canvas (128 KiB for
-  // 512², ~5× a typical medical render; anything larger is CPU re-encoded, counted in StageTimes).
-  // NM03_JPEG_OUT_CAP=<bytes> overrides (tests force the fallback with a tiny cap).
+  // Host-mapped bytes per image for the GPU encoder's stuffed output (EngineConfig::jpeg_out_cap).
   uint32_t out_cap_ = 0;
-  // JPEG export path (NM03_JPEG_D2H): 0 = the encoder stores into host-mapped memory (default);
-  // 1 = HBM + gather + one SDMA copy; 2 = HBM + a gather kernel storing the packed bytes into
-  // host-mapped memory. Measured (profiles/r2/jpeg_d2h/): 1 cuts GPU time per 64-slice batch from
-  // 96 to 75 + 4.5 µs but its D2H copies share the copy engines with the uploads (H2D time
-  // doubles) and the headline drops (138-242k vs 286-340k slices/s); 2 moves the PCIe stores into
-  // the gather (75 + 25.6 µs) for no gain. Both stay selectable for A/B runs.
-  int jpeg_d2h_ = 0;
-  // Bytes per canvas the first D2H of a batch copies (1.25 × the largest packed average seen so
-  // far, 4 KiB granules; a batch that packs more copies the rest after its completion event).
-  std::atomic<uint32_t> jpeg_est_{24u << 10};
-  // NM03_PACK_BOUNCE=0: pack into a full-size intermediate and stream-copy it (A/B of pack_stream).
-  bool pack_bounce_ = true;
-  bool spread_ = false;  // plan_batches' spread schedule (NM03_BATCH_SPREAD)
-  bool interleave_exports_ = true;  // NM03_EXPORT_INTERLEAVE: writers round-robin over output directories
-  bool host_only_ = false;  // EngineConfig::host_only / NM03_HOST_ONLY
+  bool host_only_ = false;  // EngineConfig::host_only
   // Host-only: the entropy-coded segments standing in for the GPU encoder's output (original,
   // processed) — the golden export of a phantom slice, so sizes match a real run.
   std::vector<uint8_t> tmpl_[2];
 
   explicit Impl(const EngineConfig& c) : cfg(c), place(c.device, c.cpus) {
-    if (const char* e = std::getenv("NM03_BATCH_TAPER"); e && *e) cfg.taper = *e != '0';
-    if (const char* e = std::getenv("NM03_BATCH_SPREAD"); e && *e) spread_ = *e != '0';
-    if (const char* e = std::getenv("NM03_EXPORT_INTERLEAVE"); e && *e) interleave_exports_ = *e != '0';
-    if (const char* e = std::getenv("NM03_LOAD_MODE"); e && *e)
-      read_mode_ = std::string(e) == "staged" ? dicom::ReadMode::kStaged
-                   : std::string(e) == "mapped" ? dicom::ReadMode::kMapped
-                                                : dicom::ReadMode::kDirect;
-    if (const char* e = std::getenv("NM03_LOAD_PREFIX"); e && *e) read_prefix_ = (size_t)std::atol(e);
     if (const char* e = std::getenv("NM03_PACK12"); e && *e && *e == '0') pack12_ = false;
-    if (const char* e = std::getenv("NM03_PACK_BOUNCE"); e && *e && *e == '0') pack_bounce_ = false;
-    out_cap_ = (uint32_t)std::max<size_t>(64 * 1024, (size_t)cfg.render.out_width * cfg.render.out_height / 2) + 64;
-    if (const char* e = std::getenv("NM03_JPEG_OUT_CAP"); e && *e) out_cap_ = (uint32_t)std::max(64L, std::atol(e));
-    out_cap_ = (out_cap_ + 15u) & ~15u;  // jpeg_gather_kernel moves 16-byte words
-    if (const char* e = std::getenv("NM03_JPEG_D2H"); e && *e) jpeg_d2h_ = std::clamp(std::atoi(e), 0, 2);
-    if (const char* e = std::getenv("NM03_JPEG_D2H_EST_KB"); e && *e)  // tests: force short first copies
-      jpeg_est_ = (uint32_t)std::max(1L, std::atol(e)) << 10;
-    if (const char* e = std::getenv("NM03_UPLOAD_CHUNK_KB"); e && *e) upload_chunk_ = (size_t)std::atol(e) << 10;
+    out_cap_ = cfg.jpeg_out_cap ? std::max<uint32_t>(64, cfg.jpeg_out_cap)
+                                : (uint32_t)std::max<size_t>(64 * 1024, (size_t)cfg.render.out_width * cfg.render.out_height / 2) + 64;
+    out_cap_ = (out_cap_ + 15u) & ~15u;  // 16-byte aligned segments (the encoder's dwordx4 stores)
+    upload_chunk_ = cfg.upload_chunk_kb < 0 ? (size_t)2 << 20 : (size_t)cfg.upload_chunk_kb << 10;
     host_only_ = cfg.host_only;
-    if (const char* e = std::getenv("NM03_HOST_ONLY"); e && *e) host_only_ = *e != '0';
-    if (host_only_) {
-      upload_chunk_ = 0;  // nothing to upload
-      jpeg_d2h_ = 0;
-      cfg.graphs = false;
-    }
+    if (host_only_) upload_chunk_ = 0;  // nothing to upload
     if (cfg.batch_size < 1) cfg.batch_size = 1;
     if (cfg.streams < 1) cfg.streams = 1;
     if (cfg.max_dim < 16) cfg.max_dim = 16;
@@ -394,33 +280,28 @@ struct Engine::Impl {
     const double t1 = now_s();
     // Host threads and pinned buffers on the GPU's socket (numa.h).
     pool = std::make_unique<ThreadPool>(cfg.threads, [this](int i) {
-      place.bind_worker(i, cfg.threads);
-      make_fd_table_private(private_fds_);
-      make_cred_private(private_cred_);
-      // Signals go to other threads: a pool worker's reads are never cut short (SliceFile's
-      // staged read takes a short read as the end of the file).
+      place.bind_this_thread();
+      make_fd_table_private();
+      make_cred_private();
+      // Asynchronous signals go to other threads: a pool worker's reads are never cut short.
+      // Synchronous fault signals stay unblocked (a blocked SIGSEGV/SIGBUS is forced to SIG_DFL,
+      // bypassing the crash handler and sanitizers), and so does SIGPROF for sampling profilers.
       sigset_t all;
       sigfillset(&all);
+      for (int sig : {SIGSEGV, SIGBUS, SIGFPE, SIGILL, SIGTRAP, SIGABRT, SIGPROF}) sigdelset(&all, sig);
       pthread_sigmask(SIG_BLOCK, &all, nullptr);
     });
     const double t2 = now_s();
     // Slot 0 is built here (its failure fails the constructor); the others are built by their own
     // worker threads while slot 0 already runs batches — a slot costs ≈11–18 ms of pinned and
     // device allocations and stream creation, the first one more (runtime queues), which a cold
-    // CLI run would otherwise wait for in full. NM03_EAGER_SLOTS=1 (or graphs) builds them all here.
-    // With hipGraph capture on, all slots are built here: a slot being built (device/pinned
-    // allocations, a memset on the null stream) while another slot's thread captures its batch
-    // chain invalidates that capture.
-    const char* eager_env = std::getenv("NM03_EAGER_SLOTS");
-    const bool eager = (eager_env && *eager_env == '1') || cfg.graphs;
+    // CLI run would otherwise wait for in full.
     std::string slot_ms;
     slots.resize((size_t)cfg.streams);
     place.run_bound([&] {
-      for (int i = 0; i < (eager ? cfg.streams : 1); ++i) {
-        const double ts = now_s();
-        slots[(size_t)i] = make_slot();
-        slot_ms += (i ? "/" : "") + std::to_string((int)((now_s() - ts) * 1e4) / 10.0).substr(0, 5);
-      }
+      const double ts = now_s();
+      slots[0] = make_slot();
+      slot_ms = std::to_string((int)((now_s() - ts) * 1e4) / 10.0).substr(0, 5);
     });
     const double t3 = now_s();
     start_workers();
@@ -440,8 +321,8 @@ struct Engine::Impl {
     if (shared_up_) (void)hipStreamDestroy(shared_up_);
   }
 
-  // Every slot's H2D copies go through one engine-wide stream (default; NM03_UPLOAD_STREAM=own: each
-  // slot's own stream), so at most one SDMA upload runs at a time: two or more concurrent copies
+  // Every slot's H2D copies go through one engine-wide stream (each slot's own stream was the
+  // round-3 alternative), so at most one SDMA upload runs at a time: two or more concurrent copies
   // from different streams drop the copy engine's aggregate rate on the MI355X boxes
   // (tools/h2d_probe.hip: 28 vs 53-57 GB/s), and in the bench 20-40% of the upload time had two or
   // more in flight (profiles/r3/timeline/). The slot's kernels wait on an event after its last copy.
@@ -449,15 +330,7 @@ struct Engine::Impl {
   // (4 interleaved pairs, profiles/r3/upload_stream/).
   hipStream_t shared_up_ = nullptr;
   std::mutex shared_up_m_;
-  static bool shared_upload_stream() {
-    static const bool on = [] {
-      const char* e = std::getenv("NM03_UPLOAD_STREAM");
-      return !(e && std::string(e) == "own");
-    }();
-    return on;
-  }
-  hipStream_t upload_stream_for(hipStream_t own) {
-    if (!shared_upload_stream()) return own;
+  hipStream_t upload_stream() {
     std::lock_guard<std::mutex> g(shared_up_m_);
     if (!shared_up_) check_hip(hipStreamCreateWithFlags(&shared_up_, hipStreamNonBlocking), "hipStreamCreate upload");
     return shared_up_;
@@ -529,31 +402,13 @@ struct Engine::Impl {
       return sp;
     }
     try {
-      if (read_mode_ == dicom::ReadMode::kMapped) {
-        s.map_stride = align_up((size_t)md * md * 2 + (1u << 20), 1u << 21);  // pixels + 1 MiB of header room
-        void* r = mmap(nullptr, (size_t)B * s.map_stride, PROT_NONE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
-        if (r == MAP_FAILED) throw DeviceError("cannot reserve the loader's mapping range");
-        s.map_region = static_cast<uint8_t*>(r);
-      }
       check_hip(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking), "hipStreamCreate");
-      s.up = upload_stream_for(s.stream);
+      s.up = upload_stream();
       check_hip(hipEventCreate(&s.ev0), "hipEventCreate");
       check_hip(hipEventCreate(&s.ev1), "hipEventCreate");
-      // Batch completion is waited on by the slot thread (wait_batch).
-      // Only the blocking wait mode sleeps in hipEventSynchronize and needs a blocking-sync event;
-      // the default polling wait queries it (NM03_EV2_BLOCKING=1 restores the blocking-sync event for
-      // polling too: A/B of the runtime's interrupt handling cost).
-      static const bool ev2_blocking = [] {
-        const char* e = std::getenv("NM03_EV2_BLOCKING");
-        return e && *e == '1';
-      }();
-      const bool blocking = wait_mode() == WaitMode::kBlock || (wait_mode() == WaitMode::kPoll && ev2_blocking);
-      check_hip(hipEventCreateWithFlags(&s.ev2, blocking ? hipEventBlockingSync : hipEventDefault), "hipEventCreate");
+      // Batch completion is polled by the slot thread (wait_batch): no blocking-sync event.
+      check_hip(hipEventCreateWithFlags(&s.ev2, hipEventDefault), "hipEventCreate");
       check_hip(hipHostMalloc((void**)&s.h_blob, s.blob_bytes, hipHostMallocDefault), "hipHostMalloc blob");
-      if (hipHostGetDevicePointer((void**)&s.d_hblob, s.h_blob, 0) != hipSuccess) {
-        (void)hipGetLastError();
-        s.d_hblob = nullptr;
-      }
       // +64 B tail slack: the median's packed-group loads read whole dwords (k1_median.hip).
       s.d_blob = dmalloc<uint8_t>(s.blob_bytes + 64, "hipMalloc blob");
       s.d_raw_x = dmalloc<uint16_t>(s.cap_pixels, "hipMalloc raw");
@@ -574,25 +429,8 @@ struct Engine::Impl {
       s.jw.spill = dmalloc<uint32_t>(s.jw.look_cap * 256 * 56, "hipMalloc jpeg spill");
       check_hip(hipMemset(s.jw.ticket, 0, sizeof(uint32_t) * s.cap_canvases), "memset tickets");
       const size_t out_bytes = (size_t)out_cap_ * s.cap_canvases;
-      if (jpeg_d2h_) {
-        check_hip(hipHostMalloc((void**)&s.h_out, out_bytes, jpeg_d2h_ == 2 ? hipHostMallocMapped : hipHostMallocDefault),
-                  "hipHostMalloc out");
-        if (jpeg_d2h_ == 2) check_hip(hipHostGetDevicePointer((void**)&s.d_out, s.h_out, 0), "hipHostGetDevicePointer out");
-        s.d_jraw = dmalloc<uint8_t>(out_bytes, "hipMalloc jpeg out");
-        if (jpeg_d2h_ == 1) s.d_jcomp = dmalloc<uint8_t>(out_bytes, "hipMalloc jpeg packed");
-        s.d_jsizes = dmalloc<int32_t>(s.cap_canvases, "hipMalloc jpeg sizes");
-        s.jofs.assign(s.cap_canvases, 0);
-      } else {
-        // NM03_JPEG_OUT_MEM=coherent|noncoherent overrides HIP's default coherence of the
-        // host-mapped JPEG output (A/B of where the encoder's PCIe writes are paid).
-        static const unsigned out_flags = [] {
-          const char* e = std::getenv("NM03_JPEG_OUT_MEM");
-          const std::string v = e ? e : "";
-          return hipHostMallocMapped | (v == "coherent" ? hipHostMallocCoherent : v == "noncoherent" ? hipHostMallocNonCoherent : 0u);
-        }();
-        check_hip(hipHostMalloc((void**)&s.h_out, out_bytes, out_flags), "hipHostMalloc out");
-        check_hip(hipHostGetDevicePointer((void**)&s.d_out, s.h_out, 0), "hipHostGetDevicePointer out");
-      }
+      check_hip(hipHostMalloc((void**)&s.h_out, out_bytes, hipHostMallocMapped), "hipHostMalloc out");
+      check_hip(hipHostGetDevicePointer((void**)&s.d_out, s.h_out, 0), "hipHostGetDevicePointer out");
       check_hip(hipHostMalloc((void**)&s.h_sizes, sizeof(int32_t) * s.cap_canvases, hipHostMallocMapped),
                 "hipHostMalloc sizes");
       check_hip(hipHostGetDevicePointer((void**)&s.d_sizes, s.h_sizes, 0), "hipHostGetDevicePointer sizes");
@@ -607,16 +445,10 @@ struct Engine::Impl {
   // While a batch loads, queue the H2D copy of every finished, contiguous prefix of the raw region
   // once it has grown by `upload_chunk_` bytes: the copy engine starts after a few loads instead
   // of after the whole batch (pipeline fill at the start of a run, load/upload overlap inside
-  // every batch). NM03_UPLOAD_CHUNK_KB (0 = one upload per batch after all loads) sets the minimum;
+  // every batch). EngineConfig::upload_chunk_kb (0 = one upload per batch after all loads) sets the minimum;
   // batches of large slices use a quarter of the batch (512² × 64: 8 MiB — many concurrent small
   // copies cost 10% of the upload rate there, profiles/iter5/c4_sweep.txt).
   size_t upload_chunk_ = 2u << 20;
-  // Batches whose whole upload (tables + pixels) is at most this many bytes are copied by a shader
-  // on the compute queue (launch_copy_from_host) instead of SDMA; NM03_SHADER_UPLOAD_KB, 0 = never.
-  size_t shader_upload_bytes_ = [] {
-    const char* e = std::getenv("NM03_SHADER_UPLOAD_KB");
-    return (size_t)(e && *e ? std::atoll(e) : 0) * 1024;
-  }();
 
   void upload_progress(Slot& s, size_t count) {
     size_t next = 0, seen = 0;
@@ -663,58 +495,23 @@ struct Engine::Impl {
   // ---- batch completion ----------------------------------------------------------------------
   // The slot thread waits for its batch here. A blocking-sync hipEventSynchronize still spins in
   // the runtime before it sleeps, which cost ≈0.7 ms of slot-thread CPU per batch — CPU the
-  // loader/writer pool needs. `poll` sleeps in short steps (timer slack lowered to 1 µs on slot
-  // threads) and queries the event: a few µs of CPU per batch, ≤ poll interval of added latency,
-  // hidden by the other slots in flight. NM03_EVENT_WAIT=poll|block|spin, NM03_EVENT_POLL_US.
-  enum class WaitMode { kPoll, kBlock, kSpin };
-  static WaitMode wait_mode() {
-    static const WaitMode m = [] {
-      const char* e = std::getenv("NM03_EVENT_WAIT");
-      const std::string v = e ? e : "";
-      if (v == "block") return WaitMode::kBlock;
-      if (v == "spin") return WaitMode::kSpin;
-      if (const char* sp = std::getenv("NM03_EVENT_SPIN"); sp && *sp && *sp != '0') return WaitMode::kSpin;
-      return WaitMode::kPoll;
-    }();
-    return m;
-  }
-  static int poll_us() {
-    static const int us = [] {
-      const char* e = std::getenv("NM03_EVENT_POLL_US");
-      const int v = e && *e ? std::atoi(e) : 20;
-      return v < 1 ? 1 : v;
-    }();
-    return us;
-  }
+  // loader/writer pool needs. Instead the slot sleeps in short steps (timer slack lowered to 1 µs on
+  // slot threads) and queries the event: a few µs of CPU per batch, ≤ 20 µs of added latency,
+  // hidden by the other slots in flight (profiles: tools/gpu_wait_ab.sh, round 1).
+  //
   // The slot first sleeps through most of the time its recent batches took from enqueue to
   // completion (EMA, per slice × this batch's slices), then polls: ~10 wake-ups per batch instead of
   // one per poll interval over the whole batch (each wake-up is a context switch of host CPU the
   // loaders/writers need). Per slice, so a short batch after full ones (a strong-scaling shard cut
   // into ⌈shard / streams⌉-slice batches) is not slept through at the full batches' time: fixed
   // per-batch costs make small batches slower per slice, so the scaled estimate errs short (more
-  // polls), never long. NM03_EVENT_EMA=batch restores the per-batch EMA (A/B).
+  // polls), never long.
   void wait_batch(Slot& s, hipEvent_t ev, double t_enq, int nslices) {
-    if (wait_mode() != WaitMode::kPoll) {
-      check_hip(hipEventSynchronize(ev), "batch sync");
-      return;
-    }
-    static const bool adapt = [] {
-      const char* e = std::getenv("NM03_EVENT_ADAPT");  // 0: plain polling (A/B)
-      return !(e && *e == '0');
-    }();
-    static const bool per_batch = [] {
-      const char* e = std::getenv("NM03_EVENT_EMA");
-      return e && std::string(e) == "batch";
-    }();
     // A small batch (≤ 16 slices: a strong-scaling shard's, latency-bound) spin-polls its event for
     // up to 1 ms instead of sleeping through the slot's recent per-slice mean: that mean comes from
     // full, queued batches, and scaled to 15 slices it overslept completed batches by 80–190 µs in
-    // the single-pass trace (profiles/r3/small_upload/hip_trace_inline.txt). NM03_SMALL_POLL=0: A/B.
-    static const bool small_poll = [] {
-      const char* e = std::getenv("NM03_SMALL_POLL");
-      return !(e && *e == '0');
-    }();
-    if (small_poll && nslices <= 16) {
+    // the single-pass trace (profiles/r3/small_upload/hip_trace_inline.txt).
+    if (nslices <= 16) {
       const double until = t_enq + 1e-3;
       for (;;) {
         const hipError_t e = hipEventQuery(ev);
@@ -724,14 +521,14 @@ struct Engine::Impl {
         for (int k = 0; k < 32; ++k) __builtin_ia32_pause();
       }
     }
-    const double scale = per_batch ? 1.0 : (double)std::max(1, nslices);
+    const double scale = (double)std::max(1, nslices);
     // Sleep through most of the batch's expected time (0.8 × the recent mean), in chunks of at
     // most 250 µs with an event check between them, then poll. One long sleep would feed itself:
     // a slow batch (GPU shared with another process, host CPU stolen) raises the mean, the next
     // batches oversleep by the same amount, and the mean — measured from these overslept waits —
     // decays by only ≈5% per batch. Chunked, a wait ends within one chunk of the batch's real
     // completion, so the mean tracks the GPU again after a few batches.
-    const double target = adapt ? 0.8 * s.batch_ema_s * scale : 0.0;
+    const double target = 0.8 * s.batch_ema_s * scale;
     for (;;) {
       const hipError_t e = hipEventQuery(ev);
       if (e == hipSuccess) break;
@@ -740,22 +537,26 @@ struct Engine::Impl {
       if (ahead > 100e-6)
         std::this_thread::sleep_for(std::chrono::duration<double>(std::min(ahead, 250e-6)));
       else
-        std::this_thread::sleep_for(std::chrono::microseconds(poll_us()));
+        std::this_thread::sleep_for(std::chrono::microseconds(20));
     }
     const double took = (now_s() - t_enq) / scale;
     s.batch_ema_s = s.batch_ema_s > 0 ? 0.75 * s.batch_ema_s + 0.25 * took : took;
   }
 
   // ---- loading -------------------------------------------------------------------------------
-  void load_into(Slot& s, int i, size_t item, const std::string& path, int dirfd, const char* name, SliceStatus& st,
-                 std::atomic<int64_t>& load_ns, std::atomic<int64_t>& bytes_in) {
+  void load_into(Slot& s, int i, size_t item, const std::string& path, SliceStatus& st, std::atomic<int64_t>& load_ns,
+                 std::atomic<int64_t>& bytes_in) {
     thread_local std::vector<uint8_t> buf;
     TraceRange tr("nm03.load");
     const double t0 = now_s();
     try {
       if (fault_plan().corrupt_dicom == (int64_t)item) throw SliceError("injected fault: corrupt DICOM data");
-      dicom::SliceFile file(dirfd, name, path, read_mode_, read_prefix_);
-      if (s.map_region) file.map_at(s.map_region + (size_t)i * s.map_stride, s.map_stride);
+      // Staged read: one whole-file pread into a cache-resident scratch buffer, the pack/copy into
+      // the pinned blob from there. Mapping the file instead measured 5x the loader CPU (mmap +
+      // populate + munmap under the mm lock; 47.6k vs 267k slices/s, profiles/iter6/
+      // mapped_load_ab.txt), and a pread of the pixels straight into the blob was slower too
+      // (tools/gpu_load_ab.sh): both removed in round 4.
+      dicom::SliceFile file(AT_FDCWD, path.c_str(), path, dicom::ReadMode::kStaged);
       const dicom::Header& h = file.header(buf);
       const size_t n = file.size();  // after header(): staged reads learn the size from the read
       const int md = cfg.pipe.min_dim;
@@ -798,7 +599,7 @@ struct Engine::Impl {
           const bool low12 = h.bits_stored <= 12;
           if (packable && !low12) {
             std::lock_guard<std::mutex> g(s.alloc_m);
-            credit = pack_bounce_ && s.hole_credit >= plen;
+            credit = s.hole_credit >= plen;
             if (credit) {
               s.hole_credit -= plen;
               reserve_locked(plen);
@@ -828,13 +629,8 @@ struct Engine::Impl {
               reserve_locked(packed ? plen : ulen);
             }
             uint16_t* dst = reinterpret_cast<uint16_t*>(s.h_blob + s.raw_base) + off;
-            if (packed && pack_bounce_) {
+            if (packed) {
               pack12::pack_stream(samples, npix, reinterpret_cast<uint8_t*>(dst));
-            } else if (packed) {  // A/B: full-size intermediate, then one streaming copy
-              thread_local std::vector<uint8_t> pk;
-              if (pk.size() < npix / 2 * 3 + 64) pk.resize(npix / 2 * 3 + 64);
-              pack12::pack_stream(samples, npix, pk.data());
-              dicom::stream_copy(dst, pk.data(), npix / 2 * 3);
             } else {
               file.pixels16(dst);
             }
@@ -1018,13 +814,16 @@ struct Engine::Impl {
     // The tables sit right before the raw region: with nothing uploaded early (a small batch) both
     // go as one copy — one SDMA command and one completion on the batch's critical path, not two.
     const size_t raw_end = s.raw_used.load();
-    const bool shader = s.uploaded == 0 && s.d_hblob && s.raw_base + raw_end * 2 <= shader_upload_bytes_;
-    const bool inline_up = !shader && s.uploaded == 0 && !s.upload_started && nl <= 16 && small_inline_upload();
-    hipStream_t up = shader || inline_up ? s.stream : s.up;
+    // A small batch (≤ 16 slices) with nothing uploaded early copies on its own stream, without the
+    // upload stream's events: on the shared stream every copy sat ≈ 20 µs behind the previous one
+    // (SDMA → event marker → SDMA hand-offs) and its first kernel ≈ 16–20 µs behind the copy (the
+    // cross-stream wait). 58-slice single pass 0.373–0.399 vs 0.435–0.447 ms median over 200 passes
+    // in 3 of 3 rounds (profiles/r3/small_upload/). A shader copy from host-mapped memory instead of
+    // SDMA measured no gain (profiles/r3/shader_upload/) and was removed in round 4.
+    const bool inline_up = s.uploaded == 0 && !s.upload_started && nl <= 16;
+    hipStream_t up = inline_up ? s.stream : s.up;
     if (!s.upload_started && !inline_up) check_hip(hipEventRecord(s.ev0, up), "event");
-    if (shader) {
-      launch_copy_from_host(s.d_hblob, s.d_blob, s.raw_base + raw_end * 2, s.stream);  // small batch: no SDMA
-    } else if (s.uploaded == 0) {
+    if (s.uploaded == 0) {
       check_hip(hipMemcpyAsync(s.d_blob, s.h_blob, s.raw_base + raw_end * 2, hipMemcpyHostToDevice, up),
                 "H2D tables + pixels");
     } else {
@@ -1037,81 +836,36 @@ struct Engine::Impl {
     s.uploaded = raw_end;
     if (!inline_up) check_hip(hipEventRecord(s.ev1, up), "event");
     if (up != s.stream) check_hip(hipStreamWaitEvent(s.stream, s.ev1, 0), "wait upload");
-    auto chain = [&] {
-      const auto* blob_raw = reinterpret_cast<const uint16_t*>(db + s.raw_base);
-      if (separate_unpack()) {  // A/B: the standalone K0 expansion pass before the median
-        launch_unpack(blob_raw, d_raw, d_desc, nl, s.max_w * s.max_h, s.stream);
-        launch_median(d_raw, s.d_med, d_desc, d_medt, nmed, pc.median_k, d_stats, s.stream, s.d_tile_mm);
-      } else {  // the median reads the upload directly and writes the expanded samples
-        launch_median(nullptr, s.d_med, d_desc, d_medt, nmed, pc.median_k, d_stats, s.stream, s.d_tile_mm, blob_raw,
-                      d_raw);
-      }
-      launch_sharpen_band(s.d_med, plane(kPBand), mode == 1 ? s.d_f32 : nullptr, d_desc, d_shpt, nshp, pc, d_stats,
-                          s.stream, s.d_tile_mm);
-      SrgOutputs o;
-      o.scratch = s.d_srg_scratch;
-      o.dilated = plane(kPDilated);
-      o.border_dilated = plane(kPBorderD);
-      if (mode == 1) {
-        o.region = plane(kPRegion);
-        o.eroded = plane(kPEroded);
-        o.border_region = plane(kPBorderR);
-        o.border_eroded = plane(kPBorderE);
-      }
-      launch_srg_morph(plane(kPBand), d_desc, nl, d_seeds, pc, o, s.max_w, s.max_h, s.stream);
-      (void)d_stats_c;
-      if (s.any_canvas) launch_render(d_raw, s.d_f32, s.d_bits, d_stats, d_rd, ncanv, cw, ch, s.d_canvas, s.stream);
-      JpegRenderSrc rsrc;
-      rsrc.raw = d_raw;
-      rsrc.f32 = s.d_f32;
-      rsrc.bits = s.d_bits;
-      rsrc.stats = d_stats;
-      rsrc.rd = d_rd;
-      if (jpeg_d2h_) {
-        launch_jpeg(s.d_canvas, d_jd, ncanv, cw, ch, divs, s.jw, s.d_jraw, s.d_jsizes, s.stream, &rsrc);
-        launch_jpeg_gather(s.d_jraw, out_cap_, s.d_jsizes, ncanv, jpeg_d2h_ == 2 ? s.d_out : s.d_jcomp, s.d_sizes,
-                           s.stream);
-      } else {
-        launch_jpeg(s.d_canvas, d_jd, ncanv, cw, ch, divs, s.jw, s.d_out, s.d_sizes, s.stream, &rsrc);
-      }
-    };
-    if (!cfg.graphs || sync_launches()) {
-      chain();
-    } else {
-      // The K0-vs-fused unpack switch changes the chain: part of the signature (it is read per batch).
-      const std::array<int, 11> key{nmed, nshp, nl, ncanv, s.max_w, s.max_h, (int)s.any_canvas, mode, cw, ch,
-                                    (int)separate_unpack()};
-      auto it = s.graphs.find(key);
-      if (it == s.graphs.end()) {
-        hipGraph_t g = nullptr;
-        hipGraphExec_t ge = nullptr;
-        check_hip(hipStreamBeginCapture(s.stream, hipStreamCaptureModeThreadLocal), "begin capture");
-        try {
-          chain();
-        } catch (...) {
-          (void)hipStreamEndCapture(s.stream, &g);
-          if (g) (void)hipGraphDestroy(g);
-          throw;
-        }
-        check_hip(hipStreamEndCapture(s.stream, &g), "end capture");
-        const hipError_t e = hipGraphInstantiate(&ge, g, nullptr, nullptr, 0);
-        (void)hipGraphDestroy(g);
-        check_hip(e, "graph instantiate");
-        if (s.graphs.size() >= 16) {  // bounded cache: signatures vary only with batch fill
-          (void)hipGraphExecDestroy(s.graphs.begin()->second);
-          s.graphs.erase(s.graphs.begin());
-        }
-        it = s.graphs.emplace(key, ge).first;
-      }
-      check_hip(hipGraphLaunch(it->second, s.stream), "graph launch");
+    // The median reads the upload directly (12-bit pairs decoded in its tile load) and writes the
+    // expanded samples for the render/JPEG stages. One eager launch per kernel: hipGraph replay of
+    // this 5-launch chain cost more host CPU than it saved (85k vs 110k slices/s in round 1; 283–346k
+    // eager vs 220–321k replayed in round 2, profiles/r2/graphs_threads/), removed in round 4.
+    const auto* blob_raw = reinterpret_cast<const uint16_t*>(db + s.raw_base);
+    launch_median(nullptr, s.d_med, d_desc, d_medt, nmed, pc.median_k, d_stats, s.stream, s.d_tile_mm, blob_raw, d_raw);
+    launch_sharpen_band(s.d_med, plane(kPBand), mode == 1 ? s.d_f32 : nullptr, d_desc, d_shpt, nshp, pc, d_stats,
+                        s.stream, s.d_tile_mm);
+    SrgOutputs o;
+    o.scratch = s.d_srg_scratch;
+    o.dilated = plane(kPDilated);
+    o.border_dilated = plane(kPBorderD);
+    if (mode == 1) {
+      o.region = plane(kPRegion);
+      o.eroded = plane(kPEroded);
+      o.border_region = plane(kPBorderR);
+      o.border_eroded = plane(kPBorderE);
     }
-    if (jpeg_d2h_ == 1 && ncanv > 0) {
-      s.jcopied = std::min((size_t)out_cap_ * ncanv, (size_t)jpeg_est_.load(std::memory_order_relaxed) * ncanv);
-      check_hip(hipMemcpyAsync(s.h_out, s.d_jcomp, s.jcopied, hipMemcpyDeviceToHost, s.stream), "jpeg D2H");
-    }
+    launch_srg_morph(plane(kPBand), d_desc, nl, d_seeds, pc, o, s.max_w, s.max_h, s.stream);
+    if (s.any_canvas) launch_render(d_raw, s.d_f32, s.d_bits, d_stats, d_rd, ncanv, cw, ch, s.d_canvas, s.stream);
+    JpegRenderSrc rsrc;
+    rsrc.raw = d_raw;
+    rsrc.f32 = s.d_f32;
+    rsrc.bits = s.d_bits;
+    rsrc.stats = d_stats;
+    rsrc.rd = d_rd;
+    rsrc.nrd = ncanv;
+    launch_jpeg(s.d_canvas, d_jd, ncanv, cw, ch, divs, s.jw, s.d_out, s.d_sizes, s.stream, &rsrc);
     check_hip(hipEventRecord(s.ev2, s.stream), "event");
     wait_batch(s, s.ev2, t_enq, nl);
-    if (jpeg_d2h_ && ncanv > 0) finish_jpeg_d2h(s, ncanv);
     if (acc && !inline_up) {  // an inline small upload records no split events
       float a = 0, b = 0;
       (void)hipEventElapsedTime(&a, s.ev0, s.ev1);
@@ -1121,31 +875,9 @@ struct Engine::Impl {
     }
   }
 
-  // D2H mode, after the batch's completion event: packed offsets from the mirrored sizes (the
-  // gather kernel's layout), the rest of the packed bytes if the first copy was short, and the
-  // estimate for later batches.
-  void finish_jpeg_d2h(Slot& s, int ncanv) {
-    size_t total = 0;
-    for (int k = 0; k < ncanv; ++k) {
-      s.jofs[k] = total;
-      total += jpeg_compact_bytes(s.h_sizes[k]);
-    }
-    if (jpeg_d2h_ == 2) return;
-    if (total > s.jcopied) {
-      check_hip(hipMemcpyAsync(s.h_out + s.jcopied, s.d_jcomp + s.jcopied, total - s.jcopied, hipMemcpyDeviceToHost,
-                               s.stream),
-                "jpeg D2H rest");
-      check_hip(hipStreamSynchronize(s.stream), "jpeg D2H rest");
-    }
-    const uint32_t want = (uint32_t)std::min<size_t>(out_cap_, ((total / ncanv) * 5 / 4 + 4095) & ~(size_t)4095);
-    uint32_t cur = jpeg_est_.load(std::memory_order_relaxed);
-    while (want > cur && !jpeg_est_.compare_exchange_weak(cur, want, std::memory_order_relaxed)) {
-    }
-  }
-
   // Host bytes of canvas k's GPU-encoded segment (valid when h_sizes[k] ≥ 0).
   const uint8_t* jpeg_bytes(const Slot& s, int k) const {
-    return jpeg_d2h_ ? s.h_out + s.jofs[k] : s.h_out + (size_t)k * out_cap_;
+    return s.h_out + (size_t)k * out_cap_;
   }
 
   // Bytes of canvas k's JPEG (header + segment + EOI); falls back to the CPU encoder when the
@@ -1176,19 +908,6 @@ struct Engine::Impl {
   // the wake-up is on their critical path. Full batches sleep at once (the spin would take CPU the
   // pool needs: 96-slice batches measured 374–388k with it vs 379–401k without, profiles/r3/wait_spin/).
   static int small_batch_spin(size_t count) { return count <= 16 ? 200 : 0; }
-  // A small batch (≤ 16 slices) with nothing uploaded early copies on its own stream, without the
-  // upload stream's events: on the shared stream every copy sat ≈ 20 µs behind the previous one
-  // (SDMA → event marker → SDMA hand-offs) and its first kernel ≈ 16–20 µs behind the copy (the
-  // cross-stream wait). 58-slice single pass 0.373–0.399 vs 0.435–0.447 ms median over 200 passes
-  // in 3 of 3 rounds (profiles/r3/small_upload/). NM03_SMALL_UPLOAD=shared restores the old path.
-  static bool small_inline_upload() {
-    static const bool on = [] {
-      const char* e = std::getenv("NM03_SMALL_UPLOAD");
-      return !(e && std::string(e) == "shared");
-    }();
-    return on;
-  }
-
   // `batch`: index within its run (fault injection); `prio`: engine-wide batch sequence number,
   // the host-pool priority (earlier batches first, also across queued runs).
   void process_batch(Slot& s, const std::vector<WorkItem>& items, const IoDirs& dirs, size_t batch, uint64_t prio,
@@ -1208,32 +927,16 @@ struct Engine::Impl {
     s.progress_quiet.store(false, std::memory_order_relaxed);
     std::atomic<int64_t> load_ns{0}, bytes_in{0}, write_ns{0}, bytes_out{0}, load_cpu_ns{0}, write_cpu_ns{0};
     std::string upload_error;
-    // NM03_PIN=l3: slice (first + i)'s load and export run on L3 domain (first + i) mod G, so the
-    // same files' page-cache lines meet the same CCD every pass (numa.h Placement::groups()).
-    const int G = place.groups();
-    auto worker_group = [this](int w) { return place.worker_group(w); };
-    auto for_items = [&](TaskGroup& tg, size_t n, const std::function<size_t(size_t)>& item_of,
-                         std::function<void(size_t)> fn, uint64_t pr, std::atomic<int64_t>* cpu) {
-      if (G > 1)
-        tg.for_each_grouped(n, std::move(fn), G, [&](size_t k) { return (int)(item_of(k) % (size_t)G); }, worker_group,
-                            pr, cpu);
-      else
-        tg.for_each(n, std::move(fn), pr, cpu);
-    };
     {
       TaskGroup tg(*pool);
-      for_items(
-          tg, count, [&](size_t i) { return first + i; },
+      tg.for_each(
+          count,
           [&](size_t i) {
             if (on_start) on_start(first + i);
             if (cfg.resume && outputs_exist(items[first + i])) {
               status[first + i] = SliceStatus{kSliceOk, "resumed: outputs already present"};
             } else {
-              const size_t it = first + i;
-              const int dk = dirs.dir_fd(dirs.in_fd[it]);
-              const int dfd = dk >= 0 ? dk : AT_FDCWD;
-              const char* nm = items[it].path.c_str() + (dk >= 0 ? dirs.in_name[it] : 0);
-              load_into(s, (int)i, it, items[it].path, dfd, nm, status[it], load_ns, bytes_in);
+              load_into(s, (int)i, first + i, items[first + i].path, status[first + i], load_ns, bytes_in);
             }
             if (upload_chunk_) {
               size_t lf;
@@ -1259,12 +962,6 @@ struct Engine::Impl {
         }
       }
       tg.wait(small_batch_spin(count));
-    }
-    if (s.map_region) {
-      // One unmap for the batch's file mappings (they were only read by the loads above).
-      void* r = mmap(s.map_region, count * s.map_stride, PROT_NONE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE | MAP_FIXED,
-                     -1, 0);
-      if (r == MAP_FAILED) throw DeviceError("cannot release the loader's mappings");
     }
     s.live.clear();
     for (size_t i = 0; i < count; ++i)
@@ -1301,11 +998,13 @@ struct Engine::Impl {
       // Export order: round-robin over the batch's output directories, so the pool's concurrent
       // writers spread over several patient directories. Creating a file takes its directory's
       // lock exclusively; in slice order every writer would create in the same directory.
+      // Wipe-each-pass figure 145–176k vs 128–139k slices/s (4/4 interleaved pairs,
+      // profiles/r2/export_interleave/); headline unchanged.
       std::vector<int> order(s.live.size());
-      if (interleave_exports_ && dirs.fds.size() > 1) {
+      if (dirs.ndirs > 1) {
         std::vector<std::pair<int32_t, std::vector<int>>> groups;  // (dir, live indices), first-seen order
         for (size_t c = 0; c < s.live.size(); ++c) {
-          const int32_t d = dirs.out_fd[first + s.live[c]];
+          const int32_t d = dirs.out_dir[first + s.live[c]];
           auto it = std::find_if(groups.rbegin(), groups.rend(), [&](const auto& g) { return g.first == d; });
           if (it == groups.rend()) {
             groups.push_back({d, {}});
@@ -1320,9 +1019,24 @@ struct Engine::Impl {
       } else {
         for (size_t c = 0; c < order.size(); ++c) order[c] = (int)c;
       }
+      // Are the batch's output directories being filled? (cold run: every file is created.) A
+      // directory whose state is still unknown is probed once per run with its first file.
+      bool creates = false;
+      for (int c : s.live) {
+        const size_t item = first + (size_t)c;
+        std::atomic<uint8_t>& st = dirs.creating[dirs.out_dir[item]];
+        uint8_t v = st.load(std::memory_order_relaxed);
+        if (v == 0) {
+          const std::string f = cohort::with_slash(items[item].out_dir) + cohort::stem(items[item].path) + "_original.jpg";
+          const uint8_t probe = ::access(f.c_str(), F_OK) == 0 ? 2 : (errno == ENOENT ? 1 : 2);
+          st.compare_exchange_strong(v, probe, std::memory_order_relaxed);
+          v = st.load(std::memory_order_relaxed);
+        }
+        creates = creates || v == 1;
+      }
       TaskGroup tg(*pool);
-      for_items(
-          tg, s.live.size(), [&](size_t oc) { return first + (size_t)s.live[(size_t)order[oc]]; },
+      tg.for_each(
+          s.live.size(),
           [&](size_t oc) {
             const size_t c = (size_t)order[oc];
             const size_t item = first + s.live[c];
@@ -1331,18 +1045,14 @@ struct Engine::Impl {
             TraceRange tr("nm03.export");
             try {
               if (fault_plan().fail_write == (int64_t)item) throw std::runtime_error("injected fault: export failure");
-              const int dk = dirs.dir_fd(dirs.out_fd[item]);
-              const bool rel = dk >= 0;
-              const int dfd = rel ? dk : AT_FDCWD;
-              const std::string base = (rel ? std::string() : cohort::with_slash(items[item].out_dir)) +
-                                       cohort::stem(items[item].path);
+              const std::string base = cohort::with_slash(items[item].out_dir) + cohort::stem(items[item].path);
               for (int k = 0; k < 2; ++k) {
                 const int cv = 2 * (int)c + k;
                 const std::string name = base + (k == 0 ? "_original.jpg" : "_processed.jpg");
                 const uint8_t* seg = use_fb[cv] ? fb[cv].data() : jpeg_bytes(s, cv);
                 const size_t len = use_fb[cv] ? fb[cv].size() : (size_t)s.h_sizes[cv];
-                jpeg::write_jpeg_at(dfd, rel ? items[item].out_dir : std::string(), name, jpeg_header, seg, len,
-                                    dirs.out_fd[item] >= 0 ? &dirs.creating[dirs.out_fd[item]] : nullptr);
+                jpeg::write_jpeg_at(AT_FDCWD, std::string(), name, jpeg_header, seg, len,
+                                    &dirs.creating[dirs.out_dir[item]]);
                 bytes_out += (int64_t)(jpeg_header.size() + len + 2);
               }
             } catch (const std::exception& e) {
@@ -1350,7 +1060,7 @@ struct Engine::Impl {
             }
             write_ns += (int64_t)((now_s() - t0) * 1e9);
           },
-          2 * prio + 1, &write_cpu_ns);
+          2 * prio + 1, &write_cpu_ns, creates ? cfg.create_writers : 0);
       tg.wait(small_batch_spin(count));
     }
     std::lock_guard<std::mutex> g(acc_m);
@@ -1366,46 +1076,13 @@ struct Engine::Impl {
     acc.batches += 1;
   }
 
-  // Batch schedule. Tapered (batch ≥ 16): a quarter- and a half-size batch first, so the upload
-  // engine starts after a few loads instead of a full batch (pipeline fill), full batches in the
-  // middle, and a remainder split into shrinking batches so the last kernels and exports after
-  // the final upload are short (drain). Uniform otherwise.
-  //
-  // Spread (spread_slots = slot count, NM03_BATCH_SPREAD): equal-size batches instead of full ones
-  // plus a remainder (465 slices at B = 64: 8 × 58–59 instead of 7 × 64 + 17), and a list shorter
-  // than one batch per slot (a rank's shard under strong scaling, one patient) split over up to
-  // that many slots with at least kSpreadMin slices each, so its loads, uploads, kernels and
-  // writes overlap across slots instead of running as one batch. Measured slower on the headline,
-  // config 2 and strong-scaling shards (profiles/r2/spread/): off by default.
-  static constexpr size_t kSpreadMin = 8;
-  static std::vector<std::pair<size_t, size_t>> plan_batches(size_t n, size_t B, bool taper, size_t spread_slots = 0) {
+  // Batch schedule: full batches plus a remainder. Measured and removed in round 4: a tapered
+  // schedule (small first/last batches: 209k vs 220k slices/s, 234.7k vs 232.2k re-measured) and a
+  // spread schedule (equal-size batches, short lists split over the slots: slower on the headline,
+  // config 2 and strong-scaling shards, profiles/r2/spread/).
+  static std::vector<std::pair<size_t, size_t>> plan_batches(size_t n, size_t B) {
     std::vector<std::pair<size_t, size_t>> out;
-    size_t first = 0;
-    auto take = [&](size_t c) {
-      c = std::min(c, n - first);
-      if (c) out.push_back({first, c});
-      first += c;
-    };
-    if (spread_slots > 0 && !taper && n > 0) {
-      size_t nb = (n + B - 1) / B;
-      if (nb < spread_slots) nb = std::max<size_t>(nb, std::min(spread_slots, n / kSpreadMin));
-      for (size_t b = 0; b < nb; ++b) take(n * (b + 1) / nb - n * b / nb);
-      return out;
-    }
-    if (!taper || B < 16 || n <= 2 * B) {
-      while (first < n) take(B);
-      return out;
-    }
-    take(B / 4);
-    take(B / 2);
-    while (n - first > B + B / 2) take(B);
-    const size_t left = n - first;
-    if (left > B / 2) {
-      take((left + 1) / 2);
-      const size_t rest = n - first;
-      take((rest + 1) / 2);
-    }
-    take(n - first);
+    for (size_t first = 0; first < n; first += B) out.push_back({first, std::min(B, n - first)});
     return out;
   }
 
@@ -1434,13 +1111,9 @@ struct Engine::Impl {
   std::condition_variable job_cv, done_cv;
   std::deque<std::shared_ptr<Job>> queue;  // runs with unclaimed batches, oldest first
   std::atomic<size_t> queued_jobs_{0};      // queue.size() for the idle slots' spin (no lock)
-  static int slot_spin_us() {
-    static const int us = [] {
-      const char* e = std::getenv("NM03_SLOT_SPIN_US");
-      return e && *e ? std::max(0, std::atoi(e)) : 500;
-    }();
-    return us;
-  }
+  // An idle slot spins up to 500 µs for the next run before sleeping on the job queue: +2.5-3%
+  // headline in 6/8 A/B pairs (profiles/r3/slot_spin), single pass unchanged.
+  static constexpr int kSlotSpinUs = 500;
   uint64_t seq_next = 0;
   size_t inflight = 0;  // submitted runs not finished yet
   bool quit = false;
@@ -1490,10 +1163,8 @@ struct Engine::Impl {
     for (;;) {
       std::shared_ptr<Job> j;
       size_t b;
-      // An idle slot spins up to NM03_SLOT_SPIN_US (default 500) for the next run before sleeping:
-      // +2.5-3% headline in 6/8 A/B pairs (profiles/r3/slot_spin), single pass unchanged.
-      if (const int us = slot_spin_us(); us > 0 && queued_jobs_.load(std::memory_order_acquire) == 0) {
-        const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(us);
+      if (queued_jobs_.load(std::memory_order_acquire) == 0) {
+        const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(kSlotSpinUs);
         while (queued_jobs_.load(std::memory_order_acquire) == 0 && std::chrono::steady_clock::now() < until)
           __builtin_ia32_pause();
       }
@@ -1528,12 +1199,11 @@ struct Engine::Impl {
     auto j = std::make_shared<Job>();
     j->t0 = now_s();
     j->items = std::move(items);
-    j->dirs = std::make_unique<IoDirs>(*j->items, !private_fds_);
+    j->dirs = std::make_unique<IoDirs>(*j->items);
     j->on_start = std::move(on_start);
     j->status.resize(j->items->size());
     const size_t B = batch_cap > 0 ? std::min<size_t>((size_t)batch_cap, (size_t)cfg.batch_size) : (size_t)cfg.batch_size;
-    j->batches = plan_batches(j->items->size(), B, cfg.taper,
-                              spread_ ? (size_t)cfg.streams : 0);
+    j->batches = plan_batches(j->items->size(), B);
     j->remaining = j->batches.size();
     {
       std::lock_guard<std::mutex> g(job_m);

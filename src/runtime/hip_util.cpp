@@ -21,6 +21,23 @@ bool sync_launches() {
   return on;
 }
 
+int profile_variant(const char* kernel) {
+  // NM03_PROFILE_VARIANT="jpeg=12,median=1": truncated kernel variants for time splits (output
+  // invalid; tools/gpu_jpeg_split.sh). Parsed once.
+  static const std::string spec = [] {
+    const char* s = std::getenv("NM03_PROFILE_VARIANT");
+    return std::string(s ? s : "");
+  }();
+  const std::string key = std::string(kernel) + "=";
+  for (size_t p = 0; p < spec.size();) {
+    size_t e = spec.find(',', p);
+    if (e == std::string::npos) e = spec.size();
+    if (spec.compare(p, key.size(), key) == 0) return std::atoi(spec.c_str() + p + key.size());
+    p = e + 1;
+  }
+  return 0;
+}
+
 void check_launch(const char* what) {
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) throw DeviceError(std::string("launch of ") + what + " failed: " + hipGetErrorString(e));

@@ -1,6 +1,9 @@
 #include "nm03/log.h"
 
 #include <dlfcn.h>
+#include <execinfo.h>
+#include <signal.h>
+#include <unistd.h>
 
 #include <cstdlib>
 #include <cstring>
@@ -84,6 +87,57 @@ const FaultPlan& fault_plan() {
     return f;
   }();
   return p;
+}
+
+namespace {
+
+void write_str(const char* s) {
+  ssize_t r = ::write(2, s, std::strlen(s));
+  (void)r;
+}
+
+void write_hex(uintptr_t v) {
+  char buf[2 + 16 + 1];
+  buf[0] = '0';
+  buf[1] = 'x';
+  for (int i = 0; i < 16; ++i) buf[2 + i] = "0123456789abcdef"[(v >> (60 - 4 * i)) & 15];
+  buf[18] = 0;
+  write_str(buf);
+}
+
+void crash_handler(int sig, siginfo_t* si, void*) {
+  // async-signal-safe only: write(2), backtrace (its libgcc is preloaded at install time)
+  write_str("\n[nm03] fatal signal ");
+  write_str(sig == SIGSEGV ? "SIGSEGV" : sig == SIGBUS ? "SIGBUS" : sig == SIGFPE ? "SIGFPE"
+            : sig == SIGILL ? "SIGILL" : "SIGABRT");
+  write_str(" at address ");
+  write_hex((uintptr_t)(si ? si->si_addr : nullptr));
+  write_str(", backtrace:\n");
+  void* frames[64];
+  const int n = backtrace(frames, 64);
+  backtrace_symbols_fd(frames, n, 2);
+  signal(sig, SIG_DFL);
+  raise(sig);
+}
+
+}  // namespace
+
+void install_crash_handler() {
+  static std::once_flag once;
+  std::call_once(once, [] {
+    void* warm[2];
+    (void)backtrace(warm, 2);  // loads libgcc_s now, not inside the handler
+    static char alt[64 * 1024];
+    stack_t ss{};
+    ss.ss_sp = alt;
+    ss.ss_size = sizeof alt;
+    sigaltstack(&ss, nullptr);
+    struct sigaction sa{};
+    sa.sa_sigaction = crash_handler;
+    sa.sa_flags = SA_SIGINFO | SA_ONSTACK | SA_RESETHAND;
+    sigemptyset(&sa.sa_mask);
+    for (int sig : {SIGSEGV, SIGBUS, SIGFPE, SIGILL, SIGABRT}) sigaction(sig, &sa, nullptr);
+  });
 }
 
 }  // namespace nm03

@@ -225,8 +225,6 @@ RankCpus rank_partition(const Topology& t, const std::vector<int>& rank_nodes, i
 Placement::Placement(int device, const std::vector<int>& cpus) {
   const char* e = std::getenv("NM03_NUMA");
   if (e && *e == '0') return;
-  const char* pin = std::getenv("NM03_PIN");
-  const bool per_core = pin && std::string(pin) == "core";
   if (!cpus.empty()) {  // a rank partition: exactly these CPUs (within the affinity mask)
     const std::vector<int> ok = allowed_cpus();
     for (int c : cpus)
@@ -235,58 +233,21 @@ Placement::Placement(int device, const std::vector<int>& cpus) {
   } else if (!read_line("/sys/devices/system/node/node1/cpulist").empty()) {  // multi-node host: the GPU's node
     node_ = device_node(device);
     cpus_ = node_cpus(node_);
-  } else if (per_core) {
-    cpus_ = allowed_cpus();
   }
-  if (per_core && !cpus_.empty()) cores_ = cores_of(read_topology("/sys", cpus_), cpus_);
-  if (pin && std::string(pin) == "l3" && !cpus_.empty()) {
-    const Topology t = read_topology("/sys", cpus_);
-    std::map<long, size_t> at;
-    for (int c : cpus_) {
-      const long key = (size_t)c < t.l3_of.size() ? t.l3_of[(size_t)c] : -1;
-      auto it = at.find(key);
-      if (it == at.end()) {
-        at.emplace(key, l3_groups_.size());
-        l3_groups_.push_back({c});
-      } else {
-        l3_groups_[it->second].push_back(c);
-      }
-    }
-    if (l3_groups_.size() < 2) l3_groups_.clear();  // one domain: nothing to key work to
-  }
-}
-
-static void bind_cpus(const std::vector<int>& cpus) {
-  cpu_set_t set;
-  CPU_ZERO(&set);
-  for (int c : cpus) CPU_SET(c, &set);
-  (void)pthread_setaffinity_np(pthread_self(), sizeof(set), &set);
-}
-
-void Placement::bind_worker(int i, int n) const {
-  if (cpus_.empty()) return;
-  if (!l3_groups_.empty()) {
-    bind_cpus(l3_groups_[(size_t)worker_group(i)]);
-    return;
-  }
-  if (cores_.empty() || n < 1) {
-    bind_this_thread();
-    return;
-  }
-  const size_t C = cores_.size();
-  const size_t k = (size_t)n <= C ? (size_t)i * C / (size_t)n : (size_t)i % C;
-  bind_cpus(cores_[k]);
 }
 
 void Placement::bind_this_thread() const {
   if (cpus_.empty()) return;
-  bind_cpus(cpus_);
+  cpu_set_t set;
+  CPU_ZERO(&set);
+  for (int c : cpus_) CPU_SET(c, &set);
+  (void)pthread_setaffinity_np(pthread_self(), sizeof(set), &set);
 }
 
 std::string Placement::describe() const {
   if (cpus_.empty()) return "numa: off";
   return "numa: node " + std::to_string(node_) + " (" + std::to_string(cpus_.size()) + " cpus: " +
-         format_cpulist(cpus_) + (l3_groups_.empty() ? "" : ", " + std::to_string(l3_groups_.size()) + " L3 groups") + ")";
+         format_cpulist(cpus_) + ")";
 }
 
 }  // namespace nm03::numa

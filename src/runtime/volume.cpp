@@ -487,6 +487,7 @@ std::vector<std::vector<uint8_t>> VolumeRunner::export_jpegs(const VolumeInput& 
     rs.bits = bits;
     rs.stats = V.stats.as<SliceStats>();
     rs.rd = drd;
+    rs.nrd = nc;
     launch_jpeg(X.canvas.as<uint8_t>(), reinterpret_cast<const JpegDesc*>(d_jd), nc, cw, ch, tables.div_luma, X.jw,
                 X.d_out, X.d_sizes, V.stream, &rs);
     check_hip(hipStreamSynchronize(V.stream), "export sync");

@@ -10,6 +10,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -513,29 +514,32 @@ TEST(thread_pool_for_each_exactly_once) {
   }
 }
 
-TEST(thread_pool_for_each_grouped_exactly_once_and_affine) {
+TEST(thread_pool_for_each_max_runners_exactly_once_and_bounded) {
   nm03::ThreadPool pool(6);
-  for (int groups : {1, 3, 4}) {
+  for (int cap : {0, 1, 3, 6, 9}) {
     for (size_t n : {0u, 1u, 7u, 500u}) {
       std::vector<std::atomic<int>> hits(n);
-      std::atomic<int> home{0}, away{0};
+      std::atomic<int> live{0}, peak{0};
       nm03::TaskGroup tg(pool);
-      tg.for_each_grouped(
+      tg.for_each(
           n,
           [&](size_t i) {
+            const int now = live.fetch_add(1) + 1;
+            int p = peak.load();
+            while (now > p && !peak.compare_exchange_weak(p, now)) {
+            }
             hits[i].fetch_add(1);
-            const int w = nm03::ThreadPool::current_worker();
-            ((int)(i % (size_t)groups) == w % groups ? home : away).fetch_add(1);
+            std::this_thread::sleep_for(std::chrono::microseconds(20));
+            live.fetch_sub(1);
           },
-          groups, [&](size_t i) { return (int)(i % (size_t)groups); }, [](int w) { return w; }, 3);
+          3, nullptr, cap);
       tg.wait();
       bool ok = true;
       for (auto& h : hits) ok &= h.load() == 1;
       CHECK(ok);
-      CHECK(home.load() + away.load() == (int)n);
+      CHECK(peak.load() <= (cap > 0 ? std::min(cap, 6) : 6));
     }
   }
-  CHECK(nm03::ThreadPool::current_worker() == -1);
 }
 
 TEST(thread_pool_priorities_order_a_single_worker) {

@@ -12,12 +12,12 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def _bench(tmp_path, *extra, env=None, timeout=240):
-    e = dict(os.environ, NM03_COMM_TIMEOUT_S="30", NM03_BENCH_NUMA_DATA="off")
+    e = dict(os.environ, NM03_COMM_TIMEOUT_S="30")
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
         e.pop(k, None)
     e.update(env or {})
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--dry-run", "--steps", "2", "--warmup", "1",
-           "--data-root", str(tmp_path / "data"), "--out-root", str(tmp_path / "out"), *extra]
+           "--data-root", str(tmp_path / "data"), "--out-root", str(tmp_path / "out"), "--numa-data", "off", *extra]
     return subprocess.run(cmd, cwd=str(tmp_path), env=e, capture_output=True, text=True, timeout=timeout)
 
 
@@ -59,7 +59,7 @@ def test_bench_auto_comm_records_rccl_failure(tmp_path):
 def test_bench_dead_rank_fails_job(tmp_path):
     """A rank that dies makes the job exit non-zero, naming the rank, well before the deadline."""
     t0 = time.monotonic()
-    r = _bench(tmp_path, "--gpus", "3", "--comm", "host", env={"NM03_BENCH_FAIL_RANK": "1"})
+    r = _bench(tmp_path, "--gpus", "3", "--comm", "host", env={"NM03_FAULT": "rank_exit:1"})
     dt = time.monotonic() - t0
     assert r.returncode != 0
     assert "rank 1 exited with status 5" in r.stderr
@@ -91,13 +91,13 @@ def test_bench_under_torchrun(tmp_path):
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
-    e = dict(os.environ, NM03_COMM_TIMEOUT_S="30", NM03_BENCH_NUMA_DATA="off")
+    e = dict(os.environ, NM03_COMM_TIMEOUT_S="30")
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT", "NM03_COMM_JOB"):
         e.pop(k, None)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
            "--gpus", "2", "--dry-run", "--steps", "2", "--warmup", "1",
-           "--data-root", str(tmp_path / "data"), "--out-root", str(tmp_path / "out")]
+           "--data-root", str(tmp_path / "data"), "--out-root", str(tmp_path / "out"), "--numa-data", "off"]
     r = subprocess.run(cmd, cwd=str(tmp_path), env=e, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     rec = _json_line(r.stdout)

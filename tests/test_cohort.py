@@ -114,3 +114,32 @@ def test_read_series_stacks_in_file_number_order(native, tmp_path):
     (d / "1-12.dcm").write_bytes(native.dicom_bytes(np.zeros((7, 5), np.uint16)))
     with pytest.raises(ValueError, match="differs"):
         read_series(str(d))
+
+
+def test_output_reaper_wipes_off_path(tmp_path):
+    """OutputReaper: an existing directory is empty right after wipe() (renamed aside and
+    re-created), its old files and subdirectories are deleted by the background threads (drain),
+    a missing directory is created, and trash left by a killed run in the parent is swept."""
+    from nm03_capstone_project_amd import native
+    n = native()
+    root = tmp_path / "out"
+    a, b = root / "PGBM-001", root / "PGBM-002"
+    a.mkdir(parents=True)
+    for i in range(50):
+        (a / f"{i}_original.jpg").write_bytes(b"x" * 100)
+    (a / "sub").mkdir()
+    (a / "sub" / "f").write_bytes(b"y")
+    stale = root / ".nm03-trash-1-7"
+    stale.mkdir()
+    (stale / "old.jpg").write_bytes(b"z")
+    r = n.OutputReaper(2)
+    r.wipe([str(a), str(b)])
+    assert a.is_dir() and list(a.iterdir()) == [] and b.is_dir()
+    (a / "new.jpg").write_bytes(b"n")  # the caller writes right away
+    r.drain()
+    assert sorted(p.name for p in root.iterdir()) == ["PGBM-001", "PGBM-002"]
+    assert [p.name for p in a.iterdir()] == ["new.jpg"]
+    assert r.files_reaped == 52
+    r.wipe([str(a)])  # second pass over the same parent
+    r.drain()
+    assert list(a.iterdir()) == [] and sorted(p.name for p in root.iterdir()) == ["PGBM-001", "PGBM-002"]

@@ -139,33 +139,24 @@ def _tree_bytes(items):
     return out
 
 
-@pytest.mark.parametrize("private", ["1", "0"])
-def test_host_only_private_fd_tables_identical(native, cohort_root, tmp_path, private):
-    """Pool workers with private fd tables (close_range UNSHARE) write the same files as with the
-    shared table, across two queued runs and fresh vs existing output trees. Each setting runs in a
-    fresh process: the engine reads NM03_PRIVATE_FDS once per process."""
+def test_host_only_queued_runs_fresh_and_existing_trees(native, cohort_root, tmp_path):
+    """Pool workers (private fd tables and creds) write the same files across two queued runs into
+    two trees, fresh (files created) then existing (rewritten in place)."""
     items = _items(native, cohort_root, str(tmp_path / "a"))
     items_b = _items(native, cohort_root, str(tmp_path / "b"))
-    script = (f"import sys; sys.path.insert(0, {ROOT!r}); import nm03_capstone_project_amd as nm; "
-              f"n = nm.native(); cfg = nm.PipelineConfig(batch_size=4, streams=2, threads=4).engine_config(); "
-              f"cfg.host_only = True; e = n.Engine(cfg); wa, wb = n.WorkList({items!r}), n.WorkList({items_b!r}); "
-              f"bad = 0\n"
-              f"for _ in range(2):\n"
-              f"    ta, tb = e.submit(wa), e.submit(wb)\n"
-              f"    bad += sum(len(e.wait(t)[1]) for t in (ta, tb))\n"
-              f"print(bad)")
-    r = subprocess.run([sys.executable, "-c", script], capture_output=True, text=True, timeout=300,
-                       env=dict(os.environ, NM03_PRIVATE_FDS=private))
-    assert r.returncode == 0, r.stderr[-2000:]
-    assert r.stdout.strip().splitlines()[-1] == "0"
+    eng = _engine(native, threads=4, batch_size=4, streams=2)
+    wa, wb = native.WorkList(items), native.WorkList(items_b)
+    for _ in range(2):
+        ta, tb = eng.submit(wa), eng.submit(wb)
+        assert sum(len(eng.wait(t)[1]) for t in (ta, tb)) == 0
+    del eng
     a, b = _tree_bytes(items), _tree_bytes(items_b)
     assert len(a) == 2 * len(items) and sorted(a.values()) == sorted(b.values())
 
 
-def test_private_fd_tables_do_not_hold_process_fds(native, cohort_root, tmp_path, monkeypatch):
+def test_private_fd_tables_do_not_hold_process_fds(native, cohort_root, tmp_path):
     """A worker's private table starts with stdin/out/err only: a pipe the process creates before
     the engine and closes afterwards must reach EOF while the engine (and its pool) is alive."""
-    monkeypatch.setenv("NM03_PRIVATE_FDS", "1")
     r, w = os.pipe()
     eng = _engine(native, threads=4)
     items = _items(native, cohort_root, str(tmp_path / "o"))
@@ -179,10 +170,8 @@ def test_private_fd_tables_do_not_hold_process_fds(native, cohort_root, tmp_path
     del eng
 
 
-def test_host_only_many_queued_runs_private_fds(native, cohort_root, tmp_path, monkeypatch):
-    """More runs in flight than a worker's directory-fd cache holds (LRU eviction of whole runs):
-    every run still writes every file."""
-    monkeypatch.setenv("NM03_PRIVATE_FDS", "1")
+def test_host_only_many_queued_runs(native, cohort_root, tmp_path):
+    """Eleven runs in flight at once: every run still writes every file."""
     eng = _engine(native, threads=4, batch_size=8, streams=3)
     trees = [_items(native, cohort_root, str(tmp_path / f"t{k}"))[:24] for k in range(11)]
     tickets = [eng.submit(native.WorkList(t)) for t in trees]
@@ -191,25 +180,3 @@ def test_host_only_many_queued_runs_private_fds(native, cohort_root, tmp_path, m
         assert not msgs
     for t in trees:
         assert len(_tree_bytes(t)) == 2 * len(t)
-
-
-@pytest.mark.parametrize("cred", ["1", "0"])
-def test_host_only_private_cred_identical(native, cohort_root, tmp_path, cred):
-    """Pool workers with their own struct cred (NM03_PRIVATE_CRED, the default) or the process's
-    shared one write the same bytes, twice over (create, then rewrite in place). Each setting runs in
-    a fresh process: the engine reads the variable once per process."""
-    items = _items(native, cohort_root, str(tmp_path / "o"))
-    script = (f"import sys; sys.path.insert(0, {ROOT!r}); import nm03_capstone_project_amd as nm; "
-              f"n = nm.native(); cfg = nm.PipelineConfig(batch_size=4, streams=2, threads=4).engine_config(); "
-              f"cfg.host_only = True; e = n.Engine(cfg); w = n.WorkList({items!r}); "
-              f"bad = [len(e.run_list(w)[1]) for _ in range(2)]; print(sum(bad))")
-    r = subprocess.run([sys.executable, "-c", script], capture_output=True, text=True, timeout=300,
-                       env=dict(os.environ, NM03_PRIVATE_CRED=cred))
-    assert r.returncode == 0, r.stderr[-2000:]
-    assert r.stdout.strip().splitlines()[-1] == "0"
-    ref = tmp_path / "ref"
-    ref_items = _items(native, cohort_root, str(ref))
-    st, _ = _engine(native, threads=2).run(ref_items)
-    assert all(c == 0 for c, _ in st)
-    got, want = _tree_bytes(items), _tree_bytes(ref_items)
-    assert sorted(got.values()) == sorted(want.values()) and len(got) == 2 * len(items)

@@ -248,16 +248,13 @@ def _tree(d):
 
 def test_engine_cohort_configs_identical(native, cohort_root, tmp_path):
     trees = []
-    # (batch, streams, threads, hipGraph replay); graph runs go twice through one engine so the
-    # second pass replays cached graphs.
-    for i, (b, s, t, g) in enumerate([(1, 1, 1, False), (25, 3, 8, True), (7, 2, 4, False), (64, 4, 16, True),
-                                      (64, 4, 16, False)]):
+    # (batch, streams, threads, passes through one engine): a second pass rewrites existing files.
+    for i, (b, s, t, g) in enumerate([(1, 1, 1, 1), (25, 3, 8, 2), (7, 2, 4, 1), (64, 4, 16, 2), (64, 4, 16, 1)]):
         out = str(tmp_path / f"o{i}")
         items = _items(native, cohort_root, out)
         ec = nm.PipelineConfig(batch_size=b, streams=s, threads=t).engine_config()
-        ec.graphs = g
         eng = native.Engine(ec)
-        for _ in range(2 if g else 1):
+        for _ in range(g):
             st, times = eng.run(items)
             assert all(code == 0 for code, _ in st), st
             assert times["slices_ok"] == len(items) and times["jpeg_fallbacks"] == 0
@@ -301,8 +298,8 @@ def test_engine_submit_pipelines_runs_identically(native, cohort_root, tmp_path)
     assert not msgs
 
 
-def test_engine_jpeg_cpu_fallback_identical(native, cohort_root, tmp_path, monkeypatch):
-    """Every image overflowing the GPU encoder's output capacity (NM03_JPEG_OUT_CAP forced tiny)
+def test_engine_jpeg_cpu_fallback_identical(native, cohort_root, tmp_path):
+    """Every image overflowing the GPU encoder's output capacity (EngineConfig.jpeg_out_cap tiny)
     goes through the host re-encode fallback — under 4 concurrent slots — and the files are
     byte-identical to the GPU-encoded ones; the fallbacks are counted."""
     ref_out = str(tmp_path / "ref")
@@ -310,7 +307,7 @@ def test_engine_jpeg_cpu_fallback_identical(native, cohort_root, tmp_path, monke
     cfg = nm.PipelineConfig(batch_size=6, streams=4, threads=8).engine_config()
     st, t = native.Engine(cfg).run(items)
     assert all(c == 0 for c, _ in st) and t["jpeg_fallbacks"] == 0
-    monkeypatch.setenv("NM03_JPEG_OUT_CAP", "2048")
+    cfg.jpeg_out_cap = 2048
     fb_out = str(tmp_path / "fb")
     st, t = native.Engine(cfg).run(_items(native, cohort_root, fb_out))
     assert all(c == 0 for c, _ in st)
@@ -344,7 +341,7 @@ def test_engine_fault_isolation(native, tmp_path):
 
 def test_engine_flat_label_waves_vs_golden(native, tmp_path):
     """Label images whose waves are one flat colour skip the FDCT, quantisation and zig-zag walk
-    (k4_jpeg.hip, NM03_JPEG_FLAT): every exported JPEG — all-background label images (uniform and
+    (k4_jpeg.hip): every exported JPEG — all-background label images (uniform and
     noise-only slices: no region grows), phantom slices with a partial region, and a slice whose
     region fills most of the canvas — is byte-identical to the golden encoder's."""
     d = tmp_path / "series"
@@ -440,61 +437,62 @@ def test_engine_pack12_holes_and_stored_bits(native, cohort_root, tmp_path, monk
     assert runs[0][1] == runs[1][1]
 
 
-def test_engine_fused_unpack_identical(native, cohort_root, tmp_path, monkeypatch):
-    """Upload expansion inside the median's tile load (default) vs the standalone K0 pass
-    (NM03_SEPARATE_UNPACK=1), with 12-bit packing on: byte-identical JPEGs on batches mixing packed
-    slices, a 13-bit slice (plain 16-bit blob, vector loads) and an odd-sized slice (plain blob,
-    W % 4 != 0: per-pixel loads) and a packed 200×112 slice (partial edge tiles in x and y)."""
+def test_engine_mixed_blob_layouts_identical(native, cohort_root, tmp_path, monkeypatch):
+    """The median decodes the upload in its tile load (12-bit pairs, plain 16-bit) and writes the
+    expanded samples for the render: batches mixing packed slices, a 13-bit slice (plain 16-bit
+    blob, vector loads), an odd-sized slice (plain blob, W % 4 != 0: per-pixel loads) and a packed
+    200×112 slice (partial edge tiles in x and y) give the same JPEGs with 12-bit packing on and off,
+    and the mixed slices match the golden model."""
     d = tmp_path / "mixed"
     d.mkdir()
     hi = native.phantom_slice(256, 256, 4, 11, 25, 9).astype(np.uint32) + 3000
     (d / "1-1.dcm").write_bytes(native.dicom_bytes(np.minimum(hi, 65535).astype(np.uint16)))
     (d / "1-2.dcm").write_bytes(native.dicom_bytes(native.phantom_slice(150, 203, 2, 7, 25, 3)))
     (d / "1-3.dcm").write_bytes(native.dicom_bytes(native.phantom_slice(112, 200, 2, 9, 25, 5)))
-    monkeypatch.setenv("NM03_PACK12", "1")
     runs = []
     for i, flag in enumerate(["1", "0"]):
+        monkeypatch.setenv("NM03_PACK12", flag)
         out = str(tmp_path / f"o{i}")
         items = _items(native, cohort_root, out)[:20]
         os.makedirs(os.path.join(out, "mixed"), exist_ok=True)
         extra = [(str(d / f"1-{k}.dcm"), os.path.join(out, "mixed")) for k in range(1, 4)]
         items = items[:5] + extra + items[5:]
-        monkeypatch.setenv("NM03_SEPARATE_UNPACK", flag)
         eng = native.Engine(nm.PipelineConfig(batch_size=8, streams=2, threads=4).engine_config())
         st, _ = eng.run(items)
         del eng
         runs.append(([c for c, _ in st], _tree(out)))
     assert runs[0][0] == runs[1][0] and runs[0][0].count(0) == len(runs[0][0])
     assert runs[0][1] == runs[1][1]
+    for k in range(1, 4):
+        f = str(d / f"1-{k}.dcm")
+        raw, meta = native.read_slice(f)
+        g = native.golden_run(raw, meta["type"], meta["stored_bits"], meta["slope"], meta["intercept"],
+                              native.PipelineParams(), native.RenderParams(), meta["spacing_x"], meta["spacing_y"])
+        assert runs[0][1][f"mixed/1-{k}_processed.jpg"] == g["jpeg_processed"]
+        assert runs[0][1][f"mixed/1-{k}_original.jpg"] == g["jpeg_original"]
 
 
-def test_engine_jpeg_d2h_identical(native, cohort_root, tmp_path, monkeypatch):
-    """JPEG export through HBM + gather + one SDMA copy (NM03_JPEG_D2H=1), through HBM + a gather
-    kernel storing into host-mapped memory (2) and with the encoder storing straight into
-    host-mapped memory (0): same statuses, byte-identical trees. The D2H runs
-    start with a 1 KiB-per-canvas copy estimate, so the first batches take the short-copy path (the
-    rest copied after the completion event) and later ones the grown estimate; eager and hipGraph
-    launches; a forced capacity overflow (CPU re-encode, negative sizes in the packed layout)."""
+def test_engine_jpeg_capacity_edge_identical(native, cohort_root, tmp_path):
+    """Output capacity at the edge of real segment sizes (20000 bytes: some images fit, some
+    overflow mid-image and take the CPU re-encode): statuses and trees identical to the default
+    capacity. Guards the encoder's exact end-of-range capacity check (a conservative bound once
+    let a workgroup drop its bytes while the image still reported a size)."""
     runs = []
-    for i, (d2h, graphs, cap) in enumerate([("0", False, ""), ("1", False, ""), ("1", True, ""), ("2", False, ""),
-                                            ("0", False, "20000"), ("1", False, "20000"), ("2", True, "20000")]):
+    for i, cap in enumerate([0, 20000]):
         out = str(tmp_path / f"o{i}")
         items = _items(native, cohort_root, out)[:40]
-        monkeypatch.setenv("NM03_JPEG_D2H", d2h)
-        monkeypatch.setenv("NM03_JPEG_D2H_EST_KB", "1")
-        monkeypatch.setenv("NM03_JPEG_OUT_CAP", cap)
-        eng = native.Engine(nm.PipelineConfig(batch_size=8, streams=2, threads=4, graphs=graphs).engine_config())
+        ec = nm.PipelineConfig(batch_size=8, streams=2, threads=4).engine_config()
+        ec.jpeg_out_cap = cap
+        eng = native.Engine(ec)
         st, _ = eng.run(items)
         del eng
         runs.append(([c for c, _ in st], _tree(out)))
-    for r in runs[1:]:
-        assert r[0] == runs[0][0] and r[0].count(0) == len(r[0])
-    diffs = {i: sorted(k for k in runs[0][1] if r[1].get(k) != runs[0][1][k])[:4]
-             for i, r in enumerate(runs) if r[1] != runs[0][1]}
+    assert runs[1][0] == runs[0][0] and runs[0][0].count(0) == len(runs[0][0])
+    diffs = sorted(k for k in runs[0][1] if runs[1][1].get(k) != runs[0][1][k])[:4]
     assert not diffs, diffs
 
 
-def test_engine_progressive_upload_identical(native, cohort_root, tmp_path, monkeypatch):
+def test_engine_progressive_upload_identical(native, cohort_root, tmp_path):
     """Progressive H2D (finished prefixes of a batch's raw region queued while loads run) with
     1 KiB / 64 KiB chunks vs one upload per batch: same statuses, byte-identical JPEGs, on a work
     list mixing slice sizes with unreadable and too-small files (failed loads leave holes in the
@@ -506,14 +504,15 @@ def test_engine_progressive_upload_identical(native, cohort_root, tmp_path, monk
     (d / "1-3.dcm").write_bytes(native.dicom_bytes(np.zeros((64, 64), np.uint16)))
     (d / "1-4.dcm").write_bytes(native.dicom_bytes(native.phantom_slice(512, 384, 3, 9, 25, 4)))
     runs = []
-    for i, kb in enumerate(["0", "1", "64"]):
+    for i, kb in enumerate([0, 1, 64]):
         out = str(tmp_path / f"o{i}")
         items = _items(native, cohort_root, out)[:40]
         os.makedirs(os.path.join(out, "extra"), exist_ok=True)
         extra = [(str(d / f"1-{k}.dcm"), os.path.join(out, "extra")) for k in range(1, 5)]
         items = items[:9] + extra[:2] + items[9:30] + extra[2:] + items[30:]
-        monkeypatch.setenv("NM03_UPLOAD_CHUNK_KB", kb)
-        eng = native.Engine(nm.PipelineConfig(batch_size=16, streams=3, threads=4).engine_config())
+        ec = nm.PipelineConfig(batch_size=16, streams=3, threads=4).engine_config()
+        ec.upload_chunk_kb = kb
+        eng = native.Engine(ec)
         st, _ = eng.run(items)
         del eng
         runs.append(([c for c, _ in st], _tree(out)))
@@ -523,16 +522,14 @@ def test_engine_progressive_upload_identical(native, cohort_root, tmp_path, monk
         assert tree == runs[0][1]
 
 
-def test_engine_shader_upload_and_batch_cap_identical(native, cohort_root, tmp_path, monkeypatch):
-    """Small batches uploaded by the shader copy from host-mapped memory (NM03_SHADER_UPLOAD_KB)
-    vs SDMA, with the batch cap of the single-pass measurement (run_list(items, cap)) and with the
-    private worker fd tables off: same statuses, byte-identical trees."""
+def test_engine_batch_cap_identical(native, cohort_root, tmp_path):
+    """The batch cap of the single-pass measurement (run_list(items, cap): small batches, inline
+    uploads on the slot's own stream, spin-polled completion) vs full batches: same statuses,
+    byte-identical trees."""
     runs = []
-    for i, (kb, cap, pfd) in enumerate([("0", 0, "1"), ("4096", 5, "1"), ("0", 5, "0"), ("4096", 0, "1")]):
+    for i, cap in enumerate([0, 5, 16]):
         out = str(tmp_path / f"o{i}")
         items = _items(native, cohort_root, out)[:37]
-        monkeypatch.setenv("NM03_SHADER_UPLOAD_KB", kb)
-        monkeypatch.setenv("NM03_PRIVATE_FDS", pfd)
         eng = native.Engine(nm.PipelineConfig(batch_size=16, streams=3, threads=4).engine_config())
         codes, msgs, _ = eng.run_list(native.WorkList(items), cap)
         del eng
@@ -543,9 +540,6 @@ def test_engine_shader_upload_and_batch_cap_identical(native, cohort_root, tmp_p
         assert tree == runs[0][1]
 
 
-# ---------------------------------------------------------------------------------------------
-# CLIs on the GPU: sequential ≡ parallel byte-for-byte, reference message catalogue
-# ---------------------------------------------------------------------------------------------
 def test_cli_sequential_equals_parallel(native, cohort_root, tmp_path):
     seq, par = tmp_path / "out-sequential", tmp_path / "out-parallel"
     r1 = run_bin("img_processing_sequential", "--data-root", cohort_root, "--out", str(seq))
@@ -628,11 +622,12 @@ def test_bench_multirank_one_gpu(native, tmp_path):
     import json
     import subprocess
     import sys
-    env = dict(os.environ, NM03_DEVICE_OVERRIDE="0", NM03_COMM_TIMEOUT_S="60", NM03_BENCH_NUMA_DATA="off")
+    env = dict(os.environ, NM03_DEVICE_OVERRIDE="0", NM03_COMM_TIMEOUT_S="60")
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT"):
         env.pop(k, None)
     r = subprocess.run([sys.executable, os.path.join(os.path.dirname(os.path.dirname(__file__)), "bench.py"),
-                        "--gpus", "2", "--steps", "2", "--warmup", "1", "--threads", "8",
+                        "--gpus", "2", "--steps", "2", "--warmup", "1", "--threads", "8", "--numa-data", "off",
+                        "--cli-runs", "2", "--single-passes", "5",
                         "--data-root", str(tmp_path / "d"), "--out-root", str(tmp_path / "o")],
                        env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-3000:]
@@ -640,6 +635,8 @@ def test_bench_multirank_one_gpu(native, tmp_path):
     assert rec["n_gpus"] == 2 and rec["value"] > 0 and rec["config"]["comm"]["backend"] == "host"
     assert rec["config"]["strong"]["value"] > 0 and rec["config"]["strong"]["global_batch"] * 2 == rec["config"]["global_batch"]
     assert sum(rec["config"]["per_rank"]["slices_ok"]) == 2 * rec["config"]["global_batch"]
+    cli = rec["config"]["cli_wall"]  # the whole img_processing_parallel --gpus 2, timed twice
+    assert cli["all_ok"] and cli["runs"] == 2 and cli["slices"] == rec["config"]["strong"]["global_batch"], cli
 
 
 def test_cli_test_pipeline_gpu_equals_cpu(native, cohort_root, tmp_path):
