@@ -96,6 +96,8 @@ def parse_args(argv=None):
                     help="wipe passes: rename each output directory aside and delete it on 2 background "
                          "reaper threads (cohort.h OutputReaper; the final drain is inside the clock), or "
                          "unlink everything before the pass on 8 threads (round 3)")
+    ap.add_argument("--wipe-depth", type=int, default=3,
+                    help="passes in flight (output trees) for the wipe passes")
     ap.add_argument("--create-writers", type=int, default=-1,
                     help="EngineConfig.create_writers: pool workers writing a batch's JPEGs at once while "
                          "its directories are being filled (-1 = engine default, 0 = no limit)")
@@ -320,6 +322,10 @@ def run_rank(args):
         # Pipelined passes rotate over `depth` output trees: runs in flight never write the same
         # file (pass k+depth is submitted only after pass k finished).
         depth = 1 if args.no_pipeline else pipeline_depth(len(mine))
+        if wipe and not args.no_pipeline:
+            # A wipe pass's set-up (wipe + rediscovery) runs on this thread while earlier passes are
+            # in the engine; with 3 trees it overlaps two passes instead of one.
+            depth = max(depth, args.wipe_depth)
         trees = [mine] + [_pass_items(mine, out_root, j) for j in range(1, depth)]
         works = [work] + [n.WorkList(t) for t in trees[1:]]
         # wipe: every pass first empties its patients' output directories, as every reference run
@@ -331,26 +337,31 @@ def run_rank(args):
         rediscover = wipe and scaling == "weak"
         my_out = out_root if world == 1 else os.path.join(out_root, f"replica-{rank:02d}")
 
-        def discover():
-            return plan_cohort(local_root, my_out, wipe=False).items
-
-        if rediscover and discover() != mine:
-            raise SystemExit(f"rank {rank}: rediscovered cohort differs from the planned shard")
-
         reaper = n.OutputReaper(2) if wipe and args.wipe_mode == "reaper" else None
+        # Output root of tree j (pass-j trees mirror the layout under out_root/pass-00j).
+        tree_roots = [my_out] + [os.path.join(out_root, f"pass-{j:03d}", os.path.relpath(my_out, out_root))
+                                 for j in range(1, depth)]
+
+        def discover(j, with_reaper):
+            """One native call: patients, per-patient wipe (reaper) or mkdir, series, work list."""
+            return n.WorkList.discover(local_root, tree_roots[j], reaper if with_reaper else None)
+
+        if rediscover and [tuple(x) for x in discover(0, False).items()] != [tuple(x) for x in mine]:
+            raise SystemExit(f"rank {rank}: rediscovered cohort differs from the planned shard")
 
         def pass_work(k):
             """Native work list of pass k; wipe passes first empty the pass's output tree (the
             reference's per-run rm -rf + mkdir)."""
             j = k % depth
+            if rediscover and reaper is not None:
+                return discover(j, True)  # wipes each patient directory as it goes
             if reaper is not None:
                 reaper.wipe(tree_dirs[j])
             elif wipe:
                 n.setup_output_dirs(tree_dirs[j], 8)
             if not rediscover:
                 return works[j]
-            items = discover()
-            return n.WorkList(items if j == 0 else _pass_items(items, out_root, j))
+            return discover(j, False)
 
         def passes(k_total, sink):
             if args.no_pipeline:

@@ -92,7 +92,7 @@ constexpr int kJpegWG = 256;     // luma blocks (threads) per workgroup = 64 MCU
 // 5 words apart (16 distinct banks mod 32) and its two block rows, 4 source rows apart, are offset
 // by 16 banks (disjoint sets) — the plain layout's 4-byte stride put 4 addresses on each bank.
 constexpr int kPatchLds = 5832;  // f32 elements (22.8 KiB; 256²: 18 × 324); larger footprints use global loads
-__device__ __forceinline__ int swz_col(int c, bool on) { return on ? c + (c >> 2) : c; }
+__device__ __forceinline__ int swz_col(int c) { return c + (c >> 2); }
 // One LDS region serves the render (source patch above) and then, once every block is rendered,
 // the workgroup's assembled bit range followed by its staged stuffed output bytes.
 constexpr int kUnionWords = kPatchLds + 1080;  // 27 KiB as before (4 workgroups per CU): bit ranges up to ~220 Kbit
@@ -146,18 +146,15 @@ __device__ __forceinline__ uint32_t priv_word(const uint32_t* pb, const uint32_t
 //  4. each thread writes its block's codes at its bit offset (atomicOr into the zeroed stage).
 // The last workgroup of an image publishes the total (or the overflow marker).
 // kOcc: target waves per SIMD (= workgroups per CU); kUnion: LDS words of the patch / bit-range
-// union. <4, kUnionWords> is the default; <5, kPatchLds + 232> fits 5 workgroups per CU (31.7 KiB)
-// at ≤ 96 VGPRs (NM03_JPEG_OCC=5, A/B).
+// union. 5 workgroups per CU (31.7 KiB, ≤ 96 VGPRs with spills) measured no better than 4 once
+// images were dealt round-robin (profiles/r3/jpeg_spread/split_and_occ5.txt).
 template <int kOcc, int kUnion>
 __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(kOcc))) void jpeg_fused_kernel(const uint8_t* __restrict__ canvas,
                                                              const JpegDesc* __restrict__ jd, int ncanvas, int out_w,
                                                              int out_h, QuantRecip q, JpegWork w, JpegRenderSrc rs,
                                                              uint8_t* __restrict__ out, int32_t* __restrict__ out_sizes,
-                                                             int dbgw) {
-  // dbgw: profiling variant in the low byte (NM03_JPEG_DBG), bit 8 = flat-wave path off (NM03_JPEG_FLAT=0),
-  // bit 10 = blocked image order (NM03_JPEG_SPREAD=0), bit 11 = plain staged rows (NM03_JPEG_SWIZZLE=0).
-  const int dbg = dbgw & 0xFF;
-  const bool flat_ok = !(dbgw & 0x100);
+                                                             int dbg) {
+  // dbg: profiling variant (NM03_PROFILE_VARIANT=jpeg=N; output invalid), 0 = the real encoder.
   __shared__ uint32_t actab[256];
   __shared__ uint32_t dctab[16];
   __shared__ int32_t sdc[kJpegWG];
@@ -188,13 +185,11 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(kOcc)))
   // Images are dealt round-robin over the dispatch order (workgroup b encodes image b mod
   // ncanvas): consecutive workgroups hit different ticket counters instead of `parts` of them
   // queueing on one address, and an image's parts start one `ncanvas` stride apart, so a part's
-  // predecessors have mostly finished encoding when it looks back (dbgw bit 10 / NM03_JPEG_SPREAD=0:
-  // the blocked order, A/B).
-  const bool spread = !(dbgw & 0x400);
-  const bool swz = !(dbgw & 0x800);  // swizzled gray staging (NM03_JPEG_SWIZZLE=0: plain rows, A/B)
-  const int img = spread ? (int)(blockIdx.x % (uint32_t)ncanvas) : (int)(blockIdx.x / (uint32_t)parts);
+  // predecessors have mostly finished encoding when it looks back (blocked order: 137.8–138.5 vs
+  // 118.9–119.0 µs per 96-slice batch, profiles/r3/jpeg_spread/).
+  const int img = (int)(blockIdx.x % (uint32_t)ncanvas);
   uint32_t ticket = 0;
-  if (tid == 0 && dbg != 9) {
+  if (tid == 0) {
     // The address goes through a VGPR the compiler cannot prove uniform: a uniform-address atomic
     // is rewritten into a wave-aggregated one whose result is waited for on the spot.
     // (Kept in the global address space: a flat atomic would also count in lgkmcnt and hold up
@@ -217,15 +212,11 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(kOcc)))
     // that image from the image's counter, so it only ever waits on parts whose workgroups have
     // already started — progress is guaranteed even when other kernels (other streams, other
     // processes on the same GPU) share the CUs or the queue is preempted. (Using the dispatch
-    // index as the part is ~5% faster, NM03_JPEG_DBG=9, but two encoders interleaving on the same
-    // XCDs can starve each other's predecessors: measured 2.3 s/step stalls with two ranks per
-    // GPU.) One counter per image keeps the serialised atomics per address at `parts`.
-    uint32_t p = spread ? blockIdx.x / (uint32_t)ncanvas : blockIdx.x - (uint32_t)img * (uint32_t)parts;
-    if (dbg != 9) {
-      p = ticket;
-      if (p == (uint32_t)parts - 1) atomicExch(&w.ticket[img], 0u);  // the image's last ticket
-    }
-    s_ticket = p;
+    // index as the part is ~5% faster, but two encoders interleaving on the same XCDs can starve
+    // each other's predecessors: measured 2.3 s/step stalls with two ranks per GPU.) One counter per
+    // image keeps the serialised atomics per address at `parts`.
+    if (ticket == (uint32_t)parts - 1) atomicExch(&w.ticket[img], 0u);  // the image's last ticket
+    s_ticket = ticket;
   }
   __syncthreads();
   // The part is workgroup-uniform: keep it in an SGPR.
@@ -240,8 +231,15 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(kOcc)))
   // ---- 0. stage the source rows of this workgroup in LDS (workgroup-uniform decision) ----------
   int ys0 = 0, pcols = 0;
   bool staged = false, lstaged = false;
+  // Flat label workgroup: every source pixel under the workgroup's blocks is background (label 0,
+  // no border) or inside the region (label 1, no border), so every block renders to one grey level
+  // and codes to DC diff 0 + EOB (and the MCU's chroma to 4 × "00"): 32 bits per MCU,
+  // 0x28A28A00, with only block 0's DC difference (to the previous workgroup) free. The workgroup
+  // then skips the render, the per-block coding and the scan, and fills its bit range as words.
+  bool wgflat = false;
+  int flat_v = 0;
   uint64_t* const slab = reinterpret_cast<uint64_t*>(spatch);  // label images reuse the area
-  if (d.render >= 0 && rd.kind == kRenderLabels && dbg != 12) {
+  if (d.render >= 0 && rd.kind == kRenderLabels) {
     // Label render rows: 4by .. 4by+3 for the workgroup's block rows → 8 per MCU row.
     const int m0 = part * (kJpegWG / 4), m1 = min(m0 + kJpegWG / 4, bpi >> 2) - 1;
     const int r0 = m0 / mcux, r1 = m1 / mcux;
@@ -250,21 +248,31 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(kOcc)))
       lstaged = true;
       ys0 = 8 * r0;
       pcols = nw;  // offset of the border plane
+      const int wrem = rd.src_w & 63;
+      int nonzero = 0, nonfill = 0;
       for (int i = tid; i < nw; i += kJpegWG) {
         const int j = i / wpr, k = i - j * wpr;
         const size_t wi = (size_t)clampi(ys0 + j, 0, rd.src_h - 1) * wpr + k;
-        slab[i] = rs.bits[rd.src_off + wi];
-        slab[nw + i] = rs.bits[rd.border_off + wi];
+        const uint64_t lab = rs.bits[rd.src_off + wi], brd = rs.bits[rd.border_off + wi];
+        slab[i] = lab;
+        slab[nw + i] = brd;
+        const uint64_t m = (k == wpr - 1 && wrem) ? (1ull << wrem) - 1ull : ~0ull;
+        nonzero |= ((lab | brd) & m) != 0;
+        nonfill |= ((~lab | brd) & m) != 0;
       }
-      __syncthreads();
+      const bool full = (part + 1) * kJpegWG <= bpi && dbg == 0;
+      const bool zero = __syncthreads_or(nonzero) == 0;
+      const bool fill = __syncthreads_or(nonfill) == 0;
+      wgflat = full && (zero || fill);
+      flat_v = zero ? 0 : (int)rd.fill;
     }
   }
-  if (d.render >= 0 && rd.kind == kRenderRawGray && dbg != 12) {  // dbg 12: A/B with global loads
+  if (d.render >= 0 && rd.kind == kRenderRawGray) {
     const int m0 = part * (kJpegWG / 4), m1 = min(m0 + kJpegWG / 4, bpi >> 2) - 1;
     const int r0 = m0 / mcux, r1 = m1 / mcux;
     const int nrows = 8 * (r1 - r0) + 10;
-    pcols = swz_col(rd.src_w + 1, swz) + 1;
-    if (swz) pcols += (4 - pcols % 8 + 8) % 8;  // row stride ≡ 4 (mod 8)
+    pcols = swz_col(rd.src_w + 1) + 1;
+    pcols += (4 - pcols % 8 + 8) % 8;  // row stride ≡ 4 (mod 8)
     if (nrows * pcols <= kPatchLds && !(rd.src_off & 1)) {
       staged = true;
       ys0 = 8 * r0 - 1;
@@ -291,20 +299,20 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(kOcc)))
         const int i = tid + t * kJpegWG;
         if (i < nw) {
           const int j = i / hw, k = i - j * hw;
-          spatch[j * pcols + swz_col(2 * k + 1, swz)] = value((uint16_t)(v[t] & 0xFFFFu));
-          spatch[j * pcols + swz_col(2 * k + 2, swz)] = value((uint16_t)(v[t] >> 16));
+          spatch[j * pcols + swz_col(2 * k + 1)] = value((uint16_t)(v[t] & 0xFFFFu));
+          spatch[j * pcols + swz_col(2 * k + 2)] = value((uint16_t)(v[t] >> 16));
         }
       }
       for (int i = tid + kU * kJpegWG; i < nw; i += kJpegWG) {  // larger footprints
         const int j = i / hw, k = i - j * hw;
         const uint32_t u = *reinterpret_cast<const uint32_t*>(src + (size_t)clampi(ys0 + j, 0, H - 1) * W + 2 * k);
-        spatch[j * pcols + swz_col(2 * k + 1, swz)] = value((uint16_t)(u & 0xFFFFu));
-        spatch[j * pcols + swz_col(2 * k + 2, swz)] = value((uint16_t)(u >> 16));
+        spatch[j * pcols + swz_col(2 * k + 1)] = value((uint16_t)(u & 0xFFFFu));
+        spatch[j * pcols + swz_col(2 * k + 2)] = value((uint16_t)(u >> 16));
       }
       // Clamped halo columns 0 and W+1.
       for (int i = tid; i < 2 * nrows; i += kJpegWG) {
         const int j = i >> 1, right = i & 1;
-        spatch[j * pcols + (right ? swz_col(W + 1, swz) : 0)] =
+        spatch[j * pcols + (right ? swz_col(W + 1) : 0)] =
             value(src[(size_t)clampi(ys0 + j, 0, H - 1) * W + (right ? W - 1 : 0)]);
       }
       __syncthreads();
@@ -320,7 +328,9 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(kOcc)))
   uint32_t* const pspill = w.spill + ((size_t)blockIdx.x * kJpegWG + tid) * kSpillWords;
   int dc0 = 0;
   uint32_t acbits = 0;
-  if (valid) {
+  if (wgflat) {
+    dc0 = quant_recip(64 * (flat_v - 128), q, 0);
+  } else if (valid) {
     const int mcu = b >> 2, sub = b & 3;
     const int bx = 2 * (mcu % mcux) + (sub & 1), by = 2 * (mcu / mcux) + (sub >> 1);
     int32_t blk[64];
@@ -342,14 +352,14 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(kOcc)))
       bool same = true;
 #pragma unroll
       for (int i = 1; i < 64; ++i) same = same && blk[i] == blk[0];  // 15 distinct cells after CSE
-      flat = flat_ok && __ballot(!same) == 0;
+      flat = __ballot(!same) == 0;
     } else if (staged) {
       // Patch element (j, i) = source (4by-1+j, 4bx-1+i) = staged row 4by-1+j-ys0, column 4bx+i.
       // Patch column i = source column 4bx-1+i = staged column 4bx+i → swizzled 5bx + i + (i ≥ 4).
-      const float* pp = spatch + (4 * by - 1 - ys0) * pcols + (swz ? 5 : 4) * bx;
-      render_patch_2x([&](int j, int i) { return pp[j * pcols + i + (swz && i >= 4 ? 1 : 0)]; }, win, blk);
+      const float* pp = spatch + (4 * by - 1 - ys0) * pcols + 5 * bx;
+      render_patch_2x([&](int j, int i) { return pp[j * pcols + i + (i >= 4 ? 1 : 0)]; }, win, blk);
     } else if (d.render >= 0) {
-      render_block_2x(rd, rs.raw, rs.f32, rs.bits, win, bx, by, blk, dbg == 11);
+      render_block_2x(rd, rs.raw, rs.f32, rs.bits, win, bx, by, blk);
     } else {
       const uint8_t* src = canvas + d.canvas_off + (size_t)(by * 8) * out_w + bx * 8;
 #pragma unroll
@@ -459,35 +469,60 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(kOcc)))
     if (tid == 0) s_prevdc = dcp;
   }
   __syncthreads();
-  // DC code (Huffman symbol + magnitude bits, ≤ 20 bits, right-aligned).
-  const int diff = dc0 - (tid ? sdc[tid - 1] : s_prevdc);
-  const int dn = mag_bits_fast(diff);
-  const uint32_t dce = dctab[dn];
-  const int dclen = valid ? (int)(dce >> 16) + dn : 0;
-  const uint32_t dccode = ((dce & 0xFFFFu) << dn) | ((uint32_t)(diff < 0 ? diff - 1 : diff) & ((1u << dn) - 1u));
-  const uint32_t bits = valid ? (uint32_t)dclen + acbits : 0u;
-  // ---- 3. workgroup scan, bit range assembled in LDS ----------------------------------------
-  uint32_t agg = 0;
-  const uint32_t excl = block_exclusive_scan(bits, sh, &agg);  // ends with a barrier
-  // Each block's DC code, then its AC words shifted behind it, into the workgroup's contiguous
-  // bit range (MSB-first words), in the LDS region the render patch used. A range too long for
-  // it (> ~220 Kbit: pathological detail) poisons the image, which the host then re-encodes.
-  const uint32_t nlocal = (agg + 31) >> 5;
-  const bool in_lds = nlocal + 2u <= (uint32_t)kUnion;  // workgroup-uniform
-  const uint32_t nwp = (acbits + 31) >> 5;
-  const uint32_t acpos = excl + (uint32_t)dclen;
-  if (in_lds) {
-    for (uint32_t i = tid; i <= nlocal; i += kJpegWG) swg[i] = 0u;
-    __syncthreads();
-    if (valid) {
-      const uint32_t dv = dclen ? dccode << (32 - dclen) : 0u, sh0 = excl & 31u, w0 = excl >> 5;
-      atomicOr(&swg[w0], dv >> sh0);
-      if (sh0) atomicOr(&swg[w0 + 1], dv << (32u - sh0));
-      const uint32_t shf = acpos & 31u, wa = acpos >> 5;
-      for (uint32_t i = 0; i < nwp; ++i) {
-        const uint32_t v = priv_word(pbuf, pspill, i);
-        atomicOr(&swg[wa + i], v >> shf);
-        if (shf) atomicOr(&swg[wa + i + 1], v << (32u - shf));
+  uint32_t agg = 0, nlocal = 0;
+  bool in_lds = true;
+  if (wgflat) {
+    // Block 0: its DC code (L0 bits) + EOB; then the periodic MCU pattern from its 7th bit on.
+    const int diff0 = dc0 - s_prevdc;
+    const int dn0 = mag_bits_fast(diff0);
+    const uint32_t dce0 = dctab[dn0];
+    const uint32_t L0 = (dce0 >> 16) + (uint32_t)dn0;
+    const uint32_t code0 =
+        ((dce0 & 0xFFFFu) << dn0) | ((uint32_t)(diff0 < 0 ? diff0 - 1 : diff0) & ((1u << dn0) - 1u));
+    constexpr uint32_t kMcu = 0x28A28A00u;  // (00 1010) × 4 luma blocks + 4 × 00 chroma, MSB first
+    agg = L0 + 4u + (uint32_t)(kJpegWG - 1) * 6u + (uint32_t)(kJpegWG / 4) * 8u;
+    nlocal = (agg + 31u) >> 5;
+    // Range bit k ≥ L0 + 4 is pattern bit (k − (L0 − 2)) mod 32: every word is the pattern rotated
+    // left by (2 − L0) mod 32; word 0 starts with block 0's codes.
+    const uint32_t rot = (34u - L0) & 31u;
+    const uint32_t pat = rot ? (kMcu << rot) | (kMcu >> (32u - rot)) : kMcu;
+    const uint32_t hl = L0 + 4u;  // ≤ 24 bits
+    for (uint32_t i = tid; i <= nlocal + 1u; i += kJpegWG) {
+      uint32_t v = i < nlocal ? pat : 0u;
+      if (i == 0) v = (((code0 << 4) | 0xAu) << (32u - hl)) | (pat & ((1u << (32u - hl)) - 1u));
+      if (i == nlocal - 1u && (agg & 31u)) v &= ~0u << (32u - (agg & 31u));
+      swg[i] = v;
+    }
+  } else {
+    // DC code (Huffman symbol + magnitude bits, ≤ 20 bits, right-aligned).
+    const int diff = dc0 - (tid ? sdc[tid - 1] : s_prevdc);
+    const int dn = mag_bits_fast(diff);
+    const uint32_t dce = dctab[dn];
+    const int dclen = valid ? (int)(dce >> 16) + dn : 0;
+    const uint32_t dccode = ((dce & 0xFFFFu) << dn) | ((uint32_t)(diff < 0 ? diff - 1 : diff) & ((1u << dn) - 1u));
+    const uint32_t bits = valid ? (uint32_t)dclen + acbits : 0u;
+    // ---- 3. workgroup scan, bit range assembled in LDS ----------------------------------------
+    const uint32_t excl = block_exclusive_scan(bits, sh, &agg);  // ends with a barrier
+    // Each block's DC code, then its AC words shifted behind it, into the workgroup's contiguous
+    // bit range (MSB-first words), in the LDS region the render patch used. A range too long for
+    // it (> ~220 Kbit: pathological detail) poisons the image, which the host then re-encodes.
+    nlocal = (agg + 31) >> 5;
+    in_lds = nlocal + 2u <= (uint32_t)kUnion;  // workgroup-uniform
+    const uint32_t nwp = (acbits + 31) >> 5;
+    const uint32_t acpos = excl + (uint32_t)dclen;
+    if (in_lds) {
+      for (uint32_t i = tid; i <= nlocal; i += kJpegWG) swg[i] = 0u;
+      __syncthreads();
+      if (valid) {
+        const uint32_t dv = dclen ? dccode << (32 - dclen) : 0u, sh0 = excl & 31u, w0 = excl >> 5;
+        atomicOr(&swg[w0], dv >> sh0);
+        if (sh0) atomicOr(&swg[w0 + 1], dv << (32u - sh0));
+        const uint32_t shf = acpos & 31u, wa = acpos >> 5;
+        for (uint32_t i = 0; i < nwp; ++i) {
+          const uint32_t v = priv_word(pbuf, pspill, i);
+          atomicOr(&swg[wa + i], v >> shf);
+          if (shf) atomicOr(&swg[wa + i + 1], v << (32u - shf));
+        }
       }
     }
   }
@@ -690,7 +725,7 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(kOcc)))
   uint8_t* dst = out + d.out_off + s_obase;
   // Staged bytes sit at the destination's 16-byte phase behind the bit range, so 16-byte chunks of
   // the output are 16-byte chunks of LDS (one ds_read_b128 + one dwordx4 host store per lane).
-  const uint32_t phase = dbg == 13 ? 0u : (uint32_t)((uintptr_t)dst & 15u);
+  const uint32_t phase = (uint32_t)((uintptr_t)dst & 15u);
   uint8_t* sbuf = reinterpret_cast<uint8_t*>(swg + ((s_nwords + 3u) & ~3u)) + phase;  // behind the bit range
   const bool staged_out = tot + phase <= (uint32_t)(kUnion - ((s_nwords + 3u) & ~3u)) * 4u;
   for (uint32_t j = j0; j < j1; ++j) {
@@ -709,31 +744,17 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(kOcc)))
       if (tot == 0x7FFFFFF1u) out_sizes[0] = sbuf[tid];
       return;
     }
-    if (dbg == 13) {
-      // r2 form: dword stores (byte head up to the first 4-aligned address, byte tail).
-      const uint32_t head = min(tot, (uint32_t)((4u - ((uintptr_t)dst & 3u)) & 3u));
-      if (tid < head) dst[tid] = sbuf[tid];
-      const uint32_t nd = (tot - head) >> 2;
-      uint32_t* dw = reinterpret_cast<uint32_t*>(dst + head);
-      for (uint32_t i = tid; i < nd; i += kJpegWG) {
-        const uint8_t* b = sbuf + head + 4u * i;
-        dw[i] = (uint32_t)b[0] | ((uint32_t)b[1] << 8) | ((uint32_t)b[2] << 16) | ((uint32_t)b[3] << 24);
-      }
-      const uint32_t t0 = head + 4u * nd;
-      if (t0 + tid < tot) dst[t0 + tid] = sbuf[t0 + tid];
-    } else {
-      // Chunk c covers destination bytes [16c − phase, 16c + 16 − phase) of the range; the first and
-      // last chunks may be partial (byte stores), the rest move whole.
-      const uint32_t nchunks = (phase + tot + 15u) >> 4;
-      uint8_t* const dbase = dst - phase;  // 16-byte aligned
-      const uint8_t* const lbase = sbuf - phase;
-      for (uint32_t c = tid; c < nchunks; c += kJpegWG) {
-        const uint32_t b0 = 16u * c, lo = max(b0, phase), hi = min(b0 + 16u, phase + tot);
-        if (lo == b0 && hi == b0 + 16u) {
-          *reinterpret_cast<uint4*>(dbase + b0) = *reinterpret_cast<const uint4*>(lbase + b0);
-        } else {
-          for (uint32_t k = lo; k < hi; ++k) dbase[k] = lbase[k];
-        }
+    // Chunk c covers destination bytes [16c − phase, 16c + 16 − phase) of the range; the first and
+    // last chunks may be partial (byte stores), the rest move whole.
+    const uint32_t nchunks = (phase + tot + 15u) >> 4;
+    uint8_t* const dbase = dst - phase;  // 16-byte aligned
+    const uint8_t* const lbase = sbuf - phase;
+    for (uint32_t c = tid; c < nchunks; c += kJpegWG) {
+      const uint32_t b0 = 16u * c, lo = max(b0, phase), hi = min(b0 + 16u, phase + tot);
+      if (lo == b0 && hi == b0 + 16u) {
+        *reinterpret_cast<uint4*>(dbase + b0) = *reinterpret_cast<const uint4*>(lbase + b0);
+      } else {
+        for (uint32_t k = lo; k < hi; ++k) dbase[k] = lbase[k];
       }
     }
   }

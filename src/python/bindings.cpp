@@ -589,7 +589,35 @@ PYBIND11_MODULE(_nm03, m) {
         for (auto& p : items) w.items->push_back({p.first, p.second});
         return w;
       }))
-      .def("__len__", [](const WorkList& w) { return w.items->size(); });
+      .def("__len__", [](const WorkList& w) { return w.items->size(); })
+      .def("items", [](const WorkList& w) {
+        std::vector<std::pair<std::string, std::string>> v;
+        v.reserve(w.items->size());
+        for (auto& it : *w.items) v.push_back({it.path, it.out_dir});
+        return v;
+      })
+      // A reference run's set-up in one native call (main_sequential.cpp:93-168, 32-47): discover
+      // the PGBM-* patients under data_root's cohort directory, per patient wipe (through `reaper`:
+      // rename aside + background deletion) or create <out_root>/<pid>, list its first series in
+      // reference order, and build the work list.
+      .def_static(
+          "discover",
+          [](const std::string& data_root, const std::string& out_root, cohort::OutputReaper* reaper) {
+            py::gil_scoped_release nogil;
+            WorkList w;
+            const std::string base = cohort::cohort_dir(data_root);
+            for (const auto& pid : cohort::find_patient_dirs(base)) {
+              const std::string out = out_root + "/" + pid;
+              if (reaper)
+                reaper->wipe(out);
+              else
+                cohort::make_dirs(out);
+              cohort::Series s = cohort::list_patient_series(base, pid);
+              for (auto& f : s.files) w.items->push_back({std::move(f), out});
+            }
+            return w;
+          },
+          py::arg("data_root"), py::arg("out_root"), py::arg("reaper") = nullptr);
   struct Ticket {
     RunTicket t;
   };

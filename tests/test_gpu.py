@@ -370,6 +370,43 @@ def test_engine_flat_label_waves_vs_golden(native, tmp_path):
         assert (out / f"{stem}_processed.jpg").read_bytes() == g["jpeg_processed"], stem
 
 
+def test_engine_flat_label_workgroups_vs_golden(native, tmp_path):
+    """Whole label workgroups of one level (k4_jpeg.hip wgflat: the bit range filled with the
+    0x28A28A00 MCU pattern, no render, coding or scan) next to workgroups that code normally: a slice
+    entirely in the SRG band (every workgroup flat at the fill level, the image's first DC difference
+    ≠ 0), half-band slices (fill above, background below: the boundary workgroup codes the border and
+    the next flat workgroup starts with a large negative DC difference), stripes, and a 264×256 slice
+    (the label canvas is not an exact 2× fit: generic path). Byte-identical to the golden encoder."""
+    d = tmp_path / "series"
+    d.mkdir()
+    full = np.full((256, 256), 1500, np.uint16)
+    half = np.zeros((256, 256), np.uint16)
+    half[:128] = 1500
+    halfb = np.zeros((256, 256), np.uint16)
+    halfb[128:] = 1500
+    stripes = np.zeros((256, 256), np.uint16)
+    stripes[::40] = 1500
+    stripes[:, 100:140] = 1500
+    odd = np.full((264, 256), 1500, np.uint16)
+    odd[200:] = 0
+    out = tmp_path / "out"
+    out.mkdir()
+    items = []
+    for i, a in enumerate([full, half, halfb, stripes, odd], start=1):
+        (d / f"1-{i}.dcm").write_bytes(native.dicom_bytes(a))
+        items.append((str(d / f"1-{i}.dcm"), str(out)))
+    st, times = native.Engine(nm.PipelineConfig(batch_size=8, streams=1, threads=2).engine_config()).run(items)
+    assert all(c == 0 for c, _ in st), st
+    assert times["jpeg_fallbacks"] == 0
+    for f, _ in items:
+        raw, meta = native.read_slice(f)
+        g = native.golden_run(raw, meta["type"], meta["stored_bits"], meta["slope"], meta["intercept"],
+                              native.PipelineParams(), native.RenderParams(), meta["spacing_x"], meta["spacing_y"])
+        stem = os.path.splitext(os.path.basename(f))[0]
+        assert (out / f"{stem}_processed.jpg").read_bytes() == g["jpeg_processed"], stem
+        assert (out / f"{stem}_original.jpg").read_bytes() == g["jpeg_original"], stem
+
+
 def test_engine_pack12_identical(native, cohort_root, tmp_path, monkeypatch):
     """12-bit transfer packing (nm03/pack12.h + K0 unpack) on vs off: byte-identical JPEGs and the
     same statuses, on batches mixing packable 12-bit slices, a slice with 13-bit samples (shipped as
