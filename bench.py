@@ -96,6 +96,8 @@ def parse_args(argv=None):
                     help="wipe passes: rename each output directory aside and delete it on 2 background "
                          "reaper threads (cohort.h OutputReaper; the final drain is inside the clock), or "
                          "unlink everything before the pass on 8 threads (round 3)")
+    ap.add_argument("--reaper-threads", type=int, default=4,
+                    help="background deletion threads of the wipe passes (--wipe-mode reaper)")
     ap.add_argument("--wipe-depth", type=int, default=3,
                     help="passes in flight (output trees) for the wipe passes")
     ap.add_argument("--create-writers", type=int, default=-1,
@@ -337,7 +339,7 @@ def run_rank(args):
         rediscover = wipe and scaling == "weak"
         my_out = out_root if world == 1 else os.path.join(out_root, f"replica-{rank:02d}")
 
-        reaper = n.OutputReaper(2) if wipe and args.wipe_mode == "reaper" else None
+        reaper = n.OutputReaper(args.reaper_threads) if wipe and args.wipe_mode == "reaper" else None
         # Output root of tree j (pass-j trees mirror the layout under out_root/pass-00j).
         tree_roots = [my_out] + [os.path.join(out_root, f"pass-{j:03d}", os.path.relpath(my_out, out_root))
                                  for j in range(1, depth)]
@@ -566,6 +568,7 @@ def run_rank(args):
                                                "rank0_process_cpu_ms_per_step": wiped["rank0_process_cpu_ms_per_step"],
                                                "cgroup_cpu_ms_per_step": wiped["cgroup_cpu_ms_per_step"],
                                                "wipe_mode": args.wipe_mode,
+                                               "reaper_threads": args.reaper_threads,
                                                "rank0_stage_s": wiped["rank0_stage_s"]}
         if secondary is not None:
             rec["config"][other] = {k: (round(v, 3) if isinstance(v, float) else v) for k, v in secondary.items()

@@ -58,6 +58,18 @@ class Comm {
   // `rbytes` from rank `src`; -1 = no such peer. Used for z-slab halo planes. RCCL:
   // grouped ncclSend/ncclRecv over xGMI; host comms: through the segment slots.
   virtual void sendrecv(const void* send, size_t sbytes, int dst, void* recv, size_t rbytes, int src) = 0;
+  // Device-memory forms for the z-slab exchange: `send` / `recv` / `v` are device
+  // pointers and `stream` the caller's hipStream_t. RCCL enqueues grouped ncclSend/ncclRecv (and
+  // ncclAllReduce) on `stream`, straight from and into those buffers over xGMI: no host staging and
+  // no host synchronisation for the exchange. The other comms stage through pinned host memory with
+  // asynchronous copies on `stream` and one synchronisation per call.
+  virtual void sendrecv_device(const void* send, size_t sbytes, int dst, void* recv, size_t rbytes, int src,
+                               void* stream);
+  // Sums the int64 at device address `v` over all ranks (in place) and returns the total on the
+  // host once everything enqueued on `stream` before it has completed (a bounded wait).
+  virtual int64_t allreduce_sum_i64_device(int64_t* v, void* stream);
+  // True when the device forms above move data device to device (RCCL).
+  virtual bool device_native() const { return false; }
 
   // What the transport itself reports — RCCL: ncclCommCount / ncclCommUserRank / ncclCommCuDevice —
   // so a run record can show that N ranks really formed one communicator over N devices. Host
@@ -76,10 +88,12 @@ class Comm {
 };
 
 // Deadline of one blocking collective wait: NM03_COMM_TIMEOUT_S (default 120 s). A hang detector,
-// not a phase budget: ranks started by launch_ranks wait without a deadline unless the variable is
+// not a phase budget: ranks started by launch_ranks wait up to 30 minutes unless the variable is
 // set (its supervisor turns a dead rank into the abort flag within milliseconds).
 double comm_timeout_s();
 constexpr double kNoDeadline = 1e9;  // ≈ 30 years
+// Default collective deadline of ranks under launch_ranks' supervisor (LaunchOptions::from_env).
+constexpr double kSupervisedDeadlineS = 1800.0;
 
 // ---- process-shared control segment -------------------------------------------------------------
 // Host collectives, the RCCL unique-id hand-off and the job abort flag live here.

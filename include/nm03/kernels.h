@@ -79,6 +79,10 @@ void border_volume(const uint64_t* src, uint64_t* dst, int w, int h, int d, int 
 // Cube dilation of a bit volume (size odd), separable; `tmp` same size as the volume.
 void dilate_volume(const uint64_t* src, uint64_t* dst, uint64_t* tmp, int w, int h, int d, int size,
                    hipStream_t stream, uint64_t* scratch = nullptr);
+// z-slab boundary step (volume_slabs.h), one plane: add = band ∧ touch(nb) ∧ ¬region, region |= add,
+// *added += popcount(add); touch = nb (6-connectivity) or its 3×3 in-plane dilation (26).
+void launch_slab_seed(const uint64_t* band, uint64_t* region, const uint64_t* nb, int w, int h, bool conn26,
+                      unsigned long long* added, hipStream_t stream);
 
 // K3: render canvases (out_w×out_h u8 each).
 void launch_render(const uint16_t* raw, const float* f32, const uint64_t* bits, const SliceStats* stats,

@@ -55,13 +55,19 @@ def _proc_start_time(pid):
 
 def segment_name():
     """Segment name every local rank of this job derives on its own: bench.py's job id, or the
-    spawning agent's (pid, start time) + MASTER_PORT under torchrun. (pid, start time) names one
+    spawning agent's (pid, start time) + MASTER_PORT under torchrun, plus the elastic restart count
+    and run id: a torchrun restart (--max-restarts) spawns a new generation of workers under the
+    same agent, which must not find the previous generation's segment. (pid, start time) names one
     process since boot, so a segment left behind by an earlier job can never be picked up."""
     job = os.environ.get("NM03_COMM_JOB", "")
     if job:
         return f"/nm03-comm-{job}"
     ppid = os.getppid()
-    return f"/nm03-comm-{ppid}-{_proc_start_time(ppid)}-{os.environ.get('MASTER_PORT', '0')}"
+    gen = os.environ.get("TORCHELASTIC_RESTART_COUNT", "0")
+    run = os.environ.get("TORCHELASTIC_RUN_ID", "")
+    run = "".join(c for c in run if c.isalnum())[:24]
+    return (f"/nm03-comm-{ppid}-{_proc_start_time(ppid)}-{os.environ.get('MASTER_PORT', '0')}-g{gen}"
+            + (f"-{run}" if run else ""))
 
 
 def unlink_segment(name):
@@ -81,7 +87,13 @@ def make_native_comm(rank, world, device, backend=None, timeout_s=None):
         return n.self_comm(), {"backend": "self"}
     timeout_s = float(timeout_s or n.comm_timeout_s())
     be, may_fall_back = resolve_backend(world, backend)
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+    if local_world != world:
+        raise RuntimeError(f"native comm: LOCAL_WORLD_SIZE={local_world} != WORLD_SIZE={world}: the shared-segment "
+                           "rendezvous serves one node only (launch every rank on this node)")
     name = segment_name()
+    if rank == 0:
+        unlink_segment(name)  # a segment of this name can only be a dead generation's leftover
     seg = n.shm_create(world, name)[0] if rank == 0 else n.shm_attach(name, world, timeout_s)
     # Every rank removes the name at exit in case rank 0 died before unlinking it (all ranks have
     # attached before any collective returns, so this never races an attach).

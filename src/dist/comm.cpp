@@ -398,11 +398,13 @@ LaunchOptions LaunchOptions::from_env() {
   if (const char* e = std::getenv("NM03_COMM"); e && *e) o.comm = e;
   if (const char* e = std::getenv("NM03_DEVICE_OVERRIDE"); e && *e) o.device_override = std::atoi(e);
   // Ranks under this launcher's supervisor: a dead rank raises the abort flag at once, so the
-  // collectives need no deadline for liveness. Rank 0 may plan (wipe, list, scan headers) while
+  // deadline is not what detects a dead peer. Rank 0 may plan (wipe, list, scan headers) while
   // the others wait, and ranks wait for the slowest shard at the end — healthy phases of any
-  // length. The deadline stays a hang detector, on only when NM03_COMM_TIMEOUT_S asks for one.
+  // length, so the default is generous: 30 minutes. It still turns a rank that is alive but stuck
+  // (a GPU hang) into an error on its peers instead of a job that never ends.
+  // NM03_COMM_TIMEOUT_S overrides.
   const char* t = std::getenv("NM03_COMM_TIMEOUT_S");
-  o.timeout_s = (t && *t) ? comm_timeout_s() : kNoDeadline;
+  o.timeout_s = (t && *t) ? comm_timeout_s() : kSupervisedDeadlineS;
   return o;
 }
 

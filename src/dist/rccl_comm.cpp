@@ -94,6 +94,32 @@ class RcclComm final : public Comm {
     if (rbytes) hip_ck(hipMemcpyAsync(recv, drecv, rbytes, hipMemcpyDeviceToHost, stream_), "D2H");
     wait("ncclSend/ncclRecv");
   }
+  // z-slab planes straight between device buffers on the caller's stream: nothing staged, nothing
+  // waited for here (the stream orders the exchange behind the producer and before the consumers).
+  void sendrecv_device(const void* send, size_t sbytes, int dst, void* recv, size_t rbytes, int src,
+                       void* stream) override {
+    if (dst < 0) sbytes = 0;
+    if (src < 0) rbytes = 0;
+    if (!sbytes && !rbytes) return;
+    if (!comm_) throw CommError("RCCL communicator was aborted");
+    if (seg_) seg_->check_abort(rank_);
+    auto st = static_cast<hipStream_t>(stream);
+    issue(ncclGroupStart(), "ncclGroupStart");
+    if (sbytes) issue(ncclSend(send, sbytes, ncclUint8, dst, comm_, st), "ncclSend");
+    if (rbytes) issue(ncclRecv(recv, rbytes, ncclUint8, src, comm_, st), "ncclRecv");
+    issue(ncclGroupEnd(), "ncclGroupEnd");
+  }
+  int64_t allreduce_sum_i64_device(int64_t* v, void* stream) override {
+    if (!comm_) throw CommError("RCCL communicator was aborted");
+    if (seg_) seg_->check_abort(rank_);
+    auto st = static_cast<hipStream_t>(stream);
+    if (!h_word_) hip_ck(hipHostMalloc((void**)&h_word_, 8, hipHostMallocDefault), "hipHostMalloc");
+    issue(ncclAllReduce(v, v, 1, ncclInt64, ncclSum, comm_, st), "ncclAllReduce");
+    hip_ck(hipMemcpyAsync(h_word_, v, 8, hipMemcpyDeviceToHost, st), "D2H");
+    wait("ncclAllReduce (device)", st);
+    return *h_word_;
+  }
+  bool device_native() const override { return true; }
   int transport_size() const override {
     int n = -1;
     if (!comm_ || ncclCommCount(comm_, &n) != ncclSuccess) return -1;
@@ -149,10 +175,10 @@ class RcclComm final : public Comm {
       poll_guards(what, deadline);
     }
   }
-  void wait(const char* what) {
+  void wait(const char* what, hipStream_t s = nullptr) {
     const double deadline = mono_s() + timeout_;
     for (;;) {
-      const hipError_t q = hipStreamQuery(stream_);
+      const hipError_t q = hipStreamQuery(s ? s : stream_);
       if (q == hipSuccess) return;
       if (q != hipErrorNotReady) fail(std::string(what) + ": " + hipGetErrorString(q));
       ncclResult_t ar = ncclSuccess;
@@ -188,6 +214,8 @@ class RcclComm final : public Comm {
     }
     if (buf_) (void)hipFree(buf_);
     buf_ = nullptr;
+    if (h_word_) (void)hipHostFree(h_word_);
+    h_word_ = nullptr;
     if (stream_) (void)hipStreamDestroy(stream_);
     stream_ = nullptr;
   }
@@ -198,6 +226,7 @@ class RcclComm final : public Comm {
   ncclComm_t comm_ = nullptr;
   void* buf_ = nullptr;
   size_t cap_ = 0;
+  int64_t* h_word_ = nullptr;  // pinned landing word of allreduce_sum_i64_device
 };
 
 }  // namespace

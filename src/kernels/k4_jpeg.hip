@@ -225,6 +225,13 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(kOcc)))
     if (part == 0x7FFFFFF1) out_sizes[0] = 1;
     return;
   }
+  // Profiling variants 40 / 41: only the gray (original) / only the label (processed) images are
+  // encoded; the other kind's workgroups leave after taking their ticket (their images' output is
+  // invalid). Splits the encoder's time by image kind.
+  if ((dbg == 40 && d.render >= 0 && rd.kind == kRenderLabels) || (dbg == 41 && !(d.render >= 0 && rd.kind == kRenderLabels))) {
+    if (part == 0x7FFFFFF1) out_sizes[0] = 1;
+    return;
+  }
   const int mcux = out_w >> 4;
   const int b = part * kJpegWG + tid;
   const bool valid = b < bpi;
@@ -260,7 +267,7 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(kOcc)))
         nonzero |= ((lab | brd) & m) != 0;
         nonfill |= ((~lab | brd) & m) != 0;
       }
-      const bool full = (part + 1) * kJpegWG <= bpi && dbg == 0;
+      const bool full = (part + 1) * kJpegWG <= bpi && (dbg == 0 || dbg >= 40);
       const bool zero = __syncthreads_or(nonzero) == 0;
       const bool fill = __syncthreads_or(nonfill) == 0;
       wgflat = full && (zero || fill);

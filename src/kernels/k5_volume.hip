@@ -329,4 +329,42 @@ void dilate_volume(const uint64_t* src, uint64_t* dst, uint64_t* tmp, int w, int
   check_launch("dilate_z_kernel");
 }
 
+// z-slab boundary step: one thread per plane word. The 26-connected touch is the 3×3 in-plane
+// dilation of the neighbour's plane (dilate_plane3 in volume_slabs.cpp), formed on the fly.
+__global__ __launch_bounds__(256) void slab_seed_kernel(const uint64_t* __restrict__ band, uint64_t* __restrict__ region,
+                                                        const uint64_t* __restrict__ nb, int w, int h, int wpr,
+                                                        int conn26, unsigned long long* __restrict__ added) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  uint64_t add = 0;
+  if (i < h * wpr) {
+    const int y = i / wpr, k = i - y * wpr;
+    uint64_t t = nb[i];
+    if (conn26) {
+      const uint64_t last = (w & 63) ? ((1ull << (w & 63)) - 1ull) : ~0ull;
+      auto hrow = [&](int yy) -> uint64_t {
+        if (yy < 0 || yy >= h) return 0ull;
+        const uint64_t* r = nb + (size_t)yy * wpr;
+        const uint64_t v = r[k], prev = k > 0 ? r[k - 1] : 0ull, next = k + 1 < wpr ? r[k + 1] : 0ull;
+        uint64_t acc = v | (v << 1) | (prev >> 63) | (v >> 1) | (next << 63);
+        return k == wpr - 1 ? acc & last : acc;
+      };
+      t = hrow(y - 1) | hrow(y) | hrow(y + 1);
+    }
+    add = band[i] & t & ~region[i];
+    if (add) region[i] |= add;
+  }
+  unsigned long long c = (unsigned long long)__popcll(add);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+  if ((threadIdx.x & 63) == 0 && c) atomicAdd(added, c);
+}
+
+void launch_slab_seed(const uint64_t* band, uint64_t* region, const uint64_t* nb, int w, int h, bool conn26,
+                      unsigned long long* added, hipStream_t stream) {
+  const int wpr = (w + 63) / 64, n = h * wpr;
+  if (n <= 0) return;
+  slab_seed_kernel<<<(n + 255) / 256, 256, 0, stream>>>(band, region, nb, w, h, wpr, conn26 ? 1 : 0, added);
+  check_launch("slab_seed_kernel");
+}
+
 }  // namespace nm03::gpu

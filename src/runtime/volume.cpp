@@ -98,6 +98,10 @@ struct VolumeDevice {
   uint32_t* h_flag = nullptr;         // the region growing's control words (sweep count, error)
   uint8_t* h_tables = nullptr;  // pinned staging: descriptors, tile lists, stats (reused per run)
   size_t n_medt, n_shpt;
+  // z-slab decomposition (run_slab): the two neighbour boundary planes, the added-voxel counter
+  // and the halo-extended dilation buffers, allocated on first use and kept.
+  std::unique_ptr<DevBuf> slab_nb, slab_added, ext, ext_dil, ext_tmp, ext_scr;
+  int ext_planes = 0;
   VolumeDevice(const VolumeInput& v)
       : w(v.w), h(v.h), d(v.d), wpr((v.w + 63) / 64), words((size_t)v.h * ((v.w + 63) / 64)),
         ps(((size_t)v.w * v.h + 7) / 8 * 8),
@@ -367,6 +371,75 @@ class GpuSlabGrower final : public SlabGrower {
 
 }  // namespace
 
+// Device-resident z-slab growth and dilation (volume_slabs.h steps 2 and 3 on the GPU): the slab's
+// boundary region planes go from V.region straight into the neighbours' device buffers
+// (Comm::sendrecv_device — RCCL over xGMI, or staged through pinned memory by the host comms), the
+// boundary seeding is a kernel, and the added-voxel count is all-reduced from device memory: one
+// host synchronisation per round, no pageable copies. The dilation halo is received straight into
+// the extended buffer around a device copy of the slab. Slabs thinner than the halo fall back to the
+// generic algorithm (grow_and_dilate_slabs with GpuSlabGrower).
+static SlabStats slab_grow_dilate_gpu(Comm& comm, VolumeDevice& V, int nseeds, int conn, int depth, int z0, int z1,
+                                      int dilation) {
+  const int rank = comm.rank(), n = comm.size();
+  const int d = z1 - z0, r = dilation / 2;
+  const size_t pw = V.words, pbytes = pw * 8;
+  const int below = rank > 0 ? rank - 1 : -1, above = rank + 1 < n ? rank + 1 : -1;
+  SlabStats st;
+  if (!V.slab_nb) {
+    V.slab_nb = std::make_unique<DevBuf>(2 * pbytes);
+    V.slab_added = std::make_unique<DevBuf>(8);
+  }
+  uint64_t* nb_below = V.slab_nb->as<uint64_t>();
+  uint64_t* nb_above = nb_below + pw;
+  auto* added = V.slab_added->as<int64_t>();
+  uint64_t* band = V.band.as<uint64_t>();
+  uint64_t* region = V.region.as<uint64_t>();
+  for (bool first = true;; first = false) {
+    srg_volume(band, region, V.w, V.h, d, V.seeds.as<int32_t>(), first ? nseeds : 0, conn, V.flag.as<uint32_t>(),
+               V.h_flag, V.srg_scratch.as<uint64_t>(), V.stream, first);
+    // My top plane goes up while the plane below my slab comes up from rank − 1; then the reverse.
+    comm.sendrecv_device(region + (size_t)(d - 1) * pw, pbytes, above, nb_below, pbytes, below, V.stream);
+    comm.sendrecv_device(region, pbytes, below, nb_above, pbytes, above, V.stream);
+    st.exchanged_bytes += (int64_t)((above >= 0) + (below >= 0)) * (int64_t)pbytes;
+    check_hip(hipMemsetAsync(added, 0, 8, V.stream), "memset added");
+    auto* acc = reinterpret_cast<unsigned long long*>(added);
+    if (below >= 0) launch_slab_seed(band, region, nb_below, V.w, V.h, conn == 26, acc, V.stream);
+    if (above >= 0)
+      launch_slab_seed(band + (size_t)(d - 1) * pw, region + (size_t)(d - 1) * pw, nb_above, V.w, V.h, conn == 26, acc,
+                       V.stream);
+    const int64_t total = comm.allreduce_sum_i64_device(added, V.stream);  // waits for the round
+    st.sweeps += srg_volume_result(V.h_flag);
+    ++st.rounds;
+    if (total == 0) break;
+  }
+  const int rb = std::min(r, z0), ra = std::min(r, depth - z1), de = rb + d + ra;
+  if (!V.ext || V.ext_planes < de) {
+    const size_t bytes = pbytes * (size_t)de;
+    V.ext = std::make_unique<DevBuf>(bytes);
+    V.ext_dil = std::make_unique<DevBuf>(bytes);
+    V.ext_tmp = std::make_unique<DevBuf>(bytes);
+    V.ext_scr = std::make_unique<DevBuf>(8 * std::max<size_t>(1, morph3d_scratch_words(V.w, V.h, de)));
+    V.ext_planes = de;
+  }
+  uint64_t* ext = V.ext->as<uint64_t>();
+  if (r > 0) {
+    // Top r planes up into the successor's lower halo; bottom r planes down into the predecessor's
+    // upper halo (every slab holds ≥ r planes here).
+    comm.sendrecv_device(region + (size_t)(d - r) * pw, above >= 0 ? (size_t)r * pbytes : 0, above, ext,
+                         (size_t)rb * pbytes, below, V.stream);
+    comm.sendrecv_device(region, below >= 0 ? (size_t)r * pbytes : 0, below, ext + (size_t)(rb + d) * pw,
+                         (size_t)ra * pbytes, above, V.stream);
+    st.exchanged_bytes += (int64_t)((above >= 0) + (below >= 0)) * r * (int64_t)pbytes;
+  }
+  check_hip(hipMemcpyAsync(ext + (size_t)rb * pw, region, pbytes * d, hipMemcpyDeviceToDevice, V.stream), "D2D slab");
+  dilate_volume(ext, V.ext_dil->as<uint64_t>(), V.ext_tmp->as<uint64_t>(), V.w, V.h, de, dilation, V.stream,
+                V.ext_scr->as<uint64_t>());
+  check_hip(hipMemcpyAsync(V.dil.p, V.ext_dil->as<uint64_t>() + (size_t)rb * pw, pbytes * d, hipMemcpyDeviceToDevice,
+                           V.stream),
+            "D2D slab dilation");
+  return st;
+}
+
 VolumeResult VolumeRunner::run_slab(Comm& comm, const VolumeInput& slab, int z0, int depth, const VolumeParams& p,
                                     bool want_masks, SlabStats* stats) {
   if (slab.d < 1 || slab.w < 1 || slab.h < 1) throw SliceError("empty slab");
@@ -391,9 +464,17 @@ VolumeResult VolumeRunner::run_slab(Comm& comm, const VolumeInput& slab, int z0,
     }
   if (!sx.empty())
     check_hip(hipMemcpyAsync(V.seeds.p, sx.data(), sx.size() * 4, hipMemcpyHostToDevice, V.stream), "H2D seeds");
-  GpuSlabGrower g(V, (int)(sx.size() / 3), p.connectivity == 26 ? 26 : 6);
-  const SlabStats st = grow_and_dilate_slabs(comm, g, slab.w, slab.h, depth, z0, z0 + slab.d,
-                                             p.connectivity == 26 ? 26 : 6, p.dilation_size);
+  const int conn = p.connectivity == 26 ? 26 : 6;
+  if (depth < comm.size())
+    throw std::runtime_error("z-slabs: volume depth " + std::to_string(depth) + " < " + std::to_string(comm.size()) +
+                             " ranks leaves empty slabs");
+  SlabStats st;
+  if (depth / comm.size() >= p.dilation_size / 2) {
+    st = slab_grow_dilate_gpu(comm, V, (int)(sx.size() / 3), conn, depth, z0, z0 + slab.d, p.dilation_size);
+  } else {  // slabs thinner than the dilation halo: the generic exchange (all-gather of slab ends)
+    GpuSlabGrower g(V, (int)(sx.size() / 3), conn);
+    st = grow_and_dilate_slabs(comm, g, slab.w, slab.h, depth, z0, z0 + slab.d, conn, p.dilation_size);
+  }
   check_hip(hipEventRecord(I.e1, V.stream), "event");
   check_hip(hipEventSynchronize(I.e1), "sync");
   VolumeResult r;

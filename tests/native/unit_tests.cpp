@@ -5,6 +5,7 @@
 // Host code only — no GPU is touched, so this runs in CPU-only CI.
 //
 //   build/bin/nm03_unit_tests [filter]      (exit status = number of failed checks)
+#include <dirent.h>
 #include <fcntl.h>
 #include <unistd.h>
 
@@ -540,6 +541,42 @@ TEST(thread_pool_for_each_max_runners_exactly_once_and_bounded) {
       CHECK(peak.load() <= (cap > 0 ? std::min(cap, 6) : 6));
     }
   }
+}
+
+TEST(output_reaper_wipes_in_background) {
+  char tmpl[] = "/tmp/nm03_reaper_XXXXXX";
+  const std::string root = mkdtemp(tmpl);
+  std::vector<std::string> dirs;
+  for (int d = 0; d < 6; ++d) {
+    dirs.push_back(root + "/PGBM-" + std::to_string(d));
+    nm03::cohort::make_dirs(dirs.back());
+    for (int f = 0; f < 20; ++f) {
+      FILE* fp = std::fopen((dirs.back() + "/" + std::to_string(f) + ".jpg").c_str(), "wb");
+      std::fputs("x", fp);
+      std::fclose(fp);
+    }
+  }
+  {
+    nm03::cohort::OutputReaper r(3);
+    for (int pass = 0; pass < 3; ++pass) {
+      r.wipe(dirs);
+      for (auto& d : dirs) {  // empty at once, written right away while the old files are deleted
+        FILE* fp = std::fopen((d + "/new.jpg").c_str(), "wb");
+        CHECK(fp != nullptr);
+        std::fclose(fp);
+      }
+    }
+    r.drain();
+    CHECK(r.files_reaped() == 6 * 20 + 2 * 6);
+  }
+  int entries = 0;
+  DIR* dd = opendir(root.c_str());
+  while (dirent* e = readdir(dd)) entries += e->d_name[0] != '.';
+  closedir(dd);
+  CHECK(entries == 6);  // no trash left behind
+  nm03::cohort::setup_output_dirs(dirs, 2);
+  for (auto& d : dirs) rmdir(d.c_str());
+  rmdir(root.c_str());
 }
 
 TEST(thread_pool_priorities_order_a_single_worker) {

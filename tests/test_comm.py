@@ -120,3 +120,28 @@ def test_auto_threads_respects_budget(monkeypatch):
     monkeypatch.setattr(dist, "cpu_budget", lambda: 256)
     assert dist.auto_threads(8) == 16
     assert dist.cpu_budget.__name__  # patched
+
+
+def test_segment_name_changes_with_elastic_restart(monkeypatch):
+    """Under torchrun a restarted generation of workers (same agent, same MASTER_PORT) derives a new
+    segment name (TORCHELASTIC_RESTART_COUNT / RUN_ID), so it never attaches to a segment the
+    previous generation left behind."""
+    from nm03_capstone_project_amd.parallel import native_comm as nc
+    monkeypatch.delenv("NM03_COMM_JOB", raising=False)
+    monkeypatch.setenv("MASTER_PORT", "29500")
+    monkeypatch.setenv("TORCHELASTIC_RESTART_COUNT", "0")
+    monkeypatch.setenv("TORCHELASTIC_RUN_ID", "job/1")
+    a = nc.segment_name()
+    monkeypatch.setenv("TORCHELASTIC_RESTART_COUNT", "1")
+    b = nc.segment_name()
+    assert a != b and a.startswith("/nm03-comm-") and "/" not in a[1:] and "/" not in b[1:]
+    monkeypatch.setenv("NM03_COMM_JOB", "abc")
+    assert nc.segment_name() == "/nm03-comm-abc"
+
+
+def test_native_comm_refuses_multi_node_world(monkeypatch):
+    from nm03_capstone_project_amd.parallel import native_comm as nc
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "2")
+    import pytest
+    with pytest.raises(RuntimeError, match="LOCAL_WORLD_SIZE"):
+        nc.make_native_comm(0, 4, 0, "host", timeout_s=1)
