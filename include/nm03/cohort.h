@@ -51,11 +51,12 @@ void make_dirs(const std::string& dir);
 // Why (tools/create_probe.cpp on the MI355X box, profiles/r4/create_probe/): creating and deleting
 // tmpfs files serialise on per-filesystem locks (inode accounting and the superblock's inode list),
 // not on the directory — one-directory-per-thread layouts measure the same. Deleting a JPEG pair
-// costs 5–12 µs of CPU on one thread and 23–35 µs with 16 threads deleting at once; done by 2
-// reaper threads beside the engine, the wipe costs a fraction of the CPU and no wall time.
+// costs 5–12 µs of CPU on one thread and 23–35 µs with 16 threads deleting at once; done by a few
+// reaper threads beside the engine, the wipe costs less CPU and no wall time (4 threads keep up
+// with a 465-slice pass every ≈2.3 ms: profiles/r4/cold_ab3/).
 class OutputReaper {
  public:
-  explicit OutputReaper(int threads = 2);
+  explicit OutputReaper(int threads = 4);
   ~OutputReaper();
   OutputReaper(const OutputReaper&) = delete;
   OutputReaper& operator=(const OutputReaper&) = delete;

@@ -71,7 +71,7 @@ class Placement {
   // Pins the calling thread to the placement's CPUs (no-op when inactive).
   void bind_this_thread() const;
   // Pool workers float over the whole set (bind_this_thread). Measured and removed in round 4:
-  // one physical core per worker (NM03_PIN=core: host-only 283–304k vs 365–392k slices/s) and
+  // one physical core per worker (round-3 NM03_PIN=core: host-only 283–304k vs 365–392k slices/s) and
   // workers + work keyed to L3 domains (NM03_PIN=l3: writes get slower when the threads spread
   // over more L3 domains, 17 → 29 µs per JPEG pair; profiles/r3/host_pin/, profiles/r3/pin_l3/).
   // Runs `f` with the calling thread temporarily pinned (first-touch / pinned allocations land on

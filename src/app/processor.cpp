@@ -107,6 +107,7 @@ int visible_gpu_count() {
 }
 
 AppConfig parse_args(int argc, char** argv, const std::string& which) {
+  arm_fast_exit();
   install_crash_handler();
   AppConfig c;
   c.data_root = cohort::default_data_root();
@@ -189,7 +190,7 @@ int run_sequential(const AppConfig& cfg) {
     } leak{engine_p};
     // Patient directories are wiped by renaming them aside; the deletions run on background threads
     // while the engine works (cohort.h OutputReaper) and are waited for before the run ends.
-    cohort::OutputReaper reaper(2);
+    cohort::OutputReaper reaper(4);
     const double t0 = now_s();
     StageTimes total;
     int64_t slices = 0, slices_ok = 0;
@@ -432,9 +433,9 @@ int parallel_rank(const AppConfig& cfg, int rank, int size, Comm& comm, int devi
   int64_t total_ok = 0, total_slices = 0, my_slices = 0, my_ok = 0;
   StageTimes agg;
   // Rank 0 wipes the patient directories by renaming them aside; 2 background threads delete the
-  // old files while the ranks process (cohort.h OutputReaper), waited for before the run ends.
+  // old files on 4 background threads while the ranks process (cohort.h OutputReaper), waited for before the run ends.
   std::unique_ptr<cohort::OutputReaper> reaper;
-  if (rank == 0 && !cfg.engine.resume) reaper = std::make_unique<cohort::OutputReaper>(2);
+  if (rank == 0 && !cfg.engine.resume) reaper = std::make_unique<cohort::OutputReaper>(4);
   for (int rep = 0; rep < cfg.repeat; ++rep) {
     // ---- plan on rank 0 --------------------------------------------------------------------
     std::vector<uint8_t> plan_bytes;
@@ -684,11 +685,33 @@ bool fast_exit_enabled() {
   return on;
 }
 
+namespace {
+bool g_exit_armed = false;
+void fast_exit_handler(int status, void*) {  // on_exit: receives exit()'s status
+  std::fflush(nullptr);
+  _exit(status);
+}
+}  // namespace
+
+void arm_fast_exit() {
+  // Registered before any HIP call, so it runs after every exit handler registered later — those
+  // of a profiler's tool library (rocprofv3 writes its results from one) — and before the shared
+  // libraries' destructors (HIP's static teardown: slow, and under rocprofv3 it faulted after the
+  // tool had finalised; profiles/r4/probe/c5_prof_segv_backtrace.txt).
+  if (fast_exit_enabled() && !g_exit_armed) {
+    on_exit(fast_exit_handler, nullptr);
+    g_exit_armed = true;
+  }
+}
+
 int cli_exit(int rc) {
   std::cout.flush();
   std::cerr.flush();
   std::fflush(nullptr);
-  if (fast_exit_enabled()) _exit(rc);
+  if (fast_exit_enabled()) {
+    if (!g_exit_armed) _exit(rc);
+    std::exit(rc);
+  }
   return rc;
 }
 

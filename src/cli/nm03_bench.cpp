@@ -33,6 +33,7 @@ static double now_s() {
 
 int main(int argc, char** argv) {
   nm03::install_crash_handler();
+  nm03::app::arm_fast_exit();
   std::string config = "cohort", root = nm03::cohort::default_data_root(), out = "/tmp/nm03_bench_out";
   int steps = 10, warmup = 2;
   nm03::EngineConfig ec;
@@ -247,11 +248,12 @@ int main(int argc, char** argv) {
     std::cerr << "Fatal error: " << e.what() << std::endl;
     return nm03::app::cli_exit(1);
   }
-  // Like the CLIs: flush and _exit, no static destructors. Under rocprofv3 the process used to die
-  // with SIGSEGV after main returned (exit 139): the crash handler's backtrace shows the fault in
-  // libamdhip64's own static destructor (__cxa_finalize → libamdhip64 → libhsa-runtime64), after
-  // rocprofv3's "tool finalization" — HIP's exit-time teardown calls into an HSA runtime the
-  // profiler's tool has already finalised. No nm03 frame is on that stack; the results were
-  // complete. Skipping the exit-time teardown removes the fault (gpurun_out r4, profiles/r4/).
+  // Like the CLIs: exit handlers run (rocprofv3 writes its results from one), then _exit before the
+  // shared libraries' destructors. Under rocprofv3 the process used to die with SIGSEGV after main
+  // returned (exit 139): the crash handler's backtrace shows the fault in libamdhip64's own static
+  // destructor (__cxa_finalize → libamdhip64 → libhsa-runtime64), after rocprofv3's "tool
+  // finalization" — HIP's exit-time teardown calls into an HSA runtime the profiler's tool has
+  // already finalised. No nm03 frame is on that stack; the results were complete
+  // (profiles/r4/probe/c5_prof_segv_backtrace.txt).
   return nm03::app::cli_exit(0);
 }

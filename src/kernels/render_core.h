@@ -207,7 +207,7 @@ __device__ __forceinline__ void render_block_2x(const RenderDesc& d, const uint1
         patch[j][i] = rescaled_value(key_from_raw(r, d.type, d.stored_bits), d.type, d.slope, d.intercept);
       }
     }
-  } else if (synth_src) {  // profiling variant (NM03_JPEG_DBG=11): same math, no source loads
+  } else if (synth_src) {  // synthetic source (no loads): same math; kept for kernel experiments
 #pragma unroll
     for (int j = 0; j < 6; ++j)
 #pragma unroll

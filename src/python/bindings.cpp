@@ -432,7 +432,7 @@ PYBIND11_MODULE(_nm03, m) {
     cohort::setup_output_dirs(dirs, threads);
   }, py::arg("dirs"), py::arg("threads") = 8);
   py::class_<cohort::OutputReaper>(m, "OutputReaper")
-      .def(py::init<int>(), py::arg("threads") = 2)
+      .def(py::init<int>(), py::arg("threads") = 4)
       .def("wipe", [](cohort::OutputReaper& r, const std::vector<std::string>& dirs) {
         py::gil_scoped_release nogil;
         r.wipe(dirs);
@@ -777,6 +777,85 @@ PYBIND11_MODULE(_nm03, m) {
           py::arg("comm"), py::arg("slab"), py::arg("z0"), py::arg("depth"), py::arg("params") = PipelineParams(),
           py::arg("connectivity") = 6, py::arg("dilation") = 7,
           py::arg("seeds") = std::vector<std::tuple<int, int, int>>{});
+
+  // One-process rehearsal of the z-slab decomposition: `nranks` threads, each with its own
+  // VolumeRunner (stream) on `device`, talking over loopback comms — the device-resident exchange
+  // (Comm::sendrecv_device staged through pinned memory here) without the inter-process GPU
+  // time-slicing that several rank processes on one GPU add. Runs `repeats` timed splits after one
+  // warm-up; returns the wall times (max over ranks per split, seconds), the last split's rounds /
+  // exchanged bytes per rank and its gathered masks.
+  m.def(
+      "run_volume_slabs_threads",
+      [](py::array_t<uint16_t, py::array::c_style | py::array::forcecast> vol, int nranks, const PipelineParams& p,
+         int connectivity, int dilation, int device, int repeats) {
+        if (vol.ndim() != 3) throw std::invalid_argument("volume must be (depth, height, width)");
+        const int D = (int)vol.shape(0), H = (int)vol.shape(1), W = (int)vol.shape(2);
+        if (nranks < 1 || nranks > D) throw std::invalid_argument("1 <= nranks <= depth");
+        const std::vector<uint16_t> raw = from_np<uint16_t>(vol);
+        std::vector<VolumeInput> slabs((size_t)nranks);
+        for (int r = 0; r < nranks; ++r) {
+          const auto [z0, z1] = slab_bounds(D, r, nranks);
+          VolumeInput& v = slabs[(size_t)r];
+          v.w = W;
+          v.h = H;
+          v.d = z1 - z0;
+          v.raw.assign(raw.begin() + (size_t)z0 * W * H, raw.begin() + (size_t)z1 * W * H);
+        }
+        VolumeParams vp;
+        vp.pipe = p;
+        vp.connectivity = connectivity;
+        vp.dilation_size = dilation;
+        std::vector<double> walls;
+        std::vector<VolumeResult> res((size_t)nranks);
+        std::vector<SlabStats> st((size_t)nranks);
+        {
+          py::gil_scoped_release nogil;
+          std::vector<std::unique_ptr<VolumeRunner>> runners;
+          for (int r = 0; r < nranks; ++r) runners.push_back(std::make_unique<VolumeRunner>(device));
+          auto group = make_loopback_group(nranks);
+          for (int rep = 0; rep <= repeats; ++rep) {
+            const bool last = rep == repeats;
+            std::vector<double> t((size_t)nranks);
+            std::vector<std::string> err((size_t)nranks);
+            std::vector<std::thread> th;
+            for (int r = 0; r < nranks; ++r)
+              th.emplace_back([&, r] {
+                try {
+                  const auto zz = slab_bounds(D, r, nranks);
+                  group[(size_t)r]->barrier();
+                  const auto t0 = std::chrono::steady_clock::now();
+                  res[(size_t)r] = runners[(size_t)r]->run_slab(*group[(size_t)r], slabs[(size_t)r], zz.first, D, vp,
+                                                                last, &st[(size_t)r]);
+                  t[(size_t)r] = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+                } catch (const std::exception& e) {
+                  err[(size_t)r] = e.what();
+                }
+              });
+            for (auto& x : th) x.join();
+            for (auto& e : err)
+              if (!e.empty()) throw std::runtime_error("run_volume_slabs_threads: " + e);
+            if (rep > 0) walls.push_back(*std::max_element(t.begin(), t.end()));
+          }
+        }
+        py::dict d;
+        d["walls_s"] = walls;
+        std::vector<int> rounds;
+        std::vector<int64_t> bytes;
+        std::vector<uint8_t> region, dilated;
+        for (int r = 0; r < nranks; ++r) {
+          rounds.push_back(st[(size_t)r].rounds);
+          bytes.push_back(st[(size_t)r].exchanged_bytes);
+          region.insert(region.end(), res[(size_t)r].region.begin(), res[(size_t)r].region.end());
+          dilated.insert(dilated.end(), res[(size_t)r].dilated.begin(), res[(size_t)r].dilated.end());
+        }
+        d["rounds"] = rounds;
+        d["exchanged_bytes"] = bytes;
+        d["region"] = to_np<uint8_t>(region, {D, H, W});
+        d["dilated"] = to_np<uint8_t>(dilated, {D, H, W});
+        return d;
+      },
+      py::arg("volume"), py::arg("nranks"), py::arg("params") = PipelineParams(), py::arg("connectivity") = 6,
+      py::arg("dilation") = 7, py::arg("device") = 0, py::arg("repeats") = 5);
 
   // The same decomposition on the golden model: this rank's slab of a band volume (0/1 uint8,
   // planes [z0, z0 + d) of `depth`), seeds in volume coordinates. Collective over `comm`.

@@ -135,7 +135,7 @@ struct Slot {
   size_t out_bytes = 0;
 };
 
-// Private fd tables for the host pool's workers (NM03_PRIVATE_FDS, default on). Every open and
+// Private fd tables for the host pool's workers. Every open and
 // close takes the process's fd-table lock; with 16 loader/writer threads doing three opens and
 // three closes per slice that lock (and its cache line crossing CCDs) doubled the per-file cost:
 // 23–24 µs per load and 31.7 µs per JPEG pair in 16 threads of one process vs 14.7–16.5 and

@@ -888,6 +888,25 @@ def test_volume_slabs_single_rank_equals_volume_pipeline(native):
         assert np.array_equal(r[k], ref[k]), k
 
 
+@pytest.mark.parametrize("ranks,conn,thin", [(2, 6, False), (3, 26, False), (4, 6, True)])
+def test_volume_slabs_threads_device_exchange_equals_volume(native, ranks, conn, thin):
+    """The device-resident z-slab exchange (Comm::sendrecv_device / allreduce_sum_i64_device, the
+    slab seed kernel, halos received straight into the extended dilation buffer) with N rank threads
+    on one GPU over loopback comms: region and dilation identical to the single-volume run, with a
+    region that crosses every slab boundary (several rounds). `thin`: slabs thinner than the
+    dilation halo take the generic all-gather path."""
+    d = 8 if thin else 40
+    h, w = 96, 128
+    vol = np.stack([native.phantom_slice(h, w, 2, z % 7, d, 5) for z in range(d)])
+    vol[:, 40:56, :] = 1500  # an in-band slab through every plane: the region spans all slabs
+    ref = native.VolumeRunner(0).run(vol, native.PipelineParams(), conn, 7, [])
+    r = native.run_volume_slabs_threads(vol, ranks, native.PipelineParams(), conn, 7, 0, 2)
+    assert ref["region"].sum() > 0 and len(r["walls_s"]) == 2
+    assert max(r["rounds"]) >= 2 or thin
+    assert np.array_equal(r["region"], ref["region"])
+    assert np.array_equal(r["dilated"], ref["dilated"])
+
+
 @pytest.mark.parametrize("ranks", [2, 3])
 def test_volume_cli_split_volume_identical(native, cohort_root, tmp_path, ranks):
     """img_processing_parallel --mode 3d --split-volume: every volume cut into z-slabs over N ranks
