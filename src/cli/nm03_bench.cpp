@@ -53,6 +53,8 @@ int main(int argc, char** argv) {
     else if (a == "--max-dim") ec.max_dim = std::atoi(v().c_str());
     else if (a == "--dilation-3d") dil3d = std::atoi(v().c_str());
     else if (a == "--device") ec.device = std::atoi(v().c_str());
+    else if (a == "--jpeg-wg") ec.jpeg_wg = std::atoi(v().c_str());
+    else if (a == "--bar-upload") ec.bar_upload = true;
     else if (a == "--host-only") ec.host_only = true;  // cohort: every load/pack/write, no GPU (sanitizer sweeps)
     else {
       std::cerr << "unknown option " << a << std::endl;

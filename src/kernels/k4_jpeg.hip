@@ -96,6 +96,8 @@ __device__ __forceinline__ int swz_col(int c) { return c + (c >> 2); }
 // One LDS region serves the render (source patch above) and then, once every block is rendered,
 // the workgroup's assembled bit range followed by its staged stuffed output bytes.
 constexpr int kUnionWords = kPatchLds + 1080;  // 27 KiB as before (4 workgroups per CU): bit ranges up to ~220 Kbit
+// 512-block workgroups (JpegWork::wg = 512): 34 staged rows, 2 workgroups per CU (8 waves each).
+constexpr int kUnionWords512 = 34 * 324 + 2160;
 
 constexpr int kPrivWords = 5;    // per-block Huffman bits kept in LDS (160 bits, odd stride) ...
 constexpr int kSpillWords = 56;  // ... the rest in the block's global spill slot (a block needs ≤ 1700)
@@ -148,19 +150,23 @@ __device__ __forceinline__ uint32_t priv_word(const uint32_t* pb, const uint32_t
 // kOcc: target waves per SIMD (= workgroups per CU); kUnion: LDS words of the patch / bit-range
 // union. 5 workgroups per CU (31.7 KiB, ≤ 96 VGPRs with spills) measured no better than 4 once
 // images were dealt round-robin (profiles/r3/jpeg_spread/split_and_occ5.txt).
-template <int kOcc, int kUnion>
-__global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(kOcc))) void jpeg_fused_kernel(const uint8_t* __restrict__ canvas,
+template <int kOcc, int kUnion, int kWG>
+__global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(kOcc))) void jpeg_fused_kernel(const uint8_t* __restrict__ canvas,
                                                              const JpegDesc* __restrict__ jd, int ncanvas, int out_w,
                                                              int out_h, QuantRecip q, JpegWork w, JpegRenderSrc rs,
                                                              uint8_t* __restrict__ out, int32_t* __restrict__ out_sizes,
                                                              int dbg) {
   // dbg: profiling variant (NM03_PROFILE_VARIANT=jpeg=N; output invalid), 0 = the real encoder.
+  // kWG blocks (threads) per workgroup: kWG / 4 MCUs; the gray staging area holds their rows
+  // (+ a 1-row halo each side) of a 256-wide source: 18 rows for 256, 34 for 512.
+  constexpr int kPatch = kWG == 512 ? 34 * 324 : kPatchLds;
+  static_assert(kPatch <= kUnion, "staging area exceeds the LDS union");
   __shared__ uint32_t actab[256];
   __shared__ uint32_t dctab[16];
-  __shared__ int32_t sdc[kJpegWG];
-  __shared__ uint32_t spriv[kJpegWG * kPrivWords];  // per-block AC Huffman bits
+  __shared__ int32_t sdc[kWG];
+  __shared__ uint32_t spriv[kWG * kPrivWords];  // per-block AC Huffman bits
   __shared__ uint32_t sh[17];
-  __shared__ uint32_t sff[4 * 8];
+  __shared__ uint32_t sff[(kWG / 64) * 8];
   __shared__ uint32_t s_ticket, s_obase, s_nown, s_strad_v, s_fin_v, s_f, s_nwords;
   __shared__ bool s_bad, s_strad, s_fin;
   __shared__ int32_t s_prevdc;
@@ -171,14 +177,14 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(kOcc)))
   // for the next launch instead of a separate memset launch.
   if (w.clear_words) {
     uint64_t* other = w.look + w.clear_base;
-    for (size_t i = (size_t)blockIdx.x * kJpegWG + tid; i < w.clear_words; i += (size_t)gridDim.x * kJpegWG) other[i] = 0ull;
+    for (size_t i = (size_t)blockIdx.x * kWG + tid; i < w.clear_words; i += (size_t)gridDim.x * kWG) other[i] = 0ull;
   }
   if (dbg == 8) {  // profiling variant: empty workgroup
     if (tid == 999) out_sizes[0] = 1;
     return;
   }
   const int bpi = (out_w >> 3) * (out_h >> 3);
-  const int parts = (bpi + kJpegWG - 1) / kJpegWG;
+  const int parts = (bpi + kWG - 1) / kWG;
   // The image is fixed by the dispatch index; only the part comes from the ticket. The ticket's
   // device-scope atomic is issued first, so its round trip overlaps the table and descriptor
   // loads below (issued after them it waited behind three dependent descriptor loads).
@@ -233,7 +239,7 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(kOcc)))
     return;
   }
   const int mcux = out_w >> 4;
-  const int b = part * kJpegWG + tid;
+  const int b = part * kWG + tid;
   const bool valid = b < bpi;
   // ---- 0. stage the source rows of this workgroup in LDS (workgroup-uniform decision) ----------
   int ys0 = 0, pcols = 0;
@@ -248,16 +254,16 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(kOcc)))
   uint64_t* const slab = reinterpret_cast<uint64_t*>(spatch);  // label images reuse the area
   if (d.render >= 0 && rd.kind == kRenderLabels) {
     // Label render rows: 4by .. 4by+3 for the workgroup's block rows → 8 per MCU row.
-    const int m0 = part * (kJpegWG / 4), m1 = min(m0 + kJpegWG / 4, bpi >> 2) - 1;
+    const int m0 = part * (kWG / 4), m1 = min(m0 + kWG / 4, bpi >> 2) - 1;
     const int r0 = m0 / mcux, r1 = m1 / mcux;
     const int nrows = 8 * (r1 - r0) + 8, wpr = rd.wpr, nw = nrows * wpr;
-    if (2 * nw * 2 <= kPatchLds) {  // two u64 planes in the f32 area
+    if (2 * nw * 2 <= kPatch) {  // two u64 planes in the f32 area
       lstaged = true;
       ys0 = 8 * r0;
       pcols = nw;  // offset of the border plane
       const int wrem = rd.src_w & 63;
       int nonzero = 0, nonfill = 0;
-      for (int i = tid; i < nw; i += kJpegWG) {
+      for (int i = tid; i < nw; i += kWG) {
         const int j = i / wpr, k = i - j * wpr;
         const size_t wi = (size_t)clampi(ys0 + j, 0, rd.src_h - 1) * wpr + k;
         const uint64_t lab = rs.bits[rd.src_off + wi], brd = rs.bits[rd.border_off + wi];
@@ -267,7 +273,7 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(kOcc)))
         nonzero |= ((lab | brd) & m) != 0;
         nonfill |= ((~lab | brd) & m) != 0;
       }
-      const bool full = (part + 1) * kJpegWG <= bpi && (dbg == 0 || dbg >= 40);
+      const bool full = (part + 1) * kWG <= bpi && (dbg == 0 || dbg >= 40);
       const bool zero = __syncthreads_or(nonzero) == 0;
       const bool fill = __syncthreads_or(nonfill) == 0;
       wgflat = full && (zero || fill);
@@ -275,23 +281,23 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(kOcc)))
     }
   }
   if (d.render >= 0 && rd.kind == kRenderRawGray) {
-    const int m0 = part * (kJpegWG / 4), m1 = min(m0 + kJpegWG / 4, bpi >> 2) - 1;
+    const int m0 = part * (kWG / 4), m1 = min(m0 + kWG / 4, bpi >> 2) - 1;
     const int r0 = m0 / mcux, r1 = m1 / mcux;
     const int nrows = 8 * (r1 - r0) + 10;
     pcols = swz_col(rd.src_w + 1) + 1;
     pcols += (4 - pcols % 8 + 8) % 8;  // row stride ≡ 4 (mod 8)
-    if (nrows * pcols <= kPatchLds && !(rd.src_off & 1)) {
+    if (nrows * pcols <= kPatch && !(rd.src_off & 1)) {
       staged = true;
       ys0 = 8 * r0 - 1;
       const int W = rd.src_w, H = rd.src_h, hw = W >> 1;  // W is a multiple of 8 (exact 2× fit)
       const uint16_t* src = rs.raw + rd.src_off;
       // Interior: 4-byte loads of pixel pairs, all issued before the LDS stores (one latency).
       const int nw = nrows * hw;
-      constexpr int kU = 12;  // ≥ 18 rows × 128 pairs / 256 threads for a 256² source: one round of loads
+      constexpr int kU = kWG == 512 ? 9 : 12;  // ≥ rows × 128 pairs / kWG threads for a 256² source: one round
       uint32_t v[kU];
 #pragma unroll
       for (int t = 0; t < kU; ++t) {
-        const int i = tid + t * kJpegWG;
+        const int i = tid + t * kWG;
         v[t] = 0u;
         if (i < nw) {
           const int j = i / hw, k = i - j * hw;
@@ -303,21 +309,21 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(kOcc)))
       };
 #pragma unroll
       for (int t = 0; t < kU; ++t) {
-        const int i = tid + t * kJpegWG;
+        const int i = tid + t * kWG;
         if (i < nw) {
           const int j = i / hw, k = i - j * hw;
           spatch[j * pcols + swz_col(2 * k + 1)] = value((uint16_t)(v[t] & 0xFFFFu));
           spatch[j * pcols + swz_col(2 * k + 2)] = value((uint16_t)(v[t] >> 16));
         }
       }
-      for (int i = tid + kU * kJpegWG; i < nw; i += kJpegWG) {  // larger footprints
+      for (int i = tid + kU * kWG; i < nw; i += kWG) {  // larger footprints
         const int j = i / hw, k = i - j * hw;
         const uint32_t u = *reinterpret_cast<const uint32_t*>(src + (size_t)clampi(ys0 + j, 0, H - 1) * W + 2 * k);
         spatch[j * pcols + swz_col(2 * k + 1)] = value((uint16_t)(u & 0xFFFFu));
         spatch[j * pcols + swz_col(2 * k + 2)] = value((uint16_t)(u >> 16));
       }
       // Clamped halo columns 0 and W+1.
-      for (int i = tid; i < 2 * nrows; i += kJpegWG) {
+      for (int i = tid; i < 2 * nrows; i += kWG) {
         const int j = i >> 1, right = i & 1;
         spatch[j * pcols + (right ? swz_col(W + 1) : 0)] =
             value(src[(size_t)clampi(ys0 + j, 0, H - 1) * W + (right ? W - 1 : 0)]);
@@ -332,7 +338,7 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(kOcc)))
   // so the AC stream is coded first and the DC code is prepended at assembly time.
   if (d.render >= 0 && rd.kind != kRenderLabels) win = render_window(rd, rs.stats);
   uint32_t* const pbuf = spriv + tid * kPrivWords;
-  uint32_t* const pspill = w.spill + ((size_t)blockIdx.x * kJpegWG + tid) * kSpillWords;
+  uint32_t* const pspill = w.spill + ((size_t)blockIdx.x * kWG + tid) * kSpillWords;
   int dc0 = 0;
   uint32_t acbits = 0;
   if (wgflat) {
@@ -465,7 +471,7 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(kOcc)))
   if (tid < 64) {
     int dcp = 0;
     if (part > 0 && dbg != 17) {  // dbg 17: profiling variant without the predecessor's DC (output invalid)
-      const int pb = part * kJpegWG - 1;
+      const int pb = part * kWG - 1;
       const int mcu = pb >> 2, sub = pb & 3;
       const int u = 8 * (2 * (mcu % mcux) + (sub & 1)) + (tid & 7);
       const int v = 8 * (2 * (mcu / mcux) + (sub >> 1)) + (tid >> 3);
@@ -487,14 +493,14 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(kOcc)))
     const uint32_t code0 =
         ((dce0 & 0xFFFFu) << dn0) | ((uint32_t)(diff0 < 0 ? diff0 - 1 : diff0) & ((1u << dn0) - 1u));
     constexpr uint32_t kMcu = 0x28A28A00u;  // (00 1010) × 4 luma blocks + 4 × 00 chroma, MSB first
-    agg = L0 + 4u + (uint32_t)(kJpegWG - 1) * 6u + (uint32_t)(kJpegWG / 4) * 8u;
+    agg = L0 + 4u + (uint32_t)(kWG - 1) * 6u + (uint32_t)(kWG / 4) * 8u;
     nlocal = (agg + 31u) >> 5;
     // Range bit k ≥ L0 + 4 is pattern bit (k − (L0 − 2)) mod 32: every word is the pattern rotated
     // left by (2 − L0) mod 32; word 0 starts with block 0's codes.
     const uint32_t rot = (34u - L0) & 31u;
     const uint32_t pat = rot ? (kMcu << rot) | (kMcu >> (32u - rot)) : kMcu;
     const uint32_t hl = L0 + 4u;  // ≤ 24 bits
-    for (uint32_t i = tid; i <= nlocal + 1u; i += kJpegWG) {
+    for (uint32_t i = tid; i <= nlocal + 1u; i += kWG) {
       uint32_t v = i < nlocal ? pat : 0u;
       if (i == 0) v = (((code0 << 4) | 0xAu) << (32u - hl)) | (pat & ((1u << (32u - hl)) - 1u));
       if (i == nlocal - 1u && (agg & 31u)) v &= ~0u << (32u - (agg & 31u));
@@ -518,7 +524,7 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(kOcc)))
     const uint32_t nwp = (acbits + 31) >> 5;
     const uint32_t acpos = excl + (uint32_t)dclen;
     if (in_lds) {
-      for (uint32_t i = tid; i <= nlocal; i += kJpegWG) swg[i] = 0u;
+      for (uint32_t i = tid; i <= nlocal; i += kWG) swg[i] = 0u;
       __syncthreads();
       if (valid) {
         const uint32_t dv = dclen ? dccode << (32 - dclen) : 0u, sh0 = excl & 31u, w0 = excl >> 5;
@@ -552,7 +558,7 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(kOcc)))
     // must end within the range (p + 8 ≤ A), so its count is popcount(r & (0x80808080 >> f)) over
     // the valid positions — instead of one LDS byte extraction per byte and alignment.
     const uint32_t nw = (A + 31u) >> 5;  // the range buffer has ≥ 2 words of slack (in_lds)
-    for (uint32_t j = tid; j < nw; j += kJpegWG) {
+    for (uint32_t j = tid; j < nw; j += kWG) {
       const int32_t lim = (int32_t)A - 8 - 32 * (int32_t)j;  // last q whose byte fits in the range
       if (lim < 0) continue;
       const uint64_t v = ((uint64_t)swg[j] << 32) | swg[j + 1];
@@ -577,7 +583,11 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(kOcc)))
   if (tid < 64) {
     uint32_t ff[8];
 #pragma unroll
-    for (int al = 0; al < 8; ++al) ff[al] = sff[al] + sff[8 + al] + sff[16 + al] + sff[24 + al];
+    for (int al = 0; al < 8; ++al) {
+      ff[al] = 0;
+#pragma unroll
+      for (int wq = 0; wq < kWG / 64; ++wq) ff[al] += sff[wq * 8 + al];
+    }
     const uint32_t w0 = in_lds ? swg[0] : 0u;
     const uint32_t lead = ~w0 ? (uint32_t)__builtin_clz(~w0) : 32u;
     const uint32_t head = min(min(lead, 8u), A);  // leading ones of the range
@@ -717,7 +727,7 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(kOcc)))
   // every run its output position; the stuffed bytes are staged in LDS behind the bit range and
   // copied out with consecutive lanes on consecutive bytes.
   const uint32_t nown = s_nown, f = s_f, hs = s_strad ? 1u : 0u;
-  const uint32_t per = (nown + kJpegWG - 1) / kJpegWG;
+  const uint32_t per = (nown + kWG - 1) / kWG;
   const uint32_t j0 = min(nown, tid * per), j1 = min(nown, j0 + per);
   auto owned = [&](uint32_t j) -> uint32_t {
     if (j < hs) return s_strad_v;
@@ -756,7 +766,7 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(kOcc)))
     const uint32_t nchunks = (phase + tot + 15u) >> 4;
     uint8_t* const dbase = dst - phase;  // 16-byte aligned
     const uint8_t* const lbase = sbuf - phase;
-    for (uint32_t c = tid; c < nchunks; c += kJpegWG) {
+    for (uint32_t c = tid; c < nchunks; c += kWG) {
       const uint32_t b0 = 16u * c, lo = max(b0, phase), hi = min(b0 + 16u, phase + tot);
       if (lo == b0 && hi == b0 + 16u) {
         *reinterpret_cast<uint4*>(dbase + b0) = *reinterpret_cast<const uint4*>(lbase + b0);
@@ -787,7 +797,8 @@ void launch_jpeg(const uint8_t* canvas, const JpegDesc* jd, int ncanvas, int out
   JpegRenderSrc rs;
   if (fused) rs = *fused;
   const int bpi = (out_w / 8) * (out_h / 8);
-  const int parts = (bpi + kJpegWG - 1) / kJpegWG;
+  const int wg = w.wg == 512 ? 512 : kJpegWG;
+  const int parts = (bpi + wg - 1) / wg;
   if ((size_t)parts * ncanvas > w.look_cap) throw DeviceError("launch_jpeg: look-back capacity exceeded");
   w.look_used = (size_t)parts * ncanvas;
   // NM03_PROFILE_VARIANT=jpeg=N selects truncated profiling variants (output invalid;
@@ -812,8 +823,13 @@ void launch_jpeg(const uint8_t* canvas, const JpegDesc* jd, int ncanvas, int out
     w.look_base = w.look_base ? 0 : half;
     w.prev_words = words;
   }
-  jpeg_fused_kernel<4, kUnionWords><<<parts * ncanvas, kJpegWG, 0, stream>>>(canvas, jd, ncanvas, out_w, out_h, q, w,
-                                                                              rs, out, out_sizes, dbg);
+  if (wg == 512)
+    jpeg_fused_kernel<4, kUnionWords512, 512><<<parts * ncanvas, 512, 0, stream>>>(canvas, jd, ncanvas, out_w, out_h, q,
+                                                                                   w, rs, out, out_sizes, dbg);
+  else
+    jpeg_fused_kernel<4, kUnionWords, kJpegWG><<<parts * ncanvas, kJpegWG, 0, stream>>>(canvas, jd, ncanvas, out_w,
+                                                                                       out_h, q, w, rs, out,
+                                                                                       out_sizes, dbg);
   check_launch("jpeg_fused_kernel");
 }
 

@@ -509,6 +509,63 @@ def test_engine_mixed_blob_layouts_identical(native, cohort_root, tmp_path, monk
         assert runs[0][1][f"mixed/1-{k}_original.jpg"] == g["jpeg_original"]
 
 
+def test_engine_bar_upload_identical(native, cohort_root, tmp_path):
+    """EngineConfig.bar_upload (loaders store the pixels into VRAM through the large BAR, HDP flush
+    before the kernels) vs the pinned-memory + SDMA upload: same statuses, byte-identical trees over
+    several passes through the same slots (stale-cache check), with 12-bit packed and 16-bit slices."""
+    d = tmp_path / "mixed"
+    d.mkdir()
+    hi = native.phantom_slice(256, 256, 4, 11, 25, 9).astype(np.uint32) + 3000
+    (d / "1-1.dcm").write_bytes(native.dicom_bytes(np.minimum(hi, 65535).astype(np.uint16)))
+    (d / "1-2.dcm").write_bytes(native.dicom_bytes(native.phantom_slice(150, 203, 2, 7, 25, 3)))
+    runs = []
+    for i, bar in enumerate([False, True]):
+        out = str(tmp_path / f"o{i}")
+        items = _items(native, cohort_root, out)[:60]
+        os.makedirs(os.path.join(out, "mixed"), exist_ok=True)
+        items = items[:7] + [(str(d / f"1-{k}.dcm"), os.path.join(out, "mixed")) for k in (1, 2)] + items[7:]
+        ec = nm.PipelineConfig(batch_size=16, streams=2, threads=4).engine_config()
+        ec.bar_upload = bar
+        eng = native.Engine(ec)
+        for _ in range(3):
+            st, _ = eng.run(items)
+        del eng
+        runs.append(([c for c, _ in st], _tree(out)))
+    assert runs[0][0] == runs[1][0] and runs[0][0].count(0) == len(runs[0][0])
+    diffs = sorted(k for k in runs[0][1] if runs[1][1].get(k) != runs[0][1][k])[:4]
+    assert not diffs, diffs
+
+
+def test_engine_jpeg_wg512_identical(native, cohort_root, tmp_path):
+    """512-block JPEG-encoder workgroups (EngineConfig.jpeg_wg, 8 waves) vs 256: byte-identical trees
+    on the cohort plus flat / half-band / odd-sized label images and a capacity edge."""
+    d = tmp_path / "extra"
+    d.mkdir()
+    full = np.full((256, 256), 1500, np.uint16)
+    half = np.zeros((256, 256), np.uint16)
+    half[:128] = 1500
+    (d / "1-1.dcm").write_bytes(native.dicom_bytes(full))
+    (d / "1-2.dcm").write_bytes(native.dicom_bytes(half))
+    (d / "1-3.dcm").write_bytes(native.dicom_bytes(native.phantom_slice(150, 203, 2, 7, 25, 3)))
+    runs = []
+    for i, (wg, cap) in enumerate([(256, 0), (512, 0), (512, 20000)]):
+        out = str(tmp_path / f"o{i}")
+        items = _items(native, cohort_root, out)[:50]
+        os.makedirs(os.path.join(out, "extra"), exist_ok=True)
+        items = items[:5] + [(str(d / f"1-{k}.dcm"), os.path.join(out, "extra")) for k in (1, 2, 3)] + items[5:]
+        ec = nm.PipelineConfig(batch_size=16, streams=2, threads=4).engine_config()
+        ec.jpeg_wg = wg
+        ec.jpeg_out_cap = cap
+        eng = native.Engine(ec)
+        st, _ = eng.run(items)
+        del eng
+        runs.append(([c for c, _ in st], _tree(out)))
+    for r in runs[1:]:
+        assert r[0] == runs[0][0] and r[0].count(0) == len(r[0])
+        diffs = sorted(k for k in runs[0][1] if r[1].get(k) != runs[0][1][k])[:4]
+        assert not diffs, diffs
+
+
 def test_engine_jpeg_capacity_edge_identical(native, cohort_root, tmp_path):
     """Output capacity at the edge of real segment sizes (20000 bytes: some images fit, some
     overflow mid-image and take the CPU re-encode): statuses and trees identical to the default

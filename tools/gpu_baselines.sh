@@ -21,6 +21,9 @@ timeout -k 10 120 $B/nm03_bench --config single --data-root $T/cohort/ --steps 5
 timeout -k 10 120 $B/nm03_bench --config single-cpu --data-root $T/cohort/ --steps 10 --warmup 2 > $O/c1_cpu.json || exit 112
 # config 2: one patient
 timeout -k 10 120 $B/nm03_bench --config cohort --data-root $T/patient/ --out /tmp/bl_o2 --steps 50 --warmup 5 --batch-size 25 --streams 3 > $O/c2_gpu.json || exit 121
+# config 2 as written ("per-slice streams"): one slice per launch chain, 4 slots = 4 HIP streams (the
+# box's GPU_MAX_HW_QUEUES), so up to 4 slices are in flight, each on its own stream
+timeout -k 10 120 $B/nm03_bench --config cohort --data-root $T/patient/ --out /tmp/bl_o2s --steps 50 --warmup 5 --batch-size 1 --streams 4 > $O/c2_gpu_per_slice_streams.json || exit 123
 timeout -k 10 120 $B/nm03_bench --config cpu-reference --data-root $T/patient/ --out /tmp/bl_o2c --steps 3 --warmup 1 --batch-size 25 --threads 16 > $O/c2_cpu.json || exit 122
 # config 3: full cohort (bench.py is the headline; native driver for the same work)
 timeout -k 10 300 python bench.py --steps 20 --warmup 3 --data-root $T/cohort > $O/c3_gpu_bench.json || exit 131
@@ -35,6 +38,6 @@ echo "c4 done $(date)" >> $O/progress.txt
 timeout -k 10 120 $B/nm03_bench --config volume --data-root $T/vol/ --steps 10 --warmup 2 > $O/c5_gpu.json || exit 151
 timeout -k 10 300 $B/nm03_bench --config volume-cpu --data-root $T/vol/ --steps 2 --warmup 1 --threads 16 > $O/c5_cpu.json || exit 152
 echo "c5 done $(date)" >> $O/progress.txt
-# CLI wall clock: 6 timed invocations of each unmodified CLI on the full cohort (first = cold)
-timeout -k 10 600 python3 tools/cli_wall.py "$B" "$T/cohort/" > $O/cli_wall.jsonl || exit 161
+# CLI wall clock: 10 timed invocations of each unmodified CLI on the full cohort, exact (wait4)
+timeout -k 10 600 python3 tools/cli_wall.py "$B" "$T/cohort/" 10 > $O/cli_wall.jsonl || exit 161
 echo "done $(date)" >> $O/progress.txt
