@@ -19,12 +19,20 @@ bool sync_launches();
 // real kernel. Variants truncate the kernel for time splits; their output is invalid.
 int profile_variant(const char* kernel);
 
+// Loads the code objects of the 2D pipeline's kernels (median k, sharpen, SRG, JPEG) on the current
+// device. HIP loads a translation unit's code object at the first launch of one of its kernels;
+// the CLIs call this on their start-up thread so the first batch does not pay for it.
+void preload_kernels();
+void preload_median();
+void preload_sharpen();
+void preload_srg();
+
 // K1a: k×k median of raw keys → `med` (u16 keys, same layout as raw). k ∈ {3,5,7,9}.
 // Per-slice key range: with `tile_mm` (2 u32 per tile) each tile stores its (min, max) and
 // launch_sharpen_band reduces them into stats (no atomics); without it, atomics on stats.
 // With `blob` (engine batches) the samples are read from the uploaded blob at SliceDesc::blob_off
 // (12-bit packed slices decoded on the fly) instead of `raw`, and the expanded 16-bit samples are
-// written to `raw_out` at raw_off (what launch_unpack would produce).
+// written to `raw_out` at raw_off (the samples the render stage reads).
 void launch_median(const uint16_t* raw, uint16_t* med, const SliceDesc* descs, const TileDesc* tiles, int ntiles,
                    int k, SliceStats* stats, hipStream_t stream, uint32_t* tile_mm = nullptr,
                    const uint16_t* blob = nullptr, uint16_t* raw_out = nullptr);

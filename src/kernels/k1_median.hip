@@ -246,4 +246,9 @@ void launch_median(const uint16_t* raw, uint16_t* med, const SliceDesc* descs, c
   check_launch("median_kernel");
 }
 
+void preload_median() {
+  hipFuncAttributes a;
+  (void)hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&median_kernel<7>));
+}
+
 }  // namespace nm03::gpu

@@ -293,4 +293,9 @@ void launch_sharpen_band(const uint16_t* med, uint64_t* band, float* sharpened, 
   check_launch("sharpen_band_kernel");
 }
 
+void preload_sharpen() {
+  hipFuncAttributes a;
+  (void)hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&sharpen_band_kernel<4>));
+}
+
 }  // namespace nm03::gpu

@@ -139,4 +139,9 @@ void launch_srg_morph(const uint64_t* band, const SliceDesc* descs, int nslices,
   check_launch("srg_morph_kernel");
 }
 
+void preload_srg() {
+  hipFuncAttributes a;
+  (void)hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&srg_morph_kernel<false>));
+}
+
 }  // namespace nm03::gpu

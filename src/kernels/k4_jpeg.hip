@@ -833,4 +833,12 @@ void launch_jpeg(const uint8_t* canvas, const JpegDesc* jd, int ncanvas, int out
   check_launch("jpeg_fused_kernel");
 }
 
+void preload_kernels() {
+  preload_median();
+  preload_sharpen();
+  preload_srg();
+  hipFuncAttributes a;
+  (void)hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&jpeg_fused_kernel<4, kUnionWords, kJpegWG>));
+}
+
 }  // namespace nm03::gpu
