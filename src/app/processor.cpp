@@ -697,22 +697,23 @@ bool fast_exit_enabled() {
 }
 
 namespace {
-bool g_exit_armed = false;
+std::atomic<bool> g_exit_armed{false};
 void fast_exit_handler(int status, void*) {  // on_exit: receives exit()'s status
+  if (!g_exit_armed.load()) return;          // not a CLI (e.g. the Python module): normal teardown
   std::fflush(nullptr);
   _exit(status);
 }
+// Registered when libnm03 is loaded, i.e. before the constructors of LD_PRELOADed libraries run
+// (the dynamic loader initialises a program's own dependencies first). Exit handlers run in reverse
+// order of registration, so this one runs after every handler registered later — a profiler tool's
+// (rocprofv3 registers the one that writes its results from its preloaded library's constructor) —
+// and before the destructors of the libraries libnm03 depends on (HIP's static teardown: slow, and
+// under rocprofv3 it faulted after the tool had finalised; profiles/r4/probe/c5_prof_segv_backtrace.txt).
+__attribute__((constructor)) void register_fast_exit() { on_exit(fast_exit_handler, nullptr); }
 }  // namespace
 
 void arm_fast_exit() {
-  // Registered before any HIP call, so it runs after every exit handler registered later — those
-  // of a profiler's tool library (rocprofv3 writes its results from one) — and before the shared
-  // libraries' destructors (HIP's static teardown: slow, and under rocprofv3 it faulted after the
-  // tool had finalised; profiles/r4/probe/c5_prof_segv_backtrace.txt).
-  if (fast_exit_enabled() && !g_exit_armed) {
-    on_exit(fast_exit_handler, nullptr);
-    g_exit_armed = true;
-  }
+  if (fast_exit_enabled()) g_exit_armed.store(true);
 }
 
 int cli_exit(int rc) {
@@ -720,7 +721,7 @@ int cli_exit(int rc) {
   std::cerr.flush();
   std::fflush(nullptr);
   if (fast_exit_enabled()) {
-    if (!g_exit_armed) _exit(rc);
+    if (!g_exit_armed.load()) _exit(rc);
     std::exit(rc);
   }
   return rc;
