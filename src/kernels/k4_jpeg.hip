@@ -204,7 +204,7 @@ __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(kOcc))) voi
     asm volatile("" : "+v"(tp));
     ticket = __hip_atomic_fetch_add(tp, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  actab[tid] = kHuffAcLuma.e[tid];
+  if (kWG == 256 || tid < 256) actab[tid] = kHuffAcLuma.e[tid];  // 256 entries (512-thread workgroups: half)
   if (tid < 16) dctab[tid] = tid < 12 ? kHuffDcLuma.e[tid] : 0u;
   // JpegDesc::render is -1 or img itself, so the render descriptor loads alongside the JPEG one
   // (no dependent round trip); the render window (stats of the slice) is computed where the render

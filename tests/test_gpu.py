@@ -536,9 +536,11 @@ def test_engine_bar_upload_identical(native, cohort_root, tmp_path):
     assert not diffs, diffs
 
 
-def test_engine_jpeg_wg512_identical(native, cohort_root, tmp_path):
+def test_engine_jpeg_wg512_identical(native, tmp_path):
     """512-block JPEG-encoder workgroups (EngineConfig.jpeg_wg, 8 waves) vs 256: byte-identical trees
-    on the cohort plus flat / half-band / odd-sized label images and a capacity edge."""
+    on the cohort plus flat / half-band / odd-sized label images and a capacity edge. (The first
+    512 build filled its 256-entry AC table with all 512 threads: the LDS overrun raced with the
+    ticket it published and hung a 96-slice batch on the box, gpurun_out/r4g.)"""
     d = tmp_path / "extra"
     d.mkdir()
     full = np.full((256, 256), 1500, np.uint16)
@@ -547,13 +549,16 @@ def test_engine_jpeg_wg512_identical(native, cohort_root, tmp_path):
     (d / "1-1.dcm").write_bytes(native.dicom_bytes(full))
     (d / "1-2.dcm").write_bytes(native.dicom_bytes(half))
     (d / "1-3.dcm").write_bytes(native.dicom_bytes(native.phantom_slice(150, 203, 2, 7, 25, 3)))
+    cohort = str(tmp_path / "data") + "/"
+    native.synth_cohort(cohort, patients=6, min_slices=16, max_slices=20, threads=4)
     runs = []
     for i, (wg, cap) in enumerate([(256, 0), (512, 0), (512, 20000)]):
         out = str(tmp_path / f"o{i}")
-        items = _items(native, cohort_root, out)[:50]
+        items = _items(native, cohort, out)
         os.makedirs(os.path.join(out, "extra"), exist_ok=True)
         items = items[:5] + [(str(d / f"1-{k}.dcm"), os.path.join(out, "extra")) for k in (1, 2, 3)] + items[5:]
-        ec = nm.PipelineConfig(batch_size=16, streams=2, threads=4).engine_config()
+        # Bench-sized batches (96 slices = 192 images per launch, 8 workgroups of 512 per gray image).
+        ec = nm.PipelineConfig(batch_size=96, streams=1, threads=4).engine_config()
         ec.jpeg_wg = wg
         ec.jpeg_out_cap = cap
         eng = native.Engine(ec)
