@@ -21,7 +21,8 @@ int profile_variant(const char* kernel);
 
 // Loads the code objects of the 2D pipeline's kernels (median k, sharpen, SRG, JPEG) on the current
 // device. HIP loads a translation unit's code object at the first launch of one of its kernels;
-// the CLIs call this on their start-up thread so the first batch does not pay for it.
+// Engine construction calls it (one thread, before any launch); the CLIs already on their start-up
+// thread, so the first batch does not pay for it.
 void preload_kernels();
 void preload_median();
 void preload_sharpen();

@@ -11,7 +11,6 @@
 #include <cstdlib>
 #include <cstring>
 #include <fstream>
-#include <future>
 #include <iomanip>
 #include <iostream>
 #include <sstream>
@@ -408,9 +407,7 @@ int parallel_rank(const AppConfig& cfg, int rank, int size, Comm& comm, int devi
   // plans the cohort (and scans the slice headers for the buffer size); the engine is built once
   // both are done.
   double hip_init_s = 0, engine_ctor_s = 0, kernel_load_s = 0;
-  std::promise<void> hip_up;
-  std::future<void> hip_ready = hip_up.get_future();
-  std::thread warm([device, &hip_init_s, &kernel_load_s, &hip_up] {
+  std::thread warm([device, &hip_init_s, &kernel_load_s] {
     const double t0 = now_s();
     (void)hipSetDevice(device);
     void* p = nullptr;
@@ -423,9 +420,9 @@ int parallel_rank(const AppConfig& cfg, int rank, int size, Comm& comm, int devi
     void* h = nullptr;
     if (hipHostMalloc(&h, 4096, hipHostMallocDefault) == hipSuccess) (void)hipHostFree(h);
     hip_init_s = now_s() - t0;
-    hip_up.set_value();
-    // Then the kernels' code objects, while the engine is being built: HIP would otherwise load
-    // each at its first launch, inside the first batch.
+    // Then the kernels' code objects, which HIP would otherwise load at their first launches,
+    // inside the first batch. Done before the engine exists: lazy code-object loading racing with
+    // kernel launches from the engine's threads faulted inside the HSA runtime (gpurun_out/r4j).
     const double t1 = now_s();
     gpu::preload_kernels();
     kernel_load_s = now_s() - t1;
@@ -507,7 +504,7 @@ int parallel_rank(const AppConfig& cfg, int rank, int size, Comm& comm, int devi
       // Buffers sized for the largest slice of the cohort (headers scanned by rank 0) instead of
       // the 512² maximum: less pinned memory to allocate and register at start-up.
       if (seen_dim > 0) ec.max_dim = std::min(gpu::kMaxSliceDim, std::max(64, (int)((seen_dim + 63) / 64 * 64)));
-      hip_ready.wait();
+      warm.join();
       // Where this rank runs: its GPU's PCI bus id, and a CPU partition of that GPU's NUMA node
       // disjoint from every other rank's, with a pool sized to it and to the rank's share of the
       // CPU budget (the reference's one machine-wide omp_set_num_threads(16), main_parallel.cpp:401).

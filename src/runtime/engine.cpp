@@ -287,7 +287,13 @@ struct Engine::Impl {
       throw DeviceError("canvas size must be a multiple of 16");
     if (host_only_) make_templates();
     const double t0 = now_s();
-    if (!host_only_) check_hip(hipSetDevice(cfg.device), "hipSetDevice");
+    if (!host_only_) {
+      check_hip(hipSetDevice(cfg.device), "hipSetDevice");
+      // Every code object loaded here, on one thread, before any batch is launched: HIP otherwise
+      // loads a module at the first launch of one of its kernels, from whichever slot thread gets
+      // there first (a no-op when the CLI's start-up thread already did it).
+      preload_kernels();
+    }
     const double t1 = now_s();
     // Host threads and pinned buffers on the GPU's socket (numa.h).
     pool = std::make_unique<ThreadPool>(cfg.threads, [this](int i) {

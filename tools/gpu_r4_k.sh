@@ -1,0 +1,29 @@
+#!/bin/bash
+# (gpurun) Round 4: JPEG encoder instruction mix per phase. For each truncation variant
+# (NM03_PROFILE_VARIANT=jpeg=N: 7 tables+ticket, 1 +render, 16 +FDCT+quant, 2 +AC coding,
+# 4 +scan/bit range/look-back, 0 full; 40/41 gray/label only) one rocprofv3 --pmc pass of SQ
+# counters over the isolated encoder (1 stream, batch 96). Before that: config 5 (256-slice volume)
+# under rocprofv3 --kernel-trace (exit status and CSV written), and the headline bench's kernel stats.
+# gpurun_out/r4k/.
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"; export TMPDIR=/tmp; O=gpurun_out/r4k; mkdir -p $O
+B=build/bin
+T=/tmp/r4k_vol
+$B/nm03_synth --data-root $T/ --patients 1 --min-slices 256 --max-slices 256 --threads 16 > /dev/null || exit 5
+timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $O/c5 -o c5 \
+  -- $B/nm03_bench --config volume --data-root $T/ --steps 10 --warmup 2 > $O/c5_prof.json 2> $O/c5_prof.err
+echo "profiled config 5 exit $? csv $(ls $O/c5/*kernel_stats.csv 2>/dev/null | wc -l)" > $O/c5_prof_status.txt
+rm -rf $T
+grep -q "exit 0 csv 1" $O/c5_prof_status.txt || exit 6
+timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O/bench -o k \
+  -- python3 bench.py --steps 20 --warmup 3 --single-passes 0 --cli-runs 0 --wipe-passes 0 > $O/bench.json 2> $O/bench.err || exit 7
+rm -rf /dev/shm/nm03_bench_data*
+D=/tmp/r4k_data
+$B/nm03_synth --data-root $D/ --threads 16 > /dev/null || exit 11
+C="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY SQ_BUSY_CYCLES"
+for v in 7 1 16 2 4 0 40 41; do
+  NM03_PROFILE_VARIANT=jpeg=$v timeout -s KILL 90 rocprofv3 --pmc $C --output-format csv -d $O/v$v -o k \
+    -- $B/nm03_bench --config cohort --data-root $D/ --steps 2 --warmup 1 --streams 1 --batch-size 96 \
+    > $O/v$v.log 2>&1 || exit 12
+done
+rm -rf $D
