@@ -48,7 +48,7 @@ AppConfig parse_args(int argc, char** argv, const std::string& which);
 // the HIP runtime's teardown — unpinning host buffers and releasing device memory and contexts,
 // ≈70–130 ms of a ≈0.3 s cold CLI run that the kernel driver does at exit anyway. The engines are
 // drained (every run waited for) before this point. NM03_FAST_EXIT=0 returns rc normally instead.
-// Arms the fast exit (the exit handler itself is registered when libnm03 loads; parse_args arms it).
+// Arms the fast exit (call first thing in main, before any HIP call; parse_args does).
 void arm_fast_exit();
 // Ends a CLI: flushes, then (NM03_FAST_EXIT, default on) leaves through exit() whose last handler
 // _exits — later-registered handlers (profilers) still run, the runtime's static teardown does not.

@@ -143,6 +143,13 @@ class Engine {
 
   const EngineConfig& config() const;
 
+  // Returns once no engine thread can be inside the HIP runtime between runs: the slots built
+  // lazily by their own threads are built (or given up). For a process that exits without
+  // destroying the engine (the CLIs' fast exit): exit handlers registered after the engine's
+  // libraries — the HIP runtime's own among them — must not run while a slot thread is still
+  // allocating (a hipHostMalloc faulted inside the HSA runtime that way, gpurun_out/r4j).
+  void quiesce();
+
   struct Impl;
 
  private:

@@ -186,7 +186,10 @@ int run_sequential(const AppConfig& cfg) {
     struct Leak {
       std::unique_ptr<Engine>& e;
       ~Leak() {
-        if (fast_exit_enabled()) (void)e.release();
+        if (fast_exit_enabled() && e) {
+          e->quiesce();
+          (void)e.release();
+        }
       }
     } leak{engine_p};
     // Patient directories are wiped by renaming them aside; the deletions run on background threads
@@ -679,7 +682,10 @@ int parallel_rank(const AppConfig& cfg, int rank, int size, Comm& comm, int devi
                              ", \"comm\": {\"backend\": \"" + comm.backend() + "\", \"nranks\": " +
                              std::to_string(comm.transport_size()) + "}, \"devices\": " + rank_devices_json(devices) + "}");
   }
-  if (fast_exit_enabled()) (void)engine_p.release();  // the process ends in cli_exit: no teardown
+  if (fast_exit_enabled() && engine_p) {  // the process ends in cli_exit: no teardown
+    engine_p->quiesce();
+    (void)engine_p.release();
+  }
   return 0;
 }
 
@@ -696,21 +702,17 @@ bool fast_exit_enabled() {
 namespace {
 std::atomic<bool> g_exit_armed{false};
 void fast_exit_handler(int status, void*) {  // on_exit: receives exit()'s status
-  if (!g_exit_armed.load()) return;          // not a CLI (e.g. the Python module): normal teardown
   std::fflush(nullptr);
   _exit(status);
 }
-// Registered when libnm03 is loaded, i.e. before the constructors of LD_PRELOADed libraries run
-// (the dynamic loader initialises a program's own dependencies first). Exit handlers run in reverse
-// order of registration, so this one runs after every handler registered later — a profiler tool's
-// (rocprofv3 registers the one that writes its results from its preloaded library's constructor) —
-// and before the destructors of the libraries libnm03 depends on (HIP's static teardown: slow, and
-// under rocprofv3 it faulted after the tool had finalised; profiles/r4/probe/c5_prof_segv_backtrace.txt).
-__attribute__((constructor)) void register_fast_exit() { on_exit(fast_exit_handler, nullptr); }
 }  // namespace
 
 void arm_fast_exit() {
-  if (fast_exit_enabled()) g_exit_armed.store(true);
+  // Registered in main before any HIP call: handlers registered later (the HIP runtime's, and
+  // HIP's module teardown) run first; the shared libraries' destructors (HIP's static teardown:
+  // slow, and under rocprofv3 it faulted after the tool had finalised,
+  // profiles/r4/probe/c5_prof_segv_backtrace.txt) do not run.
+  if (fast_exit_enabled() && !g_exit_armed.exchange(true)) on_exit(fast_exit_handler, nullptr);
 }
 
 int cli_exit(int rc) {

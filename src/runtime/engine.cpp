@@ -321,6 +321,7 @@ struct Engine::Impl {
       slot_ms = std::to_string((int)((now_s() - ts) * 1e4) / 10.0).substr(0, 5);
     });
     const double t3 = now_s();
+    building_ = (int)slots.size() - 1;
     start_workers();
     const double t4 = now_s();
     log_info("engine on device " + std::to_string(cfg.device) + ": batch " + std::to_string(cfg.batch_size) + ", " +
@@ -1201,18 +1202,34 @@ struct Engine::Impl {
     done_cv.notify_all();
   }
 
+  // Slots still being built by their own threads (quiesce waits for 0).
+  std::mutex build_m_;
+  std::condition_variable build_cv_;
+  int building_ = 0;
+  void quiesce() {
+    std::unique_lock<std::mutex> g(build_m_);
+    build_cv_.wait(g, [&] { return building_ <= 0; });
+  }
+
   void worker(size_t slot_index) {
     pthread_setname_np(pthread_self(), "nm03-slot");
     place.bind_this_thread();
     (void)prctl(PR_SET_TIMERSLACK, 1000UL, 0, 0, 0);  // 1 µs: short poll sleeps stay short
     if (!host_only_) (void)hipSetDevice(cfg.device);
     if (!slots[slot_index]) {  // built lazily (see the constructor); this thread is its only user
+      bool ok = true;
       try {
         slots[slot_index] = make_slot();
       } catch (const std::exception& e) {
         log_warn("engine slot " + std::to_string(slot_index) + " unavailable, running with fewer streams: " + e.what());
-        return;
+        ok = false;
       }
+      {
+        std::lock_guard<std::mutex> g(build_m_);
+        --building_;
+      }
+      build_cv_.notify_all();
+      if (!ok) return;
     }
     Slot* s = slots[slot_index].get();
     for (;;) {
@@ -1400,6 +1417,7 @@ struct Engine::Impl {
 };
 
 Engine::Engine(const EngineConfig& cfg) : impl_(std::make_unique<Impl>(cfg)) {}
+void Engine::quiesce() { impl_->quiesce(); }
 Engine::~Engine() = default;
 std::vector<SliceStatus> Engine::run(const std::vector<WorkItem>& items, StageTimes* times,
                                      const std::function<void(size_t)>& on_start, int batch_cap) {
