@@ -103,10 +103,6 @@ def parse_args(argv=None):
     ap.add_argument("--create-writers", type=int, default=-1,
                     help="EngineConfig.create_writers: pool workers writing a batch's JPEGs at once while "
                          "its directories are being filled (-1 = engine default, 0 = no limit)")
-    ap.add_argument("--bar-upload", action="store_true",
-                    help="EngineConfig.bar_upload: loaders write pixels into VRAM through the large BAR (A/B)")
-    ap.add_argument("--jpeg-wg", type=int, default=256, choices=(256, 512),
-                    help="EngineConfig.jpeg_wg: luma blocks per JPEG-encoder workgroup")
     ap.add_argument("--batch-size", type=int, default=96)
     ap.add_argument("--streams", type=int, default=4)
     ap.add_argument("--threads", type=int, default=0,
@@ -306,8 +302,6 @@ def run_rank(args):
     ecfg.host_only = args.host_only
     if args.create_writers >= 0:
         ecfg.create_writers = args.create_writers
-    ecfg.bar_upload = args.bar_upload
-    ecfg.jpeg_wg = args.jpeg_wg
     engine = _DryEngine() if args.dry_run else n.Engine(ecfg)
 
     def pipeline_depth(shard_len):
@@ -551,8 +545,6 @@ def run_rank(args):
                 "streams": args.streams,
                 "threads": args.threads,
                 "create_writers": ecfg.create_writers,
-                "bar_upload": bool(args.bar_upload),
-                "jpeg_wg": args.jpeg_wg,
                 "stream_steps": bool(args.stream_steps),
                 "pipelined_passes": not args.no_pipeline and not args.stream_steps,
                 "pipeline_depth": primary["pipeline_depth"],

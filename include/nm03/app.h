@@ -44,14 +44,17 @@ struct AppConfig {
 // Parse the shared flag set; `which` selects CLI-specific defaults. Exits on --help.
 AppConfig parse_args(int argc, char** argv, const std::string& which);
 
-// End of a CLI process: flushes stdout/stderr and leaves with _exit(rc), skipping the engine's and
-// the HIP runtime's teardown — unpinning host buffers and releasing device memory and contexts,
-// ≈70–130 ms of a ≈0.3 s cold CLI run that the kernel driver does at exit anyway. The engines are
-// drained (every run waited for) before this point. NM03_FAST_EXIT=0 returns rc normally instead.
-// Arms the fast exit (call first thing in main, before any HIP call; parse_args does).
+// End of a CLI process without teardown: the engines are drained (every run waited for, no slot
+// thread inside HIP: Engine::quiesce) and left to the kernel instead of unpinning host buffers and
+// releasing device memory and contexts (≈70–130 ms of a cold CLI run). main registers an exit
+// handler before any HIP call (arm_fast_exit; parse_args does) and ends with `return cli_exit(rc)`:
+// a profiler that finalises when main returns (rocprofv3 writes its results there; a CLI that called
+// exit() from inside main lost them, tools/exit_order) and every handler registered after the
+// armed one still run, then the armed handler _exits before the shared libraries' static
+// destructors (HIP's teardown, which faulted under rocprofv3: profiles/r4/probe/). NM03_FAST_EXIT=0:
+// normal exit with full teardown.
 void arm_fast_exit();
-// Ends a CLI: flushes, then (NM03_FAST_EXIT, default on) leaves through exit() whose last handler
-// _exits — later-registered handlers (profilers) still run, the runtime's static teardown does not.
+// Flushes stdout/stderr and returns rc (for `return cli_exit(rc);` in main).
 int cli_exit(int rc);
 bool fast_exit_enabled();
 

@@ -87,14 +87,6 @@ struct EngineConfig {
   // 4 creating at once and 35–44 µs with 16 (tools/create_probe.cpp, profiles/r4/create_probe/);
   // the other workers take the next batches' loads meanwhile.
   int create_writers = 4;
-  // Loaders write the raw pixels straight into the device blob through the GPU's large BAR (CPU
-  // write-combining stores into VRAM, an HDP flush before the batch's kernels) instead of pinned
-  // host memory + SDMA upload: 197 of the ≈426 KB of host DRAM traffic per slice less, CPU stores
-  // over PCIe instead (≈38 GB/s one thread, ≈45 GB/s aggregate on the MI355X box, tools/bar_probe.cpp).
-  bool bar_upload = false;
-  // Luma blocks per JPEG-encoder workgroup: 256 (4 waves, 4 workgroups per CU) or 512 (8 waves,
-  // 2 per CU: half the per-workgroup fixed costs — ticket, tables, predecessor DC, look-back).
-  int jpeg_wg = 256;
 };
 
 // Everything test_pipeline exports / tests inspect for one slice (host copies).

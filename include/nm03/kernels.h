@@ -111,7 +111,6 @@ struct JpegWork {
   size_t look_base = 0, clear_base = 0, clear_words = 0, prev_words = 0;  // launch_jpeg's bookkeeping
   uint32_t* ticket = nullptr;    // per-image part ticket counters (≥ ncanvas; zeroed once; self-resetting)
   uint32_t* spill = nullptr;     // look_cap × 256 × 56 words: Huffman bits of very detailed blocks
-  int wg = 256;                  // luma blocks per workgroup: 256 (4 waves) or 512 (8 waves)
 };
 // Fused-render inputs (needed when any JpegDesc.render ≥ 0).
 struct JpegRenderSrc {

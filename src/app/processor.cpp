@@ -708,10 +708,8 @@ void fast_exit_handler(int status, void*) {  // on_exit: receives exit()'s statu
 }  // namespace
 
 void arm_fast_exit() {
-  // Registered in main before any HIP call: handlers registered later (the HIP runtime's, and
-  // HIP's module teardown) run first; the shared libraries' destructors (HIP's static teardown:
-  // slow, and under rocprofv3 it faulted after the tool had finalised,
-  // profiles/r4/probe/c5_prof_segv_backtrace.txt) do not run.
+  // Registered in main before any HIP call (app.h): runs after the handlers registered later and
+  // after a profiler's end-of-main finalisation, before the libraries' static destructors.
   if (fast_exit_enabled() && !g_exit_armed.exchange(true)) on_exit(fast_exit_handler, nullptr);
 }
 
@@ -719,10 +717,6 @@ int cli_exit(int rc) {
   std::cout.flush();
   std::cerr.flush();
   std::fflush(nullptr);
-  if (fast_exit_enabled()) {
-    if (!g_exit_armed.load()) _exit(rc);
-    std::exit(rc);
-  }
   return rc;
 }
 

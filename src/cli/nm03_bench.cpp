@@ -53,8 +53,6 @@ int main(int argc, char** argv) {
     else if (a == "--max-dim") ec.max_dim = std::atoi(v().c_str());
     else if (a == "--dilation-3d") dil3d = std::atoi(v().c_str());
     else if (a == "--device") ec.device = std::atoi(v().c_str());
-    else if (a == "--jpeg-wg") ec.jpeg_wg = std::atoi(v().c_str());
-    else if (a == "--bar-upload") ec.bar_upload = true;
     else if (a == "--host-only") ec.host_only = true;  // cohort: every load/pack/write, no GPU (sanitizer sweeps)
     else {
       std::cerr << "unknown option " << a << std::endl;
@@ -250,12 +248,10 @@ int main(int argc, char** argv) {
     std::cerr << "Fatal error: " << e.what() << std::endl;
     return nm03::app::cli_exit(1);
   }
-  // Like the CLIs: exit handlers run (rocprofv3 writes its results from one), then _exit before the
-  // shared libraries' destructors. Under rocprofv3 the process used to die with SIGSEGV after main
-  // returned (exit 139): the crash handler's backtrace shows the fault in libamdhip64's own static
-  // destructor (__cxa_finalize → libamdhip64 → libhsa-runtime64), after rocprofv3's "tool
-  // finalization" — HIP's exit-time teardown calls into an HSA runtime the profiler's tool has
-  // already finalised. No nm03 frame is on that stack; the results were complete
-  // (profiles/r4/probe/c5_prof_segv_backtrace.txt).
+  // Like the CLIs: return from main (rocprofv3 writes its results when main returns), then the
+  // handler armed at the start of main _exits before the shared libraries' destructors. Under
+  // rocprofv3 a full teardown died with SIGSEGV inside libamdhip64's own static destructor, after
+  // the tool's finalisation, with no nm03 frame on the stack
+  // (profiles/r4/probe/c5_prof_segv_backtrace.txt); exiting from inside main lost the results.
   return nm03::app::cli_exit(0);
 }

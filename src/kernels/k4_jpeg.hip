@@ -96,8 +96,6 @@ __device__ __forceinline__ int swz_col(int c) { return c + (c >> 2); }
 // One LDS region serves the render (source patch above) and then, once every block is rendered,
 // the workgroup's assembled bit range followed by its staged stuffed output bytes.
 constexpr int kUnionWords = kPatchLds + 1080;  // 27 KiB as before (4 workgroups per CU): bit ranges up to ~220 Kbit
-// 512-block workgroups (JpegWork::wg = 512): 34 staged rows, 2 workgroups per CU (8 waves each).
-constexpr int kUnionWords512 = 34 * 324 + 2160;
 
 constexpr int kPrivWords = 5;    // per-block Huffman bits kept in LDS (160 bits, odd stride) ...
 constexpr int kSpillWords = 56;  // ... the rest in the block's global spill slot (a block needs ≤ 1700)
@@ -150,16 +148,18 @@ __device__ __forceinline__ uint32_t priv_word(const uint32_t* pb, const uint32_t
 // kOcc: target waves per SIMD (= workgroups per CU); kUnion: LDS words of the patch / bit-range
 // union. 5 workgroups per CU (31.7 KiB, ≤ 96 VGPRs with spills) measured no better than 4 once
 // images were dealt round-robin (profiles/r3/jpeg_spread/split_and_occ5.txt).
-template <int kOcc, int kUnion, int kWG>
-__global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(kOcc))) void jpeg_fused_kernel(const uint8_t* __restrict__ canvas,
+template <int kOcc, int kUnion>
+__global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(kOcc))) void jpeg_fused_kernel(const uint8_t* __restrict__ canvas,
                                                              const JpegDesc* __restrict__ jd, int ncanvas, int out_w,
                                                              int out_h, QuantRecip q, JpegWork w, JpegRenderSrc rs,
                                                              uint8_t* __restrict__ out, int32_t* __restrict__ out_sizes,
                                                              int dbg) {
   // dbg: profiling variant (NM03_PROFILE_VARIANT=jpeg=N; output invalid), 0 = the real encoder.
-  // kWG blocks (threads) per workgroup: kWG / 4 MCUs; the gray staging area holds their rows
-  // (+ a 1-row halo each side) of a 256-wide source: 18 rows for 256, 34 for 512.
-  constexpr int kPatch = kWG == 512 ? 34 * 324 : kPatchLds;
+  // kWG blocks (threads) per workgroup = kWG / 4 MCUs. (512-block workgroups, 8 waves and 2 per
+  // CU, halve the per-workgroup fixed costs but measured no faster: 116.8–117.6 vs 119.2 µs per
+  // 96-slice batch in the bench, profiles/r4/jpeg_wg512/.)
+  constexpr int kWG = kJpegWG;
+  constexpr int kPatch = kPatchLds;
   static_assert(kPatch <= kUnion, "staging area exceeds the LDS union");
   __shared__ uint32_t actab[256];
   __shared__ uint32_t dctab[16];
@@ -204,7 +204,7 @@ __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(kOcc))) voi
     asm volatile("" : "+v"(tp));
     ticket = __hip_atomic_fetch_add(tp, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  if (kWG == 256 || tid < 256) actab[tid] = kHuffAcLuma.e[tid];  // 256 entries (512-thread workgroups: half)
+  actab[tid] = kHuffAcLuma.e[tid];
   if (tid < 16) dctab[tid] = tid < 12 ? kHuffDcLuma.e[tid] : 0u;
   // JpegDesc::render is -1 or img itself, so the render descriptor loads alongside the JPEG one
   // (no dependent round trip); the render window (stats of the slice) is computed where the render
@@ -293,7 +293,7 @@ __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(kOcc))) voi
       const uint16_t* src = rs.raw + rd.src_off;
       // Interior: 4-byte loads of pixel pairs, all issued before the LDS stores (one latency).
       const int nw = nrows * hw;
-      constexpr int kU = kWG == 512 ? 9 : 12;  // ≥ rows × 128 pairs / kWG threads for a 256² source: one round
+      constexpr int kU = 12;  // ≥ 18 rows × 128 pairs / 256 threads for a 256² source: one round
       uint32_t v[kU];
 #pragma unroll
       for (int t = 0; t < kU; ++t) {
@@ -797,8 +797,7 @@ void launch_jpeg(const uint8_t* canvas, const JpegDesc* jd, int ncanvas, int out
   JpegRenderSrc rs;
   if (fused) rs = *fused;
   const int bpi = (out_w / 8) * (out_h / 8);
-  const int wg = w.wg == 512 ? 512 : kJpegWG;
-  const int parts = (bpi + wg - 1) / wg;
+  const int parts = (bpi + kJpegWG - 1) / kJpegWG;
   if ((size_t)parts * ncanvas > w.look_cap) throw DeviceError("launch_jpeg: look-back capacity exceeded");
   w.look_used = (size_t)parts * ncanvas;
   // NM03_PROFILE_VARIANT=jpeg=N selects truncated profiling variants (output invalid;
@@ -823,13 +822,8 @@ void launch_jpeg(const uint8_t* canvas, const JpegDesc* jd, int ncanvas, int out
     w.look_base = w.look_base ? 0 : half;
     w.prev_words = words;
   }
-  if (wg == 512)
-    jpeg_fused_kernel<4, kUnionWords512, 512><<<parts * ncanvas, 512, 0, stream>>>(canvas, jd, ncanvas, out_w, out_h, q,
-                                                                                   w, rs, out, out_sizes, dbg);
-  else
-    jpeg_fused_kernel<4, kUnionWords, kJpegWG><<<parts * ncanvas, kJpegWG, 0, stream>>>(canvas, jd, ncanvas, out_w,
-                                                                                       out_h, q, w, rs, out,
-                                                                                       out_sizes, dbg);
+  jpeg_fused_kernel<4, kUnionWords><<<parts * ncanvas, kJpegWG, 0, stream>>>(canvas, jd, ncanvas, out_w, out_h, q, w, rs,
+                                                                         out, out_sizes, dbg);
   check_launch("jpeg_fused_kernel");
 }
 
@@ -838,7 +832,7 @@ void preload_kernels() {
   preload_sharpen();
   preload_srg();
   hipFuncAttributes a;
-  (void)hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&jpeg_fused_kernel<4, kUnionWords, kJpegWG>));
+  (void)hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&jpeg_fused_kernel<4, kUnionWords>));
 }
 
 }  // namespace nm03::gpu

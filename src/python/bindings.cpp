@@ -275,8 +275,6 @@ PYBIND11_MODULE(_nm03, m) {
       .def_readwrite("jpeg_out_cap", &EngineConfig::jpeg_out_cap)
       .def_readwrite("upload_chunk_kb", &EngineConfig::upload_chunk_kb)
       .def_readwrite("create_writers", &EngineConfig::create_writers)
-      .def_readwrite("bar_upload", &EngineConfig::bar_upload)
-      .def_readwrite("jpeg_wg", &EngineConfig::jpeg_wg)
       .def_readwrite("host_only", &EngineConfig::host_only);
 
   m.def("reference_seeds", [](int w, int h) {

@@ -2,9 +2,6 @@
 #include "nm03/engine.h"
 
 #include <hip/hip_runtime_api.h>
-#include <hsa/hsa.h>
-#include <hsa/hsa_ext_amd.h>
-#include <immintrin.h>
 #include <fcntl.h>
 #include <linux/capability.h>
 #include <signal.h>
@@ -89,10 +86,8 @@ struct Slot {
   size_t max_medt = 0, max_shpt = 0;
   uint8_t* h_blob = nullptr;
   // Where the loaders write the batch's raw pixels: h_blob + raw_base (pinned host memory, uploaded by
-  // SDMA), or with EngineConfig::bar_upload the device blob's raw region itself through the GPU's
-  // large BAR (CPU write-combining stores into VRAM; no upload copy, no host DRAM pass).
+  // SDMA; host-only engines: anonymous memory).
   uint8_t* raw_cpu = nullptr;
-  volatile uint32_t* hdp_flush = nullptr;  // HDP_MEM_COHERENCY_FLUSH_CNTL (bar_upload)
   uint8_t* h_single = nullptr;  // run_single's pinned read-back area (allocated on first use)
   size_t single_bytes = 0;
   uint8_t* d_blob = nullptr;
@@ -238,7 +233,6 @@ struct Engine::Impl {
   // Host-mapped bytes per image for the GPU encoder's stuffed output (EngineConfig::jpeg_out_cap).
   uint32_t out_cap_ = 0;
   bool host_only_ = false;  // EngineConfig::host_only
-  bool bar_ = false;        // EngineConfig::bar_upload
   // Host-only: the entropy-coded segments standing in for the GPU encoder's output (original,
   // processed) — the golden export of a phantom slice, so sizes match a real run.
   std::vector<uint8_t> tmpl_[2];
@@ -250,13 +244,11 @@ struct Engine::Impl {
     out_cap_ = (out_cap_ + 15u) & ~15u;  // 16-byte aligned segments (the encoder's dwordx4 stores)
     upload_chunk_ = cfg.upload_chunk_kb < 0 ? (size_t)2 << 20 : (size_t)cfg.upload_chunk_kb << 10;
     host_only_ = cfg.host_only;
-    bar_ = cfg.bar_upload && !host_only_;
-    if (host_only_ || bar_) upload_chunk_ = 0;  // nothing to upload (bar: the loaders write VRAM)
+    if (host_only_) upload_chunk_ = 0;  // nothing to upload
     if (cfg.batch_size < 1) cfg.batch_size = 1;
     if (cfg.streams < 1) cfg.streams = 1;
     if (cfg.max_dim < 16) cfg.max_dim = 16;
     if (cfg.max_dim > kMaxSliceDim) throw DeviceError("max_dim above " + std::to_string(kMaxSliceDim) + " not supported");
-    if (cfg.jpeg_wg != 256 && cfg.jpeg_wg != 512) throw DeviceError("jpeg_wg must be 256 or 512");
     const auto& p = cfg.pipe;
     if (p.median_window != 3 && p.median_window != 5 && p.median_window != 7 && p.median_window != 9)
       throw DeviceError("median window must be 3, 5, 7 or 9");
@@ -371,25 +363,6 @@ struct Engine::Impl {
     }
   }
 
-  // bar_upload: lets the CPU agent access a device allocation through the large BAR (the coarse
-  // VRAM pool is "disallowed by default" for the CPU on MI355X, tools/bar_probe.cpp).
-  static void grant_cpu_access(void* p) {
-    hsa_agent_t cpu{};
-    bool found = false;
-    auto cb = [](hsa_agent_t a, void* data) -> hsa_status_t {
-      hsa_device_type_t t;
-      if (hsa_agent_get_info(a, HSA_AGENT_INFO_DEVICE, &t) == HSA_STATUS_SUCCESS && t == HSA_DEVICE_TYPE_CPU) {
-        *static_cast<hsa_agent_t*>(data) = a;
-        return HSA_STATUS_INFO_BREAK;
-      }
-      return HSA_STATUS_SUCCESS;
-    };
-    const hsa_status_t it = hsa_iterate_agents(cb, &cpu);
-    found = it == HSA_STATUS_INFO_BREAK;
-    if (!found || hsa_amd_agents_allow_access(1, &cpu, nullptr, p) != HSA_STATUS_SUCCESS)
-      throw DeviceError("bar_upload: the CPU cannot be granted access to device memory (no large BAR?)");
-  }
-
   std::unique_ptr<Slot> make_slot() {
     auto sp = std::make_unique<Slot>();
     Slot& s = *sp;
@@ -450,14 +423,6 @@ struct Engine::Impl {
       // +64 B tail slack: the median's packed-group loads read whole dwords (k1_median.hip).
       s.d_blob = dmalloc<uint8_t>(s.blob_bytes + 64, "hipMalloc blob");
       s.raw_cpu = s.h_blob + s.raw_base;
-      if (bar_) {
-        grant_cpu_access(s.d_blob);
-        s.raw_cpu = s.d_blob + s.raw_base;
-        hipDeviceProp_t prop{};
-        check_hip(hipGetDeviceProperties(&prop, cfg.device), "hipGetDeviceProperties");
-        if (!prop.hdpMemFlushCntl) throw DeviceError("bar_upload: no HDP flush register");
-        s.hdp_flush = prop.hdpMemFlushCntl;
-      }
       s.d_raw_x = dmalloc<uint16_t>(s.cap_pixels, "hipMalloc raw");
       s.d_med = dmalloc<uint16_t>(s.cap_pixels, "hipMalloc median");
       s.d_tile_mm = dmalloc<uint32_t>(2 * s.max_medt, "hipMalloc tile ranges");
@@ -473,7 +438,6 @@ struct Engine::Impl {
       s.jw.look = dmalloc<uint64_t>(6 * s.jw.look_cap, "hipMalloc look-back");
       check_hip(hipMemset(s.jw.look, 0, 6 * s.jw.look_cap * sizeof(uint64_t)), "memset look-back");
       s.jw.ticket = dmalloc<uint32_t>(s.cap_canvases, "hipMalloc tickets");
-      s.jw.wg = cfg.jpeg_wg == 512 ? 512 : 256;
       s.jw.spill = dmalloc<uint32_t>(s.jw.look_cap * 256 * 56, "hipMalloc jpeg spill");
       check_hip(hipMemset(s.jw.ticket, 0, sizeof(uint32_t) * s.cap_canvases), "memset tickets");
       const size_t out_bytes = (size_t)out_cap_ * s.cap_canvases;
@@ -683,7 +647,6 @@ struct Engine::Impl {
               file.pixels16(dst);
             }
           }
-          if (bar_) _mm_sfence();  // write-combining stores into VRAM: complete before the slot launches
         } catch (...) {
           if (reserved) s.allocs[idx].done.store(true, std::memory_order_release);  // space stays unused
           throw;
@@ -872,14 +835,7 @@ struct Engine::Impl {
     const bool inline_up = s.uploaded == 0 && !s.upload_started && nl <= 16;
     hipStream_t up = inline_up ? s.stream : s.up;
     if (!s.upload_started && !inline_up) check_hip(hipEventRecord(s.ev0, up), "event");
-    if (bar_) {
-      // The pixels are in VRAM already (loader stores through the BAR, each fenced): flush the HDP
-      // write path so the kernels see them, then only the tables go up.
-      _mm_sfence();
-      *s.hdp_flush = 1u;
-      (void)*s.hdp_flush;
-      check_hip(hipMemcpyAsync(s.d_blob, s.h_blob, s.raw_base, hipMemcpyHostToDevice, up), "H2D tables");
-    } else if (s.uploaded == 0) {
+    if (s.uploaded == 0) {
       check_hip(hipMemcpyAsync(s.d_blob, s.h_blob, s.raw_base + raw_end * 2, hipMemcpyHostToDevice, up),
                 "H2D tables + pixels");
     } else {
@@ -1337,7 +1293,6 @@ struct Engine::Impl {
     L.blob_off = 0;
     L.packed = false;
     std::memcpy(s.raw_cpu, in.raw.data(), in.raw.size() * sizeof(uint16_t));
-    if (bar_) _mm_sfence();
     s.live.assign(1, 0);
     build_and_run(s, 1, nullptr);
     SingleResult r;

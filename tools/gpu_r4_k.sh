@@ -8,6 +8,7 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"; export TMPDIR=/tmp; O=gpurun_out/r4k; mkdir -p $O
 B=build/bin
+timeout -k 10 400 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -p no:cacheprovider > $O/pytest_gpu.log 2>&1 || exit 4
 T=/tmp/r4k_vol
 $B/nm03_synth --data-root $T/ --patients 1 --min-slices 256 --max-slices 256 --threads 16 > /dev/null || exit 5
 timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $O/c5 -o c5 \
