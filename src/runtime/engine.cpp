@@ -309,8 +309,9 @@ struct Engine::Impl {
     slots.resize((size_t)cfg.streams);
     place.run_bound([&] {
       const double ts = now_s();
-      slots[0] = make_slot();
-      slot_ms = std::to_string((int)((now_s() - ts) * 1e4) / 10.0).substr(0, 5);
+      std::string split;
+      slots[0] = make_slot(&split);
+      slot_ms = std::to_string((int)((now_s() - ts) * 1e4) / 10.0).substr(0, 5) + " (" + split + ")";
     });
     const double t3 = now_s();
     building_ = (int)slots.size() - 1;
@@ -363,7 +364,15 @@ struct Engine::Impl {
     }
   }
 
-  std::unique_ptr<Slot> make_slot() {
+  // `split` (optional): milliseconds per allocation phase, for the start-up log.
+  std::unique_ptr<Slot> make_slot(std::string* split = nullptr) {
+    double tm = now_s();
+    auto mark = [&](const char* what) {
+      if (!split) return;
+      const double t = now_s();
+      *split += (split->empty() ? "" : ", ") + std::string(what) + " " + std::to_string((int)((t - tm) * 1e4) / 10.0).substr(0, 4);
+      tm = t;
+    };
     auto sp = std::make_unique<Slot>();
     Slot& s = *sp;
     const int B = cfg.batch_size;
@@ -415,11 +424,14 @@ struct Engine::Impl {
     try {
       check_hip(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking), "hipStreamCreate");
       s.up = upload_stream();
+      mark("streams");
       check_hip(hipEventCreate(&s.ev0), "hipEventCreate");
       check_hip(hipEventCreate(&s.ev1), "hipEventCreate");
       // Batch completion is polled by the slot thread (wait_batch): no blocking-sync event.
       check_hip(hipEventCreateWithFlags(&s.ev2, hipEventDefault), "hipEventCreate");
+      mark("events");
       check_hip(hipHostMalloc((void**)&s.h_blob, s.blob_bytes, hipHostMallocDefault), "hipHostMalloc blob");
+      mark("pinned blob");
       // +64 B tail slack: the median's packed-group loads read whole dwords (k1_median.hip).
       s.d_blob = dmalloc<uint8_t>(s.blob_bytes + 64, "hipMalloc blob");
       s.raw_cpu = s.h_blob + s.raw_base;
@@ -436,16 +448,19 @@ struct Engine::Impl {
       s.d_canvas = dmalloc<uint8_t>(canvas_bytes * s.cap_canvases, "hipMalloc canvas");
       s.jw.look_cap = (size_t)s.cap_canvases * ((blocks + 255) / 256);
       s.jw.look = dmalloc<uint64_t>(6 * s.jw.look_cap, "hipMalloc look-back");
+      mark("device buffers");
       check_hip(hipMemset(s.jw.look, 0, 6 * s.jw.look_cap * sizeof(uint64_t)), "memset look-back");
       s.jw.ticket = dmalloc<uint32_t>(s.cap_canvases, "hipMalloc tickets");
       s.jw.spill = dmalloc<uint32_t>(s.jw.look_cap * 256 * 56, "hipMalloc jpeg spill");
       check_hip(hipMemset(s.jw.ticket, 0, sizeof(uint32_t) * s.cap_canvases), "memset tickets");
+      mark("memsets");
       const size_t out_bytes = (size_t)out_cap_ * s.cap_canvases;
       check_hip(hipHostMalloc((void**)&s.h_out, out_bytes, hipHostMallocMapped), "hipHostMalloc out");
       check_hip(hipHostGetDevicePointer((void**)&s.d_out, s.h_out, 0), "hipHostGetDevicePointer out");
       check_hip(hipHostMalloc((void**)&s.h_sizes, sizeof(int32_t) * s.cap_canvases, hipHostMallocMapped),
                 "hipHostMalloc sizes");
       check_hip(hipHostGetDevicePointer((void**)&s.d_sizes, s.h_sizes, 0), "hipHostGetDevicePointer sizes");
+      mark("mapped out");
     } catch (...) {
       hip_free_all(s);
       throw;

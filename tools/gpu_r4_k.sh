@@ -18,7 +18,12 @@ rm -rf $T
 grep -q "exit 0 csv 1" $O/c5_prof_status.txt || exit 6
 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O/bench -o k \
   -- python3 bench.py --steps 20 --warmup 3 --single-passes 0 --cli-runs 0 --wipe-passes 0 > $O/bench.json 2> $O/bench.err || exit 7
-rm -rf /dev/shm/nm03_bench_data*
+DD=/dev/shm/nm03_bench_data-node0; [ -d $DD ] || DD=$(ls -d /dev/shm/nm03_bench_data* | head -1)
+for i in 1 2 3; do  # cold CLI start-up detail (engine set-up split in the info log)
+  NM03_LOG=info timeout -k 10 60 $B/img_processing_parallel --gpus 1 --data-root $DD/ --out /dev/shm/r4k_cli --quiet \
+    --json $O/cli_$i.json > $O/cli_$i.log 2>&1 || exit 8
+done
+rm -rf /dev/shm/nm03_bench_data* /dev/shm/r4k_cli
 D=/tmp/r4k_data
 $B/nm03_synth --data-root $D/ --threads 16 > /dev/null || exit 11
 C="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY SQ_BUSY_CYCLES"
