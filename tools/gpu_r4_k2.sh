@@ -1,23 +1,14 @@
 #!/bin/bash
-# (gpurun) Round 4: JPEG encoder instruction mix per phase. For each truncation variant
+# (gpurun) Round 4 (second half of tools/gpu_r4_k.sh, whose bench run had dropped its data): JPEG encoder instruction mix per phase. For each truncation variant
 # (NM03_PROFILE_VARIANT=jpeg=N: 7 tables+ticket, 1 +render, 16 +FDCT+quant, 2 +AC coding,
 # 4 +scan/bit range/look-back, 0 full; 40/41 gray/label only) one rocprofv3 --pmc pass of SQ
 # counters over the isolated encoder (1 stream, batch 96). Before that: config 5 (256-slice volume)
 # under rocprofv3 --kernel-trace (exit status and CSV written), and the headline bench's kernel stats.
 # gpurun_out/r4k/.
 set -o pipefail
-cd "$GRAFT_REPO_ROOT"; export TMPDIR=/tmp; O=gpurun_out/r4k; mkdir -p $O
+cd "$GRAFT_REPO_ROOT"; export TMPDIR=/tmp; O=gpurun_out/r4k2; mkdir -p $O
 B=build/bin
-timeout -k 10 400 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -p no:cacheprovider > $O/pytest_gpu.log 2>&1 || exit 4
-T=/tmp/r4k_vol
-$B/nm03_synth --data-root $T/ --patients 1 --min-slices 256 --max-slices 256 --threads 16 > /dev/null || exit 5
-timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $O/c5 -o c5 \
-  -- $B/nm03_bench --config volume --data-root $T/ --steps 10 --warmup 2 > $O/c5_prof.json 2> $O/c5_prof.err
-echo "profiled config 5 exit $? csv $(ls $O/c5/*kernel_stats.csv 2>/dev/null | wc -l)" > $O/c5_prof_status.txt
-rm -rf $T
-grep -q "exit 0 csv 1" $O/c5_prof_status.txt || exit 6
-timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O/bench -o k \
-  -- python3 bench.py --steps 20 --warmup 3 --single-passes 0 --cli-runs 0 --wipe-passes 0 --keep-data > $O/bench.json 2> $O/bench.err || exit 7
+timeout -k 10 200 python3 bench.py --steps 10 --warmup 2 --single-passes 0 --cli-runs 0 --wipe-passes 0 --keep-data > $O/bench.json 2> $O/bench.err || exit 7
 DD=/dev/shm/nm03_bench_data-node0; [ -d $DD ] || DD=$(ls -d /dev/shm/nm03_bench_data* | head -1)
 for i in 1 2 3; do  # cold CLI start-up detail (engine set-up split in the info log)
   NM03_LOG=info timeout -k 10 60 $B/img_processing_parallel --gpus 1 --data-root $DD/ --out /dev/shm/r4k_cli --quiet \
