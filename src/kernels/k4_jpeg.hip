@@ -51,6 +51,17 @@ __device__ __forceinline__ int16_t quant_recip(int32_t x, const QuantRecip& q, i
   return (int16_t)(x < 0 ? -v : v);
 }
 
+// i / d for 0 ≤ i < 2^16 and 1 ≤ d < 2^16 as one multiply-high by m = ceil(2^32 / d): with
+// e = m·d − 2^32 < d, i·m / 2^32 = i/d + i·e / (d·2^32), and the error term stays below
+// 2^-16 ≤ 1/d, so it never carries i/d past the next integer. The divisors here (staged row
+// widths, MCUs per row) are workgroup-uniform: m is computed once instead of the compiler's
+// ≈10-instruction float-reciprocal division per use (24 per thread in the gray staging alone).
+struct Div16 {
+  uint32_t d, m;
+  __device__ __forceinline__ explicit Div16(uint32_t dv) : d(dv), m(dv > 1u ? 0xFFFFFFFFu / dv + 1u : 0u) {}
+  __device__ __forceinline__ uint32_t q(uint32_t i) const { return d > 1u ? __umulhi(i, m) : i; }
+};
+
 __device__ __forceinline__ int wave_sum_i32(int v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -239,6 +250,7 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(kOcc)))
     return;
   }
   const int mcux = out_w >> 4;
+  const Div16 dmx((uint32_t)mcux);
   const int b = part * kWG + tid;
   const bool valid = b < bpi;
   // ---- 0. stage the source rows of this workgroup in LDS (workgroup-uniform decision) ----------
@@ -262,9 +274,10 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(kOcc)))
       ys0 = 8 * r0;
       pcols = nw;  // offset of the border plane
       const int wrem = rd.src_w & 63;
+      const Div16 dw((uint32_t)wpr);
       int nonzero = 0, nonfill = 0;
       for (int i = tid; i < nw; i += kWG) {
-        const int j = i / wpr, k = i - j * wpr;
+        const int j = (int)dw.q((uint32_t)i), k = i - j * wpr;
         const size_t wi = (size_t)clampi(ys0 + j, 0, rd.src_h - 1) * wpr + k;
         const uint64_t lab = rs.bits[rd.src_off + wi], brd = rs.bits[rd.border_off + wi];
         slab[i] = lab;
@@ -293,6 +306,7 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(kOcc)))
       const uint16_t* src = rs.raw + rd.src_off;
       // Interior: 4-byte loads of pixel pairs, all issued before the LDS stores (one latency).
       const int nw = nrows * hw;
+      const Div16 dh((uint32_t)hw);
       constexpr int kU = 12;  // ≥ 18 rows × 128 pairs / 256 threads for a 256² source: one round
       uint32_t v[kU];
 #pragma unroll
@@ -300,7 +314,7 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(kOcc)))
         const int i = tid + t * kWG;
         v[t] = 0u;
         if (i < nw) {
-          const int j = i / hw, k = i - j * hw;
+          const int j = (int)dh.q((uint32_t)i), k = i - j * hw;
           v[t] = *reinterpret_cast<const uint32_t*>(src + (size_t)clampi(ys0 + j, 0, H - 1) * W + 2 * k);
         }
       }
@@ -311,13 +325,13 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(kOcc)))
       for (int t = 0; t < kU; ++t) {
         const int i = tid + t * kWG;
         if (i < nw) {
-          const int j = i / hw, k = i - j * hw;
+          const int j = (int)dh.q((uint32_t)i), k = i - j * hw;
           spatch[j * pcols + swz_col(2 * k + 1)] = value((uint16_t)(v[t] & 0xFFFFu));
           spatch[j * pcols + swz_col(2 * k + 2)] = value((uint16_t)(v[t] >> 16));
         }
       }
       for (int i = tid + kU * kWG; i < nw; i += kWG) {  // larger footprints
-        const int j = i / hw, k = i - j * hw;
+        const int j = (int)dh.q((uint32_t)i), k = i - j * hw;
         const uint32_t u = *reinterpret_cast<const uint32_t*>(src + (size_t)clampi(ys0 + j, 0, H - 1) * W + 2 * k);
         spatch[j * pcols + swz_col(2 * k + 1)] = value((uint16_t)(u & 0xFFFFu));
         spatch[j * pcols + swz_col(2 * k + 2)] = value((uint16_t)(u >> 16));
@@ -345,7 +359,8 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(kOcc)))
     dc0 = quant_recip(64 * (flat_v - 128), q, 0);
   } else if (valid) {
     const int mcu = b >> 2, sub = b & 3;
-    const int bx = 2 * (mcu % mcux) + (sub & 1), by = 2 * (mcu / mcux) + (sub >> 1);
+    const int my = (int)dmx.q((uint32_t)mcu), mx = mcu - my * mcux;
+    const int bx = 2 * mx + (sub & 1), by = 2 * my + (sub >> 1);
     int32_t blk[64];
     // Label images are mostly background: when every block of the wave is one flat colour (76% of
     // the phantom cohort's label waves, 97.5% of its blocks) the islow FDCT of a constant block is
@@ -473,8 +488,9 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(kOcc)))
     if (part > 0 && dbg != 17) {  // dbg 17: profiling variant without the predecessor's DC (output invalid)
       const int pb = part * kWG - 1;
       const int mcu = pb >> 2, sub = pb & 3;
-      const int u = 8 * (2 * (mcu % mcux) + (sub & 1)) + (tid & 7);
-      const int v = 8 * (2 * (mcu / mcux) + (sub >> 1)) + (tid >> 3);
+      const int my = (int)dmx.q((uint32_t)mcu), mx = mcu - my * mcux;
+      const int u = 8 * (2 * mx + (sub & 1)) + (tid & 7);
+      const int v = 8 * (2 * my + (sub >> 1)) + (tid >> 3);
       const int px = d.render >= 0 ? (int)render_pixel(rd, rs.raw, rs.f32, rs.bits, win, u, v)
                                    : (int)canvas[d.canvas_off + (size_t)v * out_w + u];
       dcp = quant_recip(wave_sum_i32(px - 128), q, 0);
