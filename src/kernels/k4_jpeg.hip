@@ -318,23 +318,34 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(kOcc)))
           v[t] = *reinterpret_cast<const uint32_t*>(src + (size_t)clampi(ys0 + j, 0, H - 1) * W + 2 * k);
         }
       }
-      auto value = [&](uint16_t r) {
-        return rescaled_value(key_from_raw(r, rd.type, rd.stored_bits), rd.type, rd.slope, rd.intercept);
+      // rescaled_value(key_from_raw(r)) per staged pixel (pixel_math.h), as one bit-field extract:
+      // the key's value is the low stored_bits bits of the sample, sign-extended for signed data
+      // (v_bfe_i32 / v_bfe_u32 + one conversion); the rescale only when the image has one. Both
+      // choices are workgroup-uniform branches instead of per-pixel selects over both paths.
+      const bool sgn = rd.type == kI16, affine = rd.slope != 1.0f || rd.intercept != 0.0f;
+      const uint32_t sbits = rd.stored_bits;
+      auto value = [&](uint32_t r) {
+        float x = sgn ? (float)__builtin_amdgcn_sbfe((int)r, 0u, sbits) : (float)__builtin_amdgcn_ubfe(r, 0u, sbits);
+        if (affine) {
+          const float t = x * rd.slope;
+          x = t + rd.intercept;
+        }
+        return x;
       };
 #pragma unroll
       for (int t = 0; t < kU; ++t) {
         const int i = tid + t * kWG;
         if (i < nw) {
           const int j = (int)dh.q((uint32_t)i), k = i - j * hw;
-          spatch[j * pcols + swz_col(2 * k + 1)] = value((uint16_t)(v[t] & 0xFFFFu));
-          spatch[j * pcols + swz_col(2 * k + 2)] = value((uint16_t)(v[t] >> 16));
+          spatch[j * pcols + swz_col(2 * k + 1)] = value(v[t] & 0xFFFFu);
+          spatch[j * pcols + swz_col(2 * k + 2)] = value(v[t] >> 16);
         }
       }
       for (int i = tid + kU * kWG; i < nw; i += kWG) {  // larger footprints
         const int j = (int)dh.q((uint32_t)i), k = i - j * hw;
         const uint32_t u = *reinterpret_cast<const uint32_t*>(src + (size_t)clampi(ys0 + j, 0, H - 1) * W + 2 * k);
-        spatch[j * pcols + swz_col(2 * k + 1)] = value((uint16_t)(u & 0xFFFFu));
-        spatch[j * pcols + swz_col(2 * k + 2)] = value((uint16_t)(u >> 16));
+        spatch[j * pcols + swz_col(2 * k + 1)] = value(u & 0xFFFFu);
+        spatch[j * pcols + swz_col(2 * k + 2)] = value(u >> 16);
       }
       // Clamped halo columns 0 and W+1.
       for (int i = tid; i < 2 * nrows; i += kWG) {
