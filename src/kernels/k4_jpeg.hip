@@ -62,6 +62,12 @@ struct Div16 {
   __device__ __forceinline__ uint32_t q(uint32_t i) const { return d > 1u ? __umulhi(i, m) : i; }
 };
 
+// |quantised x| (the same quotient as quant_recip, without the sign).
+__device__ __forceinline__ uint32_t quant_mag(int32_t x, const QuantRecip& q, int n) {
+  const uint32_t a = (uint32_t)(x < 0 ? -x : x) + q.half[n];
+  return __umulhi(a, q.m[n]);
+}
+
 __device__ __forceinline__ int wave_sum_i32(int v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -435,16 +441,24 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(kOcc)))
       // instructions than the multiply/add form and no scratch spills (20 scratch instructions).
       fdct_islow_dot(blk);
       blk[0] -= 64 * 128;
-      // Quantise into packed int16 pairs first (frees the 64 int32 DCT registers), then walk the
-      // zig-zag order from those registers.
+      // Quantise into packed pairs first (frees the 64 int32 DCT registers), then walk the zig-zag
+      // order from those registers. Sign-magnitude halves: |q| in bits 0–14 (16–30), the
+      // coefficient's sign in bit 15 (31) — the coder needs |q| for the category and the sign only
+      // to complement the magnitude bits, so the quotient is never negated back (|q| < 2^14: the
+      // islow coefficients of 8-bit samples stay below 2^15 and every divisor is ≥ 2). Per pair:
+      // 2 × (abs, add, mul_hi) + one byte permute for the signs + one bit-field insert.
       uint32_t zp[32];
 #pragma unroll
       for (int k = 0; k < 64; k += 2) {
-        const int16_t a = quant_recip(blk[kNatural[k]], q, kNatural[k]);
-        const int16_t c = quant_recip(blk[kNatural[k + 1]], q, kNatural[k + 1]);
-        zp[k >> 1] = (uint32_t)(uint16_t)a | ((uint32_t)(uint16_t)c << 16);
+        const int32_t xa = blk[kNatural[k]], xc = blk[kNatural[k + 1]];
+        const uint32_t mags = quant_mag(xa, q, kNatural[k]) | (quant_mag(xc, q, kNatural[k + 1]) << 16);
+        const uint32_t signs = ((uint32_t)xa >> 16) | ((uint32_t)xc & 0xFFFF0000u);
+        zp[k >> 1] = (mags & ~0x80008000u) | (signs & 0x80008000u);
       }
-      dc0 = (int16_t)(zp[0] & 0xFFFFu);
+      {
+        const int a0 = (int)(zp[0] & 0x7FFFu);
+        dc0 = (zp[0] & 0x8000u) ? -a0 : a0;
+      }
       if (dbg == 16) {  // profiling variant: stop after the FDCT and quantisation
         uint32_t acc = 0;
 #pragma unroll
@@ -460,17 +474,19 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(kOcc)))
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
           const int k = 2 * j + h;
-          const int v = (int16_t)(word >> (16 * h));
-          if (k > 0 && __ballot(v != 0)) {
-            if (v != 0) {
+          const uint32_t half = word >> (16 * h);
+          const uint32_t av = half & 0x7FFFu;  // |q|; bit 15 of `half`: its sign
+          if (k > 0 && __ballot(av != 0)) {
+            if (av != 0) {
               int run = k - last - 1;
               while (run > 15) {
                 lw.put_sym(actab[0xF0]);
                 run -= 16;
               }
-              const int nb = mag_bits_fast(v);
+              const int nb = 32 - __builtin_clz(av);
               const uint32_t e = actab[(run << 4) + nb];  // symbol and magnitude in one put (≤ 27 bits)
-              const uint32_t mag = (uint32_t)(v < 0 ? v - 1 : v) & ((1u << nb) - 1u);
+              // Magnitude bits: q for q > 0, q − 1 = ~|q| for q < 0 (low nb bits).
+              const uint32_t mag = (av ^ (0u - ((half >> 15) & 1u))) & ((1u << nb) - 1u);
               lw.put(((e & 0xFFFFu) << nb) | mag, (int)(e >> 16) + nb);
               last = k;
             }
