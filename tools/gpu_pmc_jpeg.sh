@@ -1,19 +1,15 @@
 #!/bin/bash
-# PMC counters of the JPEG encoder profiling variants (gpurun): VARIANTS="1 6" by default.
+# (gpurun) JPEG encoder SQ counters per truncation variant (see tools/gpu_r4_k.sh), isolated engine
+# runs (1 stream, batch 96). Usage: bash tools/gpu_pmc_jpeg.sh <out-name>
 set -o pipefail
-cd "$GRAFT_REPO_ROOT"
-export TMPDIR=/tmp
-mkdir -p gpurun_out/pmcj
-D=/tmp/nm03_pmc_data
-build/bin/nm03_synth --data-root $D/ --threads 16 > /dev/null || exit 61
-for v in ${VARIANTS:-1 6}; do
-  i=0
-  for grp in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD" "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU" "SQ_WAIT_ANY SQ_INSTS_SMEM SQ_INSTS_LDS SQ_WAIT_INST_LDS"; do
-    i=$((i+1))
-    NM03_JPEG_DBG=$v timeout -k 10 180 rocprofv3 --pmc $grp --output-format csv -d gpurun_out/pmcj/v$v/p$i -o run \
-      -- build/bin/nm03_bench --config cohort --data-root $D/ --steps 1 --warmup 1 --batch-size 64 --streams 1 \
-      > gpurun_out/pmcj/v$v.p$i.log 2>&1 || exit $((70+i))
-  done
-  echo "== variant $v" >> gpurun_out/pmcj/summary.txt
-  python3 tools/pmc_summary.py gpurun_out/pmcj/v$v | grep -A16 jpeg_fused >> gpurun_out/pmcj/summary.txt
+cd "$GRAFT_REPO_ROOT"; export TMPDIR=/tmp; O=gpurun_out/${1:-pmc}; mkdir -p $O
+B=build/bin
+D=/tmp/pmc_data
+$B/nm03_synth --data-root $D/ --threads 16 > /dev/null || exit 11
+C="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY SQ_BUSY_CYCLES"
+for v in 7 1 16 2 4 0 40 41; do
+  NM03_PROFILE_VARIANT=jpeg=$v timeout -s KILL 90 rocprofv3 --pmc $C --output-format csv -d $O/v$v -o k \
+    -- $B/nm03_bench --config cohort --data-root $D/ --steps 2 --warmup 1 --streams 1 --batch-size 96 \
+    > $O/v$v.log 2>&1 || exit 12
 done
+rm -rf $D

@@ -1,67 +1,41 @@
 #!/usr/bin/env python3
-"""Aggregate rocprofv3 --pmc counter_collection.csv files per kernel (sum over dispatches).
-
-    pmc_summary.py <pmc dir> [kernel_stats.csv]
-
-With a kernel_stats.csv from a --kernel-trace --stats run of the same workload, derived rates are
-printed too: HBM/L2 bytes per dispatch and achieved bandwidth (FETCH_SIZE / WRITE_SIZE are in KiB),
-VALU and LDS activity per wave-cycle, and LDS bank-conflict cycles per LDS instruction.
-"""
+"""Summarise tools/gpu_pmc_jpeg.sh output: per-wave SQ counters of the JPEG encoder per truncation
+variant, and of every kernel in the full pipeline (variant 0). VALU-active / wave-cycles × resident
+waves per SIMD (4 for the encoder) approximates how busy the SIMDs' VALUs are.
+Usage: python tools/pmc_summary.py gpurun_out/<name>"""
 import collections
 import csv
-import glob
 import os
 import sys
 
-
-def _short(name):
-    return name.split("(")[0].replace("void ", "").replace("nm03::gpu::", "")
-
-
-def load_stats(path):
-    out = {}
-    if path and os.path.exists(path):
-        for r in csv.DictReader(open(path, newline="")):
-            out[_short(r["Name"])] = (int(r["Calls"]), float(r["AverageNs"]))
-    return out
-
-
-def main(d, stats_path=None):
-    agg = collections.defaultdict(lambda: collections.defaultdict(float))
-    disp = collections.defaultdict(lambda: collections.defaultdict(set))
-    for path in sorted(glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)):
-        for r in csv.DictReader(open(path, newline="")):
-            k = _short(r["Kernel_Name"])
-            agg[k][r["Counter_Name"]] += float(r["Counter_Value"])
-            disp[k][r["Counter_Name"]].add((path, r.get("Dispatch_Id")))
-    stats = load_stats(stats_path)
-    for k, c in sorted(agg.items()):
-        print(k)
-        waves = c.get("SQ_WAVES", 0)
-        for name, v in sorted(c.items()):
-            extra = f"   per-wave {v / waves:10.1f}" if waves and name.startswith("SQ_INSTS") else ""
-            print(f"   {name:24s} {v:16.0f}{extra}")
-        if c.get("SQ_WAVE_CYCLES"):
-            wc = c["SQ_WAVE_CYCLES"]
-            if c.get("SQ_ACTIVE_INST_VALU"):
-                print(f"   VALU active / wave-cycles = {c['SQ_ACTIVE_INST_VALU'] / wc:.3f}")
-            if c.get("SQ_ACTIVE_INST_LDS"):
-                print(f"   LDS active / wave-cycles  = {c['SQ_ACTIVE_INST_LDS'] / wc:.3f}")
-            if c.get("SQ_WAIT_INST_ANY"):
-                print(f"   waiting / wave-cycles     = {c['SQ_WAIT_INST_ANY'] / wc:.3f}")
-        if c.get("SQ_INSTS_LDS") and "SQ_LDS_BANK_CONFLICT" in c:
-            print(f"   LDS bank-conflict cycles per LDS inst = {c['SQ_LDS_BANK_CONFLICT'] / c['SQ_INSTS_LDS']:.3f}")
-        st = stats.get(k)
-        for cn, label in (("FETCH_SIZE", "read"), ("WRITE_SIZE", "written")):
-            if cn in c and disp[k][cn]:
-                per = c[cn] * 1024.0 / len(disp[k][cn])
-                line = f"   bytes {label} per dispatch = {per / 1e6:8.3f} MB"
-                if st:
-                    line += f"   -> {per / st[1]:7.1f} GB/s at the isolated {st[1] / 1e3:.1f} us"
-                print(line)
-        if st:
-            print(f"   isolated duration: {st[1] / 1e3:.1f} us avg over {st[0]} calls")
-
-
-if __name__ == "__main__":
-    main(sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc", sys.argv[2] if len(sys.argv) > 2 else None)
+d = sys.argv[1]
+names = {7: "tables + ticket", 1: "+ render / staging", 16: "+ FDCT + quantisation", 2: "+ AC coding",
+         4: "+ DC, scan, bit range, look-back", 0: "full encoder", 40: "gray images only", 41: "label images only"}
+print("JPEG encoder, per-wave averages over all dispatches (isolated engine runs, 1 stream, batch 96)")
+print(f"{'variant':40s} {'VALU':>6} {'SALU':>6} {'LDS':>5} {'wave-cyc':>9} {'VALU/wc':>8} {'wait/wc':>8}")
+full = {}
+for v in (7, 1, 16, 2, 4, 0, 40, 41):
+    p = os.path.join(d, f"v{v}", "k_counter_collection.csv")
+    if not os.path.exists(p):
+        continue
+    acc = collections.defaultdict(lambda: collections.defaultdict(float))
+    disp = collections.defaultdict(set)
+    for r in csv.DictReader(open(p)):
+        k = r["Kernel_Name"].split("(")[0].replace("void nm03::gpu::", "")
+        acc[k][r["Counter_Name"]] += float(r["Counter_Value"])
+        disp[k].add(r["Dispatch_Id"])
+    for k, c in acc.items():
+        w = c["SQ_WAVES"]
+        if "jpeg" in k and w:
+            print(f"jpeg={v:<3} {names[v]:32s} {c['SQ_INSTS_VALU']/w:6.0f} {c['SQ_INSTS_SALU']/w:6.0f} "
+                  f"{c['SQ_INSTS_LDS']/w:5.0f} {c['SQ_WAVE_CYCLES']/w:9.0f} "
+                  f"{c['SQ_ACTIVE_INST_VALU']/c['SQ_WAVE_CYCLES']:8.3f} {c['SQ_WAIT_INST_ANY']/c['SQ_WAVE_CYCLES']:8.3f}")
+        if v == 0:
+            full[k] = (len(disp[k]), c)
+print("\nEvery kernel of the full pipeline (variant 0):")
+for k, (n, c) in full.items():
+    w = c["SQ_WAVES"]
+    if not w:
+        continue
+    print(f"{k[:40]:40s} waves/dispatch {w/n:7.0f}  VALU/wave {c['SQ_INSTS_VALU']/w:6.0f}  SALU/wave {c['SQ_INSTS_SALU']/w:5.0f}  "
+          f"VALU/wc {c['SQ_ACTIVE_INST_VALU']/c['SQ_WAVE_CYCLES']:.3f}  wait/wc {c['SQ_WAIT_INST_ANY']/c['SQ_WAVE_CYCLES']:.3f}")
