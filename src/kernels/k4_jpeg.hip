@@ -324,14 +324,19 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(kOcc)))
           v[t] = *reinterpret_cast<const uint32_t*>(src + (size_t)clampi(ys0 + j, 0, H - 1) * W + 2 * k);
         }
       }
-      // rescaled_value(key_from_raw(r)) per staged pixel (pixel_math.h), as one bit-field extract:
-      // the key's value is the low stored_bits bits of the sample, sign-extended for signed data
-      // (v_bfe_i32 / v_bfe_u32 + one conversion); the rescale only when the image has one. Both
-      // choices are workgroup-uniform branches instead of per-pixel selects over both paths.
+      // rescaled_value(key_from_raw(r)) per staged pixel (pixel_math.h), without the key round
+      // trip: the value is the low stored_bits bits of the sample, sign-extended for signed data —
+      // one shift up and one arithmetic or logical shift down, selected as integers, then one
+      // int → f32 conversion; the rescale only when the image has one (workgroup-uniform).
+      // (Written with __builtin_amdgcn_sbfe / _ubfe and the select between the two conversions,
+      // the compiler folded both into one unsigned conversion and signed slices rendered wrong:
+      // tools/probes/bfe_probe.hip, test_engine_norm_tables_vs_golden.)
       const bool sgn = rd.type == kI16, affine = rd.slope != 1.0f || rd.intercept != 0.0f;
-      const uint32_t sbits = rd.stored_bits;
+      const uint32_t vsh = 32u - rd.stored_bits;
       auto value = [&](uint32_t r) {
-        float x = sgn ? (float)__builtin_amdgcn_sbfe((int)r, 0u, sbits) : (float)__builtin_amdgcn_ubfe(r, 0u, sbits);
+        const uint32_t up = r << vsh;
+        const int32_t xi = sgn ? (int32_t)up >> vsh : (int32_t)(up >> vsh);
+        float x = (float)xi;
         if (affine) {
           const float t = x * rd.slope;
           x = t + rd.intercept;
