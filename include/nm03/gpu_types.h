@@ -32,8 +32,14 @@ struct SliceDesc {
   uint32_t f32_off;    // f32 element offset for optional sharpened output
   uint32_t med_tile0;  // index of the slice's first median tile in the batch tile list
   uint32_t blob_off;   // u16 element offset of the slice as uploaded (engine batches: K0 expands it to raw_off)
+  // normalise+clip lookup table of the slice's (type, stored bits, rescale) — K1b reads
+  // lut[lut_off + key − lut_base] instead of evaluating norm_clip_key per staged key;
+  // lut_off == kNoLut: no table (the kernel evaluates the function).
+  uint32_t lut_off;
+  uint32_t lut_base;
 };
-static_assert(sizeof(SliceDesc) == 44, "SliceDesc layout");
+static_assert(sizeof(SliceDesc) == 52, "SliceDesc layout");
+inline constexpr uint32_t kNoLut = 0xFFFFFFFFu;
 // SliceDesc::flags
 inline constexpr uint16_t kSliceFlagPacked12 = 1;  // uploaded as 12-bit pairs (nm03/pack12.h)
 

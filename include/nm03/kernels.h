@@ -40,9 +40,10 @@ void launch_median(const uint16_t* raw, uint16_t* med, const SliceDesc* descs, c
 
 // K1b: normalise+clip of the median keys, separable Gaussian unsharp mask, SRG band test →
 // `band` bitmaps (u64 words, LSB = left-most pixel). Optionally the f32 sharpened image.
+// `lut` (optional): the engine's normalise+clip tables (SliceDesc::lut_off / lut_base).
 void launch_sharpen_band(const uint16_t* med, uint64_t* band, float* sharpened, const SliceDesc* descs,
                          const TileDesc* tiles, int ntiles, const PipeConsts& pc, SliceStats* stats,
-                         hipStream_t stream, const uint32_t* tile_mm = nullptr);
+                         hipStream_t stream, const uint32_t* tile_mm = nullptr, const float* lut = nullptr);
 
 // Bitmap planes produced by K2 (each null when not requested).
 struct SrgOutputs {

@@ -72,6 +72,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K <= 7 ? 4 
   const int yin_hi = min(y0 + kMedTileH, H), xin_hi = min(x0 + kMedTileW, W);
 
   uint32_t kmin = 0xFFFFu, kmax = 0u;
+  // Keys of the staged samples (key_from_raw, pixel_math.h) without per-pixel type selects: with
+  // u = the sample's low stored_bits bits, a signed sample's key (sign-extended, bit 15 flipped) is
+  // ((u ^ m) + 0x8000 − m) mod 2^16 with m = 2^(stored_bits − 1) — the sign-extension identity
+  // (u ^ m) − m — and an unsigned sample's key is u itself (m = c = 0). Two keys go into one pair
+  // word with a byte permute (the high garbage of the signed form dropped), and the tile's key range
+  // is kept as packed u16 minima / maxima (one v_pk_min_u16 / v_pk_max_u16 per pair).
+  const uint32_t ksb = d.stored_bits;
+  const uint32_t km = d.type == kI16 ? 1u << (ksb - 1u) : 0u, kc = d.type == kI16 ? 0x8000u - km : 0u;
+  auto key_pair = [&](uint32_t lo, uint32_t hi) -> uint32_t {
+    const uint32_t a = (__builtin_amdgcn_ubfe(lo, 0u, ksb) ^ km) + kc;
+    const uint32_t b = (__builtin_amdgcn_ubfe(hi, 0u, ksb) ^ km) + kc;
+    return __builtin_amdgcn_perm(b, a, 0x05040100u);  // (a & 0xFFFF) | (b << 16)
+  };
+  u16x2 pmin = as_u16x2(0xFFFFFFFFu), pmax = as_u16x2(0u);
   if ((W & 3) == 0 && (d.raw_off & 3) == 0 && (!from_blob || packed || (d.blob_off & 3) == 0)) {
     // Vector path: window pixels p = 0..71 are image columns x0-4+p (8-byte aligned groups of
     // 4). Pair column c holds window pixels c+4-R (low half) and c+36-R (high half), so a task
@@ -139,13 +153,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K <= 7 ? 4 
       for (int q = 0; q < 4; ++q) {
         const int c = 4 * gi + q - (4 - R);
         if (c < 0 || c >= PW) continue;
-        const uint32_t kl = key_from_raw(px[0][q], d.type, d.stored_bits);
-        const uint32_t kh = key_from_raw(px[1][q], d.type, d.stored_bits);
-        P[r * PS + c] = kl | (kh << 16);
-        kmin = min(kmin, min(kl, kh));
-        kmax = max(kmax, max(kl, kh));
+        const uint32_t kp = key_pair(px[0][q], px[1][q]);
+        P[r * PS + c] = kp;
+        pmin = vmin(pmin, as_u16x2(kp));
+        pmax = vmax(pmax, as_u16x2(kp));
       }
     }
+    kmin = min((uint32_t)pmin.x, (uint32_t)pmin.y);
+    kmax = max((uint32_t)pmax.x, (uint32_t)pmax.y);
   } else {
     for (int i = threadIdx.x; i < PR * PW; i += 256) {
       const int r = i / PW, c = i - r * PW;

@@ -17,6 +17,8 @@
 // golden model.
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "device_util.h"
 #include "nm03/gpu_types.h"
 #include "nm03/kernels.h"
@@ -46,7 +48,8 @@ __global__ __launch_bounds__(256) void sharpen_band_kernel(const uint16_t* __res
                                                            float* __restrict__ sharpened,
                                                            const SliceDesc* __restrict__ descs,
                                                            const TileDesc* __restrict__ tiles, PipeConsts pc,
-                                                           SliceStats* stats, const uint32_t* __restrict__ tile_mm) {
+                                                           SliceStats* stats, const uint32_t* __restrict__ tile_mm,
+                                                           const float* __restrict__ lut) {
   constexpr int TW = kShpTileW, TH = kShpTileH;
   constexpr int CW = TW + 2 * R, CH = TH + 2 * R;
   constexpr int CS = CW % 4 == 0 ? CW + 2 : CW;  // LDS row stride ≡ 2 (mod 4)
@@ -132,6 +135,16 @@ __global__ __launch_bounds__(256) void sharpen_band_kernel(const uint16_t* __res
     // banks: a ds_write_b64 is served 16 lanes at a time, bank (a/4) mod 32; lanes 0–7 write pair
     // h at dwords 4g + 2h, lanes 8–15 pair 1 − h at 4(g + 8) + 2(1 − h) ≡ the other 16 banks.
     const int rot = (threadIdx.x >> 3) & 3;
+    // Key → normalised+clipped value: the slice's lookup table (one gather from an L1/L2-resident
+    // table built on the host from the same norm_clip_key) or the function itself — its IEEE
+    // division alone is ≈13 VALU per key. The choice is workgroup-uniform: two copies of the loop.
+    auto stage = [&](auto use_lut) {
+    constexpr bool kLut = decltype(use_lut)::value;
+    const uint32_t toff = d.lut_off, tbase = d.lut_base;
+    auto conv = [&](uint16_t key) -> float {
+      if constexpr (kLut) return lut[toff + ((uint32_t)key - tbase)];  // key ≥ lut_base (its key range)
+      else return norm_clip_key(key, d.type, nc);
+    };
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
       const int i = threadIdx.x + 256 * t;
@@ -148,7 +161,7 @@ __global__ __launch_bounds__(256) void sharpen_band_kernel(const uint16_t* __res
         for (int j = 0; j < 2; ++j) {
           const int h = (j + rot) & 1;
           const int c = 4 * g + 2 * h - OFS;
-          const f32x2 kv{norm_clip_key(h ? px[2] : px[0], d.type, nc), norm_clip_key(h ? px[3] : px[1], d.type, nc)};
+          const f32x2 kv{conv(h ? px[2] : px[0]), conv(h ? px[3] : px[1])};
           if (c >= 0 && c < CW) lds_store_pair(C + r * CS + c, kv);
         }
       } else {
@@ -157,10 +170,13 @@ __global__ __launch_bounds__(256) void sharpen_band_kernel(const uint16_t* __res
           const int q = (j + rot) & 3;
           const uint16_t key = q == 0 ? px[0] : q == 1 ? px[1] : q == 2 ? px[2] : px[3];  // selects, no scratch
           const int c = 4 * g + q - OFS;
-          if (c >= 0 && c < CW) C[r * CS + c] = norm_clip_key(key, d.type, nc);
+          if (c >= 0 && c < CW) C[r * CS + c] = conv(key);
         }
       }
     }
+    };
+    if (lut && d.lut_off != kNoLut) stage(std::true_type{});
+    else stage(std::false_type{});
   } else {
     for (int i = threadIdx.x; i < CH * CW; i += 256) {
       const int r = i / CW, c = i - r * CW;
@@ -272,11 +288,11 @@ __global__ __launch_bounds__(256) void sharpen_band_kernel(const uint16_t* __res
 
 void launch_sharpen_band(const uint16_t* med, uint64_t* band, float* sharpened, const SliceDesc* descs,
                          const TileDesc* tiles, int ntiles, const PipeConsts& pc, SliceStats* stats,
-                         hipStream_t stream, const uint32_t* tile_mm) {
+                         hipStream_t stream, const uint32_t* tile_mm, const float* lut) {
   if (ntiles <= 0) return;
 #define NM03_SHARPEN_CASE(RR)                                                                              \
   case RR:                                                                                               \
-    sharpen_band_kernel<RR><<<ntiles, 256, 0, stream>>>(med, band, sharpened, descs, tiles, pc, stats, tile_mm); \
+    sharpen_band_kernel<RR><<<ntiles, 256, 0, stream>>>(med, band, sharpened, descs, tiles, pc, stats, tile_mm, lut); \
     break;
   switch (pc.mask_radius) {
     NM03_SHARPEN_CASE(0)

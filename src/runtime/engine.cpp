@@ -22,6 +22,7 @@
 #include <deque>
 #include <unordered_map>
 #include <mutex>
+#include <tuple>
 #include <thread>
 
 #include "nm03/cohort.h"
@@ -285,6 +286,7 @@ struct Engine::Impl {
       // loads a module at the first launch of one of its kernels, from whichever slot thread gets
       // there first (a no-op when the CLI's start-up thread already did it).
       preload_kernels();
+      d_lut_ = dmalloc<float>(kLutArenaFloats, "hipMalloc norm tables");
     }
     const double t1 = now_s();
     // Host threads and pinned buffers on the GPU's socket (numa.h).
@@ -330,6 +332,72 @@ struct Engine::Impl {
     for (auto& s : slots)
       if (s) hip_free_all(*s);
     if (shared_up_) (void)hipStreamDestroy(shared_up_);
+    if (d_lut_) (void)hipFree(d_lut_);
+  }
+
+  // ---- normalise+clip lookup tables (K1b) ------------------------------------------------------
+  // norm_clip_key depends on the key and the slice's (type, stored bits, slope, intercept) only;
+  // its IEEE division is ≈13 VALU per key in the sharpen's tile load. Each distinct parameter set
+  // gets a table over its 2^stored_bits possible keys (16 KiB for 12-bit data), built once on the
+  // host with the very same function and kept in a device arena; SliceDesc::lut_off / lut_base
+  // point the kernel at it. A cohort has a handful of sets; when the arena is full (or the bit
+  // depth is unusual) a slice keeps lut_off = kNoLut and the kernel evaluates the function.
+  struct LutSet {
+    uint8_t type, bits;
+    uint32_t slope, intercept;  // bit patterns
+    uint32_t off, base;
+  };
+  static constexpr size_t kLutArenaFloats = size_t(1) << 20;  // 4 MiB
+  std::mutex lut_m_;
+  std::vector<LutSet> luts_;
+  float* d_lut_ = nullptr;  // allocated by the constructor, never moved
+  size_t lut_used_ = 0;
+  // Per-thread cache of the last set looked up, tagged with the engine's serial number (not its
+  // address, which a later engine may reuse).
+  static inline std::atomic<uint64_t> engine_serials_{0};
+  const uint64_t serial_ = ++engine_serials_;
+  static uint32_t fbits(float f) {
+    uint32_t u;
+    std::memcpy(&u, &f, 4);
+    return u;
+  }
+  // (lut_off, lut_base) for the parameter set; {kNoLut, 0} when there is no table.
+  std::pair<uint32_t, uint32_t> norm_lut(uint8_t type, uint8_t bits, float slope, float intercept) {
+    if (host_only_ || bits < 1 || bits > 16) return {kNoLut, 0u};
+    const uint32_t sl = fbits(slope), ic = fbits(intercept);
+    thread_local uint64_t last_owner = 0;
+    thread_local LutSet last{};
+    if (last_owner == serial_ && last.type == type && last.bits == bits && last.slope == sl && last.intercept == ic)
+      return {last.off, last.base};
+    std::lock_guard<std::mutex> g(lut_m_);
+    for (const LutSet& e : luts_)
+      if (e.type == type && e.bits == bits && e.slope == sl && e.intercept == ic) {
+        last_owner = serial_;
+        last = e;
+        return {e.off, e.base};
+      }
+    const uint32_t n = 1u << bits;
+    if (!d_lut_ || lut_used_ + n > kLutArenaFloats) return {kNoLut, 0u};
+    // Keys of signed data are the sign-extended samples with bit 15 flipped: 0x8000 ± 2^(bits−1).
+    const uint32_t base = type == kI16 ? 0x8000u - n / 2 : 0u;
+    NormClip nc;
+    nc.slope = slope;
+    nc.intercept = intercept;
+    nc.nmin = pc.nmin;
+    nc.nmax = pc.nmax;
+    nc.nlow = pc.nlow;
+    nc.nhigh = pc.nhigh;
+    nc.cmin = pc.cmin;
+    nc.cmax = pc.cmax;
+    std::vector<float> h(n);
+    for (uint32_t i = 0; i < n; ++i) h[i] = norm_clip_key((uint16_t)(base + i), type, nc);
+    check_hip(hipMemcpy(d_lut_ + lut_used_, h.data(), n * sizeof(float), hipMemcpyHostToDevice), "H2D norm table");
+    const LutSet e{type, bits, sl, ic, (uint32_t)lut_used_, base};
+    lut_used_ += n;
+    luts_.push_back(e);
+    last_owner = serial_;
+    last = e;
+    return {e.off, e.base};
   }
 
   // Every slot's H2D copies go through one engine-wide stream (each slot's own stream was the
@@ -736,6 +804,7 @@ struct Engine::Impl {
       d.stored_bits = L.stored_bits;
       d.slope = L.slope;
       d.intercept = L.intercept;
+      std::tie(d.lut_off, d.lut_base) = norm_lut(L.type, L.stored_bits, L.slope, L.intercept);
       d.f32_off = raw_off;
       // Seeds depend on the slice size only: reuse the last size's list (a batch is nearly always
       // one size) instead of building a vector per slice on the slot thread.
@@ -870,7 +939,7 @@ struct Engine::Impl {
     const auto* blob_raw = reinterpret_cast<const uint16_t*>(db + s.raw_base);
     launch_median(nullptr, s.d_med, d_desc, d_medt, nmed, pc.median_k, d_stats, s.stream, s.d_tile_mm, blob_raw, d_raw);
     launch_sharpen_band(s.d_med, plane(kPBand), mode == 1 ? s.d_f32 : nullptr, d_desc, d_shpt, nshp, pc, d_stats,
-                        s.stream, s.d_tile_mm);
+                        s.stream, s.d_tile_mm, d_lut_);
     SrgOutputs o;
     o.scratch = s.d_srg_scratch;
     o.dilated = plane(kPDilated);

@@ -509,6 +509,42 @@ def test_engine_mixed_blob_layouts_identical(native, cohort_root, tmp_path, monk
         assert runs[0][1][f"mixed/1-{k}_original.jpg"] == g["jpeg_original"]
 
 
+def test_engine_norm_tables_vs_golden(native, tmp_path):
+    """K1b's normalise+clip lookup tables (engine.cpp norm_lut: one per (type, stored bits, slope,
+    intercept), built on the host with norm_clip_key): one batch mixing unsigned 16/12/8-bit,
+    signed 12/16-bit and rescaled slices (six distinct tables, two slices each) gives the golden
+    model's masks and JPEGs for every slice."""
+    d = tmp_path / "mix"
+    d.mkdir()
+    specs = [("u16", 16, False, 1.0, 0.0), ("u16", 12, False, 1.0, 0.0), ("i16", 12, False, 1.0, 0.0),
+             ("i16", 16, True, 1.5, 100.0), ("u16", 16, True, 0.75, -20.0), ("u8", 8, False, 1.0, 0.0)]
+    files = []
+    for k, (ty, bits, resc, slope, icpt) in enumerate(specs * 2):
+        base = native.phantom_slice(256, 256, 2, 5 + k, 25, 11 + k).astype(np.int32)
+        if ty == "i16":
+            v = (base % (1 << bits)) - (1 << (bits - 1))
+            px = (v & 0xFFFF).astype(np.uint16)
+        elif ty == "u8":
+            px = (base >> 4).astype(np.uint16) & 0xFF
+        else:
+            px = (base & ((1 << bits) - 1)).astype(np.uint16)
+        f = d / f"1-{k + 1}.dcm"
+        f.write_bytes(native.dicom_bytes(px, ty, bits, resc, slope, icpt))
+        files.append(f)
+    out = tmp_path / "o"
+    out.mkdir()
+    eng = native.Engine(nm.PipelineConfig(batch_size=16, streams=1, threads=4).engine_config())
+    st, _ = eng.run([(str(f), str(out)) for f in files])
+    assert [c for c, _ in st] == [0] * len(files)
+    for f in files:
+        raw, meta = native.read_slice(str(f))
+        g = native.golden_run(raw, meta["type"], meta["stored_bits"], meta["slope"], meta["intercept"],
+                              native.PipelineParams(), native.RenderParams(), meta["spacing_x"], meta["spacing_y"])
+        stem = f.name[:-4]
+        assert (out / f"{stem}_processed.jpg").read_bytes() == g["jpeg_processed"], stem
+        assert (out / f"{stem}_original.jpg").read_bytes() == g["jpeg_original"], stem
+
+
 def test_engine_jpeg_batch_sizes_identical(native, tmp_path):
     """JPEG encoder launches of bench size (96 slices = 192 images, 16 workgroups per gray image)
     vs batches of 16, and a capacity edge: byte-identical trees on a 100-slice cohort plus flat /
