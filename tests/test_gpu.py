@@ -545,6 +545,32 @@ def test_engine_norm_tables_vs_golden(native, tmp_path):
         assert (out / f"{stem}_original.jpg").read_bytes() == g["jpeg_original"], stem
 
 
+def test_engine_norm_table_arena_full_vs_golden(native, tmp_path):
+    """More distinct 16-bit rescale sets than the table arena holds (16 tables of 2^16 keys): the
+    later slices run with lut_off = kNoLut, i.e. K1b evaluates normalise+clip itself — same masks
+    and JPEGs as the golden model either way."""
+    d = tmp_path / "many"
+    d.mkdir()
+    files = []
+    for k in range(20):
+        px = native.phantom_slice(256, 256, 3, 7 + k, 25, 31 + k).astype(np.uint16)
+        f = d / f"1-{k + 1}.dcm"
+        f.write_bytes(native.dicom_bytes(px, "u16", 16, True, 1.0 + 0.05 * k, -10.0 * k))
+        files.append(f)
+    out = tmp_path / "o"
+    out.mkdir()
+    eng = native.Engine(nm.PipelineConfig(batch_size=8, streams=2, threads=4).engine_config())
+    st, _ = eng.run([(str(f), str(out)) for f in files])
+    assert [c for c, _ in st] == [0] * len(files)
+    for f in files:
+        raw, meta = native.read_slice(str(f))
+        g = native.golden_run(raw, meta["type"], meta["stored_bits"], meta["slope"], meta["intercept"],
+                              native.PipelineParams(), native.RenderParams(), meta["spacing_x"], meta["spacing_y"])
+        stem = f.name[:-4]
+        assert (out / f"{stem}_processed.jpg").read_bytes() == g["jpeg_processed"], stem
+        assert (out / f"{stem}_original.jpg").read_bytes() == g["jpeg_original"], stem
+
+
 def test_engine_jpeg_batch_sizes_identical(native, tmp_path):
     """JPEG encoder launches of bench size (96 slices = 192 images, 16 workgroups per gray image)
     vs batches of 16, and a capacity edge: byte-identical trees on a 100-slice cohort plus flat /
