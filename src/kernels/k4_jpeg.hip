@@ -817,7 +817,9 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(kOcc)))
     for (uint32_t c = tid; c < nchunks; c += kWG) {
       const uint32_t b0 = 16u * c, lo = max(b0, phase), hi = min(b0 + 16u, phase + tot);
       if (lo == b0 && hi == b0 + 16u) {
-        *reinterpret_cast<uint4*>(dbase + b0) = *reinterpret_cast<const uint4*>(lbase + b0);
+        // Non-temporal: the bytes go to host memory over PCIe and are never read back on the GPU.
+        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+        __builtin_nontemporal_store(*reinterpret_cast<const u32x4*>(lbase + b0), reinterpret_cast<u32x4*>(dbase + b0));
       } else {
         for (uint32_t k = lo; k < hi; ++k) dbase[k] = lbase[k];
       }
