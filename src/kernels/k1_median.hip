@@ -146,8 +146,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K <= 7 ? 4 
         // Expanded-sample side output: groups 8 and 9 are taken twice (as lo and as hi); only the
         // lo copy stores them.
         const bool store = h == 0 ? gi >= 1 : (g4 >= 10 && g4 <= 16);
-        if (store && row_in && xs >= x0 && xs < xin_hi)
-          *reinterpret_cast<uint2*>(rdst + (size_t)yy * W + xs) = v;
+        if (store && row_in && xs >= x0 && xs < xin_hi) {
+          // Non-temporal: read once, by the encoder, after the sharpen and SRG kernels (29.4 → 28.7 µs
+          // per 96-slice batch, profiles/r4/median_ntstore/).
+          typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+          __builtin_nontemporal_store(u32x2{v.x, v.y}, reinterpret_cast<u32x2*>(rdst + (size_t)yy * W + xs));
+        }
       }
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
