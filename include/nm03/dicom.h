@@ -2,12 +2,17 @@
 // DICOMFileImporter with setLoadSeries(false): test_pipeline.cpp:33-42, main_sequential.cpp:175-177).
 //
 // Supported: Part-10 files (preamble + "DICM") and bare datasets; Implicit VR LE, Explicit VR LE,
-// Explicit VR BE; 8/16-bit monochrome, signed/unsigned, BitsStored masking, modality rescale,
-// PixelSpacing, undefined-length sequences. Compressed/encapsulated pixel data and deflate are
-// rejected with a SliceError (the slice is skipped like a fast::Exception in the reference).
+// Explicit VR BE, Deflated Explicit VR LE (1.2.840.10008.1.2.1.99, zlib) and RLE Lossless
+// (1.2.840.10008.1.2.5, encapsulated PackBits segments); 8/16-bit monochrome, signed/unsigned,
+// BitsStored masking, modality rescale, PixelSpacing, undefined-length sequences, MONOCHROME1
+// (inverted at import, see Header::invert), multi-frame files (frame selection, see copy_pixels16).
+// The JPEG-family encapsulated syntaxes (baseline/lossless JPEG, JPEG-LS, JPEG 2000, ...) are
+// rejected with a SliceError: the slice is skipped and counted like a fast::Exception in the
+// reference. DCMTK behind FAST would decode them; that part of parity is unpinned (no DCMTK here).
 #pragma once
 
 #include <cstdint>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -15,7 +20,10 @@
 
 namespace nm03::dicom {
 
-enum class Syntax : uint8_t { kImplicitLE, kExplicitLE, kExplicitBE };
+enum class Syntax : uint8_t { kImplicitLE, kExplicitLE, kExplicitBE, kDeflatedLE, kRleLossless };
+
+// Name of a transfer syntax as used in messages and by the Python bindings.
+const char* syntax_name(Syntax s);
 
 struct Header {
   int rows = 0, cols = 0, frames = 1;
@@ -30,8 +38,21 @@ struct Header {
   double slice_location = 0;
   std::string photometric, transfer_syntax, sop_instance_uid, series_uid, patient_id, modality;
   Syntax syntax = Syntax::kExplicitLE;
-  size_t pixel_offset = 0;  // byte offset of (7FE0,0010) value in the buffer
+  size_t pixel_offset = 0;  // byte offset of (7FE0,0010) value in the buffer (in *decoded when set)
   size_t pixel_length = 0;  // byte length of the value field
+  // PhotometricInterpretation MONOCHROME1 (minimum = white). The importer inverts such samples
+  // within the stored bits (v → ~v & (2^BitsStored − 1), i.e. 2^B − 1 − v for unsigned data, −1 − v
+  // for signed) so every stage sees MONOCHROME2 semantics (bright = high), the presentation DCMTK
+  // hands to a viewer. With the reference's fixed-range IntensityNormalization (0..10000) this is a
+  // documented choice, not a pinned FAST behaviour.
+  bool invert = false;
+  // Deflated and RLE files: the decoded bytes (inflated dataset, or every frame's samples as native
+  // little-endian words/bytes); pixel_offset and pixel_length then refer to this buffer.
+  std::shared_ptr<const std::vector<uint8_t>> decoded;
+  size_t frame_bytes() const { return (size_t)rows * cols * (bits_allocated / 8); }
+  // Samples are little-endian words (or bytes) at pixel_offset of pixel_base().
+  bool native_le() const { return decoded || syntax != Syntax::kExplicitBE; }
+  const uint8_t* pixel_base(const uint8_t* file) const { return decoded ? decoded->data() : file; }
 };
 
 // Parse a whole file image held in memory. Throws SliceError on malformed/unsupported input.
@@ -41,9 +62,19 @@ Header parse(const uint8_t* data, size_t size);
 // the pixel data lies in the prefix (throws SliceError "Truncated" otherwise).
 Header parse_prefix(const uint8_t* data, size_t avail, size_t size);
 
-// Copy the first frame's pixels to `dst` as 16-bit words (8-bit data is widened, big-endian data
-// is byte-swapped). dst must hold rows*cols uint16.
-void copy_pixels16(const Header& h, const uint8_t* data, size_t size, uint16_t* dst);
+// Frame `frame` (0-based) as 16-bit words in `dst` (rows*cols uint16): 8-bit data is widened,
+// big-endian data byte-swapped, RLE/deflated data taken from Header::decoded, MONOCHROME1 inverted.
+// Throws SliceError when the frame does not exist.
+void copy_pixels16(const Header& h, const uint8_t* data, size_t size, uint16_t* dst, int frame = 0);
+
+// Which frame of a file the 2D pipeline imports: `policy` < 0 rejects multi-frame files with a
+// SliceError naming the frame count (a slice pipeline is handed a stack, and silently taking one of
+// its frames would hide that); policy ≥ 0 selects that frame (an error if the file has fewer).
+// Single-frame files always yield frame 0.
+int select_frame(const Header& h, int policy);
+
+// Inverts `n` samples within `bits` stored bits in place (MONOCHROME1 → MONOCHROME2).
+void invert_samples(uint16_t* px, size_t n, int bits);
 
 // Read a file completely (throws SliceError if it cannot be read).
 std::vector<uint8_t> read_file(const std::string& path);
@@ -86,13 +117,14 @@ class SliceFile {
   }
   // Parses the header (`buf` is scratch space owned by the caller and must outlive pixels16).
   const Header& header(std::vector<uint8_t>& buf);
-  // First frame as 16-bit words into dst (rows*cols elements).
-  void pixels16(uint16_t* dst);
+  // Frame `frame` as 16-bit words into dst (rows*cols elements), MONOCHROME1 inverted.
+  void pixels16(uint16_t* dst, int frame = 0);
   // True when pixels16 reads straight from the file (prefix parse, LE 16-bit data).
   bool direct() const { return !whole_; }
-  // Staged reads of little-endian 16-bit data: the first frame's samples inside the caller's
-  // scratch buffer (valid until it is reused), else nullptr.
-  const uint16_t* staged_samples() const;
+  // Staged reads of little-endian 16-bit data (including decoded RLE/deflated files): frame
+  // `frame`'s samples inside the caller's scratch buffer or the decoded buffer (valid until reused),
+  // else nullptr — also for MONOCHROME1, whose samples must go through pixels16's inversion.
+  const uint16_t* staged_samples(int frame = 0) const;
 
  private:
   void pread_all(void* dst, size_t n, size_t off);
@@ -135,8 +167,12 @@ struct WriteSpec {
   std::string study_uid = "1.2.826.0.1.3680043.10.1", series_uid = "1.2.826.0.1.3680043.10.2",
               sop_uid = "1.2.826.0.1.3680043.10.3";
   std::string modality = "MR";
+  std::string photometric = "MONOCHROME2";
+  int frames = 1;  // pixels holds frames*rows*cols samples; NumberOfFrames written when > 1
+  // kDeflatedLE: the dataset after the meta group is raw-deflated (zlib); kRleLossless: one
+  // PackBits-coded fragment per frame (MSB segment, then LSB segment for 16-bit data).
   Syntax syntax = Syntax::kExplicitLE;
-  bool preamble = true;  // write 128-byte preamble + "DICM" + file meta group
+  bool preamble = true;  // write 128-byte preamble + "DICM" + file meta group (required by kDeflatedLE/kRleLossless)
 };
 
 std::vector<uint8_t> write(const WriteSpec& spec);

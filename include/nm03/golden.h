@@ -31,7 +31,8 @@ struct SliceInput {
 };
 
 // DICOM import (setLoadSeries(false)); applies the <100 guard when `min_dim` > 0.
-SliceInput load_slice(const std::string& path, int min_dim);
+// `frame`: dicom::select_frame policy (-1 rejects multi-frame files, k ≥ 0 imports frame k).
+SliceInput load_slice(const std::string& path, int min_dim, int frame = -1);
 
 NormClip make_normclip(const SliceInput& s, const PipelineParams& p);
 

@@ -19,14 +19,18 @@ bool sync_launches();
 // real kernel. Variants truncate the kernel for time splits; their output is invalid.
 int profile_variant(const char* kernel);
 
-// Loads the code objects of the 2D pipeline's kernels (median k, sharpen, SRG, JPEG) on the current
-// device. HIP loads a translation unit's code object at the first launch of one of its kernels;
-// Engine construction calls it (one thread, before any launch); the CLIs already on their start-up
-// thread, so the first batch does not pay for it.
+// Loads the code object of every kernel translation unit (k1 median and sharpen, k2 SRG, k3 render,
+// k4 JPEG, k5 volume, k6 threshold; every template instance) on the current device. HIP loads a
+// translation unit's code object at the first launch of one of its kernels; preloading makes that
+// happen on one thread before any launch (Engine and VolumeEngine constructors), never from a slot
+// thread in the middle of a run. Fails loudly (DeviceError) when a code object does not load.
 void preload_kernels();
 void preload_median();
 void preload_sharpen();
 void preload_srg();
+void preload_render();
+void preload_volume();
+void preload_threshold();
 
 // K1a: k×k median of raw keys → `med` (u16 keys, same layout as raw). k ∈ {3,5,7,9}.
 // Per-slice key range: with `tile_mm` (2 u32 per tile) each tile stores its (min, max) and

@@ -36,6 +36,8 @@ struct PipelineParams {
   int min_dim = 100;
   // Apply DICOM modality rescale (slope/intercept) if present.
   bool apply_rescale = true;
+  // Multi-frame files (dicom::select_frame): -1 rejects them (default), k ≥ 0 imports frame k.
+  int frame = -1;
 };
 
 struct RenderParams {

@@ -17,9 +17,11 @@ def parse_dicom(data: bytes):
     return native().dicom_parse(data)
 
 
-def read_slice(path, min_dim=0):
-    """→ (uint16 [H, W] raw samples, meta dict: type, stored_bits, slope, intercept, spacing)."""
-    return native().read_slice(path, min_dim)
+def read_slice(path, min_dim=0, frame=-1):
+    """→ (uint16 [H, W] raw samples, meta dict: type, stored_bits, slope, intercept, spacing).
+    `frame`: -1 rejects multi-frame files, k >= 0 imports frame k. MONOCHROME1 samples come back
+    inverted within the stored bits (MONOCHROME2 semantics)."""
+    return native().read_slice(path, min_dim, frame)
 
 
 def dicom_bytes(pixels, **kw):

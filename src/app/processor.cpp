@@ -59,6 +59,7 @@ void usage(const std::string& which) {
             << "  --repeat N             process the cohort N times (benchmarking)\n"
             << "  --json FILE            write run metrics as JSON\n"
             << "  --resume               keep existing outputs; skip slices whose two JPEGs exist\n"
+            << "  --frame K              import frame K of multi-frame DICOM files (default: reject them)\n"
             << "  --quiet                suppress per-slice progress lines\n"
             << "env: NM03_DATA_ROOT, NM03_LOG=info|warn|error|none, NM03_ROCTX=1,\n"
             << "     NM03_FAULT=corrupt_dicom:<i>,fail_batch:<k>,fail_write:<j>,rank_exit:<r>\n"
@@ -163,6 +164,7 @@ AppConfig parse_args(int argc, char** argv, const std::string& which) {
       c.max_dim_set = true;
     }
     else if (a == "--resume") c.engine.resume = true;
+    else if (a == "--frame") c.engine.pipe.frame = std::atoi(val().c_str());
     else if (a == "--split-volume") c.split_volume = true;
     else {
       std::cerr << "unknown option " << a << " (see --help)" << std::endl;
@@ -754,7 +756,7 @@ int run_parallel(const AppConfig& cfg) {
 int run_test_pipeline(const AppConfig& cfg) {
   try {
     const std::string path = cfg.input.empty() ? cohort::test_slice_path(cfg.data_root) : cfg.input;
-    golden::SliceInput in = golden::load_slice(path, 0);  // the test pipeline has no <100 guard
+    golden::SliceInput in = golden::load_slice(path, 0, cfg.engine.pipe.frame);  // the test pipeline has no <100 guard
     const PipelineParams& p = cfg.engine.pipe;
     const RenderParams& rp = cfg.engine.render;
     std::vector<std::vector<uint8_t>> canvases, jpegs;

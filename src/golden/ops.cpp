@@ -11,9 +11,10 @@
 
 namespace nm03::golden {
 
-SliceInput load_slice(const std::string& path, int min_dim) {
+SliceInput load_slice(const std::string& path, int min_dim, int frame) {
   std::vector<uint8_t> buf = dicom::read_file(path);
   dicom::Header h = dicom::parse(buf.data(), buf.size());
+  const int f = dicom::select_frame(h, frame);
   if (min_dim > 0 && (h.cols < min_dim || h.rows < min_dim))
     throw SliceError("Image dimensions too small: " + std::to_string(h.cols) + "x" + std::to_string(h.rows));
   SliceInput s;
@@ -26,7 +27,7 @@ SliceInput load_slice(const std::string& path, int min_dim) {
   s.spacing_x = h.spacing_x;
   s.spacing_y = h.spacing_y;
   s.raw.resize((size_t)s.w * s.h);
-  dicom::copy_pixels16(h, buf.data(), buf.size(), s.raw.data());
+  dicom::copy_pixels16(h, buf.data(), buf.size(), s.raw.data(), f);
   if (s.type == kU8) s.type = kU16;  // widened; stored_bits keeps the 8-bit mask
   return s;
 }

@@ -9,6 +9,7 @@
 #include <sys/mman.h>
 #include <sys/stat.h>
 #include <unistd.h>
+#include <zlib.h>
 
 #include <algorithm>
 #include <cerrno>
@@ -154,7 +155,86 @@ uint16_t us_value(const Cursor& c, const Elem& e) {
   return c.big ? (uint16_t)((p[0] << 8) | p[1]) : (uint16_t)(p[0] | (p[1] << 8));
 }
 
+// Raw deflate stream (RFC 1951, no zlib header: PS3.5 A.5) → bytes.
+std::vector<uint8_t> inflate_raw(const uint8_t* src, size_t n) {
+  z_stream z{};
+  if (inflateInit2(&z, -MAX_WBITS) != Z_OK) throw SliceError("zlib inflateInit failed");
+  std::vector<uint8_t> out(std::max<size_t>(n * 4, 1 << 16));
+  z.next_in = const_cast<Bytef*>(src);
+  z.avail_in = (uInt)n;
+  size_t have = 0;
+  int r = Z_OK;
+  while (r != Z_STREAM_END) {
+    if (have == out.size()) out.resize(out.size() * 2);
+    z.next_out = out.data() + have;
+    z.avail_out = (uInt)(out.size() - have);
+    r = inflate(&z, Z_NO_FLUSH);
+    have = out.size() - z.avail_out;
+    if (r == Z_STREAM_END) break;
+    if (r != Z_OK) {
+      inflateEnd(&z);
+      throw SliceError("Corrupt deflated DICOM dataset");
+    }
+    if (z.avail_in == 0 && z.avail_out != 0) {  // input used up without the stream's end
+      inflateEnd(&z);
+      throw SliceError("Truncated deflated DICOM dataset");
+    }
+  }
+  inflateEnd(&z);
+  out.resize(have);
+  return out;
+}
+
+// One RLE segment (PS3.5 G.3.1, PackBits) → exactly `n` bytes at dst with stride `stride`.
+void unpackbits(const uint8_t* p, size_t len, uint8_t* dst, size_t n, size_t stride) {
+  size_t i = 0, o = 0;
+  while (o < n) {
+    if (i >= len) throw SliceError("Truncated RLE segment");
+    const int8_t c = (int8_t)p[i++];
+    if (c >= 0) {
+      const size_t k = (size_t)c + 1;
+      if (i + k > len || o + k > n) throw SliceError("Corrupt RLE literal run");
+      for (size_t j = 0; j < k; ++j) dst[(o + j) * stride] = p[i + j];
+      i += k;
+      o += k;
+    } else if (c != -128) {
+      const size_t k = (size_t)(1 - c);
+      if (i >= len || o + k > n) throw SliceError("Corrupt RLE replicate run");
+      const uint8_t v = p[i++];
+      for (size_t j = 0; j < k; ++j) dst[(o + j) * stride] = v;
+      o += k;
+    }
+  }
+}
+
+// One RLE fragment (64-byte header of segment offsets, then the segments) → one frame of native
+// little-endian samples: segment 0 holds the most significant bytes (PS3.5 G.2).
+void decode_rle_frame(const uint8_t* f, size_t len, int rows, int cols, int bytes_per_sample, uint8_t* out) {
+  if (len < 64) throw SliceError("Truncated RLE header");
+  auto le32 = [&](size_t o) { return (uint32_t)f[o] | ((uint32_t)f[o + 1] << 8) | ((uint32_t)f[o + 2] << 16) | ((uint32_t)f[o + 3] << 24); };
+  const uint32_t nseg = le32(0);
+  if ((int)nseg != bytes_per_sample) throw SliceError("RLE segment count " + std::to_string(nseg) + " does not match BitsAllocated");
+  const size_t n = (size_t)rows * cols;
+  for (uint32_t k = 0; k < nseg; ++k) {
+    const size_t a = le32(4 + 4 * k), b = k + 1 < nseg ? le32(8 + 4 * k) : len;
+    if (a < 64 || a > b || b > len) throw SliceError("Bad RLE segment offset");
+    // segment k = byte (nseg - 1 - k) of every little-endian sample
+    unpackbits(f + a, b - a, out + (nseg - 1 - k), n, (size_t)bytes_per_sample);
+  }
+}
+
 }  // namespace
+
+const char* syntax_name(Syntax s) {
+  switch (s) {
+    case Syntax::kImplicitLE: return "implicit";
+    case Syntax::kExplicitLE: return "explicit";
+    case Syntax::kExplicitBE: return "big";
+    case Syntax::kDeflatedLE: return "deflated";
+    case Syntax::kRleLossless: return "rle";
+  }
+  return "?";
+}
 
 Header parse(const uint8_t* data, size_t size) { return parse_prefix(data, size, size); }
 
@@ -184,6 +264,7 @@ Header parse_prefix(const uint8_t* data, size_t avail, size_t size) {
     if (size < 8) throw SliceError("Not a DICOM file");
   }
   const std::string& ts = h.transfer_syntax;
+  std::shared_ptr<std::vector<uint8_t>> inflated;
   if (ts == "1.2.840.10008.1.2") {
     h.syntax = Syntax::kImplicitLE;
     explicit_vr = false;
@@ -192,6 +273,16 @@ Header parse_prefix(const uint8_t* data, size_t avail, size_t size) {
   } else if (ts == "1.2.840.10008.1.2.2") {
     h.syntax = Syntax::kExplicitBE;
     c.big = true;
+  } else if (ts == "1.2.840.10008.1.2.1.99") {
+    // Deflated Explicit VR LE: everything after the meta group is one raw deflate stream.
+    h.syntax = Syntax::kDeflatedLE;
+    if (avail < full) throw SliceError("Truncated DICOM data");  // callers retry with the whole file
+    inflated = std::make_shared<std::vector<uint8_t>>(inflate_raw(data + c.pos, size - c.pos));
+    c = Cursor{inflated->data(), inflated->size(), 0, false};
+  } else if (ts == "1.2.840.10008.1.2.5") {
+    h.syntax = Syntax::kRleLossless;
+  } else if (ts.rfind("1.2.840.10008.1.2.4.", 0) == 0) {
+    throw SliceError("Unsupported compressed DICOM transfer syntax (JPEG family): " + ts);
   } else {
     throw SliceError("Unsupported DICOM transfer syntax: " + ts);
   }
@@ -200,7 +291,41 @@ Header parse_prefix(const uint8_t* data, size_t avail, size_t size) {
   while (c.has(8)) {
     Elem e = read_elem(c, explicit_vr);
     if (e.group == 0x7FE0 && e.elem == 0x0010) {
-      if (e.len == kUndefined) throw SliceError("Encapsulated (compressed) pixel data is not supported");
+      if (e.len == kUndefined) {
+        if (h.syntax != Syntax::kRleLossless)
+          throw SliceError("Encapsulated (compressed) pixel data in a native transfer syntax");
+        if (avail < full) throw SliceError("Truncated DICOM data");  // callers retry with the whole file
+        // Basic Offset Table item, then one fragment per frame (PS3.5 A.4, G.2), then the
+        // sequence delimiter.
+        std::vector<std::pair<size_t, size_t>> frags;
+        bool bot = true;
+        for (;;) {
+          Elem it = read_elem(c, true);
+          if (it.group == 0xFFFE && it.elem == 0xE0DD) break;
+          if (it.group != 0xFFFE || it.elem != 0xE000 || it.len == kUndefined) throw SliceError("Malformed encapsulated pixel data");
+          c.need(it.len);
+          if (!bot) frags.push_back({it.value_pos, it.len});
+          bot = false;
+          c.pos += it.len;
+        }
+        if (h.rows <= 0 || h.cols <= 0 || (h.bits_allocated != 8 && h.bits_allocated != 16))
+          throw SliceError("RLE image without Rows/Columns/BitsAllocated before its pixel data");
+        const int frames = std::max(1, h.frames);
+        if ((int)frags.size() != frames)
+          throw SliceError("RLE pixel data has " + std::to_string(frags.size()) + " fragments for " + std::to_string(frames) +
+                           " frame(s) (one fragment per frame is supported)");
+        const size_t fb = h.frame_bytes();
+        auto dec = std::make_shared<std::vector<uint8_t>>(fb * frames);
+        for (int f = 0; f < frames; ++f)
+          decode_rle_frame(c.d + frags[f].first, frags[f].second, h.rows, h.cols, h.bits_allocated / 8, dec->data() + f * fb);
+        h.decoded = dec;
+        h.pixel_offset = 0;
+        h.pixel_length = dec->size();
+        have_pixels = true;
+        break;
+      }
+      if (h.syntax == Syntax::kRleLossless)
+        throw SliceError("RLE Lossless transfer syntax with native (not encapsulated) pixel data");
       h.pixel_offset = e.value_pos;
       h.pixel_length = e.len;
       have_pixels = true;
@@ -278,6 +403,10 @@ Header parse_prefix(const uint8_t* data, size_t avail, size_t size) {
   if (h.rows <= 0 || h.cols <= 0) throw SliceError("DICOM image has no Rows/Columns");
   if (h.samples != 1) throw SliceError("Only single-sample (monochrome) DICOM images are supported");
   if (h.frames < 1) h.frames = 1;
+  if (inflated) h.decoded = inflated;
+  if (!h.photometric.empty() && h.photometric != "MONOCHROME1" && h.photometric != "MONOCHROME2")
+    throw SliceError("Unsupported PhotometricInterpretation: " + h.photometric);
+  h.invert = h.photometric == "MONOCHROME1";
   if (h.bits_allocated == 16) {
     h.type = h.pixel_rep ? kI16 : kU16;
   } else if (h.bits_allocated == 8) {
@@ -286,24 +415,50 @@ Header parse_prefix(const uint8_t* data, size_t avail, size_t size) {
     throw SliceError("Unsupported BitsAllocated: " + std::to_string(h.bits_allocated));
   }
   if (h.bits_stored <= 0 || h.bits_stored > h.bits_allocated) h.bits_stored = h.bits_allocated;
-  const size_t need = (size_t)h.rows * h.cols * (h.bits_allocated / 8);
-  if (h.pixel_length < need || h.pixel_offset + need > full)
-    throw SliceError("DICOM pixel data shorter than Rows*Columns");
+  // Every frame must be present (a multi-frame file's last frame is checked, not only its first).
+  const size_t need = h.frame_bytes() * (size_t)h.frames;
+  const size_t limit = h.decoded ? h.decoded->size() : full;
+  if (h.pixel_length < need || h.pixel_offset + need > limit)
+    throw SliceError(h.frames > 1 ? "DICOM pixel data shorter than NumberOfFrames*Rows*Columns"
+                                  : "DICOM pixel data shorter than Rows*Columns");
   if (!(h.slope == h.slope) || h.slope == 0.f) h.slope = 1.f;
   return h;
 }
 
-void copy_pixels16(const Header& h, const uint8_t* data, size_t size, uint16_t* dst) {
+void invert_samples(uint16_t* px, size_t n, int bits) {
+  const uint16_t mask = (uint16_t)(bits >= 16 ? 0xFFFFu : ((1u << bits) - 1u));
+  for (size_t i = 0; i < n; ++i) px[i] = (uint16_t)(~px[i] & mask);
+}
+
+int select_frame(const Header& h, int policy) {
+  if (h.frames <= 1) return 0;  // a single-frame file is its own slice under every policy
+  if (policy < 0) {
+    if (h.frames > 1)
+      throw SliceError("Multi-frame DICOM (" + std::to_string(h.frames) +
+                       " frames): the 2D pipeline imports single-frame slices (select one with --frame K)");
+    return 0;
+  }
+  if (policy >= h.frames)
+    throw SliceError("Frame " + std::to_string(policy) + " requested from a DICOM file with " + std::to_string(h.frames) +
+                     " frame(s)");
+  return policy;
+}
+
+void copy_pixels16(const Header& h, const uint8_t* data, size_t size, uint16_t* dst, int frame) {
+  if (frame < 0 || frame >= h.frames) throw SliceError("DICOM frame " + std::to_string(frame) + " out of range");
   const size_t n = (size_t)h.rows * h.cols;
-  const uint8_t* src = data + h.pixel_offset;
-  if (h.pixel_offset + n * (h.bits_allocated / 8) > size) throw SliceError("Truncated pixel data");
+  const size_t off = h.pixel_offset + (size_t)frame * h.frame_bytes();
+  const size_t limit = h.decoded ? h.decoded->size() : size;
+  if (off + n * (h.bits_allocated / 8) > limit) throw SliceError("Truncated pixel data");
+  const uint8_t* src = h.pixel_base(data) + off;
   if (h.bits_allocated == 8) {
     for (size_t i = 0; i < n; ++i) dst[i] = src[i];
-  } else if (h.syntax == Syntax::kExplicitBE) {
+  } else if (!h.native_le()) {
     for (size_t i = 0; i < n; ++i) dst[i] = (uint16_t)((src[2 * i] << 8) | src[2 * i + 1]);
   } else {
     std::memcpy(dst, src, n * 2);
   }
+  if (h.invert) invert_samples(dst, n, h.bits_stored);
 }
 
 size_t read_file_into(const std::string& path, std::vector<uint8_t>& buf) {
@@ -429,7 +584,7 @@ const Header& SliceFile::header(std::vector<uint8_t>& buf) {
       h_ = parse_prefix(buf.data(), pre, size_);
       whole_ = false;
       // Direct reads only for raw little-endian 16-bit samples; everything else is converted.
-      if (h_.bits_allocated == 16 && h_.syntax != Syntax::kExplicitBE) return h_;
+      if (h_.bits_allocated == 16 && h_.syntax != Syntax::kExplicitBE && !h_.decoded) return h_;
     } catch (const SliceError&) {
       // header longer than the prefix (or malformed): parse the whole file below
     }
@@ -442,31 +597,37 @@ const Header& SliceFile::header(std::vector<uint8_t>& buf) {
   return h_;
 }
 
-void SliceFile::pixels16(uint16_t* dst) {
+void SliceFile::pixels16(uint16_t* dst, int frame) {
+  if (frame < 0 || frame >= h_.frames) throw SliceError("DICOM frame " + std::to_string(frame) + " out of range");
+  const size_t n = (size_t)h_.rows * h_.cols * 2;
+  const size_t off = h_.pixel_offset + (size_t)frame * h_.frame_bytes();
   if (whole_) {
-    const bool raw16 = h_.bits_allocated == 16 && h_.syntax != Syntax::kExplicitBE;
-    const size_t n = (size_t)h_.rows * h_.cols * 2;
+    const bool raw16 = h_.bits_allocated == 16 && h_.native_le() && !h_.invert;
     if (raw16 && mode_ != ReadMode::kDirect) {
-      if (h_.pixel_offset + n > size_) throw SliceError("Truncated pixel data");
-      stream_copy(dst, data() + h_.pixel_offset, n);
+      const size_t limit = h_.decoded ? h_.decoded->size() : size_;
+      if (off + n > limit) throw SliceError("Truncated pixel data");
+      stream_copy(dst, h_.pixel_base(data()) + off, n);
     } else {
-      copy_pixels16(h_, data(), size_, dst);
+      copy_pixels16(h_, data(), size_, dst, frame);
     }
     return;
   }
   // Pixel bytes that came with the header read are taken from it; the rest is read into dst.
-  const size_t n = (size_t)h_.rows * h_.cols * 2;
-  size_t k = h_.pixel_offset < have_ ? std::min(n, have_ - h_.pixel_offset) : 0;
-  if (k) std::memcpy(dst, buf_->data() + h_.pixel_offset, k);
-  if (k < n) pread_all(reinterpret_cast<uint8_t*>(dst) + k, n - k, h_.pixel_offset + k);
+  size_t k = off < have_ ? std::min(n, have_ - off) : 0;
+  if (k) std::memcpy(dst, buf_->data() + off, k);
+  if (k < n) pread_all(reinterpret_cast<uint8_t*>(dst) + k, n - k, off + k);
+  if (h_.invert) invert_samples(dst, n / 2, h_.bits_stored);
 }
 
-const uint16_t* SliceFile::staged_samples() const {
+const uint16_t* SliceFile::staged_samples(int frame) const {
   if (!whole_ || mode_ == ReadMode::kDirect || !buf_) return nullptr;
-  if (h_.bits_allocated != 16 || h_.syntax == Syntax::kExplicitBE) return nullptr;
+  if (h_.bits_allocated != 16 || !h_.native_le() || h_.invert) return nullptr;
+  if (frame < 0 || frame >= h_.frames) return nullptr;
   const size_t n = (size_t)h_.rows * h_.cols * 2;
-  if (h_.pixel_offset + n > size_ || (h_.pixel_offset & 1)) return nullptr;
-  return reinterpret_cast<const uint16_t*>(data() + h_.pixel_offset);
+  const size_t off = h_.pixel_offset + (size_t)frame * h_.frame_bytes();
+  const size_t limit = h_.decoded ? h_.decoded->size() : size_;
+  if (off + n > limit || (off & 1)) return nullptr;
+  return reinterpret_cast<const uint16_t*>(h_.pixel_base(data()) + off);
 }
 
 void stream_copy(void* dst, const void* src, size_t n) {
@@ -573,10 +734,60 @@ std::string fmt_ds(double v) {
 
 }  // namespace
 
+namespace {
+
+// PackBits (PS3.5 G.3.1) of n bytes read at stride `stride`: replicate runs of ≥ 3 equal bytes,
+// literal runs otherwise, each at most 128 long.
+void packbits(const uint8_t* src, size_t n, size_t stride, std::vector<uint8_t>& out) {
+  auto at = [&](size_t i) { return src[i * stride]; };
+  size_t i = 0;
+  while (i < n) {
+    size_t r = 1;
+    while (i + r < n && r < 128 && at(i + r) == at(i)) ++r;
+    if (r >= 3) {
+      out.push_back((uint8_t)(int8_t)(1 - (int)r));
+      out.push_back(at(i));
+      i += r;
+      continue;
+    }
+    size_t l = 0;  // literal run up to the next run of ≥ 3
+    while (i + l < n && l < 128) {
+      if (i + l + 2 < n && at(i + l) == at(i + l + 1) && at(i + l) == at(i + l + 2)) break;
+      ++l;
+    }
+    out.push_back((uint8_t)(l - 1));
+    for (size_t j = 0; j < l; ++j) out.push_back(at(i + j));
+    i += l;
+  }
+  if (out.size() & 1) out.push_back(0x80);  // segments are padded to even length (no-op code)
+}
+
+std::vector<uint8_t> deflate_raw(const uint8_t* src, size_t n) {
+  z_stream z{};
+  if (deflateInit2(&z, Z_DEFAULT_COMPRESSION, Z_DEFLATED, -MAX_WBITS, 8, Z_DEFAULT_STRATEGY) != Z_OK)
+    throw std::runtime_error("zlib deflateInit failed");
+  std::vector<uint8_t> out(deflateBound(&z, (uLong)n) + 16);
+  z.next_in = const_cast<Bytef*>(src);
+  z.avail_in = (uInt)n;
+  z.next_out = out.data();
+  z.avail_out = (uInt)out.size();
+  const int r = deflate(&z, Z_FINISH);
+  deflateEnd(&z);
+  if (r != Z_STREAM_END) throw std::runtime_error("zlib deflate failed");
+  out.resize(z.total_out);
+  return out;
+}
+
+}  // namespace
+
 std::vector<uint8_t> write(const WriteSpec& s) {
   const char* ts = s.syntax == Syntax::kImplicitLE   ? "1.2.840.10008.1.2"
                    : s.syntax == Syntax::kExplicitLE ? "1.2.840.10008.1.2.1"
-                                                     : "1.2.840.10008.1.2.2";
+                   : s.syntax == Syntax::kExplicitBE ? "1.2.840.10008.1.2.2"
+                   : s.syntax == Syntax::kDeflatedLE ? "1.2.840.10008.1.2.1.99"
+                                                     : "1.2.840.10008.1.2.5";
+  if ((s.syntax == Syntax::kDeflatedLE || s.syntax == Syntax::kRleLossless) && !s.preamble)
+    throw std::runtime_error("deflated / RLE files need the file meta group (preamble)");
   const char* sop_class = "1.2.840.10008.5.1.4.1.1.4";  // MR Image Storage
   Out out;
   if (s.preamble) {
@@ -595,8 +806,10 @@ std::vector<uint8_t> write(const WriteSpec& s) {
     out.elem(0x0002, 0x0000, "UL", gl, 4, true);
     out.raw(meta.b.data(), meta.b.size());
   }
+  const size_t meta_end = out.b.size();
   const bool ex = s.syntax != Syntax::kImplicitLE;
   out.big = s.syntax == Syntax::kExplicitBE;
+  const int frames = std::max(1, s.frames);
   out.str(0x0008, 0x0008, "CS", "ORIGINAL\\PRIMARY", ex);
   out.str(0x0008, 0x0016, "UI", sop_class, ex);
   out.str(0x0008, 0x0018, "UI", s.sop_uid, ex);
@@ -612,7 +825,8 @@ std::vector<uint8_t> write(const WriteSpec& s) {
   out.str(0x0020, 0x0037, "DS", "1\\0\\0\\0\\1\\0", ex);
   out.str(0x0020, 0x1041, "DS", fmt_ds(s.position[2]), ex);
   out.us(0x0028, 0x0002, 1, ex);
-  out.str(0x0028, 0x0004, "CS", "MONOCHROME2", ex);
+  out.str(0x0028, 0x0004, "CS", s.photometric, ex);
+  if (frames > 1) out.str(0x0028, 0x0008, "IS", std::to_string(frames), ex);
   out.us(0x0028, 0x0010, (uint16_t)s.rows, ex);
   out.us(0x0028, 0x0011, (uint16_t)s.cols, ex);
   out.str(0x0028, 0x0030, "DS", fmt_ds(s.spacing_y) + "\\" + fmt_ds(s.spacing_x), ex);
@@ -626,7 +840,9 @@ std::vector<uint8_t> write(const WriteSpec& s) {
     out.str(0x0028, 0x1052, "DS", fmt_ds(s.intercept), ex);
     out.str(0x0028, 0x1053, "DS", fmt_ds(s.slope), ex);
   }
-  const size_t n = (size_t)s.rows * s.cols;
+  const size_t n = (size_t)s.rows * s.cols * frames;
+  const size_t bps = ba / 8;
+  // Native little-endian samples (big-endian for kExplicitBE) of every frame.
   std::vector<uint8_t> px(ba == 8 ? (n + (n & 1)) : n * 2, 0);
   if (ba == 8) {
     for (size_t i = 0; i < n; ++i) px[i] = s.pixels ? (uint8_t)s.pixels[i] : 0;
@@ -642,7 +858,50 @@ std::vector<uint8_t> write(const WriteSpec& s) {
       }
     }
   }
-  out.elem(0x7FE0, 0x0010, ba == 8 ? "OB" : "OW", px.data(), (uint32_t)px.size(), ex);
+  if (s.syntax == Syntax::kRleLossless) {
+    // Encapsulated: (7FE0,0010) OB of undefined length, an empty Basic Offset Table item, one
+    // fragment per frame, the sequence delimiter.
+    const size_t fpix = (size_t)s.rows * s.cols;
+    out.u16(0x7FE0);
+    out.u16(0x0010);
+    out.raw("OB", 2);
+    out.u16(0);
+    out.u32(0xFFFFFFFFu);
+    auto item = [&](uint16_t e, const std::vector<uint8_t>& v) {
+      out.u16(0xFFFE);
+      out.u16(e);
+      out.u32((uint32_t)v.size());
+      out.raw(v.data(), v.size());
+    };
+    item(0xE000, {});
+    for (int f = 0; f < frames; ++f) {
+      std::vector<uint8_t> frag(64, 0), segs;
+      std::vector<uint32_t> offs;
+      for (size_t k = 0; k < bps; ++k) {
+        offs.push_back((uint32_t)(64 + segs.size()));
+        // segment k: byte (bps - 1 - k) of each little-endian sample (MSB first)
+        packbits(px.data() + f * fpix * bps + (bps - 1 - k), fpix, bps, segs);
+      }
+      auto put = [&](size_t o, uint32_t v) {
+        for (int b = 0; b < 4; ++b) frag[o + b] = (uint8_t)(v >> (8 * b));
+      };
+      put(0, (uint32_t)bps);
+      for (size_t k = 0; k < bps; ++k) put(4 + 4 * k, offs[k]);
+      frag.insert(frag.end(), segs.begin(), segs.end());
+      item(0xE000, frag);
+    }
+    out.u16(0xFFFE);
+    out.u16(0xE0DD);
+    out.u32(0);
+  } else {
+    out.elem(0x7FE0, 0x0010, ba == 8 ? "OB" : "OW", px.data(), (uint32_t)px.size(), ex);
+  }
+  if (s.syntax == Syntax::kDeflatedLE) {
+    std::vector<uint8_t> z = deflate_raw(out.b.data() + meta_end, out.b.size() - meta_end);
+    if (z.size() & 1) z.push_back(0);  // even length
+    out.b.resize(meta_end);
+    out.b.insert(out.b.end(), z.begin(), z.end());
+  }
   return out.b;
 }
 

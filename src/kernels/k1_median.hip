@@ -267,7 +267,9 @@ void launch_median(const uint16_t* raw, uint16_t* med, const SliceDesc* descs, c
 
 void preload_median() {
   hipFuncAttributes a;
-  (void)hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&median_kernel<7>));
+  for (const void* f : {reinterpret_cast<const void*>(&median_kernel<3>), reinterpret_cast<const void*>(&median_kernel<5>),
+                        reinterpret_cast<const void*>(&median_kernel<7>), reinterpret_cast<const void*>(&median_kernel<9>)})
+    check_hip(hipFuncGetAttributes(&a, f), "preload median_kernel");
 }
 
 }  // namespace nm03::gpu

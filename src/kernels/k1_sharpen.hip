@@ -311,7 +311,11 @@ void launch_sharpen_band(const uint16_t* med, uint64_t* band, float* sharpened, 
 
 void preload_sharpen() {
   hipFuncAttributes a;
-  (void)hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&sharpen_band_kernel<4>));
+  for (const void* f : {reinterpret_cast<const void*>(&sharpen_band_kernel<0>), reinterpret_cast<const void*>(&sharpen_band_kernel<1>),
+                        reinterpret_cast<const void*>(&sharpen_band_kernel<2>), reinterpret_cast<const void*>(&sharpen_band_kernel<3>),
+                        reinterpret_cast<const void*>(&sharpen_band_kernel<4>), reinterpret_cast<const void*>(&sharpen_band_kernel<5>),
+                        reinterpret_cast<const void*>(&sharpen_band_kernel<6>), reinterpret_cast<const void*>(&sharpen_band_kernel<7>)})
+    check_hip(hipFuncGetAttributes(&a, f), "preload sharpen_band_kernel");
 }
 
 }  // namespace nm03::gpu

@@ -141,7 +141,8 @@ void launch_srg_morph(const uint64_t* band, const SliceDesc* descs, int nslices,
 
 void preload_srg() {
   hipFuncAttributes a;
-  (void)hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&srg_morph_kernel<false>));
+  for (const void* f : {reinterpret_cast<const void*>(&srg_morph_kernel<false>), reinterpret_cast<const void*>(&srg_morph_kernel<true>)})
+    check_hip(hipFuncGetAttributes(&a, f), "preload srg_morph_kernel");
 }
 
 }  // namespace nm03::gpu

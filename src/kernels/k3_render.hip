@@ -43,4 +43,9 @@ void launch_render(const uint16_t* raw, const float* f32, const uint64_t* bits, 
   check_launch("render_kernel");
 }
 
+void preload_render() {
+  hipFuncAttributes a;
+  check_hip(hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&render_kernel)), "preload render_kernel");
+}
+
 }  // namespace nm03::gpu

@@ -881,8 +881,11 @@ void preload_kernels() {
   preload_median();
   preload_sharpen();
   preload_srg();
+  preload_render();
+  preload_volume();
+  preload_threshold();
   hipFuncAttributes a;
-  (void)hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&jpeg_fused_kernel<4, kUnionWords>));
+  check_hip(hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&jpeg_fused_kernel<4, kUnionWords>)), "preload jpeg_fused_kernel");
 }
 
 }  // namespace nm03::gpu

@@ -367,4 +367,14 @@ void launch_slab_seed(const uint64_t* band, uint64_t* region, const uint64_t* nb
   check_launch("slab_seed_kernel");
 }
 
+void preload_volume() {
+  hipFuncAttributes a;
+  for (const void* f : {reinterpret_cast<const void*>(&srg3d_seed_kernel), reinterpret_cast<const void*>(&srg3d_kernel<false>),
+                        reinterpret_cast<const void*>(&srg3d_kernel<true>), reinterpret_cast<const void*>(&dilate_plane_kernel<false>),
+                        reinterpret_cast<const void*>(&dilate_plane_kernel<true>), reinterpret_cast<const void*>(&border_plane_kernel<false>),
+                        reinterpret_cast<const void*>(&border_plane_kernel<true>), reinterpret_cast<const void*>(&dilate_z_kernel),
+                        reinterpret_cast<const void*>(&slab_seed_kernel)})
+    check_hip(hipFuncGetAttributes(&a, f), "preload volume kernels");
+}
+
 }  // namespace nm03::gpu

@@ -30,4 +30,9 @@ void launch_threshold(const float* in, uint8_t* out, size_t n, float lo, float h
   check_launch("threshold_kernel");
 }
 
+void preload_threshold() {
+  hipFuncAttributes a;
+  check_hip(hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&threshold_kernel)), "preload threshold_kernel");
+}
+
 }  // namespace nm03::gpu

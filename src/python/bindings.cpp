@@ -91,6 +91,8 @@ py::dict header_dict(const dicom::Header& h) {
   d["pixel_offset"] = h.pixel_offset;
   d["pixel_length"] = h.pixel_length;
   d["frames"] = h.frames;
+  d["invert"] = h.invert;
+  d["syntax"] = dicom::syntax_name(h.syntax);
   return d;
 }
 
@@ -251,7 +253,8 @@ PYBIND11_MODULE(_nm03, m) {
       .def_readwrite("dilation_size", &PipelineParams::dilation_size)
       .def_readwrite("erosion_size", &PipelineParams::erosion_size)
       .def_readwrite("min_dim", &PipelineParams::min_dim)
-      .def_readwrite("apply_rescale", &PipelineParams::apply_rescale);
+      .def_readwrite("apply_rescale", &PipelineParams::apply_rescale)
+      .def_readwrite("frame", &PipelineParams::frame);
   py::class_<RenderParams>(m, "RenderParams")
       .def(py::init<>())
       .def_readwrite("out_width", &RenderParams::out_width)
@@ -293,21 +296,32 @@ PYBIND11_MODULE(_nm03, m) {
     std::string s = b;
     return header_dict(dicom::parse((const uint8_t*)s.data(), s.size()));
   });
-  m.def("dicom_pixels", [](py::bytes b) {
+  m.def(
+      "dicom_pixels",
+      [](py::bytes b, int frame) {
+        std::string s = b;
+        dicom::Header h = dicom::parse((const uint8_t*)s.data(), s.size());
+        std::vector<uint16_t> px((size_t)h.rows * h.cols);
+        dicom::copy_pixels16(h, (const uint8_t*)s.data(), s.size(), px.data(), frame);
+        return to_np<uint16_t>(px, {h.rows, h.cols});
+      },
+      py::arg("data"), py::arg("frame") = 0);
+  m.def("dicom_select_frame", [](py::bytes b, int policy) {
     std::string s = b;
-    dicom::Header h = dicom::parse((const uint8_t*)s.data(), s.size());
-    std::vector<uint16_t> px((size_t)h.rows * h.cols);
-    dicom::copy_pixels16(h, (const uint8_t*)s.data(), s.size(), px.data());
-    return to_np<uint16_t>(px, {h.rows, h.cols});
+    return dicom::select_frame(dicom::parse((const uint8_t*)s.data(), s.size()), policy);
   });
   m.def(
       "dicom_bytes",
       [](py::array_t<uint16_t, py::array::c_style | py::array::forcecast> px, const std::string& type, int bits_stored,
          bool write_rescale, float slope, float intercept, float sx, float sy, int instance, const std::string& patient_id,
-         const std::string& syntax, bool preamble) {
+         const std::string& syntax, bool preamble, const std::string& photometric) {
         dicom::WriteSpec w;
-        w.rows = (int)px.shape(0);
-        w.cols = (int)px.shape(1);
+        // (rows, cols) or (frames, rows, cols)
+        if (px.ndim() != 2 && px.ndim() != 3) throw std::invalid_argument("pixels must be 2D or 3D (frames, rows, cols)");
+        w.frames = px.ndim() == 3 ? (int)px.shape(0) : 1;
+        w.rows = (int)px.shape(px.ndim() - 2);
+        w.cols = (int)px.shape(px.ndim() - 1);
+        w.photometric = photometric;
         w.type = parse_type(type);
         w.bits_stored = bits_stored;
         std::vector<uint16_t> v = from_np<uint16_t>(px);
@@ -319,9 +333,12 @@ PYBIND11_MODULE(_nm03, m) {
         w.spacing_y = sy;
         w.instance_number = instance;
         w.patient_id = patient_id;
-        w.syntax = syntax == "implicit" ? dicom::Syntax::kImplicitLE
-                   : syntax == "big"    ? dicom::Syntax::kExplicitBE
-                                        : dicom::Syntax::kExplicitLE;
+        w.syntax = syntax == "implicit"   ? dicom::Syntax::kImplicitLE
+                   : syntax == "big"      ? dicom::Syntax::kExplicitBE
+                   : syntax == "deflated" ? dicom::Syntax::kDeflatedLE
+                   : syntax == "rle"      ? dicom::Syntax::kRleLossless
+                   : syntax == "explicit" ? dicom::Syntax::kExplicitLE
+                                          : throw std::invalid_argument("syntax: implicit|explicit|big|deflated|rle");
         w.preamble = preamble;
         auto b = dicom::write(w);
         return py::bytes((const char*)b.data(), b.size());
@@ -329,7 +346,7 @@ PYBIND11_MODULE(_nm03, m) {
       py::arg("pixels"), py::arg("type") = "u16", py::arg("bits_stored") = 16, py::arg("write_rescale") = false,
       py::arg("slope") = 1.f, py::arg("intercept") = 0.f, py::arg("spacing_x") = 1.f, py::arg("spacing_y") = 1.f,
       py::arg("instance") = 1, py::arg("patient_id") = "PGBM-000", py::arg("syntax") = "explicit",
-      py::arg("preamble") = true);
+      py::arg("preamble") = true, py::arg("photometric") = "MONOCHROME2");
   m.def("numa_parse_cpulist", &numa::parse_cpulist);
   m.def(
       "mhd_write",
@@ -390,21 +407,25 @@ PYBIND11_MODULE(_nm03, m) {
       py::arg("sysfs") = "/sys", py::arg("allowed") = std::vector<int>{});
   m.def(
       "read_pixels_direct",
-      [](const std::string& path, const std::string& mode, size_t prefix) {
+      [](const std::string& path, const std::string& mode, size_t prefix, int frame) {
         dicom::SliceFile f(path, mode == "staged" ? dicom::ReadMode::kStaged : dicom::ReadMode::kDirect, prefix);
         std::vector<uint8_t> scratch;
         const dicom::Header& h = f.header(scratch);
         std::vector<uint16_t> px((size_t)h.rows * h.cols + 1);  // +1: misaligned destination below
         uint16_t* dst = px.data() + 1;
-        f.pixels16(dst);
+        f.pixels16(dst, frame);
         std::vector<uint16_t> out(dst, dst + (size_t)h.rows * h.cols);
-        return py::make_tuple(to_np<uint16_t>(out, {h.rows, h.cols}), f.direct());
+        // The staged fast path's view of the same frame (None when pixels16 must convert).
+        const uint16_t* ss = f.staged_samples(frame);
+        py::object staged = py::none();
+        if (ss) staged = to_np<uint16_t>(std::vector<uint16_t>(ss, ss + (size_t)h.rows * h.cols), {h.rows, h.cols});
+        return py::make_tuple(to_np<uint16_t>(out, {h.rows, h.cols}), f.direct(), staged);
       },
-      py::arg("path"), py::arg("mode") = "direct", py::arg("prefix") = 16384);
+      py::arg("path"), py::arg("mode") = "direct", py::arg("prefix") = 16384, py::arg("frame") = 0);
   m.def(
       "read_slice",
-      [](const std::string& path, int min_dim) {
-        golden::SliceInput s = golden::load_slice(path, min_dim);
+      [](const std::string& path, int min_dim, int frame) {
+        golden::SliceInput s = golden::load_slice(path, min_dim, frame);
         py::dict meta;
         meta["type"] = s.type == kI16 ? "i16" : "u16";
         meta["stored_bits"] = s.stored_bits;
@@ -414,7 +435,7 @@ PYBIND11_MODULE(_nm03, m) {
         meta["spacing_y"] = s.spacing_y;
         return py::make_tuple(to_np<uint16_t>(s.raw, {s.h, s.w}), meta);
       },
-      py::arg("path"), py::arg("min_dim") = 0);
+      py::arg("path"), py::arg("min_dim") = 0, py::arg("frame") = -1);
 
   // ---- cohort / synthetic data -------------------------------------------------------------------
   m.def("extract_file_number", &cohort::extract_file_number);

@@ -415,6 +415,23 @@ struct Engine::Impl {
     return shared_up_;
   }
 
+  // ---- per-batch timeline (NM03_BATCH_TRACE=1) --------------------------------------------------
+  // One record per batch, in ms since the run was submitted: claimed by its slot, loads finished,
+  // kernels enqueued, GPU done, exports done. Printed by finish(): where a cold run's time goes
+  // (slot build, first-use costs, pipeline fill) without a profiler's own start-up in the way.
+  struct BatchMark {
+    int slot = 0;
+    size_t first = 0, count = 0;
+    double claim = 0, loaded = 0, enq = 0, gpu = 0, end = 0;
+  };
+  static bool batch_trace() {
+    static const bool on = [] {
+      const char* e = std::getenv("NM03_BATCH_TRACE");
+      return e && *e && *e != '0';
+    }();
+    return on;
+  }
+
   void make_templates() {
     golden::SliceInput in;
     in.w = in.h = 256;
@@ -655,6 +672,7 @@ struct Engine::Impl {
       // (tools/gpu_load_ab.sh): both removed in round 4.
       dicom::SliceFile file(AT_FDCWD, path.c_str(), path, dicom::ReadMode::kStaged);
       const dicom::Header& h = file.header(buf);
+      const int frame = dicom::select_frame(h, cfg.pipe.frame);
       const size_t n = file.size();  // after header(): staged reads learn the size from the read
       const int md = cfg.pipe.min_dim;
       if (md > 0 && (h.cols < md || h.rows < md)) {
@@ -675,7 +693,7 @@ struct Engine::Impl {
         //    16-bit size when it is still the last one, or else abandoned (a hole, paid from the
         //    credit) for a new 16-bit one. Without credit left: range check first (fits12), then
         //    pack — two passes, no hole.
-        const uint16_t* samples = pack12_ ? file.staged_samples() : nullptr;
+        const uint16_t* samples = pack12_ ? file.staged_samples(frame) : nullptr;
         const size_t plen = align_up(npix / 4 * 3, 8), ulen = align_up(npix, 8);  // u16 elements
         const bool packable = samples && pack12::available() && (npix & 15) == 0;
         const size_t cap = s.cap_pixels + s.hole_slack;
@@ -718,7 +736,7 @@ struct Engine::Impl {
                 reserve_locked(ulen);
               }
             }
-            if (!packed) file.pixels16(reinterpret_cast<uint16_t*>(s.raw_cpu) + off);
+            if (!packed) file.pixels16(reinterpret_cast<uint16_t*>(s.raw_cpu) + off, frame);
           } else {
             packed = packable && (low12 || pack12::fits12(samples, npix));
             {
@@ -729,7 +747,7 @@ struct Engine::Impl {
             if (packed) {
               pack12::pack_stream(samples, npix, reinterpret_cast<uint8_t*>(dst));
             } else {
-              file.pixels16(dst);
+              file.pixels16(dst, frame);
             }
           }
         } catch (...) {
@@ -769,7 +787,7 @@ struct Engine::Impl {
   // (seeds_*: per-thread cache of reference_seeds for build_and_run; slot threads run concurrently.)
   static inline thread_local std::vector<Seed> seeds_cache_;
   static inline thread_local int seeds_w_ = 0, seeds_h_ = 0;
-  void build_and_run(Slot& s, int mode, StageTimes* acc) {
+  void build_and_run(Slot& s, int mode, StageTimes* acc, BatchMark* mark = nullptr) {
     const int nl = (int)s.live.size();
     uint8_t* hb = s.h_blob;
     auto* stats = reinterpret_cast<SliceStats*>(hb + s.off_stats);
@@ -963,6 +981,7 @@ struct Engine::Impl {
     rsrc.nrd = ncanv;
     launch_jpeg(s.d_canvas, d_jd, ncanv, cw, ch, divs, s.jw, s.d_out, s.d_sizes, s.stream, &rsrc);
     check_hip(hipEventRecord(s.ev2, s.stream), "event");
+    if (mark) mark->enq = now_s();
     wait_batch(s, s.ev2, t_enq, nl);
     if (acc && !inline_up) {  // an inline small upload records no split events
       float a = 0, b = 0;
@@ -1010,7 +1029,8 @@ struct Engine::Impl {
   // the host-pool priority (earlier batches first, also across queued runs).
   void process_batch(Slot& s, const std::vector<WorkItem>& items, const IoDirs& dirs, size_t batch, uint64_t prio,
                      size_t first, size_t count, std::vector<SliceStatus>& status, StageTimes& acc,
-                     std::mutex& acc_m, const std::function<void(size_t)>& on_start) {
+                     std::mutex& acc_m, const std::function<void(size_t)>& on_start, BatchMark* mark = nullptr) {
+    if (mark) mark->claim = now_s();
     s.raw_used = 0;
     s.loaded.assign(count, LoadedSlice{});
     if (!s.allocs) s.allocs.reset(new Slot::Alloc[2 * (size_t)s.cap_slices]);  // ≤ 2 per slice (a hole)
@@ -1061,6 +1081,7 @@ struct Engine::Impl {
       }
       tg.wait(small_batch_spin(count));
     }
+    if (mark) mark->loaded = now_s();
     s.live.clear();
     for (size_t i = 0; i < count; ++i)
       if (s.loaded[i].ok) s.live.push_back((int)i);
@@ -1074,7 +1095,8 @@ struct Engine::Impl {
         if (!upload_error.empty()) throw DeviceError(upload_error);
         if (fault_plan().fail_batch == (int64_t)batch)
           throw DeviceError("injected fault: device batch failure");
-        build_and_run(s, 0, &local);
+        build_and_run(s, 0, &local, mark);
+        if (mark) mark->gpu = now_s();
       } catch (const std::exception& e) {
         for (int i : s.live) status[first + i] = SliceStatus{kSliceDeviceError, e.what()};
         s.live.clear();
@@ -1161,6 +1183,7 @@ struct Engine::Impl {
           2 * prio + 1, &write_cpu_ns, creates ? cfg.create_writers : 0);
       tg.wait(small_batch_spin(count));
     }
+    if (mark) mark->end = now_s();
     std::lock_guard<std::mutex> g(acc_m);
     acc.load_s += load_ns.load() * 1e-9;
     acc.write_s += write_ns.load() * 1e-9;
@@ -1203,6 +1226,7 @@ struct Engine::Impl {
     bool done = false;   // guarded by job_m
     std::exception_ptr err;
     std::mutex err_m;
+    std::vector<BatchMark> marks;  // NM03_BATCH_TRACE: one per batch (each written by its slot only)
   };
   std::vector<std::thread> workers;
   std::mutex job_m, single_m;
@@ -1236,6 +1260,14 @@ struct Engine::Impl {
     if (j.acc.jpeg_fallbacks) log_warn(std::to_string(j.acc.jpeg_fallbacks) + " JPEG(s) exceeded GPU capacity; CPU-encoded");
     log_info("run: " + std::to_string(j.items->size()) + " slices in " + std::to_string(j.acc.batches) + " batches, " +
              std::to_string(j.acc.wall_s * 1e3) + " ms, " + std::to_string(j.acc.slices_failed) + " failed");
+    if (!j.marks.empty()) {
+      std::string t = "batch trace (ms since submit: claim / loaded / enqueued / gpu done / end):";
+      auto ms = [&](double v) { return v > 0 ? std::to_string((int)((v - j.t0) * 1e4) / 10.0).substr(0, 6) : std::string("-"); };
+      for (const BatchMark& m : j.marks)
+        t += "\n  slot " + std::to_string(m.slot) + " [" + std::to_string(m.first) + "+" + std::to_string(m.count) + "] " +
+             ms(m.claim) + " / " + ms(m.loaded) + " / " + ms(m.enq) + " / " + ms(m.gpu) + " / " + ms(m.end);
+      log_msg(LogLevel::kError, t);  // printed whenever the trace was asked for
+    }
     {
       std::lock_guard<std::mutex> g(job_m);
       j.done = true;
@@ -1261,7 +1293,12 @@ struct Engine::Impl {
     if (!slots[slot_index]) {  // built lazily (see the constructor); this thread is its only user
       bool ok = true;
       try {
-        slots[slot_index] = make_slot();
+        const double tb = now_s();
+        std::string split;
+        slots[slot_index] = make_slot(batch_trace() ? &split : nullptr);
+        if (batch_trace())
+          log_msg(LogLevel::kError, "slot " + std::to_string(slot_index) + " built on its worker: " +
+                                        std::to_string((now_s() - tb) * 1e3) + " ms (" + split + ")");
       } catch (const std::exception& e) {
         log_warn("engine slot " + std::to_string(slot_index) + " unavailable, running with fewer streams: " + e.what());
         ok = false;
@@ -1294,8 +1331,14 @@ struct Engine::Impl {
       const int64_t c0 = thread_cpu_ns();
       try {
         const auto [first, count] = j->batches[b];
+        BatchMark* mk = j->marks.empty() ? nullptr : &j->marks[b];
+        if (mk) {
+          mk->slot = (int)slot_index;
+          mk->first = first;
+          mk->count = count;
+        }
         process_batch(*s, *j->items, *j->dirs, b, j->seq0 + b, first, count, j->status, j->acc, j->acc_m,
-                      j->on_start);
+                      j->on_start, mk);
       } catch (...) {
         std::lock_guard<std::mutex> g(j->err_m);
         if (!j->err) j->err = std::current_exception();
@@ -1319,6 +1362,7 @@ struct Engine::Impl {
     const size_t B = batch_cap > 0 ? std::min<size_t>((size_t)batch_cap, (size_t)cfg.batch_size) : (size_t)cfg.batch_size;
     j->batches = plan_batches(j->items->size(), B);
     j->remaining = j->batches.size();
+    if (batch_trace()) j->marks.resize(j->batches.size());
     {
       std::lock_guard<std::mutex> g(job_m);
       j->seq0 = seq_next;

@@ -26,6 +26,8 @@ namespace nm03 {
 
 using namespace nm03::gpu;
 
+// Every frame of every file, stacked in file order: a series of single-frame slices, or a
+// multi-frame file (one file = one volume), or a mix of both.
 VolumeInput load_volume(const std::vector<std::string>& files) {
   VolumeInput v;
   std::vector<uint8_t> buf;
@@ -41,12 +43,16 @@ VolumeInput load_volume(const std::vector<std::string>& files) {
       v.intercept = h.intercept;
       v.spacing_x = h.spacing_x;
       v.spacing_y = h.spacing_y;
-      v.raw.resize((size_t)v.w * v.h * files.size());
+      v.raw.reserve((size_t)v.w * v.h * files.size());
     } else if (h.cols != v.w || h.rows != v.h) {
       throw SliceError("volume slices differ in size: " + files[z]);
     }
-    dicom::copy_pixels16(h, buf.data(), n, v.raw.data() + z * (size_t)v.w * v.h);
-    ++v.d;
+    const size_t plane = (size_t)v.w * v.h;
+    for (int f = 0; f < h.frames; ++f) {
+      v.raw.resize(plane * (size_t)(v.d + 1));
+      dicom::copy_pixels16(h, buf.data(), n, v.raw.data() + (size_t)v.d * plane, f);
+      ++v.d;
+    }
   }
   return v;
 }
@@ -265,6 +271,7 @@ struct VolumeRunner::Impl {
   hipEvent_t e0 = nullptr, e1 = nullptr;
   explicit Impl(int dev) : device(dev) {
     check_hip(hipSetDevice(device), "hipSetDevice");
+    preload_kernels();  // every code object, before the first launch (kernels.h)
     check_hip(hipEventCreate(&e0), "event");
     check_hip(hipEventCreate(&e1), "event");
   }

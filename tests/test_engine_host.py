@@ -180,3 +180,32 @@ def test_host_only_many_queued_runs(native, cohort_root, tmp_path):
         assert not msgs
     for t in trees:
         assert len(_tree_bytes(t)) == 2 * len(t)
+
+
+def test_host_only_compressed_and_photometric_forms(native, tmp_path):
+    """Round 5 import forms through the engine's loader (host path): Deflated Explicit VR LE, RLE
+    Lossless and MONOCHROME1 load like plain files; a multi-frame file is a per-slice load error by
+    default and loads when a frame is selected; a JPEG-family file is skipped and counted."""
+    import numpy as np
+    d = tmp_path / "in"
+    d.mkdir()
+    good = native.phantom_slice(256, 256, 1, 3, 10, 7)
+    forms = [dict(syntax="deflated"), dict(syntax="rle"), dict(photometric="MONOCHROME1"), dict(syntax="rle", photometric="MONOCHROME1")]
+    paths = []
+    for k, kw in enumerate(forms, 1):
+        p = d / f"1-{k}.dcm"
+        p.write_bytes(native.dicom_bytes(good, bits_stored=12, **kw))
+        paths.append(p)
+    mf = d / "1-9.dcm"
+    mf.write_bytes(native.dicom_bytes(np.stack([good, good, good]), bits_stored=12, syntax="rle"))
+    paths.append(mf)
+    out = tmp_path / "out"
+    out.mkdir()
+    items = [(str(p), str(out)) for p in paths]
+    st, _ = _engine(native).run(items)
+    assert [c for c, _ in st] == [0, 0, 0, 0, 1]
+    assert "Multi-frame DICOM (3 frames)" in st[4][1]
+    st, _ = _engine(native, frame=1).run(items)
+    assert [c for c, _ in st] == [0] * 5
+    st, _ = _engine(native, frame=3).run(items)
+    assert [c for c, _ in st] == [0, 0, 0, 0, 1] and "Frame 3 requested" in st[4][1]
