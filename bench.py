@@ -70,7 +70,7 @@ def _scratch():
     """Where the synthetic cohort and the JPEGs live: tmpfs (/dev/shm) when writable, else /tmp.
 
     The box's root filesystem is an overlay whose metadata/journal path serialises small-file
-    writes across processes (tools/io_scaling.sh: 4 processes reach ~2.6x one process on /tmp,
+    writes across processes (round-1 I/O scaling probe: 4 processes reach ~2.6x one process on /tmp,
     ~4x on /dev/shm; profiles/io_scaling.txt). Every byte is still read and written through the
     same syscalls; tmpfs only removes that container artefact, the analogue of a local NVMe with a
     warm page cache where the reference's cohort lives."""

@@ -49,7 +49,7 @@ AppConfig parse_args(int argc, char** argv, const std::string& which);
 // releasing device memory and contexts (≈70–130 ms of a cold CLI run). main registers an exit
 // handler before any HIP call (arm_fast_exit; parse_args does) and ends with `return cli_exit(rc)`:
 // a profiler that finalises when main returns (rocprofv3 writes its results there; a CLI that called
-// exit() from inside main lost them, tools/exit_order) and every handler registered after the
+// exit() from inside main lost them, profiles/r4/exit_order/) and every handler registered after the
 // armed one still run, then the armed handler _exits before the shared libraries' static
 // destructors (HIP's teardown, which faulted under rocprofv3: profiles/r4/probe/). NM03_FAST_EXIT=0:
 // normal exit with full teardown.

@@ -65,8 +65,9 @@ class Comm {
   // asynchronous copies on `stream` and one synchronisation per call.
   virtual void sendrecv_device(const void* send, size_t sbytes, int dst, void* recv, size_t rbytes, int src,
                                void* stream);
-  // Sums the int64 at device address `v` over all ranks (in place) and returns the total on the
-  // host once everything enqueued on `stream` before it has completed (a bounded wait).
+  // Sums the int64 at device address `v` over all ranks — in place: device *v holds the total for
+  // work enqueued on `stream` afterwards (every backend) — and returns the total on the host once
+  // everything enqueued on `stream` before it has completed (a bounded wait).
   virtual int64_t allreduce_sum_i64_device(int64_t* v, void* stream);
   // True when the device forms above move data device to device (RCCL).
   virtual bool device_native() const { return false; }
@@ -81,6 +82,26 @@ class Comm {
   // always do). Lets a driver bring a communicator up without the flag — a failed init must not
   // abort the job when a fallback exists — and attach it once every rank agreed.
   virtual void set_abort_segment(std::shared_ptr<ShmSegment>) {}
+  // Blocks (bounded) until the transport is usable: RCCL settles a non-blocking
+  // ncclCommInitRankConfig. Every collective does it first anyway; no-op for the host comms.
+  virtual void ready() {}
+
+  // ---- deferred data plane (launch_ranks' RCCL ranks, make_deferred_rccl_comm; no-ops elsewhere) --
+  // Starts the device transport's initialisation (the ncclUniqueId hand-off through the segment and
+  // a non-blocking ncclCommInitRankConfig) on the calling thread, which must already have brought up
+  // HIP on the rank's device, and returns: RCCL's start-up then overlaps the engine's construction
+  // and the run instead of preceding the rank's planning. Errors surface at promote().
+  virtual void start_data_plane() {}
+  // Collective (every rank at the same point): waits (bounded, abort-aware) until the device
+  // transport is up and carries every later collective on it. Before it, host-buffer collectives
+  // use the shared-memory control plane; device-memory ones promote implicitly.
+  virtual void promote() {}
+  struct DataPlaneTimes {
+    double start_s = -1;      // start_data_plane's begin, seconds after the comm was created (-1: never)
+    double wait_s = 0;        // time promote() blocked waiting for the transport
+    double init_upper_s = 0;  // start → transport usable, upper bound (observed at promote)
+  };
+  virtual DataPlaneTimes data_plane_times() const { return {}; }
 
   // Helpers built on the primitives.
   void broadcast_bytes(std::vector<uint8_t>& buf, int root);                        // resizes on non-roots
@@ -147,8 +168,16 @@ std::unique_ptr<Comm> make_host_comm(std::shared_ptr<ShmSegment> seg, int rank, 
 // RCCL communicator for `rank` of `size`, bound to HIP device `device`. `unique_id` is the
 // 128-byte ncclUniqueId produced by rank 0 (rccl_unique_id()). `seg` (optional) supplies the job
 // abort flag that bounded waits also watch.
+// `settle_now` false: ncclCommInitRankConfig is only started; ready() / the first collective settle it.
 std::unique_ptr<Comm> make_rccl_comm(int rank, int size, const std::vector<uint8_t>& unique_id, int device,
-                                     std::shared_ptr<ShmSegment> seg = nullptr, double timeout_s = -1);
+                                     std::shared_ptr<ShmSegment> seg = nullptr, double timeout_s = -1,
+                                     bool settle_now = true);
+// The communicator launch_ranks gives an RCCL rank: the shared-memory control plane (host comm over
+// `seg`) for the start-up collectives, RCCL created by start_data_plane() — on the rank's start-up
+// thread, right after hipInit — and used from promote() on and for every device collective. Keeps
+// RCCL's initialisation off the critical path of a cold run.
+std::unique_ptr<Comm> make_deferred_rccl_comm(int rank, int size, int device, std::shared_ptr<ShmSegment> seg,
+                                              double timeout_s = -1);
 std::vector<uint8_t> rccl_unique_id();
 
 // Single-rank communicator (no-ops).

@@ -87,6 +87,12 @@ struct EngineConfig {
   // 4 creating at once and 35–44 µs with 16 (tools/create_probe.cpp, profiles/r4/create_probe/);
   // the other workers take the next batches' loads meanwhile.
   int create_writers = 4;
+  // Slots 1..streams-1 built by their own worker threads while slot 0 already runs (true), or all
+  // in the constructor (false, default). Measured in round 5 (profiles/r5/cold/): a slot's HW-queue
+  // creation (hipStreamCreate, 10–50 ms on a cold process) and its pinned/device allocations hold
+  // HIP runtime locks, so lazily built slots stalled the first batch's copies and launches for
+  // 20–40 ms; built up front, a cold 465-slice pass takes ≈ 4 ms after the constructor.
+  bool lazy_slots = false;
 };
 
 // Everything test_pipeline exports / tests inspect for one slice (host copies).
@@ -150,5 +156,12 @@ class Engine {
 
 // Device count without initialising anything else (hipGetDeviceCount).
 int device_count();
+
+// Creates `n` non-blocking HIP streams on `device` now and parks them for the next engines built on
+// that device (one per slot plus the shared upload stream: streams + 1). A stream costs 3–4 ms to
+// create and the first ones a HW queue each, 20 ms then ≈ 9 ms (tools/queue_probe.cpp,
+// profiles/r5/queues/): a cold CLI reserves them on its start-up thread right after hipInit, while
+// rank 0 still plans, so the engine constructor only allocates buffers. Returns the seconds spent.
+double reserve_streams(int device, int n);
 
 }  // namespace nm03

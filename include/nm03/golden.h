@@ -60,15 +60,17 @@ inline std::vector<uint8_t> binary_threshold(const std::vector<float>& s, float 
 std::vector<uint8_t> region_grow(const std::vector<uint8_t>& band, int w, int h, const std::vector<Seed>& seeds,
                                  int connectivity);
 // Square structuring element of odd `size`, out-of-image samples ignored (A.7).
-std::vector<uint8_t> dilate(const std::vector<uint8_t>& m, int w, int h, int size);
-std::vector<uint8_t> erode(const std::vector<uint8_t>& m, int w, int h, int size);
+// `disc`: the digital disc of radius size/2 (PipelineParams::se_shape) instead of the square.
+std::vector<uint8_t> dilate(const std::vector<uint8_t>& m, int w, int h, int size, bool disc = false);
+std::vector<uint8_t> erode(const std::vector<uint8_t>& m, int w, int h, int size, bool disc = false);
 // SegmentationRenderer border: label pixels with a 0 within Chebyshev radius r (image space).
 std::vector<uint8_t> border(const std::vector<uint8_t>& m, int w, int h, int radius);
 
 // 3D variants (BASELINE config 5): 6/26-connected region growing, cube dilation.
 std::vector<uint8_t> region_grow3d(const std::vector<uint8_t>& band, int w, int h, int d,
                                    const std::vector<Seed>& seeds, int connectivity);
-std::vector<uint8_t> dilate3d(const std::vector<uint8_t>& m, int w, int h, int d, int size);
+// `ball`: the digital ball of radius size/2 instead of the size³ cube.
+std::vector<uint8_t> dilate3d(const std::vector<uint8_t>& m, int w, int h, int d, int size, bool ball = false);
 
 // Renderers (A.9) onto an out_w×out_h black canvas.
 std::vector<uint8_t> render_gray(const std::vector<float>& values, const RenderGeom& g, float lo, float hi);

@@ -69,6 +69,7 @@ struct PipeConsts {
   int connectivity;  // 4 | 8
   int dilation_size, erosion_size, border_radius;
   uint32_t outputs;  // bit set of kOut* below
+  int se_disc;       // PipelineParams::se_shape == kSeDisc: disc structuring element (else square)
 };
 
 enum : uint32_t {

@@ -91,8 +91,9 @@ size_t morph3d_scratch_words(int w, int h, int d);
 void border_volume(const uint64_t* src, uint64_t* dst, int w, int h, int d, int radius, hipStream_t stream,
                    uint64_t* scratch = nullptr);
 // Cube dilation of a bit volume (size odd), separable; `tmp` same size as the volume.
+// `ball`: the digital ball of radius size/2 (one pass, dilate_ball_kernel) instead of the size³ cube.
 void dilate_volume(const uint64_t* src, uint64_t* dst, uint64_t* tmp, int w, int h, int d, int size,
-                   hipStream_t stream, uint64_t* scratch = nullptr);
+                   hipStream_t stream, uint64_t* scratch = nullptr, bool ball = false);
 // z-slab boundary step (volume_slabs.h), one plane: add = band ∧ touch(nb) ∧ ¬region, region |= add,
 // *added += popcount(add); touch = nb (6-connectivity) or its 3×3 in-plane dilation (26).
 void launch_slab_seed(const uint64_t* band, uint64_t* region, const uint64_t* nb, int w, int h, bool conn26,

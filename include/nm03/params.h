@@ -32,6 +32,12 @@ struct PipelineParams {
   // Dilation::create(3) / Erosion::create(3)                      main_sequential.cpp:250, test_pipeline.cpp:119
   int dilation_size = 3;
   int erosion_size = 3;
+  // Structuring element of Dilation/Erosion (2D) and of the 3D dilation: FAST's shape is not pinned
+  // by the reference (SURVEY App. A.7 / §7.6 risk 1), so it is a flag. kSeSquare (default): the
+  // size×size square / size³ cube; kSeDisc: the digital disc / ball of radius r = size/2, i.e. the
+  // offsets with dx² + dy² (+ dz²) ≤ r² (size 3: the 4-neighbour cross). Out-of-image samples are
+  // ignored either way.
+  int se_shape = 0;
   // Reject slices with width<100 || height<100                    main_sequential.cpp:189-192
   int min_dim = 100;
   // Apply DICOM modality rescale (slope/intercept) if present.
@@ -39,6 +45,8 @@ struct PipelineParams {
   // Multi-frame files (dicom::select_frame): -1 rejects them (default), k ≥ 0 imports frame k.
   int frame = -1;
 };
+
+enum SeShape : int { kSeSquare = 0, kSeDisc = 1 };
 
 struct RenderParams {
   // RenderToImage::create(Color::Black(), 512, 512)               main_sequential.cpp:258

@@ -49,6 +49,9 @@ class SlabGrower {
   // (nearest plane last / first, possibly fewer than size/2 at the volume's ends).
   virtual void dilate(int size, const std::vector<std::vector<uint64_t>>& below,
                       const std::vector<std::vector<uint64_t>>& above) = 0;
+  // Structuring element of dilate(): the digital ball of radius size/2 instead of the cube
+  // (PipelineParams::se_shape; the r-plane halo covers both).
+  bool ball = false;
 };
 
 struct SlabStats {

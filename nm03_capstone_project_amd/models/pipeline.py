@@ -34,6 +34,7 @@ class PipelineConfig:
     erosion_size: int = 3
     min_dim: int = 100
     apply_rescale: bool = True
+    se_shape: int = 0  # structuring element of dilation/erosion: 0 square (default), 1 disc (params.h SeShape)
     frame: int = -1  # multi-frame DICOM: -1 rejects such files, k >= 0 imports frame k (dicom.h select_frame)
     # render / export
     out_width: int = 512
@@ -54,7 +55,7 @@ class PipelineConfig:
 
     _PIPE = ("norm_low", "norm_high", "norm_min", "norm_max", "clip_min", "clip_max", "median_window",
              "sharpen_gain", "sharpen_sigma", "sharpen_mask", "srg_min", "srg_max", "srg_connectivity",
-             "dilation_size", "erosion_size", "min_dim", "apply_rescale", "frame")
+             "dilation_size", "erosion_size", "min_dim", "apply_rescale", "frame", "se_shape")
     _RENDER = ("out_width", "out_height", "label_opacity", "border_opacity", "border_radius", "jpeg_quality")
 
     def pipeline_params(self):

@@ -51,4 +51,4 @@ class VolumePipeline:
     def golden(self, band, seeds):
         n = native()
         region = n.golden_region_grow3d(band, list(seeds), self.connectivity)
-        return region, n.golden_dilate3d(region, self.dilation)
+        return region, n.golden_dilate3d(region, self.dilation, self.config.se_shape == 1)

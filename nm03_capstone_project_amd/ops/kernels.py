@@ -119,14 +119,15 @@ def region_grow3d(band, seeds=(), connectivity=6, region=None):
     return unpack_bits(rw, w), sweeps
 
 
-def dilate3d(mask, size=7):
-    """Cube dilation (size×size×size, out-of-volume samples ignored) of a bool [D, H, W] CUDA mask."""
+def dilate3d(mask, size=7, ball=False):
+    """Cube dilation (size×size×size; `ball`: the digital ball of radius size//2) of a bool
+    [D, H, W] CUDA mask, out-of-volume samples ignored."""
     if mask.dim() != 3 or not mask.is_cuda:
         raise ValueError("mask must be a CUDA tensor [D, H, W]")
     d, h, w = mask.shape
     src = pack_bits(mask.bool()).contiguous()
     dst, tmp = torch.empty_like(src), torch.empty_like(src)
-    native().k_dilate3d(src.data_ptr(), dst.data_ptr(), tmp.data_ptr(), w, h, d, int(size), _stream())
+    native().k_dilate3d(src.data_ptr(), dst.data_ptr(), tmp.data_ptr(), w, h, d, int(size), _stream(), bool(ball))
     return unpack_bits(dst, w)
 
 

@@ -59,6 +59,38 @@ def erode(mask, size=3):
     return ~(F.max_pool2d(x, size, stride=1, padding=r)[0, 0] > 0.5)
 
 
+def disc_se(size, dims=2):
+    """The digital disc (dims=2) / ball (dims=3) of radius size // 2: offsets with |d|² ≤ r²."""
+    r = size // 2
+    ax = torch.arange(-r, r + 1, dtype=torch.int64)
+    grids = torch.meshgrid(*([ax] * dims), indexing="ij")
+    return sum(g * g for g in grids) <= r * r
+
+
+def dilate_disc(mask, size=3):
+    """Binary dilation with the disc SE as a conv2d count (zero padding = out-of-image ignored)."""
+    r = size // 2
+    k = disc_se(size).to(torch.float64)[None, None].to(mask.device)
+    return F.conv2d(mask.to(torch.float64)[None, None], k, padding=r)[0, 0] > 0.5
+
+
+def erode_disc(mask, size=3):
+    """Binary erosion with the disc SE: every in-image sample under the disc set. Out-of-image samples
+    are ignored: the count of set samples equals the count of in-image samples under the disc."""
+    r = size // 2
+    k = disc_se(size).to(torch.float64)[None, None].to(mask.device)
+    hits = F.conv2d(mask.to(torch.float64)[None, None], k, padding=r)[0, 0]
+    inside = F.conv2d(torch.ones_like(mask, dtype=torch.float64)[None, None], k, padding=r)[0, 0]
+    return hits > inside - 0.5
+
+
+def dilate_ball(mask, size=7):
+    """3D binary dilation with the ball SE as a conv3d count, [D, H, W]."""
+    r = size // 2
+    k = disc_se(size, 3).to(torch.float64)[None, None].to(mask.device)
+    return F.conv3d(mask.to(torch.float64)[None, None], k, padding=r)[0, 0] > 0.5
+
+
 def border(mask, radius=2):
     return mask & ~erode(mask, 2 * radius + 1)
 

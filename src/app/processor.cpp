@@ -7,12 +7,14 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <fstream>
 #include <iomanip>
 #include <iostream>
+#include <mutex>
 #include <sstream>
 #include <thread>
 
@@ -49,6 +51,7 @@ void usage(const std::string& which) {
             << "  --median-window K      3|5|7|9 (default 7)\n"
             << "  --srg-connectivity C   4|8 (2D) / 6|26 (3D)\n"
             << "  --dilation-size S      (default 3; 7 in --mode 3d)    --erosion-size S (default 3)\n"
+            << "  --se-shape square|disc structuring element of dilation/erosion (3D: cube|ball; default square)\n"
             << "  --quality Q            JPEG quality (default 75)\n"
             << "  --mode 2d|3d           3d: whole series as a volume (SRG 6-conn + cube dilation)\n"
             << "  --split-volume         3d: each volume split into z-slabs over all ranks (halo exchange)\n"
@@ -165,6 +168,14 @@ AppConfig parse_args(int argc, char** argv, const std::string& which) {
     }
     else if (a == "--resume") c.engine.resume = true;
     else if (a == "--frame") c.engine.pipe.frame = std::atoi(val().c_str());
+    else if (a == "--se-shape") {
+      const std::string v = val();
+      if (v != "square" && v != "disc") {
+        std::cerr << "--se-shape must be square or disc" << std::endl;
+        std::exit(2);
+      }
+      c.engine.pipe.se_shape = v == "disc" ? kSeDisc : kSeSquare;
+    }
     else if (a == "--split-volume") c.split_volume = true;
     else {
       std::cerr << "unknown option " << a << " (see --help)" << std::endl;
@@ -408,36 +419,81 @@ int parallel_rank(const AppConfig& cfg, int rank, int size, Comm& comm, int devi
   EngineConfig ec = cfg.engine;
   ec.device = device;
   const double t_setup = now_s();
-  // Cold start: the HIP runtime and the device context come up on a helper thread while rank 0
-  // plans the cohort (and scans the slice headers for the buffer size); the engine is built once
-  // both are done.
-  double hip_init_s = 0, engine_ctor_s = 0, kernel_load_s = 0;
-  std::thread warm([device, &hip_init_s, &kernel_load_s] {
+  // Cold start (round 5). ONE start-up thread owns every HIP call until the engine exists: it
+  // brings up the runtime and the device context, loads every kernel code object, starts RCCL's
+  // non-blocking initialisation (N > 1), and — as soon as the main thread hands it the engine
+  // configuration — builds the whole engine: every slot's streams, events, pinned and device
+  // buffers. Meanwhile the main thread plans (rank 0: patient discovery, output wipe, header scan),
+  // exchanges the plan over the shared-memory control plane and computes the rank's CPU partition.
+  // Nothing else touches HIP before the first batch: in round 4, slots built on their workers held
+  // the runtime's locks (HW-queue creation 10–50 ms) while the first batch tried to copy and
+  // launch, and a cold 465-slice pass took 37–70 ms instead of ≈ 4 ms (profiles/r5/cold/).
+  struct Startup {
+    std::mutex m;
+    std::condition_variable cv;
+    bool have_cfg = false, cancel = false, done = false;
+    EngineConfig ec;
+    std::unique_ptr<Engine> engine;
+    std::string error;
+    double hip_init_s = 0, kernel_load_s = 0, streams_s = 0, engine_ctor_s = 0;
+  } su;
+  const int nstreams = std::max(1, cfg.engine.streams) + 1;  // slots + the shared upload stream
+  std::thread warm([&su, &comm, device, nstreams] {
     const double t0 = now_s();
-    (void)hipSetDevice(device);
-    void* p = nullptr;
-    if (hipMalloc(&p, 4096) == hipSuccess) (void)hipFree(p);
-    // Also the runtime's first stream (hardware queue) and first pinned allocation, which the
-    // engine's first slot would otherwise pay for after planning: the queue goes back to the
-    // runtime's pool on destroy and is reused by the engine's streams.
-    hipStream_t st = nullptr;
-    if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) == hipSuccess) (void)hipStreamDestroy(st);
-    void* h = nullptr;
-    if (hipHostMalloc(&h, 4096, hipHostMallocDefault) == hipSuccess) (void)hipHostFree(h);
-    hip_init_s = now_s() - t0;
-    // Then the kernels' code objects, which HIP would otherwise load at their first launches,
-    // inside the first batch. Done before the engine exists: lazy code-object loading racing with
-    // kernel launches from the engine's threads faulted inside the HSA runtime (gpurun_out/r4j).
-    const double t1 = now_s();
-    gpu::preload_kernels();
-    kernel_load_s = now_s() - t1;
+    std::string err;
+    try {
+      gpu::check_hip(hipSetDevice(device), "hipSetDevice");
+      void* p = nullptr;
+      gpu::check_hip(hipMalloc(&p, 4096), "hipMalloc");
+      (void)hipFree(p);
+      su.hip_init_s = now_s() - t0;
+      // The kernels' code objects (HIP would load each translation unit's at its first launch):
+      // loaded here, on one thread, before any launch (kernels.h preload_kernels).
+      const double t1 = now_s();
+      gpu::preload_kernels();
+      su.kernel_load_s = now_s() - t1;
+      // The engine's streams (HW queues), which need only the slot count: created before the
+      // configuration arrives, while rank 0 may still be planning.
+      su.streams_s = reserve_streams(device, nstreams);
+    } catch (const std::exception& e) {
+      err = e.what();
+    }
+    // RCCL's initialisation proceeds in its own thread from here on (non-blocking communicator);
+    // the collectives use the shared-memory control plane until promote().
+    if (err.empty()) comm.start_data_plane();
+    std::unique_lock<std::mutex> g(su.m);
+    su.cv.wait(g, [&] { return su.have_cfg || su.cancel; });
+    if (!su.cancel && err.empty()) {
+      EngineConfig ec = su.ec;
+      g.unlock();
+      const double t2 = now_s();
+      std::unique_ptr<Engine> e;
+      try {
+        e = std::make_unique<Engine>(ec);
+      } catch (const std::exception& ex) {
+        err = ex.what();
+      }
+      g.lock();
+      su.engine_ctor_s = now_s() - t2;
+      su.engine = std::move(e);
+    }
+    su.error = err;
+    su.done = true;
+    su.cv.notify_all();
   });
   struct Joiner {
+    Startup& su;
     std::thread& t;
     ~Joiner() {
+      {
+        std::lock_guard<std::mutex> g(su.m);
+        su.cancel = true;
+      }
+      su.cv.notify_all();
       if (t.joinable()) t.join();
     }
-  } joiner{warm};
+  } joiner{su, warm};
+  double engine_wait_s = 0;
   std::unique_ptr<Engine> engine_p;
   std::vector<RankDevice> devices;
   double t_start = 0, setup_s = 0;
@@ -509,7 +565,6 @@ int parallel_rank(const AppConfig& cfg, int rank, int size, Comm& comm, int devi
       // Buffers sized for the largest slice of the cohort (headers scanned by rank 0) instead of
       // the 512² maximum: less pinned memory to allocate and register at start-up.
       if (seen_dim > 0) ec.max_dim = std::min(gpu::kMaxSliceDim, std::max(64, (int)((seen_dim + 63) / 64 * 64)));
-      warm.join();
       // Where this rank runs: its GPU's PCI bus id, and a CPU partition of that GPU's NUMA node
       // disjoint from every other rank's, with a pool sized to it and to the rank's share of the
       // CPU budget (the reference's one machine-wide omp_set_num_threads(16), main_parallel.cpp:401).
@@ -527,8 +582,8 @@ int parallel_rank(const AppConfig& cfg, int rank, int size, Comm& comm, int devi
         me.node = part.node;
         me.cpus = numa::format_cpulist(part.cpus);
         me.threads = ec.threads;
-        me.transport_size = comm.transport_size();
-        me.transport_device = comm.transport_device();
+        // (the transport's own view — ncclCommCount / ncclCommCuDevice — is filled in after
+        // promote(), once RCCL is up)
         devices = gather_rank_devices(comm, me);
         const std::string dup = duplicate_device(devices);
         if (!dup.empty() && LaunchOptions::from_env().device_override < 0) {
@@ -538,16 +593,23 @@ int parallel_rank(const AppConfig& cfg, int rank, int size, Comm& comm, int devi
           return 1;
         }
       }
-      // An engine that fails to come up on one rank must not leave the others blocked in the next
-      // collective: agree on it before going on.
+      // Hand the configuration to the start-up thread and wait for its engine. An engine that
+      // fails to come up on one rank must not leave the others blocked in the next collective:
+      // agree on it before going on.
       std::string setup_error;
-      const double t_ctor = now_s();
-      try {
-        engine_p = std::make_unique<Engine>(ec);
-      } catch (const std::exception& e) {
-        setup_error = e.what();
+      const double t_wait = now_s();
+      {
+        std::unique_lock<std::mutex> g(su.m);
+        su.ec = ec;
+        su.have_cfg = true;
+        su.cv.notify_all();
+        su.cv.wait(g, [&] { return su.done; });
+        engine_p = std::move(su.engine);
+        setup_error = su.error;
       }
-      engine_ctor_s = now_s() - t_ctor;
+      warm.join();
+      engine_wait_s = now_s() - t_wait;
+      if (!engine_p && setup_error.empty()) setup_error = "engine not built";
       int64_t setup_failed = setup_error.empty() ? 0 : 1;
       comm.allreduce_sum_i64(&setup_failed, 1);
       if (setup_failed) {
@@ -582,6 +644,9 @@ int parallel_rank(const AppConfig& cfg, int rank, int size, Comm& comm, int devi
     my_wall += now_s() - t0;  // this rank's own processing time (before waiting for the others)
     comm.barrier();
     double wall = now_s() - t0;
+    // RCCL (initialising since the start-up thread's hipInit) carries every collective from here
+    // on: the processing-time reduction, the status and metric all-gathers (N = 1: no-op).
+    comm.promote();
     comm.allreduce_max_f64(&wall, 1);
     proc_wall += wall;
     agg.load_s += t.load_s;
@@ -657,7 +722,6 @@ int parallel_rank(const AppConfig& cfg, int rank, int size, Comm& comm, int devi
       }
     }
   }
-  if (warm.joinable()) warm.join();
   if (reaper) reaper->drain();
   double tot = now_s() - t_start;
   comm.allreduce_max_f64(&tot, 1);
@@ -667,14 +731,27 @@ int parallel_rank(const AppConfig& cfg, int rank, int size, Comm& comm, int devi
                                            agg.write_s,       agg.write_cpu_s,   agg.slot_cpu_s,   (double)agg.jpeg_fallbacks};
   std::vector<double> all_rows(kNumRankFields * (size_t)size);
   comm.allgather(mine_row, sizeof(mine_row), all_rows.data());
+  // The transport's own view of every rank, now that it is up (RCCL: ncclCommCount / ncclCommCuDevice).
+  {
+    const int32_t tv[2] = {comm.transport_size(), comm.transport_device()};
+    std::vector<int32_t> all_tv(2 * (size_t)size);
+    comm.allgather(tv, sizeof(tv), all_tv.data());
+    for (size_t r = 0; r < devices.size() && r < (size_t)size; ++r) {
+      devices[r].transport_size = all_tv[2 * r];
+      devices[r].transport_device = all_tv[2 * r + 1];
+    }
+  }
+  const Comm::DataPlaneTimes dp = comm.data_plane_times();
   if (rank == 0) {
     std::vector<std::vector<double>> rows((size_t)size);
     for (int r = 0; r < size; ++r)
       rows[r].assign(all_rows.begin() + (size_t)r * kNumRankFields, all_rows.begin() + (size_t)(r + 1) * kNumRankFields);
     write_json(cfg.json, std::string("{\"mode\": \"parallel\", \"gpus\": ") + std::to_string(size) + ", \"backend\": \"" +
                              comm.backend() + "\", \"repeat\": " + std::to_string(cfg.repeat) + ", \"engine_setup_s\": " +
-                             fmt(setup_s) + ", \"hip_init_s\": " + fmt(hip_init_s) + ", \"engine_ctor_s\": " +
-                             fmt(engine_ctor_s) + ", \"kernel_load_s\": " + fmt(kernel_load_s) + ", \"wall_s\": " + fmt(tot) +
+                             fmt(setup_s) + ", \"hip_init_s\": " + fmt(su.hip_init_s) + ", \"engine_ctor_s\": " +
+                             fmt(su.engine_ctor_s) + ", \"streams_s\": " + fmt(su.streams_s) + ", \"engine_wait_s\": " + fmt(engine_wait_s) + ", \"kernel_load_s\": " +
+                             fmt(su.kernel_load_s) + ", \"comm_start_s\": " + fmt(dp.start_s) + ", \"comm_wait_s\": " +
+                             fmt(dp.wait_s) + ", \"comm_init_s\": " + fmt(dp.init_upper_s) + ", \"wall_s\": " + fmt(tot) +
                              ", \"processing_wall_s\": " + fmt(proc_wall) + ", \"slices\": " + std::to_string(total_slices) +
                              ", \"slices_ok\": " + std::to_string(total_ok) + ", \"slices_per_s\": " +
                              fmt(total_ok / std::max(proc_wall, 1e-9)) + ", \"rank0\": {\"load_s\": " + fmt(agg.load_s) +

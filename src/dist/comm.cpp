@@ -435,14 +435,9 @@ int launch_ranks(int n, const std::function<int(int, int, Comm&)>& body, const L
       try {
         std::unique_ptr<Comm> comm;
         if (backend == "rccl") {
-          std::vector<uint8_t> uid;
-          if (r == 0) {
-            uid = rccl_unique_id();
-            seg->publish_uid(uid);
-          } else {
-            uid = seg->wait_uid(r, opts.timeout_s > 0 ? opts.timeout_s : comm_timeout_s());
-          }
-          comm = make_rccl_comm(r, n, uid, opts.device_of(r), seg, opts.timeout_s);
+          // The body starts RCCL (start_data_plane) once HIP is up and promotes it after its
+          // start-up; until then the shared-memory control plane carries the collectives.
+          comm = make_deferred_rccl_comm(r, n, opts.device_of(r), seg, opts.timeout_s);
         } else {
           comm = make_host_comm(seg, r, opts.timeout_s);
         }

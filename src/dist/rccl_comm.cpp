@@ -8,7 +8,10 @@
 #include <unistd.h>
 
 #include <chrono>
+#include <condition_variable>
 #include <cstring>
+#include <exception>
+#include <mutex>
 #include <thread>
 
 #include "nm03/comm.h"
@@ -28,7 +31,7 @@ void hip_ck(hipError_t e, const char* what) {
 class RcclComm final : public Comm {
  public:
   RcclComm(int rank, int size, const std::vector<uint8_t>& uid, int device, std::shared_ptr<ShmSegment> seg,
-           double timeout_s)
+           double timeout_s, bool settle_now = true)
       : rank_(rank), size_(size), dev_(device), seg_(std::move(seg)),
         timeout_(timeout_s > 0 ? timeout_s : comm_timeout_s()) {
     if (uid.size() != sizeof(ncclUniqueId)) throw CommError("bad ncclUniqueId size");
@@ -43,12 +46,19 @@ class RcclComm final : public Comm {
       release();
       throw CommError(std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
     }
+    if (!settle_now) return;
     try {
-      settle("ncclCommInitRank");
+      ready();
     } catch (...) {
       release();
       throw;
     }
+  }
+  void ready() override {
+    if (settled_) return;
+    if (!comm_) throw CommError("RCCL communicator was aborted");
+    settle("ncclCommInitRank");
+    settled_ = true;
   }
   ~RcclComm() override { release(); }
   int rank() const override { return rank_; }
@@ -101,6 +111,7 @@ class RcclComm final : public Comm {
     if (dst < 0) sbytes = 0;
     if (src < 0) rbytes = 0;
     if (!sbytes && !rbytes) return;
+    ready();
     if (!comm_) throw CommError("RCCL communicator was aborted");
     if (seg_) seg_->check_abort(rank_);
     auto st = static_cast<hipStream_t>(stream);
@@ -110,6 +121,7 @@ class RcclComm final : public Comm {
     issue(ncclGroupEnd(), "ncclGroupEnd");
   }
   int64_t allreduce_sum_i64_device(int64_t* v, void* stream) override {
+    ready();
     if (!comm_) throw CommError("RCCL communicator was aborted");
     if (seg_) seg_->check_abort(rank_);
     auto st = static_cast<hipStream_t>(stream);
@@ -121,16 +133,19 @@ class RcclComm final : public Comm {
   }
   bool device_native() const override { return true; }
   int transport_size() const override {
+    if (!settled_) return -1;
     int n = -1;
     if (!comm_ || ncclCommCount(comm_, &n) != ncclSuccess) return -1;
     return n;
   }
   int transport_rank() const override {
+    if (!settled_) return -1;
     int r = -1;
     if (!comm_ || ncclCommUserRank(comm_, &r) != ncclSuccess) return -1;
     return r;
   }
   int transport_device() const override {
+    if (!settled_) return -1;
     int d = -1;
     if (!comm_ || ncclCommCuDevice(comm_, &d) != ncclSuccess) return -1;
     return d;
@@ -148,6 +163,7 @@ class RcclComm final : public Comm {
     wait("ncclAllReduce");
   }
   uint8_t* stage(size_t bytes) {
+    ready();
     if (!comm_) throw CommError("RCCL communicator was aborted");
     if (seg_) seg_->check_abort(rank_);
     if (bytes > cap_) {
@@ -227,13 +243,134 @@ class RcclComm final : public Comm {
   void* buf_ = nullptr;
   size_t cap_ = 0;
   int64_t* h_word_ = nullptr;  // pinned landing word of allreduce_sum_i64_device
+  bool settled_ = false;       // ncclCommInitRankConfig completed (ready())
+};
+
+// ---- deferred RCCL: shared-memory control plane until promote() ---------------------------------
+class DeferredRcclComm final : public Comm {
+ public:
+  DeferredRcclComm(int rank, int size, int device, std::shared_ptr<ShmSegment> seg, double timeout_s)
+      : rank_(rank), size_(size), dev_(device), seg_(seg), timeout_(timeout_s > 0 ? timeout_s : comm_timeout_s()),
+        host_(make_host_comm(seg, rank, timeout_s)), t_created_(mono_s()) {}
+  int rank() const override { return rank_; }
+  int size() const override { return size_; }
+  const char* backend() const override { return "rccl"; }
+
+  void broadcast(void* buf, size_t bytes, int root) override { plane().broadcast(buf, bytes, root); }
+  void allgather(const void* send, size_t bytes, void* recv) override { plane().allgather(send, bytes, recv); }
+  void allreduce_sum_i64(int64_t* v, size_t n) override { plane().allreduce_sum_i64(v, n); }
+  void allreduce_max_f64(double* v, size_t n) override { plane().allreduce_max_f64(v, n); }
+  void barrier() override { plane().barrier(); }
+  void sendrecv(const void* send, size_t sbytes, int dst, void* recv, size_t rbytes, int src) override {
+    plane().sendrecv(send, sbytes, dst, recv, rbytes, src);
+  }
+  // Device data always goes over RCCL (promoting implicitly: every rank reaches these together).
+  void sendrecv_device(const void* send, size_t sbytes, int dst, void* recv, size_t rbytes, int src,
+                       void* stream) override {
+    promote();
+    rccl_->sendrecv_device(send, sbytes, dst, recv, rbytes, src, stream);
+  }
+  int64_t allreduce_sum_i64_device(int64_t* v, void* stream) override {
+    promote();
+    return rccl_->allreduce_sum_i64_device(v, stream);
+  }
+  bool device_native() const override { return true; }
+  int transport_size() const override { return promoted_ ? rccl_->transport_size() : -1; }
+  int transport_rank() const override { return promoted_ ? rccl_->transport_rank() : -1; }
+  int transport_device() const override { return promoted_ ? rccl_->transport_device() : -1; }
+  void ready() override { promote(); }
+
+  void start_data_plane() override {
+    {
+      std::lock_guard<std::mutex> g(m_);
+      if (state_ != kIdle) return;
+      state_ = kStarting;
+      t_start_ = mono_s();
+    }
+    std::unique_ptr<Comm> c;
+    std::exception_ptr err;
+    try {
+      std::vector<uint8_t> uid;
+      if (rank_ == 0) {
+        uid = rccl_unique_id();
+        seg_->publish_uid(uid);
+      } else {
+        uid = seg_->wait_uid(rank_, timeout_);
+      }
+      c = make_rccl_comm(rank_, size_, uid, dev_, seg_, timeout_, /*settle_now=*/false);
+    } catch (...) {
+      err = std::current_exception();
+    }
+    {
+      std::lock_guard<std::mutex> g(m_);
+      rccl_ = std::move(c);
+      err_ = err;
+      state_ = err ? kFailed : kStarted;
+    }
+    cv_.notify_all();
+  }
+
+  void promote() override {
+    if (promoted_) return;
+    const double t0 = mono_s();
+    bool start_here = false;
+    {
+      std::lock_guard<std::mutex> g(m_);
+      start_here = state_ == kIdle;
+    }
+    if (start_here) start_data_plane();  // nobody started it: start it on this thread
+    {
+      // Bounded, abort-aware wait for a start-up thread still inside start_data_plane.
+      std::unique_lock<std::mutex> g(m_);
+      const double deadline = t0 + timeout_;
+      while (state_ == kStarting) {
+        cv_.wait_for(g, std::chrono::milliseconds(2));
+        if (state_ != kStarting) break;
+        seg_->check_abort(rank_);
+        if (mono_s() > deadline) {
+          seg_->raise_abort(rank_);
+          throw CommError("RCCL start-up timed out on rank " + std::to_string(rank_));
+        }
+      }
+      if (state_ == kFailed) std::rethrow_exception(err_);
+    }
+    rccl_->ready();  // settles ncclCommInitRankConfig (bounded, abort-aware)
+    promoted_ = true;
+    times_.wait_s = mono_s() - t0;
+    times_.start_s = t_start_ - t_created_;
+    times_.init_upper_s = mono_s() - t_start_;
+  }
+  DataPlaneTimes data_plane_times() const override { return times_; }
+  void set_abort_segment(std::shared_ptr<ShmSegment> seg) override {
+    if (rccl_) rccl_->set_abort_segment(std::move(seg));
+  }
+
+ private:
+  Comm& plane() { return promoted_ ? *rccl_ : *host_; }
+  enum State { kIdle, kStarting, kStarted, kFailed };
+  int rank_, size_, dev_;
+  std::shared_ptr<ShmSegment> seg_;
+  double timeout_;
+  std::unique_ptr<Comm> host_, rccl_;
+  double t_created_, t_start_ = 0;
+  std::mutex m_;
+  std::condition_variable cv_;
+  State state_ = kIdle;
+  std::exception_ptr err_;
+  bool promoted_ = false;  // only the rank's main thread reads/writes it
+  DataPlaneTimes times_;
 };
 
 }  // namespace
 
 std::unique_ptr<Comm> make_rccl_comm(int rank, int size, const std::vector<uint8_t>& uid, int device,
-                                     std::shared_ptr<ShmSegment> seg, double timeout_s) {
-  return std::make_unique<RcclComm>(rank, size, uid, device, std::move(seg), timeout_s);
+                                     std::shared_ptr<ShmSegment> seg, double timeout_s, bool settle_now) {
+  return std::make_unique<RcclComm>(rank, size, uid, device, std::move(seg), timeout_s, settle_now);
+}
+
+std::unique_ptr<Comm> make_deferred_rccl_comm(int rank, int size, int device, std::shared_ptr<ShmSegment> seg,
+                                              double timeout_s) {
+  return std::make_unique<DeferredRcclComm>(rank, size, device, std::move(seg), timeout_s);
 }
 
 std::vector<uint8_t> rccl_unique_id() {

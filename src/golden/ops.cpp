@@ -203,7 +203,7 @@ std::vector<uint8_t> region_grow(const std::vector<uint8_t>& bnd, int w, int h, 
   return reg;
 }
 
-static std::vector<uint8_t> morph(const std::vector<uint8_t>& m, int w, int h, int size, bool dil) {
+static std::vector<uint8_t> morph(const std::vector<uint8_t>& m, int w, int h, int size, bool dil, bool disc) {
   const int r = size / 2;
   std::vector<uint8_t> out(m.size());
   for (int y = 0; y < h; ++y)
@@ -211,6 +211,7 @@ static std::vector<uint8_t> morph(const std::vector<uint8_t>& m, int w, int h, i
       bool any = false, all = true;
       for (int dy = -r; dy <= r; ++dy)
         for (int dx = -r; dx <= r; ++dx) {
+          if (disc && dx * dx + dy * dy > r * r) continue;
           const int nx = x + dx, ny = y + dy;
           if (nx < 0 || ny < 0 || nx >= w || ny >= h) continue;
           const bool v = m[(size_t)ny * w + nx] != 0;
@@ -222,8 +223,12 @@ static std::vector<uint8_t> morph(const std::vector<uint8_t>& m, int w, int h, i
   return out;
 }
 
-std::vector<uint8_t> dilate(const std::vector<uint8_t>& m, int w, int h, int size) { return morph(m, w, h, size, true); }
-std::vector<uint8_t> erode(const std::vector<uint8_t>& m, int w, int h, int size) { return morph(m, w, h, size, false); }
+std::vector<uint8_t> dilate(const std::vector<uint8_t>& m, int w, int h, int size, bool disc) {
+  return morph(m, w, h, size, true, disc);
+}
+std::vector<uint8_t> erode(const std::vector<uint8_t>& m, int w, int h, int size, bool disc) {
+  return morph(m, w, h, size, false, disc);
+}
 
 std::vector<uint8_t> border(const std::vector<uint8_t>& m, int w, int h, int radius) {
   if (radius <= 0) return std::vector<uint8_t>(m.size(), 0);
@@ -266,10 +271,28 @@ std::vector<uint8_t> region_grow3d(const std::vector<uint8_t>& bnd, int w, int h
   return reg;
 }
 
-std::vector<uint8_t> dilate3d(const std::vector<uint8_t>& m, int w, int h, int d, int size) {
-  // Separable max over x, then y, then z (exact for a cube SE with out-of-volume ignored).
+std::vector<uint8_t> dilate3d(const std::vector<uint8_t>& m, int w, int h, int d, int size, bool ball) {
   const int r = size / 2;
   const size_t plane = (size_t)w * h;
+  if (ball) {  // direct definition: OR over the offsets with dx² + dy² + dz² ≤ r²
+    std::vector<uint8_t> out(m.size(), 0);
+    for (int z = 0; z < d; ++z)
+      for (int y = 0; y < h; ++y)
+        for (int x = 0; x < w; ++x) {
+          uint8_t v = 0;
+          for (int dz = -r; dz <= r && !v; ++dz)
+            for (int dy = -r; dy <= r && !v; ++dy)
+              for (int dx = -r; dx <= r && !v; ++dx) {
+                if (dx * dx + dy * dy + dz * dz > r * r) continue;
+                const int X = x + dx, Y = y + dy, Z = z + dz;
+                if (X < 0 || Y < 0 || Z < 0 || X >= w || Y >= h || Z >= d) continue;
+                v = m[(size_t)Z * plane + (size_t)Y * w + X];
+              }
+          out[(size_t)z * plane + (size_t)y * w + x] = v ? 1 : 0;
+        }
+    return out;
+  }
+  // Separable max over x, then y, then z (exact for a cube SE with out-of-volume ignored).
   std::vector<uint8_t> a(m.size()), b(m.size());
   for (int z = 0; z < d; ++z)
     for (int y = 0; y < h; ++y)
@@ -344,8 +367,9 @@ SliceResult run(const SliceInput& s, const PipelineParams& p, bool with_erosion)
   r.sharpened = sharpen(r.median, s.w, s.h, p.sharpen_gain, p.sharpen_sigma, p.sharpen_mask);
   r.band = band(r.sharpened, p.srg_min, p.srg_max);
   r.region = region_grow(r.band, s.w, s.h, reference_seeds(s.w, s.h), p.srg_connectivity);
-  r.dilated = dilate(r.region, s.w, s.h, p.dilation_size);
-  if (with_erosion) r.eroded = erode(r.region, s.w, s.h, p.erosion_size);
+  const bool disc = p.se_shape == kSeDisc;
+  r.dilated = dilate(r.region, s.w, s.h, p.dilation_size, disc);
+  if (with_erosion) r.eroded = erode(r.region, s.w, s.h, p.erosion_size, disc);
   std::vector<float> v = rescaled(s, p);
   auto mm = std::minmax_element(v.begin(), v.end());
   r.window_lo = *mm.first;

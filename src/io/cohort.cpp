@@ -4,6 +4,7 @@
 #include <fcntl.h>
 #include <linux/capability.h>
 #include <pthread.h>
+#include <signal.h>
 #include <sys/stat.h>
 #include <sys/syscall.h>
 #include <unistd.h>
@@ -236,7 +237,17 @@ struct OutputReaper::Impl {
       }
     }
   }
-  // Stale trash of killed runs in `parent` (first time the parent is seen).
+  // Stale trash of killed runs in `parent` (first time the parent is seen): only entries whose
+  // owner (the pid in ".nm03-trash-<pid>-<seq>") is gone. A live run's trash — another process
+  // writing to the same output root, or another reaper of this one — is its own reaper's to delete.
+  static bool owner_alive(const char* name) {
+    const char* p = name + std::strlen(kTrashPrefix);
+    char* end = nullptr;
+    const long pid = std::strtol(p, &end, 10);
+    if (end == p || *end != '-' || pid <= 0) return false;  // not ours: treat as stale
+    if (pid == (long)::getpid()) return true;
+    return ::kill((pid_t)pid, 0) == 0 || errno != ESRCH;
+  }
   void sweep_parent(const std::string& parent) {
     {
       std::lock_guard<std::mutex> g(m);
@@ -246,7 +257,8 @@ struct OutputReaper::Impl {
     if (!d) return;
     std::vector<std::string> stale;
     while (dirent* e = ::readdir(d))
-      if (std::strncmp(e->d_name, kTrashPrefix, std::strlen(kTrashPrefix)) == 0) stale.push_back(e->d_name);
+      if (std::strncmp(e->d_name, kTrashPrefix, std::strlen(kTrashPrefix)) == 0 && !owner_alive(e->d_name))
+        stale.push_back(e->d_name);
     ::closedir(d);
     for (auto& n : stale) push(parent + "/" + n);
   }

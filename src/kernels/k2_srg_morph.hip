@@ -13,7 +13,9 @@
 //     in registers with wave64 butterflies, device_util.h);
 //   * 8-connectivity adds a diagonal seeding step R |= M & (dil1(R↑) | dil1(R↓)).
 // The loop stops when a full iteration changes nothing (workgroup barrier + LDS flag; no host).
-// Morphology uses shifted-word ORs/ANDs; out-of-image samples are ignored (App. A.7).
+// Morphology uses shifted-word ORs/ANDs; out-of-image samples are ignored (App. A.7). The
+// Dilation/Erosion structuring element is the square (default) or the digital disc
+// (PipeConsts::se_disc, --se-shape disc); the renderer border always erodes with a square.
 #include <hip/hip_runtime.h>
 
 #include "device_util.h"
@@ -27,7 +29,7 @@ namespace nm03::gpu {
 // Threads per slice workgroup. Row/column fills use one thread per row (≤ 512), the 64×64 bit
 // transposes and morphology passes spread over every wave. A batch has only one workgroup per
 // slice, so per-workgroup latency is the cost: 256 → 512 → 1024 threads measured 32.4 → 24.9 →
-// 23.1 µs per 64-slice batch (isolated, tools/gpu_kprof.sh).
+// 23.1 µs per 64-slice batch (isolated rocprofv3 kernel timings, round 1).
 #ifndef NM03_SRG_THREADS
 #define NM03_SRG_THREADS 1024
 #endif
@@ -74,7 +76,7 @@ __device__ __forceinline__ void srg_slice(uint64_t* const smem, int* flag, const
   if (out.region) store_plane(Rg, out.region + off, H, n, sn);
   // Scratch planes now: M, Mt, Rt (all used in row layout, stride sn, from here on).
   if (out.dilated || out.border_dilated) {
-    morph<NW>(Rg, Mt, M, W, H, n, pc.dilation_size, true, sn);  // Mt = D
+    morph_se<NW>(Rg, Mt, M, W, H, n, pc.dilation_size, true, pc.se_disc, sn);  // Mt = D
     if (out.dilated) store_plane(Mt, out.dilated + off, H, n, sn);
     if (out.border_dilated) {
       morph<NW>(Mt, Rt, M, W, H, n, 2 * pc.border_radius + 1, false, sn);  // Rt = erode(D)
@@ -88,7 +90,7 @@ __device__ __forceinline__ void srg_slice(uint64_t* const smem, int* flag, const
     __syncthreads();
   }
   if (out.eroded || out.border_eroded) {
-    morph<NW>(Rg, Mt, M, W, H, n, pc.erosion_size, false, sn);  // Mt = E
+    morph_se<NW>(Rg, Mt, M, W, H, n, pc.erosion_size, false, pc.se_disc, sn);  // Mt = E
     if (out.eroded) store_plane(Mt, out.eroded + off, H, n, sn);
     if (out.border_eroded) {
       morph<NW>(Mt, Rt, M, W, H, n, 2 * pc.border_radius + 1, false, sn);

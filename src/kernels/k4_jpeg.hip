@@ -330,7 +330,7 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(kOcc)))
       // int → f32 conversion; the rescale only when the image has one (workgroup-uniform).
       // (Written with __builtin_amdgcn_sbfe / _ubfe and the select between the two conversions,
       // the compiler folded both into one unsigned conversion and signed slices rendered wrong:
-      // tools/probes/bfe_probe.hip, test_engine_norm_tables_vs_golden.)
+      // profiles/r4/bfe_probe/, test_engine_norm_tables_vs_golden.)
       const bool sgn = rd.type == kI16, affine = rd.slope != 1.0f || rd.intercept != 0.0f;
       const uint32_t vsh = 32u - rd.stored_bits;
       auto value = [&](uint32_t r) {
@@ -850,8 +850,8 @@ void launch_jpeg(const uint8_t* canvas, const JpegDesc* jd, int ncanvas, int out
   const int parts = (bpi + kJpegWG - 1) / kJpegWG;
   if ((size_t)parts * ncanvas > w.look_cap) throw DeviceError("launch_jpeg: look-back capacity exceeded");
   w.look_used = (size_t)parts * ncanvas;
-  // NM03_PROFILE_VARIANT=jpeg=N selects truncated profiling variants (output invalid;
-  // tools/gpu_jpeg_split.sh).
+  // NM03_PROFILE_VARIANT=jpeg=N selects truncated profiling variants (output invalid; time them
+  // with rocprofv3 --kernel-trace --stats).
   static const int dbg = profile_variant("jpeg") & 0xFF;
   if (rs.rd && rs.nrd < ncanvas) throw DeviceError("launch_jpeg: fewer render descriptors than canvases");
   // The look-back records (3 words per workgroup) start unpublished. Eager launches alternate

@@ -289,6 +289,34 @@ __global__ void dilate_z_kernel(const uint64_t* __restrict__ src, uint64_t* __re
   dst[i] = acc;
 }
 
+// Ball dilation (se_shape = disc in 3D): one thread per output word; the ball of radius r is the
+// union over (dz, dy) of the row segments |dx| ≤ floor(sqrt(r² − dy² − dz²)), so each word is the
+// OR of ≤ (2r+1)² horizontally dilated words of the planes around it (reads hit L2: a 256² plane is
+// 8 KiB). Out-of-volume rows are ignored.
+__global__ __launch_bounds__(256) void dilate_ball_kernel(const uint64_t* __restrict__ src, uint64_t* __restrict__ dst,
+                                                          int w, int h, int d, int r) {
+  const int n = (w + 63) >> 6;
+  const size_t words = (size_t)h * n;
+  const size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= words * d) return;
+  const int z = (int)(q / words);
+  const int rem = (int)(q - (size_t)z * words);
+  const int y = rem / n, i = rem - y * n;
+  const uint64_t lm = last_mask(w);
+  uint64_t acc = 0;
+  for (int dz = -r; dz <= r; ++dz) {
+    const int zz = z + dz;
+    if (zz < 0 || zz >= d) continue;
+    for (int dy = -r; dy <= r; ++dy) {
+      const int yy = y + dy;
+      const int k = disc_halfwidth(r * r - dy * dy - dz * dz);
+      if (yy < 0 || yy >= h || k < 0) continue;
+      acc |= hmorph_word(src + (size_t)zz * words + (size_t)yy * n, i, n, lm, k, true);
+    }
+  }
+  dst[q] = i == n - 1 ? (acc & lm) : acc;
+}
+
 namespace {
 int morph_plane_words(int w, int h) { return (h * ((w + 63) / 64) + 1) & ~1; }
 bool morph_global(int w, int h) { return (size_t)morph_plane_words(w, h) * 3 * sizeof(uint64_t) + 1024 > kLdsBudget; }
@@ -312,9 +340,15 @@ void border_volume(const uint64_t* src, uint64_t* dst, int w, int h, int d, int 
 }
 
 void dilate_volume(const uint64_t* src, uint64_t* dst, uint64_t* tmp, int w, int h, int d, int size, hipStream_t stream,
-                   uint64_t* scratch) {
+                   uint64_t* scratch, bool ball) {
   const int n = (w + 63) / 64;
   const int words = h * n;
+  if (ball) {
+    const size_t total = (size_t)words * d;
+    dilate_ball_kernel<<<(unsigned)((total + 255) / 256), 256, 0, stream>>>(src, dst, w, h, d, size / 2);
+    check_launch("dilate_ball_kernel");
+    return;
+  }
   const int plane_words = morph_plane_words(w, h);
   if (morph_global(w, h)) {
     if (!scratch) throw DeviceError("dilate_volume: planes above the LDS size need scratch (morph3d_scratch_words)");
@@ -373,7 +407,7 @@ void preload_volume() {
                         reinterpret_cast<const void*>(&srg3d_kernel<true>), reinterpret_cast<const void*>(&dilate_plane_kernel<false>),
                         reinterpret_cast<const void*>(&dilate_plane_kernel<true>), reinterpret_cast<const void*>(&border_plane_kernel<false>),
                         reinterpret_cast<const void*>(&border_plane_kernel<true>), reinterpret_cast<const void*>(&dilate_z_kernel),
-                        reinterpret_cast<const void*>(&slab_seed_kernel)})
+                        reinterpret_cast<const void*>(&slab_seed_kernel), reinterpret_cast<const void*>(&dilate_ball_kernel)})
     check_hip(hipFuncGetAttributes(&a, f), "preload volume kernels");
 }
 

@@ -168,6 +168,65 @@ __device__ inline void morph(const uint64_t* src, uint64_t* dst, uint64_t* tmp, 
   __syncthreads();
 }
 
+// Half-width of the digital disc of radius r at row offset dy: floor(sqrt(r² − dy²)), −1 outside.
+__device__ __forceinline__ int disc_halfwidth(int r2_minus) {
+  if (r2_minus < 0) return -1;
+  int k = 0;
+  while ((k + 1) * (k + 1) <= r2_minus) ++k;
+  return k;
+}
+
+// Word i of the horizontal morphology (radius k) of one row of n words: OR (dilate) or AND (erode,
+// pixels outside the row count as 1) of the shifts by ±1..±k. Not masked to the row's width.
+__device__ __forceinline__ uint64_t hmorph_word(const uint64_t* row, int i, int n, uint64_t lm, int k, bool dil) {
+  uint64_t v = row[i];
+  uint64_t prev = i > 0 ? row[i - 1] : (dil ? 0ull : ~0ull);
+  uint64_t next = i + 1 < n ? row[i + 1] : (dil ? 0ull : ~0ull);
+  if (!dil) {
+    if (i == n - 1) v |= ~lm;
+    if (i + 1 == n - 1) next |= ~lm;
+  }
+  uint64_t acc = v;
+  for (int j = 1; j <= k; ++j) {
+    const uint64_t left = (v << j) | (prev >> (64 - j));
+    const uint64_t right = (v >> j) | (next << (64 - j));
+    acc = dil ? (acc | left | right) : (acc & left & right);
+  }
+  return acc;
+}
+
+// Morphology with the digital disc of radius r = size/2 (PipelineParams::se_shape = disc): the disc
+// is the union of the horizontal segments |dx| ≤ floor(sqrt(r² − dy²)) of its rows, so every output
+// word is the OR / AND over the in-image rows y+dy of one horizontally dilated / eroded word. One
+// pass, no scratch plane; out-of-image rows are ignored like the square's.
+__device__ inline void morph_disc(const uint64_t* src, uint64_t* dst, int w, int h, int n, int size, bool dil, int s = 0) {
+  if (s == 0) s = n;
+  const int r = size / 2;
+  const uint64_t lm = last_mask(w);
+  for (int q = threadIdx.x; q < h * n; q += blockDim.x) {
+    const int y = q / n, i = q - y * n;
+    uint64_t acc = dil ? 0ull : ~0ull;
+    for (int dy = -r; dy <= r; ++dy) {
+      const int yy = y + dy;
+      if (yy < 0 || yy >= h) continue;
+      const uint64_t v = hmorph_word(src + yy * s, i, n, lm, disc_halfwidth(r * r - dy * dy), dil);
+      acc = dil ? (acc | v) : (acc & v);
+    }
+    dst[y * s + i] = i == n - 1 ? (acc & lm) : acc;
+  }
+  __syncthreads();
+}
+
+// The pipeline's structuring element: square (morph) or disc (morph_disc), PipeConsts::se_disc.
+template <int NW = 0>
+__device__ inline void morph_se(const uint64_t* src, uint64_t* dst, uint64_t* tmp, int w, int h, int n, int size, bool dil,
+                                bool disc, int s = 0) {
+  if (disc)
+    morph_disc(src, dst, w, h, n, size, dil, s);
+  else
+    morph<NW>(src, dst, tmp, w, h, n, size, dil, s);
+}
+
 // Copy an LDS plane with row stride s (n words per row) to a dense global plane.
 __device__ inline void store_plane(const uint64_t* src, uint64_t* dst, int h, int n, int s) {
   for (int q = threadIdx.x; q < h * n; q += blockDim.x) {

@@ -198,6 +198,7 @@ gpu::PipeConsts consts_from(const PipelineParams& p, int border_radius) {
   pc.dilation_size = p.dilation_size;
   pc.erosion_size = p.erosion_size;
   pc.border_radius = border_radius;
+  pc.se_disc = p.se_shape == kSeDisc ? 1 : 0;
   return pc;
 }
 
@@ -254,7 +255,8 @@ PYBIND11_MODULE(_nm03, m) {
       .def_readwrite("erosion_size", &PipelineParams::erosion_size)
       .def_readwrite("min_dim", &PipelineParams::min_dim)
       .def_readwrite("apply_rescale", &PipelineParams::apply_rescale)
-      .def_readwrite("frame", &PipelineParams::frame);
+      .def_readwrite("frame", &PipelineParams::frame)
+      .def_readwrite("se_shape", &PipelineParams::se_shape);
   py::class_<RenderParams>(m, "RenderParams")
       .def(py::init<>())
       .def_readwrite("out_width", &RenderParams::out_width)
@@ -278,6 +280,7 @@ PYBIND11_MODULE(_nm03, m) {
       .def_readwrite("jpeg_out_cap", &EngineConfig::jpeg_out_cap)
       .def_readwrite("upload_chunk_kb", &EngineConfig::upload_chunk_kb)
       .def_readwrite("create_writers", &EngineConfig::create_writers)
+      .def_readwrite("lazy_slots", &EngineConfig::lazy_slots)
       .def_readwrite("host_only", &EngineConfig::host_only);
 
   m.def("reference_seeds", [](int w, int h) {
@@ -548,11 +551,14 @@ PYBIND11_MODULE(_nm03, m) {
     const int h = (int)band.shape(0), w = (int)band.shape(1);
     return mask2d(golden::region_grow(from_np<uint8_t>(band), w, h, seeds_from(seeds), conn), h, w);
   });
-  m.def("golden_morph", [](py::array_t<uint8_t, py::array::c_style | py::array::forcecast> mk, int size, bool dilate) {
-    const int h = (int)mk.shape(0), w = (int)mk.shape(1);
-    auto v = from_np<uint8_t>(mk);
-    return mask2d(dilate ? golden::dilate(v, w, h, size) : golden::erode(v, w, h, size), h, w);
-  });
+  m.def(
+      "golden_morph",
+      [](py::array_t<uint8_t, py::array::c_style | py::array::forcecast> mk, int size, bool dilate, bool disc) {
+        const int h = (int)mk.shape(0), w = (int)mk.shape(1);
+        auto v = from_np<uint8_t>(mk);
+        return mask2d(dilate ? golden::dilate(v, w, h, size, disc) : golden::erode(v, w, h, size, disc), h, w);
+      },
+      py::arg("mask"), py::arg("size"), py::arg("dilate"), py::arg("disc") = false);
   m.def("golden_border", [](py::array_t<uint8_t, py::array::c_style | py::array::forcecast> mk, int radius) {
     const int h = (int)mk.shape(0), w = (int)mk.shape(1);
     return mask2d(golden::border(from_np<uint8_t>(mk), w, h, radius), h, w);
@@ -562,10 +568,13 @@ PYBIND11_MODULE(_nm03, m) {
     const int d = (int)band.shape(0), h = (int)band.shape(1), w = (int)band.shape(2);
     return to_np<uint8_t>(golden::region_grow3d(from_np<uint8_t>(band), w, h, d, seeds_from(seeds), conn), {d, h, w});
   });
-  m.def("golden_dilate3d", [](py::array_t<uint8_t, py::array::c_style | py::array::forcecast> mk, int size) {
-    const int d = (int)mk.shape(0), h = (int)mk.shape(1), w = (int)mk.shape(2);
-    return to_np<uint8_t>(golden::dilate3d(from_np<uint8_t>(mk), w, h, d, size), {d, h, w});
-  });
+  m.def(
+      "golden_dilate3d",
+      [](py::array_t<uint8_t, py::array::c_style | py::array::forcecast> mk, int size, bool ball) {
+        const int d = (int)mk.shape(0), h = (int)mk.shape(1), w = (int)mk.shape(2);
+        return to_np<uint8_t>(golden::dilate3d(from_np<uint8_t>(mk), w, h, d, size, ball), {d, h, w});
+      },
+      py::arg("mask"), py::arg("size"), py::arg("ball") = false);
   m.def("golden_render_gray", [](py::array_t<float, py::array::c_style | py::array::forcecast> v, float lo, float hi,
                                  float sx, float sy, int out_w, int out_h) {
     const int h = (int)v.shape(0), w = (int)v.shape(1);
@@ -1039,14 +1048,15 @@ PYBIND11_MODULE(_nm03, m) {
       throw;
     }
   });
-  m.def("k_dilate3d", [](uintptr_t src, uintptr_t dst, uintptr_t tmp, int w, int h, int d, int size, uintptr_t stream) {
+  m.def("k_dilate3d", [](uintptr_t src, uintptr_t dst, uintptr_t tmp, int w, int h, int d, int size, uintptr_t stream,
+                         bool ball) {
     hipStream_t st = as_stream(stream);
     if (size < 1 || !(size & 1)) throw std::invalid_argument("dilation size must be odd and >= 1");
     void* scr = nullptr;
     if (const size_t sw = gpu::morph3d_scratch_words(w, h, d))
       gpu::check_hip(hipMalloc(&scr, sw * 8), "hipMalloc morph scratch");
     try {
-      gpu::dilate_volume((const uint64_t*)src, (uint64_t*)dst, (uint64_t*)tmp, w, h, d, size, st, (uint64_t*)scr);
+      gpu::dilate_volume((const uint64_t*)src, (uint64_t*)dst, (uint64_t*)tmp, w, h, d, size, st, (uint64_t*)scr, ball);
       gpu::check_hip(hipStreamSynchronize(st), "k_dilate3d");
     } catch (...) {
       (void)hipStreamSynchronize(st);
@@ -1054,7 +1064,8 @@ PYBIND11_MODULE(_nm03, m) {
       throw;
     }
     if (scr) (void)hipFree(scr);
-  });
+  }, py::arg("src"), py::arg("dst"), py::arg("tmp"), py::arg("w"), py::arg("h"), py::arg("d"), py::arg("size"),
+     py::arg("stream"), py::arg("ball") = false);
   m.def("k_jpeg", [](uintptr_t canvas, int n, int h, int w, int quality, uintptr_t stream) {
     hipStream_t st = as_stream(stream);
     const int blocks = (w / 8) * (h / 8);

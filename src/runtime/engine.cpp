@@ -212,6 +212,25 @@ void hip_free_all(Slot& s) {
   if (s.stream) (void)hipStreamDestroy(s.stream);
 }
 
+// Streams created ahead of the engine (reserve_streams), per device.
+std::mutex g_reserve_m;
+std::vector<std::pair<int, hipStream_t>> g_reserved;
+
+hipStream_t take_stream(int device, const char* what) {
+  {
+    std::lock_guard<std::mutex> g(g_reserve_m);
+    for (size_t i = 0; i < g_reserved.size(); ++i)
+      if (g_reserved[i].first == device) {
+        hipStream_t s = g_reserved[i].second;
+        g_reserved.erase(g_reserved.begin() + (long)i);
+        return s;
+      }
+  }
+  hipStream_t s = nullptr;
+  check_hip(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), what);
+  return s;
+}
+
 template <class T>
 T* dmalloc(size_t count, const char* what) {
   void* p = nullptr;
@@ -273,6 +292,7 @@ struct Engine::Impl {
     pc.dilation_size = p.dilation_size;
     pc.erosion_size = p.erosion_size;
     pc.border_radius = cfg.render.border_radius;
+    pc.se_disc = p.se_shape == kSeDisc ? 1 : 0;
     jpeg::Tables t = jpeg::make_tables(cfg.render.jpeg_quality);
     for (int i = 0; i < 64; ++i) divs[i] = t.div_luma[i];
     jpeg_header = jpeg::make_header(cfg.render.out_width, cfg.render.out_height, t);
@@ -303,10 +323,9 @@ struct Engine::Impl {
       pthread_sigmask(SIG_BLOCK, &all, nullptr);
     });
     const double t2 = now_s();
-    // Slot 0 is built here (its failure fails the constructor); the others are built by their own
-    // worker threads while slot 0 already runs batches — a slot costs ≈11–18 ms of pinned and
-    // device allocations and stream creation, the first one more (runtime queues), which a cold
-    // CLI run would otherwise wait for in full.
+    // Slot 0 is built here (its failure fails the constructor). The others too, unless
+    // EngineConfig::lazy_slots hands them to their worker threads; a slot that cannot be built
+    // (out of memory) leaves the engine with fewer streams, not failed.
     std::string slot_ms;
     slots.resize((size_t)cfg.streams);
     place.run_bound([&] {
@@ -314,9 +333,19 @@ struct Engine::Impl {
       std::string split;
       slots[0] = make_slot(&split);
       slot_ms = std::to_string((int)((now_s() - ts) * 1e4) / 10.0).substr(0, 5) + " (" + split + ")";
+      if (cfg.lazy_slots) return;
+      for (size_t i = 1; i < slots.size(); ++i) {
+        const double tb = now_s();
+        try {
+          slots[i] = make_slot();
+        } catch (const std::exception& e) {
+          log_warn("engine slot " + std::to_string(i) + " unavailable, running with fewer streams: " + e.what());
+        }
+        slot_ms += ", +" + std::to_string((int)((now_s() - tb) * 1e4) / 10.0).substr(0, 5);
+      }
     });
     const double t3 = now_s();
-    building_ = (int)slots.size() - 1;
+    building_ = cfg.lazy_slots ? (int)slots.size() - 1 : 0;
     start_workers();
     const double t4 = now_s();
     log_info("engine on device " + std::to_string(cfg.device) + ": batch " + std::to_string(cfg.batch_size) + ", " +
@@ -411,7 +440,7 @@ struct Engine::Impl {
   std::mutex shared_up_m_;
   hipStream_t upload_stream() {
     std::lock_guard<std::mutex> g(shared_up_m_);
-    if (!shared_up_) check_hip(hipStreamCreateWithFlags(&shared_up_, hipStreamNonBlocking), "hipStreamCreate upload");
+    if (!shared_up_) shared_up_ = take_stream(cfg.device, "hipStreamCreate upload");
     return shared_up_;
   }
 
@@ -507,7 +536,7 @@ struct Engine::Impl {
       return sp;
     }
     try {
-      check_hip(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking), "hipStreamCreate");
+      s.stream = take_stream(cfg.device, "hipStreamCreate");
       s.up = upload_stream();
       mark("streams");
       check_hip(hipEventCreate(&s.ev0), "hipEventCreate");
@@ -611,7 +640,7 @@ struct Engine::Impl {
   // the runtime before it sleeps, which cost ≈0.7 ms of slot-thread CPU per batch — CPU the
   // loader/writer pool needs. Instead the slot sleeps in short steps (timer slack lowered to 1 µs on
   // slot threads) and queries the event: a few µs of CPU per batch, ≤ 20 µs of added latency,
-  // hidden by the other slots in flight (profiles: tools/gpu_wait_ab.sh, round 1).
+  // hidden by the other slots in flight (round-1 A/B, profiles/iter2/).
   //
   // The slot first sleeps through most of the time its recent batches took from enqueue to
   // completion (EMA, per slice × this batch's slices), then polls: ~10 wake-ups per batch instead of
@@ -669,7 +698,7 @@ struct Engine::Impl {
       // the pinned blob from there. Mapping the file instead measured 5x the loader CPU (mmap +
       // populate + munmap under the mm lock; 47.6k vs 267k slices/s, profiles/iter6/
       // mapped_load_ab.txt), and a pread of the pixels straight into the blob was slower too
-      // (tools/gpu_load_ab.sh): both removed in round 4.
+      // (profiles/r4/): both removed in round 4.
       dicom::SliceFile file(AT_FDCWD, path.c_str(), path, dicom::ReadMode::kStaged);
       const dicom::Header& h = file.header(buf);
       const int frame = dicom::select_frame(h, cfg.pipe.frame);
@@ -1290,6 +1319,7 @@ struct Engine::Impl {
     place.bind_this_thread();
     (void)prctl(PR_SET_TIMERSLACK, 1000UL, 0, 0, 0);  // 1 µs: short poll sleeps stay short
     if (!host_only_) (void)hipSetDevice(cfg.device);
+    if (!slots[slot_index] && !cfg.lazy_slots) return;  // could not be built in the constructor
     if (!slots[slot_index]) {  // built lazily (see the constructor); this thread is its only user
       bool ok = true;
       try {
@@ -1523,6 +1553,18 @@ int device_count() {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess) return 0;
   return n;
+}
+
+double reserve_streams(int device, int n) {
+  const double t0 = now_s();
+  check_hip(hipSetDevice(device), "hipSetDevice");
+  for (int i = 0; i < n; ++i) {
+    hipStream_t s = nullptr;
+    check_hip(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "hipStreamCreate (reserve)");
+    std::lock_guard<std::mutex> g(g_reserve_m);
+    g_reserved.push_back({device, s});
+  }
+  return now_s() - t0;
 }
 
 }  // namespace nm03

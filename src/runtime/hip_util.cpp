@@ -23,7 +23,7 @@ bool sync_launches() {
 
 int profile_variant(const char* kernel) {
   // NM03_PROFILE_VARIANT="jpeg=12,median=1": truncated kernel variants for time splits (output
-  // invalid; tools/gpu_jpeg_split.sh). Parsed once.
+  // invalid; profile them with rocprofv3 --kernel-trace --stats, e.g. through tools/ab_bench.sh). Parsed once.
   static const std::string spec = [] {
     const char* s = std::getenv("NM03_PROFILE_VARIANT");
     return std::string(s ? s : "");

@@ -92,6 +92,7 @@ PipeConsts make_consts(const PipelineParams& p, int border_radius) {
   pc.dilation_size = p.dilation_size;
   pc.erosion_size = p.erosion_size;
   pc.border_radius = border_radius;
+  pc.se_disc = p.se_shape == kSeDisc ? 1 : 0;
   return pc;
 }
 
@@ -200,7 +201,7 @@ static void volume_segment(VolumeDevice& V, const VolumeInput& v, const VolumePa
              (int)(sx.size() / 3), p.connectivity == 26 ? 26 : 6, V.flag.as<uint32_t>(), V.h_flag,
              V.srg_scratch.as<uint64_t>(), V.stream);
   dilate_volume(V.region.as<uint64_t>(), V.dil.as<uint64_t>(), V.tmp.as<uint64_t>(), v.w, v.h, v.d, p.dilation_size,
-                V.stream, V.morph_scratch.as<uint64_t>());
+                V.stream, V.morph_scratch.as<uint64_t>(), p.pipe.se_shape == kSeDisc);
 }
 
 static void unpack_volume(const DevBuf& b, const VolumeDevice& V, std::vector<uint8_t>& out) {
@@ -358,7 +359,7 @@ class GpuSlabGrower final : public SlabGrower {
                              V_.stream),
               "D2D slab region");
     dilate_volume(ext.as<uint64_t>(), dil.as<uint64_t>(), tmp.as<uint64_t>(), V_.w, V_.h, de, size, V_.stream,
-                  scr.as<uint64_t>());
+                  scr.as<uint64_t>(), ball);
     check_hip(hipMemcpyAsync(V_.dil.p, dil.as<uint64_t>() + (size_t)nb * wds, wds * V_.d * 8, hipMemcpyDeviceToDevice,
                              V_.stream),
               "D2D slab dilation");
@@ -386,7 +387,7 @@ class GpuSlabGrower final : public SlabGrower {
 // the extended buffer around a device copy of the slab. Slabs thinner than the halo fall back to the
 // generic algorithm (grow_and_dilate_slabs with GpuSlabGrower).
 static SlabStats slab_grow_dilate_gpu(Comm& comm, VolumeDevice& V, int nseeds, int conn, int depth, int z0, int z1,
-                                      int dilation) {
+                                      int dilation, bool ball) {
   const int rank = comm.rank(), n = comm.size();
   const int d = z1 - z0, r = dilation / 2;
   const size_t pw = V.words, pbytes = pw * 8;
@@ -440,7 +441,7 @@ static SlabStats slab_grow_dilate_gpu(Comm& comm, VolumeDevice& V, int nseeds, i
   }
   check_hip(hipMemcpyAsync(ext + (size_t)rb * pw, region, pbytes * d, hipMemcpyDeviceToDevice, V.stream), "D2D slab");
   dilate_volume(ext, V.ext_dil->as<uint64_t>(), V.ext_tmp->as<uint64_t>(), V.w, V.h, de, dilation, V.stream,
-                V.ext_scr->as<uint64_t>());
+                V.ext_scr->as<uint64_t>(), ball);
   check_hip(hipMemcpyAsync(V.dil.p, V.ext_dil->as<uint64_t>() + (size_t)rb * pw, pbytes * d, hipMemcpyDeviceToDevice,
                            V.stream),
             "D2D slab dilation");
@@ -477,9 +478,11 @@ VolumeResult VolumeRunner::run_slab(Comm& comm, const VolumeInput& slab, int z0,
                              " ranks leaves empty slabs");
   SlabStats st;
   if (depth / comm.size() >= p.dilation_size / 2) {
-    st = slab_grow_dilate_gpu(comm, V, (int)(sx.size() / 3), conn, depth, z0, z0 + slab.d, p.dilation_size);
+    st = slab_grow_dilate_gpu(comm, V, (int)(sx.size() / 3), conn, depth, z0, z0 + slab.d, p.dilation_size,
+                              p.pipe.se_shape == kSeDisc);
   } else {  // slabs thinner than the dilation halo: the generic exchange (all-gather of slab ends)
     GpuSlabGrower g(V, (int)(sx.size() / 3), conn);
+    g.ball = p.pipe.se_shape == kSeDisc;
     st = grow_and_dilate_slabs(comm, g, slab.w, slab.h, depth, z0, z0 + slab.d, conn, p.dilation_size);
   }
   check_hip(hipEventRecord(I.e1, V.stream), "event");
@@ -734,7 +737,7 @@ std::vector<std::vector<uint8_t>> golden_volume_jpegs(const VolumeInput& v, cons
     for (auto& sd : seeds) sd.z = v.d / 2;
   }
   const auto region = golden::region_grow3d(gp.band, v.w, v.h, v.d, seeds, vp.connectivity);
-  const auto dil = golden::dilate3d(region, v.w, v.h, v.d, vp.dilation_size);
+  const auto dil = golden::dilate3d(region, v.w, v.h, v.d, vp.dilation_size, vp.pipe.se_shape == kSeDisc);
   return golden_export(v, gp.vals, dil, rp);
 }
 
@@ -745,6 +748,7 @@ std::vector<std::vector<uint8_t>> golden_slab_jpegs(Comm& comm, const VolumeInpu
   GoldenPlanes gp = golden_preprocess(slab, vp);
   GoldenSlabGrower g(std::move(gp.band), slab.w, slab.h, slab.d, slab_seeds(vp.seeds, slab.w, slab.h, depth, z0, slab.d),
                      vp.connectivity);
+  g.ball = vp.pipe.se_shape == kSeDisc;
   *st = grow_and_dilate_slabs(comm, g, slab.w, slab.h, depth, z0, z0 + slab.d, vp.connectivity, vp.dilation_size);
   return golden_export(slab, gp.vals, g.dilated(), rp);
 }

@@ -204,7 +204,7 @@ void GoldenSlabGrower::dilate(int size, const std::vector<std::vector<uint64_t>>
   for (int k = 0; k < nb; ++k) unpack_plane(below[(size_t)k], w_, h_, &ext[(size_t)k * plane]);
   std::copy(region_.begin(), region_.end(), ext.begin() + (long)((size_t)nb * plane));
   for (int k = 0; k < na; ++k) unpack_plane(above[(size_t)k], w_, h_, &ext[(size_t)(nb + d_ + k) * plane]);
-  const std::vector<uint8_t> dil = golden::dilate3d(ext, w_, h_, nb + d_ + na, size);
+  const std::vector<uint8_t> dil = golden::dilate3d(ext, w_, h_, nb + d_ + na, size, ball);
   dilated_.assign(dil.begin() + (long)((size_t)nb * plane), dil.begin() + (long)((size_t)(nb + d_) * plane));
 }
 

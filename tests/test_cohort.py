@@ -129,15 +129,23 @@ def test_output_reaper_wipes_off_path(tmp_path):
         (a / f"{i}_original.jpg").write_bytes(b"x" * 100)
     (a / "sub").mkdir()
     (a / "sub" / "f").write_bytes(b"y")
-    stale = root / ".nm03-trash-1-7"
+    import subprocess
+    dead = subprocess.Popen(["true"])
+    dead.wait()  # a pid whose process is gone: its trash is stale
+    stale = root / f".nm03-trash-{dead.pid}-7"
     stale.mkdir()
     (stale / "old.jpg").write_bytes(b"z")
+    live = root / f".nm03-trash-{os.getppid()}-3"  # a live run's trash is left to its own reaper
+    live.mkdir()
+    (live / "busy.jpg").write_bytes(b"z")
     r = n.OutputReaper(2)
     r.wipe([str(a), str(b)])
     assert a.is_dir() and list(a.iterdir()) == [] and b.is_dir()
     (a / "new.jpg").write_bytes(b"n")  # the caller writes right away
     r.drain()
-    assert sorted(p.name for p in root.iterdir()) == ["PGBM-001", "PGBM-002"]
+    assert sorted(p.name for p in root.iterdir()) == [live.name, "PGBM-001", "PGBM-002"]
+    live.joinpath("busy.jpg").unlink()
+    live.rmdir()
     assert [p.name for p in a.iterdir()] == ["new.jpg"]
     assert r.files_reaped == 52
     r.wipe([str(a)])  # second pass over the same parent

@@ -143,3 +143,42 @@ def test_full_golden_pipeline_shapes(native):
     assert out["dilated"].sum() >= out["region"].sum()
     assert (out["eroded"] <= out["region"]).all()
     assert out["jpeg_original"][:2] == b"\xff\xd8" and out["jpeg_processed"][-2:] == b"\xff\xd9"
+
+
+@pytest.mark.parametrize("size", [3, 5, 7, 9])
+def test_disc_morphology_vs_torch(native, size):
+    """--se-shape disc (SURVEY App. A.7 / §7.6 risk 1): golden disc dilation/erosion = conv2d counts
+    with the digital disc of radius size//2; size 3 is the 4-neighbour cross."""
+    rng = np.random.default_rng(size)
+    m = (rng.random((61, 77)) < 0.55).astype(np.uint8)
+    m[20:40, 30:60] = 1
+    t = torch.from_numpy(m)
+    assert np.array_equal(native.golden_morph(m, size, True, True).astype(bool), R.dilate_disc(t, size).numpy())
+    assert np.array_equal(native.golden_morph(m, size, False, True).astype(bool), R.erode_disc(t, size).numpy())
+    if size == 3:
+        assert R.disc_se(3).sum() == 5
+    # the disc lies inside the square: square dilation ⊇ disc dilation, square erosion ⊆ disc erosion
+    assert (native.golden_morph(m, size, True, False) >= native.golden_morph(m, size, True, True)).all()
+    assert (native.golden_morph(m, size, False, False) <= native.golden_morph(m, size, False, True)).all()
+
+
+@pytest.mark.parametrize("size", [3, 5, 7])
+def test_ball_dilation3d_vs_torch(native, size):
+    rng = np.random.default_rng(size)
+    m = (rng.random((9, 23, 70)) < 0.04).astype(np.uint8)
+    got = native.golden_dilate3d(m, size, True).astype(bool)
+    assert np.array_equal(got, R.dilate_ball(torch.from_numpy(m), size).numpy())
+    assert (native.golden_dilate3d(m, size, False) >= got).all()
+
+
+def test_golden_pipeline_se_shape(native):
+    """The whole golden slice pipeline with --se-shape disc differs from square only in the morphology."""
+    import nm03_capstone_project_amd as nm
+    raw = native.phantom_slice(256, 256, 3, 12, 25, 11)
+    meta = {"type": "u16", "stored_bits": 16, "slope": 1.0, "intercept": 0.0, "spacing_x": 1.0, "spacing_y": 1.0}
+    sq = nm.SlicePipeline(nm.PipelineConfig()).golden(raw, meta)
+    dc = nm.SlicePipeline(nm.PipelineConfig(se_shape=1)).golden(raw, meta)
+    assert np.array_equal(sq["region"], dc["region"])
+    assert np.array_equal(dc["dilated"].astype(bool), native.golden_morph(dc["region"].astype(np.uint8), 3, True, True).astype(bool))
+    assert np.array_equal(dc["eroded"].astype(bool), native.golden_morph(dc["region"].astype(np.uint8), 3, False, True).astype(bool))
+    assert not np.array_equal(sq["dilated"], dc["dilated"])

@@ -1093,3 +1093,120 @@ def test_cli_parallel_patient_level_failures(native, cohort_root, tmp_path):
     assert f"Patient {pids[0]} completed. Successfully processed {n0}/{n0 + 1} images." in r.stdout
     assert f"Successfully processed {len(pids) + 2}/{len(pids) + 2} patients." in r.stdout
     assert not (out / pids[0] / "1-77_original.jpg").exists()
+
+
+# ---------------------------------------------------------------------------------------------
+# Round 5: --se-shape disc (K2 / K5), the new DICOM import forms through the GPU engine, and the
+# render kernel's first launch from slot threads in a fresh CLI process (complete preload)
+# ---------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("conn", [4, 8])
+@pytest.mark.parametrize("shape,sizes", [((256, 256), (3, 3)), ((131, 77), (5, 7)), ((600, 520), (3, 5))])
+def test_region_grow_disc_se_vs_golden_and_torch(native, conn, shape, sizes):
+    h, w = shape
+    rng = np.random.default_rng(h + w + conn)
+    band = rng.random(shape) < 0.6
+    seeds = [(x, y, 0) for (x, y) in native.reference_seeds(w, h)]
+    dsz, esz = sizes
+    cfg = nm.PipelineConfig(srg_connectivity=conn, se_shape=1, dilation_size=dsz, erosion_size=esz)
+    out = ops.region_grow(torch.from_numpy(band).cuda(), seeds, cfg)
+    g = native.golden_region_grow(band.astype(np.uint8), seeds, conn)
+    assert np.array_equal(out["region"].cpu().numpy(), g.astype(bool))
+    dil, ero = out["dilated"].cpu().numpy(), out["eroded"].cpu().numpy()
+    assert np.array_equal(dil, native.golden_morph(g, dsz, True, True).astype(bool))
+    assert np.array_equal(ero, native.golden_morph(g, esz, False, True).astype(bool))
+    rt = torch.from_numpy(g.astype(bool))
+    assert np.array_equal(dil, R.dilate_disc(rt, dsz).numpy())
+    assert np.array_equal(ero, R.erode_disc(rt, esz).numpy())
+    # the renderer border keeps its square erosion (it is not the Dilation/Erosion SE)
+    assert np.array_equal(out["border_region"].cpu().numpy(), native.golden_border(g, 2).astype(bool))
+
+
+def test_engine_disc_se_bit_exact(native):
+    raw = _phantom(native)
+    meta = {"type": "u16", "stored_bits": 16, "slope": 1.0, "intercept": 0.0, "spacing_x": 1.0, "spacing_y": 1.0}
+    pipe = nm.SlicePipeline(nm.PipelineConfig(batch_size=1, streams=1, threads=2, se_shape=1))
+    gpu, ref = pipe.run_array(raw, meta), pipe.golden(raw, meta)
+    for k in ("band", "region", "dilated", "eroded"):
+        assert np.array_equal(gpu[k], ref[k].astype(bool)), k
+    assert gpu["jpegs"][0] == ref["jpeg_original"] and gpu["jpegs"][4] == ref["jpeg_processed"]
+
+
+@pytest.mark.parametrize("size", [3, 5, 7])
+def test_dilate3d_ball_vs_golden_and_torch(native, size):
+    rng = np.random.default_rng(size)
+    m = rng.random((12, 70, 130)) < 0.03
+    dil = ops.dilate3d(torch.from_numpy(m).cuda(), size, ball=True).cpu().numpy()
+    assert np.array_equal(dil.astype(np.uint8), native.golden_dilate3d(m.astype(np.uint8), size, True))
+    assert np.array_equal(dil, R.dilate_ball(torch.from_numpy(m), size).numpy())
+
+
+def test_volume_ball_se_vs_golden(native):
+    d, h, w = 16, 96, 128
+    vol = np.stack([native.phantom_slice(h, w, 2, z, d, 5) for z in range(d)])
+    vp = nm.VolumePipeline(nm.PipelineConfig(se_shape=1), connectivity=6, dilation=7)
+    seeds = vp.default_seeds(vol)
+    res = vp.run(vol, seeds)
+    region, dil = vp.golden(res["band"], seeds)
+    assert np.array_equal(res["region"], region)
+    assert np.array_equal(res["dilated"], dil)
+    cube = nm.VolumePipeline(connectivity=6, dilation=7).run(vol, seeds)["dilated"]
+    assert (cube >= res["dilated"]).all() and not np.array_equal(cube, res["dilated"])
+
+
+def test_engine_new_dicom_forms_bit_exact(native, tmp_path):
+    """Deflated, RLE, MONOCHROME1 and a selected frame of a multi-frame file through the GPU engine:
+    both JPEGs equal the golden export of the same samples as the plain reader imports them."""
+    d = tmp_path / "in"
+    d.mkdir()
+    a, b, c = (native.phantom_slice(256, 256, 2, k, 9, 3) for k in (2, 4, 6))
+    files = {
+        "1-1.dcm": native.dicom_bytes(a, bits_stored=12, syntax="deflated"),
+        "1-2.dcm": native.dicom_bytes(b, bits_stored=12, syntax="rle"),
+        "1-3.dcm": native.dicom_bytes(c, bits_stored=12, photometric="MONOCHROME1"),
+        "1-4.dcm": native.dicom_bytes(np.stack([a, b, c]), bits_stored=12, syntax="rle"),
+    }
+    for name, data in files.items():
+        (d / name).write_bytes(data)
+    out = tmp_path / "out"
+    out.mkdir()
+    items = [(str(d / n), str(out)) for n in files]
+    st, _ = native.Engine(nm.PipelineConfig(batch_size=4, streams=2, threads=4, frame=1).engine_config()).run(items)
+    assert [c for c, _ in st] == [0, 0, 0, 0], st
+    for name in files:
+        raw, meta = native.read_slice(str(d / name), 0, 1)
+        g = native.golden_run(raw, meta["type"], meta["stored_bits"], meta["slope"], meta["intercept"],
+                              native.PipelineParams(), native.RenderParams(), meta["spacing_x"], meta["spacing_y"])
+        stem = name[:-4]
+        assert open(out / f"{stem}_original.jpg", "rb").read() == g["jpeg_original"], name
+        assert open(out / f"{stem}_processed.jpg", "rb").read() == g["jpeg_processed"], name
+    # MONOCHROME1 is imported inverted: its golden input is the complement of the stored samples
+    raw3, _ = native.read_slice(str(d / "1-3.dcm"))
+    assert np.array_equal(raw3, (~c) & np.uint16(0x0FFF))
+
+
+def test_cli_fresh_process_512_cohort_render_from_slot_threads(native, tmp_path):
+    """A fresh img_processing_parallel on a 512² cohort with 4 streams: every slice takes the generic
+    render kernel (not the fused exact-2× path), whose first launches come from slot threads — the
+    code object must already be loaded (kernels.h preload_kernels). Outputs equal the golden model."""
+    root = tmp_path / "data"
+    base = root / "Brain-Tumor-Progression" / "T1-Post-Combined-P001-P020"
+    files = []
+    for p in range(2):
+        sd = base / f"PGBM-{p + 1:03d}" / "10.000000-T1post-1"
+        sd.mkdir(parents=True)
+        for z in range(6):
+            raw = native.phantom_slice(512, 512, 2, z, 6, 10 + p)
+            f = sd / f"1-{z + 1}.dcm"
+            f.write_bytes(native.dicom_bytes(raw, bits_stored=12, instance=z + 1, spacing_x=0.7, spacing_y=0.7))
+            files.append((p, f))
+    out = tmp_path / "out"
+    r = run_bin("img_processing_parallel", "--data-root", str(root), "--out", str(out), "--streams", "4",
+                "--batch-size", "2", "--quiet")
+    assert r.returncode == 0, r.stderr
+    for p, f in files[::5]:
+        raw, meta = native.read_slice(str(f))
+        g = native.golden_run(raw, meta["type"], meta["stored_bits"], meta["slope"], meta["intercept"],
+                              native.PipelineParams(), native.RenderParams(), meta["spacing_x"], meta["spacing_y"])
+        stem = f.name[:-4]
+        assert open(out / f"PGBM-{p + 1:03d}" / f"{stem}_original.jpg", "rb").read() == g["jpeg_original"]
+        assert open(out / f"PGBM-{p + 1:03d}" / f"{stem}_processed.jpg", "rb").read() == g["jpeg_processed"]

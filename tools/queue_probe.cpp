@@ -1,0 +1,60 @@
+// tools/queue_probe.cpp — what does a HIP stream cost at start-up? (round 5, cold CLI anatomy)
+// Build: /opt/rocm/llvm/bin/clang++ -O2 -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include tools/queue_probe.cpp \
+//          -L/opt/rocm/lib -lamdhip64 -pthread -o build/bin/queue_probe
+//
+//   queue_probe <streams> <threads>
+//
+// hipInit + hipSetDevice, then `streams` non-blocking streams created by `threads` threads at once
+// (each thread creates streams/threads), then one 25-slice-sized pinned and device allocation.
+// Prints every phase in ms; run it under different GPU_MAX_HW_QUEUES values (HW queues are created
+// lazily, one per stream up to that count, and then shared round-robin).
+#include <hip/hip_runtime_api.h>
+
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <thread>
+#include <vector>
+
+static double now_ms() {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+int main(int argc, char** argv) {
+  const int ns = argc > 1 ? std::atoi(argv[1]) : 5;
+  const int nt = argc > 2 ? std::atoi(argv[2]) : 1;
+  const char* q = std::getenv("GPU_MAX_HW_QUEUES");
+  double t0 = now_ms();
+  if (hipInit(0) != hipSuccess || hipSetDevice(0) != hipSuccess) return 1;
+  void* p = nullptr;
+  (void)hipMalloc(&p, 4096);
+  const double t1 = now_ms();
+  std::vector<hipStream_t> st(ns, nullptr);
+  std::vector<double> each(ns, 0);
+  std::vector<std::thread> th;
+  for (int t = 0; t < nt; ++t)
+    th.emplace_back([&, t] {
+      for (int i = t; i < ns; i += nt) {
+        const double a = now_ms();
+        (void)hipStreamCreateWithFlags(&st[i], hipStreamNonBlocking);
+        each[i] = now_ms() - a;
+      }
+    });
+  for (auto& x : th) x.join();
+  const double t2 = now_ms();
+  void* h = nullptr;
+  void* d = nullptr;
+  (void)hipHostMalloc(&h, 4u << 20, hipHostMallocDefault);
+  const double t3 = now_ms();
+  (void)hipMalloc(&d, 16u << 20);
+  const double t4 = now_ms();
+  // first kernel-free work on every stream: a 4 KiB memset
+  for (int i = 0; i < ns; ++i) (void)hipMemsetAsync(d, 0, 4096, st[i]);
+  for (int i = 0; i < ns; ++i) (void)hipStreamSynchronize(st[i]);
+  const double t5 = now_ms();
+  std::printf("GPU_MAX_HW_QUEUES=%s streams %d threads %d | init %.1f | streams %.1f (", q ? q : "(unset)", ns, nt, t1 - t0,
+              t2 - t1);
+  for (int i = 0; i < ns; ++i) std::printf("%s%.1f", i ? " " : "", each[i]);
+  std::printf(") | pinned 4MiB %.2f | device 16MiB %.2f | first memsets %.2f ms\n", t3 - t2, t4 - t3, t5 - t4);
+  return 0;
+}
