@@ -39,6 +39,9 @@ struct AppConfig {
   // --mode 3d --split-volume: every patient's volume is decomposed into z-slabs over all ranks
   // (volume_slabs.h) instead of sharding whole patients over the ranks.
   bool split_volume = false;
+  // CLOCK_REALTIME when parse_args began (the --json record's "main_unix_s"): with the launcher's
+  // own clock it splits a cold run's wall into process start-up (exec → main) and the rest.
+  double main_unix_s = 0;
 };
 
 // Parse the shared flag set; `which` selects CLI-specific defaults. Exits on --help.

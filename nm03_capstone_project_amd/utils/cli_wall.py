@@ -18,6 +18,7 @@ import time
 def run_once(argv, timeout_s=120.0, env=None):
     """Run argv once; returns {rc, wall_s, user_s, sys_s, maxrss_kb, stderr_tail}."""
     with tempfile.TemporaryFile() as err:
+        launch_unix = time.time()
         t0 = time.perf_counter()
         p = subprocess.Popen(argv, stdout=subprocess.DEVNULL, stderr=err, env=env)
         done = threading.Event()
@@ -38,7 +39,8 @@ def run_once(argv, timeout_s=120.0, env=None):
         err.seek(0)
         tail = err.read()[-400:].decode(errors="replace")
     return {"rc": p.returncode, "wall_s": round(wall, 6), "user_s": round(ru.ru_utime, 6),
-            "sys_s": round(ru.ru_stime, 6), "maxrss_kb": ru.ru_maxrss, "stderr_tail": tail}
+            "sys_s": round(ru.ru_stime, 6), "maxrss_kb": ru.ru_maxrss, "stderr_tail": tail,
+            "launch_unix_s": launch_unix}
 
 
 def time_cli(argv, runs=10, json_path=None, timeout_s=120.0, env=None):
@@ -56,6 +58,11 @@ def time_cli(argv, runs=10, json_path=None, timeout_s=120.0, env=None):
                     r["phases"] = json.load(f)
             except (OSError, ValueError):
                 pass
+            ph = r.get("phases") or {}
+            main_unix = ph.pop("main_unix_s", None)
+            if isinstance(main_unix, (int, float)):
+                # exec → main: dynamic loading of the CLI and its libraries, before any of our code
+                ph["pre_main_s"] = round(main_unix - r["launch_unix_s"], 6)
         rows.append(r)
     walls = sorted(r["wall_s"] for r in rows)
     ok = all(r["rc"] == 0 for r in rows)

@@ -112,9 +112,11 @@ int visible_gpu_count() {
 }
 
 AppConfig parse_args(int argc, char** argv, const std::string& which) {
+  const double main_unix = std::chrono::duration<double>(std::chrono::system_clock::now().time_since_epoch()).count();
   arm_fast_exit();
   install_crash_handler();
   AppConfig c;
+  c.main_unix_s = main_unix;
   c.data_root = cohort::default_data_root();
   c.out_dir = which == "test_pipeline" ? "../out-test" : which == "img_processing_sequential" ? "../out-sequential" : "../out-parallel";
   if (which == "img_processing_sequential") {
@@ -746,7 +748,8 @@ int parallel_rank(const AppConfig& cfg, int rank, int size, Comm& comm, int devi
     std::vector<std::vector<double>> rows((size_t)size);
     for (int r = 0; r < size; ++r)
       rows[r].assign(all_rows.begin() + (size_t)r * kNumRankFields, all_rows.begin() + (size_t)(r + 1) * kNumRankFields);
-    write_json(cfg.json, std::string("{\"mode\": \"parallel\", \"gpus\": ") + std::to_string(size) + ", \"backend\": \"" +
+    write_json(cfg.json, std::string("{\"mode\": \"parallel\", \"gpus\": ") + std::to_string(size) + ", \"main_unix_s\": " +
+                             fmt(cfg.main_unix_s, 17) + ", \"backend\": \"" +
                              comm.backend() + "\", \"repeat\": " + std::to_string(cfg.repeat) + ", \"engine_setup_s\": " +
                              fmt(setup_s) + ", \"hip_init_s\": " + fmt(su.hip_init_s) + ", \"engine_ctor_s\": " +
                              fmt(su.engine_ctor_s) + ", \"streams_s\": " + fmt(su.streams_s) + ", \"engine_wait_s\": " + fmt(engine_wait_s) + ", \"kernel_load_s\": " +

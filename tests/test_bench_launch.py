@@ -29,23 +29,25 @@ def _json_line(out):
 
 @pytest.mark.parametrize("n", [2, 3])
 def test_bench_self_launch_n_ranks(tmp_path, n):
-    """`python bench.py --gpus N` starts N ranks itself: n_gpus, per-rank arrays, weak + strong."""
+    """`python bench.py --gpus N` starts N ranks itself: n_gpus, per-rank arrays; the headline is
+    BASELINE config 3 as written (strong: one cohort sharded), weak scaling the secondary."""
     r = _bench(tmp_path, "--gpus", str(n), "--comm", "host")
     assert r.returncode == 0, r.stderr
     rec = _json_line(r.stdout)
     assert rec["n_gpus"] == n and rec["config"]["parallelism"] == f"dp{n}"
+    assert rec["scaling"] == "strong"
     assert rec["config"]["comm"]["backend"] == "host"
-    assert rec["config"]["global_batch"] == n * rec["config"]["strong"]["global_batch"]  # weak: N replicas
+    cohort = rec["config"]["global_batch"]
+    assert rec["config"]["weak"]["global_batch"] == n * cohort  # weak: N replicas
     pr = rec["config"]["per_rank"]
     assert all(len(v) == n for v in pr.values())
-    # weak: every rank processes one full cohort per step
-    cohort = rec["config"]["strong"]["global_batch"]
-    assert pr["slices"] == [float(cohort * 2)] * n
     # strong: one cohort sharded, every slice exactly once
-    assert sum(rec["config"]["strong"]["per_rank"]["slices"]) == cohort * 2
-    # passes in flight: 2 for a full cohort per rank (465 ≥ 4 slots × 96), 4 for a shard below one
-    # batch per slot
-    assert rec["config"]["pipeline_depth"] == 2 and rec["config"]["strong"]["pipeline_depth"] == 4
+    assert sum(pr["slices"]) == cohort * 2
+    # weak: every rank processes one full cohort per step
+    assert rec["config"]["weak"]["per_rank"]["slices"] == [float(cohort * 2)] * n
+    # passes in flight: 4 for a shard below one batch per slot, 2 for a full cohort per rank
+    # (465 ≥ 4 slots × 96)
+    assert rec["config"]["pipeline_depth"] == 4 and rec["config"]["weak"]["pipeline_depth"] == 2
 
 
 def test_bench_auto_comm_records_rccl_failure(tmp_path):

@@ -765,10 +765,12 @@ def test_bench_multirank_one_gpu(native, tmp_path):
     assert r.returncode == 0, r.stderr[-3000:]
     rec = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
     assert rec["n_gpus"] == 2 and rec["value"] > 0 and rec["config"]["comm"]["backend"] == "host"
-    assert rec["config"]["strong"]["value"] > 0 and rec["config"]["strong"]["global_batch"] * 2 == rec["config"]["global_batch"]
-    assert sum(rec["config"]["per_rank"]["slices_ok"]) == 2 * rec["config"]["global_batch"]
+    # headline: BASELINE config 3 as written (one cohort sharded); weak scaling (2 replicas) secondary
+    assert rec["scaling"] == "strong"
+    assert rec["config"]["weak"]["value"] > 0 and rec["config"]["weak"]["global_batch"] == 2 * rec["config"]["global_batch"]
+    assert sum(rec["config"]["per_rank"]["slices_ok"]) == 2 * rec["config"]["global_batch"]  # 2 steps
     cli = rec["config"]["cli_wall"]  # the whole img_processing_parallel --gpus 2, timed twice
-    assert cli["all_ok"] and cli["runs"] == 2 and cli["slices"] == rec["config"]["strong"]["global_batch"], cli
+    assert cli["all_ok"] and cli["runs"] == 2 and cli["slices"] == rec["config"]["global_batch"], cli
 
 
 def test_cli_test_pipeline_gpu_equals_cpu(native, cohort_root, tmp_path):
