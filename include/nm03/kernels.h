@@ -8,6 +8,7 @@
 
 #include "nm03/common.h"
 #include "nm03/gpu_types.h"
+#include "nm03/pixel_math.h"
 
 namespace nm03::gpu {
 
@@ -31,6 +32,13 @@ void preload_srg();
 void preload_render();
 void preload_volume();
 void preload_threshold();
+
+// The engine's per-format normalise+clip table (n = 2^stored_bits keys from `base`), built on the
+// device on `stream` with the shared pixel_math.h function.
+void launch_build_norm_lut(float* out, uint32_t n, uint32_t base, uint8_t type, const NormClip& nc, hipStream_t stream);
+// The first host→device copy of a process initialises the runtime's copy path (≈ 10 ms on a cold
+// MI355X process, profiles/r5/cold/): one 4 MiB pinned H2D on `stream` (the SDMA path), synchronised.
+void warm_copy_path(hipStream_t stream);
 
 // K1a: k×k median of raw keys → `med` (u16 keys, same layout as raw). k ∈ {3,5,7,9}.
 // Per-slice key range: with `tile_mm` (2 u32 per tile) each tile stores its (min, max) and

@@ -309,12 +309,29 @@ void launch_sharpen_band(const uint16_t* med, uint64_t* band, float* sharpened, 
   check_launch("sharpen_band_kernel");
 }
 
+// Normalise+clip table of one slice format (engine.cpp norm_lut): out[i] = norm_clip_key(base + i)
+// for the 2^bits keys of the format, with the very function the sharpen's fallback path and the
+// golden model evaluate (pixel_math.h, no FP contraction): bit-identical to a host-built table,
+// without a synchronous pageable host→device copy on a slot thread.
+__global__ __launch_bounds__(256) void build_norm_lut_kernel(float* __restrict__ out, uint32_t n, uint32_t base,
+                                                             uint8_t type, NormClip nc) {
+  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+  if (i < n) out[i] = norm_clip_key((uint16_t)(base + i), type, nc);
+}
+
+void launch_build_norm_lut(float* out, uint32_t n, uint32_t base, uint8_t type, const NormClip& nc, hipStream_t stream) {
+  if (!n) return;
+  build_norm_lut_kernel<<<(n + 255) / 256, 256, 0, stream>>>(out, n, base, type, nc);
+  check_launch("build_norm_lut_kernel");
+}
+
 void preload_sharpen() {
   hipFuncAttributes a;
   for (const void* f : {reinterpret_cast<const void*>(&sharpen_band_kernel<0>), reinterpret_cast<const void*>(&sharpen_band_kernel<1>),
                         reinterpret_cast<const void*>(&sharpen_band_kernel<2>), reinterpret_cast<const void*>(&sharpen_band_kernel<3>),
                         reinterpret_cast<const void*>(&sharpen_band_kernel<4>), reinterpret_cast<const void*>(&sharpen_band_kernel<5>),
-                        reinterpret_cast<const void*>(&sharpen_band_kernel<6>), reinterpret_cast<const void*>(&sharpen_band_kernel<7>)})
+                        reinterpret_cast<const void*>(&sharpen_band_kernel<6>), reinterpret_cast<const void*>(&sharpen_band_kernel<7>),
+                        reinterpret_cast<const void*>(&build_norm_lut_kernel)})
     check_hip(hipFuncGetAttributes(&a, f), "preload sharpen_band_kernel");
 }
 

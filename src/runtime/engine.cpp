@@ -136,6 +136,8 @@ struct Slot {
   double batch_ema_s = 0;  // enqueue → completion time per slice of recent batches (wait_batch)
   // Host-only engine (EngineConfig::host_only): h_blob / h_out are plain mappings, no device side.
   bool host_only = false;
+  // h_blob / h_out / h_sizes live in the engine's pinned arenas (freed with the engine, not here).
+  bool arena = false;
   size_t out_bytes = 0;
 };
 
@@ -199,9 +201,11 @@ void hip_free_all(Slot& s) {
     delete[] s.h_sizes;
     return;
   }
-  if (s.h_blob) (void)hipHostFree(s.h_blob);
-  if (s.h_out) (void)hipHostFree(s.h_out);
-  if (s.h_sizes) (void)hipHostFree(s.h_sizes);
+  if (!s.arena) {
+    if (s.h_blob) (void)hipHostFree(s.h_blob);
+    if (s.h_out) (void)hipHostFree(s.h_out);
+    if (s.h_sizes) (void)hipHostFree(s.h_sizes);
+  }
   if (s.h_single) (void)hipHostFree(s.h_single);
   for (void* p : {(void*)s.d_blob, (void*)s.d_raw_x, (void*)s.d_med, (void*)s.d_tile_mm, (void*)s.d_f32, (void*)s.d_bits, (void*)s.d_srg_scratch, (void*)s.d_canvas,
                   (void*)s.jw.look, (void*)s.jw.ticket, (void*)s.jw.spill})
@@ -331,13 +335,14 @@ struct Engine::Impl {
     place.run_bound([&] {
       const double ts = now_s();
       std::string split;
-      slots[0] = make_slot(&split);
+      if (!host_only_ && !cfg.lazy_slots) make_arenas((int)slots.size());
+      slots[0] = make_slot(&split, 0);
       slot_ms = std::to_string((int)((now_s() - ts) * 1e4) / 10.0).substr(0, 5) + " (" + split + ")";
       if (cfg.lazy_slots) return;
       for (size_t i = 1; i < slots.size(); ++i) {
         const double tb = now_s();
         try {
-          slots[i] = make_slot();
+          slots[i] = make_slot(nullptr, (int)i);
         } catch (const std::exception& e) {
           log_warn("engine slot " + std::to_string(i) + " unavailable, running with fewer streams: " + e.what());
         }
@@ -362,6 +367,8 @@ struct Engine::Impl {
       if (s) hip_free_all(*s);
     if (shared_up_) (void)hipStreamDestroy(shared_up_);
     if (d_lut_) (void)hipFree(d_lut_);
+    if (pin_arena_) (void)hipHostFree(pin_arena_);
+    if (map_arena_) (void)hipHostFree(map_arena_);
   }
 
   // ---- normalise+clip lookup tables (K1b) ------------------------------------------------------
@@ -390,8 +397,10 @@ struct Engine::Impl {
     std::memcpy(&u, &f, 4);
     return u;
   }
-  // (lut_off, lut_base) for the parameter set; {kNoLut, 0} when there is no table.
-  std::pair<uint32_t, uint32_t> norm_lut(uint8_t type, uint8_t bits, float slope, float intercept) {
+  // (lut_off, lut_base) for the parameter set; {kNoLut, 0} when there is no table. A new table is
+  // built on the device on the calling slot's `stream` and waited for before it is published (once
+  // per format and engine; other slots find it only when it is complete).
+  std::pair<uint32_t, uint32_t> norm_lut(uint8_t type, uint8_t bits, float slope, float intercept, hipStream_t stream) {
     if (host_only_ || bits < 1 || bits > 16) return {kNoLut, 0u};
     const uint32_t sl = fbits(slope), ic = fbits(intercept);
     thread_local uint64_t last_owner = 0;
@@ -418,9 +427,8 @@ struct Engine::Impl {
     nc.nhigh = pc.nhigh;
     nc.cmin = pc.cmin;
     nc.cmax = pc.cmax;
-    std::vector<float> h(n);
-    for (uint32_t i = 0; i < n; ++i) h[i] = norm_clip_key((uint16_t)(base + i), type, nc);
-    check_hip(hipMemcpy(d_lut_ + lut_used_, h.data(), n * sizeof(float), hipMemcpyHostToDevice), "H2D norm table");
+    launch_build_norm_lut(d_lut_ + lut_used_, n, base, type, nc, stream);
+    check_hip(hipStreamSynchronize(stream), "norm table");
     const LutSet e{type, bits, sl, ic, (uint32_t)lut_used_, base};
     lut_used_ += n;
     luts_.push_back(e);
@@ -478,17 +486,25 @@ struct Engine::Impl {
     }
   }
 
-  // `split` (optional): milliseconds per allocation phase, for the start-up log.
-  std::unique_ptr<Slot> make_slot(std::string* split = nullptr) {
-    double tm = now_s();
-    auto mark = [&](const char* what) {
-      if (!split) return;
-      const double t = now_s();
-      *split += (split->empty() ? "" : ", ") + std::string(what) + " " + std::to_string((int)((t - tm) * 1e4) / 10.0).substr(0, 4);
-      tm = t;
-    };
-    auto sp = std::make_unique<Slot>();
-    Slot& s = *sp;
+  // Pinned host memory of every constructor-built slot in two allocations (one page-locked, one
+  // host-mapped) instead of three per slot: each hipHostMalloc costs ≈ 0.7–1.1 ms on a cold process
+  // whatever its size (tools/queue_probe.cpp), the bulk of the engine constructor.
+  uint8_t* pin_arena_ = nullptr;
+  uint8_t* map_arena_ = nullptr;
+  uint8_t* map_arena_dev_ = nullptr;
+  size_t pin_stride_ = 0, map_stride_ = 0;
+  void make_arenas(int n) {
+    Slot probe;
+    layout(probe);
+    pin_stride_ = align_up(probe.blob_bytes, 4096);
+    map_stride_ = align_up((size_t)out_cap_ * probe.cap_canvases + sizeof(int32_t) * probe.cap_canvases, 4096);
+    check_hip(hipHostMalloc((void**)&pin_arena_, pin_stride_ * n, hipHostMallocDefault), "hipHostMalloc blob arena");
+    check_hip(hipHostMalloc((void**)&map_arena_, map_stride_ * n, hipHostMallocMapped), "hipHostMalloc out arena");
+    check_hip(hipHostGetDevicePointer((void**)&map_arena_dev_, map_arena_, 0), "hipHostGetDevicePointer out arena");
+  }
+
+  // Capacities and blob layout of a slot (no allocation).
+  void layout(Slot& s) const {
     const int B = cfg.batch_size;
     const int md = cfg.max_dim;
     s.cap_slices = B;
@@ -516,6 +532,23 @@ struct Engine::Impl {
     s.raw_base = o;
     s.hole_slack = (size_t)std::max(cfg.threads, 1) * align_up((size_t)md * md / 4 * 3, 8);
     s.blob_bytes = o + (s.cap_pixels + s.hole_slack) * sizeof(uint16_t);
+  }
+
+  // `split` (optional): milliseconds per allocation phase, for the start-up log. `arena_slot` ≥ 0:
+  // the slot's pinned buffers are that part of the engine's arenas (make_arenas).
+  std::unique_ptr<Slot> make_slot(std::string* split = nullptr, int arena_slot = -1) {
+    double tm = now_s();
+    auto mark = [&](const char* what) {
+      if (!split) return;
+      const double t = now_s();
+      *split += (split->empty() ? "" : ", ") + std::string(what) + " " + std::to_string((int)((t - tm) * 1e4) / 10.0).substr(0, 4);
+      tm = t;
+    };
+    auto sp = std::make_unique<Slot>();
+    Slot& s = *sp;
+    layout(s);
+    const int B = cfg.batch_size;
+    const int md = cfg.max_dim;
     if (host_only_) {
       s.host_only = true;
       s.out_bytes = (size_t)out_cap_ * s.cap_canvases;
@@ -544,7 +577,12 @@ struct Engine::Impl {
       // Batch completion is polled by the slot thread (wait_batch): no blocking-sync event.
       check_hip(hipEventCreateWithFlags(&s.ev2, hipEventDefault), "hipEventCreate");
       mark("events");
-      check_hip(hipHostMalloc((void**)&s.h_blob, s.blob_bytes, hipHostMallocDefault), "hipHostMalloc blob");
+      if (arena_slot >= 0 && pin_arena_) {
+        s.arena = true;
+        s.h_blob = pin_arena_ + (size_t)arena_slot * pin_stride_;
+      } else {
+        check_hip(hipHostMalloc((void**)&s.h_blob, s.blob_bytes, hipHostMallocDefault), "hipHostMalloc blob");
+      }
       mark("pinned blob");
       // +64 B tail slack: the median's packed-group loads read whole dwords (k1_median.hip).
       s.d_blob = dmalloc<uint8_t>(s.blob_bytes + 64, "hipMalloc blob");
@@ -571,11 +609,19 @@ struct Engine::Impl {
       check_hip(hipMemsetAsync(s.jw.ticket, 0, sizeof(uint32_t) * s.cap_canvases, s.stream), "memset tickets");
       mark("memsets");
       const size_t out_bytes = (size_t)out_cap_ * s.cap_canvases;
-      check_hip(hipHostMalloc((void**)&s.h_out, out_bytes, hipHostMallocMapped), "hipHostMalloc out");
-      check_hip(hipHostGetDevicePointer((void**)&s.d_out, s.h_out, 0), "hipHostGetDevicePointer out");
-      check_hip(hipHostMalloc((void**)&s.h_sizes, sizeof(int32_t) * s.cap_canvases, hipHostMallocMapped),
-                "hipHostMalloc sizes");
-      check_hip(hipHostGetDevicePointer((void**)&s.d_sizes, s.h_sizes, 0), "hipHostGetDevicePointer sizes");
+      if (s.arena) {
+        const size_t off = (size_t)arena_slot * map_stride_;
+        s.h_out = map_arena_ + off;
+        s.d_out = map_arena_dev_ + off;
+        s.h_sizes = reinterpret_cast<int32_t*>(map_arena_ + off + out_bytes);
+        s.d_sizes = reinterpret_cast<int32_t*>(map_arena_dev_ + off + out_bytes);
+      } else {
+        check_hip(hipHostMalloc((void**)&s.h_out, out_bytes, hipHostMallocMapped), "hipHostMalloc out");
+        check_hip(hipHostGetDevicePointer((void**)&s.d_out, s.h_out, 0), "hipHostGetDevicePointer out");
+        check_hip(hipHostMalloc((void**)&s.h_sizes, sizeof(int32_t) * s.cap_canvases, hipHostMallocMapped),
+                  "hipHostMalloc sizes");
+        check_hip(hipHostGetDevicePointer((void**)&s.d_sizes, s.h_sizes, 0), "hipHostGetDevicePointer sizes");
+      }
       mark("mapped out");
     } catch (...) {
       hip_free_all(s);
@@ -853,7 +899,7 @@ struct Engine::Impl {
       d.stored_bits = L.stored_bits;
       d.slope = L.slope;
       d.intercept = L.intercept;
-      std::tie(d.lut_off, d.lut_base) = norm_lut(L.type, L.stored_bits, L.slope, L.intercept);
+      std::tie(d.lut_off, d.lut_base) = norm_lut(L.type, L.stored_bits, L.slope, L.intercept, s.stream);
       d.f32_off = raw_off;
       // Seeds depend on the slice size only: reuse the last size's list (a batch is nearly always
       // one size) instead of building a vector per slice on the slot thread.
@@ -1561,6 +1607,9 @@ double reserve_streams(int device, int n) {
   for (int i = 0; i < n; ++i) {
     hipStream_t s = nullptr;
     check_hip(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "hipStreamCreate (reserve)");
+    // The process's first host→device copy brings up the runtime's copy path (≈ 10 ms cold): here,
+    // not in the first batch's upload, where it held the slot threads (profiles/r5/cold/).
+    if (i == 0) warm_copy_path(s);
     std::lock_guard<std::mutex> g(g_reserve_m);
     g_reserved.push_back({device, s});
   }

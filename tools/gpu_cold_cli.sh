@@ -11,23 +11,36 @@ R=$GRAFT_REPO_ROOT
 D=/dev/shm/cold_data
 CLI="$R/build/bin/img_processing_parallel --data-root $D/ --out /dev/shm/cold_out --quiet"
 timeout -k 5 60 build/bin/nm03_synth --data-root $D/ --threads 16 > /dev/null || exit 1
-for q in ${QUEUES:-4 2 1}; do
-  timeout -k 10 300 python3 - "$q" "$D" "$O" <<'PY' || exit 2
+# Interleaved: run r of every GPU_MAX_HW_QUEUES value before run r + 1 (box drift hits all alike).
+timeout -k 10 600 python3 - "$D" "$O" <<'PY' || exit 2
 import json, os, sys
 sys.path.insert(0, os.environ["GRAFT_REPO_ROOT"])
 from nm03_capstone_project_amd.utils.cli_wall import time_cli
-q, d, o = sys.argv[1:4]
-js = f"/tmp/cold_q{q}.json"
-argv = [os.path.join(os.environ["GRAFT_REPO_ROOT"], "build/bin/img_processing_parallel"), "--data-root", d + "/",
-        "--out", "/dev/shm/cold_out", "--quiet", "--json", js]
-env = dict(os.environ, GPU_MAX_HW_QUEUES=q)
-res = time_cli(argv, runs=int(os.environ.get("RUNS", "7")), json_path=js, env=env)
-res["GPU_MAX_HW_QUEUES"] = q
-with open(os.path.join(o, "cli_wall.jsonl"), "a") as f:
-    f.write(json.dumps(res) + "\n")
-print(q, res["wall_median_s"], res.get("phases_median_s"))
+d, o = sys.argv[1:3]
+queues = os.environ.get("QUEUES", "4 2 1").split()
+rows = {q: [] for q in queues}
+for r in range(int(os.environ.get("RUNS", "7"))):
+    for q in queues:
+        js = f"/tmp/cold_q{q}.json"
+        argv = [os.path.join(os.environ["GRAFT_REPO_ROOT"], "build/bin/img_processing_parallel"), "--data-root",
+                d + "/", "--out", "/dev/shm/cold_out", "--quiet", "--json", js]
+        res = time_cli(argv, runs=1, json_path=js, env=dict(os.environ, GPU_MAX_HW_QUEUES=q))
+        rows[q].append(res)
+        with open(os.path.join(o, "cli_runs.jsonl"), "a") as f:
+            f.write(json.dumps({"GPU_MAX_HW_QUEUES": q, "run": r, **res}) + "\n")
+for q in queues:
+    walls = sorted(x["wall_median_s"] for x in rows[q])
+    ph = {}
+    for x in rows[q]:
+        for k, v in (x.get("phases_median_s") or {}).items():
+            ph.setdefault(k, []).append(v)
+    med = {k: round(sorted(v)[len(v) // 2], 4) for k, v in ph.items()}
+    line = {"GPU_MAX_HW_QUEUES": q, "wall_median_s": walls[len(walls) // 2], "walls_s": [x["wall_median_s"] for x in rows[q]],
+            "phases_median_s": med}
+    with open(os.path.join(o, "cli_wall.jsonl"), "a") as f:
+        f.write(json.dumps(line) + "\n")
+    print(json.dumps(line))
 PY
-done
 for r in 1 2; do
   (cd /tmp && NM03_BATCH_TRACE=1 NM03_LOG=info timeout -k 10 60 $CLI --json $R/$O/trace_$r.json > $R/$O/trace_$r.log 2>&1) || exit 3
 done
