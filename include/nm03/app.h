@@ -19,10 +19,10 @@ struct AppConfig {
   std::string data_root;  // default: cohort::default_data_root()
   std::string out_dir;    // default per CLI: ../out-sequential, ../out-parallel, ../out-test
   EngineConfig engine;
-  // Ranks, one process per GPU. 0 = every visible GPU: the no-argument img_processing_parallel
-  // uses the whole node, as the reference's omp_set_num_threads(16) uses the whole laptop
-  // (main_parallel.cpp:401).
-  int gpus = 0;
+  // Ranks, one process per GPU (--gpus). kGpusAuto (default): as many visible GPUs as the cohort
+  // repays (resolve_gpus); kGpusAll (--gpus all): every visible GPU, as the reference's
+  // omp_set_num_threads(16) uses the whole laptop (main_parallel.cpp:401); N ≥ 1: exactly N.
+  int gpus = -1;
   bool quiet = false;
   bool cpu = false;        // test_pipeline: golden CPU path (BASELINE config 1)
   bool montage = true;     // test_pipeline: 5-view montage JPEG (headless MultiViewWindow)
@@ -69,8 +69,24 @@ int run_test_pipeline(const AppConfig& cfg);
 // HIP/ROCR_VISIBLE_DEVICES), so the launcher can still fork safely afterwards.
 int visible_gpu_count();
 
-// Ranks for img_processing_parallel: --gpus N, or every visible GPU when unset. Throws when N
-// exceeds the visible GPUs and no NM03_DEVICE_OVERRIDE shares one device between ranks.
-int resolve_gpus(const AppConfig& cfg, const LaunchOptions& lo);
+constexpr int kGpusAuto = -1, kGpusAll = 0;
+// A rank is worth its start-up only with this many slices to process: a cold rank costs ≈ 150–300 ms
+// of ROCm start-up (hipInit, HW queues) that does not shrink with more ranks (started concurrently,
+// 8 processes on one GPU finish within 1.3–3× of one: profiles/r5/startup/), while a cold MI355X
+// pass runs ≈ 35–40k slices/s; below ≈ 4k slices per rank the extra ranks only add their start-up
+// and RCCL's (profiles/r5/cold/, docs/ROUND5_RESPONSE.md).
+constexpr int kAutoSlicesPerRank = 4096;
+
+// Ranks for img_processing_parallel: --gpus N; every visible GPU for --gpus all; for the default
+// (auto) ceil(slices / kAutoSlicesPerRank) clamped to [1, visible] when `slices` ≥ 0 is known, else
+// every visible GPU. Throws when N exceeds the visible GPUs and no NM03_DEVICE_OVERRIDE shares one
+// device between ranks.
+int resolve_gpus(const AppConfig& cfg, const LaunchOptions& lo, int64_t slices = -1);
+// The auto policy alone: ceil(slices / kAutoSlicesPerRank) clamped to [1, max(1, visible)].
+int auto_gpus(int64_t slices, int visible);
+
+// Slices of the cohort under cfg.data_root, counted from the directory listings only (no file is
+// opened, no HIP call): what the auto rank count needs before the ranks are forked. -1 on error.
+int64_t count_cohort_slices(const AppConfig& cfg);
 
 }  // namespace nm03::app

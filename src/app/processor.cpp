@@ -43,7 +43,8 @@ void usage(const std::string& which) {
   std::cout << "usage: " << which << " [options]\n"
             << "  --data-root DIR        dataset root (default $NM03_DATA_ROOT or ../data/)\n"
             << "  --out DIR              output root (default ../out-" << (which == "test_pipeline" ? "test" : which == "img_processing_sequential" ? "sequential" : "parallel") << ")\n"
-            << "  --gpus N|all           data-parallel ranks, one process per MI355X (parallel CLI)\n"
+            << "  --gpus N|all|auto      data-parallel ranks, one process per MI355X (parallel CLI; default auto:\n"
+            << "                         one rank per 4096 slices of the cohort, at most every visible GPU)\n"
             << "  --device N             GPU for a single-rank run\n"
             << "  --batch-size N         slices per GPU batch (default 25)\n"
             << "  --streams N            batches in flight per GPU (default 3)\n"
@@ -140,7 +141,7 @@ AppConfig parse_args(int argc, char** argv, const std::string& which) {
     else if (a == "--out") c.out_dir = val();
     else if (a == "--gpus") {
       std::string v = val();
-      c.gpus = v == "all" ? 0 : std::max(1, std::atoi(v.c_str()));
+      c.gpus = v == "all" ? kGpusAll : v == "auto" ? kGpusAuto : std::max(1, std::atoi(v.c_str()));
     } else if (a == "--device") c.engine.device = std::atoi(val().c_str());
     else if (a == "--batch-size") c.engine.batch_size = std::atoi(val().c_str());
     else if (a == "--streams") c.engine.streams = std::atoi(val().c_str());
@@ -748,7 +749,9 @@ int parallel_rank(const AppConfig& cfg, int rank, int size, Comm& comm, int devi
     std::vector<std::vector<double>> rows((size_t)size);
     for (int r = 0; r < size; ++r)
       rows[r].assign(all_rows.begin() + (size_t)r * kNumRankFields, all_rows.begin() + (size_t)(r + 1) * kNumRankFields);
-    write_json(cfg.json, std::string("{\"mode\": \"parallel\", \"gpus\": ") + std::to_string(size) + ", \"main_unix_s\": " +
+    const std::string req = cfg.gpus == kGpusAuto ? "\"auto\"" : cfg.gpus == kGpusAll ? "\"all\"" : std::to_string(cfg.gpus);
+    write_json(cfg.json, std::string("{\"mode\": \"parallel\", \"gpus\": ") + std::to_string(size) +
+                             ", \"gpus_requested\": " + req + ", \"main_unix_s\": " +
                              fmt(cfg.main_unix_s, 17) + ", \"backend\": \"" +
                              comm.backend() + "\", \"repeat\": " + std::to_string(cfg.repeat) + ", \"engine_setup_s\": " +
                              fmt(setup_s) + ", \"hip_init_s\": " + fmt(su.hip_init_s) + ", \"engine_ctor_s\": " +
@@ -802,9 +805,31 @@ int cli_exit(int rc) {
   return rc;
 }
 
-int resolve_gpus(const AppConfig& cfg, const LaunchOptions& lo) {
+int64_t count_cohort_slices(const AppConfig& cfg) {
+  try {
+    const std::string base = cohort::cohort_dir(cfg.data_root);
+    int64_t n = 0;
+    for (const auto& pid : cohort::find_patient_dirs(base)) {
+      try {
+        n += (int64_t)cohort::list_patient_series(base, pid).files.size();
+      } catch (const std::exception&) {
+      }
+    }
+    return n;
+  } catch (const std::exception&) {
+    return -1;
+  }
+}
+
+int auto_gpus(int64_t slices, int visible) {
+  const int64_t want = (std::max<int64_t>(slices, 0) + kAutoSlicesPerRank - 1) / kAutoSlicesPerRank;
+  return (int)std::max<int64_t>(1, std::min<int64_t>(std::max(1, visible), want));
+}
+
+int resolve_gpus(const AppConfig& cfg, const LaunchOptions& lo, int64_t slices) {
   const int visible = visible_gpu_count();
-  const int n = cfg.gpus > 0 ? cfg.gpus : std::max(1, visible);  // default: every visible GPU
+  int n = cfg.gpus > 0 ? cfg.gpus : std::max(1, visible);  // --gpus N, or every visible GPU
+  if (cfg.gpus == kGpusAuto && slices >= 0) n = auto_gpus(slices, n);
   if (n > 1 && lo.device_override < 0 && visible > 0 && n > visible)
     throw std::runtime_error("--gpus " + std::to_string(n) + " exceeds the " + std::to_string(visible) +
                              " visible GPU(s); set NM03_DEVICE_OVERRIDE=<device> to run several ranks on one GPU");
@@ -816,7 +841,8 @@ int run_parallel(const AppConfig& cfg) {
     cohort::make_dirs(cfg.out_dir);  // OptimizedParallelProcessor ctor (main_parallel.cpp:219-231)
     if (cfg.mode == "3d") return run_volume_cohort(cfg);
     LaunchOptions lo = LaunchOptions::from_env();
-    const int n = resolve_gpus(cfg, lo);
+    // auto: size the job to the cohort, counted from its directory listings before any fork
+    const int n = resolve_gpus(cfg, lo, cfg.gpus == kGpusAuto ? count_cohort_slices(cfg) : -1);
     std::vector<int> rank_devices;
     for (int r = 0; r < n; ++r)
       rank_devices.push_back(n > 1 ? lo.device_of(r) : lo.device_override >= 0 ? lo.device_override : cfg.engine.device);

@@ -14,6 +14,7 @@
 #include <cstring>
 #include <thread>
 
+#include "nm03/app.h"
 #include "nm03/cohort.h"
 #include "nm03/comm.h"
 #include "nm03/dicom.h"
@@ -442,6 +443,14 @@ PYBIND11_MODULE(_nm03, m) {
 
   // ---- cohort / synthetic data -------------------------------------------------------------------
   m.def("extract_file_number", &cohort::extract_file_number);
+  // img_processing_parallel's default rank count (app.h): policy and the listing-only slice count.
+  m.def("auto_gpus", &app::auto_gpus, py::arg("slices"), py::arg("visible"));
+  m.def("auto_slices_per_rank", [] { return app::kAutoSlicesPerRank; });
+  m.def("count_cohort_slices", [](const std::string& data_root) {
+    app::AppConfig c;
+    c.data_root = cohort::with_slash(data_root);
+    return app::count_cohort_slices(c);
+  });
   m.def("default_data_root", &cohort::default_data_root);
   m.def("cohort_dir", &cohort::cohort_dir);
   m.def("test_slice_path", &cohort::test_slice_path);

@@ -1032,7 +1032,7 @@ int run_volume_cohort(const AppConfig& cfg) {
   LaunchOptions lo = LaunchOptions::from_env();
   int n = 1;
   if (cfg.cpu) {  // golden model: the ranks are CPU processes over the host comm (default 1)
-    n = std::max(1, cfg.gpus);
+    n = std::max(1, cfg.gpus);  // auto / all: 1
     lo.comm = "host";
   } else {
     n = resolve_gpus(cfg, lo);

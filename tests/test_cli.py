@@ -175,3 +175,19 @@ def test_native_bench_cohort_host_only(native, cohort_root, tmp_path):
     n = rec["slices_per_step"]
     files = [p for d in out.iterdir() for p in d.iterdir()]
     assert len(files) == 2 * n and all(p.read_bytes()[:2] == b"\xff\xd8" for p in files)
+
+
+def test_parallel_default_rank_count_policy(native, cohort_root):
+    """img_processing_parallel without --gpus (auto): one rank per kAutoSlicesPerRank slices of the
+    cohort, at least 1, at most every visible GPU; the count comes from directory listings only."""
+    per = native.auto_slices_per_rank()
+    assert per == 4096
+    assert native.auto_gpus(465, 8) == 1          # the T1+C cohort: one GPU
+    assert native.auto_gpus(per, 8) == 1 and native.auto_gpus(per + 1, 8) == 2
+    assert native.auto_gpus(10000, 8) == 3        # BASELINE config 4
+    assert native.auto_gpus(10 ** 6, 8) == 8      # capped at the visible GPUs
+    assert native.auto_gpus(0, 8) == 1 and native.auto_gpus(50000, 0) == 1
+    n = native.count_cohort_slices(cohort_root)
+    base = native.cohort_dir(cohort_root)
+    assert n == sum(len(native.list_patient_series(base, p)[1]) for p in native.find_patient_dirs(base))
+    assert native.count_cohort_slices("/nonexistent/") == -1
