@@ -73,7 +73,9 @@ std::vector<uint8_t> region_grow3d(const std::vector<uint8_t>& band, int w, int 
 std::vector<uint8_t> dilate3d(const std::vector<uint8_t>& m, int w, int h, int d, int size, bool ball = false);
 
 // Renderers (A.9) onto an out_w×out_h black canvas.
-std::vector<uint8_t> render_gray(const std::vector<float>& values, const RenderGeom& g, float lo, float hi);
+// `nearest`: RenderParams::filter == kFilterNearest (the source pixel under each canvas pixel's centre).
+std::vector<uint8_t> render_gray(const std::vector<float>& values, const RenderGeom& g, float lo, float hi,
+                                 bool nearest = false);
 std::vector<uint8_t> render_labels(const std::vector<uint8_t>& label, const std::vector<uint8_t>& border_mask,
                                    const RenderGeom& g, uint8_t fill, uint8_t border_value);
 

@@ -89,7 +89,8 @@ struct RenderDesc {
   uint8_t kind;
   uint8_t type, stored_bits;
   uint8_t fill, border_value;
-  uint8_t pad0[3];
+  uint8_t filter;       // gray kinds: RenderFilter (0 bilinear, 1 nearest); labels: always nearest
+  uint8_t pad0[2];
   uint32_t slice;       // stats index
   uint32_t src_off;     // u16 elements (raw) / f32 elements / u64 words (labels)
   uint32_t border_off;  // u64 words (labels)

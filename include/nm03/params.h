@@ -58,7 +58,13 @@ struct RenderParams {
   int border_radius = 2;
   // ImageFileExporter .jpg → Qt/libjpeg default quality 75.
   int jpeg_quality = 75;
+  // Interpolation of the gray renders (original / preprocessed image; labels are always nearest):
+  // FAST's ImageRenderer filtering is not pinned by the reference (main_sequential.cpp:259), so it is
+  // a flag (--render-filter). kFilterBilinear (default) or kFilterNearest.
+  int filter = 0;
 };
+
+enum RenderFilter : int { kFilterBilinear = 0, kFilterNearest = 1 };
 
 // Adaptive seed points of the reference (main_sequential.cpp:214-241): centre, centre ± (W/8, H/8)
 // and a grid x∈[W/4, 3W/4) step W/10 (same for y). Integer division as in the reference.

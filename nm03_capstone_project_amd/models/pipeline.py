@@ -43,6 +43,7 @@ class PipelineConfig:
     border_opacity: float = 1.0
     border_radius: int = 2
     jpeg_quality: int = 75
+    render_filter: int = 0  # gray renders: 0 bilinear (default), 1 nearest (params.h RenderFilter)
     # engine
     batch_size: int = 25
     streams: int = 3
@@ -68,6 +69,7 @@ class PipelineConfig:
         r = native().RenderParams()
         for k in self._RENDER:
             setattr(r, k, getattr(self, k))
+        r.filter = self.render_filter
         return r
 
     def engine_config(self):

@@ -114,9 +114,10 @@ def region_grow(bnd, seeds, connectivity=4):
         reg = nxt
 
 
-def render_gray(values, lo, hi, out_w=512, out_h=512):
+def render_gray(values, lo, hi, out_w=512, out_h=512, nearest=False):
     """Bilinear 2× (generally: fit) render of an [H, W] float image onto out_h×out_w, f32 math
-    in the contract order (pixel_math.h), window [lo, hi] → uint8."""
+    in the contract order (pixel_math.h), window [lo, hi] → uint8. `nearest`: the source pixel under
+    each canvas pixel's centre instead (--render-filter nearest)."""
     h, w = values.shape
     scale = min(out_w / w, out_h / h)
     ox, oy = (out_w - w * scale) / 2, (out_h - h * scale) / 2
@@ -138,6 +139,8 @@ def render_gray(values, lo, hi, out_w=512, out_h=512):
     top = (1 - wx) * a + wx * b
     bot = (1 - wx) * c + wx * d
     val = (1 - wy)[:, None] * top + wy[:, None] * bot
+    if nearest:
+        val = values[torch.floor(sy).long().clamp(0, h - 1)][:, torch.floor(sx).long().clamp(0, w - 1)]
     inv = torch.tensor(1.0, dtype=torch.float32) / torch.tensor(hi - lo, dtype=torch.float32) if hi > lo else torch.tensor(0.0)
     g = ((val - lo) * inv.to(val.device)).clamp(0, 1)
     out = torch.floor(g * 255 + 0.5).to(torch.uint8)

@@ -53,6 +53,7 @@ void usage(const std::string& which) {
             << "  --srg-connectivity C   4|8 (2D) / 6|26 (3D)\n"
             << "  --dilation-size S      (default 3; 7 in --mode 3d)    --erosion-size S (default 3)\n"
             << "  --se-shape square|disc structuring element of dilation/erosion (3D: cube|ball; default square)\n"
+            << "  --render-filter bilinear|nearest  interpolation of the gray renders (default bilinear)\n"
             << "  --quality Q            JPEG quality (default 75)\n"
             << "  --mode 2d|3d           3d: whole series as a volume (SRG 6-conn + cube dilation)\n"
             << "  --split-volume         3d: each volume split into z-slabs over all ranks (halo exchange)\n"
@@ -171,6 +172,14 @@ AppConfig parse_args(int argc, char** argv, const std::string& which) {
     }
     else if (a == "--resume") c.engine.resume = true;
     else if (a == "--frame") c.engine.pipe.frame = std::atoi(val().c_str());
+    else if (a == "--render-filter") {
+      const std::string v = val();
+      if (v != "bilinear" && v != "nearest") {
+        std::cerr << "--render-filter must be bilinear or nearest" << std::endl;
+        std::exit(2);
+      }
+      c.engine.render.filter = v == "nearest" ? kFilterNearest : kFilterBilinear;
+    }
     else if (a == "--se-shape") {
       const std::string v = val();
       if (v != "square" && v != "disc") {

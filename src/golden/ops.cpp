@@ -317,9 +317,23 @@ std::vector<uint8_t> dilate3d(const std::vector<uint8_t>& m, int w, int h, int d
   return a;
 }
 
-std::vector<uint8_t> render_gray(const std::vector<float>& v, const RenderGeom& g, float lo, float hi) {
+std::vector<uint8_t> render_gray(const std::vector<float>& v, const RenderGeom& g, float lo, float hi, bool nearest) {
   std::vector<uint8_t> out((size_t)g.out_w * g.out_h, 0);
   const float inv = window_inv(lo, hi);
+  if (nearest) {
+    for (int u = 0; u < g.out_h; ++u) {
+      const float sy = render_src_coord(u, g.oy, g.invy);
+      if (!(sy >= 0.0f && sy < (float)g.src_h)) continue;
+      const int y = clampi((int)std::floor(sy), 0, g.src_h - 1);
+      for (int t = 0; t < g.out_w; ++t) {
+        const float sx = render_src_coord(t, g.ox, g.invx);
+        if (!(sx >= 0.0f && sx < (float)g.src_w)) continue;
+        const int x = clampi((int)std::floor(sx), 0, g.src_w - 1);
+        out[(size_t)u * g.out_w + t] = gray_u8(v[(size_t)y * g.src_w + x], lo, inv);
+      }
+    }
+    return out;
+  }
   for (int u = 0; u < g.out_h; ++u) {
     const float sy = render_src_coord(u, g.oy, g.invy);
     if (!(sy >= 0.0f && sy < (float)g.src_h)) continue;
@@ -380,7 +394,7 @@ SliceResult run(const SliceInput& s, const PipelineParams& p, bool with_erosion)
 SliceJpegs export_jpegs(const SliceInput& s, const SliceResult& r, const PipelineParams& p, const RenderParams& rp) {
   RenderGeom g = make_render_geom(s.w, s.h, s.spacing_x, s.spacing_y, rp.out_width, rp.out_height);
   SliceJpegs j;
-  std::vector<uint8_t> c0 = render_gray(rescaled(s, p), g, r.window_lo, r.window_hi);
+  std::vector<uint8_t> c0 = render_gray(rescaled(s, p), g, r.window_lo, r.window_hi, rp.filter == kFilterNearest);
   j.original = jpeg::encode_gray420(c0.data(), g.out_w, g.out_h, g.out_w, rp.jpeg_quality);
   std::vector<uint8_t> bm = border(r.dilated, s.w, s.h, rp.border_radius);
   std::vector<uint8_t> c1 =
@@ -397,8 +411,9 @@ StageImages test_pipeline_images(const SliceInput& in, const PipelineParams& p, 
   const uint8_t fill = opacity_u8(rp.label_opacity), bv = opacity_u8(rp.border_opacity);
   auto mm = std::minmax_element(r.sharpened.begin(), r.sharpened.end());
   auto& c = out.canvases;
-  c.push_back(render_gray(rescaled(in, p), g, r.window_lo, r.window_hi));
-  c.push_back(render_gray(r.sharpened, g, *mm.first, *mm.second));
+  const bool nearest = rp.filter == kFilterNearest;
+  c.push_back(render_gray(rescaled(in, p), g, r.window_lo, r.window_hi, nearest));
+  c.push_back(render_gray(r.sharpened, g, *mm.first, *mm.second, nearest));
   c.push_back(render_labels(r.region, border(r.region, in.w, in.h, rp.border_radius), g, fill, bv));
   c.push_back(render_labels(r.eroded, border(r.eroded, in.w, in.h, rp.border_radius), g, fill, bv));
   c.push_back(render_labels(r.dilated, border(r.dilated, in.w, in.h, rp.border_radius), g, fill, bv));

@@ -55,6 +55,10 @@ __device__ __forceinline__ uint32_t render_pixel(const RenderDesc& d, const uint
     const int y = clampi((int)floorf(sy), 0, H - 1), x = clampi((int)floorf(sx), 0, W - 1);
     return render_label_pixel(d, bits, x, y);
   }
+  if (d.filter == 1) {  // --render-filter nearest: the source pixel under the canvas pixel's centre
+    const int y = clampi((int)floorf(sy), 0, H - 1), x = clampi((int)floorf(sx), 0, W - 1);
+    return gray_u8(render_src_value(d, raw, f32, x, y), win.lo, win.inv);
+  }
   const float fy = sy - 0.5f, fx = sx - 0.5f;
   const float y0f = floorf(fy), x0f = floorf(fx);
   const float wy = fy - y0f, wx = fx - x0f;

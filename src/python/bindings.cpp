@@ -265,7 +265,8 @@ PYBIND11_MODULE(_nm03, m) {
       .def_readwrite("label_opacity", &RenderParams::label_opacity)
       .def_readwrite("border_opacity", &RenderParams::border_opacity)
       .def_readwrite("border_radius", &RenderParams::border_radius)
-      .def_readwrite("jpeg_quality", &RenderParams::jpeg_quality);
+      .def_readwrite("jpeg_quality", &RenderParams::jpeg_quality)
+      .def_readwrite("filter", &RenderParams::filter);
   py::class_<EngineConfig>(m, "EngineConfig")
       .def(py::init<>())
       .def_readwrite("device", &EngineConfig::device)
@@ -584,12 +585,16 @@ PYBIND11_MODULE(_nm03, m) {
         return to_np<uint8_t>(golden::dilate3d(from_np<uint8_t>(mk), w, h, d, size, ball), {d, h, w});
       },
       py::arg("mask"), py::arg("size"), py::arg("ball") = false);
-  m.def("golden_render_gray", [](py::array_t<float, py::array::c_style | py::array::forcecast> v, float lo, float hi,
-                                 float sx, float sy, int out_w, int out_h) {
-    const int h = (int)v.shape(0), w = (int)v.shape(1);
-    RenderGeom g = make_render_geom(w, h, sx, sy, out_w, out_h);
-    return to_np<uint8_t>(golden::render_gray(from_np<float>(v), g, lo, hi), {out_h, out_w});
-  });
+  m.def(
+      "golden_render_gray",
+      [](py::array_t<float, py::array::c_style | py::array::forcecast> v, float lo, float hi, float sx, float sy, int out_w,
+         int out_h, bool nearest) {
+        const int h = (int)v.shape(0), w = (int)v.shape(1);
+        RenderGeom g = make_render_geom(w, h, sx, sy, out_w, out_h);
+        return to_np<uint8_t>(golden::render_gray(from_np<float>(v), g, lo, hi, nearest), {out_h, out_w});
+      },
+      py::arg("values"), py::arg("lo"), py::arg("hi"), py::arg("sx"), py::arg("sy"), py::arg("out_w"), py::arg("out_h"),
+      py::arg("nearest") = false);
   m.def("golden_render_labels", [](py::array_t<uint8_t, py::array::c_style | py::array::forcecast> lab,
                                    py::array_t<uint8_t, py::array::c_style | py::array::forcecast> brd, float sx, float sy,
                                    int out_w, int out_h, int fill, int bv) {

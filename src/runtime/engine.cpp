@@ -928,6 +928,7 @@ struct Engine::Impl {
         r.stored_bits = L.stored_bits;
         r.fill = fill;
         r.border_value = bval;
+        r.filter = (uint8_t)(cfg.render.filter == kFilterNearest ? 1 : 0);
         r.slice = (uint32_t)c;
         r.src_w = (uint16_t)L.w;
         r.src_h = (uint16_t)L.h;
@@ -970,7 +971,8 @@ struct Engine::Impl {
       j.out_cap = out_cap_;
       // Export runs render straight into the JPEG block kernel when the fit is an exact 2× (the
       // canvas is never materialised); test runs keep canvases for inspection.
-      j.render = (mode == 0 && render_is_exact_2x(rd[k], cw, ch)) ? k : -1;
+      // (a nearest-filtered gray render always takes the canvas path: the fused 2× render is bilinear)
+      j.render = (mode == 0 && render_is_exact_2x(rd[k], cw, ch) && (rd[k].kind == kRenderLabels || !rd[k].filter)) ? k : -1;
       if (j.render < 0) s.any_canvas = true;
     }
     s.ncanvas = ncanv;

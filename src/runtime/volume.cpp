@@ -539,6 +539,7 @@ std::vector<std::vector<uint8_t>> VolumeRunner::export_jpegs(const VolumeInput& 
       RenderDesc& r = rd[k];
       std::memset(&r, 0, sizeof(r));
       r.kind = (k & 1) ? kRenderLabels : kRenderRawGray;
+      r.filter = (uint8_t)(rp.filter == kFilterNearest ? 1 : 0);
       r.type = (uint8_t)v.type;
       r.stored_bits = (uint8_t)v.stored_bits;
       r.fill = fill;
@@ -561,7 +562,7 @@ std::vector<std::vector<uint8_t>> VolumeRunner::export_jpegs(const VolumeInput& 
       j.canvas_off = (uint32_t)(k * canvas_bytes);
       j.out_off = (uint64_t)k * kVolOutCap;
       j.out_cap = kVolOutCap;
-      j.render = render_is_exact_2x(r, cw, ch) ? k : -1;
+      j.render = render_is_exact_2x(r, cw, ch) && (r.kind == kRenderLabels || !r.filter) ? k : -1;
       any_canvas |= j.render < 0;
     }
     auto* d_rd = X.tables.as<uint8_t>();
@@ -719,7 +720,7 @@ std::vector<std::vector<uint8_t>> golden_export(const VolumeInput& v, const std:
   for (int z = 0; z < v.d; ++z) {
     const auto mm = std::minmax_element(vals[z].begin(), vals[z].end());
     std::vector<uint8_t> lab(dil.begin() + z * plane, dil.begin() + (z + 1) * plane);
-    const auto c0 = golden::render_gray(vals[z], g, *mm.first, *mm.second);
+    const auto c0 = golden::render_gray(vals[z], g, *mm.first, *mm.second, rp.filter == kFilterNearest);
     const auto c1 = golden::render_labels(lab, golden::border(lab, v.w, v.h, rp.border_radius), g,
                                           opacity_u8(rp.label_opacity), opacity_u8(rp.border_opacity));
     files[2 * z] = jpeg::encode_gray420(c0.data(), rp.out_width, rp.out_height, rp.out_width, rp.jpeg_quality);

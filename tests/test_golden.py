@@ -182,3 +182,20 @@ def test_golden_pipeline_se_shape(native):
     assert np.array_equal(dc["dilated"].astype(bool), native.golden_morph(dc["region"].astype(np.uint8), 3, True, True).astype(bool))
     assert np.array_equal(dc["eroded"].astype(bool), native.golden_morph(dc["region"].astype(np.uint8), 3, False, True).astype(bool))
     assert not np.array_equal(sq["dilated"], dc["dilated"])
+
+
+@pytest.mark.parametrize("shape,spacing", [((256, 256), (1.0, 1.0)), ((200, 160), (0.9, 1.2))])
+def test_render_nearest_vs_torch(native, shape, spacing):
+    """--render-filter nearest: the golden gray render equals the torch reference's nearest sampling
+    (exact-2× fits and general fits); bilinear stays the default."""
+    h, w = shape
+    v = native.phantom_slice(h, w, 2, 3, 9, 5).astype(np.float32)
+    lo, hi = float(v.min()), float(v.max())
+    sx, sy = spacing
+    got = native.golden_render_gray(v, lo, hi, sx, sy, 512, 512, True)
+    if sx == sy:
+        ref = R.render_gray(torch.from_numpy(v), lo, hi, nearest=True).numpy()
+        assert np.array_equal(got, ref)
+    bil = native.golden_render_gray(v, lo, hi, sx, sy, 512, 512)
+    assert not np.array_equal(got, bil)
+    assert np.array_equal(bil, native.golden_render_gray(v, lo, hi, sx, sy, 512, 512, False))

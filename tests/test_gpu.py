@@ -1212,3 +1212,26 @@ def test_cli_fresh_process_512_cohort_render_from_slot_threads(native, tmp_path)
         stem = f.name[:-4]
         assert open(out / f"PGBM-{p + 1:03d}" / f"{stem}_original.jpg", "rb").read() == g["jpeg_original"]
         assert open(out / f"PGBM-{p + 1:03d}" / f"{stem}_processed.jpg", "rb").read() == g["jpeg_processed"]
+
+
+def test_engine_render_nearest_bit_exact(native, cohort_root, tmp_path):
+    """--render-filter nearest through the GPU: every stage image of one slice (K3 canvases) and a
+    cohort run's export pairs (the nearest gray renders leave the fused 2× path for K3) equal the
+    golden model."""
+    raw = _phantom(native)
+    meta = {"type": "u16", "stored_bits": 16, "slope": 1.0, "intercept": 0.0, "spacing_x": 1.0, "spacing_y": 1.0}
+    pipe = nm.SlicePipeline(nm.PipelineConfig(batch_size=1, streams=1, threads=2, render_filter=1))
+    gpu, ref = pipe.run_array(raw, meta), pipe.golden(raw, meta)
+    assert gpu["jpegs"][0] == ref["jpeg_original"] and gpu["jpegs"][4] == ref["jpeg_processed"]
+    out = str(tmp_path / "o")
+    items = _items(native, cohort_root, out)[:30]
+    cfg = nm.PipelineConfig(batch_size=8, streams=2, threads=4, render_filter=1)
+    st, _ = native.Engine(cfg.engine_config()).run(items)
+    assert all(c == 0 for c, _ in st)
+    for f, od in items[::7]:
+        r, m = native.read_slice(f)
+        g = native.golden_run(r, m["type"], m["stored_bits"], m["slope"], m["intercept"], native.PipelineParams(),
+                              cfg.render_params(), m["spacing_x"], m["spacing_y"])
+        stem = os.path.splitext(os.path.basename(f))[0]
+        assert open(os.path.join(od, stem + "_original.jpg"), "rb").read() == g["jpeg_original"]
+        assert open(os.path.join(od, stem + "_processed.jpg"), "rb").read() == g["jpeg_processed"]
