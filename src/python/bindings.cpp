@@ -1276,6 +1276,22 @@ PYBIND11_MODULE(_nm03, m) {
         c.allreduce_max_f64(v.data(), v.size());
         return v;
       })
+      .def("start_data_plane", [](Comm& c) {
+        py::gil_scoped_release nogil;
+        c.start_data_plane();
+      })
+      .def("promote", [](Comm& c) {
+        py::gil_scoped_release nogil;
+        c.promote();
+      })
+      .def_property_readonly("data_plane_times", [](const Comm& c) {
+        const Comm::DataPlaneTimes t = c.data_plane_times();
+        py::dict d;
+        d["start_s"] = t.start_s;
+        d["wait_s"] = t.wait_s;
+        d["init_upper_s"] = t.init_upper_s;
+        return d;
+      })
       .def_property_readonly("transport_size", &Comm::transport_size)
       .def_property_readonly("transport_rank", &Comm::transport_rank)
       .def_property_readonly("transport_device", &Comm::transport_device)
@@ -1343,6 +1359,9 @@ PYBIND11_MODULE(_nm03, m) {
     return make_rccl_comm(rank, size, v, device, seg, t);
   }, py::arg("rank"), py::arg("size"), py::arg("unique_id"), py::arg("device"), py::arg("segment") = nullptr,
      py::arg("timeout_s") = -1.0);
+  m.def("deferred_rccl_comm", [](int rank, int size, int device, std::shared_ptr<ShmSegment> seg, double t) {
+    return make_deferred_rccl_comm(rank, size, device, std::move(seg), t);
+  }, py::arg("rank"), py::arg("size"), py::arg("device"), py::arg("segment"), py::arg("timeout_s") = -1.0);
   m.def("comm_timeout_s", &comm_timeout_s);
   py::register_exception<CommError>(m, "CommError", PyExc_RuntimeError);
 }

@@ -145,3 +145,21 @@ def test_native_comm_refuses_multi_node_world(monkeypatch):
     import pytest
     with pytest.raises(RuntimeError, match="LOCAL_WORLD_SIZE"):
         nc.make_native_comm(0, 4, 0, "host", timeout_s=1)
+
+
+def test_deferred_rccl_comm_control_plane_without_gpu(native):
+    """Before promote() the deferred RCCL communicator is the shared-memory host comm (no HIP): the
+    start-up collectives work on a machine without a GPU, and promote() reports RCCL's failure as a
+    CommError instead of hanging."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("CPU-only check")
+    seg, name = native.shm_create(1)
+    c = native.deferred_rccl_comm(0, 1, 0, seg, 5.0)
+    c.barrier()
+    assert c.broadcast_bytes(b"work-list", 0) == b"work-list"
+    assert c.allreduce_max([2.5]) == [2.5]
+    assert c.transport_size == -1 and c.data_plane_times["start_s"] == -1
+    with pytest.raises(RuntimeError):
+        c.promote()
+    seg.wait_attached_and_unlink(5.0)

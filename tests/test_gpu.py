@@ -1235,3 +1235,21 @@ def test_engine_render_nearest_bit_exact(native, cohort_root, tmp_path):
         stem = os.path.splitext(os.path.basename(f))[0]
         assert open(os.path.join(od, stem + "_original.jpg"), "rb").read() == g["jpeg_original"]
         assert open(os.path.join(od, stem + "_processed.jpg"), "rb").read() == g["jpeg_processed"]
+
+
+def test_deferred_rccl_comm_single_rank(native):
+    """The communicator launch_ranks gives RCCL ranks: shared-memory control plane until promote(),
+    RCCL started by start_data_plane() and carrying every collective afterwards (one rank: a second
+    needs a second GPU)."""
+    seg, name = native.shm_create(1)
+    c = native.deferred_rccl_comm(0, 1, 0, seg, 30.0)
+    assert c.backend == "rccl" and c.transport_size == -1  # RCCL not up yet
+    c.barrier()
+    assert c.broadcast_bytes(b"plan" * 100, 0) == b"plan" * 100
+    c.start_data_plane()
+    c.promote()
+    assert c.transport_size == 1 and c.transport_device == 0
+    assert c.allreduce_sum([3, 4]) == [3, 4] and c.allgather_bytes(b"xy") == [b"xy"]
+    t = c.data_plane_times
+    assert t["start_s"] >= 0 and t["init_upper_s"] >= t["wait_s"] >= 0
+    seg.wait_attached_and_unlink(5.0)
