@@ -77,6 +77,16 @@ void write_json(const std::string& path, const std::string& body) {
   f << body << "\n";
 }
 
+std::string json_escape(const std::string& s) {
+  std::string o;
+  for (char ch : s) {
+    if (ch == '"' || ch == '\\') o += '\\';
+    if ((unsigned char)ch < 0x20) ch = ' ';
+    o += ch;
+  }
+  return o;
+}
+
 std::string fmt(double v, int p = 6) {
   std::ostringstream o;
   o << std::setprecision(p) << v;
@@ -774,7 +784,9 @@ int parallel_rank(const AppConfig& cfg, int rank, int size, Comm& comm, int devi
                              ", \"write_s\": " + fmt(agg.write_s) + ", \"jpeg_fallbacks\": " +
                              std::to_string(agg.jpeg_fallbacks) + "}, \"per_rank\": " + per_rank_json(rows) +
                              ", \"comm\": {\"backend\": \"" + comm.backend() + "\", \"nranks\": " +
-                             std::to_string(comm.transport_size()) + "}, \"devices\": " + rank_devices_json(devices) + "}");
+                             std::to_string(comm.transport_size()) +
+                             (comm.fallback_error().empty() ? std::string() : ", \"rccl_error\": \"" + json_escape(comm.fallback_error()) + "\"") +
+                             "}, \"devices\": " + rank_devices_json(devices) + "}");
   }
   if (fast_exit_enabled() && engine_p) {  // the process ends in cli_exit: no teardown
     engine_p->quiesce();

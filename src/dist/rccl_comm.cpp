@@ -254,7 +254,7 @@ class DeferredRcclComm final : public Comm {
         host_(make_host_comm(seg, rank, timeout_s)), t_created_(mono_s()) {}
   int rank() const override { return rank_; }
   int size() const override { return size_; }
-  const char* backend() const override { return "rccl"; }
+  const char* backend() const override { return fallback_ ? "host" : "rccl"; }
 
   void broadcast(void* buf, size_t bytes, int root) override { plane().broadcast(buf, bytes, root); }
   void allgather(const void* send, size_t bytes, void* recv) override { plane().allgather(send, bytes, recv); }
@@ -268,13 +268,15 @@ class DeferredRcclComm final : public Comm {
   void sendrecv_device(const void* send, size_t sbytes, int dst, void* recv, size_t rbytes, int src,
                        void* stream) override {
     promote();
+    if (fallback_) return Comm::sendrecv_device(send, sbytes, dst, recv, rbytes, src, stream);  // staged, host plane
     rccl_->sendrecv_device(send, sbytes, dst, recv, rbytes, src, stream);
   }
   int64_t allreduce_sum_i64_device(int64_t* v, void* stream) override {
     promote();
+    if (fallback_) return Comm::allreduce_sum_i64_device(v, stream);
     return rccl_->allreduce_sum_i64_device(v, stream);
   }
-  bool device_native() const override { return true; }
+  bool device_native() const override { return !fallback_; }
   int transport_size() const override { return promoted_ ? rccl_->transport_size() : -1; }
   int transport_rank() const override { return promoted_ ? rccl_->transport_rank() : -1; }
   int transport_device() const override { return promoted_ ? rccl_->transport_device() : -1; }
@@ -310,8 +312,11 @@ class DeferredRcclComm final : public Comm {
     cv_.notify_all();
   }
 
+  // Every rank brings RCCL up, then the ranks agree on the control plane: all up → every later
+  // collective on RCCL; any rank failed (an RCCL error, not a dead peer: the job abort flag still
+  // ends the job) → all stay on the control plane and say so (backend() "host", fallback_error()).
   void promote() override {
-    if (promoted_) return;
+    if (promoted_ || fallback_) return;
     const double t0 = mono_s();
     bool start_here = false;
     {
@@ -319,27 +324,41 @@ class DeferredRcclComm final : public Comm {
       start_here = state_ == kIdle;
     }
     if (start_here) start_data_plane();  // nobody started it: start it on this thread
-    {
-      // Bounded, abort-aware wait for a start-up thread still inside start_data_plane.
-      std::unique_lock<std::mutex> g(m_);
-      const double deadline = t0 + timeout_;
-      while (state_ == kStarting) {
-        cv_.wait_for(g, std::chrono::milliseconds(2));
-        if (state_ != kStarting) break;
-        seg_->check_abort(rank_);
-        if (mono_s() > deadline) {
-          seg_->raise_abort(rank_);
-          throw CommError("RCCL start-up timed out on rank " + std::to_string(rank_));
+    std::string err;
+    try {
+      {
+        // Bounded, abort-aware wait for a start-up thread still inside start_data_plane.
+        std::unique_lock<std::mutex> g(m_);
+        const double deadline = t0 + timeout_;
+        while (state_ == kStarting) {
+          cv_.wait_for(g, std::chrono::milliseconds(2));
+          if (state_ != kStarting) break;
+          seg_->check_abort(rank_);
+          if (mono_s() > deadline) {
+            seg_->raise_abort(rank_);
+            throw CommError("RCCL start-up timed out on rank " + std::to_string(rank_));
+          }
         }
+        if (state_ == kFailed) std::rethrow_exception(err_);
       }
-      if (state_ == kFailed) std::rethrow_exception(err_);
+      rccl_->ready();  // settles ncclCommInitRankConfig (bounded, abort-aware)
+    } catch (const std::exception& e) {
+      if (seg_->aborted()) throw;  // a peer died: the job ends, no fallback
+      err = e.what();
     }
-    rccl_->ready();  // settles ncclCommInitRankConfig (bounded, abort-aware)
-    promoted_ = true;
+    int64_t failed = err.empty() ? 0 : 1;
+    host_->allreduce_sum_i64(&failed, 1);  // agreement on the control plane
     times_.wait_s = mono_s() - t0;
     times_.start_s = t_start_ - t_created_;
     times_.init_upper_s = mono_s() - t_start_;
+    if (failed == 0) {
+      promoted_ = true;
+      return;
+    }
+    fallback_ = true;
+    fallback_error_ = err.empty() ? std::to_string(failed) + " rank(s) could not bring RCCL up" : err;
   }
+  std::string fallback_error() const override { return fallback_error_; }
   DataPlaneTimes data_plane_times() const override { return times_; }
   void set_abort_segment(std::shared_ptr<ShmSegment> seg) override {
     if (rccl_) rccl_->set_abort_segment(std::move(seg));
@@ -358,6 +377,8 @@ class DeferredRcclComm final : public Comm {
   State state_ = kIdle;
   std::exception_ptr err_;
   bool promoted_ = false;  // only the rank's main thread reads/writes it
+  bool fallback_ = false;  // RCCL failed on some rank: the control plane carries everything
+  std::string fallback_error_;
   DataPlaneTimes times_;
 };
 

@@ -1292,6 +1292,7 @@ PYBIND11_MODULE(_nm03, m) {
         d["init_upper_s"] = t.init_upper_s;
         return d;
       })
+      .def_property_readonly("fallback_error", &Comm::fallback_error)
       .def_property_readonly("transport_size", &Comm::transport_size)
       .def_property_readonly("transport_rank", &Comm::transport_rank)
       .def_property_readonly("transport_device", &Comm::transport_device)

@@ -149,8 +149,9 @@ def test_native_comm_refuses_multi_node_world(monkeypatch):
 
 def test_deferred_rccl_comm_control_plane_without_gpu(native):
     """Before promote() the deferred RCCL communicator is the shared-memory host comm (no HIP): the
-    start-up collectives work on a machine without a GPU, and promote() reports RCCL's failure as a
-    CommError instead of hanging."""
+    start-up collectives work on a machine without a GPU; promote() finds RCCL unusable, the ranks
+    agree on it over the control plane and stay there (backend "host", the reason recorded) instead
+    of failing or hanging."""
     import torch
     if torch.cuda.is_available():
         pytest.skip("CPU-only check")
@@ -160,6 +161,7 @@ def test_deferred_rccl_comm_control_plane_without_gpu(native):
     assert c.broadcast_bytes(b"work-list", 0) == b"work-list"
     assert c.allreduce_max([2.5]) == [2.5]
     assert c.transport_size == -1 and c.data_plane_times["start_s"] == -1
-    with pytest.raises(RuntimeError):
-        c.promote()
+    c.promote()
+    assert c.backend == "host" and c.fallback_error and c.transport_size == -1
+    assert c.allreduce_sum([7]) == [7] and c.broadcast_bytes(b"after", 0) == b"after"
     seg.wait_attached_and_unlink(5.0)
