@@ -130,6 +130,10 @@ def parse_args(argv=None):
                     help="submit the K timed cohort passes as one work stream (the engine pipelines across pass "
                          "boundaries as it does across patients) instead of one engine call per pass; every pass "
                          "writes its own output tree")
+    ap.add_argument("--emulate-shard-of", type=int, default=1,
+                    help="one rank only: measure rank 0's strong-scaling shard of an N-rank job (465 / N slices "
+                         "per pass) — the per-GPU rate of config 3 at N GPUs without N GPUs (host DRAM and CPU "
+                         "contention between ranks not included); the JSON says so")
     ap.add_argument("--host-only", action="store_true",
                     help="host path only (EngineConfig.host_only): every DICOM load and JPEG write of a real "
                          "run, the GPU stages replaced by fixed JPEG segments; measures slices per host "
@@ -318,6 +322,8 @@ def run_rank(args):
         plan = CohortPlan.from_bytes(comm.broadcast_bytes(plan_bytes, 0))
         items = plan.items
         lo, hi = shard_bounds(len(items), rank, world)
+        if world == 1 and args.emulate_shard_of > 1 and scaling == "strong":
+            hi = len(items) // args.emulate_shard_of  # rank 0's share of an N-rank job
         return localize_items(items[lo:hi], roots[0], local_root), len(items)
 
     def measure(scaling, out_root, steps, warmup, wipe=False):
@@ -580,6 +586,11 @@ def run_rank(args):
             rec["config"].setdefault("strong", {}).update(sp)
         if cli is not None:
             rec["config"]["cli_wall"] = cli
+        if args.emulate_shard_of > 1 and world == 1:
+            rec["metric"] = (f"EMULATION, not the headline: one GPU processing rank 0's strong-scaling shard of "
+                             f"a {args.emulate_shard_of}-rank job per step")
+            rec["vs_baseline"] = None
+            rec["config"]["emulate_shard_of"] = args.emulate_shard_of
         if args.host_only:
             rec["metric"] = "host path only: DICOM loads + JPEG writes per s (GPU stages replaced by fixed segments)"
             rec["vs_baseline"] = None
