@@ -7,13 +7,46 @@
 // out-*/PGBM-XXXX/<stem>_{original,processed}.jpg and no-argument defaults.
 #pragma once
 
+#include <condition_variable>
+#include <memory>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "nm03/comm.h"
 #include "nm03/engine.h"
 
 namespace nm03::app {
+
+// A CLI's cold start: one start-up thread, begun at construction, owns every HIP call until the engine
+// exists — hipInit, every kernel code object, `nstreams` reserved streams plus the copy engine's first
+// use, `comm->start_data_plane()` (RCCL ranks) — and then builds the engine from the configuration
+// the caller hands to build() once it is known (the caller plans meanwhile). Destruction without
+// build() cancels and joins.
+class EngineStartup {
+ public:
+  struct Times {
+    double hip_init_s = 0, kernel_load_s = 0, streams_s = 0, engine_ctor_s = 0;
+  };
+  EngineStartup(int device, int nstreams, Comm* comm = nullptr);
+  ~EngineStartup();
+  EngineStartup(const EngineStartup&) = delete;
+  EngineStartup& operator=(const EngineStartup&) = delete;
+  // Hands over the configuration and waits for the engine; nullptr with *error set on failure.
+  std::unique_ptr<Engine> build(const EngineConfig& ec, std::string* error);
+  const Times& times() const { return times_; }  // valid after build()
+
+ private:
+  std::mutex m_;
+  std::condition_variable cv_;
+  bool have_cfg_ = false, cancel_ = false, done_ = false;
+  EngineConfig ec_;
+  std::unique_ptr<Engine> engine_;
+  std::string error_;
+  Times times_;
+  std::thread warm_;
+};
 
 struct AppConfig {
   std::string data_root;  // default: cohort::default_data_root()
@@ -42,6 +75,8 @@ struct AppConfig {
   // CLOCK_REALTIME when parse_args began (the --json record's "main_unix_s"): with the launcher's
   // own clock it splits a cold run's wall into process start-up (exec → main) and the rest.
   double main_unix_s = 0;
+  // GPU_MAX_HW_QUEUES for the process (--hw-queues; 0 = leave the environment's value).
+  int hw_queues = 2;
 };
 
 // Parse the shared flag set; `which` selects CLI-specific defaults. Exits on --help.

@@ -102,6 +102,9 @@ class Comm {
     double init_upper_s = 0;  // start → transport usable, upper bound (observed at promote)
   };
   virtual DataPlaneTimes data_plane_times() const { return {}; }
+  // Non-empty when promote() found the device transport unusable on some rank and every rank stayed
+  // on the control plane (the reason); "" otherwise.
+  virtual std::string fallback_error() const { return ""; }
 
   // Helpers built on the primitives.
   void broadcast_bytes(std::vector<uint8_t>& buf, int root);                        // resizes on non-roots

@@ -65,6 +65,7 @@ void usage(const std::string& which) {
             << "  --json FILE            write run metrics as JSON\n"
             << "  --resume               keep existing outputs; skip slices whose two JPEGs exist\n"
             << "  --frame K              import frame K of multi-frame DICOM files (default: reject them)\n"
+            << "  --hw-queues N          HIP hardware queues of this process (GPU_MAX_HW_QUEUES; default 2, 0 = environment)\n"
             << "  --quiet                suppress per-slice progress lines\n"
             << "env: NM03_DATA_ROOT, NM03_LOG=info|warn|error|none, NM03_ROCTX=1,\n"
             << "     NM03_FAULT=corrupt_dicom:<i>,fail_batch:<k>,fail_write:<j>,rank_exit:<r>\n"
@@ -182,6 +183,7 @@ AppConfig parse_args(int argc, char** argv, const std::string& which) {
     }
     else if (a == "--resume") c.engine.resume = true;
     else if (a == "--frame") c.engine.pipe.frame = std::atoi(val().c_str());
+    else if (a == "--hw-queues") c.hw_queues = std::max(0, std::atoi(val().c_str()));
     else if (a == "--render-filter") {
       const std::string v = val();
       if (v != "bilinear" && v != "nearest") {
@@ -204,6 +206,12 @@ AppConfig parse_args(int argc, char** argv, const std::string& which) {
       std::exit(2);
     }
   }
+  // HW queues of the process, set before anything initialises HIP (rank processes inherit it).
+  // Every stream past the first costs a new HW queue (≈ 9 ms cold) until GPU_MAX_HW_QUEUES is
+  // reached, then ≈ 3–4 ms on a shared one: 2 queues cut the start-up thread's stream reservation from
+  // 56 to 45 ms (interleaved cold runs, profiles/r5/cold/cli_wall.jsonl) with the same warm throughput
+  // (--repeat 30: 121k vs 117k slices/s, profiles/r5/queues/).
+  if (c.hw_queues > 0) setenv("GPU_MAX_HW_QUEUES", std::to_string(c.hw_queues).c_str(), 1);
   return c;
 }
 
@@ -212,10 +220,14 @@ AppConfig parse_args(int argc, char** argv, const std::string& which) {
 // =============================================================================================
 int run_sequential(const AppConfig& cfg) {
   try {
+    // HIP start-up and the engine's construction on the start-up thread while the output root is set up.
+    EngineStartup su(cfg.engine.device, std::max(1, cfg.engine.streams) + 1);
     // SequentialImageProcessor ctor: base output dir (main_sequential.cpp:81-91).
     cohort::make_dirs(cfg.out_dir);
     const std::string base = cohort::cohort_dir(cfg.data_root);
-    auto engine_p = std::make_unique<Engine>(cfg.engine);
+    std::string setup_error;
+    auto engine_p = su.build(cfg.engine, &setup_error);
+    if (!engine_p) throw std::runtime_error(setup_error);
     Engine& engine = *engine_p;
     // The process ends in cli_exit: the engine's buffers are left to the kernel, not unpinned.
     struct Leak {
@@ -435,6 +447,90 @@ int scan_max_dim(const std::vector<PatientPlan>& plan, int threads) {
   return md.load();
 }
 
+}  // namespace
+
+// Cold start (round 5). ONE start-up thread owns every HIP call until the engine exists: it brings up
+// the runtime and the device context, loads every kernel code object, reserves the engine's streams
+// (HW queues) and brings up the copy engine, starts RCCL's non-blocking initialisation (N > 1), and —
+// as soon as the caller hands it the engine configuration (build()) — builds the whole engine: every
+// slot's events, pinned and device buffers. Meanwhile the calling thread plans (cohort discovery,
+// output wipe, header scan), exchanges the plan over the shared-memory control plane and computes the
+// rank's CPU partition. In round 4, slots built on their workers held the runtime's locks (HW-queue
+// creation 10–50 ms) while the first batch tried to copy and launch, and a cold 465-slice pass took
+// 37–70 ms instead of ≈ 4.5 ms (profiles/r5/cold/).
+EngineStartup::EngineStartup(int device, int nstreams, Comm* comm) {
+  warm_ = std::thread([this, device, nstreams, comm] {
+    const double t0 = now_s();
+    std::string err;
+    try {
+      gpu::check_hip(hipSetDevice(device), "hipSetDevice");
+      void* p = nullptr;
+      gpu::check_hip(hipMalloc(&p, 4096), "hipMalloc");
+      (void)hipFree(p);
+      times_.hip_init_s = now_s() - t0;
+      // The kernels' code objects (HIP would load each translation unit's at its first launch):
+      // loaded here, on one thread, before any launch (kernels.h preload_kernels).
+      const double t1 = now_s();
+      gpu::preload_kernels();
+      times_.kernel_load_s = now_s() - t1;
+      // The engine's streams (HW queues) need only the slot count: created before the configuration
+      // arrives, while rank 0 may still be planning.
+      times_.streams_s = reserve_streams(device, nstreams);
+    } catch (const std::exception& e) {
+      err = e.what();
+    }
+    // RCCL's initialisation proceeds in its own thread from here on (non-blocking communicator); the
+    // collectives use the shared-memory control plane until promote().
+    if (err.empty() && comm) comm->start_data_plane();
+    std::unique_lock<std::mutex> g(m_);
+    cv_.wait(g, [&] { return have_cfg_ || cancel_; });
+    if (!cancel_ && err.empty()) {
+      const EngineConfig ec = ec_;
+      g.unlock();
+      const double t2 = now_s();
+      std::unique_ptr<Engine> e;
+      try {
+        e = std::make_unique<Engine>(ec);
+      } catch (const std::exception& ex) {
+        err = ex.what();
+      }
+      g.lock();
+      times_.engine_ctor_s = now_s() - t2;
+      engine_ = std::move(e);
+    }
+    error_ = err;
+    done_ = true;
+    cv_.notify_all();
+  });
+}
+
+EngineStartup::~EngineStartup() {
+  {
+    std::lock_guard<std::mutex> g(m_);
+    cancel_ = true;
+  }
+  cv_.notify_all();
+  if (warm_.joinable()) warm_.join();
+}
+
+std::unique_ptr<Engine> EngineStartup::build(const EngineConfig& ec, std::string* error) {
+  std::unique_ptr<Engine> e;
+  {
+    std::unique_lock<std::mutex> g(m_);
+    ec_ = ec;
+    have_cfg_ = true;
+    cv_.notify_all();
+    cv_.wait(g, [&] { return done_; });
+    e = std::move(engine_);
+    if (error) *error = error_;
+  }
+  warm_.join();
+  if (!e && error && error->empty()) *error = "engine not built";
+  return e;
+}
+
+namespace {
+
 // `rank_devices`: the HIP device of every rank (one node), for the CPU partition of this rank.
 int parallel_rank(const AppConfig& cfg, int rank, int size, Comm& comm, int device, const std::vector<int>& rank_devices) {
   const std::string base = cohort::cohort_dir(cfg.data_root);
@@ -450,71 +546,7 @@ int parallel_rank(const AppConfig& cfg, int rank, int size, Comm& comm, int devi
   // Nothing else touches HIP before the first batch: in round 4, slots built on their workers held
   // the runtime's locks (HW-queue creation 10–50 ms) while the first batch tried to copy and
   // launch, and a cold 465-slice pass took 37–70 ms instead of ≈ 4 ms (profiles/r5/cold/).
-  struct Startup {
-    std::mutex m;
-    std::condition_variable cv;
-    bool have_cfg = false, cancel = false, done = false;
-    EngineConfig ec;
-    std::unique_ptr<Engine> engine;
-    std::string error;
-    double hip_init_s = 0, kernel_load_s = 0, streams_s = 0, engine_ctor_s = 0;
-  } su;
-  const int nstreams = std::max(1, cfg.engine.streams) + 1;  // slots + the shared upload stream
-  std::thread warm([&su, &comm, device, nstreams] {
-    const double t0 = now_s();
-    std::string err;
-    try {
-      gpu::check_hip(hipSetDevice(device), "hipSetDevice");
-      void* p = nullptr;
-      gpu::check_hip(hipMalloc(&p, 4096), "hipMalloc");
-      (void)hipFree(p);
-      su.hip_init_s = now_s() - t0;
-      // The kernels' code objects (HIP would load each translation unit's at its first launch):
-      // loaded here, on one thread, before any launch (kernels.h preload_kernels).
-      const double t1 = now_s();
-      gpu::preload_kernels();
-      su.kernel_load_s = now_s() - t1;
-      // The engine's streams (HW queues), which need only the slot count: created before the
-      // configuration arrives, while rank 0 may still be planning.
-      su.streams_s = reserve_streams(device, nstreams);
-    } catch (const std::exception& e) {
-      err = e.what();
-    }
-    // RCCL's initialisation proceeds in its own thread from here on (non-blocking communicator);
-    // the collectives use the shared-memory control plane until promote().
-    if (err.empty()) comm.start_data_plane();
-    std::unique_lock<std::mutex> g(su.m);
-    su.cv.wait(g, [&] { return su.have_cfg || su.cancel; });
-    if (!su.cancel && err.empty()) {
-      EngineConfig ec = su.ec;
-      g.unlock();
-      const double t2 = now_s();
-      std::unique_ptr<Engine> e;
-      try {
-        e = std::make_unique<Engine>(ec);
-      } catch (const std::exception& ex) {
-        err = ex.what();
-      }
-      g.lock();
-      su.engine_ctor_s = now_s() - t2;
-      su.engine = std::move(e);
-    }
-    su.error = err;
-    su.done = true;
-    su.cv.notify_all();
-  });
-  struct Joiner {
-    Startup& su;
-    std::thread& t;
-    ~Joiner() {
-      {
-        std::lock_guard<std::mutex> g(su.m);
-        su.cancel = true;
-      }
-      su.cv.notify_all();
-      if (t.joinable()) t.join();
-    }
-  } joiner{su, warm};
+  EngineStartup su(device, std::max(1, cfg.engine.streams) + 1, &comm);  // slots + the shared upload stream
   double engine_wait_s = 0;
   std::unique_ptr<Engine> engine_p;
   std::vector<RankDevice> devices;
@@ -620,16 +652,7 @@ int parallel_rank(const AppConfig& cfg, int rank, int size, Comm& comm, int devi
       // agree on it before going on.
       std::string setup_error;
       const double t_wait = now_s();
-      {
-        std::unique_lock<std::mutex> g(su.m);
-        su.ec = ec;
-        su.have_cfg = true;
-        su.cv.notify_all();
-        su.cv.wait(g, [&] { return su.done; });
-        engine_p = std::move(su.engine);
-        setup_error = su.error;
-      }
-      warm.join();
+      engine_p = su.build(ec, &setup_error);
       engine_wait_s = now_s() - t_wait;
       if (!engine_p && setup_error.empty()) setup_error = "engine not built";
       int64_t setup_failed = setup_error.empty() ? 0 : 1;
@@ -773,9 +796,9 @@ int parallel_rank(const AppConfig& cfg, int rank, int size, Comm& comm, int devi
                              ", \"gpus_requested\": " + req + ", \"main_unix_s\": " +
                              fmt(cfg.main_unix_s, 17) + ", \"backend\": \"" +
                              comm.backend() + "\", \"repeat\": " + std::to_string(cfg.repeat) + ", \"engine_setup_s\": " +
-                             fmt(setup_s) + ", \"hip_init_s\": " + fmt(su.hip_init_s) + ", \"engine_ctor_s\": " +
-                             fmt(su.engine_ctor_s) + ", \"streams_s\": " + fmt(su.streams_s) + ", \"engine_wait_s\": " + fmt(engine_wait_s) + ", \"kernel_load_s\": " +
-                             fmt(su.kernel_load_s) + ", \"comm_start_s\": " + fmt(dp.start_s) + ", \"comm_wait_s\": " +
+                             fmt(setup_s) + ", \"hip_init_s\": " + fmt(su.times().hip_init_s) + ", \"engine_ctor_s\": " +
+                             fmt(su.times().engine_ctor_s) + ", \"streams_s\": " + fmt(su.times().streams_s) + ", \"engine_wait_s\": " + fmt(engine_wait_s) + ", \"kernel_load_s\": " +
+                             fmt(su.times().kernel_load_s) + ", \"comm_start_s\": " + fmt(dp.start_s) + ", \"comm_wait_s\": " +
                              fmt(dp.wait_s) + ", \"comm_init_s\": " + fmt(dp.init_upper_s) + ", \"wall_s\": " + fmt(tot) +
                              ", \"processing_wall_s\": " + fmt(proc_wall) + ", \"slices\": " + std::to_string(total_slices) +
                              ", \"slices_ok\": " + std::to_string(total_ok) + ", \"slices_per_s\": " +
@@ -882,6 +905,9 @@ int run_parallel(const AppConfig& cfg) {
 // =============================================================================================
 int run_test_pipeline(const AppConfig& cfg) {
   try {
+    // GPU path: HIP start-up and the engine's streams on the start-up thread while the slice loads.
+    std::unique_ptr<EngineStartup> su;
+    if (!cfg.cpu) su = std::make_unique<EngineStartup>(cfg.engine.device, 2);
     const std::string path = cfg.input.empty() ? cohort::test_slice_path(cfg.data_root) : cfg.input;
     golden::SliceInput in = golden::load_slice(path, 0, cfg.engine.pipe.frame);  // the test pipeline has no <100 guard
     const PipelineParams& p = cfg.engine.pipe;
@@ -903,8 +929,10 @@ int run_test_pipeline(const AppConfig& cfg) {
       ec.batch_size = 1;
       ec.streams = 1;
       ec.max_dim = std::max({ec.max_dim, in.w, in.h});
-      Engine engine(ec);
-      SingleResult r = engine.run_single(in);
+      std::string setup_error;
+      std::unique_ptr<Engine> engine = su->build(ec, &setup_error);
+      if (!engine) throw std::runtime_error(setup_error);
+      SingleResult r = engine->run_single(in);
       canvases = std::move(r.canvases);
       jpegs = std::move(r.jpegs);
       d_sharp = std::move(r.sharpened);

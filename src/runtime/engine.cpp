@@ -219,6 +219,18 @@ void hip_free_all(Slot& s) {
 // Streams created ahead of the engine (reserve_streams), per device.
 std::mutex g_reserve_m;
 std::vector<std::pair<int, hipStream_t>> g_reserved;
+std::vector<int> g_copy_warm;  // devices whose copy path was brought up (warm_copy_path), guarded by g_reserve_m
+
+// The first host→device copy of a process on `device` brings up the runtime's copy path: once per
+// device, on the caller's stream, before any batch (reserve_streams or the engine constructor).
+void warm_copy_once(int device, hipStream_t stream) {
+  {
+    std::lock_guard<std::mutex> g(g_reserve_m);
+    if (std::find(g_copy_warm.begin(), g_copy_warm.end(), device) != g_copy_warm.end()) return;
+    g_copy_warm.push_back(device);
+  }
+  warm_copy_path(stream);
+}
 
 hipStream_t take_stream(int device, const char* what) {
   {
@@ -349,6 +361,7 @@ struct Engine::Impl {
         slot_ms += ", +" + std::to_string((int)((now_s() - tb) * 1e4) / 10.0).substr(0, 5);
       }
     });
+    if (!host_only_ && slots[0]) warm_copy_once(cfg.device, slots[0]->stream);  // no-op after reserve_streams
     const double t3 = now_s();
     building_ = cfg.lazy_slots ? (int)slots.size() - 1 : 0;
     start_workers();
@@ -1609,9 +1622,11 @@ double reserve_streams(int device, int n) {
   for (int i = 0; i < n; ++i) {
     hipStream_t s = nullptr;
     check_hip(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "hipStreamCreate (reserve)");
-    // The process's first host→device copy brings up the runtime's copy path (≈ 10 ms cold): here,
-    // not in the first batch's upload, where it held the slot threads (profiles/r5/cold/).
-    if (i == 0) warm_copy_path(s);
+    // The process's first host→device copy brings up the runtime's copy path (≈ 7.5 ms cold): here,
+    // not in the first batch's upload, where it held the slot threads (profiles/r5/cold/). (On a
+    // second thread, overlapping the other streams' creation, it saved 2 ms of 45: not kept,
+    // profiles/r5/cold/variants_cli_wall.jsonl.)
+    if (i == 0) warm_copy_once(device, s);
     std::lock_guard<std::mutex> g(g_reserve_m);
     g_reserved.push_back({device, s});
   }

@@ -17,17 +17,29 @@ import json, os, sys
 sys.path.insert(0, os.environ["GRAFT_REPO_ROOT"])
 from nm03_capstone_project_amd.utils.cli_wall import time_cli
 d, o = sys.argv[1:3]
-queues = os.environ.get("QUEUES", "4 2 1").split()
+# VARIANTS: ";"-separated, each "-" or "NAME=VAL,NAME=VAL" (environment) with an optional
+# "ARGS=..." (CLI flags); QUEUES (legacy): one variant per --hw-queues value.
+if os.environ.get("VARIANTS"):
+    queues = os.environ["VARIANTS"].split(";")
+else:
+    queues = [f"ARGS=--hw-queues {q}" for q in os.environ.get("QUEUES", "4 2 1").split()]
 rows = {q: [] for q in queues}
 for r in range(int(os.environ.get("RUNS", "7"))):
-    for q in queues:
-        js = f"/tmp/cold_q{q}.json"
+    for k, q in enumerate(queues):
+        js = f"/tmp/cold_v{k}.json"
+        env, extra = dict(os.environ), []
+        for kv in ([] if q == "-" else q.split(",")):
+            name, val = kv.split("=", 1)
+            if name == "ARGS":
+                extra += val.split()
+            else:
+                env[name] = val
         argv = [os.path.join(os.environ["GRAFT_REPO_ROOT"], "build/bin/img_processing_parallel"), "--data-root",
-                d + "/", "--out", "/dev/shm/cold_out", "--quiet", "--json", js]
-        res = time_cli(argv, runs=1, json_path=js, env=dict(os.environ, GPU_MAX_HW_QUEUES=q))
+                d + "/", "--out", "/dev/shm/cold_out", "--quiet", "--json", js] + extra
+        res = time_cli(argv, runs=1, json_path=js, env=env)
         rows[q].append(res)
         with open(os.path.join(o, "cli_runs.jsonl"), "a") as f:
-            f.write(json.dumps({"GPU_MAX_HW_QUEUES": q, "run": r, **res}) + "\n")
+            f.write(json.dumps({"variant": q, "run": r, **res}) + "\n")
 for q in queues:
     walls = sorted(x["wall_median_s"] for x in rows[q])
     ph = {}
@@ -35,7 +47,7 @@ for q in queues:
         for k, v in (x.get("phases_median_s") or {}).items():
             ph.setdefault(k, []).append(v)
     med = {k: round(sorted(v)[len(v) // 2], 4) for k, v in ph.items()}
-    line = {"GPU_MAX_HW_QUEUES": q, "wall_median_s": walls[len(walls) // 2], "walls_s": [x["wall_median_s"] for x in rows[q]],
+    line = {"variant": q, "wall_median_s": walls[len(walls) // 2], "walls_s": [x["wall_median_s"] for x in rows[q]],
             "phases_median_s": med}
     with open(os.path.join(o, "cli_wall.jsonl"), "a") as f:
         f.write(json.dumps(line) + "\n")
