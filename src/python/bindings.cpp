@@ -1173,9 +1173,12 @@ PYBIND11_MODULE(_nm03, m) {
       // (n > 2) returns 7 after the collectives; "die": the last rank exits 3 while the others
       // block in a barrier (abort flag); "hang": the last rank sleeps while the others wait in
       // a barrier (deadline, then SIGTERM from the supervisor). Returns the job's exit status.
-      [](int n, const std::string& mode, double timeout_s, double grace_s) {
+      // comm "rccl": the ranks get launch_ranks' deferred RCCL communicator; after the collectives each
+      // starts RCCL and promotes — without a GPU every rank fails to bring RCCL up, they agree on it
+      // and the last collectives run on the control plane.
+      [](int n, const std::string& mode, double timeout_s, double grace_s, const std::string& comm) {
         LaunchOptions o;
-        o.comm = "host";
+        o.comm = comm;
         o.timeout_s = timeout_s;
         o.grace_s = grace_s;
         py::gil_scoped_release nogil;
@@ -1212,12 +1215,18 @@ PYBIND11_MODULE(_nm03, m) {
                 std::this_thread::sleep_for(std::chrono::seconds(600));
                 return 0;
               }
+              c.start_data_plane();
+              c.promote();  // ranks on different planes afterwards would hang the next collective
+              int64_t one = 1;
+              c.allreduce_sum_i64(&one, 1);
+              if (one != size) return 18;
               c.barrier();
               return 0;
             },
             o);
       },
-      py::arg("n"), py::arg("mode") = "exit", py::arg("timeout_s") = -1.0, py::arg("grace_s") = 5.0);
+      py::arg("n"), py::arg("mode") = "exit", py::arg("timeout_s") = -1.0, py::arg("grace_s") = 5.0,
+      py::arg("comm") = "host");
 
   // ---- native communicators (bench.py and other Python drivers) ------------------------------------
   // Host/RCCL comms for ranks started by torchrun or bench.py's own launcher; the rendezvous

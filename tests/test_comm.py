@@ -165,3 +165,14 @@ def test_deferred_rccl_comm_control_plane_without_gpu(native):
     assert c.backend == "host" and c.fallback_error and c.transport_size == -1
     assert c.allreduce_sum([7]) == [7] and c.broadcast_bytes(b"after", 0) == b"after"
     seg.wait_attached_and_unlink(5.0)
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_launcher_deferred_rccl_falls_back_together(native, n):
+    """launch_ranks' RCCL ranks without a GPU: the start-up collectives run on the shared-memory
+    control plane, every rank's RCCL bring-up fails, the ranks agree on it in promote() and finish on
+    the control plane — the job succeeds instead of hanging or failing one rank."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("CPU-only check")
+    assert native.launcher_selftest(n, "ok", 30.0, 5.0, "rccl") == 0
