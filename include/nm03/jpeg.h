@@ -1,9 +1,10 @@
 // nm03/jpeg.h — host side of the JPEG exporter (replaces FAST ImageFileExporter → Qt → libjpeg,
-// main_sequential.cpp:61-73). Produces baseline JFIF, 3 components (Y=gray, Cb=Cr=128), 4:2:0,
-// quality-scaled Annex K tables, standard Huffman tables, byte-compatible with libjpeg(-turbo).
+// main_sequential.cpp:61-73). Produces baseline JFIF, 3 components (Y=gray, Cb=Cr=128), 4:2:0 by
+// default (4:4:4 and a one-component gray file on request: jpeg::Sampling), quality-scaled Annex K
+// tables, standard Huffman tables, byte-compatible with libjpeg(-turbo).
 //
 // The GPU encoder (k4_jpeg.hip) produces the entropy-coded segment; the host prepends
-// `make_header` and appends EOI. `encode_gray420` is the single-threaded golden encoder.
+// `make_header` and appends EOI. `encode_gray` is the single-threaded golden encoder.
 #pragma once
 
 #include <atomic>
@@ -25,16 +26,19 @@ struct Tables {
 
 Tables make_tables(int quality);
 
-// SOI, APP0(JFIF 1.01), DQT×2, SOF0, DHT×4, SOS for a w×h image with 2x2/1x1/1x1 sampling.
-std::vector<uint8_t> make_header(int width, int height, const Tables& t);
+// SOI, APP0(JFIF 1.01), DQT, SOF0, DHT, SOS for a w×h image: YCbCr with 2x2/1x1/1x1 (4:2:0) or
+// 1x1/1x1/1x1 (4:4:4) sampling — DQT×2, DHT×4 — or one gray component — DQT×1, DHT×2.
+std::vector<uint8_t> make_header(int width, int height, const Tables& t, Sampling s = kSampling420);
 
-// Golden single-thread encode of an 8-bit gray plane as YCbCr 4:2:0 (complete file bytes).
-std::vector<uint8_t> encode_gray420(const uint8_t* gray, int width, int height, int stride, int quality);
+// Golden single-thread encode of an 8-bit gray plane (complete file bytes): YCbCr 4:2:0 by
+// default (Y = gray, Cb = Cr = 128), or 4:4:4, or a one-component gray file.
+std::vector<uint8_t> encode_gray(const uint8_t* gray, int width, int height, int stride, int quality,
+                                 Sampling s = kSampling420);
 
 // Entropy-coded segment only (stuffed, padded with 1-bits), no markers. Used for tests against
-// the GPU encoder.
-std::vector<uint8_t> encode_scan_gray420(const uint8_t* gray, int width, int height, int stride,
-                                         const Tables& t);
+// the GPU encoder and as the engine's fallback for an image the GPU encoder gives up on.
+std::vector<uint8_t> encode_scan_gray(const uint8_t* gray, int width, int height, int stride, const Tables& t,
+                                      Sampling s = kSampling420);
 
 // Write header + scan + EOI to a file (single writev-style write).
 void write_jpeg_file(const std::string& path, const std::vector<uint8_t>& header, const uint8_t* scan,

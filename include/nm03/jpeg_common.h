@@ -15,6 +15,12 @@
 
 namespace nm03::jpeg {
 
+// Component layout of the exported file. The reference's Qt writer is not pinned on this point
+// (SURVEY §7.6 risk 1): an RGB(A) QImage goes out as YCbCr 4:2:0 (libjpeg's default, the
+// default here), a Grayscale8 one as a single-component file. 4:4:4 is libjpeg with
+// 1×1 chroma sampling. Gray canvases make the chroma blocks all-zero in both YCbCr forms.
+enum Sampling : int { kSampling420 = 0, kSampling444 = 1, kSamplingGray = 2 };
+
 // Zig-zag index → natural (row-major) index.
 inline constexpr uint8_t kNatural[64] = {
     0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,  12, 19, 26, 33, 40, 48,

@@ -62,6 +62,9 @@ struct RenderParams {
   // FAST's ImageRenderer filtering is not pinned by the reference (main_sequential.cpp:259), so it is
   // a flag (--render-filter). kFilterBilinear (default) or kFilterNearest.
   int filter = 0;
+  // Component layout of the JPEG files (jpeg::Sampling, --jpeg-sampling): YCbCr 4:2:0 (default),
+  // 4:4:4, or a one-component gray file — which one Qt writes for FAST's image is not pinned.
+  int jpeg_sampling = 0;
 };
 
 enum RenderFilter : int { kFilterBilinear = 0, kFilterNearest = 1 };

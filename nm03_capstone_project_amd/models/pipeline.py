@@ -44,6 +44,7 @@ class PipelineConfig:
     border_radius: int = 2
     jpeg_quality: int = 75
     render_filter: int = 0  # gray renders: 0 bilinear (default), 1 nearest (params.h RenderFilter)
+    jpeg_sampling: int = 0  # JPEG files: 0 YCbCr 4:2:0 (default), 1 YCbCr 4:4:4, 2 one gray component
     # engine
     batch_size: int = 25
     streams: int = 3
@@ -57,7 +58,8 @@ class PipelineConfig:
     _PIPE = ("norm_low", "norm_high", "norm_min", "norm_max", "clip_min", "clip_max", "median_window",
              "sharpen_gain", "sharpen_sigma", "sharpen_mask", "srg_min", "srg_max", "srg_connectivity",
              "dilation_size", "erosion_size", "min_dim", "apply_rescale", "frame", "se_shape")
-    _RENDER = ("out_width", "out_height", "label_opacity", "border_opacity", "border_radius", "jpeg_quality")
+    _RENDER = ("out_width", "out_height", "label_opacity", "border_opacity", "border_radius", "jpeg_quality",
+               "jpeg_sampling")
 
     def pipeline_params(self):
         p = native().PipelineParams()

@@ -131,14 +131,19 @@ def dilate3d(mask, size=7, ball=False):
     return unpack_bits(dst, w)
 
 
-def jpeg_encode(canvas, quality=75, header=True):
+JPEG_SAMPLING = {"420": 0, "444": 1, "gray": 2}
+
+
+def jpeg_encode(canvas, quality=75, header=True, sampling="420"):
     """GPU JPEG of uint8 gray canvases [N,H,W] (H, W multiples of 16) → list of bytes (complete
-    JFIF files when header=True, else the entropy-coded segments)."""
+    JFIF files when header=True, else the entropy-coded segments). `sampling`: "420" (YCbCr
+    4:2:0, the default), "444" (YCbCr 4:4:4) or "gray" (one component)."""
     c = _as3d(canvas)
     _check(c, (torch.uint8,), "canvas")
     n, h, w = c.shape
-    segs = native().k_jpeg(c.data_ptr(), n, h, w, int(quality), _stream())
+    samp = JPEG_SAMPLING[sampling] if isinstance(sampling, str) else int(sampling)
+    segs = native().k_jpeg(c.data_ptr(), n, h, w, int(quality), _stream(), samp)
     if not header:
         return segs
-    hdr = native().jpeg_header(w, h, int(quality))
+    hdr = native().jpeg_header(w, h, int(quality), samp)
     return [None if s is None else hdr + s + b"\xff\xd9" for s in segs]

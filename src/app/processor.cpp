@@ -55,6 +55,7 @@ void usage(const std::string& which) {
             << "  --se-shape square|disc structuring element of dilation/erosion (3D: cube|ball; default square)\n"
             << "  --render-filter bilinear|nearest  interpolation of the gray renders (default bilinear)\n"
             << "  --quality Q            JPEG quality (default 75)\n"
+            << "  --jpeg-sampling 420|444|gray  JPEG component layout: YCbCr 4:2:0 (default), 4:4:4, one gray component\n"
             << "  --mode 2d|3d           3d: whole series as a volume (SRG 6-conn + cube dilation)\n"
             << "  --split-volume         3d: each volume split into z-slabs over all ranks (halo exchange)\n"
             << "  --input FILE           test_pipeline: slice to process\n"
@@ -184,6 +185,14 @@ AppConfig parse_args(int argc, char** argv, const std::string& which) {
     else if (a == "--resume") c.engine.resume = true;
     else if (a == "--frame") c.engine.pipe.frame = std::atoi(val().c_str());
     else if (a == "--hw-queues") c.hw_queues = std::max(0, std::atoi(val().c_str()));
+    else if (a == "--jpeg-sampling") {
+      const std::string v = val();
+      if (v != "420" && v != "444" && v != "gray") {
+        std::cerr << "--jpeg-sampling must be 420, 444 or gray" << std::endl;
+        std::exit(2);
+      }
+      c.engine.render.jpeg_sampling = v == "gray" ? jpeg::kSamplingGray : v == "444" ? jpeg::kSampling444 : jpeg::kSampling420;
+    }
     else if (a == "--render-filter") {
       const std::string v = val();
       if (v != "bilinear" && v != "nearest") {
@@ -963,7 +972,7 @@ int run_test_pipeline(const AppConfig& cfg) {
       std::vector<uint8_t> m((size_t)mw * ch, 0);
       for (int k = 0; k < 5; ++k)
         for (int y = 0; y < ch; ++y) std::memcpy(&m[(size_t)y * mw + k * cw], &canvases[k][(size_t)y * cw], cw);
-      auto j = jpeg::encode_gray420(m.data(), mw, ch, mw, rp.jpeg_quality);
+      auto j = jpeg::encode_gray(m.data(), mw, ch, mw, rp.jpeg_quality, (jpeg::Sampling)rp.jpeg_sampling);
       std::ofstream f(cfg.out_dir + "/multi_view.jpg", std::ios::binary | std::ios::trunc);
       f.write((const char*)j.data(), (std::streamsize)j.size());
     }

@@ -395,11 +395,11 @@ SliceJpegs export_jpegs(const SliceInput& s, const SliceResult& r, const Pipelin
   RenderGeom g = make_render_geom(s.w, s.h, s.spacing_x, s.spacing_y, rp.out_width, rp.out_height);
   SliceJpegs j;
   std::vector<uint8_t> c0 = render_gray(rescaled(s, p), g, r.window_lo, r.window_hi, rp.filter == kFilterNearest);
-  j.original = jpeg::encode_gray420(c0.data(), g.out_w, g.out_h, g.out_w, rp.jpeg_quality);
+  j.original = jpeg::encode_gray(c0.data(), g.out_w, g.out_h, g.out_w, rp.jpeg_quality, (jpeg::Sampling)rp.jpeg_sampling);
   std::vector<uint8_t> bm = border(r.dilated, s.w, s.h, rp.border_radius);
   std::vector<uint8_t> c1 =
       render_labels(r.dilated, bm, g, opacity_u8(rp.label_opacity), opacity_u8(rp.border_opacity));
-  j.processed = jpeg::encode_gray420(c1.data(), g.out_w, g.out_h, g.out_w, rp.jpeg_quality);
+  j.processed = jpeg::encode_gray(c1.data(), g.out_w, g.out_h, g.out_w, rp.jpeg_quality, (jpeg::Sampling)rp.jpeg_sampling);
   return j;
 }
 
@@ -417,8 +417,8 @@ StageImages test_pipeline_images(const SliceInput& in, const PipelineParams& p, 
   c.push_back(render_labels(r.region, border(r.region, in.w, in.h, rp.border_radius), g, fill, bv));
   c.push_back(render_labels(r.eroded, border(r.eroded, in.w, in.h, rp.border_radius), g, fill, bv));
   c.push_back(render_labels(r.dilated, border(r.dilated, in.w, in.h, rp.border_radius), g, fill, bv));
-  for (auto& cv : c) out.jpegs.push_back(jpeg::encode_gray420(cv.data(), rp.out_width, rp.out_height, rp.out_width,
-                                                               rp.jpeg_quality));
+  for (auto& cv : c) out.jpegs.push_back(jpeg::encode_gray(cv.data(), rp.out_width, rp.out_height, rp.out_width,
+                                                            rp.jpeg_quality, (jpeg::Sampling)rp.jpeg_sampling));
   if (stages) *stages = std::move(r);
   return out;
 }

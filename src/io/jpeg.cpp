@@ -1,5 +1,5 @@
 // Host JPEG pieces: marker writer and the golden CPU encoder. The GPU path in
-// src/kernels/k4_jpeg.hip must produce the same entropy-coded bytes as encode_scan_gray420.
+// src/kernels/k4_jpeg.hip must produce the same entropy-coded bytes as encode_scan_gray.
 #include "nm03/jpeg.h"
 
 #include <fcntl.h>
@@ -105,7 +105,9 @@ void encode_block(BitWriter& w, const int16_t* zz, int& last_dc, const HuffEnc& 
 
 }  // namespace
 
-std::vector<uint8_t> make_header(int width, int height, const Tables& t) {
+std::vector<uint8_t> make_header(int width, int height, const Tables& t, Sampling s) {
+  const bool gray = s == kSamplingGray;
+  const int nc = gray ? 1 : 3;
   std::vector<uint8_t> b;
   b.reserve(700);
   b.push_back(0xFF);
@@ -113,62 +115,91 @@ std::vector<uint8_t> make_header(int width, int height, const Tables& t) {
   // APP0 JFIF 1.01, no units, 1:1 density, no thumbnail (libjpeg defaults).
   const uint8_t app0[] = {0xFF, 0xE0, 0x00, 0x10, 'J', 'F', 'I', 'F', 0x00, 0x01, 0x01, 0x00, 0x00, 0x01, 0x00, 0x01, 0x00, 0x00};
   b.insert(b.end(), app0, app0 + sizeof(app0));
+  // libjpeg writes the tables the frame's components use: DQT before SOF0, DHT (per scan
+  // component: DC then AC, each table once) before SOS.
   put_dqt(b, 0, t.qluma);
-  put_dqt(b, 1, t.qchroma);
+  if (!gray) put_dqt(b, 1, t.qchroma);
   // SOF0
   b.push_back(0xFF);
   b.push_back(0xC0);
-  put16(b, 8 + 3 * 3);
+  put16(b, 8 + 3 * nc);
   b.push_back(8);
   put16(b, height);
   put16(b, width);
-  b.push_back(3);
-  const uint8_t comps[9] = {1, 0x22, 0, 2, 0x11, 1, 3, 0x11, 1};
-  b.insert(b.end(), comps, comps + 9);
+  b.push_back((uint8_t)nc);
+  const uint8_t comps[9] = {1, (uint8_t)(s == kSampling420 ? 0x22 : 0x11), 0, 2, 0x11, 1, 3, 0x11, 1};
+  b.insert(b.end(), comps, comps + 3 * nc);
   put_dht(b, 0x00, kDcLumaBits, kDcLumaVals);
   put_dht(b, 0x10, kAcLumaBits, kAcLumaVals);
-  put_dht(b, 0x01, kDcChromaBits, kDcChromaVals);
-  put_dht(b, 0x11, kAcChromaBits, kAcChromaVals);
+  if (!gray) {
+    put_dht(b, 0x01, kDcChromaBits, kDcChromaVals);
+    put_dht(b, 0x11, kAcChromaBits, kAcChromaVals);
+  }
   // SOS
   b.push_back(0xFF);
   b.push_back(0xDA);
-  put16(b, 6 + 2 * 3);
-  b.push_back(3);
+  put16(b, 6 + 2 * nc);
+  b.push_back((uint8_t)nc);
   const uint8_t sos[6] = {1, 0x00, 2, 0x11, 3, 0x11};
-  b.insert(b.end(), sos, sos + 6);
+  b.insert(b.end(), sos, sos + 2 * nc);
   b.push_back(0);
   b.push_back(63);
   b.push_back(0);
   return b;
 }
 
-std::vector<uint8_t> encode_scan_gray420(const uint8_t* gray, int width, int height, int stride, const Tables& t) {
+namespace {
+
+// Luma block (bx, by) of the gray plane, edge-replicated past the image (libjpeg's
+// expand_right_edge and bottom-row replication), transformed and quantised into zig-zag order.
+void luma_block(const uint8_t* gray, int width, int height, int stride, int bx, int by, const Tables& t, int16_t* zz) {
+  int32_t blk[64];
+  for (int r = 0; r < 8; ++r) {
+    const int y = by * 8 + r < height ? by * 8 + r : height - 1;
+    for (int c = 0; c < 8; ++c) {
+      const int x = bx * 8 + c < width ? bx * 8 + c : width - 1;
+      blk[r * 8 + c] = (int32_t)gray[(size_t)y * stride + x] - 128;
+    }
+  }
+  fdct_islow(blk);
+  for (int k = 0; k < 64; ++k) zz[k] = quantize(blk[kNatural[k]], t.div_luma[kNatural[k]]);
+}
+
+}  // namespace
+
+std::vector<uint8_t> encode_scan_gray(const uint8_t* gray, int width, int height, int stride, const Tables& t,
+                                      Sampling s) {
   std::vector<uint8_t> out;
   out.reserve((size_t)width * height / 8);
   BitWriter w(out);
-  // libjpeg pads each component to whole blocks by edge replication and fills MCU padding with
-  // dummy blocks whose DC repeats the previous block (jccoefct.c compress_data).
   const int bw = (width + 7) / 8, bh = (height + 7) / 8;
-  const int mcux = (width + 15) / 16, mcuy = (height + 15) / 16;
   int last_dc_y = 0, last_dc_cb = 0, last_dc_cr = 0;
-  int32_t blk[64];
   int16_t zz[64];
-  std::vector<int16_t> dc_row((size_t)mcux * 2, 0);
   int16_t zero_zz[64] = {0};
+  if (s != kSampling420) {
+    // One luma block per MCU in raster order (a one-component scan is never interleaved; 4:4:4
+    // interleaves the Y, Cb and Cr blocks of each 8×8 MCU). No padding blocks.
+    for (int by = 0; by < bh; ++by)
+      for (int bx = 0; bx < bw; ++bx) {
+        luma_block(gray, width, height, stride, bx, by, t, zz);
+        encode_block(w, zz, last_dc_y, kHuffDcLuma, kHuffAcLuma);
+        if (s == kSampling444) {
+          encode_block(w, zero_zz, last_dc_cb, kHuffDcChroma, kHuffAcChroma);
+          encode_block(w, zero_zz, last_dc_cr, kHuffDcChroma, kHuffAcChroma);
+        }
+      }
+    w.flush();
+    return out;
+  }
+  // 4:2:0: libjpeg pads each component to whole blocks by edge replication and fills MCU padding
+  // with dummy blocks whose DC repeats the previous block (jccoefct.c compress_data).
+  const int mcux = (width + 15) / 16, mcuy = (height + 15) / 16;
   for (int my = 0; my < mcuy; ++my) {
     for (int mx = 0; mx < mcux; ++mx) {
       for (int sub = 0; sub < 4; ++sub) {
         const int by = my * 2 + (sub >> 1), bx = mx * 2 + (sub & 1);
         if (by < bh && bx < bw) {
-          for (int r = 0; r < 8; ++r) {
-            const int y = by * 8 + r < height ? by * 8 + r : height - 1;
-            for (int c = 0; c < 8; ++c) {
-              const int x = bx * 8 + c < width ? bx * 8 + c : width - 1;
-              blk[r * 8 + c] = (int32_t)gray[(size_t)y * stride + x] - 128;
-            }
-          }
-          fdct_islow(blk);
-          for (int k = 0; k < 64; ++k) zz[k] = quantize(blk[kNatural[k]], t.div_luma[kNatural[k]]);
+          luma_block(gray, width, height, stride, bx, by, t, zz);
         } else {
           // Dummy block: zero AC, DC = previous block's DC in this MCU row of the component.
           std::memset(zz, 0, sizeof(zz));
@@ -185,11 +216,11 @@ std::vector<uint8_t> encode_scan_gray420(const uint8_t* gray, int width, int hei
   return out;
 }
 
-std::vector<uint8_t> encode_gray420(const uint8_t* gray, int width, int height, int stride, int quality) {
+std::vector<uint8_t> encode_gray(const uint8_t* gray, int width, int height, int stride, int quality, Sampling s) {
   Tables t = make_tables(quality);
-  std::vector<uint8_t> f = make_header(width, height, t);
-  std::vector<uint8_t> s = encode_scan_gray420(gray, width, height, stride, t);
-  f.insert(f.end(), s.begin(), s.end());
+  std::vector<uint8_t> f = make_header(width, height, t, s);
+  std::vector<uint8_t> sc = encode_scan_gray(gray, width, height, stride, t, s);
+  f.insert(f.end(), sc.begin(), sc.end());
   f.push_back(0xFF);
   f.push_back(0xD9);
   return f;

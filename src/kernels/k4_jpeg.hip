@@ -163,9 +163,12 @@ __device__ __forceinline__ uint32_t priv_word(const uint32_t* pb, const uint32_t
 //  4. each thread writes its block's codes at its bit offset (atomicOr into the zeroed stage).
 // The last workgroup of an image publishes the total (or the overflow marker).
 // kOcc: target waves per SIMD (= workgroups per CU); kUnion: LDS words of the patch / bit-range
-// union. 5 workgroups per CU (31.7 KiB, ≤ 96 VGPRs with spills) measured no better than 4 once
+// union; kSamp: jpeg::Sampling — 4:2:0 scans MCUs of 2×2 luma blocks followed by the MCU's two
+// all-zero chroma blocks; 4:4:4 scans the luma blocks in raster order, each followed by its two
+// chroma blocks; gray scans them in raster order alone. (One instance per layout: the default
+// 4:2:0 code is unchanged by the other two.) 5 workgroups per CU (31.7 KiB, ≤ 96 VGPRs with spills) measured no better than 4 once
 // images were dealt round-robin (profiles/r3/jpeg_spread/split_and_occ5.txt).
-template <int kOcc, int kUnion>
+template <int kOcc, int kUnion, int kSamp>
 __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(kOcc))) void jpeg_fused_kernel(const uint8_t* __restrict__ canvas,
                                                              const JpegDesc* __restrict__ jd, int ncanvas, int out_w,
                                                              int out_h, QuantRecip q, JpegWork w, JpegRenderSrc rs,
@@ -177,6 +180,10 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(kOcc)))
   // 96-slice batch in the bench, profiles/r4/jpeg_wg512/.)
   constexpr int kWG = kJpegWG;
   constexpr int kPatch = kPatchLds;
+  constexpr bool k420 = kSamp == kSampling420;
+  // Scan units (MCUs) per workgroup and the canvas rows (source rows of the 2× render: half) of one
+  // row of units.
+  constexpr int kUnitBlocks = k420 ? 4 : 1, kUnitRows = k420 ? 16 : 8;
   static_assert(kPatch <= kUnion, "staging area exceeds the LDS union");
   __shared__ uint32_t actab[256];
   __shared__ uint32_t dctab[16];
@@ -255,8 +262,21 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(kOcc)))
     if (part == 0x7FFFFFF1) out_sizes[0] = 1;
     return;
   }
-  const int mcux = out_w >> 4;
+  // Units (MCUs) per row: 16×16 (4:2:0) or 8×8 (4:4:4, gray) canvas pixels each.
+  const int mcux = k420 ? out_w >> 4 : out_w >> 3;
   const Div16 dmx((uint32_t)mcux);
+  // Scan block b → luma block column/row of the canvas.
+  auto block_xy = [&](int bb, int& bx, int& by) {
+    if (k420) {
+      const int mcu = bb >> 2, sub = bb & 3;
+      const int my = (int)dmx.q((uint32_t)mcu), mx = mcu - my * mcux;
+      bx = 2 * mx + (sub & 1);
+      by = 2 * my + (sub >> 1);
+    } else {
+      by = (int)dmx.q((uint32_t)bb);
+      bx = bb - by * mcux;
+    }
+  };
   const int b = part * kWG + tid;
   const bool valid = b < bpi;
   // ---- 0. stage the source rows of this workgroup in LDS (workgroup-uniform decision) ----------
@@ -271,13 +291,13 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(kOcc)))
   int flat_v = 0;
   uint64_t* const slab = reinterpret_cast<uint64_t*>(spatch);  // label images reuse the area
   if (d.render >= 0 && rd.kind == kRenderLabels) {
-    // Label render rows: 4by .. 4by+3 for the workgroup's block rows → 8 per MCU row.
-    const int m0 = part * (kWG / 4), m1 = min(m0 + kWG / 4, bpi >> 2) - 1;
+    // Label render rows: 4by .. 4by+3 for the workgroup's block rows → 8 per MCU row (4:2:0).
+    const int m0 = part * (kWG / kUnitBlocks), m1 = min(m0 + kWG / kUnitBlocks, bpi / kUnitBlocks) - 1;
     const int r0 = m0 / mcux, r1 = m1 / mcux;
-    const int nrows = 8 * (r1 - r0) + 8, wpr = rd.wpr, nw = nrows * wpr;
+    const int nrows = (kUnitRows / 2) * (r1 - r0 + 1), wpr = rd.wpr, nw = nrows * wpr;
     if (2 * nw * 2 <= kPatch) {  // two u64 planes in the f32 area
       lstaged = true;
-      ys0 = 8 * r0;
+      ys0 = (kUnitRows / 2) * r0;
       pcols = nw;  // offset of the border plane
       const int wrem = rd.src_w & 63;
       const Div16 dw((uint32_t)wpr);
@@ -295,19 +315,19 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(kOcc)))
       const bool full = (part + 1) * kWG <= bpi && (dbg == 0 || dbg >= 40);
       const bool zero = __syncthreads_or(nonzero) == 0;
       const bool fill = __syncthreads_or(nonfill) == 0;
-      wgflat = full && (zero || fill);
+      wgflat = k420 && full && (zero || fill);  // the word pattern below is the 4:2:0 MCU's
       flat_v = zero ? 0 : (int)rd.fill;
     }
   }
   if (d.render >= 0 && rd.kind == kRenderRawGray) {
-    const int m0 = part * (kWG / 4), m1 = min(m0 + kWG / 4, bpi >> 2) - 1;
+    const int m0 = part * (kWG / kUnitBlocks), m1 = min(m0 + kWG / kUnitBlocks, bpi / kUnitBlocks) - 1;
     const int r0 = m0 / mcux, r1 = m1 / mcux;
-    const int nrows = 8 * (r1 - r0) + 10;
+    const int nrows = (kUnitRows / 2) * (r1 - r0 + 1) + 2;
     pcols = swz_col(rd.src_w + 1) + 1;
     pcols += (4 - pcols % 8 + 8) % 8;  // row stride ≡ 4 (mod 8)
     if (nrows * pcols <= kPatch && !(rd.src_off & 1)) {
       staged = true;
-      ys0 = 8 * r0 - 1;
+      ys0 = (kUnitRows / 2) * r0 - 1;
       const int W = rd.src_w, H = rd.src_h, hw = W >> 1;  // W is a multiple of 8 (exact 2× fit)
       const uint16_t* src = rs.raw + rd.src_off;
       // Interior: 4-byte loads of pixel pairs, all issued before the LDS stores (one latency).
@@ -380,9 +400,8 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(kOcc)))
   if (wgflat) {
     dc0 = quant_recip(64 * (flat_v - 128), q, 0);
   } else if (valid) {
-    const int mcu = b >> 2, sub = b & 3;
-    const int my = (int)dmx.q((uint32_t)mcu), mx = mcu - my * mcux;
-    const int bx = 2 * mx + (sub & 1), by = 2 * my + (sub >> 1);
+    int bx, by;
+    block_xy(b, bx, by);
     int32_t blk[64];
     // Label images are mostly background: when every block of the wave is one flat colour (76% of
     // the phantom cohort's label waves, 97.5% of its blocks) the islow FDCT of a constant block is
@@ -500,7 +519,7 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(kOcc)))
       }
     }
     if (last < 63) lw.put_sym(actab[0x00]);
-    if ((b & 3) == 3) {  // the MCU's Cb and Cr blocks of a gray image: DC diff 0 + EOB each
+    if (kSamp == kSampling444 || (k420 && (b & 3) == 3)) {  // the MCU's Cb and Cr blocks of a gray image: DC diff 0 + EOB each
       lw.put_sym(kHuffDcChroma.e[0]);
       lw.put_sym(kHuffAcChroma.e[0]);
       lw.put_sym(kHuffDcChroma.e[0]);
@@ -518,11 +537,10 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(kOcc)))
   if (tid < 64) {
     int dcp = 0;
     if (part > 0 && dbg != 17) {  // dbg 17: profiling variant without the predecessor's DC (output invalid)
-      const int pb = part * kWG - 1;
-      const int mcu = pb >> 2, sub = pb & 3;
-      const int my = (int)dmx.q((uint32_t)mcu), mx = mcu - my * mcux;
-      const int u = 8 * (2 * mx + (sub & 1)) + (tid & 7);
-      const int v = 8 * (2 * my + (sub >> 1)) + (tid >> 3);
+      int pbx, pby;
+      block_xy(part * kWG - 1, pbx, pby);
+      const int u = 8 * pbx + (tid & 7);
+      const int v = 8 * pby + (tid >> 3);
       const int px = d.render >= 0 ? (int)render_pixel(rd, rs.raw, rs.f32, rs.bits, win, u, v)
                                    : (int)canvas[d.canvas_off + (size_t)v * out_w + u];
       dcp = quant_recip(wave_sum_i32(px - 128), q, 0);
@@ -833,8 +851,10 @@ bool render_is_exact_2x(const RenderDesc& r, int out_w, int out_h) {
 }
 
 void launch_jpeg(const uint8_t* canvas, const JpegDesc* jd, int ncanvas, int out_w, int out_h, const int32_t* div_luma,
-                 JpegWork& w, uint8_t* out, int32_t* out_sizes, hipStream_t stream, const JpegRenderSrc* fused) {
+                 JpegWork& w, uint8_t* out, int32_t* out_sizes, hipStream_t stream, const JpegRenderSrc* fused,
+                 int sampling) {
   if (ncanvas <= 0) return;
+  if (sampling < kSampling420 || sampling > kSamplingGray) throw DeviceError("launch_jpeg: unknown sampling");
   if (out_w % 16 || out_h % 16) throw DeviceError("GPU JPEG encoder needs canvas dims that are multiples of 16");
   if (!w.look || !w.ticket || !w.spill) throw DeviceError("launch_jpeg: JpegWork incomplete");
   if (w.look_base && w.look_base != 3 * w.look_cap) throw DeviceError("launch_jpeg: look area state corrupt");
@@ -872,8 +892,10 @@ void launch_jpeg(const uint8_t* canvas, const JpegDesc* jd, int ncanvas, int out
     w.look_base = w.look_base ? 0 : half;
     w.prev_words = words;
   }
-  jpeg_fused_kernel<4, kUnionWords><<<parts * ncanvas, kJpegWG, 0, stream>>>(canvas, jd, ncanvas, out_w, out_h, q, w, rs,
-                                                                         out, out_sizes, dbg);
+  auto* kern = sampling == kSampling420   ? &jpeg_fused_kernel<4, kUnionWords, kSampling420>
+              : sampling == kSampling444 ? &jpeg_fused_kernel<4, kUnionWords, kSampling444>
+                                         : &jpeg_fused_kernel<4, kUnionWords, kSamplingGray>;
+  kern<<<parts * ncanvas, kJpegWG, 0, stream>>>(canvas, jd, ncanvas, out_w, out_h, q, w, rs, out, out_sizes, dbg);
   check_launch("jpeg_fused_kernel");
 }
 
@@ -885,7 +907,12 @@ void preload_kernels() {
   preload_volume();
   preload_threshold();
   hipFuncAttributes a;
-  check_hip(hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&jpeg_fused_kernel<4, kUnionWords>)), "preload jpeg_fused_kernel");
+  check_hip(hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&jpeg_fused_kernel<4, kUnionWords, kSampling420>)),
+            "preload jpeg_fused_kernel");
+  check_hip(hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&jpeg_fused_kernel<4, kUnionWords, kSampling444>)),
+            "preload jpeg_fused_kernel 4:4:4");
+  check_hip(hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&jpeg_fused_kernel<4, kUnionWords, kSamplingGray>)),
+            "preload jpeg_fused_kernel gray");
 }
 
 }  // namespace nm03::gpu

@@ -266,7 +266,8 @@ PYBIND11_MODULE(_nm03, m) {
       .def_readwrite("border_opacity", &RenderParams::border_opacity)
       .def_readwrite("border_radius", &RenderParams::border_radius)
       .def_readwrite("jpeg_quality", &RenderParams::jpeg_quality)
-      .def_readwrite("filter", &RenderParams::filter);
+      .def_readwrite("filter", &RenderParams::filter)
+      .def_readwrite("jpeg_sampling", &RenderParams::jpeg_sampling);
   py::class_<EngineConfig>(m, "EngineConfig")
       .def(py::init<>())
       .def_readwrite("device", &EngineConfig::device)
@@ -608,13 +609,22 @@ PYBIND11_MODULE(_nm03, m) {
   // ---- JPEG --------------------------------------------------------------------------------------
   m.def("jpeg_encode_gray420", [](py::array_t<uint8_t, py::array::c_style | py::array::forcecast> g, int quality) {
     const int h = (int)g.shape(0), w = (int)g.shape(1);
-    auto b = jpeg::encode_gray420(g.data(), w, h, w, quality);
+    auto b = jpeg::encode_gray(g.data(), w, h, w, quality);
     return py::bytes((const char*)b.data(), b.size());
   }, py::arg("gray"), py::arg("quality") = 75);
-  m.def("jpeg_header", [](int w, int h, int quality) {
-    auto b = jpeg::make_header(w, h, jpeg::make_tables(quality));
+  // sampling: jpeg::Sampling (0 YCbCr 4:2:0, 1 YCbCr 4:4:4, 2 one gray component).
+  m.def("jpeg_encode_gray", [](py::array_t<uint8_t, py::array::c_style | py::array::forcecast> g, int quality,
+                               int sampling) {
+    if (sampling < 0 || sampling > 2) throw std::invalid_argument("sampling must be 0, 1 or 2");
+    const int h = (int)g.shape(0), w = (int)g.shape(1);
+    auto b = jpeg::encode_gray(g.data(), w, h, w, quality, (jpeg::Sampling)sampling);
     return py::bytes((const char*)b.data(), b.size());
-  });
+  }, py::arg("gray"), py::arg("quality") = 75, py::arg("sampling") = 0);
+  m.def("jpeg_header", [](int w, int h, int quality, int sampling) {
+    if (sampling < 0 || sampling > 2) throw std::invalid_argument("sampling must be 0, 1 or 2");
+    auto b = jpeg::make_header(w, h, jpeg::make_tables(quality), (jpeg::Sampling)sampling);
+    return py::bytes((const char*)b.data(), b.size());
+  }, py::arg("w"), py::arg("h"), py::arg("quality") = 75, py::arg("sampling") = 0);
   m.def("jpeg_quant_tables", [](int quality) {
     auto t = jpeg::make_tables(quality);
     return py::make_tuple(std::vector<int>(t.qluma, t.qluma + 64), std::vector<int>(t.qchroma, t.qchroma + 64));
@@ -1080,7 +1090,7 @@ PYBIND11_MODULE(_nm03, m) {
     if (scr) (void)hipFree(scr);
   }, py::arg("src"), py::arg("dst"), py::arg("tmp"), py::arg("w"), py::arg("h"), py::arg("d"), py::arg("size"),
      py::arg("stream"), py::arg("ball") = false);
-  m.def("k_jpeg", [](uintptr_t canvas, int n, int h, int w, int quality, uintptr_t stream) {
+  m.def("k_jpeg", [](uintptr_t canvas, int n, int h, int w, int quality, uintptr_t stream, int sampling) {
     hipStream_t st = as_stream(stream);
     const int blocks = (w / 8) * (h / 8);
     const uint32_t out_cap = 512 * 1024 + 64;
@@ -1113,7 +1123,7 @@ PYBIND11_MODULE(_nm03, m) {
     int32_t divs[64];
     gpu::jpeg_divisors(quality, divs);
     gpu::launch_jpeg((const uint8_t*)canvas, (const gpu::JpegDesc*)(dev + o_jd), n, w, h, divs, wk, dev + o_out,
-                     (int32_t*)(dev + o_sz), st);
+                     (int32_t*)(dev + o_sz), st, nullptr, sampling);
     std::vector<int32_t> sizes(n);
     gpu::check_hip(hipMemcpyAsync(sizes.data(), dev + o_sz, 4 * n, hipMemcpyDeviceToHost, st), "D2H");
     gpu::check_hip(hipStreamSynchronize(st), "k_jpeg");
@@ -1128,7 +1138,8 @@ PYBIND11_MODULE(_nm03, m) {
       res.append(py::bytes(b));
     }
     return res;
-  });
+  }, py::arg("canvas"), py::arg("n"), py::arg("h"), py::arg("w"), py::arg("quality"), py::arg("stream"),
+     py::arg("sampling") = 0);
 
   // ---- comm self-tests (CPU) ------------------------------------------------------------------------
   m.def("loopback_selftest", [](int n) {

@@ -311,7 +311,10 @@ struct Engine::Impl {
     pc.se_disc = p.se_shape == kSeDisc ? 1 : 0;
     jpeg::Tables t = jpeg::make_tables(cfg.render.jpeg_quality);
     for (int i = 0; i < 64; ++i) divs[i] = t.div_luma[i];
-    jpeg_header = jpeg::make_header(cfg.render.out_width, cfg.render.out_height, t);
+    if (cfg.render.jpeg_sampling < jpeg::kSampling420 || cfg.render.jpeg_sampling > jpeg::kSamplingGray)
+      throw std::invalid_argument("jpeg_sampling must be 0 (4:2:0), 1 (4:4:4) or 2 (gray)");
+    jpeg_header = jpeg::make_header(cfg.render.out_width, cfg.render.out_height, t,
+                                    (jpeg::Sampling)cfg.render.jpeg_sampling);
     if (cfg.render.out_width % 16 || cfg.render.out_height % 16)
       throw DeviceError("canvas size must be a multiple of 16");
     if (host_only_) make_templates();
@@ -1069,7 +1072,8 @@ struct Engine::Impl {
     rsrc.stats = d_stats;
     rsrc.rd = d_rd;
     rsrc.nrd = ncanv;
-    launch_jpeg(s.d_canvas, d_jd, ncanv, cw, ch, divs, s.jw, s.d_out, s.d_sizes, s.stream, &rsrc);
+    launch_jpeg(s.d_canvas, d_jd, ncanv, cw, ch, divs, s.jw, s.d_out, s.d_sizes, s.stream, &rsrc,
+                cfg.render.jpeg_sampling);
     check_hip(hipEventRecord(s.ev2, s.stream), "event");
     if (mark) mark->enq = now_s();
     wait_batch(s, s.ev2, t_enq, nl);
@@ -1105,7 +1109,7 @@ struct Engine::Impl {
     check_hip(hipMemcpy(canvas.data(), s.d_canvas + (size_t)k * cw * ch, canvas.size(), hipMemcpyDeviceToHost),
               "canvas D2H");
     jpeg::Tables t = jpeg::make_tables(cfg.render.jpeg_quality);
-    fallback = jpeg::encode_scan_gray420(canvas.data(), cw, ch, cw, t);
+    fallback = jpeg::encode_scan_gray(canvas.data(), cw, ch, cw, t, (jpeg::Sampling)cfg.render.jpeg_sampling);
     if (fallbacks) ++*fallbacks;
     return false;
   }

@@ -524,7 +524,8 @@ std::vector<std::vector<uint8_t>> VolumeRunner::export_jpegs(const VolumeInput& 
   check_hip(hipMemcpyAsync(bits, V.dil.p, vol_words * 8, hipMemcpyDeviceToDevice, V.stream), "D2D labels");
   border_volume(bits, bits + vol_words, v.w, v.h, v.d, rp.border_radius, V.stream, V.morph_scratch.as<uint64_t>());
   const jpeg::Tables tables = jpeg::make_tables(rp.jpeg_quality);
-  const std::vector<uint8_t> header = jpeg::make_header(cw, ch, tables);
+  const jpeg::Sampling samp = (jpeg::Sampling)rp.jpeg_sampling;
+  const std::vector<uint8_t> header = jpeg::make_header(cw, ch, tables, samp);
   const RenderGeom g = make_render_geom(v.w, v.h, v.spacing_x, v.spacing_y, cw, ch);
   const uint8_t fill = opacity_u8(rp.label_opacity), bval = opacity_u8(rp.border_opacity);
   const size_t canvas_bytes = (size_t)cw * ch;
@@ -581,7 +582,7 @@ std::vector<std::vector<uint8_t>> VolumeRunner::export_jpegs(const VolumeInput& 
     rs.rd = drd;
     rs.nrd = nc;
     launch_jpeg(X.canvas.as<uint8_t>(), reinterpret_cast<const JpegDesc*>(d_jd), nc, cw, ch, tables.div_luma, X.jw,
-                X.d_out, X.d_sizes, V.stream, &rs);
+                X.d_out, X.d_sizes, V.stream, &rs, samp);
     check_hip(hipStreamSynchronize(V.stream), "export sync");
     bool rendered = any_canvas;
     for (int k = 0; k < nc; ++k) {
@@ -600,7 +601,7 @@ std::vector<std::vector<uint8_t>> VolumeRunner::export_jpegs(const VolumeInput& 
         check_hip(hipMemcpy(canvas.data(), X.canvas.as<uint8_t>() + (size_t)k * canvas_bytes, canvas_bytes,
                             hipMemcpyDeviceToHost),
                   "canvas D2H");
-        const auto scan = jpeg::encode_scan_gray420(canvas.data(), cw, ch, cw, tables);
+        const auto scan = jpeg::encode_scan_gray(canvas.data(), cw, ch, cw, tables, samp);
         f.insert(f.end(), scan.begin(), scan.end());
         if (st) ++st->jpeg_fallbacks;
       }
@@ -723,8 +724,10 @@ std::vector<std::vector<uint8_t>> golden_export(const VolumeInput& v, const std:
     const auto c0 = golden::render_gray(vals[z], g, *mm.first, *mm.second, rp.filter == kFilterNearest);
     const auto c1 = golden::render_labels(lab, golden::border(lab, v.w, v.h, rp.border_radius), g,
                                           opacity_u8(rp.label_opacity), opacity_u8(rp.border_opacity));
-    files[2 * z] = jpeg::encode_gray420(c0.data(), rp.out_width, rp.out_height, rp.out_width, rp.jpeg_quality);
-    files[2 * z + 1] = jpeg::encode_gray420(c1.data(), rp.out_width, rp.out_height, rp.out_width, rp.jpeg_quality);
+    files[2 * z] = jpeg::encode_gray(c0.data(), rp.out_width, rp.out_height, rp.out_width, rp.jpeg_quality,
+                                     (jpeg::Sampling)rp.jpeg_sampling);
+    files[2 * z + 1] = jpeg::encode_gray(c1.data(), rp.out_width, rp.out_height, rp.out_width, rp.jpeg_quality,
+                                     (jpeg::Sampling)rp.jpeg_sampling);
   }
   return files;
 }

@@ -305,7 +305,7 @@ TEST(pack12_stream_exact_bytes) {
 TEST(jpeg_container) {
   std::vector<uint8_t> img(64 * 48);
   for (size_t i = 0; i < img.size(); ++i) img[i] = (uint8_t)(i % 251);
-  const auto j = nm03::jpeg::encode_gray420(img.data(), 64, 48, 64, 75);
+  const auto j = nm03::jpeg::encode_gray(img.data(), 64, 48, 64, 75);
   CHECK(j.size() > 200 && j[0] == 0xFF && j[1] == 0xD8);                    // SOI
   CHECK(j[j.size() - 2] == 0xFF && j[j.size() - 1] == 0xD9);                  // EOI
   const auto t = nm03::jpeg::make_tables(75);

@@ -29,6 +29,31 @@ def test_test_pipeline_cpu(native, cohort_root, tmp_path):
     assert im.size == (2560, 512)
 
 
+@pytest.mark.parametrize("flag,mode,layer", [("gray", "L", None), ("444", "RGB", (1, 1, 1, 0)),
+                                              ("420", "RGB", (1, 2, 2, 0))])
+def test_test_pipeline_cpu_jpeg_sampling(native, cohort_root, tmp_path, flag, mode, layer):
+    """--jpeg-sampling: every export (and the montage) in the chosen layout, equal to golden_run
+    with RenderParams.jpeg_sampling set."""
+    out = tmp_path / "o"
+    r = run_bin("test_pipeline", "--cpu", "--jpeg-sampling", flag, "--data-root", cohort_root, "--out", str(out))
+    assert r.returncode == 0, r.stderr
+    rp = native.RenderParams()
+    rp.jpeg_sampling = {"420": 0, "444": 1, "gray": 2}[flag]
+    raw, meta = native.read_slice(native.test_slice_path(cohort_root))
+    g = native.golden_run(raw, meta["type"], meta["stored_bits"], meta["slope"], meta["intercept"],
+                          native.PipelineParams(), rp, meta["spacing_x"], meta["spacing_y"])
+    assert (out / "original_image.jpg").read_bytes() == g["jpeg_original"]
+    assert (out / "final_dilated_result.jpg").read_bytes() == g["jpeg_processed"]
+    PIL = pytest.importorskip("PIL.Image")
+    for name in ("original_image.jpg", "segmentation.jpg", "multi_view.jpg"):
+        im = PIL.open(io.BytesIO((out / name).read_bytes()))
+        assert im.mode == mode
+        if layer:
+            assert im.layer[0] == layer
+    r = run_bin("test_pipeline", "--cpu", "--jpeg-sampling", "422", "--data-root", cohort_root, "--out", str(out))
+    assert r.returncode == 2 and "--jpeg-sampling" in r.stderr
+
+
 def test_cli_help_and_bad_flag():
     for tool in ("test_pipeline", "img_processing_sequential", "img_processing_parallel"):
         r = run_bin(tool, "--help")

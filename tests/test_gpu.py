@@ -185,6 +185,27 @@ def test_jpeg_kernel_vs_golden_and_libjpeg(native, kind):
     assert outs[0] == bio.getvalue()
 
 
+@pytest.mark.parametrize("sampling", [1, 2])
+@pytest.mark.parametrize("shape", [(3, 512, 512), (2, 48, 80), (2, 272, 400)])
+def test_jpeg_kernel_other_samplings(native, sampling, shape):
+    """--jpeg-sampling 444 / gray on K4: raster-order MCUs (workgroups start mid-row: the
+    predecessor DC of a part), byte-identical to the golden encoder and to libjpeg via Pillow."""
+    rng = np.random.default_rng(sampling * 7 + shape[1])
+    c = rng.integers(0, 256, size=shape, dtype=np.uint8)
+    c[1, : shape[1] // 2] = np.where(c[1, : shape[1] // 2] > 128, 153, 0)  # flat label-like half
+    outs = ops.jpeg_encode(torch.from_numpy(c).cuda(), 75, sampling=sampling)
+    PIL = pytest.importorskip("PIL.Image")
+    for i in range(shape[0]):
+        assert outs[i] is not None
+        assert outs[i] == native.jpeg_encode_gray(c[i], 75, sampling)
+        bio = io.BytesIO()
+        if sampling == 2:
+            PIL.fromarray(c[i]).save(bio, format="JPEG", quality=75)
+        else:
+            PIL.fromarray(c[i]).convert("RGB").save(bio, format="JPEG", quality=75, subsampling=0)
+        assert outs[i] == bio.getvalue()
+
+
 def test_jpeg_capacity_overflow_reports(native):
     # 1024×1024 noise exceeds the per-image staging cap → None (callers fall back to the CPU)
     c = np.random.default_rng(0).integers(0, 256, size=(1, 1024, 1024), dtype=np.uint8)
@@ -1235,6 +1256,33 @@ def test_engine_render_nearest_bit_exact(native, cohort_root, tmp_path):
         stem = os.path.splitext(os.path.basename(f))[0]
         assert open(os.path.join(od, stem + "_original.jpg"), "rb").read() == g["jpeg_original"]
         assert open(os.path.join(od, stem + "_processed.jpg"), "rb").read() == g["jpeg_processed"]
+
+
+@pytest.mark.parametrize("sampling", [1, 2])
+def test_engine_jpeg_sampling_bit_exact(native, cohort_root, tmp_path, sampling):
+    """--jpeg-sampling 444 / gray through the engine: the fused render + encode of a cohort run
+    (staged gray and label rows, flat label waves) and one slice's five stage JPEGs equal the golden
+    model, whose encoder is byte-identical to libjpeg (tests/test_jpeg.py)."""
+    raw = _phantom(native)
+    meta = {"type": "u16", "stored_bits": 16, "slope": 1.0, "intercept": 0.0, "spacing_x": 1.0, "spacing_y": 1.0}
+    pipe = nm.SlicePipeline(nm.PipelineConfig(batch_size=1, streams=1, threads=2, jpeg_sampling=sampling))
+    gpu, ref = pipe.run_array(raw, meta), pipe.golden(raw, meta)
+    assert gpu["jpegs"][0] == ref["jpeg_original"] and gpu["jpegs"][4] == ref["jpeg_processed"]
+    out = str(tmp_path / "o")
+    items = _items(native, cohort_root, out)[:40]
+    cfg = nm.PipelineConfig(batch_size=8, streams=2, threads=4, jpeg_sampling=sampling)
+    st, _ = native.Engine(cfg.engine_config()).run(items)
+    assert all(c == 0 for c, _ in st)
+    for f, od in items[::5]:
+        r, m = native.read_slice(f)
+        g = native.golden_run(r, m["type"], m["stored_bits"], m["slope"], m["intercept"], native.PipelineParams(),
+                              cfg.render_params(), m["spacing_x"], m["spacing_y"])
+        stem = os.path.splitext(os.path.basename(f))[0]
+        orig = open(os.path.join(od, stem + "_original.jpg"), "rb").read()
+        assert orig == g["jpeg_original"]
+        assert open(os.path.join(od, stem + "_processed.jpg"), "rb").read() == g["jpeg_processed"]
+    PIL = pytest.importorskip("PIL.Image")
+    assert PIL.open(io.BytesIO(orig)).mode == ("L" if sampling == 2 else "RGB")
 
 
 def test_deferred_rccl_comm_single_rank(native):
