@@ -848,6 +848,21 @@ def test_volume_cli_gpu_equals_golden(native, cohort_root, tmp_path):
     assert j["gpus"] == 2 and len(j["per_rank_wall_s"]) == 2
 
 
+def test_volume_cli_jpeg_sampling_gray_equals_golden(native, cohort_root, tmp_path):
+    """--mode 3d --jpeg-sampling gray: the GPU plane export (gray instance of K4, fused renders)
+    equals the golden 3D export in the same layout, and the files are one-component JPEGs."""
+    g, c = tmp_path / "gpu", tmp_path / "cpu"
+    for out, extra in ((g, []), (c, ["--cpu"])):
+        r = run_bin("img_processing_parallel", "--mode", "3d", "--jpeg-sampling", "gray", *extra, "--data-root",
+                    cohort_root, "--out", str(out))
+        assert r.returncode == 0, r.stderr
+    tg, tc = _tree(str(g)), _tree(str(c))
+    assert len(tg) > 0 and tg == tc
+    PIL = pytest.importorskip("PIL.Image")
+    f = next(p for p in g.rglob("*.jpg"))
+    assert PIL.open(f).mode == "L"
+
+
 def test_volume_run_series_equals_golden(native, tmp_path):
     """VolumePipeline.run_series on a DICOM series directory (written out of order on disk, 1-10
     after 1-9) equals run() on the stacked planes and the golden 3D model."""
