@@ -155,8 +155,13 @@ uint16_t us_value(const Cursor& c, const Elem& e) {
   return c.big ? (uint16_t)((p[0] << 8) | p[1]) : (uint16_t)(p[0] | (p[1] << 8));
 }
 
+// Largest inflated dataset accepted (DICOM element lengths are 32-bit; a 2 GiB dataset is far
+// beyond any slice or series file): a small crafted stream cannot make the reader allocate more.
+constexpr size_t kMaxInflated = size_t(1) << 31;
+
 // Raw deflate stream (RFC 1951, no zlib header: PS3.5 A.5) → bytes.
 std::vector<uint8_t> inflate_raw(const uint8_t* src, size_t n) {
+  if (n > 0xFFFFFFFFu) throw SliceError("Deflated DICOM dataset too large");
   z_stream z{};
   if (inflateInit2(&z, -MAX_WBITS) != Z_OK) throw SliceError("zlib inflateInit failed");
   std::vector<uint8_t> out(std::max<size_t>(n * 4, 1 << 16));
@@ -165,7 +170,13 @@ std::vector<uint8_t> inflate_raw(const uint8_t* src, size_t n) {
   size_t have = 0;
   int r = Z_OK;
   while (r != Z_STREAM_END) {
-    if (have == out.size()) out.resize(out.size() * 2);
+    if (have == out.size()) {
+      if (out.size() >= kMaxInflated) {
+        inflateEnd(&z);
+        throw SliceError("Deflated DICOM dataset inflates beyond 2 GiB");
+      }
+      out.resize(std::min(out.size() * 2, kMaxInflated));
+    }
     z.next_out = out.data() + have;
     z.avail_out = (uInt)(out.size() - have);
     r = inflate(&z, Z_NO_FLUSH);
@@ -315,6 +326,11 @@ Header parse_prefix(const uint8_t* data, size_t avail, size_t size) {
           throw SliceError("RLE pixel data has " + std::to_string(frags.size()) + " fragments for " + std::to_string(frames) +
                            " frame(s) (one fragment per frame is supported)");
         const size_t fb = h.frame_bytes();
+        // PackBits expands at most 64× (a 2-byte replicate run → 128 bytes): a fragment too short
+        // for its frame is corrupt, found before the frame buffers are allocated.
+        for (int f = 0; f < frames; ++f)
+          if (fb > 64 * frags[f].second) throw SliceError("RLE fragment too short for a " + std::to_string(h.rows) + "x" +
+                                                           std::to_string(h.cols) + " frame");
         auto dec = std::make_shared<std::vector<uint8_t>>(fb * frames);
         for (int f = 0; f < frames; ++f)
           decode_rle_frame(c.d + frags[f].first, frags[f].second, h.rows, h.cols, h.bits_allocated / 8, dec->data() + f * fb);

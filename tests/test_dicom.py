@@ -195,6 +195,17 @@ def test_rle_corrupt_segment_rejected(native):
         native.dicom_parse(bytes(b[:-60]))  # cut into the last fragment
 
 
+def test_rle_oversized_frame_rejected_before_allocation(native):
+    """Rows/Columns patched to 65535×65535 on a tiny RLE file: rejected from the fragment length
+    (PackBits expands ≤ 64×) instead of allocating the 8 GiB frame."""
+    b = bytearray(native.dicom_bytes(np.zeros((8, 8), np.uint16), syntax="rle"))
+    for elem in (b"\x28\x00\x10\x00US\x02\x00", b"\x28\x00\x11\x00US\x02\x00"):
+        i = b.index(elem) + len(elem)
+        b[i:i + 2] = b"\xff\xff"
+    with pytest.raises(Exception, match="RLE fragment too short"):
+        native.dicom_parse(bytes(b))
+
+
 @pytest.mark.parametrize("ptype,bits", [("u16", 12), ("i16", 12), ("u16", 16), ("u8", 8)])
 def test_monochrome1_inverted_at_import(native, tmp_path, ptype, bits):
     rng = np.random.default_rng(6)

@@ -1,7 +1,8 @@
 #!/bin/bash
 # (gpurun) Cold CLI anatomy: whole-process walls of img_processing_parallel by GPU_MAX_HW_QUEUES
 # (exact wait4 timing + the CLI's own phase split incl. exec → main), per-batch timelines of fresh
-# runs (NM03_BATCH_TRACE=1), and one rocprofv3 trace of a cold run (kernels, copies, HIP API).
+# runs (NM03_BATCH_TRACE=1), and one rocprofv3 trace of a cold run (kernels, copies, HIP and HSA API:
+# what the runtime calls inside hipInit and the first stream creations).
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
@@ -57,7 +58,7 @@ for r in 1 2; do
   (cd /tmp && NM03_BATCH_TRACE=1 NM03_LOG=info timeout -k 10 60 $CLI --json $R/$O/trace_$r.json > $R/$O/trace_$r.log 2>&1) || exit 3
 done
 cd /tmp || exit 4
-NM03_ROCTX=1 timeout -k 10 120 rocprofv3 --kernel-trace --memory-copy-trace --marker-trace --hip-runtime-trace \
+NM03_ROCTX=1 timeout -k 10 120 rocprofv3 --kernel-trace --memory-copy-trace --marker-trace --hip-runtime-trace --hsa-trace \
   --output-format csv -d $R/$O/trace -o cli -- $R/build/bin/img_processing_parallel --data-root $D/ \
   --out /dev/shm/cold_out --quiet --json $R/$O/traced.json > $R/$O/traced.log 2>&1 || exit 5
 rm -rf $D /dev/shm/cold_out
