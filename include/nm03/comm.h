@@ -145,7 +145,9 @@ class ShmSegment {
   void check_abort(int self) const;
 
   // RCCL unique id (128 bytes) published by rank 0, awaited by the others (deadline + abort).
+  // publish_uid_failed: rank 0 could not create one; waiters throw at once instead of timing out.
   void publish_uid(const std::vector<uint8_t>& uid);
+  void publish_uid_failed();
   std::vector<uint8_t> wait_uid(int self, double timeout_s) const;
 
   // Generation barrier across all ranks of the segment; deadline + abort aware.

@@ -294,7 +294,12 @@ class DeferredRcclComm final : public Comm {
     try {
       std::vector<uint8_t> uid;
       if (rank_ == 0) {
-        uid = rccl_unique_id();
+        try {
+          uid = rccl_unique_id();
+        } catch (...) {
+          seg_->publish_uid_failed();  // the other ranks fail fast and agree on the fallback
+          throw;
+        }
         seg_->publish_uid(uid);
       } else {
         uid = seg_->wait_uid(rank_, timeout_);
@@ -361,6 +366,7 @@ class DeferredRcclComm final : public Comm {
   std::string fallback_error() const override { return fallback_error_; }
   DataPlaneTimes data_plane_times() const override { return times_; }
   void set_abort_segment(std::shared_ptr<ShmSegment> seg) override {
+    std::lock_guard<std::mutex> g(m_);  // rccl_ is written by the start-up thread
     if (rccl_) rccl_->set_abort_segment(std::move(seg));
   }
 

@@ -212,6 +212,10 @@ void ShmSegment::publish_uid(const std::vector<uint8_t>& uid) {
   h_->uid_ready.store((uint32_t)uid.size(), std::memory_order_release);
 }
 
+constexpr uint32_t kUidFailed = 0xFFFFFFFFu;
+
+void ShmSegment::publish_uid_failed() { h_->uid_ready.store(kUidFailed, std::memory_order_release); }
+
 std::vector<uint8_t> ShmSegment::wait_uid(int self, double timeout_s) const {
   const double deadline = mono_s() + timeout_s;
   uint32_t len;
@@ -220,6 +224,7 @@ std::vector<uint8_t> ShmSegment::wait_uid(int self, double timeout_s) const {
     if (mono_s() > deadline) throw CommError("timed out waiting for the RCCL unique id from rank 0");
     std::this_thread::sleep_for(std::chrono::microseconds(200));
   }
+  if (len == kUidFailed) throw CommError("rank 0 could not create the RCCL unique id");
   return std::vector<uint8_t>(h_->uid, h_->uid + len);
 }
 
