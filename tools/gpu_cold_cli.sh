@@ -14,12 +14,13 @@ CLI="$R/build/bin/img_processing_parallel --data-root $D/ --out /dev/shm/cold_ou
 timeout -k 5 60 build/bin/nm03_synth --data-root $D/ --threads 16 > /dev/null || exit 1
 # Interleaved: run r of every GPU_MAX_HW_QUEUES value before run r + 1 (box drift hits all alike).
 timeout -k 10 600 python3 - "$D" "$O" <<'PY' || exit 2
-import json, os, sys
+import json, os, sys, time
 sys.path.insert(0, os.environ["GRAFT_REPO_ROOT"])
 from nm03_capstone_project_amd.utils.cli_wall import time_cli
 d, o = sys.argv[1:3]
 # VARIANTS: ";"-separated, each "-" or "NAME=VAL,NAME=VAL" (environment) with an optional
-# "ARGS=..." (CLI flags); QUEUES (legacy): one variant per --hw-queues value.
+# "ARGS=..." (CLI flags) and "SLEEP=s" (pause before the run: time since the previous GPU process
+# exited); QUEUES (legacy): one variant per --hw-queues value.
 if os.environ.get("VARIANTS"):
     queues = os.environ["VARIANTS"].split(";")
 else:
@@ -33,6 +34,8 @@ for r in range(int(os.environ.get("RUNS", "7"))):
             name, val = kv.split("=", 1)
             if name == "ARGS":
                 extra += val.split()
+            elif name == "SLEEP":
+                time.sleep(float(val))
             else:
                 env[name] = val
         argv = [os.path.join(os.environ["GRAFT_REPO_ROOT"], "build/bin/img_processing_parallel"), "--data-root",
