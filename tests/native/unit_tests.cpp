@@ -242,6 +242,73 @@ TEST(dicom_rejects_garbage) {
   CHECK(threw);
 }
 
+// Mutation fuzz of the reader (tests/test_dicom_fuzz.py does the same through Python): here it runs
+// inside tools/sanitize_check.sh's ASan / UBSan builds, which also catch reads past a buffer that
+// would not crash. Every syntax and a multi-frame file as seeds; flips, 0xFF runs, truncations,
+// small integers over 4-byte fields; deterministic xorshift.
+TEST(dicom_mutation_fuzz) {
+  using namespace nm03::dicom;
+  std::vector<std::vector<uint8_t>> seeds;
+  auto px = ramp(3 * 12 * 16, 4093);
+  for (auto& v : px) v &= 0x0FFF;
+  for (Syntax sx : {Syntax::kExplicitLE, Syntax::kImplicitLE, Syntax::kExplicitBE, Syntax::kDeflatedLE,
+                    Syntax::kRleLossless})
+    for (int frames : {1, 3}) {
+      WriteSpec ws;
+      ws.rows = 12;
+      ws.cols = 16;
+      ws.bits_stored = 12;
+      ws.frames = frames;
+      ws.pixels = px.data();
+      ws.syntax = sx;
+      seeds.push_back(write(ws));
+    }
+  uint64_t r = 0x9E3779B97F4A7C15ull;
+  auto rnd = [&](uint64_t n) {
+    r ^= r << 13, r ^= r >> 7, r ^= r << 17;
+    return n ? r % n : 0;
+  };
+  int parsed = 0, rejected = 0;
+  for (const auto& s : seeds)
+    for (int it = 0; it < 1500; ++it) {
+      std::vector<uint8_t> b = s;
+      switch (rnd(4)) {
+        case 0:
+          for (int k = 0, n = 1 + (int)rnd(7); k < n; ++k) b[rnd(b.size())] = (uint8_t)rnd(256);
+          break;
+        case 1: {
+          const size_t i = rnd(b.size() - 4);
+          for (size_t k = 0, n = 2 + rnd(3); k < n; ++k) b[i + k] = 0xFF;
+          break;
+        }
+        case 2:
+          b.resize(rnd(b.size()));
+          break;
+        default: {
+          const size_t i = rnd(b.size() - 4);
+          const uint32_t v = (uint32_t)rnd(1u << 20);
+          std::memcpy(&b[i], &v, 4);
+        }
+      }
+      try {
+        const Header h = parse(b.data(), b.size());
+        ++parsed;
+        const int frames = std::max(1, h.frames);
+        if ((size_t)h.rows * h.cols * frames > ((size_t)1 << 22)) continue;
+        std::vector<uint16_t> out((size_t)h.rows * h.cols);
+        for (int f = 0; f < frames; ++f) {
+          try {
+            copy_pixels16(h, b.data(), b.size(), out.data(), f);
+          } catch (const std::exception&) {
+          }
+        }
+      } catch (const std::exception&) {
+        ++rejected;
+      }
+    }
+  CHECK(parsed > 100 && rejected > 100);
+}
+
 TEST(pack12_round_trip_and_declines) {
   using namespace nm03::pack12;
   if (!available()) return;  // no AVX2: the engine ships 16-bit samples
