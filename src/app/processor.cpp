@@ -67,6 +67,8 @@ void usage(const std::string& which) {
             << "  --resume               keep existing outputs; skip slices whose two JPEGs exist\n"
             << "  --frame K              import frame K of multi-frame DICOM files (default: reject them)\n"
             << "  --hw-queues N          HIP hardware queues of this process (GPU_MAX_HW_QUEUES; default 2, 0 = environment)\n"
+            << "  --copy-engine auto|sdma|blit  host<->GPU copies: DMA engines or shader copies (auto: blit for\n"
+            << "                         2D jobs of <= 4096 slices per rank, whose cold start the DMA queue's set-up dominates)\n"
             << "  --quiet                suppress per-slice progress lines\n"
             << "env: NM03_DATA_ROOT, NM03_LOG=info|warn|error|none, NM03_ROCTX=1,\n"
             << "     NM03_FAULT=corrupt_dicom:<i>,fail_batch:<k>,fail_write:<j>,rank_exit:<r>\n"
@@ -185,6 +187,14 @@ AppConfig parse_args(int argc, char** argv, const std::string& which) {
     else if (a == "--resume") c.engine.resume = true;
     else if (a == "--frame") c.engine.pipe.frame = std::atoi(val().c_str());
     else if (a == "--hw-queues") c.hw_queues = std::max(0, std::atoi(val().c_str()));
+    else if (a == "--copy-engine") {
+      const std::string v = val();
+      if (v != "auto" && v != "sdma" && v != "blit") {
+        std::cerr << "--copy-engine must be auto, sdma or blit" << std::endl;
+        std::exit(2);
+      }
+      c.copy_engine = v == "sdma" ? kCopySdma : v == "blit" ? kCopyBlit : kCopyAuto;
+    }
     else if (a == "--jpeg-sampling") {
       const std::string v = val();
       if (v != "420" && v != "444" && v != "gray") {
@@ -229,6 +239,7 @@ AppConfig parse_args(int argc, char** argv, const std::string& which) {
 // =============================================================================================
 int run_sequential(const AppConfig& cfg) {
   try {
+    apply_copy_engine(cfg, cfg.copy_engine == kCopyAuto ? count_cohort_slices(cfg) : -1);
     // HIP start-up and the engine's construction on the start-up thread while the output root is set up.
     EngineStartup su(cfg.engine.device, std::max(1, cfg.engine.streams) + 1);
     // SequentialImageProcessor ctor: base output dir (main_sequential.cpp:81-91).
@@ -804,7 +815,8 @@ int parallel_rank(const AppConfig& cfg, int rank, int size, Comm& comm, int devi
     write_json(cfg.json, std::string("{\"mode\": \"parallel\", \"gpus\": ") + std::to_string(size) +
                              ", \"gpus_requested\": " + req + ", \"main_unix_s\": " +
                              fmt(cfg.main_unix_s, 17) + ", \"backend\": \"" +
-                             comm.backend() + "\", \"repeat\": " + std::to_string(cfg.repeat) + ", \"engine_setup_s\": " +
+                             comm.backend() + "\", \"copy_engine\": \"" + copy_engine_name() + "\", \"repeat\": " +
+                             std::to_string(cfg.repeat) + ", \"engine_setup_s\": " +
                              fmt(setup_s) + ", \"hip_init_s\": " + fmt(su.times().hip_init_s) + ", \"engine_ctor_s\": " +
                              fmt(su.times().engine_ctor_s) + ", \"streams_s\": " + fmt(su.times().streams_s) + ", \"engine_wait_s\": " + fmt(engine_wait_s) + ", \"kernel_load_s\": " +
                              fmt(su.times().kernel_load_s) + ", \"comm_start_s\": " + fmt(dp.start_s) + ", \"comm_wait_s\": " +
@@ -874,6 +886,27 @@ int64_t count_cohort_slices(const AppConfig& cfg) {
   }
 }
 
+// What the process's HIP runtime uses (read from the environment it starts with).
+const char* copy_engine_name() {
+  const char* v = std::getenv("HSA_ENABLE_SDMA");
+  return v && std::string(v) == "0" ? "blit" : "sdma";
+}
+
+bool apply_copy_engine(const AppConfig& cfg, int64_t slices_per_rank) {
+  // The first DMA copy of a process sets up the copy engine's queue inside
+  // hsa_amd_memory_async_copy_on_engine: 8.7 ms on the cold start's critical path (HIP + HSA API
+  // trace, profiles/r5/cold_env/). Shader (blit) copies run on the compute queues that exist anyway:
+  // interleaved cold CLIs on the 465-slice cohort, streams + warm-up 42.7 → 33.6 ms, processing
+  // 4.2 → 4.5 ms (profiles/r5/cold_env2/). Large jobs keep the DMA engines (PCIe-bound config 4
+  // measured 15% slower with shader uploads, ARCHITECTURE.md §6).
+  bool blit = cfg.copy_engine == kCopyBlit;
+  if (cfg.copy_engine == kCopyAuto)
+    blit = cfg.mode != "3d" && slices_per_rank >= 0 && slices_per_rank <= kBlitMaxSlicesPerRank &&
+           std::getenv("HSA_ENABLE_SDMA") == nullptr;
+  if (blit) setenv("HSA_ENABLE_SDMA", "0", 1);
+  return blit;
+}
+
 int auto_gpus(int64_t slices, int visible) {
   const int64_t want = (std::max<int64_t>(slices, 0) + kAutoSlicesPerRank - 1) / kAutoSlicesPerRank;
   return (int)std::max<int64_t>(1, std::min<int64_t>(std::max(1, visible), want));
@@ -892,10 +925,15 @@ int resolve_gpus(const AppConfig& cfg, const LaunchOptions& lo, int64_t slices) 
 int run_parallel(const AppConfig& cfg) {
   try {
     cohort::make_dirs(cfg.out_dir);  // OptimizedParallelProcessor ctor (main_parallel.cpp:219-231)
-    if (cfg.mode == "3d") return run_volume_cohort(cfg);
+    if (cfg.mode == "3d") {
+      apply_copy_engine(cfg, -1);  // auto keeps the DMA engines for volumes (32 MB per 256³ upload)
+      return run_volume_cohort(cfg);
+    }
     LaunchOptions lo = LaunchOptions::from_env();
     // auto: size the job to the cohort, counted from its directory listings before any fork
-    const int n = resolve_gpus(cfg, lo, cfg.gpus == kGpusAuto ? count_cohort_slices(cfg) : -1);
+    const int64_t slices = cfg.gpus == kGpusAuto || cfg.copy_engine == kCopyAuto ? count_cohort_slices(cfg) : -1;
+    const int n = resolve_gpus(cfg, lo, cfg.gpus == kGpusAuto ? slices : -1);
+    apply_copy_engine(cfg, slices < 0 ? -1 : (slices + n - 1) / n);
     std::vector<int> rank_devices;
     for (int r = 0; r < n; ++r)
       rank_devices.push_back(n > 1 ? lo.device_of(r) : lo.device_override >= 0 ? lo.device_override : cfg.engine.device);
@@ -916,7 +954,10 @@ int run_test_pipeline(const AppConfig& cfg) {
   try {
     // GPU path: HIP start-up and the engine's streams on the start-up thread while the slice loads.
     std::unique_ptr<EngineStartup> su;
-    if (!cfg.cpu) su = std::make_unique<EngineStartup>(cfg.engine.device, 2);
+    if (!cfg.cpu) {
+      apply_copy_engine(cfg, 1);  // one slice
+      su = std::make_unique<EngineStartup>(cfg.engine.device, 2);
+    }
     const std::string path = cfg.input.empty() ? cohort::test_slice_path(cfg.data_root) : cfg.input;
     golden::SliceInput in = golden::load_slice(path, 0, cfg.engine.pipe.frame);  // the test pipeline has no <100 guard
     const PipelineParams& p = cfg.engine.pipe;

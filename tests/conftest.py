@@ -33,4 +33,5 @@ def run_bin(name, *args, cwd=None, env=None, timeout=600):
     e = dict(os.environ)
     if env:
         e.update(env)
+    e = {k: v for k, v in e.items() if v is not None}  # env={"X": None} removes X
     return subprocess.run([exe, *args], cwd=cwd, env=e, capture_output=True, text=True, timeout=timeout)

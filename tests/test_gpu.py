@@ -739,6 +739,25 @@ def test_cli_parallel_multirank_identical(native, cohort_root, tmp_path, ranks):
     assert sum(pr["slices_ok"]) == len(t1) // 2
 
 
+def test_cli_copy_engine_auto_blit_and_sdma_identical(native, cohort_root, tmp_path):
+    """--copy-engine: the small test cohort takes shader (blit) copies by default (auto: ≤ 4096
+    slices per rank), --copy-engine sdma the DMA engines; both JSON records say which, and the
+    exported trees are identical (and equal the golden model on a sample)."""
+    import json
+    outs = {}
+    for flag in ("auto", "sdma", "blit"):
+        d = tmp_path / flag
+        r = run_bin("img_processing_parallel", "--data-root", cohort_root, "--out", str(d), "--gpus", "1",
+                    "--copy-engine", flag, "--json", str(tmp_path / f"{flag}.json"), env={"HSA_ENABLE_SDMA": None})
+        assert r.returncode == 0, r.stderr
+        j = json.load(open(tmp_path / f"{flag}.json"))
+        assert j["copy_engine"] == ("sdma" if flag == "sdma" else "blit"), flag
+        outs[flag] = _tree(str(d))
+    assert len(outs["auto"]) > 0 and outs["auto"] == outs["sdma"] == outs["blit"]
+    r = run_bin("img_processing_parallel", "--copy-engine", "dma", "--data-root", cohort_root, "--out", str(tmp_path / "x"))
+    assert r.returncode == 2
+
+
 def test_cli_parallel_dead_rank_fails_job(native, cohort_root, tmp_path):
     """A rank that dies mid-job (after the plan broadcast) fails the job promptly with its id."""
     import time
