@@ -25,7 +25,8 @@ int profile_variant(const char* kernel);
 // translation unit's code object at the first launch of one of its kernels; preloading makes that
 // happen on one thread before any launch (Engine and VolumeEngine constructors), never from a slot
 // thread in the middle of a run. Fails loudly (DeviceError) when a code object does not load.
-void preload_kernels();
+// with_volume = false leaves out k5 volume and k6 threshold, which the 2D engine never launches.
+void preload_kernels(bool with_volume = true);
 void preload_median();
 void preload_sharpen();
 void preload_srg();

@@ -491,7 +491,7 @@ EngineStartup::EngineStartup(int device, int nstreams, Comm* comm) {
       // The kernels' code objects (HIP would load each translation unit's at its first launch):
       // loaded here, on one thread, before any launch (kernels.h preload_kernels).
       const double t1 = now_s();
-      gpu::preload_kernels();
+      gpu::preload_kernels(/*with_volume=*/false);  // the 2D engine's code objects
       times_.kernel_load_s = now_s() - t1;
       // The engine's streams (HW queues) need only the slot count: created before the configuration
       // arrives, while rank 0 may still be planning.

@@ -899,13 +899,15 @@ void launch_jpeg(const uint8_t* canvas, const JpegDesc* jd, int ncanvas, int out
   check_launch("jpeg_fused_kernel");
 }
 
-void preload_kernels() {
+void preload_kernels(bool with_volume) {
   preload_median();
   preload_sharpen();
   preload_srg();
   preload_render();
-  preload_volume();
-  preload_threshold();
+  if (with_volume) {
+    preload_volume();
+    preload_threshold();
+  }
   hipFuncAttributes a;
   check_hip(hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&jpeg_fused_kernel<4, kUnionWords, kSampling420>)),
             "preload jpeg_fused_kernel");

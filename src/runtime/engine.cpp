@@ -323,8 +323,9 @@ struct Engine::Impl {
       check_hip(hipSetDevice(cfg.device), "hipSetDevice");
       // Every code object loaded here, on one thread, before any batch is launched: HIP otherwise
       // loads a module at the first launch of one of its kernels, from whichever slot thread gets
-      // there first (a no-op when the CLI's start-up thread already did it).
-      preload_kernels();
+      // there first (a no-op when the CLI's start-up thread already did it). The 2D engine never
+      // launches the volume or threshold kernels.
+      preload_kernels(/*with_volume=*/false);
       d_lut_ = dmalloc<float>(kLutArenaFloats, "hipMalloc norm tables");
     }
     const double t1 = now_s();
