@@ -1,12 +1,21 @@
 #!/bin/bash
 # (gpurun) HIP stream / HW-queue creation cost at start-up (tools/queue_probe.cpp), the cold CLI
-# with fewer HW queues, and hipInit by NUMA node (PART=numa|queues|all).
+# with fewer HW queues, hipInit by NUMA node, and the comgr pre-load (PART=numa|queues|comgr|all).
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
 O=gpurun_out/${1:-r5queues}
 mkdir -p "$O"
 R=$GRAFT_REPO_ROOT
+if [ "${PART:-all}" = comgr ]; then
+  # When does the HIP runtime map libamd_comgr, and does loading it on a second thread while
+  # hipInit runs shorten the start-up? Interleaved, 3 streams per run.
+  for r in $(seq 1 ${RUNS:-10}); do
+    echo "plain $(GPU_MAX_HW_QUEUES=2 timeout -k 5 60 build/bin/queue_probe 3 1)" >> $O/comgr_probe.txt || exit 8
+    echo "pre   $(GPU_MAX_HW_QUEUES=2 PROBE_PREDLOPEN=1 timeout -k 5 60 build/bin/queue_probe 3 1)" >> $O/comgr_probe.txt || exit 9
+  done
+  echo done; exit 0
+fi
 if [ "${PART:-all}" = numa ] || [ "${PART:-all}" = all ]; then
   # Is the cold hipInit bimodal by the NUMA node the initialising thread runs on? queue_probe
   # (hipInit + first allocation + 1 stream) pinned to each node's CPUs (taskset, before any HIP call)

@@ -8,10 +8,16 @@
 // (each thread creates streams/threads), then one 25-slice-sized pinned and device allocation.
 // Prints every phase in ms; run it under different GPU_MAX_HW_QUEUES values (HW queues are created
 // lazily, one per stream up to that count, and then shared round-robin).
+// PROBE_PREDLOPEN=1: a second thread dlopens libamd_comgr (the HIP runtime's code-object library,
+// ≈ 8 ms to load) at start, while the main thread runs hipInit; the probe also prints after which
+// phase the library is mapped.
 #include <hip/hip_runtime_api.h>
+
+#include <dlfcn.h>
 
 #include <chrono>
 #include <cstdio>
+#include <cstring>
 #include <cstdlib>
 #include <thread>
 #include <vector>
@@ -20,15 +26,36 @@ static double now_ms() {
   return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
+static bool comgr_mapped() {
+  FILE* f = std::fopen("/proc/self/maps", "r");
+  if (!f) return false;
+  char l[1024];
+  bool m = false;
+  while (!m && std::fgets(l, sizeof(l), f)) m = std::strstr(l, "libamd_comgr") != nullptr;
+  std::fclose(f);
+  return m;
+}
+
 int main(int argc, char** argv) {
   const int ns = argc > 1 ? std::atoi(argv[1]) : 5;
   const int nt = argc > 2 ? std::atoi(argv[2]) : 1;
   const char* q = std::getenv("GPU_MAX_HW_QUEUES");
-  double t0 = now_ms();
+  const bool pre = std::getenv("PROBE_PREDLOPEN") && std::atoi(std::getenv("PROBE_PREDLOPEN"));
+  double t0 = now_ms(), t_pre = 0;
+  std::thread pre_th;
+  if (pre)
+    pre_th = std::thread([&] {
+      const double a = now_ms();
+      (void)dlopen("libamd_comgr.so.3", RTLD_LAZY | RTLD_GLOBAL);
+      t_pre = now_ms() - a;
+    });
+  const bool mapped0 = comgr_mapped();
   if (hipInit(0) != hipSuccess || hipSetDevice(0) != hipSuccess) return 1;
   void* p = nullptr;
   (void)hipMalloc(&p, 4096);
   const double t1 = now_ms();
+  const bool mapped1 = comgr_mapped();
+  if (pre_th.joinable()) pre_th.join();
   std::vector<hipStream_t> st(ns, nullptr);
   std::vector<double> each(ns, 0);
   std::vector<std::thread> th;
@@ -55,6 +82,9 @@ int main(int argc, char** argv) {
   std::printf("GPU_MAX_HW_QUEUES=%s streams %d threads %d | init %.1f | streams %.1f (", q ? q : "(unset)", ns, nt, t1 - t0,
               t2 - t1);
   for (int i = 0; i < ns; ++i) std::printf("%s%.1f", i ? " " : "", each[i]);
-  std::printf(") | pinned 4MiB %.2f | device 16MiB %.2f | first memsets %.2f ms\n", t3 - t2, t4 - t3, t5 - t4);
+  std::printf(") | pinned 4MiB %.2f | device 16MiB %.2f | first memsets %.2f ms", t3 - t2, t4 - t3, t5 - t4);
+  std::printf(" | comgr mapped: start %d, after init %d, end %d%s", (int)mapped0, (int)mapped1, (int)comgr_mapped(),
+              pre ? "" : "\n");
+  if (pre) std::printf(" | predlopen %.1f ms\n", t_pre);
   return 0;
 }
