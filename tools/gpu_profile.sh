@@ -12,6 +12,8 @@ timeout -k 10 300 python bench.py --steps 5 --warmup 2 --keep-output > gpurun_ou
 echo "bench ok $(date)" >> $P
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_bench -o bench -- python3 bench.py --steps 3 --warmup 1 > gpurun_out/prof_bench.log 2>&1 || exit 22
 echo "rocprof ok $(date)" >> $P
+# the bench removes its own cohort at exit: the CPU reference and the CLIs get one of their own
+$B/nm03_synth --data-root /tmp/nm03_bench_data/ --threads 16 > /dev/null || exit 20
 timeout -k 10 400 $B/nm03_bench --config cpu-reference --data-root /tmp/nm03_bench_data/ --out /tmp/cpuref_out --steps 2 --warmup 1 --threads 16 --batch-size 25 > gpurun_out/cpu_reference.log 2>&1 || exit 23
 echo "cpuref ok $(date)" >> $P
 ( time $B/img_processing_parallel --data-root /tmp/nm03_bench_data/ --out /tmp/o_par --quiet --json gpurun_out/cli_parallel.json ) > gpurun_out/cli_parallel.log 2>&1 || exit 24
