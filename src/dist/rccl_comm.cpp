@@ -3,6 +3,7 @@
 // (ncclConfig_t.blocking = 0) so that initialisation, like every later wait, is a bounded poll:
 // a peer that died or never arrived ends in ncclCommAbort + CommError after NM03_COMM_TIMEOUT_S
 // (or at once when the launcher raised the job abort flag), never in a hang.
+#include <dlfcn.h>
 #include <hip/hip_runtime_api.h>
 #include <rccl/rccl.h>
 #include <unistd.h>
@@ -13,6 +14,7 @@
 #include <exception>
 #include <mutex>
 #include <thread>
+#include <type_traits>
 
 #include "nm03/comm.h"
 
@@ -28,6 +30,71 @@ void hip_ck(hipError_t e, const char* what) {
   if (e != hipSuccess) throw CommError(std::string(what) + ": " + hipGetErrorString(e));
 }
 
+// RCCL's entry points, resolved from librccl when the first communicator needs them. Linking
+// librccl (573 MB, with its device code registered with the HIP runtime by its static
+// constructors) put ≈ 3 ms into every process's start-up before main, single-rank runs included;
+// loaded here it costs a multi-rank job nothing on the critical path (the deferred communicator
+// starts RCCL on the start-up thread while the ranks process).
+struct RcclApi {
+#define NM03_RCCL_FN(name) decltype(&::name) name = nullptr;
+  NM03_RCCL_FN(ncclGetUniqueId)
+  NM03_RCCL_FN(ncclCommInitRankConfig)
+  NM03_RCCL_FN(ncclGetErrorString)
+  NM03_RCCL_FN(ncclBroadcast)
+  NM03_RCCL_FN(ncclAllGather)
+  NM03_RCCL_FN(ncclAllReduce)
+  NM03_RCCL_FN(ncclSend)
+  NM03_RCCL_FN(ncclRecv)
+  NM03_RCCL_FN(ncclGroupStart)
+  NM03_RCCL_FN(ncclGroupEnd)
+  NM03_RCCL_FN(ncclCommCount)
+  NM03_RCCL_FN(ncclCommUserRank)
+  NM03_RCCL_FN(ncclCommCuDevice)
+  NM03_RCCL_FN(ncclCommGetAsyncError)
+  NM03_RCCL_FN(ncclCommAbort)
+  NM03_RCCL_FN(ncclCommDestroy)
+#undef NM03_RCCL_FN
+  std::string error;  // why the library or a symbol could not be loaded (empty: usable)
+};
+
+const RcclApi& rccl_api() {
+  static const RcclApi api = [] {
+    RcclApi a;
+    void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+    if (!h) h = dlopen(ROCM_LIB_DIR "/librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+    if (!h) {
+      const char* e = dlerror();
+      a.error = std::string("cannot load librccl.so.1: ") + (e ? e : "unknown error");
+      return a;
+    }
+    auto sym = [&](auto& fn, const char* name) {
+      fn = reinterpret_cast<std::remove_reference_t<decltype(fn)>>(dlsym(h, name));
+      if (!fn && a.error.empty()) a.error = std::string("librccl.so.1 lacks ") + name;
+    };
+#define NM03_RCCL_SYM(name) sym(a.name, #name);
+    NM03_RCCL_SYM(ncclGetUniqueId)
+    NM03_RCCL_SYM(ncclCommInitRankConfig)
+    NM03_RCCL_SYM(ncclGetErrorString)
+    NM03_RCCL_SYM(ncclBroadcast)
+    NM03_RCCL_SYM(ncclAllGather)
+    NM03_RCCL_SYM(ncclAllReduce)
+    NM03_RCCL_SYM(ncclSend)
+    NM03_RCCL_SYM(ncclRecv)
+    NM03_RCCL_SYM(ncclGroupStart)
+    NM03_RCCL_SYM(ncclGroupEnd)
+    NM03_RCCL_SYM(ncclCommCount)
+    NM03_RCCL_SYM(ncclCommUserRank)
+    NM03_RCCL_SYM(ncclCommCuDevice)
+    NM03_RCCL_SYM(ncclCommGetAsyncError)
+    NM03_RCCL_SYM(ncclCommAbort)
+    NM03_RCCL_SYM(ncclCommDestroy)
+#undef NM03_RCCL_SYM
+    return a;
+  }();
+  if (!api.error.empty()) throw CommError(api.error);
+  return api;
+}
+
 class RcclComm final : public Comm {
  public:
   RcclComm(int rank, int size, const std::vector<uint8_t>& uid, int device, std::shared_ptr<ShmSegment> seg,
@@ -41,10 +108,10 @@ class RcclComm final : public Comm {
     hip_ck(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "hipStreamCreate");
     ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
     cfg.blocking = 0;
-    ncclResult_t r = ncclCommInitRankConfig(&comm_, size_, id, rank_, &cfg);
+    ncclResult_t r = rccl_api().ncclCommInitRankConfig(&comm_, size_, id, rank_, &cfg);
     if (r != ncclSuccess && r != ncclInProgress) {
       release();
-      throw CommError(std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+      throw CommError(std::string("ncclCommInitRank: ") + rccl_api().ncclGetErrorString(r));
     }
     if (!settle_now) return;
     try {
@@ -69,7 +136,7 @@ class RcclComm final : public Comm {
     if (!bytes) return;
     uint8_t* d = stage(bytes);
     if (rank_ == root) hip_ck(hipMemcpyAsync(d, buf, bytes, hipMemcpyHostToDevice, stream_), "H2D");
-    issue(ncclBroadcast(d, d, bytes, ncclUint8, root, comm_, stream_), "ncclBroadcast");
+    issue(rccl_api().ncclBroadcast(d, d, bytes, ncclUint8, root, comm_, stream_), "ncclBroadcast");
     hip_ck(hipMemcpyAsync(buf, d, bytes, hipMemcpyDeviceToHost, stream_), "D2H");
     wait("ncclBroadcast");
   }
@@ -78,7 +145,7 @@ class RcclComm final : public Comm {
     uint8_t* d = stage(bytes * (size_t)(size_ + 1));
     uint8_t* dsend = d + bytes * (size_t)size_;
     hip_ck(hipMemcpyAsync(dsend, send, bytes, hipMemcpyHostToDevice, stream_), "H2D");
-    issue(ncclAllGather(dsend, d, bytes, ncclUint8, comm_, stream_), "ncclAllGather");
+    issue(rccl_api().ncclAllGather(dsend, d, bytes, ncclUint8, comm_, stream_), "ncclAllGather");
     hip_ck(hipMemcpyAsync(recv, d, bytes * size_, hipMemcpyDeviceToHost, stream_), "D2H");
     wait("ncclAllGather");
   }
@@ -97,10 +164,10 @@ class RcclComm final : public Comm {
     if (sbytes) hip_ck(hipMemcpyAsync(d, send, sbytes, hipMemcpyHostToDevice, stream_), "H2D");
     // One group: the send to the successor and the receive from the predecessor progress
     // together (a halo exchange where every rank sends first would otherwise deadlock).
-    issue(ncclGroupStart(), "ncclGroupStart");
-    if (sbytes) issue(ncclSend(d, sbytes, ncclUint8, dst, comm_, stream_), "ncclSend");
-    if (rbytes) issue(ncclRecv(drecv, rbytes, ncclUint8, src, comm_, stream_), "ncclRecv");
-    issue(ncclGroupEnd(), "ncclGroupEnd");
+    issue(rccl_api().ncclGroupStart(), "ncclGroupStart");
+    if (sbytes) issue(rccl_api().ncclSend(d, sbytes, ncclUint8, dst, comm_, stream_), "ncclSend");
+    if (rbytes) issue(rccl_api().ncclRecv(drecv, rbytes, ncclUint8, src, comm_, stream_), "ncclRecv");
+    issue(rccl_api().ncclGroupEnd(), "ncclGroupEnd");
     if (rbytes) hip_ck(hipMemcpyAsync(recv, drecv, rbytes, hipMemcpyDeviceToHost, stream_), "D2H");
     wait("ncclSend/ncclRecv");
   }
@@ -115,10 +182,10 @@ class RcclComm final : public Comm {
     if (!comm_) throw CommError("RCCL communicator was aborted");
     if (seg_) seg_->check_abort(rank_);
     auto st = static_cast<hipStream_t>(stream);
-    issue(ncclGroupStart(), "ncclGroupStart");
-    if (sbytes) issue(ncclSend(send, sbytes, ncclUint8, dst, comm_, st), "ncclSend");
-    if (rbytes) issue(ncclRecv(recv, rbytes, ncclUint8, src, comm_, st), "ncclRecv");
-    issue(ncclGroupEnd(), "ncclGroupEnd");
+    issue(rccl_api().ncclGroupStart(), "ncclGroupStart");
+    if (sbytes) issue(rccl_api().ncclSend(send, sbytes, ncclUint8, dst, comm_, st), "ncclSend");
+    if (rbytes) issue(rccl_api().ncclRecv(recv, rbytes, ncclUint8, src, comm_, st), "ncclRecv");
+    issue(rccl_api().ncclGroupEnd(), "ncclGroupEnd");
   }
   int64_t allreduce_sum_i64_device(int64_t* v, void* stream) override {
     ready();
@@ -126,7 +193,7 @@ class RcclComm final : public Comm {
     if (seg_) seg_->check_abort(rank_);
     auto st = static_cast<hipStream_t>(stream);
     if (!h_word_) hip_ck(hipHostMalloc((void**)&h_word_, 8, hipHostMallocDefault), "hipHostMalloc");
-    issue(ncclAllReduce(v, v, 1, ncclInt64, ncclSum, comm_, st), "ncclAllReduce");
+    issue(rccl_api().ncclAllReduce(v, v, 1, ncclInt64, ncclSum, comm_, st), "ncclAllReduce");
     hip_ck(hipMemcpyAsync(h_word_, v, 8, hipMemcpyDeviceToHost, st), "D2H");
     wait("ncclAllReduce (device)", st);
     return *h_word_;
@@ -135,19 +202,19 @@ class RcclComm final : public Comm {
   int transport_size() const override {
     if (!settled_) return -1;
     int n = -1;
-    if (!comm_ || ncclCommCount(comm_, &n) != ncclSuccess) return -1;
+    if (!comm_ || rccl_api().ncclCommCount(comm_, &n) != ncclSuccess) return -1;
     return n;
   }
   int transport_rank() const override {
     if (!settled_) return -1;
     int r = -1;
-    if (!comm_ || ncclCommUserRank(comm_, &r) != ncclSuccess) return -1;
+    if (!comm_ || rccl_api().ncclCommUserRank(comm_, &r) != ncclSuccess) return -1;
     return r;
   }
   int transport_device() const override {
     if (!settled_) return -1;
     int d = -1;
-    if (!comm_ || ncclCommCuDevice(comm_, &d) != ncclSuccess) return -1;
+    if (!comm_ || rccl_api().ncclCommCuDevice(comm_, &d) != ncclSuccess) return -1;
     return d;
   }
   void set_abort_segment(std::shared_ptr<ShmSegment> seg) override { seg_ = std::move(seg); }
@@ -158,7 +225,7 @@ class RcclComm final : public Comm {
     const size_t bytes = n * 8;
     uint8_t* d = stage(bytes);
     hip_ck(hipMemcpyAsync(d, v, bytes, hipMemcpyHostToDevice, stream_), "H2D");
-    issue(ncclAllReduce(d, d, n, t, op, comm_, stream_), "ncclAllReduce");
+    issue(rccl_api().ncclAllReduce(d, d, n, t, op, comm_, stream_), "ncclAllReduce");
     hip_ck(hipMemcpyAsync(v, d, bytes, hipMemcpyDeviceToHost, stream_), "D2H");
     wait("ncclAllReduce");
   }
@@ -177,17 +244,17 @@ class RcclComm final : public Comm {
   // A non-blocking communicator may return ncclInProgress from an enqueue: poll until settled.
   void issue(ncclResult_t r, const char* what) {
     if (r == ncclSuccess) return;
-    if (r != ncclInProgress) fail(std::string(what) + ": " + ncclGetErrorString(r));
+    if (r != ncclInProgress) fail(std::string(what) + ": " + rccl_api().ncclGetErrorString(r));
     settle(what);
   }
   void settle(const char* what) {
     const double deadline = mono_s() + timeout_;
     for (;;) {
       ncclResult_t ar = ncclSuccess;
-      const ncclResult_t q = ncclCommGetAsyncError(comm_, &ar);
-      if (q != ncclSuccess) fail(std::string(what) + ": ncclCommGetAsyncError: " + ncclGetErrorString(q));
+      const ncclResult_t q = rccl_api().ncclCommGetAsyncError(comm_, &ar);
+      if (q != ncclSuccess) fail(std::string(what) + ": ncclCommGetAsyncError: " + rccl_api().ncclGetErrorString(q));
       if (ar == ncclSuccess) return;
-      if (ar != ncclInProgress) fail(std::string(what) + ": " + ncclGetErrorString(ar));
+      if (ar != ncclInProgress) fail(std::string(what) + ": " + rccl_api().ncclGetErrorString(ar));
       poll_guards(what, deadline);
     }
   }
@@ -198,8 +265,8 @@ class RcclComm final : public Comm {
       if (q == hipSuccess) return;
       if (q != hipErrorNotReady) fail(std::string(what) + ": " + hipGetErrorString(q));
       ncclResult_t ar = ncclSuccess;
-      if (ncclCommGetAsyncError(comm_, &ar) != ncclSuccess || (ar != ncclSuccess && ar != ncclInProgress))
-        fail(std::string(what) + ": RCCL async error: " + ncclGetErrorString(ar));
+      if (rccl_api().ncclCommGetAsyncError(comm_, &ar) != ncclSuccess || (ar != ncclSuccess && ar != ncclInProgress))
+        fail(std::string(what) + ": RCCL async error: " + rccl_api().ncclGetErrorString(ar));
       poll_guards(what, deadline);
     }
   }
@@ -217,7 +284,7 @@ class RcclComm final : public Comm {
   }
   [[noreturn]] void fail(const std::string& msg) {
     if (comm_) {
-      (void)ncclCommAbort(comm_);
+      (void)rccl_api().ncclCommAbort(comm_);
       comm_ = nullptr;
     }
     throw CommError(msg);
@@ -225,7 +292,7 @@ class RcclComm final : public Comm {
   void release() {
     if (comm_) {
       // A healthy communicator is destroyed; an aborted one was already released by fail().
-      (void)ncclCommDestroy(comm_);
+      (void)rccl_api().ncclCommDestroy(comm_);
       comm_ = nullptr;
     }
     if (buf_) (void)hipFree(buf_);
@@ -402,8 +469,8 @@ std::unique_ptr<Comm> make_deferred_rccl_comm(int rank, int size, int device, st
 
 std::vector<uint8_t> rccl_unique_id() {
   ncclUniqueId id;
-  const ncclResult_t r = ncclGetUniqueId(&id);
-  if (r != ncclSuccess) throw CommError(std::string("ncclGetUniqueId: ") + ncclGetErrorString(r));
+  const ncclResult_t r = rccl_api().ncclGetUniqueId(&id);
+  if (r != ncclSuccess) throw CommError(std::string("ncclGetUniqueId: ") + rccl_api().ncclGetErrorString(r));
   std::vector<uint8_t> v(sizeof(id));
   std::memcpy(v.data(), &id, sizeof(id));
   return v;
