@@ -49,6 +49,38 @@ def test_vector_median_equals_median_on_quantised_data(native, img, k):
     assert np.array_equal(native.golden_vector_median(c, k), native.golden_median(c, k))
 
 
+def _disc(size, dims=2):
+    r = size // 2
+    g = np.indices((2 * r + 1,) * dims) - r
+    return (g * g).sum(axis=0) <= r * r
+
+
+@SETTINGS
+@given(m=masks(), size=st.sampled_from([1, 3, 5, 7, 9]))
+def test_disc_morphology_equals_scipy(native, m, size):
+    """--se-shape disc: digital disc of radius size/2 (|d|² ≤ r²), out-of-image samples ignored;
+    dilation and erosion are duals through the complement with that border convention."""
+    se = _disc(size)
+    dil = scipy_ndimage.binary_dilation(m.astype(bool), structure=se)
+    ero = scipy_ndimage.binary_erosion(m.astype(bool), structure=se, border_value=1)
+    gd = native.golden_morph(m, size, True, True).astype(bool)
+    ge = native.golden_morph(m, size, False, True).astype(bool)
+    assert np.array_equal(gd, dil) and np.array_equal(ge, ero)
+    assert np.array_equal(ge, ~native.golden_morph((1 - m).astype(np.uint8), size, True, True).astype(bool))
+    assert (gd >= m.astype(bool)).all() and (ge <= m.astype(bool)).all()  # extensive / anti-extensive
+
+
+@settings(max_examples=15, deadline=None, suppress_health_check=[HealthCheck.function_scoped_fixture])
+@given(seed=st.integers(0, 2**31 - 1), size=st.sampled_from([3, 5, 7]), density=st.floats(0.01, 0.2))
+def test_ball_dilation_equals_scipy(native, seed, size, density):
+    """--mode 3d --se-shape disc: the digital ball of radius size/2."""
+    m = (np.random.default_rng(seed).random((9, 14, 11)) < density).astype(np.uint8)
+    ref = scipy_ndimage.binary_dilation(m.astype(bool), structure=_disc(size, 3))
+    assert np.array_equal(native.golden_dilate3d(m, size, True).astype(bool), ref)
+    cube = scipy_ndimage.binary_dilation(m.astype(bool), structure=np.ones((size,) * 3, bool))
+    assert np.array_equal(native.golden_dilate3d(m, size, False).astype(bool), cube)
+
+
 @SETTINGS
 @given(m=masks(), size=st.sampled_from([1, 3, 5, 7]))
 def test_morphology_equals_scipy(native, m, size):
