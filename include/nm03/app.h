@@ -83,7 +83,8 @@ struct AppConfig {
 };
 
 enum CopyEngine : int { kCopyAuto = 0, kCopySdma = 1, kCopyBlit = 2 };
-// kCopyAuto picks blit copies up to this many slices per rank: a process's first DMA copy costs
+// kCopyAuto picks blit copies up to this many slices per rank (all --repeat passes counted): a
+// process's first DMA copy costs
 // ≈ 9 ms (the copy engine's queue), shader copies ≈ 0.7 µs more per 256² slice than DMA.
 constexpr int kBlitMaxSlicesPerRank = 4096;
 

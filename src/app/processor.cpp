@@ -239,7 +239,8 @@ AppConfig parse_args(int argc, char** argv, const std::string& which) {
 // =============================================================================================
 int run_sequential(const AppConfig& cfg) {
   try {
-    apply_copy_engine(cfg, cfg.copy_engine == kCopyAuto ? count_cohort_slices(cfg) : -1);
+    const int64_t cohort_slices = cfg.copy_engine == kCopyAuto ? count_cohort_slices(cfg) : -1;
+    apply_copy_engine(cfg, cohort_slices < 0 ? -1 : cohort_slices * std::max(1, cfg.repeat));
     // HIP start-up and the engine's construction on the start-up thread while the output root is set up.
     EngineStartup su(cfg.engine.device, std::max(1, cfg.engine.streams) + 1);
     // SequentialImageProcessor ctor: base output dir (main_sequential.cpp:81-91).
@@ -933,7 +934,7 @@ int run_parallel(const AppConfig& cfg) {
     // auto: size the job to the cohort, counted from its directory listings before any fork
     const int64_t slices = cfg.gpus == kGpusAuto || cfg.copy_engine == kCopyAuto ? count_cohort_slices(cfg) : -1;
     const int n = resolve_gpus(cfg, lo, cfg.gpus == kGpusAuto ? slices : -1);
-    apply_copy_engine(cfg, slices < 0 ? -1 : (slices + n - 1) / n);
+    apply_copy_engine(cfg, slices < 0 ? -1 : (slices + n - 1) / n * std::max(1, cfg.repeat));
     std::vector<int> rank_devices;
     for (int r = 0; r < n; ++r)
       rank_devices.push_back(n > 1 ? lo.device_of(r) : lo.device_override >= 0 ? lo.device_override : cfg.engine.device);
