@@ -282,13 +282,10 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(kOcc)))
   // ---- 0. stage the source rows of this workgroup in LDS (workgroup-uniform decision) ----------
   int ys0 = 0, pcols = 0;
   bool staged = false, lstaged = false;
-  // Flat label workgroup: every source pixel under the workgroup's blocks is background (label 0,
-  // no border) or inside the region (label 1, no border), so every block renders to one grey level
-  // and codes to DC diff 0 + EOB (and the MCU's chroma to 4 × "00"): 32 bits per MCU,
-  // 0x28A28A00, with only block 0's DC difference (to the previous workgroup) free. The workgroup
-  // then skips the render, the per-block coding and the scan, and fills its bit range as words.
-  bool wgflat = false;
-  int flat_v = 0;
+  // (A flat-label-workgroup shortcut — a workgroup whose label rows were all background or all
+  // region filled its bit range with the repeating MCU pattern instead of coding — was removed in
+  // round 5: its extra live state gave the kernel a 36-byte private segment, and the kernel without
+  // it measured 105.2–105.8 vs 106.8–107.2 µs per 96-slice batch, profiles/r5/jpeg_flat/.)
   uint64_t* const slab = reinterpret_cast<uint64_t*>(spatch);  // label images reuse the area
   if (d.render >= 0 && rd.kind == kRenderLabels) {
     // Label render rows: 4by .. 4by+3 for the workgroup's block rows → 8 per MCU row (4:2:0).
@@ -299,24 +296,14 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(kOcc)))
       lstaged = true;
       ys0 = (kUnitRows / 2) * r0;
       pcols = nw;  // offset of the border plane
-      const int wrem = rd.src_w & 63;
       const Div16 dw((uint32_t)wpr);
-      int nonzero = 0, nonfill = 0;
       for (int i = tid; i < nw; i += kWG) {
         const int j = (int)dw.q((uint32_t)i), k = i - j * wpr;
         const size_t wi = (size_t)clampi(ys0 + j, 0, rd.src_h - 1) * wpr + k;
-        const uint64_t lab = rs.bits[rd.src_off + wi], brd = rs.bits[rd.border_off + wi];
-        slab[i] = lab;
-        slab[nw + i] = brd;
-        const uint64_t m = (k == wpr - 1 && wrem) ? (1ull << wrem) - 1ull : ~0ull;
-        nonzero |= ((lab | brd) & m) != 0;
-        nonfill |= ((~lab | brd) & m) != 0;
+        slab[i] = rs.bits[rd.src_off + wi];
+        slab[nw + i] = rs.bits[rd.border_off + wi];
       }
-      const bool full = (part + 1) * kWG <= bpi && (dbg == 0 || dbg >= 40);
-      const bool zero = __syncthreads_or(nonzero) == 0;
-      const bool fill = __syncthreads_or(nonfill) == 0;
-      wgflat = k420 && full && (zero || fill);  // the word pattern below is the 4:2:0 MCU's
-      flat_v = zero ? 0 : (int)rd.fill;
+      __syncthreads();
     }
   }
   if (d.render >= 0 && rd.kind == kRenderRawGray) {
@@ -397,9 +384,7 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(kOcc)))
   uint32_t* const pspill = w.spill + ((size_t)blockIdx.x * kWG + tid) * kSpillWords;
   int dc0 = 0;
   uint32_t acbits = 0;
-  if (wgflat) {
-    dc0 = quant_recip(64 * (flat_v - 128), q, 0);
-  } else if (valid) {
+  if (valid) {
     int bx, by;
     block_xy(b, bx, by);
     int32_t blk[64];
@@ -550,58 +535,34 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(kOcc)))
   __syncthreads();
   uint32_t agg = 0, nlocal = 0;
   bool in_lds = true;
-  if (wgflat) {
-    // Block 0: its DC code (L0 bits) + EOB; then the periodic MCU pattern from its 7th bit on.
-    const int diff0 = dc0 - s_prevdc;
-    const int dn0 = mag_bits_fast(diff0);
-    const uint32_t dce0 = dctab[dn0];
-    const uint32_t L0 = (dce0 >> 16) + (uint32_t)dn0;
-    const uint32_t code0 =
-        ((dce0 & 0xFFFFu) << dn0) | ((uint32_t)(diff0 < 0 ? diff0 - 1 : diff0) & ((1u << dn0) - 1u));
-    constexpr uint32_t kMcu = 0x28A28A00u;  // (00 1010) × 4 luma blocks + 4 × 00 chroma, MSB first
-    agg = L0 + 4u + (uint32_t)(kWG - 1) * 6u + (uint32_t)(kWG / 4) * 8u;
-    nlocal = (agg + 31u) >> 5;
-    // Range bit k ≥ L0 + 4 is pattern bit (k − (L0 − 2)) mod 32: every word is the pattern rotated
-    // left by (2 − L0) mod 32; word 0 starts with block 0's codes.
-    const uint32_t rot = (34u - L0) & 31u;
-    const uint32_t pat = rot ? (kMcu << rot) | (kMcu >> (32u - rot)) : kMcu;
-    const uint32_t hl = L0 + 4u;  // ≤ 24 bits
-    for (uint32_t i = tid; i <= nlocal + 1u; i += kWG) {
-      uint32_t v = i < nlocal ? pat : 0u;
-      if (i == 0) v = (((code0 << 4) | 0xAu) << (32u - hl)) | (pat & ((1u << (32u - hl)) - 1u));
-      if (i == nlocal - 1u && (agg & 31u)) v &= ~0u << (32u - (agg & 31u));
-      swg[i] = v;
-    }
-  } else {
-    // DC code (Huffman symbol + magnitude bits, ≤ 20 bits, right-aligned).
-    const int diff = dc0 - (tid ? sdc[tid - 1] : s_prevdc);
-    const int dn = mag_bits_fast(diff);
-    const uint32_t dce = dctab[dn];
-    const int dclen = valid ? (int)(dce >> 16) + dn : 0;
-    const uint32_t dccode = ((dce & 0xFFFFu) << dn) | ((uint32_t)(diff < 0 ? diff - 1 : diff) & ((1u << dn) - 1u));
-    const uint32_t bits = valid ? (uint32_t)dclen + acbits : 0u;
-    // ---- 3. workgroup scan, bit range assembled in LDS ----------------------------------------
-    const uint32_t excl = block_exclusive_scan(bits, sh, &agg);  // ends with a barrier
-    // Each block's DC code, then its AC words shifted behind it, into the workgroup's contiguous
-    // bit range (MSB-first words), in the LDS region the render patch used. A range too long for
-    // it (> ~220 Kbit: pathological detail) poisons the image, which the host then re-encodes.
-    nlocal = (agg + 31) >> 5;
-    in_lds = nlocal + 2u <= (uint32_t)kUnion;  // workgroup-uniform
-    const uint32_t nwp = (acbits + 31) >> 5;
-    const uint32_t acpos = excl + (uint32_t)dclen;
-    if (in_lds) {
-      for (uint32_t i = tid; i <= nlocal; i += kWG) swg[i] = 0u;
-      __syncthreads();
-      if (valid) {
-        const uint32_t dv = dclen ? dccode << (32 - dclen) : 0u, sh0 = excl & 31u, w0 = excl >> 5;
-        atomicOr(&swg[w0], dv >> sh0);
-        if (sh0) atomicOr(&swg[w0 + 1], dv << (32u - sh0));
-        const uint32_t shf = acpos & 31u, wa = acpos >> 5;
-        for (uint32_t i = 0; i < nwp; ++i) {
-          const uint32_t v = priv_word(pbuf, pspill, i);
-          atomicOr(&swg[wa + i], v >> shf);
-          if (shf) atomicOr(&swg[wa + i + 1], v << (32u - shf));
-        }
+  // DC code (Huffman symbol + magnitude bits, ≤ 20 bits, right-aligned).
+  const int diff = dc0 - (tid ? sdc[tid - 1] : s_prevdc);
+  const int dn = mag_bits_fast(diff);
+  const uint32_t dce = dctab[dn];
+  const int dclen = valid ? (int)(dce >> 16) + dn : 0;
+  const uint32_t dccode = ((dce & 0xFFFFu) << dn) | ((uint32_t)(diff < 0 ? diff - 1 : diff) & ((1u << dn) - 1u));
+  const uint32_t bits = valid ? (uint32_t)dclen + acbits : 0u;
+  // ---- 3. workgroup scan, bit range assembled in LDS ----------------------------------------
+  const uint32_t excl = block_exclusive_scan(bits, sh, &agg);  // ends with a barrier
+  // Each block's DC code, then its AC words shifted behind it, into the workgroup's contiguous
+  // bit range (MSB-first words), in the LDS region the render patch used. A range too long for
+  // it (> ~220 Kbit: pathological detail) poisons the image, which the host then re-encodes.
+  nlocal = (agg + 31) >> 5;
+  in_lds = nlocal + 2u <= (uint32_t)kUnion;  // workgroup-uniform
+  const uint32_t nwp = (acbits + 31) >> 5;
+  const uint32_t acpos = excl + (uint32_t)dclen;
+  if (in_lds) {
+    for (uint32_t i = tid; i <= nlocal; i += kWG) swg[i] = 0u;
+    __syncthreads();
+    if (valid) {
+      const uint32_t dv = dclen ? dccode << (32 - dclen) : 0u, sh0 = excl & 31u, w0 = excl >> 5;
+      atomicOr(&swg[w0], dv >> sh0);
+      if (sh0) atomicOr(&swg[w0 + 1], dv << (32u - sh0));
+      const uint32_t shf = acpos & 31u, wa = acpos >> 5;
+      for (uint32_t i = 0; i < nwp; ++i) {
+        const uint32_t v = priv_word(pbuf, pspill, i);
+        atomicOr(&swg[wa + i], v >> shf);
+        if (shf) atomicOr(&swg[wa + i + 1], v << (32u - shf));
       }
     }
   }
