@@ -567,7 +567,13 @@ int parallel_rank(const AppConfig& cfg, int rank, int size, Comm& comm, int devi
   // Nothing else touches HIP before the first batch: in round 4, slots built on their workers held
   // the runtime's locks (HW-queue creation 10–50 ms) while the first batch tried to copy and
   // launch, and a cold 465-slice pass took 37–70 ms instead of ≈ 4 ms (profiles/r5/cold/).
-  EngineStartup su(device, std::max(1, cfg.engine.streams) + 1, &comm);  // slots + the shared upload stream
+  // A 2D job's collectives are control data (the work list, counts, timing rows: a few KB in all),
+  // which the node's shared-memory control plane carries; RCCL (loaded and initialised per rank,
+  // 0.3–2 s on a node, longer than the job's processing) is brought up only when asked for
+  // (NM03_COMM=rccl) — device data exchange (--split-volume) brings it up by itself.
+  const char* comm_env = std::getenv("NM03_COMM");
+  const bool data_plane = size > 1 && comm_env && std::string(comm_env) == "rccl";
+  EngineStartup su(device, std::max(1, cfg.engine.streams) + 1, data_plane ? &comm : nullptr);  // slots + upload stream
   double engine_wait_s = 0;
   std::unique_ptr<Engine> engine_p;
   std::vector<RankDevice> devices;
@@ -710,9 +716,9 @@ int parallel_rank(const AppConfig& cfg, int rank, int size, Comm& comm, int devi
     my_wall += now_s() - t0;  // this rank's own processing time (before waiting for the others)
     comm.barrier();
     double wall = now_s() - t0;
-    // RCCL (initialising since the start-up thread's hipInit) carries every collective from here
-    // on: the processing-time reduction, the status and metric all-gathers (N = 1: no-op).
-    comm.promote();
+    // With NM03_COMM=rccl, RCCL (initialising since the start-up thread's hipInit) carries every
+    // collective from here on: the processing-time reduction, the status and metric all-gathers.
+    if (data_plane) comm.promote();
     comm.allreduce_max_f64(&wall, 1);
     proc_wall += wall;
     agg.load_s += t.load_s;
@@ -816,7 +822,8 @@ int parallel_rank(const AppConfig& cfg, int rank, int size, Comm& comm, int devi
     write_json(cfg.json, std::string("{\"mode\": \"parallel\", \"gpus\": ") + std::to_string(size) +
                              ", \"gpus_requested\": " + req + ", \"main_unix_s\": " +
                              fmt(cfg.main_unix_s, 17) + ", \"backend\": \"" +
-                             comm.backend() + "\", \"copy_engine\": \"" + copy_engine_name() + "\", \"repeat\": " +
+                             std::string(data_plane || size == 1 ? comm.backend() : "host") + "\", \"copy_engine\": \"" +
+                             copy_engine_name() + "\", \"repeat\": " +
                              std::to_string(cfg.repeat) + ", \"engine_setup_s\": " +
                              fmt(setup_s) + ", \"hip_init_s\": " + fmt(su.times().hip_init_s) + ", \"engine_ctor_s\": " +
                              fmt(su.times().engine_ctor_s) + ", \"streams_s\": " + fmt(su.times().streams_s) + ", \"engine_wait_s\": " + fmt(engine_wait_s) + ", \"kernel_load_s\": " +
@@ -828,7 +835,8 @@ int parallel_rank(const AppConfig& cfg, int rank, int size, Comm& comm, int devi
                              ", \"h2d_s\": " + fmt(agg.h2d_s) + ", \"kernels_s\": " + fmt(agg.kernels_s) +
                              ", \"write_s\": " + fmt(agg.write_s) + ", \"jpeg_fallbacks\": " +
                              std::to_string(agg.jpeg_fallbacks) + "}, \"per_rank\": " + per_rank_json(rows) +
-                             ", \"comm\": {\"backend\": \"" + comm.backend() + "\", \"nranks\": " +
+                             ", \"comm\": {\"backend\": \"" + std::string(data_plane || size == 1 ? comm.backend() : "host") +
+                             "\", \"nranks\": " +
                              std::to_string(comm.transport_size()) +
                              (comm.fallback_error().empty() ? std::string() : ", \"rccl_error\": \"" + json_escape(comm.fallback_error()) + "\"") +
                              "}, \"devices\": " + rank_devices_json(devices) + "}");
