@@ -723,6 +723,35 @@ TEST(cli_defaults_are_reference_literals) {
   CHECK(c.out_dir.find("out-parallel") != std::string::npos);
 }
 
+TEST(copy_engine_policy) {
+  // --copy-engine auto: shader copies for 2D jobs up to kBlitMaxSlicesPerRank slices per rank (all
+  // --repeat passes counted by the caller), unless HSA_ENABLE_SDMA is already set; sdma never
+  // touches the environment; blit always sets it; volumes keep the DMA engines under auto.
+  using namespace nm03::app;
+  const char* saved = std::getenv("HSA_ENABLE_SDMA");
+  const std::string keep = saved ? saved : "";
+  AppConfig c;
+  unsetenv("HSA_ENABLE_SDMA");
+  CHECK(apply_copy_engine(c, 465) && std::string(copy_engine_name()) == "blit");
+  unsetenv("HSA_ENABLE_SDMA");
+  CHECK(!apply_copy_engine(c, kBlitMaxSlicesPerRank + 1) && std::string(copy_engine_name()) == "sdma");
+  CHECK(!apply_copy_engine(c, -1));  // unknown size: leave the DMA engines
+  setenv("HSA_ENABLE_SDMA", "1", 1);
+  CHECK(!apply_copy_engine(c, 10));  // the user's setting wins
+  unsetenv("HSA_ENABLE_SDMA");
+  c.mode = "3d";
+  CHECK(!apply_copy_engine(c, 10));
+  c.mode = "2d";
+  c.copy_engine = kCopySdma;
+  CHECK(!apply_copy_engine(c, 10) && std::getenv("HSA_ENABLE_SDMA") == nullptr);
+  c.copy_engine = kCopyBlit;
+  CHECK(apply_copy_engine(c, 1 << 20) && std::string(copy_engine_name()) == "blit");
+  if (saved)
+    setenv("HSA_ENABLE_SDMA", keep.c_str(), 1);
+  else
+    unsetenv("HSA_ENABLE_SDMA");
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
