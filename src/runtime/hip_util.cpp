@@ -48,6 +48,9 @@ void check_launch(const char* what) {
 }
 
 void warm_copy_path(hipStream_t stream) {
+  // Shader copies (HSA_ENABLE_SDMA=0, the CLI's --copy-engine for short jobs) run on the compute
+  // queues with the blit kernels the runtime loaded with the first stream: nothing to bring up.
+  if (const char* e = std::getenv("HSA_ENABLE_SDMA"); e && std::string(e) == "0") return;
   // Large enough for the copy engine (SDMA) path the engine's uploads take: a 4 KiB copy is done
   // another way and left the first batch's upload paying ≈ 7.5 ms (profiles/r5/cold/).
   constexpr size_t kBytes = size_t(4) << 20;
