@@ -59,6 +59,7 @@ struct AppConfig {
   bool quiet = false;
   bool cpu = false;        // test_pipeline: golden CPU path (BASELINE config 1)
   bool montage = true;     // test_pipeline: 5-view montage JPEG (headless MultiViewWindow)
+  bool html = false;       // test_pipeline --html: the five views as a page (MultiViewWindow 2300×450)
   std::string json;        // metrics file
   std::string mode = "2d"; // 2d | 3d
   std::string input;       // test_pipeline: explicit slice path

@@ -61,6 +61,7 @@ void usage(const std::string& which) {
             << "  --input FILE           test_pipeline: slice to process\n"
             << "  --cpu                  test_pipeline / --mode 3d: golden CPU model instead of the GPU\n"
             << "  --no-montage           test_pipeline: skip the 5-view montage JPEG\n"
+            << "  --html                 test_pipeline: also write multi_view.html, the five views in a 2300x450 window\n"
             << "  --dump-mhd DIR         test_pipeline: write stage arrays as MetaImage (.mhd/.raw)\n"
             << "  --repeat N             process the cohort N times (benchmarking)\n"
             << "  --json FILE            write run metrics as JSON\n"
@@ -176,6 +177,7 @@ AppConfig parse_args(int argc, char** argv, const std::string& which) {
     else if (a == "--input") c.input = val();
     else if (a == "--cpu") c.cpu = true;
     else if (a == "--no-montage") c.montage = false;
+    else if (a == "--html") c.html = true;
     else if (a == "--dump-mhd") c.dump_mhd = val();
     else if (a == "--repeat") c.repeat = std::max(1, std::atoi(val().c_str()));
     else if (a == "--json") c.json = val();
@@ -1025,6 +1027,21 @@ int run_test_pipeline(const AppConfig& cfg) {
       auto j = jpeg::encode_gray(m.data(), mw, ch, mw, rp.jpeg_quality, (jpeg::Sampling)rp.jpeg_sampling);
       std::ofstream f(cfg.out_dir + "/multi_view.jpg", std::ios::binary | std::ios::trunc);
       f.write((const char*)j.data(), (std::streamsize)j.size());
+    }
+    if (cfg.html) {
+      // The reference's viewer, MultiViewWindow::create(5, Color::Black(), 2300, 450, false)
+      // (test_pipeline.cpp:148-158): five views side by side on black in a 2300×450 window. A browser
+      // shows the exported stage images the same way, each view scaled to fit its 460×450 cell.
+      std::ofstream f(cfg.out_dir + "/multi_view.html", std::ios::trunc);
+      f << "<!DOCTYPE html>\n<html><head><meta charset=\"utf-8\"><title>Medical Image Processing Stages</title>\n"
+        << "<style>body{margin:0;background:#000}#w{display:flex;width:2300px;height:450px}"
+        << "figure{margin:0;flex:1;display:flex;flex-direction:column;align-items:center;justify-content:center}"
+        << "img{max-width:460px;max-height:420px}figcaption{color:#ccc;font:13px sans-serif}</style></head>\n"
+        << "<body><div id=\"w\">\n";
+      for (int k = 0; k < 5; ++k)
+        f << "<figure><img src=\"" << names[k] << ".jpg\" alt=\"" << names[k] << "\"><figcaption>" << names[k]
+          << "</figcaption></figure>\n";
+      f << "</div></body></html>\n";
     }
     if (!cfg.quiet)
       std::cout << "Medical Image Processing Stages: " << (cfg.cpu ? "CPU golden model" : "MI355X") << ", "

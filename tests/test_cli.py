@@ -54,6 +54,18 @@ def test_test_pipeline_cpu_jpeg_sampling(native, cohort_root, tmp_path, flag, mo
     assert r.returncode == 2 and "--jpeg-sampling" in r.stderr
 
 
+def test_test_pipeline_html_viewer(cohort_root, tmp_path):
+    """--html: the reference's 5-view window (MultiViewWindow 2300x450) as a page over the exported
+    stage images."""
+    out = tmp_path / "o"
+    r = run_bin("test_pipeline", "--cpu", "--html", "--data-root", cohort_root, "--out", str(out))
+    assert r.returncode == 0, r.stderr
+    page = (out / "multi_view.html").read_text()
+    assert "width:2300px;height:450px" in page
+    for name in ("original_image", "preprocessed_image", "segmentation", "erosion_result", "final_dilated_result"):
+        assert f'src="{name}.jpg"' in page and (out / f"{name}.jpg").exists()
+
+
 def test_cli_help_and_bad_flag():
     for tool in ("test_pipeline", "img_processing_sequential", "img_processing_parallel"):
         r = run_bin(tool, "--help")
