@@ -1,41 +1,30 @@
 #!/usr/bin/env python3
-"""Summarise tools/gpu_pmc_jpeg.sh output: per-wave SQ counters of the JPEG encoder per truncation
-variant, and of every kernel in the full pipeline (variant 0). VALU-active / wave-cycles × resident
-waves per SIMD (4 for the encoder) approximates how busy the SIMDs' VALUs are.
-Usage: python tools/pmc_summary.py gpurun_out/<name>"""
+"""Summarise tools/gpu_pmc.sh output: the SQ counters of every kernel, summed over the run's
+dispatches across the per-group passes (gpurun_out/pmc/p*/run_counter_collection.csv), as per-wave
+instruction counts and per-wave-cycle activity. VALU-active / wave-cycles × resident waves per SIMD
+approximates how busy the SIMDs' VALUs are.
+Usage: python tools/pmc_summary.py gpurun_out/pmc"""
 import collections
 import csv
+import glob
 import os
 import sys
 
-d = sys.argv[1]
-names = {7: "tables + ticket", 1: "+ render / staging", 16: "+ FDCT + quantisation", 2: "+ AC coding",
-         4: "+ DC, scan, bit range, look-back", 0: "full encoder", 40: "gray images only", 41: "label images only"}
-print("JPEG encoder, per-wave averages over all dispatches (isolated engine runs, 1 stream, batch 96)")
-print(f"{'variant':40s} {'VALU':>6} {'SALU':>6} {'LDS':>5} {'wave-cyc':>9} {'VALU/wc':>8} {'wait/wc':>8}")
-full = {}
-for v in (7, 1, 16, 2, 4, 0, 40, 41):
-    p = os.path.join(d, f"v{v}", "k_counter_collection.csv")
-    if not os.path.exists(p):
-        continue
-    acc = collections.defaultdict(lambda: collections.defaultdict(float))
-    disp = collections.defaultdict(set)
+d = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc"
+acc = collections.defaultdict(lambda: collections.defaultdict(float))
+for p in sorted(glob.glob(os.path.join(d, "p*", "*counter_collection.csv"))):
     for r in csv.DictReader(open(p)):
         k = r["Kernel_Name"].split("(")[0].replace("void nm03::gpu::", "")
+        if "rocclr" in k:
+            continue
         acc[k][r["Counter_Name"]] += float(r["Counter_Value"])
-        disp[k].add(r["Dispatch_Id"])
-    for k, c in acc.items():
-        w = c["SQ_WAVES"]
-        if "jpeg" in k and w:
-            print(f"jpeg={v:<3} {names[v]:32s} {c['SQ_INSTS_VALU']/w:6.0f} {c['SQ_INSTS_SALU']/w:6.0f} "
-                  f"{c['SQ_INSTS_LDS']/w:5.0f} {c['SQ_WAVE_CYCLES']/w:9.0f} "
-                  f"{c['SQ_ACTIVE_INST_VALU']/c['SQ_WAVE_CYCLES']:8.3f} {c['SQ_WAIT_INST_ANY']/c['SQ_WAVE_CYCLES']:8.3f}")
-        if v == 0:
-            full[k] = (len(disp[k]), c)
-print("\nEvery kernel of the full pipeline (variant 0):")
-for k, (n, c) in full.items():
-    w = c["SQ_WAVES"]
-    if not w:
-        continue
-    print(f"{k[:40]:40s} waves/dispatch {w/n:7.0f}  VALU/wave {c['SQ_INSTS_VALU']/w:6.0f}  SALU/wave {c['SQ_INSTS_SALU']/w:5.0f}  "
-          f"VALU/wc {c['SQ_ACTIVE_INST_VALU']/c['SQ_WAVE_CYCLES']:.3f}  wait/wc {c['SQ_WAIT_INST_ANY']/c['SQ_WAVE_CYCLES']:.3f}")
+print(f"{'kernel':40s} {'waves':>8} {'VALU/w':>7} {'SALU/w':>7} {'LDS/w':>6} {'VALU/wc':>8} {'wait/wc':>8} "
+      f"{'LDSbc/LDSact':>12} {'VMEMrd/w':>8} {'VMEMwr/w':>8}")
+for k, c in sorted(acc.items()):
+    w = c.get("SQ_WAVES", 0.0) or 1.0
+    wc = c.get("SQ_WAVE_CYCLES", 0.0) or 1.0
+    lds_act = c.get("SQ_ACTIVE_INST_LDS", 0.0) or 1.0
+    print(f"{k[:40]:40s} {w:8.0f} {c.get('SQ_INSTS_VALU', 0) / w:7.0f} {c.get('SQ_INSTS_SALU', 0) / w:7.0f} "
+          f"{c.get('SQ_INSTS_LDS', 0) / w:6.0f} {c.get('SQ_ACTIVE_INST_VALU', 0) / wc:8.3f} "
+          f"{c.get('SQ_WAIT_INST_ANY', 0) / wc:8.3f} {c.get('SQ_LDS_BANK_CONFLICT', 0) / lds_act:12.3f} "
+          f"{c.get('SQ_INSTS_VMEM_RD', 0) / w:8.1f} {c.get('SQ_INSTS_VMEM_WR', 0) / w:8.1f}")
