@@ -76,8 +76,9 @@ struct AppConfig {
   // CLOCK_REALTIME when parse_args began (the --json record's "main_unix_s"): with the launcher's
   // own clock it splits a cold run's wall into process start-up (exec → main) and the rest.
   double main_unix_s = 0;
-  // GPU_MAX_HW_QUEUES for the process (--hw-queues; 0 = leave the environment's value).
-  int hw_queues = 2;
+  // GPU_MAX_HW_QUEUES for the process (--hw-queues; 0 = leave the environment's value; -1 = auto:
+  // 1 for the short jobs that take shader copies, else 2 — see apply_copy_engine).
+  int hw_queues = -1;
   // Host↔device copies (--copy-engine): kCopySdma (the DMA engines), kCopyBlit (shader copies on the
   // compute queues: HSA_ENABLE_SDMA=0) or kCopyAuto (blit for short 2D jobs, see apply_copy_engine).
   int copy_engine = 0;
@@ -136,7 +137,8 @@ int64_t count_cohort_slices(const AppConfig& cfg);
 
 // Sets the process's copy path before anything initialises HIP (rank processes inherit it):
 // HSA_ENABLE_SDMA=0 for kCopyBlit, and for kCopyAuto when 0 ≤ slices_per_rank ≤ kBlitMaxSlicesPerRank
-// and the environment does not already set HSA_ENABLE_SDMA. Returns whether blit copies were chosen.
+// and the environment does not already set HSA_ENABLE_SDMA; with --hw-queues auto also
+// GPU_MAX_HW_QUEUES (1 with shader copies, else 2). Returns whether blit copies were chosen.
 bool apply_copy_engine(const AppConfig& cfg, int64_t slices_per_rank);
 // "blit" when the process runs with HSA_ENABLE_SDMA=0, else "sdma" (the CLI --json records it).
 const char* copy_engine_name();

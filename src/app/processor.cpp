@@ -67,7 +67,8 @@ void usage(const std::string& which) {
             << "  --json FILE            write run metrics as JSON\n"
             << "  --resume               keep existing outputs; skip slices whose two JPEGs exist\n"
             << "  --frame K              import frame K of multi-frame DICOM files (default: reject them)\n"
-            << "  --hw-queues N          HIP hardware queues of this process (GPU_MAX_HW_QUEUES; default 2, 0 = environment)\n"
+            << "  --hw-queues N|auto     HIP hardware queues of this process (GPU_MAX_HW_QUEUES; auto: 1 for short jobs on\n"
+            << "                         shader copies, else 2; 0 = environment)\n"
             << "  --copy-engine auto|sdma|blit  host<->GPU copies: DMA engines or shader copies (auto: blit for\n"
             << "                         2D jobs of <= 4096 slices per rank, whose cold start the DMA queue's set-up dominates)\n"
             << "  --quiet                suppress per-slice progress lines\n"
@@ -188,7 +189,10 @@ AppConfig parse_args(int argc, char** argv, const std::string& which) {
     }
     else if (a == "--resume") c.engine.resume = true;
     else if (a == "--frame") c.engine.pipe.frame = std::atoi(val().c_str());
-    else if (a == "--hw-queues") c.hw_queues = std::max(0, std::atoi(val().c_str()));
+    else if (a == "--hw-queues") {
+      const std::string v = val();
+      c.hw_queues = v == "auto" ? -1 : std::max(0, std::atoi(v.c_str()));
+    }
     else if (a == "--copy-engine") {
       const std::string v = val();
       if (v != "auto" && v != "sdma" && v != "blit") {
@@ -231,7 +235,8 @@ AppConfig parse_args(int argc, char** argv, const std::string& which) {
   // Every stream past the first costs a new HW queue (≈ 9 ms cold) until GPU_MAX_HW_QUEUES is
   // reached, then ≈ 3–4 ms on a shared one: 2 queues cut the start-up thread's stream reservation from
   // 56 to 45 ms (interleaved cold runs, profiles/r5/cold/cli_wall.jsonl) with the same warm throughput
-  // (--repeat 30: 121k vs 117k slices/s, profiles/r5/queues/).
+  // (--repeat 30: 121k vs 117k slices/s, profiles/r5/queues/). auto (-1) is resolved with the copy path
+  // (apply_copy_engine).
   if (c.hw_queues > 0) setenv("GPU_MAX_HW_QUEUES", std::to_string(c.hw_queues).c_str(), 1);
   return c;
 }
@@ -915,6 +920,10 @@ bool apply_copy_engine(const AppConfig& cfg, int64_t slices_per_rank) {
     blit = cfg.mode != "3d" && slices_per_rank >= 0 && slices_per_rank <= kBlitMaxSlicesPerRank &&
            std::getenv("HSA_ENABLE_SDMA") == nullptr;
   if (blit) setenv("HSA_ENABLE_SDMA", "0", 1);
+  // With shader copies the copies need no queue of their own and a short job no concurrency between
+  // slots: one HW queue saves the second queue's creation (streams 32–35 → 25–26 ms, processing
+  // 4.6–5.0 vs 4.8–4.9 ms, profiles/r5/cold_exitq/); longer jobs keep 2.
+  if (cfg.hw_queues < 0) setenv("GPU_MAX_HW_QUEUES", blit ? "1" : "2", 1);
   return blit;
 }
 

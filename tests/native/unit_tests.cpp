@@ -730,11 +730,15 @@ TEST(copy_engine_policy) {
   using namespace nm03::app;
   const char* saved = std::getenv("HSA_ENABLE_SDMA");
   const std::string keep = saved ? saved : "";
+  const char* savedq = std::getenv("GPU_MAX_HW_QUEUES");
+  const std::string keepq = savedq ? savedq : "";
   AppConfig c;
   unsetenv("HSA_ENABLE_SDMA");
   CHECK(apply_copy_engine(c, 465) && std::string(copy_engine_name()) == "blit");
+  CHECK(std::string(std::getenv("GPU_MAX_HW_QUEUES")) == "1");  // --hw-queues auto with shader copies
   unsetenv("HSA_ENABLE_SDMA");
   CHECK(!apply_copy_engine(c, kBlitMaxSlicesPerRank + 1) && std::string(copy_engine_name()) == "sdma");
+  CHECK(std::string(std::getenv("GPU_MAX_HW_QUEUES")) == "2");
   CHECK(!apply_copy_engine(c, -1));  // unknown size: leave the DMA engines
   setenv("HSA_ENABLE_SDMA", "1", 1);
   CHECK(!apply_copy_engine(c, 10));  // the user's setting wins
@@ -750,6 +754,10 @@ TEST(copy_engine_policy) {
     setenv("HSA_ENABLE_SDMA", keep.c_str(), 1);
   else
     unsetenv("HSA_ENABLE_SDMA");
+  if (savedq)
+    setenv("GPU_MAX_HW_QUEUES", keepq.c_str(), 1);
+  else
+    unsetenv("GPU_MAX_HW_QUEUES");
 }
 
 }  // namespace
