@@ -922,7 +922,8 @@ bool apply_copy_engine(const AppConfig& cfg, int64_t slices_per_rank) {
   if (blit) setenv("HSA_ENABLE_SDMA", "0", 1);
   // With shader copies the copies need no queue of their own and a short job no concurrency between
   // slots: one HW queue saves the second queue's creation (streams 32–35 → 25–26 ms, processing
-  // 4.6–5.0 vs 4.8–4.9 ms, profiles/r5/cold_exitq/); longer jobs keep 2.
+  // 4.6–5.0 vs 4.8–4.9 ms, profiles/r5/cold_exitq/; 9 interleaved pairs: engine wait 41.5 vs 45.9 ms,
+  // processing 5.1 vs 4.7 ms, profiles/r5/cold_hq/); longer jobs keep 2.
   if (cfg.hw_queues < 0) setenv("GPU_MAX_HW_QUEUES", blit ? "1" : "2", 1);
   return blit;
 }
