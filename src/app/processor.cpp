@@ -378,7 +378,8 @@ int run_sequential(const AppConfig& cfg) {
 
 // =============================================================================================
 // img_processing_parallel — N ranks, one MI355X each, global work list sharded in contiguous
-// blocks; rank 0 plans (directories, ordering) and prints; RCCL carries plan and results.
+// blocks; rank 0 plans (directories, ordering) and prints; the shared-memory control plane (or RCCL,
+// NM03_COMM=rccl) carries plan and results.
 // =============================================================================================
 namespace {
 
@@ -479,7 +480,8 @@ int scan_max_dim(const std::vector<PatientPlan>& plan, int threads) {
 
 // Cold start (round 5). ONE start-up thread owns every HIP call until the engine exists: it brings up
 // the runtime and the device context, loads every kernel code object, reserves the engine's streams
-// (HW queues) and brings up the copy engine, starts RCCL's non-blocking initialisation (N > 1), and —
+// (HW queues) and brings up the copy engine, starts RCCL's non-blocking initialisation when a comm is
+// given (NM03_COMM=rccl), and —
 // as soon as the caller hands it the engine configuration (build()) — builds the whole engine: every
 // slot's events, pinned and device buffers. Meanwhile the calling thread plans (cohort discovery,
 // output wipe, header scan), exchanges the plan over the shared-memory control plane and computes the
@@ -566,8 +568,8 @@ int parallel_rank(const AppConfig& cfg, int rank, int size, Comm& comm, int devi
   ec.device = device;
   const double t_setup = now_s();
   // Cold start (round 5). ONE start-up thread owns every HIP call until the engine exists: it
-  // brings up the runtime and the device context, loads every kernel code object, starts RCCL's
-  // non-blocking initialisation (N > 1), and — as soon as the main thread hands it the engine
+  // brings up the runtime and the device context, loads the 2D kernels' code objects, starts RCCL's
+  // non-blocking initialisation (NM03_COMM=rccl only, see below), and — as soon as the main thread hands it the engine
   // configuration — builds the whole engine: every slot's streams, events, pinned and device
   // buffers. Meanwhile the main thread plans (rank 0: patient discovery, output wipe, header scan),
   // exchanges the plan over the shared-memory control plane and computes the rank's CPU partition.
