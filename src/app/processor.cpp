@@ -562,7 +562,8 @@ std::unique_ptr<Engine> EngineStartup::build(const EngineConfig& ec, std::string
 namespace {
 
 // `rank_devices`: the HIP device of every rank (one node), for the CPU partition of this rank.
-int parallel_rank(const AppConfig& cfg, int rank, int size, Comm& comm, int device, const std::vector<int>& rank_devices) {
+int parallel_rank(const AppConfig& cfg, int rank, int size, Comm& comm, int device, const std::vector<int>& rank_devices,
+                  int64_t work_per_rank) {
   const std::string base = cohort::cohort_dir(cfg.data_root);
   EngineConfig ec = cfg.engine;
   ec.device = device;
@@ -576,12 +577,15 @@ int parallel_rank(const AppConfig& cfg, int rank, int size, Comm& comm, int devi
   // Nothing else touches HIP before the first batch: in round 4, slots built on their workers held
   // the runtime's locks (HW-queue creation 10–50 ms) while the first batch tried to copy and
   // launch, and a cold 465-slice pass took 37–70 ms instead of ≈ 4 ms (profiles/r5/cold/).
-  // A 2D job's collectives are control data (the work list, counts, timing rows: a few KB in all),
-  // which the node's shared-memory control plane carries; RCCL (loaded and initialised per rank,
-  // 0.3–2 s on a node, longer than the job's processing) is brought up only when asked for
-  // (NM03_COMM=rccl) — device data exchange (--split-volume) brings it up by itself.
+  // A 2D job's collectives are control data (the work list, counts, timing rows: a few KB in all).
+  // RCCL starts on the start-up thread and carries the collectives after the run (promote()) when
+  // the job is long enough to amortise bringing it up — more than kBlitMaxSlicesPerRank slices per
+  // rank (all --repeat passes), the same bound as the copy path — or when NM03_COMM=rccl asks for it;
+  // a short job stays on the node's shared-memory control plane and never waits for, or loads, RCCL
+  // (NM03_COMM=host: never). Device data exchange (--split-volume) brings RCCL up by itself.
   const char* comm_env = std::getenv("NM03_COMM");
-  const bool data_plane = size > 1 && comm_env && std::string(comm_env) == "rccl";
+  const std::string comm_mode = comm_env && *comm_env ? comm_env : "auto";
+  const bool data_plane = size > 1 && (comm_mode == "rccl" || (comm_mode == "auto" && work_per_rank > kBlitMaxSlicesPerRank));
   EngineStartup su(device, std::max(1, cfg.engine.streams) + 1, data_plane ? &comm : nullptr);  // slots + upload stream
   double engine_wait_s = 0;
   std::unique_ptr<Engine> engine_p;
@@ -954,14 +958,15 @@ int run_parallel(const AppConfig& cfg) {
     }
     LaunchOptions lo = LaunchOptions::from_env();
     // auto: size the job to the cohort, counted from its directory listings before any fork
-    const int64_t slices = cfg.gpus == kGpusAuto || cfg.copy_engine == kCopyAuto ? count_cohort_slices(cfg) : -1;
+    const int64_t slices = count_cohort_slices(cfg);  // rank count, copy path and comm policy (≈ 1 ms of listings)
     const int n = resolve_gpus(cfg, lo, cfg.gpus == kGpusAuto ? slices : -1);
-    apply_copy_engine(cfg, slices < 0 ? -1 : (slices + n - 1) / n * std::max(1, cfg.repeat));
+    apply_copy_engine(cfg, slices < 0 ? -1 : (slices + n - 1) / n * std::max(1, cfg.repeat));  // per rank
     std::vector<int> rank_devices;
     for (int r = 0; r < n; ++r)
       rank_devices.push_back(n > 1 ? lo.device_of(r) : lo.device_override >= 0 ? lo.device_override : cfg.engine.device);
+    const int64_t work_per_rank = slices < 0 ? -1 : (slices + n - 1) / n * std::max(1, cfg.repeat);
     return launch_ranks(n, [&](int rank, int size, Comm& comm) {
-      return parallel_rank(cfg, rank, size, comm, rank_devices[(size_t)rank], rank_devices);
+      return parallel_rank(cfg, rank, size, comm, rank_devices[(size_t)rank], rank_devices, work_per_rank);
     }, lo);
   } catch (const std::exception& e) {
     std::cerr << "Fatal error: " << e.what() << std::endl;  // :407-408
