@@ -54,6 +54,13 @@ int main(int argc, char** argv) {
     else if (a == "--dilation-3d") dil3d = std::atoi(v().c_str());
     else if (a == "--device") ec.device = std::atoi(v().c_str());
     else if (a == "--host-only") ec.host_only = true;  // cohort: every load/pack/write, no GPU (sanitizer sweeps)
+    // The FAST-unpinned choices (app.h flags of the CLIs) for timing their kernel paths.
+    else if (a == "--jpeg-sampling") {
+      const std::string s = v();
+      ec.render.jpeg_sampling = s == "gray" ? 2 : s == "444" ? 1 : 0;
+    }
+    else if (a == "--se-shape") ec.pipe.se_shape = v() == "disc" ? nm03::kSeDisc : nm03::kSeSquare;
+    else if (a == "--render-filter") ec.render.filter = v() == "nearest" ? nm03::kFilterNearest : nm03::kFilterBilinear;
     else {
       std::cerr << "unknown option " << a << std::endl;
       return 2;
