@@ -411,7 +411,11 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(kOcc)))
       // Patch element (j, i) = source (4by-1+j, 4bx-1+i) = staged row 4by-1+j-ys0, column 4bx+i.
       // Patch column i = source column 4bx-1+i = staged column 4bx+i → swizzled 5bx + i + (i ≥ 4).
       const float* pp = spatch + (4 * by - 1 - ys0) * pcols + 5 * bx;
-      render_patch_2x([&](int j, int i) { return pp[j * pcols + i + (i >= 4 ? 1 : 0)]; }, win, blk);
+      auto fetch = [&](int j, int i) { return pp[j * pcols + i + (i >= 4 ? 1 : 0)]; };
+      if (rd.filter == 1)  // --render-filter nearest (workgroup-uniform: one image per workgroup)
+        render_patch_2x_nearest(fetch, win, blk);
+      else
+        render_patch_2x(fetch, win, blk);
     } else if (d.render >= 0) {
       render_block_2x(rd, rs.raw, rs.f32, rs.bits, win, bx, by, blk);
     } else {

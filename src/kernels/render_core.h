@@ -134,6 +134,23 @@ __device__ __forceinline__ void render_patch_2x(Fetch&& fetch, RWindow win, int3
   }
 }
 
+// --render-filter nearest on an exact 2× fit: canvas pixel (8bx + c, 8by + r) samples source
+// (4bx + c/2, 4by + r/2) — floor of its centre's source coordinate, render_pixel's nearest path —
+// which is patch element (r/2 + 1, c/2 + 1): 16 distinct values, each covering a 2×2 canvas cell.
+template <class Fetch>
+__device__ __forceinline__ void render_patch_2x_nearest(Fetch&& fetch, RWindow win, int32_t* px) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int32_t g = (int32_t)gray_u8(fetch(j + 1, i + 1), win.lo, win.inv);
+      px[(2 * j) * 8 + 2 * i] = g;
+      px[(2 * j) * 8 + 2 * i + 1] = g;
+      px[(2 * j + 1) * 8 + 2 * i] = g;
+      px[(2 * j + 1) * 8 + 2 * i + 1] = g;
+    }
+}
+
 // Exact-2× label render of the 8×8 canvas block (bx, by): canvas columns 8bx..8bx+7 map to source
 // columns 4bx..4bx+3, always inside one 64-bit word k = 4bx/64 of the label and border rows;
 // words(y, k, lab, brd) returns word k of source row y (edge-clamped row index).
@@ -224,7 +241,10 @@ __device__ __forceinline__ void render_block_2x(const RenderDesc& d, const uint1
       for (int i = 0; i < 6; ++i) patch[j][i] = render_src_value(d, raw, f32, clampi(sx0 + i, 0, W - 1), y);
     }
   }
-  render_patch_2x([&](int j, int i) { return patch[j][i]; }, win, px);
+  if (d.filter == 1)
+    render_patch_2x_nearest([&](int j, int i) { return patch[j][i]; }, win, px);
+  else
+    render_patch_2x([&](int j, int i) { return patch[j][i]; }, win, px);
 }
 
 }  // namespace nm03::gpu

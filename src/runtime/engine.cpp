@@ -987,9 +987,9 @@ struct Engine::Impl {
       j.out_off = (uint64_t)k * out_cap_;
       j.out_cap = out_cap_;
       // Export runs render straight into the JPEG block kernel when the fit is an exact 2× (the
-      // canvas is never materialised); test runs keep canvases for inspection.
-      // (a nearest-filtered gray render always takes the canvas path: the fused 2× render is bilinear)
-      j.render = (mode == 0 && render_is_exact_2x(rd[k], cw, ch) && (rd[k].kind == kRenderLabels || !rd[k].filter)) ? k : -1;
+      // canvas is never materialised; bilinear and nearest gray renders alike); test runs keep
+      // canvases for inspection.
+      j.render = (mode == 0 && render_is_exact_2x(rd[k], cw, ch)) ? k : -1;
       if (j.render < 0) s.any_canvas = true;
     }
     s.ncanvas = ncanv;

@@ -563,7 +563,7 @@ std::vector<std::vector<uint8_t>> VolumeRunner::export_jpegs(const VolumeInput& 
       j.canvas_off = (uint32_t)(k * canvas_bytes);
       j.out_off = (uint64_t)k * kVolOutCap;
       j.out_cap = kVolOutCap;
-      j.render = render_is_exact_2x(r, cw, ch) && (r.kind == kRenderLabels || !r.filter) ? k : -1;
+      j.render = render_is_exact_2x(r, cw, ch) ? k : -1;
       any_canvas |= j.render < 0;
     }
     auto* d_rd = X.tables.as<uint8_t>();
