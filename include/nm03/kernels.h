@@ -141,7 +141,11 @@ struct JpegRenderSrc {
 };
 void launch_jpeg(const uint8_t* canvas, const JpegDesc* jd, int ncanvas, int out_w, int out_h, const int32_t* div_luma,
                  JpegWork& w, uint8_t* out, int32_t* out_sizes, hipStream_t stream,
-                 const JpegRenderSrc* fused = nullptr, int sampling = 0);  // jpeg::Sampling
+                 const JpegRenderSrc* fused = nullptr, int sampling = 0,  // jpeg::Sampling
+                 bool nearest = false);  // fused gray renders use --render-filter nearest (4:2:0 only)
+// Whether the fused encoder renders --render-filter nearest gray images for this layout (else callers
+// render them into canvases first).
+inline bool jpeg_fuses_nearest(int sampling) { return sampling == 0; }
 // K6: binary threshold lo ≤ x ≤ hi → u8 0/1 (in 16-byte aligned, out 4-byte aligned).
 void launch_threshold(const float* in, uint8_t* out, size_t n, float lo, float hi, hipStream_t stream);
 

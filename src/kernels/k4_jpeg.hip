@@ -168,7 +168,7 @@ __device__ __forceinline__ uint32_t priv_word(const uint32_t* pb, const uint32_t
 // chroma blocks; gray scans them in raster order alone. (One instance per layout: the default
 // 4:2:0 code is unchanged by the other two.) 5 workgroups per CU (31.7 KiB, ≤ 96 VGPRs with spills) measured no better than 4 once
 // images were dealt round-robin (profiles/r3/jpeg_spread/split_and_occ5.txt).
-template <int kOcc, int kUnion, int kSamp>
+template <int kOcc, int kUnion, int kSamp, bool kNearest>
 __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(kOcc))) void jpeg_fused_kernel(const uint8_t* __restrict__ canvas,
                                                              const JpegDesc* __restrict__ jd, int ncanvas, int out_w,
                                                              int out_h, QuantRecip q, JpegWork w, JpegRenderSrc rs,
@@ -412,12 +412,12 @@ __global__ __launch_bounds__(kJpegWG) __attribute__((amdgpu_waves_per_eu(kOcc)))
       // Patch column i = source column 4bx-1+i = staged column 4bx+i → swizzled 5bx + i + (i ≥ 4).
       const float* pp = spatch + (4 * by - 1 - ys0) * pcols + 5 * bx;
       auto fetch = [&](int j, int i) { return pp[j * pcols + i + (i >= 4 ? 1 : 0)]; };
-      if (rd.filter == 1)  // --render-filter nearest (workgroup-uniform: one image per workgroup)
+      if (kNearest)  // --render-filter nearest: its own instance (launch_jpeg)
         render_patch_2x_nearest(fetch, win, blk);
       else
         render_patch_2x(fetch, win, blk);
     } else if (d.render >= 0) {
-      render_block_2x(rd, rs.raw, rs.f32, rs.bits, win, bx, by, blk);
+      render_block_2x<kNearest>(rd, rs.raw, rs.f32, rs.bits, win, bx, by, blk);
     } else {
       const uint8_t* src = canvas + d.canvas_off + (size_t)(by * 8) * out_w + bx * 8;
 #pragma unroll
@@ -817,7 +817,7 @@ bool render_is_exact_2x(const RenderDesc& r, int out_w, int out_h) {
 
 void launch_jpeg(const uint8_t* canvas, const JpegDesc* jd, int ncanvas, int out_w, int out_h, const int32_t* div_luma,
                  JpegWork& w, uint8_t* out, int32_t* out_sizes, hipStream_t stream, const JpegRenderSrc* fused,
-                 int sampling) {
+                 int sampling, bool nearest) {
   if (ncanvas <= 0) return;
   if (sampling < kSampling420 || sampling > kSamplingGray) throw DeviceError("launch_jpeg: unknown sampling");
   if (out_w % 16 || out_h % 16) throw DeviceError("GPU JPEG encoder needs canvas dims that are multiples of 16");
@@ -857,9 +857,13 @@ void launch_jpeg(const uint8_t* canvas, const JpegDesc* jd, int ncanvas, int out
     w.look_base = w.look_base ? 0 : half;
     w.prev_words = words;
   }
-  auto* kern = sampling == kSampling420   ? &jpeg_fused_kernel<4, kUnionWords, kSampling420>
-              : sampling == kSampling444 ? &jpeg_fused_kernel<4, kUnionWords, kSampling444>
-                                         : &jpeg_fused_kernel<4, kUnionWords, kSamplingGray>;
+  // Fused gray renders with --render-filter nearest have their own 4:2:0 instance; callers send the
+  // other layouts' nearest renders through canvases (jpeg_fuses_nearest).
+  if (nearest && sampling != kSampling420) throw DeviceError("launch_jpeg: fused nearest renders need 4:2:0");
+  auto* kern = nearest                    ? &jpeg_fused_kernel<4, kUnionWords, kSampling420, true>
+               : sampling == kSampling420 ? &jpeg_fused_kernel<4, kUnionWords, kSampling420, false>
+               : sampling == kSampling444 ? &jpeg_fused_kernel<4, kUnionWords, kSampling444, false>
+                                          : &jpeg_fused_kernel<4, kUnionWords, kSamplingGray, false>;
   kern<<<parts * ncanvas, kJpegWG, 0, stream>>>(canvas, jd, ncanvas, out_w, out_h, q, w, rs, out, out_sizes, dbg);
   check_launch("jpeg_fused_kernel");
 }
@@ -874,11 +878,13 @@ void preload_kernels(bool with_volume) {
     preload_threshold();
   }
   hipFuncAttributes a;
-  check_hip(hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&jpeg_fused_kernel<4, kUnionWords, kSampling420>)),
+  check_hip(hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&jpeg_fused_kernel<4, kUnionWords, kSampling420, false>)),
             "preload jpeg_fused_kernel");
-  check_hip(hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&jpeg_fused_kernel<4, kUnionWords, kSampling444>)),
+  check_hip(hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&jpeg_fused_kernel<4, kUnionWords, kSampling420, true>)),
+            "preload jpeg_fused_kernel nearest");
+  check_hip(hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&jpeg_fused_kernel<4, kUnionWords, kSampling444, false>)),
             "preload jpeg_fused_kernel 4:4:4");
-  check_hip(hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&jpeg_fused_kernel<4, kUnionWords, kSamplingGray>)),
+  check_hip(hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&jpeg_fused_kernel<4, kUnionWords, kSamplingGray, false>)),
             "preload jpeg_fused_kernel gray");
 }
 

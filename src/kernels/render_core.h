@@ -198,6 +198,9 @@ __device__ __forceinline__ void render_labels_exact2x(const RenderDesc& d, Words
 
 // Fused 2× render of the 8×8 canvas block (bx, by) into px[64] (row-major), for a RenderDesc
 // with render_is_exact_2x(): the block's source footprint is a 6×6 patch (gray) or 4×4 (labels).
+// kNearest: gray renders with --render-filter nearest (a compile-time choice: the bilinear encoder's
+// code stays as it was).
+template <bool kNearest = false>
 __device__ __forceinline__ void render_block_2x(const RenderDesc& d, const uint16_t* raw, const float* f32,
                                                 const uint64_t* bits, RWindow win, int bx, int by, int32_t* px,
                                                 bool synth_src = false) {
@@ -241,7 +244,7 @@ __device__ __forceinline__ void render_block_2x(const RenderDesc& d, const uint1
       for (int i = 0; i < 6; ++i) patch[j][i] = render_src_value(d, raw, f32, clampi(sx0 + i, 0, W - 1), y);
     }
   }
-  if (d.filter == 1)
+  if (kNearest)
     render_patch_2x_nearest([&](int j, int i) { return patch[j][i]; }, win, px);
   else
     render_patch_2x([&](int j, int i) { return patch[j][i]; }, win, px);

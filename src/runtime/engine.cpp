@@ -989,7 +989,10 @@ struct Engine::Impl {
       // Export runs render straight into the JPEG block kernel when the fit is an exact 2× (the
       // canvas is never materialised; bilinear and nearest gray renders alike); test runs keep
       // canvases for inspection.
-      j.render = (mode == 0 && render_is_exact_2x(rd[k], cw, ch)) ? k : -1;
+      j.render = (mode == 0 && render_is_exact_2x(rd[k], cw, ch) &&
+                  (rd[k].kind == kRenderLabels || !rd[k].filter || jpeg_fuses_nearest(cfg.render.jpeg_sampling)))
+                     ? k
+                     : -1;
       if (j.render < 0) s.any_canvas = true;
     }
     s.ncanvas = ncanv;
@@ -1074,7 +1077,7 @@ struct Engine::Impl {
     rsrc.rd = d_rd;
     rsrc.nrd = ncanv;
     launch_jpeg(s.d_canvas, d_jd, ncanv, cw, ch, divs, s.jw, s.d_out, s.d_sizes, s.stream, &rsrc,
-                cfg.render.jpeg_sampling);
+                cfg.render.jpeg_sampling, cfg.render.filter == kFilterNearest && jpeg_fuses_nearest(cfg.render.jpeg_sampling));
     check_hip(hipEventRecord(s.ev2, s.stream), "event");
     if (mark) mark->enq = now_s();
     wait_batch(s, s.ev2, t_enq, nl);

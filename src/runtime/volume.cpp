@@ -563,7 +563,7 @@ std::vector<std::vector<uint8_t>> VolumeRunner::export_jpegs(const VolumeInput& 
       j.canvas_off = (uint32_t)(k * canvas_bytes);
       j.out_off = (uint64_t)k * kVolOutCap;
       j.out_cap = kVolOutCap;
-      j.render = render_is_exact_2x(r, cw, ch) ? k : -1;
+      j.render = render_is_exact_2x(r, cw, ch) && (r.kind == kRenderLabels || !r.filter || jpeg_fuses_nearest(samp)) ? k : -1;
       any_canvas |= j.render < 0;
     }
     auto* d_rd = X.tables.as<uint8_t>();
@@ -582,7 +582,7 @@ std::vector<std::vector<uint8_t>> VolumeRunner::export_jpegs(const VolumeInput& 
     rs.rd = drd;
     rs.nrd = nc;
     launch_jpeg(X.canvas.as<uint8_t>(), reinterpret_cast<const JpegDesc*>(d_jd), nc, cw, ch, tables.div_luma, X.jw,
-                X.d_out, X.d_sizes, V.stream, &rs, samp);
+                X.d_out, X.d_sizes, V.stream, &rs, samp, rp.filter == kFilterNearest && jpeg_fuses_nearest(samp));
     check_hip(hipStreamSynchronize(V.stream), "export sync");
     bool rendered = any_canvas;
     for (int k = 0; k < nc; ++k) {

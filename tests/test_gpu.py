@@ -1269,18 +1269,20 @@ def test_cli_fresh_process_512_cohort_render_from_slot_threads(native, tmp_path)
         assert open(out / f"PGBM-{p + 1:03d}" / f"{stem}_processed.jpg", "rb").read() == g["jpeg_processed"]
 
 
-def test_engine_render_nearest_bit_exact(native, cohort_root, tmp_path):
+@pytest.mark.parametrize("sampling", [0, 2])
+def test_engine_render_nearest_bit_exact(native, cohort_root, tmp_path, sampling):
     """--render-filter nearest through the GPU: every stage image of one slice (K3 canvases) and a
-    cohort run's export pairs (the nearest gray renders leave the fused 2× path for K3) equal the
-    golden model."""
+    cohort run's export pairs equal the golden model — 4:2:0 renders nearest gray images inside the
+    fused encoder (its own instance), the other layouts through K3 canvases."""
     raw = _phantom(native)
     meta = {"type": "u16", "stored_bits": 16, "slope": 1.0, "intercept": 0.0, "spacing_x": 1.0, "spacing_y": 1.0}
-    pipe = nm.SlicePipeline(nm.PipelineConfig(batch_size=1, streams=1, threads=2, render_filter=1))
+    pipe = nm.SlicePipeline(nm.PipelineConfig(batch_size=1, streams=1, threads=2, render_filter=1,
+                                              jpeg_sampling=sampling))
     gpu, ref = pipe.run_array(raw, meta), pipe.golden(raw, meta)
     assert gpu["jpegs"][0] == ref["jpeg_original"] and gpu["jpegs"][4] == ref["jpeg_processed"]
     out = str(tmp_path / "o")
     items = _items(native, cohort_root, out)[:30]
-    cfg = nm.PipelineConfig(batch_size=8, streams=2, threads=4, render_filter=1)
+    cfg = nm.PipelineConfig(batch_size=8, streams=2, threads=4, render_filter=1, jpeg_sampling=sampling)
     st, _ = native.Engine(cfg.engine_config()).run(items)
     assert all(c == 0 for c, _ in st)
     for f, od in items[::7]:
