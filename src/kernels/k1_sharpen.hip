@@ -62,7 +62,7 @@ __global__ __launch_bounds__(256) void sharpen_band_kernel(const uint16_t* __res
   static_assert(CS % 4 == 2, "pair alignment");
   __shared__ __attribute__((aligned(16))) float C[CH * CS];
   __shared__ __attribute__((aligned(16))) float T[TH * CS];
-  const TileDesc t = tiles[blockIdx.x];
+  const TileDesc t = tiles[xcd_tile(blockIdx.x, gridDim.x)];
   const SliceDesc d = descs[t.slice];
   const int x0 = t.tx * TW, y0 = t.ty * TH;
   const int W = d.w, H = d.h;

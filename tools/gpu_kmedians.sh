@@ -28,4 +28,5 @@ for r in $(seq ${ROUNDS:-2}); do
     i=$((i + 1))
   done
 done
-cat $O/summary.txt
+
+python tools/kernel_medians.py --summary $O/summary.txt
