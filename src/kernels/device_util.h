@@ -121,14 +121,4 @@ __device__ __forceinline__ uint64_t wave_transpose64(uint64_t x, int lane) {
   return x;
 }
 
-// XCD-aware tile order: the dispatcher deals workgroups round-robin over the 8 XCDs (workgroup b runs on
-// XCD b mod 8), so mapping b to logical tile (b mod 8)·⌈n/8⌉ + b/8 (remainder-adjusted) gives each XCD a
-// contiguous run of tiles, whose shared halo rows then hit that XCD's L2. A bijection on [0, n).
-// Used by K1b (sharpen: 20.4 → 19.0 µs per 96-slice batch); K1a's median got slower with it
-// (28.4 → 29.8 µs), so it keeps the plain order (profiles/r5/xcd/).
-__device__ __forceinline__ uint32_t xcd_tile(uint32_t b, uint32_t n) {
-  const uint32_t x = b & 7u, k = b >> 3, q = n >> 3, r = n & 7u;
-  return (x < r ? x * (q + 1u) : r * (q + 1u) + (x - r) * q) + k;
-}
-
 }  // namespace nm03::gpu

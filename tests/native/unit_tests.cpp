@@ -28,6 +28,7 @@
 #include "nm03/comm.h"
 #include "nm03/dicom.h"
 #include "nm03/golden.h"
+#include "nm03/gpu_types.h"
 #include "nm03/jpeg.h"
 #include "nm03/jpeg_common.h"
 #include "nm03/numa.h"
@@ -383,6 +384,26 @@ TEST(jpeg_container) {
   for (size_t i = hdr.size(); i + 2 < j.size(); ++i)
     if (j[i] == 0xFF && j[i + 1] != 0x00) ok = false;
   CHECK(ok);
+}
+
+TEST(xcd_tile_order_is_a_bijection) {
+  // Every grid size: each workgroup gets a distinct tile, all tiles are covered, and the workgroups
+  // of one XCD (b mod 8) take a contiguous run.
+  for (uint32_t n = 1; n <= 2100; ++n) {
+    std::vector<int> seen(n, 0);
+    std::vector<uint32_t> lo(8, UINT32_MAX), hi(8, 0), cnt(8, 0);
+    for (uint32_t b = 0; b < n; ++b) {
+      const uint32_t t = nm03::gpu::xcd_tile(b, n);
+      CHECK(t < n);
+      ++seen[t];
+      lo[b & 7] = std::min(lo[b & 7], t);
+      hi[b & 7] = std::max(hi[b & 7], t);
+      ++cnt[b & 7];
+    }
+    for (uint32_t t = 0; t < n; ++t) CHECK(seen[t] == 1);
+    for (int x = 0; x < 8; ++x)
+      if (cnt[x]) CHECK(hi[x] - lo[x] + 1 == cnt[x]);
+  }
 }
 
 TEST(fdct_dot_form_bit_equal) {
