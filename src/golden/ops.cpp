@@ -112,7 +112,10 @@ std::vector<float> vector_median(const std::vector<float>& img, int w, int h, in
   return out;
 }
 
-std::vector<float> sharpen(const std::vector<float>& img, int w, int h, float gain, float sigma, int mask) {
+// Contract order shared with K1b: vertical pass, then horizontal, taps ascending, each tap one fused
+// multiply-add (IEEE fma: one rounding, so host and v_pk_fma_f32 agree bit for bit).
+__attribute__((target("fma"))) std::vector<float> sharpen(const std::vector<float>& img, int w, int h, float gain,
+                                                          float sigma, int mask) {
   float g[64];
   gaussian_taps(sigma, mask, g);
   const int R = mask / 2;
@@ -121,8 +124,7 @@ std::vector<float> sharpen(const std::vector<float>& img, int w, int h, float ga
     for (int x = 0; x < w; ++x) {
       float acc = 0.0f;
       for (int i = -R; i <= R; ++i) {
-        float t = g[i + R] * img[(size_t)clampi(y + i, 0, h - 1) * w + x];
-        acc = acc + t;
+        acc = std::fma(g[i + R], img[(size_t)clampi(y + i, 0, h - 1) * w + x], acc);
       }
       tmp[(size_t)y * w + x] = acc;
     }
@@ -130,8 +132,7 @@ std::vector<float> sharpen(const std::vector<float>& img, int w, int h, float ga
     for (int x = 0; x < w; ++x) {
       float acc = 0.0f;
       for (int j = -R; j <= R; ++j) {
-        float t = g[j + R] * tmp[(size_t)y * w + clampi(x + j, 0, w - 1)];
-        acc = acc + t;
+        acc = std::fma(g[j + R], tmp[(size_t)y * w + clampi(x + j, 0, w - 1)], acc);
       }
       const float c = img[(size_t)y * w + x];
       out[(size_t)y * w + x] = sharpen_combine(c, acc, gain);

@@ -11,10 +11,10 @@
 //     pairs held in registers (each LDS value read once instead of 2R+1 times);
 //  3. horizontal pass + combine + band: a thread owns 16 columns of a row (register window of
 //     overlapping pairs); the band bits of the four 16-column segments form the row's mask word.
-// Both passes compute two outputs per packed f32 instruction.
+// Both passes compute two outputs per packed f32 instruction (one v_pk_fma_f32 per tap).
 // The Gaussian is applied separably in the contract order of golden::sharpen (vertical, then
-// horizontal, taps ascending, no FMA contraction), so the result is bit-identical to the CPU
-// golden model.
+// horizontal, taps ascending, one fma per tap; no implicit contraction anywhere), so the result is
+// bit-identical to the CPU golden model.
 #include <hip/hip_runtime.h>
 
 #include <type_traits>
@@ -28,7 +28,7 @@ namespace nm03::gpu {
 
 constexpr int kMaxR = 7;
 
-// Two adjacent f32 in one register pair: the stencil passes run on packed f32 (v_pk_mul_f32 /
+// Two adjacent f32 in one register pair: the stencil passes run on packed f32 (v_pk_fma_f32 /
 // v_pk_add_f32, per-lane IEEE rounding, so results are those of the scalar ops).
 //
 // LDS layout: row stride CS ≡ 2 (mod 4) dwords, so every even column pair is 8-byte aligned and
@@ -41,6 +41,10 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ f32x2 lds_pair(const float* p) { return f32x2{p[0], p[1]}; }
 __device__ __forceinline__ f32x2 lds_pair_a(const float* p) { return *reinterpret_cast<const f32x2*>(p); }
 __device__ __forceinline__ void lds_store_pair(float* p, f32x2 v) { *reinterpret_cast<f32x2*>(p) = v; }
+// One tap on two outputs: v_pk_fma_f32 (IEEE fma per lane, as std::fma in golden::sharpen).
+__device__ __forceinline__ f32x2 pk_fma(float t, f32x2 v, f32x2 acc) {
+  return __builtin_elementwise_fma(f32x2{t, t}, v, acc);
+}
 static_assert(kShpTileW == 64 && kShpTileH == 64, "sharpen tile is 64x64");
 
 template <int R>
@@ -187,7 +191,7 @@ __global__ __launch_bounds__(256) void sharpen_band_kernel(const uint16_t* __res
   __syncthreads();
 
   // ---- 2. vertical pass: columns (c, c+1), rows [r0, r0 + RB) from a register window of
-  //         column pairs; every tap is one v_pk_mul_f32 + one v_pk_add_f32 for two outputs --------
+  //         column pairs; every tap is one v_pk_fma_f32 for two outputs ------------------------------
   constexpr int CP = CW / 2;  // CW = 64 + 2R is even
   // Task → (block, pair): the first 32·NB tasks take pairs 0..31 (a 16-lane group of a b64 access
   // stays inside one row block: conflict-free), the (CP − 32)·NB remaining pairs follow.
@@ -211,10 +215,7 @@ __global__ __launch_bounds__(256) void sharpen_band_kernel(const uint16_t* __res
     for (int rr = 0; rr < RB; ++rr) {
       f32x2 acc = 0.0f;
 #pragma unroll
-      for (int k = 0; k <= 2 * R; ++k) {
-        const f32x2 p = pc.taps[k] * win[rr + k];
-        acc = acc + p;
-      }
+      for (int k = 0; k <= 2 * R; ++k) acc = pk_fma(pc.taps[k], win[rr + k], acc);
       lds_store_pair(T + (r0 + rr) * CS + c, acc);
     }
   }
@@ -241,10 +242,7 @@ __global__ __launch_bounds__(256) void sharpen_band_kernel(const uint16_t* __res
     for (int j = 0; j < 16; j += 2) {
       f32x2 acc = 0.0f;
 #pragma unroll
-      for (int k = 0; k <= 2 * R; ++k) {
-        const f32x2 p = pc.taps[k] * pw[j + k];
-        acc = acc + p;
-      }
+      for (int k = 0; k <= 2 * R; ++k) acc = pk_fma(pc.taps[k], pw[j + k], acc);
       // sharpen_combine (pixel_math.h) on both lanes: s = c + gain·(c − b), same rounding steps.
       const float* cp = C + (r + R) * CS + 16 * seg + j + R;
       f32x2 cv;
