@@ -2,8 +2,9 @@
 // both are monotone), ImageSharpening (9×9 Gaussian unsharp mask, main_sequential.cpp:208-210)
 // and the SeededRegionGrowing band test [0.74, 0.91] (main_sequential.cpp:232-233).
 //
-// One workgroup = 256 threads = a 64×64 output tile; the mask radius R is a template parameter
-// (compile-time tile geometry: no runtime divisions in the index math).
+// One workgroup = 256 threads = two 64×64 output tiles in turn (the second tile's loads issued with
+// the first's); the mask radius R is a template parameter (compile-time tile geometry: no runtime
+// divisions in the index math).
 //  1. the clamp-to-edge (64+2R)² input tile is loaded in 8-byte groups of 4 median keys
 //     (per-key clamped loads only where a group leaves the image), normalised+clipped once per
 //     key and kept in LDS as f32;
