@@ -11,9 +11,20 @@
 // PROBE_PREDLOPEN=1: a second thread dlopens libamd_comgr (the HIP runtime's code-object library,
 // ≈ 8 ms to load) at start, while the main thread runs hipInit; the probe also prints after which
 // phase the library is mapped.
+// PROBE_SAMPLE=1: a 200 µs wall-clock timer on the main thread samples the interrupted PC during
+// hipInit; the probe prints hipInit's time and the top library:symbol locations (slow vs fast mode).
 #include <hip/hip_runtime_api.h>
 
 #include <dlfcn.h>
+#include <signal.h>
+#include <sys/syscall.h>
+#include <time.h>
+#include <ucontext.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <map>
+#include <string>
 
 #include <chrono>
 #include <cstdio>
@@ -36,6 +47,55 @@ static bool comgr_mapped() {
   return m;
 }
 
+static void* g_pcs[8192];
+static volatile int g_npc = 0;
+static void on_sample(int, siginfo_t*, void* uc) {
+  const int i = g_npc;
+  if (i < 8192) {
+    g_pcs[i] = (void*)((ucontext_t*)uc)->uc_mcontext.gregs[REG_RIP];
+    g_npc = i + 1;
+  }
+}
+struct Sampler {
+  timer_t tm{};
+  bool on = false;
+  void start() {
+    struct sigaction sa{};
+    sa.sa_sigaction = on_sample;
+    sa.sa_flags = SA_SIGINFO | SA_RESTART;
+    sigaction(SIGRTMIN, &sa, nullptr);
+    sigevent ev{};
+    ev.sigev_notify = SIGEV_THREAD_ID;
+    ev.sigev_signo = SIGRTMIN;
+    ev._sigev_un._tid = (pid_t)syscall(SYS_gettid);
+    if (timer_create(CLOCK_MONOTONIC, &ev, &tm) != 0) return;
+    itimerspec it{};
+    it.it_interval.tv_nsec = it.it_value.tv_nsec = 200000;
+    timer_settime(tm, 0, &it, nullptr);
+    on = true;
+  }
+  void stop(double init_ms) {
+    if (!on) return;
+    timer_delete(tm);
+    std::map<std::string, int> hist;
+    for (int i = 0; i < g_npc; ++i) {
+      Dl_info di{};
+      std::string k = "?";
+      if (dladdr(g_pcs[i], &di) && di.dli_fname) {
+        const char* b = std::strrchr(di.dli_fname, '/');
+        k = std::string(b ? b + 1 : di.dli_fname) + ":" + (di.dli_sname ? di.dli_sname : "?");
+      }
+      ++hist[k];
+    }
+    std::vector<std::pair<int, std::string>> v;
+    for (auto& e : hist) v.push_back({e.second, e.first});
+    std::sort(v.rbegin(), v.rend());
+    std::printf("sample hipInit %.1f ms, %d samples:", init_ms, (int)g_npc);
+    for (size_t i = 0; i < v.size() && i < 8; ++i) std::printf(" | %d %s", v[i].first, v[i].second.substr(0, 60).c_str());
+    std::printf("\n");
+  }
+};
+
 int main(int argc, char** argv) {
   const int ns = argc > 1 ? std::atoi(argv[1]) : 5;
   const int nt = argc > 2 ? std::atoi(argv[2]) : 1;
@@ -50,10 +110,15 @@ int main(int argc, char** argv) {
       t_pre = now_ms() - a;
     });
   const bool mapped0 = comgr_mapped();
+  Sampler smp;
+  const bool sample = std::getenv("PROBE_SAMPLE") && std::atoi(std::getenv("PROBE_SAMPLE"));
+  const double ti = now_ms();
+  if (sample) smp.start();
   if (hipInit(0) != hipSuccess || hipSetDevice(0) != hipSuccess) return 1;
   void* p = nullptr;
   (void)hipMalloc(&p, 4096);
   const double t1 = now_ms();
+  if (sample) smp.stop(t1 - ti);
   const bool mapped1 = comgr_mapped();
   if (pre_th.joinable()) pre_th.join();
   std::vector<hipStream_t> st(ns, nullptr);
