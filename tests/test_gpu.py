@@ -73,14 +73,17 @@ def test_sharpen_band_vs_golden_and_torch(native):
     p = native.PipelineParams()
     c = native.golden_norm_clip(mk, "u16", 16, 1.0, 0.0, p)
     gs = native.golden_sharpen(c, 2.0, 0.5, 9, False)
-    assert np.array_equal(s, gs)  # bit-exact: same separable order, no FMA contraction
+    assert np.array_equal(s, gs)  # bit-exact: same separable order, one fma per tap on both sides
     ref = R.sharpen(torch.from_numpy(c)).numpy()
     assert np.abs(s - ref).max() < 2e-6
     assert np.array_equal(band.cpu().numpy(), (gs >= np.float32(0.74)) & (gs <= np.float32(0.91)))
 
 
-def test_sharpen_band_odd_size_rescale(native):
-    raw = _phantom(native, 150, 203)
+@pytest.mark.parametrize("shape", [(150, 203), (64, 320), (64, 130)])
+def test_sharpen_band_odd_size_rescale(native, shape):
+    """Odd widths (per-pixel staging) and odd tile counts (a workgroup takes two 64×64 tiles; the
+    last one may have a single tile)."""
+    raw = _phantom(native, *shape)
     mk = native.golden_median_u16(raw, 7)
     t = torch.from_numpy(mk.view(np.int16)).cuda()
     s, band = ops.sharpen_band(t, slope=1.25, intercept=-40.0)
@@ -88,6 +91,21 @@ def test_sharpen_band_odd_size_rescale(native):
     c = native.golden_norm_clip(mk, "u16", 16, 1.25, -40.0, p)
     gs = native.golden_sharpen(c, 2.0, 0.5, 9, False)
     assert np.array_equal(s.cpu().numpy(), gs)
+
+
+def test_sharpen_band_batched_odd_tile_count(native):
+    """3 slices × 3 tiles: workgroups whose two tiles belong to different slices, and a last
+    workgroup with one tile."""
+    raws = [_phantom(native, 64, 192) for _ in range(3)]
+    raws[1] = raws[1][:, ::-1].copy()
+    raws[2] = (raws[2] // 2).astype(np.uint16)
+    mks = np.stack([native.golden_median_u16(r, 7) for r in raws])
+    s, band = ops.sharpen_band(torch.from_numpy(mks.view(np.int16)).cuda())
+    p = native.PipelineParams()
+    for i in range(3):
+        gs = native.golden_sharpen(native.golden_norm_clip(mks[i], "u16", 16, 1.0, 0.0, p), 2.0, 0.5, 9, False)
+        assert np.array_equal(s[i].cpu().numpy(), gs)
+        assert np.array_equal(band[i].cpu().numpy(), (gs >= np.float32(0.74)) & (gs <= np.float32(0.91)))
 
 
 # ---------------------------------------------------------------------------------------------
