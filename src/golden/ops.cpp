@@ -113,9 +113,11 @@ std::vector<float> vector_median(const std::vector<float>& img, int w, int h, in
 }
 
 // Contract order shared with K1b: vertical pass, then horizontal, taps ascending, each tap one fused
-// multiply-add (IEEE fma: one rounding, so host and v_pk_fma_f32 agree bit for bit).
-__attribute__((target("fma"))) std::vector<float> sharpen(const std::vector<float>& img, int w, int h, float gain,
-                                                          float sigma, int mask) {
+// multiply-add (IEEE fma: one rounding, so host and v_pk_fma_f32 agree bit for bit). Hosts without
+// FMA3 run the default clone, whose std::fma is libm's correctly rounded one: the same results.
+__attribute__((target_clones("fma", "default"))) std::vector<float> sharpen(const std::vector<float>& img, int w,
+                                                                            int h, float gain, float sigma,
+                                                                            int mask) {
   float g[64];
   gaussian_taps(sigma, mask, g);
   const int R = mask / 2;
