@@ -88,7 +88,9 @@ def parse_args(argv=None):
                     help="which figure is the headline value (default strong: BASELINE config 3, one cohort "
                          "sharded over the ranks); the other is reported next to it")
     ap.add_argument("--no-secondary", action="store_true", help="skip the other scaling mode's measurement")
-    ap.add_argument("--wipe-passes", type=int, default=20,
+    # 150 wipe passes ≈ 0.3-0.7 s timed (20 passes were 43 ms: one 10 ms hiccup or the reaper's final
+    # drain moved the figure by 25-40%).
+    ap.add_argument("--wipe-passes", type=int, default=150,
                     help="also time this many passes that each first wipe their output directories (the "
                          "reference's per-run rm -rf; reported as config.wipe_each_pass; 0 = skip)")
     # 96 slices × 4 slots: 5 batches per 465-slice pass instead of 8 at 64 × 6; won 10 of 11
@@ -147,6 +149,11 @@ def parse_args(argv=None):
                          "reported as config.cli_wall (0 = skip)")
     ap.add_argument("--numa-data", choices=("auto", "off"), default="auto",
                     help="auto: one input copy per NUMA node, each rank reads the copy on its GPU's node")
+    ap.add_argument("--cpu-profile", default="",
+                    help="sample the host CPU over the headline's timed steps (cpu_sampler.h) into PATH.rank<r>; "
+                         "symbolise with tools/cpu_profile.py")
+    ap.add_argument("--cpu-profile-period-us", type=int, default=250,
+                    help="one sample per this much process CPU time (--cpu-profile)")
     return ap.parse_args(argv)
 
 
@@ -326,7 +333,7 @@ def run_rank(args):
             hi = len(items) // args.emulate_shard_of  # rank 0's share of an N-rank job
         return localize_items(items[lo:hi], roots[0], local_root), len(items)
 
-    def measure(scaling, out_root, steps, warmup, wipe=False):
+    def measure(scaling, out_root, steps, warmup, wipe=False, profile=""):
         mine, global_items = shard(scaling, out_root)
         work = n.WorkList(mine)  # the shard's work list in native form (built once, like the plan)
         # Pipelined passes rotate over `depth` output trees: runs in flight never write the same
@@ -407,6 +414,8 @@ def run_rank(args):
         cg0 = cgroup_cpu_stat()
         ru0 = resource.getrusage(resource.RUSAGE_SELF)
         th0 = thread_cpu_by_name()
+        if profile and not n.cpu_profile_start(args.cpu_profile_period_us):
+            raise SystemExit(f"rank {rank}: cannot start the CPU sampler")
         t0 = time.perf_counter()
         if stream is not None:
             with _roctx_range("bench.steps"):
@@ -425,6 +434,9 @@ def run_rank(args):
         if reaper is not None:
             reaper.drain()  # the timed passes' deletions are part of their cost
         t_own = time.perf_counter() - t0  # this rank's own time, before waiting for the others
+        if profile:
+            nsamp = n.cpu_profile_stop(f"{profile}.rank{rank}")
+            print(f"bench: rank {rank}: {nsamp} CPU samples -> {profile}.rank{rank}", file=sys.stderr, flush=True)
         if torch.cuda.is_available():
             torch.cuda.synchronize()
         comm.barrier()
@@ -491,7 +503,7 @@ def run_rank(args):
         times.sort()
         return round(times[len(times) // 2] * 1e3, 4), round(times[0] * 1e3, 4)
 
-    primary = measure(args.scaling, args.out_root, args.steps, args.warmup)
+    primary = measure(args.scaling, args.out_root, args.steps, args.warmup, profile=args.cpu_profile)
     len_mine_primary = [primary["per_rank"]["slices"][rank] / args.steps]
     secondary = None
     other = "strong" if args.scaling == "weak" else "weak"
@@ -573,6 +585,7 @@ def run_rank(args):
                                                            if (args.scaling == "weak" or world == 1) else "wipe + mkdir",
                                                "ms_per_step": round(wiped["ms_per_step"], 3),
                                                "steps": args.wipe_passes,
+                                               "timed_s": round(wiped["ms_per_step"] * args.wipe_passes / 1e3, 4),
                                                "rank0_process_cpu_ms_per_step": wiped["rank0_process_cpu_ms_per_step"],
                                                "cgroup_cpu_ms_per_step": wiped["cgroup_cpu_ms_per_step"],
                                                "wipe_mode": args.wipe_mode,

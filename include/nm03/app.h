@@ -7,7 +7,9 @@
 // out-*/PGBM-XXXX/<stem>_{original,processed}.jpg and no-argument defaults.
 #pragma once
 
+#include <atomic>
 #include <condition_variable>
+#include <functional>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -21,15 +23,25 @@ namespace nm03::app {
 
 // A CLI's cold start: one start-up thread, begun at construction, owns every HIP call until the engine
 // exists — hipInit, every kernel code object, `nstreams` reserved streams plus the copy engine's first
-// use, `comm->start_data_plane()` (RCCL ranks) — and then builds the engine from the configuration
-// the caller hands to build() once it is known (the caller plans meanwhile). Destruction without
-// build() cancels and joins.
+// use — then, for RCCL ranks, starts AND settles the data plane (`comm->start_data_plane()`,
+// `settle_data_plane()`: RCCL is up before the engine's construction begins, never concurrent with
+// it), and then builds the engine from the configuration the caller hands to build() once it is
+// known (the caller plans meanwhile). A failed HIP start-up is published to the peers
+// (`fail_data_plane`) so that they do not wait for this rank's RCCL. Destruction without build()
+// cancels (an unsettled data plane is abandoned) and joins.
 class EngineStartup {
  public:
   struct Times {
-    double hip_init_s = 0, kernel_load_s = 0, streams_s = 0, engine_ctor_s = 0;
+    double hip_init_s = 0, kernel_load_s = 0, streams_s = 0, data_plane_s = 0, config_wait_s = 0, engine_ctor_s = 0;
+  };
+  // What the start-up thread does, in order; the CLI's are HIP calls (the device constructor),
+  // tests inject fakes (tests/native/unit_tests.cpp, run under TSan by tools/sanitize_check.sh).
+  struct Hooks {
+    std::function<void(Times&)> prepare;                                  // throws on failure
+    std::function<std::unique_ptr<Engine>(const EngineConfig&)> build;    // throws on failure
   };
   EngineStartup(int device, int nstreams, Comm* comm = nullptr);
+  EngineStartup(Hooks hooks, Comm* comm);
   ~EngineStartup();
   EngineStartup(const EngineStartup&) = delete;
   EngineStartup& operator=(const EngineStartup&) = delete;
@@ -38,9 +50,11 @@ class EngineStartup {
   const Times& times() const { return times_; }  // valid after build()
 
  private:
+  void start(Hooks hooks, Comm* comm);
   std::mutex m_;
   std::condition_variable cv_;
   bool have_cfg_ = false, cancel_ = false, done_ = false;
+  std::atomic<bool> cancel_flag_{false};  // cancel_, readable by the data plane's settle loop
   EngineConfig ec_;
   std::unique_ptr<Engine> engine_;
   std::string error_;

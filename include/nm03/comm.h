@@ -24,6 +24,7 @@
 // for the CLI launcher's supervised ranks unless the variable is set.
 #pragma once
 
+#include <atomic>
 #include <cstddef>
 #include <cstdint>
 #include <functional>
@@ -86,20 +87,36 @@ class Comm {
   // ncclCommInitRankConfig. Every collective does it first anyway; no-op for the host comms.
   virtual void ready() {}
 
-  // ---- deferred data plane (launch_ranks' RCCL ranks, make_deferred_rccl_comm; no-ops elsewhere) --
+  // Non-blocking readiness of a transport whose initialisation was started without settling it
+  // (make_rccl_comm settle_now=false): true once usable; throws CommError when it failed.
+  virtual bool poll_ready() { return true; }
+  // Abandons the transport without a collective (ncclCommAbort): a peer could not bring it up.
+  virtual void abort_transport() {}
+
+  // ---- deferred data plane (launch_ranks' RCCL ranks, make_deferred_comm; no-ops elsewhere) -----
   // Starts the device transport's initialisation (the ncclUniqueId hand-off through the segment and
   // a non-blocking ncclCommInitRankConfig) on the calling thread, which must already have brought up
-  // HIP on the rank's device, and returns: RCCL's start-up then overlaps the engine's construction
-  // and the run instead of preceding the rank's planning. Errors surface at promote().
+  // HIP on the rank's device. Errors are published to the peers through the segment at once and
+  // surface at promote().
   virtual void start_data_plane() {}
+  // After start_data_plane(), on the same thread: waits (bounded, abort- and `cancel`-aware) until
+  // this rank's transport is usable or some rank's start failed (then it is abandoned, and every
+  // rank learns it through the segment instead of waiting for a peer that never joins). The CLI's
+  // start-up thread settles RCCL here, BEFORE it builds the engine: RCCL's initialisation never
+  // overlaps the engine's construction or its launches.
+  virtual void settle_data_plane(const std::atomic<bool>* cancel = nullptr) { (void)cancel; }
+  // This rank cannot start its data plane (e.g. its HIP start-up failed): tells the peers through the
+  // segment (rank 0 also unblocks their wait for the unique id) so that they fall back at once.
+  virtual void fail_data_plane(const std::string& why) { (void)why; }
   // Collective (every rank at the same point): waits (bounded, abort-aware) until the device
   // transport is up and carries every later collective on it. Before it, host-buffer collectives
   // use the shared-memory control plane; device-memory ones promote implicitly.
   virtual void promote() {}
   struct DataPlaneTimes {
     double start_s = -1;      // start_data_plane's begin, seconds after the comm was created (-1: never)
+    double settle_s = 0;      // time settle_data_plane() waited for the transport (start-up thread)
     double wait_s = 0;        // time promote() blocked waiting for the transport
-    double init_upper_s = 0;  // start → transport usable, upper bound (observed at promote)
+    double init_upper_s = 0;  // start → transport usable, upper bound (observed at settle or promote)
   };
   virtual DataPlaneTimes data_plane_times() const { return {}; }
   // Non-empty when promote() found the device transport unusable on some rank and every rank stayed
@@ -145,10 +162,15 @@ class ShmSegment {
   void check_abort(int self) const;
 
   // RCCL unique id (128 bytes) published by rank 0, awaited by the others (deadline + abort).
-  // publish_uid_failed: rank 0 could not create one; waiters throw at once instead of timing out.
+  // publish_uid_failed: rank 0 could not create one; waiters throw at once instead of timing out
+  // (so do they when some rank marked its data plane failed).
   void publish_uid(const std::vector<uint8_t>& uid);
   void publish_uid_failed();
   std::vector<uint8_t> wait_uid(int self, double timeout_s) const;
+  // Data-plane start-up failure of some rank (the first one is recorded): peers settling their own
+  // transport abandon it instead of waiting for a rank that never joins. Not a job abort.
+  void mark_data_plane_failed(int rank);
+  int data_plane_failed_rank() const;  // -1 when no rank failed
 
   // Generation barrier across all ranks of the segment; deadline + abort aware.
   void barrier(int self, double timeout_s);
@@ -177,10 +199,22 @@ std::unique_ptr<Comm> make_host_comm(std::shared_ptr<ShmSegment> seg, int rank, 
 std::unique_ptr<Comm> make_rccl_comm(int rank, int size, const std::vector<uint8_t>& unique_id, int device,
                                      std::shared_ptr<ShmSegment> seg = nullptr, double timeout_s = -1,
                                      bool settle_now = true);
+// How a deferred communicator makes its data plane: rank 0's unique id, and every rank's transport
+// from it (initialisation started, not settled). rccl_data_plane(): RCCL. Tests inject fakes that
+// succeed, fail, stall or never become ready on chosen ranks (tests/native/unit_tests.cpp).
+struct DataPlaneFactory {
+  std::function<std::vector<uint8_t>()> unique_id;
+  std::function<std::unique_ptr<Comm>(int rank, int size, const std::vector<uint8_t>& uid, int device,
+                                      std::shared_ptr<ShmSegment> seg, double timeout_s)>
+      make;
+};
+DataPlaneFactory rccl_data_plane();
 // The communicator launch_ranks gives an RCCL rank: the shared-memory control plane (host comm over
-// `seg`) for the start-up collectives, RCCL created by start_data_plane() — on the rank's start-up
-// thread, right after hipInit — and used from promote() on and for every device collective. Keeps
-// RCCL's initialisation off the critical path of a cold run.
+// `seg`) for the start-up collectives, the data plane created by start_data_plane() and settled by
+// settle_data_plane() — both on the rank's start-up thread, after hipInit and before the engine is
+// built — and used from promote() on and for every device collective.
+std::unique_ptr<Comm> make_deferred_comm(int rank, int size, int device, std::shared_ptr<ShmSegment> seg,
+                                         double timeout_s, DataPlaneFactory factory);
 std::unique_ptr<Comm> make_deferred_rccl_comm(int rank, int size, int device, std::shared_ptr<ShmSegment> seg,
                                               double timeout_s = -1);
 std::vector<uint8_t> rccl_unique_id();
@@ -191,7 +225,9 @@ std::unique_ptr<Comm> make_self_comm();
 // ---- launcher ----------------------------------------------------------------------------------
 struct LaunchOptions {
   // "rccl" | "host" | "auto" (default; NM03_COMM overrides): RCCL when every rank has its own
-  // GPU, the host comm when ranks share one (device_override ≥ 0).
+  // GPU, the host comm when ranks share one (device_override ≥ 0). An explicit "rccl" also gives a
+  // single-rank job the deferred RCCL communicator (one rank, no fork): the multi-rank start-up,
+  // settle and promotion path, exercisable on a one-GPU box.
   std::string comm = "auto";
   // ≥ 0: every rank uses this HIP device (NM03_DEVICE_OVERRIDE), e.g. N ranks on a one-GPU box.
   int device_override = -1;

@@ -67,8 +67,9 @@ void usage(const std::string& which) {
             << "  --json FILE            write run metrics as JSON\n"
             << "  --resume               keep existing outputs; skip slices whose two JPEGs exist\n"
             << "  --frame K              import frame K of multi-frame DICOM files (default: reject them)\n"
-            << "  --hw-queues N|auto     HIP hardware queues of this process (GPU_MAX_HW_QUEUES; auto: 1 for short jobs on\n"
-            << "                         shader copies, else 2; 0 = environment)\n"
+            << "  --hw-queues N|auto     HIP hardware queues of this process (GPU_MAX_HW_QUEUES, 1..32; auto: 1 for short\n"
+            << "                         2D jobs on shader copies unless the environment chose a value, else unchanged;\n"
+            << "                         0 = environment)\n"
             << "  --copy-engine auto|sdma|blit  host<->GPU copies: DMA engines or shader copies (auto: blit for\n"
             << "                         2D jobs of <= 4096 slices per rank, whose cold start the DMA queue's set-up dominates)\n"
             << "  --quiet                suppress per-slice progress lines\n"
@@ -191,7 +192,14 @@ AppConfig parse_args(int argc, char** argv, const std::string& which) {
     else if (a == "--frame") c.engine.pipe.frame = std::atoi(val().c_str());
     else if (a == "--hw-queues") {
       const std::string v = val();
-      c.hw_queues = v == "auto" ? -1 : std::max(0, std::atoi(v.c_str()));
+      char* end = nullptr;
+      const long q = v == "auto" ? -1 : std::strtol(v.c_str(), &end, 10);
+      if (v != "auto" && (end == v.c_str() || *end || q < 0 || q > 32)) {  // the runtime refuses more than 32
+        std::cerr << "--hw-queues must be auto or 0..32 (0 = leave GPU_MAX_HW_QUEUES as the environment sets it)"
+                  << std::endl;
+        std::exit(2);
+      }
+      c.hw_queues = (int)q;
     }
     else if (a == "--copy-engine") {
       const std::string v = val();
@@ -480,47 +488,74 @@ int scan_max_dim(const std::vector<PatientPlan>& plan, int threads) {
 
 // Cold start (round 5). ONE start-up thread owns every HIP call until the engine exists: it brings up
 // the runtime and the device context, loads every kernel code object, reserves the engine's streams
-// (HW queues) and brings up the copy engine, starts RCCL's non-blocking initialisation when a comm is
-// given (NM03_COMM=rccl), and —
-// as soon as the caller hands it the engine configuration (build()) — builds the whole engine: every
-// slot's events, pinned and device buffers. Meanwhile the calling thread plans (cohort discovery,
-// output wipe, header scan), exchanges the plan over the shared-memory control plane and computes the
-// rank's CPU partition. In round 4, slots built on their workers held the runtime's locks (HW-queue
-// creation 10–50 ms) while the first batch tried to copy and launch, and a cold 465-slice pass took
-// 37–70 ms instead of ≈ 4.5 ms (profiles/r5/cold/).
+// (HW queues) and brings up the copy engine, starts and settles RCCL when a comm is given (round 6:
+// settled BEFORE the engine is built, so RCCL's own threads never allocate, create streams or load
+// code objects while the engine is constructed or launches — the hazard class of round 4's HSA
+// fault), and — as soon as the caller hands it the engine configuration (build()) —
+// builds the whole engine: every slot's events, pinned and device buffers. Meanwhile the calling
+// thread plans (cohort discovery, output wipe, header scan), exchanges the plan over the
+// shared-memory control plane and computes the rank's CPU partition. In round 4, slots built on their
+// workers held the runtime's locks (HW-queue creation 10–50 ms) while the first batch tried to copy
+// and launch, and a cold 465-slice pass took 37–70 ms instead of ≈ 4.5 ms (profiles/r5/cold/).
 EngineStartup::EngineStartup(int device, int nstreams, Comm* comm) {
-  warm_ = std::thread([this, device, nstreams, comm] {
+  Hooks h;
+  h.prepare = [device, nstreams](Times& t) {
     const double t0 = now_s();
+    gpu::check_hip(hipSetDevice(device), "hipSetDevice");
+    void* p = nullptr;
+    gpu::check_hip(hipMalloc(&p, 4096), "hipMalloc");
+    (void)hipFree(p);
+    t.hip_init_s = now_s() - t0;
+    // The kernels' code objects (HIP would load each translation unit's at its first launch):
+    // loaded here, on one thread, before any launch (kernels.h preload_kernels).
+    const double t1 = now_s();
+    gpu::preload_kernels(/*with_volume=*/false);  // the 2D engine's code objects
+    t.kernel_load_s = now_s() - t1;
+    // The engine's streams (HW queues) need only the slot count: created before the configuration
+    // arrives, while rank 0 may still be planning.
+    t.streams_s = reserve_streams(device, nstreams);
+  };
+  h.build = [](const EngineConfig& ec) { return std::make_unique<Engine>(ec); };
+  start(std::move(h), comm);
+}
+
+EngineStartup::EngineStartup(Hooks hooks, Comm* comm) { start(std::move(hooks), comm); }
+
+void EngineStartup::start(Hooks hooks, Comm* comm) {
+  warm_ = std::thread([this, hooks = std::move(hooks), comm] {
     std::string err;
+    Times t;
     try {
-      gpu::check_hip(hipSetDevice(device), "hipSetDevice");
-      void* p = nullptr;
-      gpu::check_hip(hipMalloc(&p, 4096), "hipMalloc");
-      (void)hipFree(p);
-      times_.hip_init_s = now_s() - t0;
-      // The kernels' code objects (HIP would load each translation unit's at its first launch):
-      // loaded here, on one thread, before any launch (kernels.h preload_kernels).
-      const double t1 = now_s();
-      gpu::preload_kernels(/*with_volume=*/false);  // the 2D engine's code objects
-      times_.kernel_load_s = now_s() - t1;
-      // The engine's streams (HW queues) need only the slot count: created before the configuration
-      // arrives, while rank 0 may still be planning.
-      times_.streams_s = reserve_streams(device, nstreams);
+      hooks.prepare(t);
     } catch (const std::exception& e) {
       err = e.what();
     }
-    // RCCL's initialisation proceeds in its own thread from here on (non-blocking communicator); the
-    // collectives use the shared-memory control plane until promote().
-    if (err.empty() && comm) comm->start_data_plane();
+    if (comm) {
+      const double td = now_s();
+      if (err.empty()) {
+        // RCCL's non-blocking initialisation, settled here: every rank's start-up thread waits for
+        // its own communicator (or learns through the segment that some rank's failed) before any
+        // engine exists. Errors surface at promote(), where the ranks agree on them.
+        comm->start_data_plane();
+        comm->settle_data_plane(&cancel_flag_);
+      } else {
+        comm->fail_data_plane("rank start-up failed: " + err);  // peers stop waiting for this rank
+      }
+      t.data_plane_s = now_s() - td;
+    }
     std::unique_lock<std::mutex> g(m_);
+    times_ = t;
+    const double tw = now_s();
     cv_.wait(g, [&] { return have_cfg_ || cancel_; });
+    times_.config_wait_s = now_s() - tw;
     if (!cancel_ && err.empty()) {
       const EngineConfig ec = ec_;
       g.unlock();
       const double t2 = now_s();
       std::unique_ptr<Engine> e;
       try {
-        e = std::make_unique<Engine>(ec);
+        e = hooks.build(ec);
+        if (!e) err = "engine not built";
       } catch (const std::exception& ex) {
         err = ex.what();
       }
@@ -539,6 +574,7 @@ EngineStartup::~EngineStartup() {
     std::lock_guard<std::mutex> g(m_);
     cancel_ = true;
   }
+  cancel_flag_.store(true, std::memory_order_release);
   cv_.notify_all();
   if (warm_.joinable()) warm_.join();
 }
@@ -569,25 +605,28 @@ int parallel_rank(const AppConfig& cfg, int rank, int size, Comm& comm, int devi
   ec.device = device;
   const double t_setup = now_s();
   // Cold start (round 5). ONE start-up thread owns every HIP call until the engine exists: it
-  // brings up the runtime and the device context, loads the 2D kernels' code objects, starts RCCL's
-  // non-blocking initialisation (NM03_COMM=rccl only, see below), and — as soon as the main thread hands it the engine
-  // configuration — builds the whole engine: every slot's streams, events, pinned and device
+  // brings up the runtime and the device context, loads the 2D kernels' code objects, starts and
+  // settles RCCL (data-plane jobs only, see below), and — as soon as the main thread hands it the
+  // engine configuration — builds the whole engine: every slot's streams, events, pinned and device
   // buffers. Meanwhile the main thread plans (rank 0: patient discovery, output wipe, header scan),
   // exchanges the plan over the shared-memory control plane and computes the rank's CPU partition.
   // Nothing else touches HIP before the first batch: in round 4, slots built on their workers held
   // the runtime's locks (HW-queue creation 10–50 ms) while the first batch tried to copy and
   // launch, and a cold 465-slice pass took 37–70 ms instead of ≈ 4 ms (profiles/r5/cold/).
   // A 2D job's collectives are control data (the work list, counts, timing rows: a few KB in all).
-  // RCCL starts on the start-up thread and carries the collectives after the run (promote()) when
-  // the job is long enough to amortise bringing it up — more than kBlitMaxSlicesPerRank slices per
-  // rank (all --repeat passes), the same bound as the copy path — or when NM03_COMM=rccl asks for it;
-  // a short job stays on the node's shared-memory control plane and never waits for, or loads, RCCL
-  // (NM03_COMM=host: never). Device data exchange (--split-volume) brings RCCL up by itself.
+  // RCCL is brought up on the start-up thread — started and settled before the engine is built — and
+  // carries the collectives after the run (promote()) when the job is long enough to amortise it —
+  // more than kBlitMaxSlicesPerRank slices per rank (all --repeat passes), the same bound as the copy
+  // path — or when NM03_COMM=rccl asks for it (also at one rank: launch_ranks then gives the rank the
+  // deferred communicator); a short job stays on the node's shared-memory control plane and never
+  // waits for, or loads, RCCL (NM03_COMM=host: never). Device data exchange (--split-volume) brings
+  // RCCL up by itself.
   const char* comm_env = std::getenv("NM03_COMM");
   const std::string comm_mode = comm_env && *comm_env ? comm_env : "auto";
-  const bool data_plane = size > 1 && (comm_mode == "rccl" || (comm_mode == "auto" && work_per_rank > kBlitMaxSlicesPerRank));
+  const bool data_plane =
+      comm_mode == "rccl" || (size > 1 && comm_mode == "auto" && work_per_rank > kBlitMaxSlicesPerRank);
   EngineStartup su(device, std::max(1, cfg.engine.streams) + 1, data_plane ? &comm : nullptr);  // slots + upload stream
-  double engine_wait_s = 0;
+  double engine_wait_s = 0, plan_s = 0, setup_tail_s = 0;
   std::unique_ptr<Engine> engine_p;
   std::vector<RankDevice> devices;
   double t_start = 0, setup_s = 0;
@@ -692,6 +731,7 @@ int parallel_rank(const AppConfig& cfg, int rank, int size, Comm& comm, int devi
       // agree on it before going on.
       std::string setup_error;
       const double t_wait = now_s();
+      plan_s = t_wait - t_setup;
       engine_p = su.build(ec, &setup_error);
       engine_wait_s = now_s() - t_wait;
       if (!engine_p && setup_error.empty()) setup_error = "engine not built";
@@ -704,6 +744,7 @@ int parallel_rank(const AppConfig& cfg, int rank, int size, Comm& comm, int devi
       }
       t_start = now_s();
       setup_s = t_start - t_setup;
+      setup_tail_s = t_start - t_wait - engine_wait_s;
     }
     Engine& engine = *engine_p;
     if (fault_plan().rank_exit == rank && size > 1) {  // NM03_FAULT=rank_exit:<r>: a rank dies mid-job
@@ -840,7 +881,11 @@ int parallel_rank(const AppConfig& cfg, int rank, int size, Comm& comm, int devi
                              std::to_string(cfg.repeat) + ", \"engine_setup_s\": " +
                              fmt(setup_s) + ", \"hip_init_s\": " + fmt(su.times().hip_init_s) + ", \"engine_ctor_s\": " +
                              fmt(su.times().engine_ctor_s) + ", \"streams_s\": " + fmt(su.times().streams_s) + ", \"engine_wait_s\": " + fmt(engine_wait_s) + ", \"kernel_load_s\": " +
-                             fmt(su.times().kernel_load_s) + ", \"comm_start_s\": " + fmt(dp.start_s) + ", \"comm_wait_s\": " +
+                             fmt(su.times().kernel_load_s) + ", \"data_plane_s\": " + fmt(su.times().data_plane_s) +
+                             ", \"config_wait_s\": " + fmt(su.times().config_wait_s) + ", \"plan_s\": " + fmt(plan_s) +
+                             ", \"setup_tail_s\": " + fmt(setup_tail_s) + ", \"data_plane\": " +
+                             (data_plane ? "true" : "false") + ", \"comm_settle_s\": " + fmt(dp.settle_s) +
+                             ", \"comm_start_s\": " + fmt(dp.start_s) + ", \"comm_wait_s\": " +
                              fmt(dp.wait_s) + ", \"comm_init_s\": " + fmt(dp.init_upper_s) + ", \"wall_s\": " + fmt(tot) +
                              ", \"processing_wall_s\": " + fmt(proc_wall) + ", \"slices\": " + std::to_string(total_slices) +
                              ", \"slices_ok\": " + std::to_string(total_ok) + ", \"slices_per_s\": " +
@@ -929,8 +974,14 @@ bool apply_copy_engine(const AppConfig& cfg, int64_t slices_per_rank) {
   // With shader copies the copies need no queue of their own and a short job no concurrency between
   // slots: one HW queue saves the second queue's creation (streams 32–35 → 25–26 ms, processing
   // 4.6–5.0 vs 4.8–4.9 ms, profiles/r5/cold_exitq/; 9 interleaved pairs: engine wait 41.5 vs 45.9 ms,
-  // processing 5.1 vs 4.7 ms, profiles/r5/cold_hq/); longer jobs keep 2.
-  if (cfg.hw_queues < 0) setenv("GPU_MAX_HW_QUEUES", blit ? "1" : "2", 1);
+  // processing 5.1 vs 4.7 ms, profiles/r5/cold_hq/). Only that measured case is overridden: every
+  // other job (DMA copies, volumes, long jobs, whose start-up is amortised) keeps the environment's
+  // value, and so does a short job whose environment chose a value other than HIP's default of 4
+  // (the boxes export the default itself).
+  if (cfg.hw_queues < 0 && blit) {
+    const char* q = std::getenv("GPU_MAX_HW_QUEUES");
+    if (!q || !*q || std::string(q) == "4") setenv("GPU_MAX_HW_QUEUES", "1", 1);
+  }
   return blit;
 }
 

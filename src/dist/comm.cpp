@@ -410,6 +410,13 @@ LaunchOptions LaunchOptions::from_env() {
 
 int launch_ranks(int n, const std::function<int(int, int, Comm&)>& body, const LaunchOptions& opts) {
   if (n <= 1) {
+    if (opts.comm == "rccl") {
+      // An explicit RCCL request keeps the multi-rank communicator's life cycle (deferred start on
+      // the start-up thread, settle, promotion) at one rank, in this process.
+      auto seg = ShmSegment::create_anonymous(1);
+      auto c = make_deferred_rccl_comm(0, 1, opts.device_of(0), seg, opts.timeout_s);
+      return body(0, 1, *c);
+    }
     auto c = make_self_comm();
     return body(0, 1, *c);
   }

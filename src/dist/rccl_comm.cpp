@@ -9,7 +9,6 @@
 #include <unistd.h>
 
 #include <chrono>
-#include <condition_variable>
 #include <cstring>
 #include <exception>
 #include <mutex>
@@ -127,6 +126,23 @@ class RcclComm final : public Comm {
     settle("ncclCommInitRank");
     settled_ = true;
   }
+  bool poll_ready() override {
+    if (settled_) return true;
+    if (!comm_) throw CommError("RCCL communicator was aborted");
+    ncclResult_t ar = ncclSuccess;
+    const ncclResult_t q = rccl_api().ncclCommGetAsyncError(comm_, &ar);
+    if (q != ncclSuccess) fail(std::string("ncclCommInitRank: ncclCommGetAsyncError: ") + rccl_api().ncclGetErrorString(q));
+    if (ar == ncclInProgress) return false;
+    if (ar != ncclSuccess) fail(std::string("ncclCommInitRank: ") + rccl_api().ncclGetErrorString(ar));
+    settled_ = true;
+    return true;
+  }
+  void abort_transport() override {
+    if (comm_) {
+      (void)rccl_api().ncclCommAbort(comm_);
+      comm_ = nullptr;
+    }
+  }
   ~RcclComm() override { release(); }
   int rank() const override { return rank_; }
   int size() const override { return size_; }
@@ -178,6 +194,7 @@ class RcclComm final : public Comm {
     if (dst < 0) sbytes = 0;
     if (src < 0) rbytes = 0;
     if (!sbytes && !rbytes) return;
+    bind_device();
     ready();
     if (!comm_) throw CommError("RCCL communicator was aborted");
     if (seg_) seg_->check_abort(rank_);
@@ -188,6 +205,7 @@ class RcclComm final : public Comm {
     issue(rccl_api().ncclGroupEnd(), "ncclGroupEnd");
   }
   int64_t allreduce_sum_i64_device(int64_t* v, void* stream) override {
+    bind_device();
     ready();
     if (!comm_) throw CommError("RCCL communicator was aborted");
     if (seg_) seg_->check_abort(rank_);
@@ -229,7 +247,13 @@ class RcclComm final : public Comm {
     hip_ck(hipMemcpyAsync(v, d, bytes, hipMemcpyDeviceToHost, stream_), "D2H");
     wait("ncclAllReduce");
   }
+  // Collectives may run on any thread of the rank (the CLI's main thread never called hipSetDevice:
+  // the start-up thread owns the device until the engine exists): every entry point that makes HIP
+  // calls selects the communicator's device first, so staging buffers and copies land on it, not on
+  // the calling thread's default device 0.
+  void bind_device() { hip_ck(hipSetDevice(dev_), "hipSetDevice"); }
   uint8_t* stage(size_t bytes) {
+    bind_device();
     ready();
     if (!comm_) throw CommError("RCCL communicator was aborted");
     if (seg_) seg_->check_abort(rank_);
@@ -313,148 +337,6 @@ class RcclComm final : public Comm {
   bool settled_ = false;       // ncclCommInitRankConfig completed (ready())
 };
 
-// ---- deferred RCCL: shared-memory control plane until promote() ---------------------------------
-class DeferredRcclComm final : public Comm {
- public:
-  DeferredRcclComm(int rank, int size, int device, std::shared_ptr<ShmSegment> seg, double timeout_s)
-      : rank_(rank), size_(size), dev_(device), seg_(seg), timeout_(timeout_s > 0 ? timeout_s : comm_timeout_s()),
-        host_(make_host_comm(seg, rank, timeout_s)), t_created_(mono_s()) {}
-  int rank() const override { return rank_; }
-  int size() const override { return size_; }
-  const char* backend() const override { return fallback_ ? "host" : "rccl"; }
-
-  void broadcast(void* buf, size_t bytes, int root) override { plane().broadcast(buf, bytes, root); }
-  void allgather(const void* send, size_t bytes, void* recv) override { plane().allgather(send, bytes, recv); }
-  void allreduce_sum_i64(int64_t* v, size_t n) override { plane().allreduce_sum_i64(v, n); }
-  void allreduce_max_f64(double* v, size_t n) override { plane().allreduce_max_f64(v, n); }
-  void barrier() override { plane().barrier(); }
-  void sendrecv(const void* send, size_t sbytes, int dst, void* recv, size_t rbytes, int src) override {
-    plane().sendrecv(send, sbytes, dst, recv, rbytes, src);
-  }
-  // Device data always goes over RCCL (promoting implicitly: every rank reaches these together).
-  void sendrecv_device(const void* send, size_t sbytes, int dst, void* recv, size_t rbytes, int src,
-                       void* stream) override {
-    promote();
-    if (fallback_) return Comm::sendrecv_device(send, sbytes, dst, recv, rbytes, src, stream);  // staged, host plane
-    rccl_->sendrecv_device(send, sbytes, dst, recv, rbytes, src, stream);
-  }
-  int64_t allreduce_sum_i64_device(int64_t* v, void* stream) override {
-    promote();
-    if (fallback_) return Comm::allreduce_sum_i64_device(v, stream);
-    return rccl_->allreduce_sum_i64_device(v, stream);
-  }
-  bool device_native() const override { return !fallback_; }
-  int transport_size() const override { return promoted_ ? rccl_->transport_size() : -1; }
-  int transport_rank() const override { return promoted_ ? rccl_->transport_rank() : -1; }
-  int transport_device() const override { return promoted_ ? rccl_->transport_device() : -1; }
-  void ready() override { promote(); }
-
-  void start_data_plane() override {
-    {
-      std::lock_guard<std::mutex> g(m_);
-      if (state_ != kIdle) return;
-      state_ = kStarting;
-      t_start_ = mono_s();
-    }
-    std::unique_ptr<Comm> c;
-    std::exception_ptr err;
-    try {
-      std::vector<uint8_t> uid;
-      if (rank_ == 0) {
-        try {
-          uid = rccl_unique_id();
-        } catch (...) {
-          seg_->publish_uid_failed();  // the other ranks fail fast and agree on the fallback
-          throw;
-        }
-        seg_->publish_uid(uid);
-      } else {
-        uid = seg_->wait_uid(rank_, timeout_);
-      }
-      c = make_rccl_comm(rank_, size_, uid, dev_, seg_, timeout_, /*settle_now=*/false);
-    } catch (...) {
-      err = std::current_exception();
-    }
-    {
-      std::lock_guard<std::mutex> g(m_);
-      rccl_ = std::move(c);
-      err_ = err;
-      state_ = err ? kFailed : kStarted;
-    }
-    cv_.notify_all();
-  }
-
-  // Every rank brings RCCL up, then the ranks agree on the control plane: all up → every later
-  // collective on RCCL; any rank failed (an RCCL error, not a dead peer: the job abort flag still
-  // ends the job) → all stay on the control plane and say so (backend() "host", fallback_error()).
-  void promote() override {
-    if (promoted_ || fallback_) return;
-    const double t0 = mono_s();
-    bool start_here = false;
-    {
-      std::lock_guard<std::mutex> g(m_);
-      start_here = state_ == kIdle;
-    }
-    if (start_here) start_data_plane();  // nobody started it: start it on this thread
-    std::string err;
-    try {
-      {
-        // Bounded, abort-aware wait for a start-up thread still inside start_data_plane.
-        std::unique_lock<std::mutex> g(m_);
-        const double deadline = t0 + timeout_;
-        while (state_ == kStarting) {
-          cv_.wait_for(g, std::chrono::milliseconds(2));
-          if (state_ != kStarting) break;
-          seg_->check_abort(rank_);
-          if (mono_s() > deadline) {
-            seg_->raise_abort(rank_);
-            throw CommError("RCCL start-up timed out on rank " + std::to_string(rank_));
-          }
-        }
-        if (state_ == kFailed) std::rethrow_exception(err_);
-      }
-      rccl_->ready();  // settles ncclCommInitRankConfig (bounded, abort-aware)
-    } catch (const std::exception& e) {
-      if (seg_->aborted()) throw;  // a peer died: the job ends, no fallback
-      err = e.what();
-    }
-    int64_t failed = err.empty() ? 0 : 1;
-    host_->allreduce_sum_i64(&failed, 1);  // agreement on the control plane
-    times_.wait_s = mono_s() - t0;
-    times_.start_s = t_start_ - t_created_;
-    times_.init_upper_s = mono_s() - t_start_;
-    if (failed == 0) {
-      promoted_ = true;
-      return;
-    }
-    fallback_ = true;
-    fallback_error_ = err.empty() ? std::to_string(failed) + " rank(s) could not bring RCCL up" : err;
-  }
-  std::string fallback_error() const override { return fallback_error_; }
-  DataPlaneTimes data_plane_times() const override { return times_; }
-  void set_abort_segment(std::shared_ptr<ShmSegment> seg) override {
-    std::lock_guard<std::mutex> g(m_);  // rccl_ is written by the start-up thread
-    if (rccl_) rccl_->set_abort_segment(std::move(seg));
-  }
-
- private:
-  Comm& plane() { return promoted_ ? *rccl_ : *host_; }
-  enum State { kIdle, kStarting, kStarted, kFailed };
-  int rank_, size_, dev_;
-  std::shared_ptr<ShmSegment> seg_;
-  double timeout_;
-  std::unique_ptr<Comm> host_, rccl_;
-  double t_created_, t_start_ = 0;
-  std::mutex m_;
-  std::condition_variable cv_;
-  State state_ = kIdle;
-  std::exception_ptr err_;
-  bool promoted_ = false;  // only the rank's main thread reads/writes it
-  bool fallback_ = false;  // RCCL failed on some rank: the control plane carries everything
-  std::string fallback_error_;
-  DataPlaneTimes times_;
-};
-
 }  // namespace
 
 std::unique_ptr<Comm> make_rccl_comm(int rank, int size, const std::vector<uint8_t>& uid, int device,
@@ -462,9 +344,12 @@ std::unique_ptr<Comm> make_rccl_comm(int rank, int size, const std::vector<uint8
   return std::make_unique<RcclComm>(rank, size, uid, device, std::move(seg), timeout_s, settle_now);
 }
 
-std::unique_ptr<Comm> make_deferred_rccl_comm(int rank, int size, int device, std::shared_ptr<ShmSegment> seg,
-                                              double timeout_s) {
-  return std::make_unique<DeferredRcclComm>(rank, size, device, std::move(seg), timeout_s);
+DataPlaneFactory rccl_data_plane() {
+  DataPlaneFactory f;
+  f.unique_id = [] { return rccl_unique_id(); };
+  f.make = [](int rank, int size, const std::vector<uint8_t>& uid, int device, std::shared_ptr<ShmSegment> seg,
+              double timeout_s) { return make_rccl_comm(rank, size, uid, device, std::move(seg), timeout_s, /*settle_now=*/false); };
+  return f;
 }
 
 std::vector<uint8_t> rccl_unique_id() {

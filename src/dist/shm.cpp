@@ -50,6 +50,7 @@ struct ShmSegment::Header {
   std::atomic<uint32_t> abort;
   std::atomic<uint32_t> attached;
   std::atomic<uint32_t> uid_ready;
+  std::atomic<int32_t> dp_failed_rank;  // first rank whose data plane could not start (-1: none)
   uint8_t uid[128];
 };
 static_assert(sizeof(ShmSegment::Header) <= kHeaderBytes, "header too large");
@@ -85,6 +86,7 @@ static void init_header(ShmSegment::Header* h, int n, size_t slot_bytes) {
   h->abort.store(0);
   h->attached.store(1);  // the creator
   h->uid_ready.store(0);
+  h->dp_failed_rank.store(-1);
   std::atomic_thread_fence(std::memory_order_seq_cst);
   reinterpret_cast<std::atomic<uint64_t>*>(&h->magic)->store(kMagic, std::memory_order_release);
 }
@@ -221,12 +223,20 @@ std::vector<uint8_t> ShmSegment::wait_uid(int self, double timeout_s) const {
   uint32_t len;
   while ((len = h_->uid_ready.load(std::memory_order_acquire)) == 0) {
     check_abort(self);
+    if (const int f = data_plane_failed_rank(); f >= 0)
+      throw CommError("rank " + std::to_string(f) + " could not start the data plane");
     if (mono_s() > deadline) throw CommError("timed out waiting for the RCCL unique id from rank 0");
     std::this_thread::sleep_for(std::chrono::microseconds(200));
   }
   if (len == kUidFailed) throw CommError("rank 0 could not create the RCCL unique id");
   return std::vector<uint8_t>(h_->uid, h_->uid + len);
 }
+
+void ShmSegment::mark_data_plane_failed(int rank) {
+  int32_t none = -1;
+  h_->dp_failed_rank.compare_exchange_strong(none, rank, std::memory_order_acq_rel);
+}
+int ShmSegment::data_plane_failed_rank() const { return h_->dp_failed_rank.load(std::memory_order_acquire); }
 
 void ShmSegment::barrier(int self, double timeout_s) {
   check_abort(self);

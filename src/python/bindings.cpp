@@ -17,6 +17,7 @@
 #include "nm03/app.h"
 #include "nm03/cohort.h"
 #include "nm03/comm.h"
+#include "nm03/cpu_sampler.h"
 #include "nm03/dicom.h"
 #include "nm03/engine.h"
 #include "nm03/metaimage.h"
@@ -785,6 +786,10 @@ PYBIND11_MODULE(_nm03, m) {
            py::arg("raw"), py::arg("type") = "u16", py::arg("stored_bits") = 16, py::arg("slope") = 1.f,
            py::arg("intercept") = 0.f, py::arg("spacing_x") = 1.f, py::arg("spacing_y") = 1.f);
   m.def("device_count", &device_count);
+  // CPU sampling profiler (cpu_sampler.h; bench.py --cpu-profile, tools/cpu_profile.py).
+  m.def("cpu_profile_start", &prof::sampler_start, py::arg("period_us") = 250, py::arg("max_samples") = 1 << 20,
+        py::arg("depth") = 24);
+  m.def("cpu_profile_stop", &prof::sampler_stop, py::arg("path"), py::call_guard<py::gil_scoped_release>());
 
   // ---- 3D ---------------------------------------------------------------------------------------------
   m.def(
@@ -1300,6 +1305,11 @@ PYBIND11_MODULE(_nm03, m) {
         py::gil_scoped_release nogil;
         c.start_data_plane();
       })
+      .def("settle_data_plane", [](Comm& c) {
+        py::gil_scoped_release nogil;
+        c.settle_data_plane(nullptr);
+      })
+      .def("fail_data_plane", [](Comm& c, const std::string& why) { c.fail_data_plane(why); }, py::arg("why"))
       .def("promote", [](Comm& c) {
         py::gil_scoped_release nogil;
         c.promote();
@@ -1308,6 +1318,7 @@ PYBIND11_MODULE(_nm03, m) {
         const Comm::DataPlaneTimes t = c.data_plane_times();
         py::dict d;
         d["start_s"] = t.start_s;
+        d["settle_s"] = t.settle_s;
         d["wait_s"] = t.wait_s;
         d["init_upper_s"] = t.init_upper_s;
         return d;

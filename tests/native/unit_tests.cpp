@@ -27,6 +27,7 @@
 #include "nm03/cohort.h"
 #include "nm03/comm.h"
 #include "nm03/dicom.h"
+#include "nm03/engine.h"
 #include "nm03/golden.h"
 #include "nm03/gpu_types.h"
 #include "nm03/jpeg.h"
@@ -755,11 +756,16 @@ TEST(copy_engine_policy) {
   const std::string keepq = savedq ? savedq : "";
   AppConfig c;
   unsetenv("HSA_ENABLE_SDMA");
+  setenv("GPU_MAX_HW_QUEUES", "4", 1);  // HIP's default, as the boxes export it
   CHECK(apply_copy_engine(c, 465) && std::string(copy_engine_name()) == "blit");
   CHECK(std::string(std::getenv("GPU_MAX_HW_QUEUES")) == "1");  // --hw-queues auto with shader copies
   unsetenv("HSA_ENABLE_SDMA");
+  setenv("GPU_MAX_HW_QUEUES", "3", 1);  // a deliberate choice is kept
+  CHECK(apply_copy_engine(c, 465) && std::string(std::getenv("GPU_MAX_HW_QUEUES")) == "3");
+  unsetenv("HSA_ENABLE_SDMA");
+  unsetenv("GPU_MAX_HW_QUEUES");
   CHECK(!apply_copy_engine(c, kBlitMaxSlicesPerRank + 1) && std::string(copy_engine_name()) == "sdma");
-  CHECK(std::string(std::getenv("GPU_MAX_HW_QUEUES")) == "2");
+  CHECK(std::getenv("GPU_MAX_HW_QUEUES") == nullptr);  // long jobs: environment untouched
   CHECK(!apply_copy_engine(c, -1));  // unknown size: leave the DMA engines
   setenv("HSA_ENABLE_SDMA", "1", 1);
   CHECK(!apply_copy_engine(c, 10));  // the user's setting wins
@@ -779,6 +785,301 @@ TEST(copy_engine_policy) {
     setenv("GPU_MAX_HW_QUEUES", keepq.c_str(), 1);
   else
     unsetenv("GPU_MAX_HW_QUEUES");
+}
+
+// ---- deferred data plane + start-up hand-off (run under TSan by sanitize_check.sh) --
+// Ranks are threads sharing one anonymous segment (its futex barrier and flags work across threads as
+// across processes); the data plane is a fake whose readiness, failure and stalls are chosen per rank.
+struct FakeSpec {
+  bool make_throws = false;   // factory.make fails on this rank
+  int ready_after_ms = 0;     // poll_ready true after this long (-1: never)
+  bool poll_throws = false;   // poll_ready reports a transport error
+  int make_sleep_ms = 0;      // make() blocks this long first
+};
+
+class FakeDataPlane final : public nm03::Comm {
+ public:
+  FakeDataPlane(nm03::Comm* lb, int ready_after_ms, bool poll_throws, std::atomic<int>* aborts)
+      : lb_(lb), poll_throws_(poll_throws), aborts_(aborts),
+        ready_at_(ready_after_ms < 0 ? std::chrono::steady_clock::time_point::max()
+                                     : std::chrono::steady_clock::now() + std::chrono::milliseconds(ready_after_ms)) {}
+  int rank() const override { return lb_->rank(); }
+  int size() const override { return lb_->size(); }
+  const char* backend() const override { return "fake"; }
+  void broadcast(void* b, size_t n, int root) override { lb_->broadcast(b, n, root); }
+  void allgather(const void* s, size_t n, void* r) override { lb_->allgather(s, n, r); }
+  void allreduce_sum_i64(int64_t* v, size_t n) override { lb_->allreduce_sum_i64(v, n); }
+  void allreduce_max_f64(double* v, size_t n) override { lb_->allreduce_max_f64(v, n); }
+  void barrier() override { lb_->barrier(); }
+  void sendrecv(const void* s, size_t sb, int d, void* r, size_t rb, int src) override { lb_->sendrecv(s, sb, d, r, rb, src); }
+  bool poll_ready() override {
+    if (aborted_) throw nm03::CommError("fake transport was aborted");
+    if (poll_throws_) throw nm03::CommError("fake transport error");
+    return std::chrono::steady_clock::now() >= ready_at_;
+  }
+  void abort_transport() override {
+    if (!aborted_) aborts_->fetch_add(1);
+    aborted_ = true;
+  }
+
+ private:
+  nm03::Comm* lb_;
+  bool poll_throws_;
+  std::atomic<int>* aborts_;
+  std::chrono::steady_clock::time_point ready_at_;
+  bool aborted_ = false;  // start-up thread only (settle), or the main thread after it
+};
+
+struct FakeWorld {
+  int n;
+  std::shared_ptr<nm03::ShmSegment> seg;
+  std::vector<std::unique_ptr<nm03::Comm>> lb;  // what the fake transports carry
+  std::vector<FakeSpec> spec;
+  std::atomic<int> aborts{0}, made{0};
+  explicit FakeWorld(int n_) : n(n_), seg(nm03::ShmSegment::create_anonymous(n_, 1 << 16)), lb(nm03::make_loopback_group(n_)),
+                               spec((size_t)n_) {}
+  nm03::DataPlaneFactory factory() {
+    nm03::DataPlaneFactory f;
+    f.unique_id = [] { return std::vector<uint8_t>(16, 7); };
+    f.make = [this](int r, int, const std::vector<uint8_t>& uid, int, std::shared_ptr<nm03::ShmSegment>, double)
+        -> std::unique_ptr<nm03::Comm> {
+      if (uid != std::vector<uint8_t>(16, 7)) throw nm03::CommError("bad uid");
+      const FakeSpec& sp = spec[(size_t)r];
+      if (sp.make_sleep_ms) std::this_thread::sleep_for(std::chrono::milliseconds(sp.make_sleep_ms));
+      if (sp.make_throws) throw nm03::CommError("fake make failed on rank " + std::to_string(r));
+      made.fetch_add(1);
+      return std::make_unique<FakeDataPlane>(lb[(size_t)r].get(), sp.ready_after_ms, sp.poll_throws, &aborts);
+    };
+    return f;
+  }
+};
+
+struct RankOutcome {
+  std::string backend, fallback, error;
+  int64_t sum = 0;
+  double promote_s = 0;
+};
+
+// Every rank: a start-up thread (start + settle, or fail_data_plane when `fail_start`) while its main
+// thread runs a control-plane collective, then promote() and one collective on whatever plane won.
+std::vector<RankOutcome> run_fake_world(FakeWorld& w, double timeout_s, std::vector<bool> fail_start = {},
+                                        int abort_rank_after_ms = -1) {
+  fail_start.resize((size_t)w.n, false);
+  std::vector<RankOutcome> out((size_t)w.n);
+  std::vector<std::thread> ranks;
+  const auto f = w.factory();
+  for (int r = 0; r < w.n; ++r)
+    ranks.emplace_back([&, r] {
+      RankOutcome& o = out[(size_t)r];
+      try {
+        auto c = nm03::make_deferred_comm(r, w.n, 0, w.seg, timeout_s, f);
+        std::thread su([&] {
+          if (fail_start[(size_t)r])
+            c->fail_data_plane("injected start-up failure");
+          else {
+            c->start_data_plane();
+            c->settle_data_plane(nullptr);
+          }
+        });
+        c->barrier();  // control plane meanwhile
+        if (abort_rank_after_ms >= 0 && r == 0) {
+          std::this_thread::sleep_for(std::chrono::milliseconds(abort_rank_after_ms));
+          w.seg->raise_abort(w.n - 1);  // rank n-1 "died" while the others start
+        }
+        const auto t0 = std::chrono::steady_clock::now();
+        try {
+          c->promote();
+        } catch (const std::exception& e) {
+          o.error = e.what();
+        }
+        o.promote_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        su.join();
+        if (o.error.empty()) {
+          int64_t v = r + 1;
+          c->allreduce_sum_i64(&v, 1);
+          o.sum = v;
+          o.backend = c->backend();
+          o.fallback = c->fallback_error();
+        }
+      } catch (const std::exception& e) {
+        o.error = std::string("outer: ") + e.what();
+      }
+    });
+  for (auto& t : ranks) t.join();
+  return out;
+}
+
+TEST(deferred_comm_all_ranks_promote) {
+  FakeWorld w(4);
+  for (int r = 0; r < 4; ++r) w.spec[(size_t)r].ready_after_ms = 5 * r;
+  const auto o = run_fake_world(w, 20.0);
+  for (const auto& x : o) {
+    CHECK(x.error.empty());
+    CHECK(x.backend == "fake");
+    CHECK(x.fallback.empty());
+    CHECK(x.sum == 10);
+  }
+  CHECK(w.made.load() == 4 && w.aborts.load() == 0);
+}
+
+TEST(deferred_comm_one_rank_fails_make_all_fall_back_fast) {
+  // one rank failing in make_rccl_comm left the healthy ranks in ready() until the deadline.
+  FakeWorld w(3);
+  w.spec[1].make_throws = true;
+  w.spec[0].ready_after_ms = -1;  // would never be ready by itself: only the failure flag ends its wait
+  w.spec[2].ready_after_ms = -1;
+  const auto t0 = std::chrono::steady_clock::now();
+  const auto o = run_fake_world(w, 30.0);
+  const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  for (const auto& x : o) {
+    CHECK(x.error.empty());
+    CHECK(x.backend == "host");
+    CHECK(!x.fallback.empty());
+    CHECK(x.sum == 6);  // the control plane carries the collective
+  }
+  CHECK(s < 5.0);
+  CHECK(w.aborts.load() == 2);  // the two healthy transports were abandoned
+  CHECK(w.seg->data_plane_failed_rank() == 1);
+}
+
+TEST(deferred_comm_rank0_startup_failure_unblocks_uid_waiters) {
+  // rank 0's start-up failing before start_data_plane left the others in wait_uid().
+  FakeWorld w(3);
+  const auto t0 = std::chrono::steady_clock::now();
+  const auto o = run_fake_world(w, 30.0, {true, false, false});
+  const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  for (const auto& x : o) {
+    CHECK(x.error.empty());
+    CHECK(x.backend == "host" && !x.fallback.empty() && x.sum == 6);
+  }
+  CHECK(s < 5.0);
+  CHECK(w.made.load() == 0);
+}
+
+TEST(deferred_comm_stalled_rank_times_out_and_all_fall_back) {
+  FakeWorld w(3);
+  w.spec[2].ready_after_ms = -1;  // never ready: its own settle times out
+  w.spec[0].ready_after_ms = -1;  // the others only become ready with every peer (as RCCL's bootstrap)
+  w.spec[1].ready_after_ms = -1;
+  const auto o = run_fake_world(w, 0.5);
+  for (const auto& x : o) {
+    CHECK(x.error.empty());
+    CHECK(x.backend == "host" && !x.fallback.empty() && x.sum == 6);
+  }
+  CHECK(w.aborts.load() == 3);
+}
+
+TEST(deferred_comm_transport_error_falls_back) {
+  FakeWorld w(2);
+  w.spec[0].poll_throws = true;
+  w.spec[1].ready_after_ms = -1;
+  const auto o = run_fake_world(w, 30.0);
+  for (const auto& x : o) CHECK(x.error.empty() && x.backend == "host" && x.sum == 3);
+}
+
+TEST(deferred_comm_peer_abort_during_start_ends_the_job) {
+  // A dead peer is not a fallback: promote() throws on every live rank once the abort flag is up,
+  // while start-up threads are still inside make() / settle.
+  FakeWorld w(3);
+  for (auto& sp : w.spec) {
+    sp.make_sleep_ms = 100;
+    sp.ready_after_ms = -1;
+  }
+  const auto o = run_fake_world(w, 30.0, {}, 20);
+  for (const auto& x : o) CHECK(!x.error.empty());
+  CHECK(w.seg->aborted() && w.seg->abort_rank() == 2);
+}
+
+TEST(engine_startup_hands_over_and_settles_first) {
+  // The start-up thread settles the data plane before it builds; build() sees the hook's engine.
+  FakeWorld w(1);
+  w.spec[0].ready_after_ms = 30;
+  auto c = nm03::make_deferred_comm(0, 1, 0, w.seg, 10.0, w.factory());
+  std::atomic<int> order{0};
+  int prepared_at = -1, built_at = -1;
+  nm03::app::EngineStartup::Hooks h;
+  h.prepare = [&](nm03::app::EngineStartup::Times& t) {
+    prepared_at = order++;
+    t.hip_init_s = 0.001;
+  };
+  h.build = [&](const nm03::EngineConfig& ec) {
+    built_at = order++;
+    return std::make_unique<nm03::Engine>(ec);
+  };
+  nm03::EngineConfig ec;
+  ec.host_only = true;
+  ec.threads = 1;
+  ec.streams = 1;
+  ec.batch_size = 1;
+  ec.max_dim = 64;
+  std::unique_ptr<nm03::Engine> e;
+  std::string err;
+  {
+    nm03::app::EngineStartup su(h, c.get());
+    std::this_thread::sleep_for(std::chrono::milliseconds(5));
+    e = su.build(ec, &err);
+    CHECK(su.times().data_plane_s >= 0.02);  // waited for the transport before building
+    CHECK(su.times().engine_ctor_s > 0);
+  }
+  CHECK(err.empty() && e != nullptr);
+  CHECK(prepared_at == 0 && built_at == 1);
+  c->promote();
+  CHECK(std::string(c->backend()) == "fake");
+  CHECK(c->data_plane_times().settle_s >= 0.02);
+}
+
+TEST(engine_startup_prepare_failure_tells_peers) {
+  FakeWorld w(2);
+  w.spec[1].ready_after_ms = -1;
+  auto c0 = nm03::make_deferred_comm(0, 2, 0, w.seg, 30.0, w.factory());
+  auto c1 = nm03::make_deferred_comm(1, 2, 0, w.seg, 30.0, w.factory());
+  nm03::app::EngineStartup::Hooks bad, good;
+  bad.prepare = [](nm03::app::EngineStartup::Times&) { throw std::runtime_error("injected hipInit failure"); };
+  bad.build = [](const nm03::EngineConfig&) -> std::unique_ptr<nm03::Engine> { return nullptr; };
+  good.prepare = [](nm03::app::EngineStartup::Times&) {};
+  good.build = [](const nm03::EngineConfig&) -> std::unique_ptr<nm03::Engine> { return nullptr; };
+  const auto t0 = std::chrono::steady_clock::now();
+  std::string err0, err1, b0, b1;
+  std::thread r1([&] {
+    nm03::app::EngineStartup su(good, c1.get());
+    nm03::EngineConfig ec;
+    (void)su.build(ec, &err1);
+    c1->promote();
+    b1 = c1->backend();
+  });
+  {
+    nm03::app::EngineStartup su(bad, c0.get());
+    nm03::EngineConfig ec;
+    (void)su.build(ec, &err0);
+    c0->promote();
+    b0 = c0->backend();
+  }
+  r1.join();
+  const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  CHECK(err0.find("injected hipInit failure") != std::string::npos);
+  CHECK(err1 == "engine not built");
+  CHECK(b0 == "host" && b1 == "host");
+  CHECK(s < 5.0);
+}
+
+TEST(engine_startup_cancel_while_settling) {
+  // Destroyed without build() while its data plane can never become ready: cancel ends the settle.
+  FakeWorld w(1);
+  w.spec[0].ready_after_ms = -1;
+  auto c = nm03::make_deferred_comm(0, 1, 0, w.seg, 60.0, w.factory());
+  nm03::app::EngineStartup::Hooks h;
+  h.prepare = [](nm03::app::EngineStartup::Times&) {};
+  h.build = [](const nm03::EngineConfig&) -> std::unique_ptr<nm03::Engine> { return nullptr; };
+  const auto t0 = std::chrono::steady_clock::now();
+  {
+    nm03::app::EngineStartup su(h, c.get());
+    std::this_thread::sleep_for(std::chrono::milliseconds(20));
+  }
+  const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  CHECK(s < 2.0);
+  CHECK(w.aborts.load() == 1);
+  c->promote();  // one rank: agrees with itself on the fallback
+  CHECK(std::string(c->backend()) == "host");
 }
 
 }  // namespace

@@ -1,0 +1,240 @@
+#!/usr/bin/env python3
+"""Symbolise and attribute an nm03 CPU sample file (src/runtime/cpu_sampler.cpp, bench.py --cpu-profile).
+
+    python tools/cpu_profile.py gpurun_out/prof/cpu.rank0 [--top 30] [--json out.json]
+
+Frames are mapped to (module, ELF virtual address) through the recorded module map and the
+modules' PT_LOAD headers, then named by llvm-symbolizer (inlined frames expanded: the build
+carries host line tables). Reported:
+  * samples per thread group (nm03-pool / nm03-slot / interpreter / runtime threads);
+  * self time per function (innermost frame), per thread group;
+  * the pool's time by task (a DICOM load, a JPEG-pair write, idle spinning, queue hand-off) and, for
+    loads and writes, by phase: the first frame from the leaf that matches a phase's patterns.
+"""
+import argparse
+import collections
+import json
+import os
+import struct
+import subprocess
+import sys
+
+SYMBOLIZER = "/opt/rocm/lib/llvm/bin/llvm-symbolizer"
+
+# (phase, substrings of a frame's function name), tried leaf-first per sample.
+LOAD_PHASES = [
+    ("open (path lookup)", ["__libc_open64", "open64", "__open64", "openat", "__GI___open"]),
+    ("pread (page cache copy)", ["pread"]),
+    ("close", ["__close", "close_nocancel", "__libc_close"]),
+    ("12-bit pack", ["pack12::"]),
+    ("DICOM parse", ["dicom::parse", "dicom::(anonymous namespace)", "Header"]),
+    ("slot bookkeeping (locks, allocs, wakeups)", ["pthread_mutex", "lll_lock", "futex", "__lll", "notify_one",
+                                                    "condition_variable", "load_into"]),
+    ("string / alloc", ["malloc", "free", "operator new", "operator delete", "basic_string", "memcpy", "memmove"]),
+]
+WRITE_PHASES = [
+    ("open/create", ["open64", "openat", "__libc_open64"]),
+    ("pwritev/write", ["pwrite", "writev", "__libc_write", "__write"]),
+    ("close", ["__close", "close_nocancel"]),
+    ("ftruncate", ["ftruncate"]),
+    ("path strings / alloc", ["malloc", "free", "operator new", "operator delete", "basic_string", "memcpy"]),
+    ("other write work", ["write_jpeg_at", "jpeg::"]),
+]
+
+
+def load_phdrs(path, cache={}):
+    """PT_LOAD (p_offset, p_vaddr, p_filesz) of an ELF64 file."""
+    if path in cache:
+        return cache[path]
+    segs = []
+    try:
+        with open(path, "rb") as f:
+            h = f.read(64)
+            if h[:4] == b"\x7fELF" and h[4] == 2:
+                phoff, = struct.unpack_from("<Q", h, 32)
+                phentsize, phnum = struct.unpack_from("<HH", h, 54)
+                f.seek(phoff)
+                ph = f.read(phentsize * phnum)
+                for i in range(phnum):
+                    p_type, _flags, p_offset, p_vaddr, _paddr, p_filesz = struct.unpack_from("<IIQQQQ", ph, i * phentsize)
+                    if p_type == 1:
+                        segs.append((p_offset, p_vaddr, p_filesz))
+    except OSError:
+        pass
+    cache[path] = segs
+    return segs
+
+
+def parse(path):
+    maps, threads, stacks = [], {}, []
+    meta = {}
+    with open(path) as f:
+        for line in f:
+            p = line.split()
+            if not p or p[0].startswith("#"):
+                continue
+            if p[0] == "map":
+                maps.append((int(p[1], 16), int(p[2], 16), int(p[3], 16), " ".join(p[4:])))
+            elif p[0] == "thread":
+                threads[int(p[1])] = p[2] if len(p) > 2 else "?"
+            elif p[0] == "s":
+                stacks.append((int(p[1]), int(p[2]), [int(x, 16) for x in p[3:]]))
+            elif p[0] == "period_us":
+                meta["period_us"] = int(p[1])
+            elif p[0] == "samples":
+                meta["samples"] = int(p[1])
+                meta["dropped"] = int(p[3])
+    return meta, maps, threads, stacks
+
+
+def to_module(addr, maps):
+    for lo, hi, off, path in maps:
+        if lo <= addr < hi:
+            foff = addr - lo + off
+            for p_off, p_vaddr, p_sz in load_phdrs(path):
+                if p_off <= foff < p_off + p_sz:
+                    return path, p_vaddr + (foff - p_off)
+            return path, foff
+    return None, addr
+
+
+def symbolize(requests):
+    """{path: set(vaddr)} -> {(path, vaddr): [function names, innermost first]}."""
+    out = {}
+    for path, addrs in requests.items():
+        addrs = sorted(addrs)
+        if not os.path.exists(path):
+            for a in addrs:
+                out[(path, a)] = [f"{os.path.basename(path)}+{a:#x}"]
+            continue
+        inp = "".join(f"{a:#x}\n" for a in addrs)
+        try:
+            r = subprocess.run([SYMBOLIZER, f"--obj={path}", "--functions=linkage", "--demangle", "--inlines",
+                                "--output-style=JSON"], input=inp, capture_output=True, text=True, timeout=600)
+            rows = [json.loads(x) for x in r.stdout.splitlines() if x.strip()]
+        except (OSError, subprocess.TimeoutExpired, ValueError):
+            rows = []
+        for a, row in zip(addrs, rows):
+            names = [s.get("FunctionName") or "??" for s in row.get("Symbol", [])]
+            names = [n for n in names if n and n != "??"] or [f"{os.path.basename(path)}+{a:#x}"]
+            out[(path, a)] = names
+        for a in addrs:
+            out.setdefault((path, a), [f"{os.path.basename(path)}+{a:#x}"])
+    return out
+
+
+def group_of(name):
+    if name.startswith("nm03-pool"):
+        return "nm03-pool"
+    if name.startswith("nm03-slot"):
+        return "nm03-slot"
+    if name.startswith("nm03-reap"):
+        return "nm03-reaper"
+    if name.startswith("python"):
+        return "main (python)"
+    return "other: " + name
+
+
+def classify(frames, phases):
+    for fn in frames:
+        for phase, pats in phases:
+            if any(p in fn for p in pats):
+                return phase
+    return "other"
+
+
+def analyse(path, top=30):
+    meta, maps, threads, stacks = parse(path)
+    req = collections.defaultdict(set)
+    for _, _, pcs in stacks:
+        for k, pc in enumerate(pcs):
+            mod, va = to_module(pc if k == 0 else pc - 1, maps)  # return addresses: the call site
+            if mod:
+                req[mod].add(va)
+    syms = symbolize(req)
+
+    def frames_of(pcs):
+        out = []
+        for k, pc in enumerate(pcs):
+            mod, va = to_module(pc if k == 0 else pc - 1, maps)
+            out.extend(syms.get((mod, va), [f"{pc:#x}"]) if mod else [f"{pc:#x}"])
+        return out
+
+    total = sum(c for c, _, _ in stacks)
+    groups = collections.Counter()
+    self_by_group = collections.defaultdict(collections.Counter)
+    pool_task = collections.Counter()
+    load_phase = collections.Counter()
+    write_phase = collections.Counter()
+    for count, tid, pcs in stacks:
+        g = group_of(threads.get(tid, "?"))
+        groups[g] += count
+        fr = frames_of(pcs)
+        leaf = fr[0] if fr else "?"
+        self_by_group[g][leaf] += count
+        if g != "nm03-pool":
+            continue
+        joined = " | ".join(fr)
+        if "load_into" in joined:
+            pool_task["DICOM load"] += count
+            load_phase[classify(fr, LOAD_PHASES)] += count
+        elif "write_jpeg_at" in joined:
+            pool_task["JPEG pair write"] += count
+            write_phase[classify(fr, WRITE_PHASES)] += count
+        elif "ThreadPool::loop" in joined and ("pause" in leaf or "steady_clock" in joined or "loop" in leaf):
+            pool_task["idle spin (ThreadPool::loop)"] += count
+        elif "TaskGroup" in joined or "ThreadPool" in joined:
+            pool_task["queue hand-off (ThreadPool / TaskGroup)"] += count
+        else:
+            pool_task["other"] += count
+    res = {"file": path, "samples": total, "period_us": meta.get("period_us"), "dropped": meta.get("dropped"),
+           "groups": dict(groups.most_common()), "pool_task": dict(pool_task.most_common()),
+           "load_phase": dict(load_phase.most_common()), "write_phase": dict(write_phase.most_common()),
+           "self_top": {g: c.most_common(top) for g, c in self_by_group.items()}}
+    return res
+
+
+def report(res, out=sys.stdout):
+    tot = max(res["samples"], 1)
+    pct = lambda c, d=tot: f"{100.0 * c / max(d, 1):5.1f}%"
+    print(f"{res['file']}: {res['samples']} samples (dropped {res['dropped']})", file=out)
+    print("\nsamples by thread group:", file=out)
+    for g, c in res["groups"].items():
+        print(f"  {pct(c)}  {c:7d}  {g}", file=out)
+    pool = res["groups"].get("nm03-pool", 0)
+    if pool:
+        print("\nnm03-pool by task (% of pool samples):", file=out)
+        for t, c in res["pool_task"].items():
+            print(f"  {pct(c, pool)}  {c:7d}  {t}", file=out)
+        for title, key in (("DICOM load", "load_phase"), ("JPEG pair write", "write_phase")):
+            sub = sum(res[key].values())
+            if not sub:
+                continue
+            print(f"\n{title} by phase (% of its samples):", file=out)
+            for t, c in res[key].items():
+                print(f"  {pct(c, sub)}  {c:7d}  {t}", file=out)
+    for g, rows in res["self_top"].items():
+        gc = res["groups"].get(g, 1)
+        print(f"\nself time, {g} (% of the group):", file=out)
+        for fn, c in rows:
+            print(f"  {pct(c, gc)}  {c:7d}  {fn[:150]}", file=out)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("files", nargs="+")
+    ap.add_argument("--top", type=int, default=25)
+    ap.add_argument("--json", default="")
+    a = ap.parse_args()
+    all_res = []
+    for f in a.files:
+        r = analyse(f, a.top)
+        report(r)
+        all_res.append(r)
+    if a.json:
+        with open(a.json, "w") as f:
+            json.dump(all_res, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
