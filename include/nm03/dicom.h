@@ -2,12 +2,14 @@
 // DICOMFileImporter with setLoadSeries(false): test_pipeline.cpp:33-42, main_sequential.cpp:175-177).
 //
 // Supported: Part-10 files (preamble + "DICM") and bare datasets; Implicit VR LE, Explicit VR LE,
-// Explicit VR BE, Deflated Explicit VR LE (1.2.840.10008.1.2.1.99, zlib) and RLE Lossless
-// (1.2.840.10008.1.2.5, encapsulated PackBits segments); 8/16-bit monochrome, signed/unsigned,
+// Explicit VR BE, Deflated Explicit VR LE (1.2.840.10008.1.2.1.99, zlib), RLE Lossless
+// (1.2.840.10008.1.2.5, encapsulated PackBits segments) and lossless JPEG — JPEG Lossless First-Order
+// Prediction (1.2.840.10008.1.2.4.70) and JPEG Lossless Process 14 (1.2.840.10008.1.2.4.57), decoded
+// on the host (nm03/jpeg_lossless.h); 8/16-bit monochrome, signed/unsigned,
 // BitsStored masking, modality rescale, PixelSpacing, undefined-length sequences, MONOCHROME1
 // (inverted at import, see Header::invert), multi-frame files (frame selection, see copy_pixels16).
-// The JPEG-family encapsulated syntaxes (baseline/lossless JPEG, JPEG-LS, JPEG 2000, ...) are
-// rejected with a SliceError: the slice is skipped and counted like a fast::Exception in the
+// The other JPEG-family encapsulated syntaxes (baseline/extended lossy JPEG, JPEG-LS, JPEG 2000, ...)
+// are rejected with a SliceError: the slice is skipped and counted like a fast::Exception in the
 // reference. DCMTK behind FAST would decode them; that part of parity is unpinned (no DCMTK here).
 #pragma once
 
@@ -20,7 +22,7 @@
 
 namespace nm03::dicom {
 
-enum class Syntax : uint8_t { kImplicitLE, kExplicitLE, kExplicitBE, kDeflatedLE, kRleLossless };
+enum class Syntax : uint8_t { kImplicitLE, kExplicitLE, kExplicitBE, kDeflatedLE, kRleLossless, kJpegLossless };
 
 // Name of a transfer syntax as used in messages and by the Python bindings.
 const char* syntax_name(Syntax s);
@@ -46,8 +48,8 @@ struct Header {
   // hands to a viewer. With the reference's fixed-range IntensityNormalization (0..10000) this is a
   // documented choice, not a pinned FAST behaviour.
   bool invert = false;
-  // Deflated and RLE files: the decoded bytes (inflated dataset, or every frame's samples as native
-  // little-endian words/bytes); pixel_offset and pixel_length then refer to this buffer.
+  // Deflated, RLE and lossless JPEG files: the decoded bytes (inflated dataset, or every frame's
+  // samples as native little-endian words/bytes); pixel_offset and pixel_length then refer to this buffer.
   std::shared_ptr<const std::vector<uint8_t>> decoded;
   size_t frame_bytes() const { return (size_t)rows * cols * (bits_allocated / 8); }
   // Samples are little-endian words (or bytes) at pixel_offset of pixel_base().
@@ -170,8 +172,12 @@ struct WriteSpec {
   std::string photometric = "MONOCHROME2";
   int frames = 1;  // pixels holds frames*rows*cols samples; NumberOfFrames written when > 1
   // kDeflatedLE: the dataset after the meta group is raw-deflated (zlib); kRleLossless: one
-  // PackBits-coded fragment per frame (MSB segment, then LSB segment for 16-bit data).
+  // PackBits-coded fragment per frame (MSB segment, then LSB segment for 16-bit data);
+  // kJpegLossless: one lossless JPEG per frame (precision = BitsStored), selection value
+  // `jpeg_predictor` (1: transfer syntax .4.70, else .4.57), restart markers every
+  // `jpeg_restart_rows` rows (0: none), each frame split into `jpeg_fragments` fragments.
   Syntax syntax = Syntax::kExplicitLE;
+  int jpeg_predictor = 1, jpeg_restart_rows = 0, jpeg_fragments = 1;
   bool preamble = true;  // write 128-byte preamble + "DICM" + file meta group (required by kDeflatedLE/kRleLossless)
 };
 

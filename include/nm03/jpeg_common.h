@@ -7,6 +7,12 @@
 // PASS1_BITS=2, outputs scaled by 8), rounding division by 8·Q, the Annex K tables scaled for
 // quality 75, zig-zag order and the standard (Annex K.3) Huffman codes.  A gray canvas maps to
 // Y = gray, Cb = Cr = 128 exactly under libjpeg's RGB→YCbCr, so chroma blocks are all-zero.
+//
+// Acknowledgement: the forward DCT below follows the arithmetic of the Independent JPEG Group's
+// jfdctint.c ("islow", the Loeffler–Ligtenberg–Moschytz algorithm as implemented by the IJG) step
+// for step, because byte identity with libjpeg requires the same rounding at every stage, and the
+// quality scaling follows IJG jcparam.c. This software is based in part on the work of the
+// Independent JPEG Group. The tables are ITU T.81 Annex K.
 #pragma once
 
 #include <cstdint>

@@ -3,6 +3,7 @@
 // main_parallel.cpp:78-80). Only what a 2D monochrome slice import needs is interpreted; every
 // other element is skipped structurally (including undefined-length sequences).
 #include "nm03/dicom.h"
+#include "nm03/jpeg_lossless.h"
 
 #include <fcntl.h>
 #include <immintrin.h>
@@ -234,6 +235,62 @@ void decode_rle_frame(const uint8_t* f, size_t len, int rows, int cols, int byte
   }
 }
 
+// Lossless JPEG frames (PS3.5 A.4): one frame's fragments concatenated (a single-frame image may
+// span several fragments; a multi-frame one has one fragment per frame), decoded and stored as
+// native little-endian samples. The codec's precision must fit BitsAllocated; signed data is
+// sign-extended from BitsStored like the native encodings written by this repo (the codec carries the
+// stored bit patterns).
+void decode_jpeg_lossless_frames(Header& h, const uint8_t* d, const std::vector<std::pair<size_t, size_t>>& frags, int frames) {
+  if (frags.empty()) throw SliceError("JPEG pixel data without fragments");
+  if (frames > 1 && (int)frags.size() != frames)
+    throw SliceError("JPEG pixel data has " + std::to_string(frags.size()) + " fragments for " + std::to_string(frames) +
+                     " frames (one fragment per frame is supported for multi-frame images)");
+  const size_t fpix = (size_t)h.rows * h.cols, fb = h.frame_bytes();
+  size_t total = 0;
+  for (const auto& f : frags) total += f.second;
+  if (fpix * frames > total * 8 + 64 * (size_t)frames)  // ≥ 1 bit per sample
+    throw SliceError("JPEG fragment too short for a " + std::to_string(h.rows) + "x" + std::to_string(h.cols) + " frame");
+  auto dec = std::make_shared<std::vector<uint8_t>>(fb * frames);
+  std::vector<uint8_t> joined;
+  std::vector<uint16_t> px;
+  for (int f = 0; f < frames; ++f) {
+    const uint8_t* src;
+    size_t len;
+    if (frames == 1 && frags.size() > 1) {
+      joined.clear();
+      for (const auto& fr : frags) joined.insert(joined.end(), d + fr.first, d + fr.first + fr.second);
+      src = joined.data();
+      len = joined.size();
+    } else {
+      src = d + frags[f].first;
+      len = frags[f].second;
+    }
+    const jpegll::Info info = jpegll::decode(src, len, px);
+    if (info.rows != h.rows || info.cols != h.cols)
+      throw SliceError("JPEG frame is " + std::to_string(info.cols) + "x" + std::to_string(info.rows) + ", the dataset says " +
+                       std::to_string(h.cols) + "x" + std::to_string(h.rows));
+    if (info.precision > h.bits_allocated)
+      throw SliceError("JPEG precision " + std::to_string(info.precision) + " exceeds BitsAllocated " +
+                       std::to_string(h.bits_allocated));
+    uint8_t* o = dec->data() + f * fb;
+    const int bs = h.bits_stored > 0 ? h.bits_stored : h.bits_allocated;
+    const bool sext = h.pixel_rep == 1 && bs < 16 && h.bits_allocated == 16;
+    for (size_t i = 0; i < fpix; ++i) {
+      uint16_t v = px[i];
+      if (h.bits_allocated == 8) {
+        o[i] = (uint8_t)v;
+        continue;
+      }
+      if (sext && (v >> (bs - 1) & 1)) v = (uint16_t)(v | (uint16_t)(0xFFFFu << bs));
+      o[2 * i] = (uint8_t)v;
+      o[2 * i + 1] = (uint8_t)(v >> 8);
+    }
+  }
+  h.decoded = dec;
+  h.pixel_offset = 0;
+  h.pixel_length = dec->size();
+}
+
 }  // namespace
 
 const char* syntax_name(Syntax s) {
@@ -243,6 +300,7 @@ const char* syntax_name(Syntax s) {
     case Syntax::kExplicitBE: return "big";
     case Syntax::kDeflatedLE: return "deflated";
     case Syntax::kRleLossless: return "rle";
+    case Syntax::kJpegLossless: return "jpeg-lossless";
   }
   return "?";
 }
@@ -292,6 +350,8 @@ Header parse_prefix(const uint8_t* data, size_t avail, size_t size) {
     c = Cursor{inflated->data(), inflated->size(), 0, false};
   } else if (ts == "1.2.840.10008.1.2.5") {
     h.syntax = Syntax::kRleLossless;
+  } else if (ts == "1.2.840.10008.1.2.4.70" || ts == "1.2.840.10008.1.2.4.57") {
+    h.syntax = Syntax::kJpegLossless;  // lossless JPEG, process 14 (SV1 / any selection value)
   } else if (ts.rfind("1.2.840.10008.1.2.4.", 0) == 0) {
     throw SliceError("Unsupported compressed DICOM transfer syntax (JPEG family): " + ts);
   } else {
@@ -303,7 +363,8 @@ Header parse_prefix(const uint8_t* data, size_t avail, size_t size) {
     Elem e = read_elem(c, explicit_vr);
     if (e.group == 0x7FE0 && e.elem == 0x0010) {
       if (e.len == kUndefined) {
-        if (h.syntax != Syntax::kRleLossless)
+        const bool jpeg = h.syntax == Syntax::kJpegLossless;
+        if (h.syntax != Syntax::kRleLossless && !jpeg)
           throw SliceError("Encapsulated (compressed) pixel data in a native transfer syntax");
         if (avail < full) throw SliceError("Truncated DICOM data");  // callers retry with the whole file
         // Basic Offset Table item, then one fragment per frame (PS3.5 A.4, G.2), then the
@@ -320,8 +381,13 @@ Header parse_prefix(const uint8_t* data, size_t avail, size_t size) {
           c.pos += it.len;
         }
         if (h.rows <= 0 || h.cols <= 0 || (h.bits_allocated != 8 && h.bits_allocated != 16))
-          throw SliceError("RLE image without Rows/Columns/BitsAllocated before its pixel data");
+          throw SliceError(std::string(jpeg ? "JPEG" : "RLE") + " image without Rows/Columns/BitsAllocated before its pixel data");
         const int frames = std::max(1, h.frames);
+        if (jpeg) {
+          decode_jpeg_lossless_frames(h, c.d, frags, frames);
+          have_pixels = true;
+          break;
+        }
         if ((int)frags.size() != frames)
           throw SliceError("RLE pixel data has " + std::to_string(frags.size()) + " fragments for " + std::to_string(frames) +
                            " frame(s) (one fragment per frame is supported)");
@@ -340,8 +406,9 @@ Header parse_prefix(const uint8_t* data, size_t avail, size_t size) {
         have_pixels = true;
         break;
       }
-      if (h.syntax == Syntax::kRleLossless)
-        throw SliceError("RLE Lossless transfer syntax with native (not encapsulated) pixel data");
+      if (h.syntax == Syntax::kRleLossless || h.syntax == Syntax::kJpegLossless)
+        throw SliceError(std::string(h.syntax == Syntax::kRleLossless ? "RLE Lossless" : "JPEG Lossless") +
+                         " transfer syntax with native (not encapsulated) pixel data");
       h.pixel_offset = e.value_pos;
       h.pixel_length = e.len;
       have_pixels = true;
@@ -801,9 +868,12 @@ std::vector<uint8_t> write(const WriteSpec& s) {
                    : s.syntax == Syntax::kExplicitLE ? "1.2.840.10008.1.2.1"
                    : s.syntax == Syntax::kExplicitBE ? "1.2.840.10008.1.2.2"
                    : s.syntax == Syntax::kDeflatedLE ? "1.2.840.10008.1.2.1.99"
-                                                     : "1.2.840.10008.1.2.5";
-  if ((s.syntax == Syntax::kDeflatedLE || s.syntax == Syntax::kRleLossless) && !s.preamble)
-    throw std::runtime_error("deflated / RLE files need the file meta group (preamble)");
+                   : s.syntax == Syntax::kJpegLossless
+                       ? (s.jpeg_predictor == 1 ? "1.2.840.10008.1.2.4.70" : "1.2.840.10008.1.2.4.57")
+                       : "1.2.840.10008.1.2.5";
+  const bool encapsulated = s.syntax == Syntax::kRleLossless || s.syntax == Syntax::kJpegLossless;
+  if ((s.syntax == Syntax::kDeflatedLE || encapsulated) && !s.preamble)
+    throw std::runtime_error("deflated / RLE / JPEG files need the file meta group (preamble)");
   const char* sop_class = "1.2.840.10008.5.1.4.1.1.4";  // MR Image Storage
   Out out;
   if (s.preamble) {
@@ -874,9 +944,9 @@ std::vector<uint8_t> write(const WriteSpec& s) {
       }
     }
   }
-  if (s.syntax == Syntax::kRleLossless) {
+  if (encapsulated) {
     // Encapsulated: (7FE0,0010) OB of undefined length, an empty Basic Offset Table item, one
-    // fragment per frame, the sequence delimiter.
+    // fragment per frame (JPEG: optionally several), the sequence delimiter.
     const size_t fpix = (size_t)s.rows * s.cols;
     out.u16(0x7FE0);
     out.u16(0x0010);
@@ -890,7 +960,18 @@ std::vector<uint8_t> write(const WriteSpec& s) {
       out.raw(v.data(), v.size());
     };
     item(0xE000, {});
-    for (int f = 0; f < frames; ++f) {
+    for (int f = 0; s.syntax == Syntax::kJpegLossless && f < frames; ++f) {
+      std::vector<uint16_t> fr(fpix);
+      for (size_t i = 0; i < fpix; ++i) fr[i] = s.pixels ? s.pixels[f * fpix + i] : 0;
+      std::vector<uint8_t> j = jpegll::encode(fr.data(), s.rows, s.cols, std::max(2, bs), s.jpeg_predictor, 0,
+                                              s.jpeg_restart_rows);
+      if (j.size() & 1) j.push_back(0);  // even item length (a trailing pad byte after EOI)
+      const int nf = frames == 1 ? std::max(1, s.jpeg_fragments) : 1;
+      const size_t step = (j.size() / nf + 1) & ~(size_t)1;
+      for (size_t o = 0; o < j.size(); o += step)
+        item(0xE000, std::vector<uint8_t>(j.begin() + (long)o, j.begin() + (long)std::min(j.size(), o + step)));
+    }
+    for (int f = 0; s.syntax == Syntax::kRleLossless && f < frames; ++f) {
       std::vector<uint8_t> frag(64, 0), segs;
       std::vector<uint32_t> offs;
       for (size_t k = 0; k < bps; ++k) {

@@ -24,6 +24,7 @@
 #include "nm03/numa.h"
 #include "nm03/golden.h"
 #include "nm03/jpeg.h"
+#include "nm03/jpeg_lossless.h"
 #include "nm03/kernels.h"
 #include "nm03/synth.h"
 #include "nm03/volume.h"
@@ -321,8 +322,12 @@ PYBIND11_MODULE(_nm03, m) {
       "dicom_bytes",
       [](py::array_t<uint16_t, py::array::c_style | py::array::forcecast> px, const std::string& type, int bits_stored,
          bool write_rescale, float slope, float intercept, float sx, float sy, int instance, const std::string& patient_id,
-         const std::string& syntax, bool preamble, const std::string& photometric) {
+         const std::string& syntax, bool preamble, const std::string& photometric, int jpeg_predictor,
+         int jpeg_restart_rows, int jpeg_fragments) {
         dicom::WriteSpec w;
+        w.jpeg_predictor = jpeg_predictor;
+        w.jpeg_restart_rows = jpeg_restart_rows;
+        w.jpeg_fragments = jpeg_fragments;
         // (rows, cols) or (frames, rows, cols)
         if (px.ndim() != 2 && px.ndim() != 3) throw std::invalid_argument("pixels must be 2D or 3D (frames, rows, cols)");
         w.frames = px.ndim() == 3 ? (int)px.shape(0) : 1;
@@ -344,8 +349,9 @@ PYBIND11_MODULE(_nm03, m) {
                    : syntax == "big"      ? dicom::Syntax::kExplicitBE
                    : syntax == "deflated" ? dicom::Syntax::kDeflatedLE
                    : syntax == "rle"      ? dicom::Syntax::kRleLossless
+                   : syntax == "jpeg-lossless" ? dicom::Syntax::kJpegLossless
                    : syntax == "explicit" ? dicom::Syntax::kExplicitLE
-                                          : throw std::invalid_argument("syntax: implicit|explicit|big|deflated|rle");
+                                          : throw std::invalid_argument("syntax: implicit|explicit|big|deflated|rle|jpeg-lossless");
         w.preamble = preamble;
         auto b = dicom::write(w);
         return py::bytes((const char*)b.data(), b.size());
@@ -353,7 +359,27 @@ PYBIND11_MODULE(_nm03, m) {
       py::arg("pixels"), py::arg("type") = "u16", py::arg("bits_stored") = 16, py::arg("write_rescale") = false,
       py::arg("slope") = 1.f, py::arg("intercept") = 0.f, py::arg("spacing_x") = 1.f, py::arg("spacing_y") = 1.f,
       py::arg("instance") = 1, py::arg("patient_id") = "PGBM-000", py::arg("syntax") = "explicit",
-      py::arg("preamble") = true, py::arg("photometric") = "MONOCHROME2");
+      py::arg("preamble") = true, py::arg("photometric") = "MONOCHROME2", py::arg("jpeg_predictor") = 1,
+      py::arg("jpeg_restart_rows") = 0, py::arg("jpeg_fragments") = 1);
+  m.def("jpeg_lossless_decode", [](py::bytes b) {
+    const std::string s = b;
+    std::vector<uint16_t> px;
+    const jpegll::Info i = jpegll::decode((const uint8_t*)s.data(), s.size(), px);
+    py::dict d;
+    d["precision"] = i.precision;
+    d["predictor"] = i.predictor;
+    d["point_transform"] = i.point_transform;
+    d["restart_interval"] = i.restart_interval;
+    d["pixels"] = to_np(px, {(py::ssize_t)i.rows, (py::ssize_t)i.cols});
+    return d;
+  });
+  m.def("jpeg_lossless_encode", [](py::array_t<uint16_t, py::array::c_style | py::array::forcecast> px, int precision,
+                                   int predictor, int pt, int restart_rows) {
+    if (px.ndim() != 2) throw std::invalid_argument("pixels must be 2D");
+    std::vector<uint16_t> v = from_np<uint16_t>(px);
+    auto j = jpegll::encode(v.data(), (int)px.shape(0), (int)px.shape(1), precision, predictor, pt, restart_rows);
+    return py::bytes((const char*)j.data(), j.size());
+  }, py::arg("pixels"), py::arg("precision") = 16, py::arg("predictor") = 1, py::arg("pt") = 0, py::arg("restart_rows") = 0);
   m.def("numa_parse_cpulist", &numa::parse_cpulist);
   m.def(
       "mhd_write",

@@ -254,7 +254,7 @@ TEST(dicom_mutation_fuzz) {
   auto px = ramp(3 * 12 * 16, 4093);
   for (auto& v : px) v &= 0x0FFF;
   for (Syntax sx : {Syntax::kExplicitLE, Syntax::kImplicitLE, Syntax::kExplicitBE, Syntax::kDeflatedLE,
-                    Syntax::kRleLossless})
+                    Syntax::kRleLossless, Syntax::kJpegLossless})
     for (int frames : {1, 3}) {
       WriteSpec ws;
       ws.rows = 12;
@@ -264,6 +264,12 @@ TEST(dicom_mutation_fuzz) {
       ws.pixels = px.data();
       ws.syntax = sx;
       seeds.push_back(write(ws));
+      if (sx == Syntax::kJpegLossless && frames == 1) {  // restart markers, predictor 7, split fragments
+        ws.jpeg_restart_rows = 3;
+        ws.jpeg_predictor = 7;
+        ws.jpeg_fragments = 2;
+        seeds.push_back(write(ws));
+      }
     }
   uint64_t r = 0x9E3779B97F4A7C15ull;
   auto rnd = [&](uint64_t n) {

@@ -183,14 +183,15 @@ def test_host_only_many_queued_runs(native, cohort_root, tmp_path):
 
 
 def test_host_only_compressed_and_photometric_forms(native, tmp_path):
-    """Round 5 import forms through the engine's loader (host path): Deflated Explicit VR LE, RLE
-    Lossless and MONOCHROME1 load like plain files; a multi-frame file is a per-slice load error by
+    """Round 5/6 import forms through the engine's loader (host path): Deflated Explicit VR LE, RLE
+    Lossless, lossless JPEG (.4.70 / .4.57, split fragments) and MONOCHROME1 load like plain files; a multi-frame file is a per-slice load error by
     default and loads when a frame is selected; a JPEG-family file is skipped and counted."""
     import numpy as np
     d = tmp_path / "in"
     d.mkdir()
     good = native.phantom_slice(256, 256, 1, 3, 10, 7)
-    forms = [dict(syntax="deflated"), dict(syntax="rle"), dict(photometric="MONOCHROME1"), dict(syntax="rle", photometric="MONOCHROME1")]
+    forms = [dict(syntax="deflated"), dict(syntax="rle"), dict(photometric="MONOCHROME1"), dict(syntax="rle", photometric="MONOCHROME1"),
+             dict(syntax="jpeg-lossless"), dict(syntax="jpeg-lossless", jpeg_predictor=6, jpeg_fragments=2)]
     paths = []
     for k, kw in enumerate(forms, 1):
         p = d / f"1-{k}.dcm"
@@ -202,10 +203,15 @@ def test_host_only_compressed_and_photometric_forms(native, tmp_path):
     out = tmp_path / "out"
     out.mkdir()
     items = [(str(p), str(out)) for p in paths]
+    nf = len(forms)
     st, _ = _engine(native).run(items)
-    assert [c for c, _ in st] == [0, 0, 0, 0, 1]
-    assert "Multi-frame DICOM (3 frames)" in st[4][1]
+    assert [c for c, _ in st] == [0] * nf + [1]
+    assert "Multi-frame DICOM (3 frames)" in st[nf][1]
     st, _ = _engine(native, frame=1).run(items)
-    assert [c for c, _ in st] == [0] * 5
+    assert [c for c, _ in st] == [0] * (nf + 1)
     st, _ = _engine(native, frame=3).run(items)
-    assert [c for c, _ in st] == [0, 0, 0, 0, 1] and "Frame 3 requested" in st[4][1]
+    assert [c for c, _ in st] == [0] * nf + [1] and "Frame 3 requested" in st[nf][1]
+    # lossless JPEG (round 6) loads the same samples as the plain encoding
+    for p in paths[4:6]:
+        raw, _ = native.read_slice(str(p))
+        assert np.array_equal(raw, good)

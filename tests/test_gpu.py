@@ -1229,8 +1229,9 @@ def test_volume_ball_se_vs_golden(native):
 
 
 def test_engine_new_dicom_forms_bit_exact(native, tmp_path):
-    """Deflated, RLE, MONOCHROME1 and a selected frame of a multi-frame file through the GPU engine:
-    both JPEGs equal the golden export of the same samples as the plain reader imports them."""
+    """Deflated, RLE, lossless JPEG, MONOCHROME1 and a selected frame of a multi-frame file through the
+    GPU engine: both JPEGs equal the golden export of the same samples as the plain reader imports them
+    (lossless JPEG: the decoded samples equal the plain encoding's; parity with DCMTK unpinned)."""
     d = tmp_path / "in"
     d.mkdir()
     a, b, c = (native.phantom_slice(256, 256, 2, k, 9, 3) for k in (2, 4, 6))
@@ -1239,6 +1240,10 @@ def test_engine_new_dicom_forms_bit_exact(native, tmp_path):
         "1-2.dcm": native.dicom_bytes(b, bits_stored=12, syntax="rle"),
         "1-3.dcm": native.dicom_bytes(c, bits_stored=12, photometric="MONOCHROME1"),
         "1-4.dcm": native.dicom_bytes(np.stack([a, b, c]), bits_stored=12, syntax="rle"),
+        # round 6: lossless JPEG (SV1 = .4.70; SV5 with restart markers and split fragments = .4.57)
+        "1-5.dcm": native.dicom_bytes(a, bits_stored=12, syntax="jpeg-lossless"),
+        "1-6.dcm": native.dicom_bytes(c, bits_stored=12, syntax="jpeg-lossless", jpeg_predictor=5,
+                                      jpeg_restart_rows=32, jpeg_fragments=3),
     }
     for name, data in files.items():
         (d / name).write_bytes(data)
@@ -1246,7 +1251,7 @@ def test_engine_new_dicom_forms_bit_exact(native, tmp_path):
     out.mkdir()
     items = [(str(d / n), str(out)) for n in files]
     st, _ = native.Engine(nm.PipelineConfig(batch_size=4, streams=2, threads=4, frame=1).engine_config()).run(items)
-    assert [c for c, _ in st] == [0, 0, 0, 0], st
+    assert [c for c, _ in st] == [0] * len(files), st
     for name in files:
         raw, meta = native.read_slice(str(d / name), 0, 1)
         g = native.golden_run(raw, meta["type"], meta["stored_bits"], meta["slope"], meta["intercept"],
@@ -1254,6 +1259,8 @@ def test_engine_new_dicom_forms_bit_exact(native, tmp_path):
         stem = name[:-4]
         assert open(out / f"{stem}_original.jpg", "rb").read() == g["jpeg_original"], name
         assert open(out / f"{stem}_processed.jpg", "rb").read() == g["jpeg_processed"], name
+    for name, src in (("1-5.dcm", a), ("1-6.dcm", c)):
+        assert np.array_equal(native.read_slice(str(d / name))[0], src)
     # MONOCHROME1 is imported inverted: its golden input is the complement of the stored samples
     raw3, _ = native.read_slice(str(d / "1-3.dcm"))
     assert np.array_equal(raw3, (~c) & np.uint16(0x0FFF))
@@ -1355,3 +1362,49 @@ def test_deferred_rccl_comm_single_rank(native):
     t = c.data_plane_times
     assert t["start_s"] >= 0 and t["init_upper_s"] >= t["wait_s"] >= 0
     seg.wait_attached_and_unlink(5.0)
+
+
+def test_cli_parallel_rccl_data_plane_one_rank(native, cohort_root, tmp_path):
+    """the CLI's RCCL path on hardware. NM03_COMM=rccl at one rank takes launch_ranks'
+    deferred communicator: the start-up thread brings HIP up, starts AND settles RCCL, then builds the
+    engine (RCCL is never initialising while the engine is constructed or launches); after the run the
+    collectives are promoted onto RCCL. Outputs equal the default run and the golden model."""
+    import json
+    ref, out = tmp_path / "ref", tmp_path / "rccl"
+    r0 = run_bin("img_processing_parallel", "--data-root", cohort_root, "--out", str(ref), "--gpus", "1", "--quiet")
+    assert r0.returncode == 0, r0.stderr
+    js = tmp_path / "rccl.json"
+    r = run_bin("img_processing_parallel", "--data-root", cohort_root, "--out", str(out), "--gpus", "1", "--quiet",
+                "--repeat", "2", "--json", str(js), env={"NM03_COMM": "rccl", "NM03_COMM_TIMEOUT_S": "60"}, timeout=240)
+    assert r.returncode == 0, r.stderr
+    j = json.load(open(js))
+    assert j["data_plane"] is True and j["backend"] == "rccl", j
+    assert j["comm"]["backend"] == "rccl" and j["comm"]["nranks"] == 1 and "rccl_error" not in j["comm"], j["comm"]
+    assert j["devices"]["transport_size"] == [1] and j["devices"]["transport_device"] == [0]
+    assert j["comm_settle_s"] > 0 and j["data_plane_s"] >= j["comm_settle_s"]
+    assert j["slices_ok"] == j["slices"] and j["slices"] > 0
+    t_ref, t_out = _tree(str(ref)), _tree(str(out))
+    assert t_ref == t_out and len(t_out) == j["slices"]  # two JPEGs per slice; --repeat 2 counts each twice
+    for pid in ("PGBM-001", "PGBM-003"):
+        _, files = native.list_patient_series(native.cohort_dir(cohort_root), pid)
+        f = files[len(files) // 2]
+        raw, meta = native.read_slice(f)
+        g = native.golden_run(raw, meta["type"], meta["stored_bits"], meta["slope"], meta["intercept"],
+                              native.PipelineParams(), native.RenderParams(), meta["spacing_x"], meta["spacing_y"])
+        stem = os.path.splitext(os.path.basename(f))[0]
+        assert open(out / pid / f"{stem}_original.jpg", "rb").read() == g["jpeg_original"]
+        assert open(out / pid / f"{stem}_processed.jpg", "rb").read() == g["jpeg_processed"]
+
+
+@pytest.mark.skipif(torch.cuda.device_count() < 2, reason="needs two GPUs (RCCL refuses two ranks on one device)")
+def test_cli_parallel_rccl_two_devices(native, cohort_root, tmp_path):
+    """two ranks on distinct devices with NM03_COMM=rccl promote onto RCCL; rank 1's
+    collectives run on its main thread, which never selected device 1 itself (RcclComm binds it)."""
+    import json
+    js = tmp_path / "m.json"
+    r = run_bin("img_processing_parallel", "--data-root", cohort_root, "--out", str(tmp_path / "o"), "--gpus", "2",
+                "--quiet", "--json", str(js), env={"NM03_COMM": "rccl", "NM03_COMM_TIMEOUT_S": "60"}, timeout=240)
+    assert r.returncode == 0, r.stderr
+    j = json.load(open(js))
+    assert j["backend"] == "rccl" and j["comm"]["nranks"] == 2 and j["devices"]["transport_device"] == [0, 1]
+    assert sum(j["per_rank"]["slices_ok"]) == j["slices"]
