@@ -156,5 +156,8 @@ int64_t count_cohort_slices(const AppConfig& cfg);
 bool apply_copy_engine(const AppConfig& cfg, int64_t slices_per_rank);
 // "blit" when the process runs with HSA_ENABLE_SDMA=0, else "sdma" (the CLI --json records it).
 const char* copy_engine_name();
+// The process runs with one HIP hardware queue (GPU_MAX_HW_QUEUES=1): the CLIs then give their
+// engine one shared stream (EngineConfig::shared_stream).
+bool one_hw_queue();
 
 }  // namespace nm03::app

@@ -74,10 +74,22 @@ struct EngineConfig {
   // into the output buffer (what the encoder's PCIe stores would leave in memory). Measures the
   // host side's CPU per slice on its own, on any machine (bench.py --host-only).
   bool host_only = false;
-  // Host-mapped bytes per image for the GPU encoder's stuffed output (0 = half the canvas: 128 KiB
-  // for 512², ~5x a typical medical render). Larger images are CPU re-encoded (StageTimes counts
-  // them); tests force that path with a tiny capacity.
+  // Host-mapped bytes per image for the GPU encoder's stuffed output (0 = a quarter of the canvas:
+  // 64 KiB for 512², ≈ 5× a typical medical render of 12 KiB; round 5 used half the canvas, whose
+  // pinning was a third of a cold CLI's engine constructor). Larger images are CPU re-encoded
+  // (StageTimes counts them); tests force that path with a tiny capacity.
   uint32_t jpeg_out_cap = 0;
+  // Every slot and the uploads on ONE HIP stream (false: a stream per slot plus a shared upload
+  // stream). For processes limited to one HW queue (GPU_MAX_HW_QUEUES=1, the CLIs' short jobs), where
+  // separate streams add no device concurrency — they all feed the same queue in submission order —
+  // but each costs ≈ 3.8 ms to create on a cold process. The slots' host work (loads, writes) still
+  // overlaps: each slot waits on its own batch's event.
+  bool shared_stream = false;
+  // Slack in each slot's raw region for single-pass packing of slices wider than 12 bits (u16 elements
+  // per pool thread; -1 = one 3/4-size slice per thread, 0 = none: such slices are range-checked
+  // first and packed in a second pass). The CLIs pass 0 when rank 0's header scan saw no slice with
+  // more than 12 stored bits: 1.5 MB less pinned memory per slot.
+  int pack_slack = -1;
   // Progressive upload: a batch's finished prefix of raw pixels is queued for H2D once it has grown
   // by this many KiB while its loads still run (-1 = 2048; 0 = one upload per batch after all loads).
   int upload_chunk_kb = -1;

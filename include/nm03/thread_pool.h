@@ -4,7 +4,10 @@
 // so patient and batch boundaries never idle the workers.
 #pragma once
 
+#include <linux/futex.h>
 #include <pthread.h>
+#include <sys/syscall.h>
+#include <unistd.h>
 #include <time.h>
 
 #include <algorithm>
@@ -22,10 +25,35 @@
 
 namespace nm03 {
 
+// A mutex whose contended path spins (try_lock with pause) before it sleeps. The pool's critical
+// sections are a heap push/pop of a few hundred ns, taken by up to 16 workers at the same instant (a
+// for_each fans out one runner per worker): with std::mutex alone the losers slept in the kernel and
+// their unlockers paid a futex wake — 8–11% of the pool's CPU in the round-6 sampling profile
+// (profiles/r6/cpu_profile/). Spinning keeps the lock word uncontended (no futex wake on unlock).
+class SpinThenBlockMutex {
+ public:
+  void lock() {
+    for (int i = 0; i < 4096; ++i) {
+      if (m_.try_lock()) return;
+      __builtin_ia32_pause();
+    }
+    m_.lock();
+  }
+  bool try_lock() { return m_.try_lock(); }
+  void unlock() { m_.unlock(); }
+
+ private:
+  std::mutex m_;
+};
+
 // Tasks carry a priority (lower runs first; FIFO among equals). The engine uses the batch index,
 // so the loads and exports of earlier batches overtake later ones: the first batch reaches the GPU
 // after ~batch/threads loads instead of after every in-flight slot's loads (pipeline fill), and the
 // last batches' exports are not queued behind anything (drain).
+//
+// Idle workers spin on the queue size, then sleep on a futex word that every push bumps (an
+// eventcount): a wake-up costs a futex wake only when a worker sleeps, and woken workers do not
+// queue up on a condition variable's mutex (the round-6 profile's lock waits inside loop()).
 class ThreadPool {
  public:
   // `on_start(i)` runs first on worker thread i (e.g. CPU pinning).
@@ -41,11 +69,11 @@ class ThreadPool {
   }
   ~ThreadPool() {
     {
-      std::lock_guard<std::mutex> g(m_);
+      std::lock_guard<SpinThenBlockMutex> g(m_);
       stop_ = true;
     }
-    stop_flag_.store(true, std::memory_order_relaxed);
-    cv_.notify_all();
+    stop_flag_.store(true, std::memory_order_seq_cst);
+    wake(1 << 30);
     for (auto& t : workers_) t.join();
   }
   ThreadPool(const ThreadPool&) = delete;
@@ -53,21 +81,18 @@ class ThreadPool {
 
   void submit(std::function<void()> f, uint64_t prio = 0) {
     {
-      std::lock_guard<std::mutex> g(m_);
+      std::lock_guard<SpinThenBlockMutex> g(m_);
       push(std::move(f), prio);
     }
-    cv_.notify_one();
+    wake(1);
   }
   // `n` copies of `f` under one lock (bulk fan-out of a parallel-for).
   void submit_n(int n, const std::function<void()>& f, uint64_t prio = 0) {
     {
-      std::lock_guard<std::mutex> g(m_);
+      std::lock_guard<SpinThenBlockMutex> g(m_);
       for (int i = 0; i < n; ++i) push(f, prio);
     }
-    if (n == 1)
-      cv_.notify_one();
-    else
-      cv_.notify_all();
+    wake(n);
   }
   int size() const { return (int)workers_.size(); }
   // Index of the calling pool worker thread (-1 outside any pool).
@@ -88,41 +113,64 @@ class ThreadPool {
     std::push_heap(q_.begin(), q_.end(), later);
     queued_.store(q_.size(), std::memory_order_relaxed);
   }
-  // Spin (polling the queue size without the lock) for up to spin_us before sleeping on the
-  // condition variable: a task submitted shortly after the queue ran dry starts without a futex
-  // wake-up and the scheduler's wake-up latency.
+  // After a push (outside the lock): bump the eventcount, wake up to n sleepers.
+  void wake(int n) {
+    wake_seq_.fetch_add(1, std::memory_order_seq_cst);
+    if (sleepers_.load(std::memory_order_seq_cst) > 0)
+      syscall(SYS_futex, reinterpret_cast<uint32_t*>(&wake_seq_), FUTEX_WAKE_PRIVATE, n, nullptr, nullptr, 0);
+  }
+  // Spin (polling the queue size without the lock) for up to spin_us before sleeping: a task
+  // submitted shortly after the queue ran dry starts without a futex wake-up and the scheduler's
+  // wake-up latency.
   // Measured on the shared boxes (profiles/r3/pool_spin/): 0 / 50 / 200 µs gave 329–398k /
   // 345–398k / 357–398k slices/s over 4 interleaved rounds at equal host CPU per step — equal on
   // quiet boxes, up to +20% when other tenants load the host (delayed wake-ups).
   static constexpr int kSpinUs = 200;
   void loop() {
     for (;;) {
-      std::function<void()> f;
       if (queued_.load(std::memory_order_relaxed) == 0) {
         const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(kSpinUs);
-        while (queued_.load(std::memory_order_relaxed) == 0 && !stop_flag_.load(std::memory_order_relaxed) &&
-               std::chrono::steady_clock::now() < until)
+        // the clock is read every 64 polls, not every poll (a vDSO call each)
+        for (int k = 0; queued_.load(std::memory_order_relaxed) == 0 && !stop_flag_.load(std::memory_order_relaxed);
+             ++k) {
           __builtin_ia32_pause();
+          if ((k & 63) == 63 && std::chrono::steady_clock::now() >= until) break;
+        }
       }
+      std::function<void()> f;
+      uint32_t seq = 0;
       {
-        std::unique_lock<std::mutex> g(m_);
-        cv_.wait(g, [this] { return stop_ || !q_.empty(); });
-        if (stop_ && q_.empty()) return;
-        std::pop_heap(q_.begin(), q_.end(), later);
-        f = std::move(q_.back().f);
-        q_.pop_back();
-        queued_.store(q_.size(), std::memory_order_relaxed);
+        std::lock_guard<SpinThenBlockMutex> g(m_);
+        if (!q_.empty()) {
+          std::pop_heap(q_.begin(), q_.end(), later);
+          f = std::move(q_.back().f);
+          q_.pop_back();
+          queued_.store(q_.size(), std::memory_order_relaxed);
+        } else {
+          if (stop_) return;
+          seq = wake_seq_.load(std::memory_order_seq_cst);  // a push after this unlock bumps it
+        }
       }
-      f();
+      if (f) {
+        f();
+        continue;
+      }
+      sleepers_.fetch_add(1, std::memory_order_seq_cst);
+      while (wake_seq_.load(std::memory_order_seq_cst) == seq && !stop_flag_.load(std::memory_order_seq_cst)) {
+        timespec ts{0, 50 * 1000 * 1000};  // bounded: a missed wake-up costs at most this
+        syscall(SYS_futex, reinterpret_cast<uint32_t*>(&wake_seq_), FUTEX_WAIT_PRIVATE, seq, &ts, nullptr, 0);
+      }
+      sleepers_.fetch_sub(1, std::memory_order_seq_cst);
     }
   }
   std::vector<std::thread> workers_;
   std::vector<Task> q_;  // binary heap on (prio, seq)
   std::atomic<size_t> queued_{0};     // q_.size(), readable without the lock (spin phase)
   std::atomic<bool> stop_flag_{false};
+  std::atomic<uint32_t> wake_seq_{0};  // eventcount: bumped by every push (futex word)
+  std::atomic<int> sleepers_{0};
   uint64_t seq_ = 0;
-  std::mutex m_;
-  std::condition_variable cv_;
+  SpinThenBlockMutex m_;
   bool stop_ = false;
 };
 
@@ -132,16 +180,14 @@ inline int64_t thread_cpu_now_ns() {
   return (int64_t)ts.tv_sec * 1000000000 + ts.tv_nsec;
 }
 
-// Counts outstanding tasks; wait() blocks until all submitted through it finished.
+// Counts outstanding tasks; wait() blocks until all submitted through it finished. The count is an
+// atomic: only the task that brings it to zero takes the mutex (to wake a sleeping waiter), so the
+// 16 runners of a for_each finishing together do not queue on a lock.
 class TaskGroup {
  public:
   explicit TaskGroup(ThreadPool& p) : pool_(p) {}
   void run(std::function<void()> f, uint64_t prio = 0) {
-    {
-      std::lock_guard<std::mutex> g(m_);
-      ++pending_;
-      pending_a_.store(pending_, std::memory_order_release);
-    }
+    pending_.fetch_add(1, std::memory_order_acq_rel);
     pool_.submit(
         [this, f = std::move(f)] {
           f();
@@ -164,11 +210,7 @@ class TaskGroup {
     auto st = std::make_shared<ForEach>();
     st->n = n;
     st->fn = std::move(fn);
-    {
-      std::lock_guard<std::mutex> g(m_);
-      pending_ += (size_t)runners;
-      pending_a_.store(pending_, std::memory_order_release);
-    }
+    pending_.fetch_add((size_t)runners, std::memory_order_acq_rel);
     pool_.submit_n(
         runners,
         [this, st, cpu_ns] {
@@ -183,13 +225,14 @@ class TaskGroup {
   // continues without a wake-up.
   void wait(int spin_us = 0) {
     const int spin = spin_us;
-    if (spin > 0 && pending_a_.load(std::memory_order_acquire) != 0) {
+    if (spin > 0 && pending_.load(std::memory_order_acquire) != 0) {
       const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(spin);
-      while (pending_a_.load(std::memory_order_acquire) != 0 && std::chrono::steady_clock::now() < until)
+      while (pending_.load(std::memory_order_acquire) != 0 && std::chrono::steady_clock::now() < until)
         __builtin_ia32_pause();
     }
+    // Under m_ even when the count is already zero: the finishing task may still hold it (done()).
     std::unique_lock<std::mutex> g(m_);
-    cv_.wait(g, [this] { return pending_ == 0; });
+    cv_.wait(g, [this] { return pending_.load(std::memory_order_acquire) == 0; });
   }
   ~TaskGroup() { wait(); }
 
@@ -200,16 +243,19 @@ class TaskGroup {
     std::function<void(size_t)> fn;
   };
   void done(size_t k) {
+    // Lock-free unless this task may finish the group. The final decrement happens under m_: a
+    // waiter that sees the count reach zero without the lock then takes m_ before it returns (and
+    // the group may be destroyed), so it cannot return while the finishing task still uses m_ or cv_.
+    size_t cur = pending_.load(std::memory_order_acquire);
+    while (cur > k)
+      if (pending_.compare_exchange_weak(cur, cur - k, std::memory_order_acq_rel, std::memory_order_acquire)) return;
     std::lock_guard<std::mutex> g(m_);
-    pending_ -= k;
-    pending_a_.store(pending_, std::memory_order_release);
-    if (pending_ == 0) cv_.notify_all();
+    if (pending_.fetch_sub(k, std::memory_order_acq_rel) == k) cv_.notify_all();
   }
   ThreadPool& pool_;
   std::mutex m_;
   std::condition_variable cv_;
-  size_t pending_ = 0;
-  std::atomic<size_t> pending_a_{0};  // pending_, readable without the lock (wait's spin phase)
+  std::atomic<size_t> pending_{0};
 };
 
 }  // namespace nm03

@@ -257,12 +257,14 @@ int run_sequential(const AppConfig& cfg) {
     const int64_t cohort_slices = cfg.copy_engine == kCopyAuto ? count_cohort_slices(cfg) : -1;
     apply_copy_engine(cfg, cohort_slices < 0 ? -1 : cohort_slices * std::max(1, cfg.repeat));
     // HIP start-up and the engine's construction on the start-up thread while the output root is set up.
-    EngineStartup su(cfg.engine.device, std::max(1, cfg.engine.streams) + 1);
+    EngineConfig ec = cfg.engine;
+    ec.shared_stream = one_hw_queue();  // as in parallel_rank
+    EngineStartup su(ec.device, ec.shared_stream ? 1 : std::max(1, ec.streams) + 1);
     // SequentialImageProcessor ctor: base output dir (main_sequential.cpp:81-91).
     cohort::make_dirs(cfg.out_dir);
     const std::string base = cohort::cohort_dir(cfg.data_root);
     std::string setup_error;
-    auto engine_p = su.build(cfg.engine, &setup_error);
+    auto engine_p = su.build(ec, &setup_error);
     if (!engine_p) throw std::runtime_error(setup_error);
     Engine& engine = *engine_p;
     // The process ends in cli_exit: the engine's buffers are left to the kernel, not unpinned.
@@ -454,24 +456,32 @@ std::string per_rank_json(const std::vector<std::vector<double>>& rows) {
   return o.str();
 }
 
-// Largest slice dimension over the plan's files (16 KiB header prefix per file, parsed on a small
-// thread pool); unreadable files are skipped (they fail in the engine's loader as usual).
-int scan_max_dim(const std::vector<PatientPlan>& plan, int threads) {
+// Largest slice dimension and largest BitsStored over the plan's files (16 KiB header prefix per
+// file, parsed on a small thread pool); unreadable files are skipped (they fail in the engine's loader
+// as usual). The engine is sized from them: buffers for the largest slice instead of the 512² maximum,
+// and no single-pass packing slack when no slice stores more than 12 bits.
+struct HeaderScan {
+  int max_dim = 0, max_bits = 0;
+};
+HeaderScan scan_headers(const std::vector<PatientPlan>& plan, int threads) {
   std::vector<const std::string*> files;
   for (const auto& p : plan)
     for (const auto& f : p.files) files.push_back(&f);
-  std::atomic<int> md{0};
+  std::atomic<int> md{0}, mb{0};
   std::atomic<size_t> next{0};
+  auto raise = [](std::atomic<int>& a, int v) {
+    int cur = a.load();
+    while (v > cur && !a.compare_exchange_weak(cur, v)) {
+    }
+  };
   auto work = [&] {
     std::vector<uint8_t> buf;
     for (size_t i; (i = next.fetch_add(1)) < files.size();) {
       try {
         dicom::SliceFile f(*files[i], dicom::ReadMode::kDirect, 16384);
         const dicom::Header& h = f.header(buf);
-        const int m = std::max(h.rows, h.cols);
-        int cur = md.load();
-        while (m > cur && !md.compare_exchange_weak(cur, m)) {
-        }
+        raise(md, std::max(h.rows, h.cols));
+        raise(mb, h.bits_stored > 0 ? h.bits_stored : h.bits_allocated);
       } catch (const std::exception&) {
       }
     }
@@ -481,7 +491,7 @@ int scan_max_dim(const std::vector<PatientPlan>& plan, int threads) {
   for (int t = 1; t < nt; ++t) th.emplace_back(work);
   work();
   for (auto& t : th) t.join();
-  return md.load();
+  return {md.load(), mb.load()};
 }
 
 }  // namespace
@@ -625,7 +635,11 @@ int parallel_rank(const AppConfig& cfg, int rank, int size, Comm& comm, int devi
   const std::string comm_mode = comm_env && *comm_env ? comm_env : "auto";
   const bool data_plane =
       comm_mode == "rccl" || (size > 1 && comm_mode == "auto" && work_per_rank > kBlitMaxSlicesPerRank);
-  EngineStartup su(device, std::max(1, cfg.engine.streams) + 1, data_plane ? &comm : nullptr);  // slots + upload stream
+  // One HW queue (--hw-queues auto for short jobs on shader copies, or the user's 1): every slot
+  // shares one HIP stream — separate streams would feed the same queue anyway — and the start-up
+  // thread creates one stream instead of slots + 1 (≈ 3.8 ms each on a cold process).
+  ec.shared_stream = one_hw_queue();
+  EngineStartup su(device, ec.shared_stream ? 1 : std::max(1, cfg.engine.streams) + 1, data_plane ? &comm : nullptr);
   double engine_wait_s = 0, plan_s = 0, setup_tail_s = 0;
   std::unique_ptr<Engine> engine_p;
   std::vector<RankDevice> devices;
@@ -679,7 +693,10 @@ int parallel_rank(const AppConfig& cfg, int rank, int size, Comm& comm, int devi
       }
       plan_bytes = encode_plan(plan);
       ByteWriter dims;
-      dims.u32(!engine_p && !cfg.max_dim_set ? (uint32_t)scan_max_dim(plan, cfg.engine.threads) : 0u);
+      HeaderScan hs;
+      if (!engine_p && !cfg.max_dim_set) hs = scan_headers(plan, cfg.engine.threads);
+      dims.u32((uint32_t)hs.max_bits);
+      dims.u32((uint32_t)hs.max_dim);
       plan_bytes.insert(plan_bytes.end(), dims.b.begin(), dims.b.end());
     }
     comm.allreduce_sum_i64(&fatal, 1);
@@ -688,16 +705,21 @@ int parallel_rank(const AppConfig& cfg, int rank, int size, Comm& comm, int devi
       return 1;
     }
     comm.broadcast_bytes(plan_bytes, 0);  // ncclBroadcast of the serialized work list
-    uint32_t seen_dim = 0;
-    if (plan_bytes.size() >= 4) {
-      ByteReader dr(plan_bytes.data() + plan_bytes.size() - 4, 4);
+    uint32_t seen_dim = 0, seen_bits = 0;
+    if (plan_bytes.size() >= 8) {
+      ByteReader dr(plan_bytes.data() + plan_bytes.size() - 8, 8);
+      seen_bits = dr.u32();
       seen_dim = dr.u32();
-      plan_bytes.resize(plan_bytes.size() - 4);
+      plan_bytes.resize(plan_bytes.size() - 8);
     }
     if (!engine_p) {
       // Buffers sized for the largest slice of the cohort (headers scanned by rank 0) instead of
       // the 512² maximum: less pinned memory to allocate and register at start-up.
       if (seen_dim > 0) ec.max_dim = std::min(gpu::kMaxSliceDim, std::max(64, (int)((seen_dim + 63) / 64 * 64)));
+      // No slice stores more than 12 bits: every packable slice packs in one pass without a
+      // reservation that might have to be abandoned, so the slots need no slack (a wider slice
+      // arriving anyway still loads: range check, then pack).
+      if (seen_bits > 0 && seen_bits <= 12) ec.pack_slack = 0;
       // Where this rank runs: its GPU's PCI bus id, and a CPU partition of that GPU's NUMA node
       // disjoint from every other rank's, with a pool sized to it and to the rank's share of the
       // CPU budget (the reference's one machine-wide omp_set_num_threads(16), main_parallel.cpp:401).
@@ -877,7 +899,8 @@ int parallel_rank(const AppConfig& cfg, int rank, int size, Comm& comm, int devi
                              ", \"gpus_requested\": " + req + ", \"main_unix_s\": " +
                              fmt(cfg.main_unix_s, 17) + ", \"backend\": \"" +
                              std::string(data_plane || size == 1 ? comm.backend() : "host") + "\", \"copy_engine\": \"" +
-                             copy_engine_name() + "\", \"repeat\": " +
+                             copy_engine_name() + "\", \"shared_stream\": " + (ec.shared_stream ? "true" : "false") +
+                             ", \"pack_slack\": " + std::to_string(ec.pack_slack) + ", \"repeat\": " +
                              std::to_string(cfg.repeat) + ", \"engine_setup_s\": " +
                              fmt(setup_s) + ", \"hip_init_s\": " + fmt(su.times().hip_init_s) + ", \"engine_ctor_s\": " +
                              fmt(su.times().engine_ctor_s) + ", \"streams_s\": " + fmt(su.times().streams_s) + ", \"engine_wait_s\": " + fmt(engine_wait_s) + ", \"kernel_load_s\": " +
@@ -951,6 +974,11 @@ int64_t count_cohort_slices(const AppConfig& cfg) {
   } catch (const std::exception&) {
     return -1;
   }
+}
+
+bool one_hw_queue() {
+  const char* q = std::getenv("GPU_MAX_HW_QUEUES");
+  return q && std::string(q) == "1";
 }
 
 // What the process's HIP runtime uses (read from the environment it starts with).

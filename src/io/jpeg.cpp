@@ -276,8 +276,10 @@ void write_jpeg_at(int dirfd, const std::string& dir, const std::string& name, c
       iov[idx].iov_len -= adv;
     }
   }
-  struct stat st;
-  if (!fresh && fstat(fd, &st) == 0 && (size_t)st.st_size > total && ftruncate(fd, (off_t)total) != 0) {
+  // The previous file's size by lseek(SEEK_END) (an fstat copies a whole struct stat: 1.3% of the
+  // pool's CPU in the round-6 profile).
+  const off_t end = fresh ? 0 : ::lseek(fd, 0, SEEK_END);
+  if (end > (off_t)total && ftruncate(fd, (off_t)total) != 0) {
     ::close(fd);
     throw std::runtime_error("Truncate failed: " + path());
   }

@@ -75,6 +75,7 @@ struct Slot {
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
   hipStream_t up = nullptr;  // stream of this slot's H2D copies: its own stream, or the engine's shared one
+  bool owns_stream = true;   // false: EngineConfig::shared_stream (the engine destroys it)
   int cap_slices = 0, cap_canvases = 0;
   size_t cap_pixels = 0;  // u16 elements of expanded samples per batch (device raw/median buffers)
   // The blob's raw region also holds `hole_slack` u16 of slack for abandoned 12-bit reservations
@@ -109,20 +110,29 @@ struct Slot {
   uint8_t* d_out = nullptr;
   int32_t* h_sizes = nullptr;
   int32_t* d_sizes = nullptr;
-  std::atomic<size_t> raw_used{0};
   std::vector<LoadedSlice> loaded;
   // Progressive upload: raw-region allocations in offset order with a done flag each; the slot
   // thread uploads the longest finished prefix while later loads are still running.
   struct Alloc {
-    size_t off = 0, len = 0;  // u16 elements
+    size_t off = 0, len = 0;  // u16 elements; written before `done` is released
     std::atomic<bool> done{false};
   };
   std::unique_ptr<Alloc[]> allocs;
-  size_t n_allocs = 0;
-  std::mutex alloc_m;
+  size_t max_allocs = 0;
+  // Allocation word, claimed lock-free by the loaders: the number of allocations (bits 40..63) and
+  // the u16 elements of the raw region in use (bits 0..39), so that allocation k always lies at a
+  // higher offset than allocation k−1 (one CAS per load; round 5 took alloc_m for it, and the
+  // loaders' contention on that and on prog_m was ≈ 8% of the pool's CPU, profiles/r6/cpu_profile/).
+  static constexpr int kAllocShift = 40;
+  static constexpr uint64_t kUsedMask = (uint64_t(1) << kAllocShift) - 1;
+  std::atomic<uint64_t> alloc_word{0};
+  size_t raw_used() const { return (size_t)(alloc_word.load(std::memory_order_acquire) & kUsedMask); }
+  size_t n_allocs() const { return (size_t)(alloc_word.load(std::memory_order_acquire) >> kAllocShift); }
+  std::mutex alloc_m;  // hole_credit only (slices wider than 12 bits)
   std::mutex prog_m;
   std::condition_variable prog_cv;
-  size_t loads_finished = 0;  // guarded by prog_m
+  std::atomic<size_t> loads_finished{0};
+  std::atomic<bool> prog_waiting{false};  // the slot thread sleeps (or is about to) on prog_cv
   // Set by upload_progress when the whole batch fits in one upload chunk: loaders stop notifying
   // (a wake-up of the slot thread per load, on CPUs the loaders need, for nothing to upload early).
   std::atomic<bool> progress_quiet{false};
@@ -213,7 +223,7 @@ void hip_free_all(Slot& s) {
   if (s.ev0) (void)hipEventDestroy(s.ev0);
   if (s.ev1) (void)hipEventDestroy(s.ev1);
   if (s.ev2) (void)hipEventDestroy(s.ev2);
-  if (s.stream) (void)hipStreamDestroy(s.stream);
+  if (s.stream && s.owns_stream) (void)hipStreamDestroy(s.stream);
 }
 
 // Streams created ahead of the engine (reserve_streams), per device.
@@ -276,7 +286,7 @@ struct Engine::Impl {
   explicit Impl(const EngineConfig& c) : cfg(c), place(c.device, c.cpus) {
     if (const char* e = std::getenv("NM03_PACK12"); e && *e && *e == '0') pack12_ = false;
     out_cap_ = cfg.jpeg_out_cap ? std::max<uint32_t>(64, cfg.jpeg_out_cap)
-                                : (uint32_t)std::max<size_t>(64 * 1024, (size_t)cfg.render.out_width * cfg.render.out_height / 2) + 64;
+                                : (uint32_t)std::max<size_t>(32 * 1024, (size_t)cfg.render.out_width * cfg.render.out_height / 4) + 64;
     out_cap_ = (out_cap_ + 15u) & ~15u;  // 16-byte aligned segments (the encoder's dwordx4 stores)
     upload_chunk_ = cfg.upload_chunk_kb < 0 ? (size_t)2 << 20 : (size_t)cfg.upload_chunk_kb << 10;
     host_only_ = cfg.host_only;
@@ -486,6 +496,14 @@ struct Engine::Impl {
     return on;
   }
 
+  static bool event_timing() {
+    static const bool on = [] {
+      const char* e = std::getenv("NM03_EVENT_TIMING");
+      return !(e && *e == '0');
+    }();
+    return on;
+  }
+
   void make_templates() {
     golden::SliceInput in;
     in.w = in.h = 256;
@@ -547,7 +565,8 @@ struct Engine::Impl {
     s.off_jpeg = o;
     o = align_up(o + (size_t)s.cap_canvases * sizeof(JpegDesc), kAlign);
     s.raw_base = o;
-    s.hole_slack = (size_t)std::max(cfg.threads, 1) * align_up((size_t)md * md / 4 * 3, 8);
+    s.hole_slack = cfg.pack_slack < 0 ? (size_t)std::max(cfg.threads, 1) * align_up((size_t)md * md / 4 * 3, 8)
+                                      : (size_t)cfg.pack_slack * std::max(cfg.threads, 1);
     s.blob_bytes = o + (s.cap_pixels + s.hole_slack) * sizeof(uint16_t);
   }
 
@@ -586,13 +605,21 @@ struct Engine::Impl {
       return sp;
     }
     try {
-      s.stream = take_stream(cfg.device, "hipStreamCreate");
-      s.up = upload_stream();
+      if (cfg.shared_stream) {
+        s.stream = s.up = upload_stream();  // the engine's one stream (destroyed by ~Impl)
+        s.owns_stream = false;
+      } else {
+        s.stream = take_stream(cfg.device, "hipStreamCreate");
+        s.up = upload_stream();
+      }
       mark("streams");
-      check_hip(hipEventCreate(&s.ev0), "hipEventCreate");
-      check_hip(hipEventCreate(&s.ev1), "hipEventCreate");
+      // NM03_EVENT_TIMING=0 (experiment): events without timestamps; StageTimes then has no h2d /
+      // kernel split.
+      const unsigned ef = event_timing() ? hipEventDefault : hipEventDisableTiming;
+      check_hip(hipEventCreateWithFlags(&s.ev0, ef), "hipEventCreate");
+      check_hip(hipEventCreateWithFlags(&s.ev1, ef), "hipEventCreate");
       // Batch completion is polled by the slot thread (wait_batch): no blocking-sync event.
-      check_hip(hipEventCreateWithFlags(&s.ev2, hipEventDefault), "hipEventCreate");
+      check_hip(hipEventCreateWithFlags(&s.ev2, ef), "hipEventCreate");
       mark("events");
       if (arena_slot >= 0 && pin_arena_) {
         s.arena = true;
@@ -662,16 +689,16 @@ struct Engine::Impl {
     for (;;) {
       bool all;
       {
+        // Loaders count without the lock and take it only to wake this thread when it announced that
+        // it sleeps (prog_waiting, seq_cst on both sides: a count that raced past the check is seen).
         std::unique_lock<std::mutex> g(s.prog_m);
-        s.prog_cv.wait(g, [&] { return s.loads_finished != seen; });
-        seen = s.loads_finished;
+        s.prog_waiting.store(true, std::memory_order_seq_cst);
+        s.prog_cv.wait(g, [&] { return s.loads_finished.load(std::memory_order_seq_cst) != seen; });
+        s.prog_waiting.store(false, std::memory_order_relaxed);
+        seen = s.loads_finished.load(std::memory_order_acquire);
         all = seen == count;
       }
-      size_t n;
-      {
-        std::lock_guard<std::mutex> g(s.alloc_m);
-        n = s.n_allocs;
-      }
+      const size_t n = s.n_allocs();
       size_t end = s.uploaded;
       while (next < n && s.allocs[next].done.load(std::memory_order_acquire)) {
         end = s.allocs[next].off + s.allocs[next].len;
@@ -791,15 +818,23 @@ struct Engine::Impl {
         const size_t cap = s.cap_pixels + s.hole_slack;
         size_t idx = 0, off = 0;
         bool packed = false, reserved = false, credit = false;
-        auto reserve_locked = [&](size_t len) {
-          const size_t o = s.raw_used.load(std::memory_order_relaxed);
-          if (o + len > cap) throw SliceError("batch pixel capacity exceeded");
-          s.raw_used.store(o + len, std::memory_order_relaxed);
-          idx = s.n_allocs++;
-          s.allocs[idx].off = o;
+        // Claims `len` elements at the end of the raw region and the next allocation index in one
+        // CAS (Slot::alloc_word); the entry's offset and length are published by its `done` flag.
+        auto reserve = [&](size_t len) {
+          uint64_t w = s.alloc_word.load(std::memory_order_relaxed);
+          for (;;) {
+            const size_t used = (size_t)(w & Slot::kUsedMask), n = (size_t)(w >> Slot::kAllocShift);
+            if (used + len > cap) throw SliceError("batch pixel capacity exceeded");
+            if (n >= s.max_allocs) throw SliceError("batch allocation table full");
+            const uint64_t nw = ((uint64_t)(n + 1) << Slot::kAllocShift) | (uint64_t)(used + len);
+            if (s.alloc_word.compare_exchange_weak(w, nw, std::memory_order_acq_rel, std::memory_order_relaxed)) {
+              idx = n;
+              off = used;
+              break;
+            }
+          }
+          s.allocs[idx].off = off;
           s.allocs[idx].len = len;
-          s.allocs[idx].done.store(false, std::memory_order_relaxed);
-          off = o;
           reserved = true;
         };
         try {
@@ -807,34 +842,34 @@ struct Engine::Impl {
           if (packable && !low12) {
             std::lock_guard<std::mutex> g(s.alloc_m);
             credit = s.hole_credit >= plen;
-            if (credit) {
-              s.hole_credit -= plen;
-              reserve_locked(plen);
-            }
+            if (credit) s.hole_credit -= plen;
           }
           if (credit) {
+            reserve(plen);
             uint8_t* dst = reinterpret_cast<uint8_t*>(reinterpret_cast<uint16_t*>(s.raw_cpu) + off);
             packed = pack12::pack_stream_checked(samples, npix, dst);
-            {
+            if (packed) {
               std::lock_guard<std::mutex> g(s.alloc_m);
-              if (packed) {
-                s.hole_credit += plen;
-              } else if (s.raw_used.load(std::memory_order_relaxed) == off + plen && off + ulen <= cap) {
-                s.raw_used.store(off + ulen, std::memory_order_relaxed);  // grow in place
+              s.hole_credit += plen;
+            } else {
+              // Grow in place while this is still the last allocation, else leave a hole (uploaded,
+              // unused; paid from the credit) and take a 16-bit allocation.
+              uint64_t last = ((uint64_t)(idx + 1) << Slot::kAllocShift) | (uint64_t)(off + plen);
+              const uint64_t grown = ((uint64_t)(idx + 1) << Slot::kAllocShift) | (uint64_t)(off + ulen);
+              if (off + ulen <= cap &&
+                  s.alloc_word.compare_exchange_strong(last, grown, std::memory_order_acq_rel, std::memory_order_relaxed)) {
                 s.allocs[idx].len = ulen;
+                std::lock_guard<std::mutex> g(s.alloc_m);
                 s.hole_credit += plen;
               } else {
-                s.allocs[idx].done.store(true, std::memory_order_release);  // a hole: uploaded, unused
-                reserve_locked(ulen);
+                s.allocs[idx].done.store(true, std::memory_order_release);
+                reserve(ulen);
               }
+              file.pixels16(reinterpret_cast<uint16_t*>(s.raw_cpu) + off, frame);
             }
-            if (!packed) file.pixels16(reinterpret_cast<uint16_t*>(s.raw_cpu) + off, frame);
           } else {
             packed = packable && (low12 || pack12::fits12(samples, npix));
-            {
-              std::lock_guard<std::mutex> g(s.alloc_m);
-              reserve_locked(packed ? plen : ulen);
-            }
+            reserve(packed ? plen : ulen);
             uint16_t* dst = reinterpret_cast<uint16_t*>(s.raw_cpu) + off;
             if (packed) {
               pack12::pack_stream(samples, npix, reinterpret_cast<uint8_t*>(dst));
@@ -1026,7 +1061,7 @@ struct Engine::Impl {
     // Tables, then the raw pixels not already queued by upload_progress (all of them without it).
     // The tables sit right before the raw region: with nothing uploaded early (a small batch) both
     // go as one copy — one SDMA command and one completion on the batch's critical path, not two.
-    const size_t raw_end = s.raw_used.load();
+    const size_t raw_end = s.raw_used();
     // A small batch (≤ 16 slices) with nothing uploaded early copies on its own stream, without the
     // upload stream's events: on the shared stream every copy sat ≈ 20 µs behind the previous one
     // (SDMA → event marker → SDMA hand-offs) and its first kernel ≈ 16–20 µs behind the copy (the
@@ -1081,7 +1116,7 @@ struct Engine::Impl {
     check_hip(hipEventRecord(s.ev2, s.stream), "event");
     if (mark) mark->enq = now_s();
     wait_batch(s, s.ev2, t_enq, nl);
-    if (acc && !inline_up) {  // an inline small upload records no split events
+    if (acc && !inline_up && event_timing()) {  // an inline small upload records no split events
       float a = 0, b = 0;
       (void)hipEventElapsedTime(&a, s.ev0, s.ev1);
       (void)hipEventElapsedTime(&b, s.ev1, s.ev2);
@@ -1129,17 +1164,17 @@ struct Engine::Impl {
                      size_t first, size_t count, std::vector<SliceStatus>& status, StageTimes& acc,
                      std::mutex& acc_m, const std::function<void(size_t)>& on_start, BatchMark* mark = nullptr) {
     if (mark) mark->claim = now_s();
-    s.raw_used = 0;
     s.loaded.assign(count, LoadedSlice{});
-    if (!s.allocs) s.allocs.reset(new Slot::Alloc[2 * (size_t)s.cap_slices]);  // ≤ 2 per slice (a hole)
-    s.n_allocs = 0;
+    if (!s.allocs) {
+      s.max_allocs = 2 * (size_t)s.cap_slices;  // ≤ 2 per slice (a hole)
+      s.allocs.reset(new Slot::Alloc[s.max_allocs]);
+    }
+    for (size_t k = 0; k < s.max_allocs; ++k) s.allocs[k].done.store(false, std::memory_order_relaxed);
+    s.alloc_word.store(0, std::memory_order_relaxed);
     s.hole_credit = s.hole_slack;
     s.uploaded = 0;
     s.upload_started = false;
-    {
-      std::lock_guard<std::mutex> g(s.prog_m);
-      s.loads_finished = 0;
-    }
+    s.loads_finished.store(0, std::memory_order_relaxed);
     s.progress_quiet.store(false, std::memory_order_relaxed);
     std::atomic<int64_t> load_ns{0}, bytes_in{0}, write_ns{0}, bytes_out{0}, load_cpu_ns{0}, write_cpu_ns{0};
     std::string upload_error;
@@ -1155,16 +1190,16 @@ struct Engine::Impl {
               load_into(s, (int)i, first + i, items[first + i].path, status[first + i], load_ns, bytes_in);
             }
             if (upload_chunk_) {
-              size_t lf;
-              {
-                std::lock_guard<std::mutex> g(s.prog_m);
-                lf = ++s.loads_finished;
-              }
+              const size_t lf = s.loads_finished.fetch_add(1, std::memory_order_seq_cst) + 1;
               // Every 4th load (and the last) wakes the slot thread: an upload chunk is ≥ 2 MiB
               // (≥ 20 slices of 256²), so finer wake-ups only cost context switches on the CPUs
-              // the loaders run on.
-              if (!s.progress_quiet.load(std::memory_order_relaxed) && ((lf & 3) == 0 || lf == count))
+              // the loaders run on. The lock is taken only when the slot thread sleeps (or is about
+              // to: it then re-checks the count under the lock this waits for).
+              if (!s.progress_quiet.load(std::memory_order_relaxed) && ((lf & 3) == 0 || lf == count) &&
+                  s.prog_waiting.load(std::memory_order_seq_cst)) {
+                { std::lock_guard<std::mutex> g(s.prog_m); }
                 s.prog_cv.notify_one();
+              }
             }
           },
           2 * prio, &load_cpu_ns);
@@ -1505,7 +1540,7 @@ struct Engine::Impl {
     check_hip(hipSetDevice(cfg.device), "hipSetDevice");
     Slot& s = *slots[0];
     if (in.w > cfg.max_dim || in.h > cfg.max_dim) throw DeviceError("slice exceeds engine max_dim");
-    s.raw_used = align_up((size_t)in.w * in.h, 8);
+    s.alloc_word.store(align_up((size_t)in.w * in.h, 8), std::memory_order_relaxed);  // one region, no allocation entries
     s.uploaded = 0;
     s.upload_started = false;
     s.loaded.assign(1, LoadedSlice{});

@@ -98,25 +98,77 @@ def to_module(addr, maps):
     return None, addr
 
 
+def dynsym(path, cache={}):
+    """Sorted (vaddr, name) of a module's dynamic symbols (stripped system libraries)."""
+    if path not in cache:
+        syms = []
+        try:
+            r = subprocess.run(["nm", "-D", "--defined-only", path], capture_output=True, text=True, timeout=120)
+            for line in r.stdout.splitlines():
+                p = line.split()
+                if len(p) == 3 and p[1] in "TtWi":
+                    syms.append((int(p[0], 16), p[2].split("@")[0]))
+        except (OSError, subprocess.TimeoutExpired, ValueError):
+            pass
+        cache[path] = sorted(syms)
+    return cache[path]
+
+
+def nearest_dynsym(path, a):
+    syms = dynsym(path)
+    lo, hi = 0, len(syms)
+    while lo < hi:
+        mid = (lo + hi) // 2
+        if syms[mid][0] <= a:
+            lo = mid + 1
+        else:
+            hi = mid
+    if lo == 0:
+        return None
+    base, name = syms[lo - 1]
+    # glibc 2.35: __lll_lock_wait / __lll_lock_wake (contended pthread mutexes, not exported) follow the
+    # exported *_private variants; name them by their futex role.
+    if name == "__lll_lock_wait_private" and a - base >= 0x60:
+        return "__lll_lock_wait (futex wait, contended mutex)"
+    if name == "__lll_lock_wake_private" and a - base >= 0x20:
+        return "__lll_lock_wake (futex wake, contended mutex)"
+    return f"{name}+{a - base:#x}"
+
+
+def local_path(path, alias={}):
+    """A module recorded on the GPU box (scratch checkout) → the same file in this checkout."""
+    if os.path.exists(path):
+        return path
+    if path not in alias:
+        here = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+        cand = os.path.join(here, "nm03_capstone_project_amd", "lib", os.path.basename(path))
+        alias[path] = cand if "nm03_capstone_project_amd/lib/" in path and os.path.exists(cand) else path
+    return alias[path]
+
+
 def symbolize(requests):
     """{path: set(vaddr)} -> {(path, vaddr): [function names, innermost first]}."""
     out = {}
     for path, addrs in requests.items():
+        obj = local_path(path)
         addrs = sorted(addrs)
-        if not os.path.exists(path):
+        if not os.path.exists(obj):
             for a in addrs:
                 out[(path, a)] = [f"{os.path.basename(path)}+{a:#x}"]
             continue
         inp = "".join(f"{a:#x}\n" for a in addrs)
         try:
-            r = subprocess.run([SYMBOLIZER, f"--obj={path}", "--functions=linkage", "--demangle", "--inlines",
+            r = subprocess.run([SYMBOLIZER, f"--obj={obj}", "--functions=linkage", "--demangle", "--inlines",
                                 "--output-style=JSON"], input=inp, capture_output=True, text=True, timeout=600)
             rows = [json.loads(x) for x in r.stdout.splitlines() if x.strip()]
         except (OSError, subprocess.TimeoutExpired, ValueError):
             rows = []
         for a, row in zip(addrs, rows):
             names = [s.get("FunctionName") or "??" for s in row.get("Symbol", [])]
-            names = [n for n in names if n and n != "??"] or [f"{os.path.basename(path)}+{a:#x}"]
+            names = [n for n in names if n and n != "??"]
+            if not names:
+                nd = nearest_dynsym(obj, a)
+                names = [nd] if nd else [f"{os.path.basename(path)}+{a:#x}"]
             out[(path, a)] = names
         for a in addrs:
             out.setdefault((path, a), [f"{os.path.basename(path)}+{a:#x}"])
@@ -161,6 +213,7 @@ def analyse(path, top=30):
         return out
 
     total = sum(c for c, _, _ in stacks)
+    lock_callers = collections.Counter()
     groups = collections.Counter()
     self_by_group = collections.defaultdict(collections.Counter)
     pool_task = collections.Counter()
@@ -172,6 +225,11 @@ def analyse(path, top=30):
         fr = frames_of(pcs)
         leaf = fr[0] if fr else "?"
         self_by_group[g][leaf] += count
+        if any(f.startswith("__lll_lock") or f.startswith("__pthread_mutex") or "pthread_cond" in f for f in fr[:3]):
+            # first frame of our code above the lock: who contends
+            own = next((f for f in fr if "nm03::" in f or "ThreadPool" in f or "TaskGroup" in f or "Slot" in f
+                        or "Engine" in f or "std::condition_variable" in f), fr[-1] if fr else "?")
+            lock_callers[f"{g}: {leaf[:40]} <- {own[:110]}"] += count
         if g != "nm03-pool":
             continue
         joined = " | ".join(fr)
@@ -190,7 +248,8 @@ def analyse(path, top=30):
     res = {"file": path, "samples": total, "period_us": meta.get("period_us"), "dropped": meta.get("dropped"),
            "groups": dict(groups.most_common()), "pool_task": dict(pool_task.most_common()),
            "load_phase": dict(load_phase.most_common()), "write_phase": dict(write_phase.most_common()),
-           "self_top": {g: c.most_common(top) for g, c in self_by_group.items()}}
+           "self_top": {g: c.most_common(top) for g, c in self_by_group.items()},
+           "lock_callers": lock_callers.most_common(top)}
     return res
 
 
@@ -213,6 +272,10 @@ def report(res, out=sys.stdout):
             print(f"\n{title} by phase (% of its samples):", file=out)
             for t, c in res[key].items():
                 print(f"  {pct(c, sub)}  {c:7d}  {t}", file=out)
+    if res.get("lock_callers"):
+        print("\nmutex / futex samples by caller (% of all samples):", file=out)
+        for k, c in res["lock_callers"]:
+            print(f"  {pct(c)}  {c:7d}  {k}", file=out)
     for g, rows in res["self_top"].items():
         gc = res["groups"].get(g, 1)
         print(f"\nself time, {g} (% of the group):", file=out)

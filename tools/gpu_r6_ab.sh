@@ -1,0 +1,56 @@
+#!/bin/bash
+# Round 6: interleaved A/B of the round-start build (abprev/: its bench.py, package and CLI) against
+# this tree — headline bench (host CPU per step) and cold CLI walls — plus a symbolised CPU profile of
+# this tree. Usage: gpurun -- 'bash tools/gpu_r6_ab.sh [bench|cold|prof]...' → gpurun_out/r6_ab/
+set -o pipefail
+O=gpurun_out/r6_ab
+mkdir -p $O
+export PYTHONUNBUFFERED=1
+steps="${*:-bench cold prof}"
+D=/dev/shm/nm03_bench_data
+for s in $steps; do
+  case $s in
+    bench)
+      for r in 1 2 3; do
+        for v in old new new_noevt; do
+          S=bench.py; e=""
+          [ $v = old ] && S=abprev/bench.py
+          [ $v = new_noevt ] && e="NM03_EVENT_TIMING=0"
+          timeout -k 10 240 env $e python -u $S --keep-data --data-root $D --steps ${STEPS:-2000} --warmup 5 --no-secondary \
+            --wipe-passes 0 --single-passes 0 --cli-runs 0 > $O/bench_${v}_$r.json 2>> $O/bench.err || exit 1
+        done
+      done
+      ;;
+    cold)
+      [ -d $D ] || timeout -k 10 240 python -u bench.py --keep-data --data-root $D --steps 2 --warmup 1 --no-secondary \
+        --wipe-passes 0 --single-passes 0 --cli-runs 0 > /dev/null 2>&1 || exit 1
+      timeout -k 10 600 python -u tools/cold_ab.py $D/ ${ROUNDS:-12} old=abprev/bin:abprev/nm03_capstone_project_amd/lib \
+        new=build/bin > $O/cold_ab.jsonl 2> $O/cold_ab.err || exit 1
+      cat $O/cold_ab.jsonl | cut -c1-400
+      ;;
+    prof)
+      timeout -k 10 240 python -u bench.py --keep-data --data-root $D --steps 4000 --warmup 5 --no-secondary --wipe-passes 0 \
+        --single-passes 0 --cli-runs 0 --cpu-profile $O/cpu > $O/bench_prof.json 2> $O/bench_prof.err || exit 1
+      timeout -k 10 600 python tools/cpu_profile.py $O/cpu.rank0 --top 40 --json $O/cpu_profile.json \
+        > $O/cpu_profile.txt 2>&1 || exit 1
+      head -45 $O/cpu_profile.txt | cut -c1-200
+      ;;
+  esac
+done
+python3 - <<'PY'
+import glob, json, statistics, collections
+d = collections.defaultdict(list)
+for f in sorted(glob.glob("gpurun_out/r6_ab/bench_*_[0-9].json")):
+    v = f.split("bench_")[1].rsplit("_", 1)[0]
+    try:
+        j = json.loads(open(f).read().strip().splitlines()[-1])
+    except Exception:
+        continue
+    c = j["config"]
+    d[v].append((j["value"], c["rank0_process_cpu_ms_per_step"], c["rank0_thread_cpu_ms_per_step"]))
+for v, rows in d.items():
+    print(v, "value median", round(statistics.median(r[0] for r in rows)), "cpu/step median",
+          round(statistics.median(r[1] for r in rows), 3), [r[2] for r in rows])
+PY
+rm -rf /dev/shm/nm03_bench_data /dev/shm/nm03_bench_out
+echo done
