@@ -22,6 +22,10 @@
 //                        insert the stuffing: 2.65 MB written + read back per batch, two launches.)
 #include <hip/hip_runtime.h>
 
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+
 #include <cstdlib>
 
 #include "device_util.h"
@@ -869,23 +873,43 @@ void launch_jpeg(const uint8_t* canvas, const JpegDesc* jd, int ncanvas, int out
 }
 
 void preload_kernels(bool with_volume) {
+  // NM03_PRELOAD_TRACE=1: milliseconds per translation unit on stderr (what a cold start pays for
+  // each code object).
+  static const bool trace = [] {
+    const char* e = std::getenv("NM03_PRELOAD_TRACE");
+    return e && *e == '1';
+  }();
+  auto t = std::chrono::steady_clock::now();
+  auto lap = [&](const char* what) {
+    if (!trace) return;
+    const auto n = std::chrono::steady_clock::now();
+    std::fprintf(stderr, "[nm03 preload] %s %.3f ms\n", what, std::chrono::duration<double, std::milli>(n - t).count());
+    t = n;
+  };
   preload_median();
+  lap("k1_median");
   preload_sharpen();
+  lap("k1_sharpen");
   preload_srg();
+  lap("k2_srg_morph");
   preload_render();
+  lap("k3_render");
   if (with_volume) {
     preload_volume();
     preload_threshold();
+    lap("k5_volume+k6_threshold");
   }
   hipFuncAttributes a;
   check_hip(hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&jpeg_fused_kernel<4, kUnionWords, kSampling420, false>)),
             "preload jpeg_fused_kernel");
+  lap("k4_jpeg (first instance)");
   check_hip(hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&jpeg_fused_kernel<4, kUnionWords, kSampling420, true>)),
             "preload jpeg_fused_kernel nearest");
   check_hip(hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&jpeg_fused_kernel<4, kUnionWords, kSampling444, false>)),
             "preload jpeg_fused_kernel 4:4:4");
   check_hip(hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&jpeg_fused_kernel<4, kUnionWords, kSamplingGray, false>)),
             "preload jpeg_fused_kernel gray");
+  lap("k4_jpeg (other instances)");
 }
 
 }  // namespace nm03::gpu

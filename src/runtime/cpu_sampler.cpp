@@ -6,7 +6,10 @@
 //   samples <written> dropped <n>
 //   map <start> <end> <file offset> <path>          executable mappings (hex), from /proc/self/maps
 //   thread <tid> <name>
-//   s <count> <tid> <pc0> <pc1> ...                 one distinct (thread, call chain), leaf first (hex)
+//   s <count> <tid> <rsi> <pc0> <pc1> ...           one distinct (thread, RSI, call chain), leaf first (hex);
+//                                                   RSI at the interrupted pc: after a system call it
+//                                                   still holds the call's second argument (an ioctl's
+//                                                   request code, a futex's operation)
 #include "nm03/cpu_sampler.h"
 
 #include <dirent.h>
@@ -43,7 +46,7 @@ std::atomic<bool> g_on{false};         // the handler records
 std::atomic<int> g_inside{0};          // handlers currently running
 std::atomic<size_t> g_next{0};         // next record
 std::atomic<size_t> g_dropped{0};
-std::unique_ptr<uint64_t[]> g_buf;     // records of g_stride words: tid, frames, pc...
+std::unique_ptr<uint64_t[]> g_buf;     // records of g_stride words: tid, frames, rsi, pc...
 size_t g_cap = 0, g_stride = 0;
 int g_depth = 0, g_period_us = 0;
 std::vector<timer_t> g_timers;  // one per thread alive at start()
@@ -59,16 +62,17 @@ void on_sigprof(int, siginfo_t*, void* ctx) {
       void* bt[kMaxDepth + 4];
       const int n = backtrace(bt, g_depth + 4);
       const uintptr_t pc = (uintptr_t)static_cast<ucontext_t*>(ctx)->uc_mcontext.gregs[REG_RIP];
+      r[2] = (uint64_t)static_cast<ucontext_t*>(ctx)->uc_mcontext.gregs[REG_RSI];
       // Skip the handler's own frames and the signal trampoline: the chain starts at the
       // interrupted pc (the unwinder reports it exactly for the frame under a signal frame).
       int k = 0;
       while (k < n && (uintptr_t)bt[k] != pc) ++k;
       int m = 0;
       if (k == n) {
-        r[2] = pc;  // unwinding did not reach it: the pc alone
+        r[3] = pc;  // unwinding did not reach it: the pc alone
         m = 1;
       } else {
-        for (; k < n && m < g_depth; ++k) r[2 + m++] = (uint64_t)(uintptr_t)bt[k];
+        for (; k < n && m < g_depth; ++k) r[3 + m++] = (uint64_t)(uintptr_t)bt[k];
       }
       r[1] = (uint64_t)m;
       r[0] = (uint64_t)::syscall(SYS_gettid);
@@ -105,7 +109,7 @@ bool sampler_start(int period_us, size_t max_samples, int depth) {
     (void)backtrace(warm, 4);  // loads libgcc_s here, never inside the handler
   }
   g_depth = depth;
-  g_stride = 2 + (size_t)depth;
+  g_stride = 3 + (size_t)depth;
   g_cap = max_samples;
   g_buf.reset(new uint64_t[g_cap * g_stride]);
   g_next = 0;
@@ -175,14 +179,14 @@ size_t sampler_stop(const std::string& path) {
   for (size_t i = 0; i < n; ++i) {
     const uint64_t* r = g_buf.get() + i * g_stride;
     const size_t m = std::min<uint64_t>(r[1], (uint64_t)g_depth);
-    std::vector<uint64_t> key(r, r + 2 + m);
+    std::vector<uint64_t> key(r, r + 3 + m);
     key[1] = 0;
     ++stacks[key];
     tids.insert(r[0]);
   }
   FILE* f = std::fopen(path.c_str(), "w");
   if (!f) return 0;
-  std::fprintf(f, "# nm03 cpu samples v1\nperiod_us %d\nsamples %zu dropped %zu\n", g_period_us, n, g_dropped.load());
+  std::fprintf(f, "# nm03 cpu samples v2\nperiod_us %d\nsamples %zu dropped %zu\n", g_period_us, n, g_dropped.load());
   {
     std::ifstream maps("/proc/self/maps");
     std::string line;
@@ -198,7 +202,7 @@ size_t sampler_stop(const std::string& path) {
   for (uint64_t t : tids) std::fprintf(f, "thread %llu %s\n", (unsigned long long)t, thread_name(t).c_str());
   for (const auto& [key, count] : stacks) {
     std::fprintf(f, "s %llu %llu", (unsigned long long)count, (unsigned long long)key[0]);
-    for (size_t k = 2; k < key.size(); ++k) std::fprintf(f, " %llx", (unsigned long long)key[k]);
+    for (size_t k = 2; k < key.size(); ++k) std::fprintf(f, " %llx", (unsigned long long)key[k]);  // rsi, pcs
     std::fputc('\n', f);
   }
   std::fclose(f);

@@ -133,6 +133,9 @@ struct Slot {
   std::condition_variable prog_cv;
   std::atomic<size_t> loads_finished{0};
   std::atomic<bool> prog_waiting{false};  // the slot thread sleeps (or is about to) on prog_cv
+  // The finished-load count at which the sleeping slot thread wants to be woken: the next upload
+  // chunk's worth of slices (one wake-up per chunk, ≈ 4 per 96-slice batch, instead of one per 4 loads).
+  std::atomic<size_t> wake_at{0};
   // Set by upload_progress when the whole batch fits in one upload chunk: loaders stop notifying
   // (a wake-up of the slot thread per load, on CPUs the loaders need, for nothing to upload early).
   std::atomic<bool> progress_quiet{false};
@@ -692,6 +695,14 @@ struct Engine::Impl {
         // Loaders count without the lock and take it only to wake this thread when it announced that
         // it sleeps (prog_waiting, seq_cst on both sides: a count that raced past the check is seen).
         std::unique_lock<std::mutex> g(s.prog_m);
+        // Wake at the load count whose slices (of the first one's size) fill the next chunk; loads
+        // that finish out of order just make a wake-up find a shorter prefix and sleep again.
+        size_t target = seen + 1;
+        if (chunk) {  // set once allocation 0 is done: its length is final
+          const size_t per = s.allocs[0].len * 2;
+          if (per) target = std::max(target, (s.uploaded * 2 + chunk + per - 1) / per);
+        }
+        s.wake_at.store(target, std::memory_order_seq_cst);
         s.prog_waiting.store(true, std::memory_order_seq_cst);
         s.prog_cv.wait(g, [&] { return s.loads_finished.load(std::memory_order_seq_cst) != seen; });
         s.prog_waiting.store(false, std::memory_order_relaxed);
@@ -1175,6 +1186,7 @@ struct Engine::Impl {
     s.uploaded = 0;
     s.upload_started = false;
     s.loads_finished.store(0, std::memory_order_relaxed);
+    s.wake_at.store(0, std::memory_order_relaxed);
     s.progress_quiet.store(false, std::memory_order_relaxed);
     std::atomic<int64_t> load_ns{0}, bytes_in{0}, write_ns{0}, bytes_out{0}, load_cpu_ns{0}, write_cpu_ns{0};
     std::string upload_error;
@@ -1191,11 +1203,13 @@ struct Engine::Impl {
             }
             if (upload_chunk_) {
               const size_t lf = s.loads_finished.fetch_add(1, std::memory_order_seq_cst) + 1;
-              // Every 4th load (and the last) wakes the slot thread: an upload chunk is ≥ 2 MiB
-              // (≥ 20 slices of 256²), so finer wake-ups only cost context switches on the CPUs
-              // the loaders run on. The lock is taken only when the slot thread sleeps (or is about
-              // to: it then re-checks the count under the lock this waits for).
-              if (!s.progress_quiet.load(std::memory_order_relaxed) && ((lf & 3) == 0 || lf == count) &&
+              // The load that reaches the slot thread's wake_at (the next upload chunk's worth; and
+              // the last load) wakes it: an upload chunk is ≥ 2 MiB (≥ 20 slices of 256²), so finer
+              // wake-ups only cost context switches on the CPUs the loaders run on. The lock is taken
+              // only when the slot thread sleeps (or is about to: it then re-checks the count under
+              // the lock this waits for).
+              if (!s.progress_quiet.load(std::memory_order_relaxed) &&
+                  (lf >= s.wake_at.load(std::memory_order_seq_cst) || lf == count) &&
                   s.prog_waiting.load(std::memory_order_seq_cst)) {
                 { std::lock_guard<std::mutex> g(s.prog_m); }
                 s.prog_cv.notify_one();

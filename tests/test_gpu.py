@@ -1408,3 +1408,51 @@ def test_cli_parallel_rccl_two_devices(native, cohort_root, tmp_path):
     j = json.load(open(js))
     assert j["backend"] == "rccl" and j["comm"]["nranks"] == 2 and j["devices"]["transport_device"] == [0, 1]
     assert sum(j["per_rank"]["slices_ok"]) == j["slices"]
+
+
+@pytest.mark.parametrize("shape,spacing", [((256, 256), (1.0, 1.0)), ((200, 160), (1.0, 1.0))])
+def test_gpu_canvases_vs_torch_reference(native, cohort_root, tmp_path, shape, spacing):
+    """the GPU renders held directly against the plain-PyTorch references
+    (ops.reference.render_gray / render_labels), not only transitively through the golden model.
+    (1) K3 `render_kernel` canvases of run_single (original, sharpened, region / eroded / dilated
+    labels): gray within 1 level (f32 evaluation order), labels exact. (2) The fused K4 render of an
+    exact-2× export, which never materialises a canvas: its label JPEG equals the CPU encoding
+    (byte-identical to libjpeg) of the torch label canvas, and its gray JPEG decodes to the decoded
+    CPU encoding of the torch gray canvas within JPEG rounding."""
+    h, w = shape
+    raw = native.phantom_slice(h, w, 3, 12, 25, 7)
+    meta = {"type": "u16", "stored_bits": 16, "slope": 1.0, "intercept": 0.0, "spacing_x": spacing[0],
+            "spacing_y": spacing[1]}
+    pipe = nm.SlicePipeline(nm.PipelineConfig(batch_size=1, streams=1, threads=2))
+    gpu = pipe.run_array(raw, meta)
+    dev = torch.device("cuda")
+    v = torch.from_numpy(raw.astype(np.float32)).to(dev)
+    ref = R.render_gray(v, float(raw.min()), float(raw.max())).cpu().numpy()
+    c0 = np.asarray(gpu["canvases"][0])
+    assert c0.shape == (512, 512) and np.abs(c0.astype(int) - ref.astype(int)).max() <= 1
+    assert (c0 != ref).mean() < 0.01
+    sh = torch.from_numpy(np.asarray(gpu["sharpened"], np.float32).reshape(h, w)).to(dev)
+    ref_s = R.render_gray(sh, float(sh.min()), float(sh.max())).cpu().numpy()
+    assert np.abs(np.asarray(gpu["canvases"][1]).astype(int) - ref_s.astype(int)).max() <= 1
+    for k, plane in ((2, "region"), (3, "eroded"), (4, "dilated")):
+        lab = torch.from_numpy(np.asarray(gpu[plane]).reshape(h, w).astype(bool)).to(dev)
+        ref_l = R.render_labels(lab, R.border(lab, 2)).cpu().numpy()
+        assert np.array_equal(np.asarray(gpu["canvases"][k]), ref_l), plane
+    if shape != (256, 256):
+        return
+    # (2) fused exact-2× export path through the engine
+    d = tmp_path / "in"
+    d.mkdir()
+    (d / "1-1.dcm").write_bytes(native.dicom_bytes(raw))
+    out = tmp_path / "out"
+    out.mkdir()
+    st, times = native.Engine(nm.PipelineConfig(batch_size=4, streams=1, threads=2).engine_config()).run(
+        [(str(d / "1-1.dcm"), str(out))])
+    assert st[0][0] == 0
+    lab = torch.from_numpy(np.asarray(gpu["dilated"]).reshape(h, w).astype(bool)).to(dev)
+    ref_l = R.render_labels(lab, R.border(lab, 2)).cpu().numpy()
+    assert open(out / "1-1_processed.jpg", "rb").read() == native.jpeg_encode_gray420(ref_l, 75)
+    PIL = pytest.importorskip("PIL.Image")
+    got = np.asarray(PIL.open(out / "1-1_original.jpg").convert("L"), dtype=np.int32)
+    want = np.asarray(PIL.open(io.BytesIO(native.jpeg_encode_gray420(ref, 75))).convert("L"), dtype=np.int32)
+    assert R.psnr(torch.from_numpy(got), torch.from_numpy(want)) > 45.0

@@ -38,4 +38,5 @@ for name, rs in rows.items():
     print(json.dumps({"variant": name, "runs": len(rs), "all_ok": all(x["all_ok"] for x in rs),
                       "wall_median_s": round(statistics.median(walls), 6), "wall_min_s": round(min(walls), 6),
                       "walls_s": [round(w, 4) for w in walls],
-                      "phases_median_s": {k: round(statistics.median(v), 6) for k, v in sorted(ph.items())}}), flush=True)
+                      "phases_median_s": {k: round(statistics.median(v), 6) for k, v in sorted(ph.items())},
+                      "failures": [f for x in rs for f in x.get("failures", [])][:2]}), flush=True)

@@ -66,19 +66,28 @@ def load_phdrs(path, cache={}):
 
 
 def parse(path):
+    """Returns meta, maps, threads, stacks [(count, tid, [pc...])] and rsi {stack index: rsi} (v2 files)."""
     maps, threads, stacks = [], {}, []
-    meta = {}
+    meta = {"version": 1, "rsi": []}
     with open(path) as f:
         for line in f:
             p = line.split()
-            if not p or p[0].startswith("#"):
+            if not p:
+                continue
+            if p[0] == "#":
+                if "v2" in line:
+                    meta["version"] = 2
                 continue
             if p[0] == "map":
                 maps.append((int(p[1], 16), int(p[2], 16), int(p[3], 16), " ".join(p[4:])))
             elif p[0] == "thread":
                 threads[int(p[1])] = p[2] if len(p) > 2 else "?"
             elif p[0] == "s":
-                stacks.append((int(p[1]), int(p[2]), [int(x, 16) for x in p[3:]]))
+                if meta["version"] >= 2:
+                    meta["rsi"].append(int(p[3], 16))
+                    stacks.append((int(p[1]), int(p[2]), [int(x, 16) for x in p[4:]]))
+                else:
+                    stacks.append((int(p[1]), int(p[2]), [int(x, 16) for x in p[3:]]))
             elif p[0] == "period_us":
                 meta["period_us"] = int(p[1])
             elif p[0] == "samples":
@@ -175,6 +184,20 @@ def symbolize(requests):
     return out
 
 
+# /usr/include/linux/kfd_ioctl.h: AMDKFD_IOC_* numbers ('K', nr); the size bits vary by struct.
+KFD_IOCTL_NR = {0x01: "GET_VERSION", 0x02: "CREATE_QUEUE", 0x03: "DESTROY_QUEUE", 0x04: "SET_MEMORY_POLICY",
+                0x05: "GET_CLOCK_COUNTERS", 0x06: "GET_PROCESS_APERTURES", 0x07: "UPDATE_QUEUE",
+                0x08: "CREATE_EVENT", 0x09: "DESTROY_EVENT", 0x0A: "SET_EVENT", 0x0B: "RESET_EVENT",
+                0x0C: "WAIT_EVENTS", 0x16: "ALLOC_MEMORY_OF_GPU", 0x17: "FREE_MEMORY_OF_GPU",
+                0x18: "MAP_MEMORY_TO_GPU", 0x19: "UNMAP_MEMORY_FROM_GPU", 0x20: "GET_TILE_CONFIG"}
+
+
+def kfd_ioctl_name(req):
+    if (req >> 8) & 0xFF != ord("K"):
+        return "not a KFD ioctl"
+    return "AMDKFD_IOC_" + KFD_IOCTL_NR.get(req & 0xFF, f"nr {req & 0xFF:#x}")
+
+
 def group_of(name):
     if name.startswith("nm03-pool"):
         return "nm03-pool"
@@ -214,17 +237,20 @@ def analyse(path, top=30):
 
     total = sum(c for c, _, _ in stacks)
     lock_callers = collections.Counter()
+    ioctls = collections.Counter()
     groups = collections.Counter()
     self_by_group = collections.defaultdict(collections.Counter)
     pool_task = collections.Counter()
     load_phase = collections.Counter()
     write_phase = collections.Counter()
-    for count, tid, pcs in stacks:
+    for si, (count, tid, pcs) in enumerate(stacks):
         g = group_of(threads.get(tid, "?"))
         groups[g] += count
         fr = frames_of(pcs)
         leaf = fr[0] if fr else "?"
         self_by_group[g][leaf] += count
+        if leaf == "ioctl" and meta["rsi"]:
+            ioctls[f"{g}: ioctl request {meta['rsi'][si]:#x} ({kfd_ioctl_name(meta['rsi'][si])})"] += count
         if any(f.startswith("__lll_lock") or f.startswith("__pthread_mutex") or "pthread_cond" in f for f in fr[:3]):
             # first frame of our code above the lock: who contends
             own = next((f for f in fr if "nm03::" in f or "ThreadPool" in f or "TaskGroup" in f or "Slot" in f
@@ -249,7 +275,7 @@ def analyse(path, top=30):
            "groups": dict(groups.most_common()), "pool_task": dict(pool_task.most_common()),
            "load_phase": dict(load_phase.most_common()), "write_phase": dict(write_phase.most_common()),
            "self_top": {g: c.most_common(top) for g, c in self_by_group.items()},
-           "lock_callers": lock_callers.most_common(top)}
+           "lock_callers": lock_callers.most_common(top), "ioctls": ioctls.most_common(top)}
     return res
 
 
@@ -272,6 +298,10 @@ def report(res, out=sys.stdout):
             print(f"\n{title} by phase (% of its samples):", file=out)
             for t, c in res[key].items():
                 print(f"  {pct(c, sub)}  {c:7d}  {t}", file=out)
+    if res.get("ioctls"):
+        print("\nioctl samples by request code (% of all samples):", file=out)
+        for k, c in res["ioctls"]:
+            print(f"  {pct(c)}  {c:7d}  {k}", file=out)
     if res.get("lock_callers"):
         print("\nmutex / futex samples by caller (% of all samples):", file=out)
         for k, c in res["lock_callers"]:

@@ -11,8 +11,8 @@ D=/dev/shm/nm03_bench_data
 for s in $steps; do
   case $s in
     bench)
-      for r in 1 2 3; do
-        for v in old new new_noevt; do
+      for r in $(seq ${ROUNDS_B:-4}); do
+        for v in ${VARIANTS:-old new}; do
           S=bench.py; e=""
           [ $v = old ] && S=abprev/bench.py
           [ $v = new_noevt ] && e="NM03_EVENT_TIMING=0"
@@ -22,10 +22,11 @@ for s in $steps; do
       done
       ;;
     cold)
-      [ -d $D ] || timeout -k 10 240 python -u bench.py --keep-data --data-root $D --steps 2 --warmup 1 --no-secondary \
-        --wipe-passes 0 --single-passes 0 --cli-runs 0 > /dev/null 2>&1 || exit 1
-      timeout -k 10 600 python -u tools/cold_ab.py $D/ ${ROUNDS:-12} old=abprev/bin:abprev/nm03_capstone_project_amd/lib \
+      C=/dev/shm/nm03_cold_cohort
+      [ -d $C ] || build/bin/nm03_synth --data-root $C/ --threads 16 > /dev/null || exit 1
+      timeout -k 10 600 python -u tools/cold_ab.py $C/ ${ROUNDS:-12} old=abprev/bin:abprev/nm03_capstone_project_amd/lib \
         new=build/bin > $O/cold_ab.jsonl 2> $O/cold_ab.err || exit 1
+      rm -rf $C /tmp/cold_ab_old /tmp/cold_ab_new
       cat $O/cold_ab.jsonl | cut -c1-400
       ;;
     prof)

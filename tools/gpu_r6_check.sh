@@ -3,6 +3,7 @@
 # binary that ran is the one symbolised, on the box), and an interleaved A/B of HIP/ROCr runtime
 # knobs against the runtime thread that burns a CPU in ioctl (profiles/r6/cpu_profile/).
 # Usage: gpurun -- 'bash tools/gpu_r6_check.sh [tests|prof|knobs]...'  → gpurun_out/r6_check/
+#        KNOBS="base A=1 B=0" selects the knob variants.
 set -o pipefail
 O=gpurun_out/r6_check
 mkdir -p $O
@@ -26,7 +27,7 @@ for s in $steps; do
       ;;
     knobs)
       for r in 1 2; do
-        for v in base HSA_ENABLE_INTERRUPT=0 ROC_ACTIVE_WAIT_TIMEOUT=0 ROC_SIGNAL_POOL_SIZE=64; do
+        for v in ${KNOBS:-base HSA_ENABLE_INTERRUPT=0 ROC_ACTIVE_WAIT_TIMEOUT=0 ROC_SIGNAL_POOL_SIZE=64}; do
           e=""; [ "$v" != base ] && e="$v"
           timeout -k 10 240 env $e $B --steps 2000 --warmup 5 --no-secondary --wipe-passes 0 --single-passes 0 \
             --cli-runs 0 > $O/knob_${v}_$r.json 2>> $O/knobs.err || exit 1
