@@ -5,10 +5,12 @@
 // Explicit VR BE, Deflated Explicit VR LE (1.2.840.10008.1.2.1.99, zlib), RLE Lossless
 // (1.2.840.10008.1.2.5, encapsulated PackBits segments) and lossless JPEG — JPEG Lossless First-Order
 // Prediction (1.2.840.10008.1.2.4.70) and JPEG Lossless Process 14 (1.2.840.10008.1.2.4.57), decoded
-// on the host (nm03/jpeg_lossless.h); 8/16-bit monochrome, signed/unsigned,
+// on the host (nm03/jpeg_lossless.h), and lossy JPEG Baseline (1.2.840.10008.1.2.4.50) and Extended
+// (1.2.840.10008.1.2.4.51, 12-bit) with the IJG islow inverse DCT (nm03/jpeg_dct.h); 8/16-bit
+// monochrome, signed/unsigned,
 // BitsStored masking, modality rescale, PixelSpacing, undefined-length sequences, MONOCHROME1
 // (inverted at import, see Header::invert), multi-frame files (frame selection, see copy_pixels16).
-// The other JPEG-family encapsulated syntaxes (baseline/extended lossy JPEG, JPEG-LS, JPEG 2000, ...)
+// The other JPEG-family encapsulated syntaxes (progressive JPEG, JPEG-LS, JPEG 2000, ...)
 // are rejected with a SliceError: the slice is skipped and counted like a fast::Exception in the
 // reference. DCMTK behind FAST would decode them; that part of parity is unpinned (no DCMTK here).
 #pragma once
@@ -22,7 +24,16 @@
 
 namespace nm03::dicom {
 
-enum class Syntax : uint8_t { kImplicitLE, kExplicitLE, kExplicitBE, kDeflatedLE, kRleLossless, kJpegLossless };
+enum class Syntax : uint8_t {
+  kImplicitLE,
+  kExplicitLE,
+  kExplicitBE,
+  kDeflatedLE,
+  kRleLossless,
+  kJpegLossless,   // 1.2.840.10008.1.2.4.70 / .4.57 (nm03/jpeg_lossless.h)
+  kJpegBaseline,   // 1.2.840.10008.1.2.4.50: 8-bit sequential DCT (nm03/jpeg_dct.h)
+  kJpegExtended,   // 1.2.840.10008.1.2.4.51: 8/12-bit sequential DCT
+};
 
 // Name of a transfer syntax as used in messages and by the Python bindings.
 const char* syntax_name(Syntax s);
@@ -176,8 +187,11 @@ struct WriteSpec {
   // kJpegLossless: one lossless JPEG per frame (precision = BitsStored), selection value
   // `jpeg_predictor` (1: transfer syntax .4.70, else .4.57), restart markers every
   // `jpeg_restart_rows` rows (0: none), each frame split into `jpeg_fragments` fragments.
+  // kJpegBaseline / kJpegExtended: one lossy DCT JPEG per frame (8-bit / 12-bit samples, the stored
+  // bits clamped to the precision) at `jpeg_quality`, restart markers every `jpeg_restart_rows` block
+  // rows (0: none).
   Syntax syntax = Syntax::kExplicitLE;
-  int jpeg_predictor = 1, jpeg_restart_rows = 0, jpeg_fragments = 1;
+  int jpeg_predictor = 1, jpeg_restart_rows = 0, jpeg_fragments = 1, jpeg_quality = 90;
   bool preamble = true;  // write 128-byte preamble + "DICM" + file meta group (required by kDeflatedLE/kRleLossless)
 };
 

@@ -25,27 +25,6 @@
 
 namespace nm03 {
 
-// A mutex whose contended path spins (try_lock with pause) before it sleeps. The pool's critical
-// sections are a heap push/pop of a few hundred ns, taken by up to 16 workers at the same instant (a
-// for_each fans out one runner per worker): with std::mutex alone the losers slept in the kernel and
-// their unlockers paid a futex wake — 8–11% of the pool's CPU in the round-6 sampling profile
-// (profiles/r6/cpu_profile/). Spinning keeps the lock word uncontended (no futex wake on unlock).
-class SpinThenBlockMutex {
- public:
-  void lock() {
-    for (int i = 0; i < 4096; ++i) {
-      if (m_.try_lock()) return;
-      __builtin_ia32_pause();
-    }
-    m_.lock();
-  }
-  bool try_lock() { return m_.try_lock(); }
-  void unlock() { m_.unlock(); }
-
- private:
-  std::mutex m_;
-};
-
 // Tasks carry a priority (lower runs first; FIFO among equals). The engine uses the batch index,
 // so the loads and exports of earlier batches overtake later ones: the first batch reaches the GPU
 // after ~batch/threads loads instead of after every in-flight slot's loads (pipeline fill), and the
@@ -53,7 +32,9 @@ class SpinThenBlockMutex {
 //
 // Idle workers spin on the queue size, then sleep on a futex word that every push bumps (an
 // eventcount): a wake-up costs a futex wake only when a worker sleeps, and woken workers do not
-// queue up on a condition variable's mutex (the round-6 profile's lock waits inside loop()).
+// queue up again on a condition variable's mutex when they return from the wait. (A spin-then-block
+// lock for the heap was tried in round 6 and made it worse: 13% of the pool's CPU in try_lock,
+// profiles/r6/cpu_profile/.)
 class ThreadPool {
  public:
   // `on_start(i)` runs first on worker thread i (e.g. CPU pinning).
@@ -69,7 +50,7 @@ class ThreadPool {
   }
   ~ThreadPool() {
     {
-      std::lock_guard<SpinThenBlockMutex> g(m_);
+      std::lock_guard<std::mutex> g(m_);
       stop_ = true;
     }
     stop_flag_.store(true, std::memory_order_seq_cst);
@@ -81,7 +62,7 @@ class ThreadPool {
 
   void submit(std::function<void()> f, uint64_t prio = 0) {
     {
-      std::lock_guard<SpinThenBlockMutex> g(m_);
+      std::lock_guard<std::mutex> g(m_);
       push(std::move(f), prio);
     }
     wake(1);
@@ -89,7 +70,7 @@ class ThreadPool {
   // `n` copies of `f` under one lock (bulk fan-out of a parallel-for).
   void submit_n(int n, const std::function<void()>& f, uint64_t prio = 0) {
     {
-      std::lock_guard<SpinThenBlockMutex> g(m_);
+      std::lock_guard<std::mutex> g(m_);
       for (int i = 0; i < n; ++i) push(f, prio);
     }
     wake(n);
@@ -140,7 +121,7 @@ class ThreadPool {
       std::function<void()> f;
       uint32_t seq = 0;
       {
-        std::lock_guard<SpinThenBlockMutex> g(m_);
+        std::lock_guard<std::mutex> g(m_);
         if (!q_.empty()) {
           std::pop_heap(q_.begin(), q_.end(), later);
           f = std::move(q_.back().f);
@@ -170,7 +151,7 @@ class ThreadPool {
   std::atomic<uint32_t> wake_seq_{0};  // eventcount: bumped by every push (futex word)
   std::atomic<int> sleepers_{0};
   uint64_t seq_ = 0;
-  SpinThenBlockMutex m_;
+  std::mutex m_;
   bool stop_ = false;
 };
 

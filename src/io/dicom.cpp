@@ -3,6 +3,7 @@
 // main_parallel.cpp:78-80). Only what a 2D monochrome slice import needs is interpreted; every
 // other element is skipped structurally (including undefined-length sequences).
 #include "nm03/dicom.h"
+#include "nm03/jpeg_dct.h"
 #include "nm03/jpeg_lossless.h"
 
 #include <fcntl.h>
@@ -235,7 +236,7 @@ void decode_rle_frame(const uint8_t* f, size_t len, int rows, int cols, int byte
   }
 }
 
-// Lossless JPEG frames (PS3.5 A.4): one frame's fragments concatenated (a single-frame image may
+// JPEG frames (PS3.5 A.4; lossless or sequential DCT by the transfer syntax): one frame's fragments concatenated (a single-frame image may
 // span several fragments; a multi-frame one has one fragment per frame), decoded and stored as
 // native little-endian samples. The codec's precision must fit BitsAllocated; signed data is
 // sign-extended from BitsStored like the native encodings written by this repo (the codec carries the
@@ -265,12 +266,21 @@ void decode_jpeg_lossless_frames(Header& h, const uint8_t* d, const std::vector<
       src = d + frags[f].first;
       len = frags[f].second;
     }
-    const jpegll::Info info = jpegll::decode(src, len, px);
-    if (info.rows != h.rows || info.cols != h.cols)
-      throw SliceError("JPEG frame is " + std::to_string(info.cols) + "x" + std::to_string(info.rows) + ", the dataset says " +
+    int rows = 0, cols = 0, precision = 0;
+    if (h.syntax == Syntax::kJpegLossless) {
+      const jpegll::Info info = jpegll::decode(src, len, px);
+      rows = info.rows, cols = info.cols, precision = info.precision;
+    } else {
+      const jpegdct::Info info = jpegdct::decode(src, len, px);
+      if (h.syntax == Syntax::kJpegBaseline && info.precision != 8)
+        throw SliceError("JPEG Baseline transfer syntax with " + std::to_string(info.precision) + "-bit samples");
+      rows = info.rows, cols = info.cols, precision = info.precision;
+    }
+    if (rows != h.rows || cols != h.cols)
+      throw SliceError("JPEG frame is " + std::to_string(cols) + "x" + std::to_string(rows) + ", the dataset says " +
                        std::to_string(h.cols) + "x" + std::to_string(h.rows));
-    if (info.precision > h.bits_allocated)
-      throw SliceError("JPEG precision " + std::to_string(info.precision) + " exceeds BitsAllocated " +
+    if (precision > h.bits_allocated)
+      throw SliceError("JPEG precision " + std::to_string(precision) + " exceeds BitsAllocated " +
                        std::to_string(h.bits_allocated));
     uint8_t* o = dec->data() + f * fb;
     const int bs = h.bits_stored > 0 ? h.bits_stored : h.bits_allocated;
@@ -301,6 +311,8 @@ const char* syntax_name(Syntax s) {
     case Syntax::kDeflatedLE: return "deflated";
     case Syntax::kRleLossless: return "rle";
     case Syntax::kJpegLossless: return "jpeg-lossless";
+    case Syntax::kJpegBaseline: return "jpeg-baseline";
+    case Syntax::kJpegExtended: return "jpeg-extended";
   }
   return "?";
 }
@@ -352,6 +364,10 @@ Header parse_prefix(const uint8_t* data, size_t avail, size_t size) {
     h.syntax = Syntax::kRleLossless;
   } else if (ts == "1.2.840.10008.1.2.4.70" || ts == "1.2.840.10008.1.2.4.57") {
     h.syntax = Syntax::kJpegLossless;  // lossless JPEG, process 14 (SV1 / any selection value)
+  } else if (ts == "1.2.840.10008.1.2.4.50") {
+    h.syntax = Syntax::kJpegBaseline;  // lossy 8-bit sequential DCT, process 1
+  } else if (ts == "1.2.840.10008.1.2.4.51") {
+    h.syntax = Syntax::kJpegExtended;  // lossy 8/12-bit sequential DCT, processes 2 & 4
   } else if (ts.rfind("1.2.840.10008.1.2.4.", 0) == 0) {
     throw SliceError("Unsupported compressed DICOM transfer syntax (JPEG family): " + ts);
   } else {
@@ -363,7 +379,8 @@ Header parse_prefix(const uint8_t* data, size_t avail, size_t size) {
     Elem e = read_elem(c, explicit_vr);
     if (e.group == 0x7FE0 && e.elem == 0x0010) {
       if (e.len == kUndefined) {
-        const bool jpeg = h.syntax == Syntax::kJpegLossless;
+        const bool jpeg = h.syntax == Syntax::kJpegLossless || h.syntax == Syntax::kJpegBaseline ||
+                          h.syntax == Syntax::kJpegExtended;
         if (h.syntax != Syntax::kRleLossless && !jpeg)
           throw SliceError("Encapsulated (compressed) pixel data in a native transfer syntax");
         if (avail < full) throw SliceError("Truncated DICOM data");  // callers retry with the whole file
@@ -406,8 +423,9 @@ Header parse_prefix(const uint8_t* data, size_t avail, size_t size) {
         have_pixels = true;
         break;
       }
-      if (h.syntax == Syntax::kRleLossless || h.syntax == Syntax::kJpegLossless)
-        throw SliceError(std::string(h.syntax == Syntax::kRleLossless ? "RLE Lossless" : "JPEG Lossless") +
+      if (h.syntax == Syntax::kRleLossless || h.syntax == Syntax::kJpegLossless || h.syntax == Syntax::kJpegBaseline ||
+          h.syntax == Syntax::kJpegExtended)
+        throw SliceError(std::string(h.syntax == Syntax::kRleLossless ? "RLE Lossless" : "JPEG") +
                          " transfer syntax with native (not encapsulated) pixel data");
       h.pixel_offset = e.value_pos;
       h.pixel_length = e.len;
@@ -870,8 +888,11 @@ std::vector<uint8_t> write(const WriteSpec& s) {
                    : s.syntax == Syntax::kDeflatedLE ? "1.2.840.10008.1.2.1.99"
                    : s.syntax == Syntax::kJpegLossless
                        ? (s.jpeg_predictor == 1 ? "1.2.840.10008.1.2.4.70" : "1.2.840.10008.1.2.4.57")
-                       : "1.2.840.10008.1.2.5";
-  const bool encapsulated = s.syntax == Syntax::kRleLossless || s.syntax == Syntax::kJpegLossless;
+                   : s.syntax == Syntax::kJpegBaseline ? "1.2.840.10008.1.2.4.50"
+                   : s.syntax == Syntax::kJpegExtended ? "1.2.840.10008.1.2.4.51"
+                                                       : "1.2.840.10008.1.2.5";
+  const bool dct = s.syntax == Syntax::kJpegBaseline || s.syntax == Syntax::kJpegExtended;
+  const bool encapsulated = s.syntax == Syntax::kRleLossless || s.syntax == Syntax::kJpegLossless || dct;
   if ((s.syntax == Syntax::kDeflatedLE || encapsulated) && !s.preamble)
     throw std::runtime_error("deflated / RLE / JPEG files need the file meta group (preamble)");
   const char* sop_class = "1.2.840.10008.5.1.4.1.1.4";  // MR Image Storage
@@ -960,11 +981,18 @@ std::vector<uint8_t> write(const WriteSpec& s) {
       out.raw(v.data(), v.size());
     };
     item(0xE000, {});
-    for (int f = 0; s.syntax == Syntax::kJpegLossless && f < frames; ++f) {
+    for (int f = 0; (s.syntax == Syntax::kJpegLossless || dct) && f < frames; ++f) {
       std::vector<uint16_t> fr(fpix);
       for (size_t i = 0; i < fpix; ++i) fr[i] = s.pixels ? s.pixels[f * fpix + i] : 0;
-      std::vector<uint8_t> j = jpegll::encode(fr.data(), s.rows, s.cols, std::max(2, bs), s.jpeg_predictor, 0,
-                                              s.jpeg_restart_rows);
+      std::vector<uint8_t> j;
+      if (dct) {
+        const int prec = s.syntax == Syntax::kJpegBaseline || bs <= 8 ? 8 : 12;
+        const uint16_t mx = (uint16_t)((1u << prec) - 1), m = (uint16_t)((1u << bs) - 1);
+        for (auto& v : fr) v = std::min<uint16_t>((uint16_t)(v & m), mx);
+        j = jpegdct::encode(fr.data(), s.rows, s.cols, prec, s.jpeg_quality, s.jpeg_restart_rows * ((s.cols + 7) / 8));
+      } else {
+        j = jpegll::encode(fr.data(), s.rows, s.cols, std::max(2, bs), s.jpeg_predictor, 0, s.jpeg_restart_rows);
+      }
       if (j.size() & 1) j.push_back(0);  // even item length (a trailing pad byte after EOI)
       const int nf = frames == 1 ? std::max(1, s.jpeg_fragments) : 1;
       const size_t step = (j.size() / nf + 1) & ~(size_t)1;

@@ -24,6 +24,7 @@
 #include "nm03/numa.h"
 #include "nm03/golden.h"
 #include "nm03/jpeg.h"
+#include "nm03/jpeg_dct.h"
 #include "nm03/jpeg_lossless.h"
 #include "nm03/kernels.h"
 #include "nm03/synth.h"
@@ -323,8 +324,9 @@ PYBIND11_MODULE(_nm03, m) {
       [](py::array_t<uint16_t, py::array::c_style | py::array::forcecast> px, const std::string& type, int bits_stored,
          bool write_rescale, float slope, float intercept, float sx, float sy, int instance, const std::string& patient_id,
          const std::string& syntax, bool preamble, const std::string& photometric, int jpeg_predictor,
-         int jpeg_restart_rows, int jpeg_fragments) {
+         int jpeg_restart_rows, int jpeg_fragments, int jpeg_quality) {
         dicom::WriteSpec w;
+        w.jpeg_quality = jpeg_quality;
         w.jpeg_predictor = jpeg_predictor;
         w.jpeg_restart_rows = jpeg_restart_rows;
         w.jpeg_fragments = jpeg_fragments;
@@ -350,8 +352,10 @@ PYBIND11_MODULE(_nm03, m) {
                    : syntax == "deflated" ? dicom::Syntax::kDeflatedLE
                    : syntax == "rle"      ? dicom::Syntax::kRleLossless
                    : syntax == "jpeg-lossless" ? dicom::Syntax::kJpegLossless
+                   : syntax == "jpeg-baseline" ? dicom::Syntax::kJpegBaseline
+                   : syntax == "jpeg-extended" ? dicom::Syntax::kJpegExtended
                    : syntax == "explicit" ? dicom::Syntax::kExplicitLE
-                                          : throw std::invalid_argument("syntax: implicit|explicit|big|deflated|rle|jpeg-lossless");
+                                          : throw std::invalid_argument("syntax: implicit|explicit|big|deflated|rle|jpeg-lossless|jpeg-baseline|jpeg-extended");
         w.preamble = preamble;
         auto b = dicom::write(w);
         return py::bytes((const char*)b.data(), b.size());
@@ -360,7 +364,25 @@ PYBIND11_MODULE(_nm03, m) {
       py::arg("slope") = 1.f, py::arg("intercept") = 0.f, py::arg("spacing_x") = 1.f, py::arg("spacing_y") = 1.f,
       py::arg("instance") = 1, py::arg("patient_id") = "PGBM-000", py::arg("syntax") = "explicit",
       py::arg("preamble") = true, py::arg("photometric") = "MONOCHROME2", py::arg("jpeg_predictor") = 1,
-      py::arg("jpeg_restart_rows") = 0, py::arg("jpeg_fragments") = 1);
+      py::arg("jpeg_restart_rows") = 0, py::arg("jpeg_fragments") = 1, py::arg("jpeg_quality") = 90);
+  m.def("jpeg_dct_decode", [](py::bytes b) {
+    const std::string s = b;
+    std::vector<uint16_t> px;
+    const jpegdct::Info i = jpegdct::decode((const uint8_t*)s.data(), s.size(), px);
+    py::dict d;
+    d["precision"] = i.precision;
+    d["sof"] = i.sof;
+    d["restart_interval"] = i.restart_interval;
+    d["pixels"] = to_np(px, {(py::ssize_t)i.rows, (py::ssize_t)i.cols});
+    return d;
+  });
+  m.def("jpeg_dct_encode", [](py::array_t<uint16_t, py::array::c_style | py::array::forcecast> px, int precision,
+                              int quality, int restart_blocks) {
+    if (px.ndim() != 2) throw std::invalid_argument("pixels must be 2D");
+    std::vector<uint16_t> v = from_np<uint16_t>(px);
+    auto j = jpegdct::encode(v.data(), (int)px.shape(0), (int)px.shape(1), precision, quality, restart_blocks);
+    return py::bytes((const char*)j.data(), j.size());
+  }, py::arg("pixels"), py::arg("precision") = 8, py::arg("quality") = 90, py::arg("restart_blocks") = 0);
   m.def("jpeg_lossless_decode", [](py::bytes b) {
     const std::string s = b;
     std::vector<uint16_t> px;

@@ -254,7 +254,7 @@ TEST(dicom_mutation_fuzz) {
   auto px = ramp(3 * 12 * 16, 4093);
   for (auto& v : px) v &= 0x0FFF;
   for (Syntax sx : {Syntax::kExplicitLE, Syntax::kImplicitLE, Syntax::kExplicitBE, Syntax::kDeflatedLE,
-                    Syntax::kRleLossless, Syntax::kJpegLossless})
+                    Syntax::kRleLossless, Syntax::kJpegLossless, Syntax::kJpegExtended})
     for (int frames : {1, 3}) {
       WriteSpec ws;
       ws.rows = 12;

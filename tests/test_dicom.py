@@ -93,8 +93,11 @@ def test_rejects_compressed_and_garbage(native):
         native.dicom_parse(b"\x00" * 50)
     px = np.zeros((8, 8), dtype=np.uint16)
     b = native.dicom_bytes(px)
-    # JPEG-family syntaxes are skipped and counted (the reference's per-slice catch)
+    # JPEG-family syntaxes without a decoder here are skipped and counted (the reference's per-slice
+    # catch); the decoded ones (.4.50/.51/.57/.70) over native pixel data are malformed
     with pytest.raises(Exception, match="JPEG family"):
+        native.dicom_parse(_with_syntax(b, "1.2.840.10008.1.2.4.80"))  # JPEG-LS
+    with pytest.raises(Exception, match="not encapsulated"):
         native.dicom_parse(_with_syntax(b, "1.2.840.10008.1.2.4.50"))
     with pytest.raises(Exception, match="transfer syntax"):
         native.dicom_parse(_with_syntax(b, "1.2.840.10008.1.2.4.90"))

@@ -191,7 +191,8 @@ def test_host_only_compressed_and_photometric_forms(native, tmp_path):
     d.mkdir()
     good = native.phantom_slice(256, 256, 1, 3, 10, 7)
     forms = [dict(syntax="deflated"), dict(syntax="rle"), dict(photometric="MONOCHROME1"), dict(syntax="rle", photometric="MONOCHROME1"),
-             dict(syntax="jpeg-lossless"), dict(syntax="jpeg-lossless", jpeg_predictor=6, jpeg_fragments=2)]
+             dict(syntax="jpeg-lossless"), dict(syntax="jpeg-lossless", jpeg_predictor=6, jpeg_fragments=2),
+             dict(syntax="jpeg-extended")]
     paths = []
     for k, kw in enumerate(forms, 1):
         p = d / f"1-{k}.dcm"

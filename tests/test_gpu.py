@@ -1244,6 +1244,8 @@ def test_engine_new_dicom_forms_bit_exact(native, tmp_path):
         "1-5.dcm": native.dicom_bytes(a, bits_stored=12, syntax="jpeg-lossless"),
         "1-6.dcm": native.dicom_bytes(c, bits_stored=12, syntax="jpeg-lossless", jpeg_predictor=5,
                                       jpeg_restart_rows=32, jpeg_fragments=3),
+        # lossy JPEG Extended (12-bit DCT, .4.51): golden input = the same decoded samples
+        "1-7.dcm": native.dicom_bytes(b, bits_stored=12, syntax="jpeg-extended", jpeg_quality=90),
     }
     for name, data in files.items():
         (d / name).write_bytes(data)
