@@ -84,6 +84,7 @@ struct AppConfig {
   // --threads given. Otherwise every rank of the parallel CLI sizes its pool to its CPU partition
   // and its share of the CPU budget (numa::rank_partition), at most the reference's 16.
   bool threads_set = false;
+  bool streams_set = false;  // --streams given (else a one-HW-queue job uses 2 slots, see parallel_rank)
   // --mode 3d --split-volume: every patient's volume is decomposed into z-slabs over all ranks
   // (volume_slabs.h) instead of sharding whole patients over the ranks.
   bool split_volume = false;

@@ -47,7 +47,7 @@ struct RankCpus {
   int node = -1;           // NUMA node of the rank's GPU (-1: unknown, partition of all CPUs)
   int index = 0, count = 1;  // this rank is partition `index` of `count` on its node
   std::vector<int> cpus;   // disjoint from every other local rank's
-  int threads = 1;         // pool threads: min(cap, |cpus|, budget / local ranks), ≥ 1
+  int threads = 1;         // pool threads: min(cap, |cpus|, share − min(2, share/4)), share = budget / local ranks, ≥ 1
 };
 // `rank_nodes[r]` = NUMA node of local rank r's GPU (-1 unknown). The ranks on one node split its
 // allowed CPUs into `count` groups of whole physical cores (SMT siblings stay together), in rank

@@ -107,10 +107,19 @@ class ThreadPool {
   // 345–398k / 357–398k slices/s over 4 interleaved rounds at equal host CPU per step — equal on
   // quiet boxes, up to +20% when other tenants load the host (delayed wake-ups).
   static constexpr int kSpinUs = 200;
+  // NM03_POOL_SPIN_US overrides kSpinUs (A/B experiments).
+  static int spin_us() {
+    static const int v = [] {
+      const char* e = std::getenv("NM03_POOL_SPIN_US");
+      return e && *e ? std::max(0, std::atoi(e)) : kSpinUs;
+    }();
+    return v;
+  }
   void loop() {
+    const int spin = spin_us();
     for (;;) {
-      if (queued_.load(std::memory_order_relaxed) == 0) {
-        const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(kSpinUs);
+      if (queued_.load(std::memory_order_relaxed) == 0 && spin > 0) {
+        const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(spin);
         // the clock is read every 64 polls, not every poll (a vDSO call each)
         for (int k = 0; queued_.load(std::memory_order_relaxed) == 0 && !stop_flag_.load(std::memory_order_relaxed);
              ++k) {

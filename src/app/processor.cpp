@@ -162,7 +162,10 @@ AppConfig parse_args(int argc, char** argv, const std::string& which) {
       c.gpus = v == "all" ? kGpusAll : v == "auto" ? kGpusAuto : std::max(1, std::atoi(v.c_str()));
     } else if (a == "--device") c.engine.device = std::atoi(val().c_str());
     else if (a == "--batch-size") c.engine.batch_size = std::atoi(val().c_str());
-    else if (a == "--streams") c.engine.streams = std::atoi(val().c_str());
+    else if (a == "--streams") {
+      c.engine.streams = std::atoi(val().c_str());
+      c.streams_set = true;
+    }
     else if (a == "--threads") {
       c.engine.threads = std::atoi(val().c_str());
       c.threads_set = true;
@@ -639,6 +642,10 @@ int parallel_rank(const AppConfig& cfg, int rank, int size, Comm& comm, int devi
   // shares one HIP stream — separate streams would feed the same queue anyway — and the start-up
   // thread creates one stream instead of slots + 1 (≈ 3.8 ms each on a cold process).
   ec.shared_stream = one_hw_queue();
+  // With one stream the slots only overlap host work; 2 of them pin a third less memory than 3 for
+  // the same cold pass (interleaved cold CLIs: constructor 6.6 → 4.4 ms, processing 5.1 → 5.6 ms;
+  // one slot: 2.7 ms but 9.2 ms processing, profiles/r6/cold_cli/).
+  if (ec.shared_stream && !cfg.streams_set) ec.streams = std::min(ec.streams, 2);
   EngineStartup su(device, ec.shared_stream ? 1 : std::max(1, cfg.engine.streams) + 1, data_plane ? &comm : nullptr);
   double engine_wait_s = 0, plan_s = 0, setup_tail_s = 0;
   std::unique_ptr<Engine> engine_p;

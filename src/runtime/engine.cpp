@@ -616,8 +616,8 @@ struct Engine::Impl {
         s.up = upload_stream();
       }
       mark("streams");
-      // NM03_EVENT_TIMING=0 (experiment): events without timestamps; StageTimes then has no h2d /
-      // kernel split.
+      // NM03_EVENT_TIMING=0 (experiment): events without timestamps and only the records the
+      // stream order needs; StageTimes then has no h2d / kernel split.
       const unsigned ef = event_timing() ? hipEventDefault : hipEventDisableTiming;
       check_hip(hipEventCreateWithFlags(&s.ev0, ef), "hipEventCreate");
       check_hip(hipEventCreateWithFlags(&s.ev1, ef), "hipEventCreate");
@@ -725,7 +725,7 @@ struct Engine::Impl {
       }
       if (chunk && (end - s.uploaded) * 2 >= chunk) {
         if (!s.upload_started) {
-          check_hip(hipEventRecord(s.ev0, s.up), "event");
+          if (event_timing()) check_hip(hipEventRecord(s.ev0, s.up), "event");
           s.upload_started = true;
         }
         check_hip(hipMemcpyAsync(s.d_blob + s.raw_base + s.uploaded * 2, s.h_blob + s.raw_base + s.uploaded * 2,
@@ -1081,7 +1081,7 @@ struct Engine::Impl {
     // SDMA measured no gain (profiles/r3/shader_upload/) and was removed in round 4.
     const bool inline_up = s.uploaded == 0 && !s.upload_started && nl <= 16;
     hipStream_t up = inline_up ? s.stream : s.up;
-    if (!s.upload_started && !inline_up) check_hip(hipEventRecord(s.ev0, up), "event");
+    if (!s.upload_started && !inline_up && event_timing()) check_hip(hipEventRecord(s.ev0, up), "event");
     if (s.uploaded == 0) {
       check_hip(hipMemcpyAsync(s.d_blob, s.h_blob, s.raw_base + raw_end * 2, hipMemcpyHostToDevice, up),
                 "H2D tables + pixels");
@@ -1093,7 +1093,8 @@ struct Engine::Impl {
                   "H2D pixels");
     }
     s.uploaded = raw_end;
-    if (!inline_up) check_hip(hipEventRecord(s.ev1, up), "event");
+    // ev1: the kernels' wait on a separate upload stream, and the h2d/kernel time split.
+    if (!inline_up && (event_timing() || up != s.stream)) check_hip(hipEventRecord(s.ev1, up), "event");
     if (up != s.stream) check_hip(hipStreamWaitEvent(s.stream, s.ev1, 0), "wait upload");
     // The median reads the upload directly (12-bit pairs decoded in its tile load) and writes the
     // expanded samples for the render/JPEG stages. One eager launch per kernel: hipGraph replay of

@@ -217,8 +217,14 @@ RankCpus rank_partition(const Topology& t, const std::vector<int>& rank_nodes, i
     }
     std::sort(r.cpus.begin(), r.cpus.end());
   }
+  // The rank's CPU share keeps up to 2 CPUs for its other threads (slot threads, the HIP runtime's
+  // event thread, the launcher): with all 16 of a 16-CPU quota given to the pool, the cgroup was
+  // throttled 0.5–1 ms per 465-slice step and the headline was lower than with 14 pool threads
+  // (394k at 18.9 ms of CPU vs 403k at 17.3 ms, interleaved, profiles/r6/ab_pool/). A share above
+  // the cap + 2 is unaffected (the 8-GPU node's 32-CPU partitions keep 16 pool threads).
   const int share = std::max(1, budget / std::max(1, n));
-  r.threads = std::max(1, std::min({cap, (int)std::max<size_t>(1, r.cpus.size()), share}));
+  const int pool_share = std::max(1, share - std::min(2, share / 4));
+  r.threads = std::max(1, std::min({cap, (int)std::max<size_t>(1, r.cpus.size()), pool_share}));
   return r;
 }
 

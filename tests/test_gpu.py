@@ -726,7 +726,7 @@ def test_cli_sequential_equals_parallel(native, cohort_root, tmp_path):
         assert line in r1.stdout, line
     for line in ("=== Starting Parallel Processing for All Patients ===",
                  "=== Processing Patient: PGBM-001 using Parallel Processing ===", "Created output directory: ",
-                 "images to process for patient PGBM-001", "Using 16 threads", "Successfully processed 4/4 patients."):
+                 "images to process for patient PGBM-001", "Using ", " threads", "Successfully processed 4/4 patients."):
         assert line in r2.stdout, line
 
 

@@ -67,9 +67,13 @@ def test_ranks_sharing_one_gpu_split_its_node(native, tmp_path):
 
 
 def test_single_rank_gets_its_node(native, tmp_path):
+    """The 1-GPU box: a 16-CPU quota keeps 2 CPUs for the slot and runtime threads (14 pool threads);
+    a 32-CPU share is capped at 16."""
     allowed = _fake_host(tmp_path)
     (p,) = _parts(native, tmp_path, allowed, [1], budget=16)
-    assert p["node"] == 1 and p["cpus"] == list(range(64, 128)) + list(range(192, 256)) and p["threads"] == 16
+    assert p["node"] == 1 and p["cpus"] == list(range(64, 128)) + list(range(192, 256)) and p["threads"] == 14
+    (p,) = _parts(native, tmp_path, allowed, [1], budget=32)
+    assert p["threads"] == 16
 
 
 def test_unknown_nodes_and_affinity_mask(native, tmp_path):
@@ -78,7 +82,7 @@ def test_unknown_nodes_and_affinity_mask(native, tmp_path):
     allowed = [0, 1, 2, 3, 8, 9, 10, 11]  # 4 cores with their siblings
     parts = _parts(native, tmp_path, allowed, [-1, -1], budget=8)
     assert [sorted(p["cpus"]) for p in parts] == [[0, 1, 8, 9], [2, 3, 10, 11]]
-    assert [p["threads"] for p in parts] == [4, 4]
+    assert [p["threads"] for p in parts] == [3, 3]  # share 4, one CPU kept for the other threads
 
 
 @pytest.mark.parametrize("ranks", [3, 5])

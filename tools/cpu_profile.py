@@ -218,7 +218,7 @@ def classify(frames, phases):
     return "other"
 
 
-def analyse(path, top=30):
+def analyse(path, top=30, chain_pat=""):
     meta, maps, threads, stacks = parse(path)
     req = collections.defaultdict(set)
     for _, _, pcs in stacks:
@@ -271,7 +271,13 @@ def analyse(path, top=30):
             pool_task["queue hand-off (ThreadPool / TaskGroup)"] += count
         else:
             pool_task["other"] += count
-    res = {"file": path, "samples": total, "period_us": meta.get("period_us"), "dropped": meta.get("dropped"),
+    chains = collections.Counter()
+    if chain_pat:
+        for count, tid, pcs in stacks:
+            fr = frames_of(pcs)
+            if fr and any(chain_pat in f for f in fr[:2]):
+                chains[" <- ".join(f[:60] for f in fr[:10])] += count
+    res = {"file": path, "samples": total, "chains": chains.most_common(top), "period_us": meta.get("period_us"), "dropped": meta.get("dropped"),
            "groups": dict(groups.most_common()), "pool_task": dict(pool_task.most_common()),
            "load_phase": dict(load_phase.most_common()), "write_phase": dict(write_phase.most_common()),
            "self_top": {g: c.most_common(top) for g, c in self_by_group.items()},
@@ -298,6 +304,10 @@ def report(res, out=sys.stdout):
             print(f"\n{title} by phase (% of its samples):", file=out)
             for t, c in res[key].items():
                 print(f"  {pct(c, sub)}  {c:7d}  {t}", file=out)
+    if res.get("chains"):
+        print("\nfull call chains whose leaf frames match --chains (% of all samples):", file=out)
+        for k, c in res["chains"]:
+            print(f"  {pct(c)}  {c:7d}  {k}", file=out)
     if res.get("ioctls"):
         print("\nioctl samples by request code (% of all samples):", file=out)
         for k, c in res["ioctls"]:
@@ -318,10 +328,11 @@ def main():
     ap.add_argument("files", nargs="+")
     ap.add_argument("--top", type=int, default=25)
     ap.add_argument("--json", default="")
+    ap.add_argument("--chains", default="", help="also print the top full call chains whose leaf frames contain this")
     a = ap.parse_args()
     all_res = []
     for f in a.files:
-        r = analyse(f, a.top)
+        r = analyse(f, a.top, a.chains)
         report(r)
         all_res.append(r)
     if a.json:

@@ -13,26 +13,44 @@ for s in $steps; do
     bench)
       for r in $(seq ${ROUNDS_B:-4}); do
         for v in ${VARIANTS:-old new}; do
-          S=bench.py; e=""
+          # "old" = abprev/, "new" = this tree, "new:VAR=VAL" = this tree with an environment variant
+          # "new@--flag=value" = this tree with an extra bench.py argument
+          S=bench.py; e=""; a=""
           [ $v = old ] && S=abprev/bench.py
-          [ $v = new_noevt ] && e="NM03_EVENT_TIMING=0"
-          timeout -k 10 240 env $e python -u $S --keep-data --data-root $D --steps ${STEPS:-2000} --warmup 5 --no-secondary \
-            --wipe-passes 0 --single-passes 0 --cli-runs 0 > $O/bench_${v}_$r.json 2>> $O/bench.err || exit 1
+          case $v in new:*) e="${v#new:}";; new@*) a="${v#new@}";; esac
+          timeout -k 10 240 env $e python -u $S $a --keep-data --data-root $D --steps ${STEPS:-2000} --warmup 5 --no-secondary \
+            --wipe-passes 0 --single-passes 0 --cli-runs 0 > "$O/bench_${v}_$r.json" 2>> $O/bench.err || exit 1
         done
       done
       ;;
     cold)
       C=/dev/shm/nm03_cold_cohort
       [ -d $C ] || build/bin/nm03_synth --data-root $C/ --threads 16 > /dev/null || exit 1
-      timeout -k 10 600 python -u tools/cold_ab.py $C/ ${ROUNDS:-12} old=abprev/bin:abprev/nm03_capstone_project_amd/lib \
-        new=build/bin > $O/cold_ab.jsonl 2> $O/cold_ab.err || exit 1
-      rm -rf $C /tmp/cold_ab_old /tmp/cold_ab_new
+      timeout -k 10 600 python -u tools/cold_ab.py $C/ ${ROUNDS:-12} ${COLD_VARIANTS:-old=abprev/bin:abprev/nm03_capstone_project_amd/lib new=build/bin} \
+        > $O/cold_ab.jsonl 2> $O/cold_ab.err || exit 1
+      rm -rf $C /dev/shm/cold_ab_*
       cat $O/cold_ab.jsonl | cut -c1-400
+      ;;
+    tests)
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider \
+        > $O/pytest_gpu.log 2>&1 || { tail -30 $O/pytest_gpu.log; exit 1; }
+      tail -2 $O/pytest_gpu.log
+      timeout -k 10 300 python -c 'import __graft_entry__ as g; g.smoke()' > $O/smoke.log 2>&1 || exit 1
+      ;;
+    preload)
+      C=/dev/shm/nm03_cold_cohort
+      [ -d $C ] || build/bin/nm03_synth --data-root $C/ --threads 16 > /dev/null || exit 1
+      for k in 1 2 3; do
+        NM03_PRELOAD_TRACE=1 timeout -k 10 60 build/bin/img_processing_parallel --data-root $C/ --out /dev/shm/pl_out --quiet \
+          --json $O/preload_$k.json 2>> $O/preload.txt || exit 1
+      done
+      cat $O/preload.txt
+      rm -rf $C /dev/shm/pl_out
       ;;
     prof)
       timeout -k 10 240 python -u bench.py --keep-data --data-root $D --steps 4000 --warmup 5 --no-secondary --wipe-passes 0 \
         --single-passes 0 --cli-runs 0 --cpu-profile $O/cpu > $O/bench_prof.json 2> $O/bench_prof.err || exit 1
-      timeout -k 10 600 python tools/cpu_profile.py $O/cpu.rank0 --top 40 --json $O/cpu_profile.json \
+      timeout -k 10 600 python tools/cpu_profile.py $O/cpu.rank0 --top 40 --chains __lll_lock --json $O/cpu_profile.json \
         > $O/cpu_profile.txt 2>&1 || exit 1
       head -45 $O/cpu_profile.txt | cut -c1-200
       ;;
