@@ -74,10 +74,10 @@ struct EngineConfig {
   // into the output buffer (what the encoder's PCIe stores would leave in memory). Measures the
   // host side's CPU per slice on its own, on any machine (bench.py --host-only).
   bool host_only = false;
-  // Host-mapped bytes per image for the GPU encoder's stuffed output (0 = a quarter of the canvas:
-  // 64 KiB for 512², ≈ 5× a typical medical render of 12 KiB; round 5 used half the canvas, whose
-  // pinning was a third of a cold CLI's engine constructor). Larger images are CPU re-encoded
-  // (StageTimes counts them); tests force that path with a tiny capacity.
+  // Host-mapped bytes per image for the GPU encoder's stuffed output (0 = 3/8 of the canvas: 96 KiB
+  // for 512² — full-contrast noise renders to 86.6 KB, a phantom slice to 14 KB; round 5 used half
+  // the canvas, whose pinning was a third of a cold CLI's engine constructor). Larger images are CPU
+  // re-encoded (StageTimes counts them); tests force that path with a tiny capacity.
   uint32_t jpeg_out_cap = 0;
   // Every slot and the uploads on ONE HIP stream (false: a stream per slot plus a shared upload
   // stream). For processes limited to one HW queue (GPU_MAX_HW_QUEUES=1, the CLIs' short jobs), where

@@ -289,7 +289,7 @@ struct Engine::Impl {
   explicit Impl(const EngineConfig& c) : cfg(c), place(c.device, c.cpus) {
     if (const char* e = std::getenv("NM03_PACK12"); e && *e && *e == '0') pack12_ = false;
     out_cap_ = cfg.jpeg_out_cap ? std::max<uint32_t>(64, cfg.jpeg_out_cap)
-                                : (uint32_t)std::max<size_t>(32 * 1024, (size_t)cfg.render.out_width * cfg.render.out_height / 4) + 64;
+                                : (uint32_t)std::max<size_t>(32 * 1024, (size_t)cfg.render.out_width * cfg.render.out_height * 3 / 8) + 64;
     out_cap_ = (out_cap_ + 15u) & ~15u;  // 16-byte aligned segments (the encoder's dwordx4 stores)
     upload_chunk_ = cfg.upload_chunk_kb < 0 ? (size_t)2 << 20 : (size_t)cfg.upload_chunk_kb << 10;
     host_only_ = cfg.host_only;
