@@ -80,8 +80,9 @@ struct Slot {
   size_t cap_pixels = 0;  // u16 elements of expanded samples per batch (device raw/median buffers)
   // The blob's raw region also holds `hole_slack` u16 of slack for abandoned 12-bit reservations
   // (a checked single-pass pack that found a wide sample, see load_one); `hole_credit` is what is
-  // left of it in the current batch (under alloc_m).
-  size_t hole_slack = 0, hole_credit = 0;
+  // left of it in the current batch (an atomic: taken and returned without a lock).
+  size_t hole_slack = 0;
+  std::atomic<size_t> hole_credit{0};
   // blob layout (byte offsets)
   size_t off_stats = 0, off_desc = 0, off_medt = 0, off_shpt = 0, off_seeds = 0, off_render = 0, off_jpeg = 0,
          raw_base = 0, blob_bytes = 0;
@@ -128,7 +129,6 @@ struct Slot {
   std::atomic<uint64_t> alloc_word{0};
   size_t raw_used() const { return (size_t)(alloc_word.load(std::memory_order_acquire) & kUsedMask); }
   size_t n_allocs() const { return (size_t)(alloc_word.load(std::memory_order_acquire) >> kAllocShift); }
-  std::mutex alloc_m;  // hole_credit only (slices wider than 12 bits)
   std::mutex prog_m;
   std::condition_variable prog_cv;
   std::atomic<size_t> loads_finished{0};
@@ -850,18 +850,18 @@ struct Engine::Impl {
         };
         try {
           const bool low12 = h.bits_stored <= 12;
-          if (packable && !low12) {
-            std::lock_guard<std::mutex> g(s.alloc_m);
-            credit = s.hole_credit >= plen;
-            if (credit) s.hole_credit -= plen;
+          if (packable && !low12) {  // take plen of credit if there is that much (lock-free)
+            size_t c = s.hole_credit.load(std::memory_order_relaxed);
+            while (c >= plen && !s.hole_credit.compare_exchange_weak(c, c - plen, std::memory_order_acq_rel)) {
+            }
+            credit = c >= plen;
           }
           if (credit) {
             reserve(plen);
             uint8_t* dst = reinterpret_cast<uint8_t*>(reinterpret_cast<uint16_t*>(s.raw_cpu) + off);
             packed = pack12::pack_stream_checked(samples, npix, dst);
             if (packed) {
-              std::lock_guard<std::mutex> g(s.alloc_m);
-              s.hole_credit += plen;
+              s.hole_credit.fetch_add(plen, std::memory_order_acq_rel);
             } else {
               // Grow in place while this is still the last allocation, else leave a hole (uploaded,
               // unused; paid from the credit) and take a 16-bit allocation.
@@ -870,8 +870,7 @@ struct Engine::Impl {
               if (off + ulen <= cap &&
                   s.alloc_word.compare_exchange_strong(last, grown, std::memory_order_acq_rel, std::memory_order_relaxed)) {
                 s.allocs[idx].len = ulen;
-                std::lock_guard<std::mutex> g(s.alloc_m);
-                s.hole_credit += plen;
+                s.hole_credit.fetch_add(plen, std::memory_order_acq_rel);
               } else {
                 s.allocs[idx].done.store(true, std::memory_order_release);
                 reserve(ulen);
@@ -1183,7 +1182,7 @@ struct Engine::Impl {
     }
     for (size_t k = 0; k < s.max_allocs; ++k) s.allocs[k].done.store(false, std::memory_order_relaxed);
     s.alloc_word.store(0, std::memory_order_relaxed);
-    s.hole_credit = s.hole_slack;
+    s.hole_credit.store(s.hole_slack, std::memory_order_relaxed);
     s.uploaded = 0;
     s.upload_started = false;
     s.loads_finished.store(0, std::memory_order_relaxed);
