@@ -875,9 +875,9 @@ void launch_jpeg(const uint8_t* canvas, const JpegDesc* jd, int ncanvas, int out
 void preload_kernels(bool with_volume) {
   // NM03_PRELOAD_TRACE=1: milliseconds per translation unit on stderr (what a cold start pays for
   // each code object).
-  static const bool trace = [] {
+  static const int trace = [] {
     const char* e = std::getenv("NM03_PRELOAD_TRACE");
-    return e && *e == '1';
+    return e && *e ? std::atoi(e) : 0;  // 2: the same loads in reverse order (first-use cost vs size)
   }();
   auto t = std::chrono::steady_clock::now();
   auto lap = [&](const char* what) {
@@ -886,6 +886,14 @@ void preload_kernels(bool with_volume) {
     std::fprintf(stderr, "[nm03 preload] %s %.3f ms\n", what, std::chrono::duration<double, std::milli>(n - t).count());
     t = n;
   };
+  if (trace == 2) {
+    preload_render();
+    lap("k3_render");
+    preload_srg();
+    lap("k2_srg_morph");
+    preload_sharpen();
+    lap("k1_sharpen");
+  }
   preload_median();
   lap("k1_median");
   preload_sharpen();

@@ -748,7 +748,8 @@ def test_cli_parallel_multirank_identical(native, cohort_root, tmp_path, ranks):
     t1, tn = _tree(str(g1)), _tree(str(gn))
     assert t1 == tn and len(t1) > 0
     # rank 0 prints the whole cohort in patient order: identical apart from the paths and threads
-    norm = lambda s, d: s.replace(str(d), "OUT").replace("Using 4 threads", "Using 16 threads")  # noqa: E731
+    import re
+    norm = lambda s, d: re.sub(r"Using \d+ threads", "Using T threads", s.replace(str(d), "OUT"))  # noqa: E731
     assert norm(one.stdout, g1) == norm(many.stdout, gn)
     j = json.load(open(tmp_path / "m.json"))
     assert j["gpus"] == ranks and j["backend"] == "host"

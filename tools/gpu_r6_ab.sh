@@ -41,8 +41,11 @@ for s in $steps; do
       C=/dev/shm/nm03_cold_cohort
       [ -d $C ] || build/bin/nm03_synth --data-root $C/ --threads 16 > /dev/null || exit 1
       for k in 1 2 3; do
-        NM03_PRELOAD_TRACE=1 timeout -k 10 60 build/bin/img_processing_parallel --data-root $C/ --out /dev/shm/pl_out --quiet \
-          --json $O/preload_$k.json 2>> $O/preload.txt || exit 1
+        for t in 1 2; do
+          echo "== NM03_PRELOAD_TRACE=$t run $k" >> $O/preload.txt
+          NM03_PRELOAD_TRACE=$t timeout -k 10 60 build/bin/img_processing_parallel --data-root $C/ --out /dev/shm/pl_out --quiet \
+            --json $O/preload_${t}_$k.json > /dev/null 2>> $O/preload.txt || exit 1
+        done
       done
       cat $O/preload.txt
       rm -rf $C /dev/shm/pl_out
