@@ -153,8 +153,11 @@ class DeferredComm final : public Comm {
     std::string err;
     try {
       std::unique_lock<std::mutex> g(m_);
-      // Bounded, abort-aware wait for a start-up thread still inside start/settle.
-      const double deadline = t0 + timeout_;
+      // Bounded, abort-aware wait for a start-up thread still inside start/settle. That thread began
+      // before t0 (else state_ was kIdle and this thread started it) and is itself bounded: the uid
+      // wait by timeout_, the settle loop by its own timeout_ — so this net must outlast both, or a
+      // slow start (a loaded host) ends here as a job abort instead of the settle's agreed fallback.
+      const double deadline = t0 + 2 * timeout_ + 1.0;
       while (state_ == kStarting || state_ == kSettling) {
         cv_.wait_for(g, std::chrono::milliseconds(2));
         if (state_ != kStarting && state_ != kSettling) break;

@@ -879,15 +879,22 @@ std::vector<RankOutcome> run_fake_world(FakeWorld& w, double timeout_s, std::vec
       RankOutcome& o = out[(size_t)r];
       try {
         auto c = nm03::make_deferred_comm(r, w.n, 0, w.seg, timeout_s, f);
+        std::atomic<bool> began{false};
         std::thread su([&] {
-          if (fail_start[(size_t)r])
+          if (fail_start[(size_t)r]) {
             c->fail_data_plane("injected start-up failure");
-          else {
+            began.store(true);
+          } else {
+            began.store(true);  // start_data_plane() moves the state off kIdle before it can block
             c->start_data_plane();
             c->settle_data_plane(nullptr);
           }
         });
         c->barrier();  // control plane meanwhile
+        // As in the CLI, promote() comes after the start-up thread's hand-off: a promote() that found
+        // the plane idle would start it on this thread (a loaded host could otherwise let rank 0's main
+        // thread overtake its injected start-up failure).
+        while (!began.load()) std::this_thread::sleep_for(std::chrono::microseconds(50));
         if (abort_rank_after_ms >= 0 && r == 0) {
           std::this_thread::sleep_for(std::chrono::milliseconds(abort_rank_after_ms));
           w.seg->raise_abort(w.n - 1);  // rank n-1 "died" while the others start
