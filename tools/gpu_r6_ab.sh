@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round 6: interleaved A/B of the round-start build (abprev/: its bench.py, package and CLI) against
 # this tree — headline bench (host CPU per step) and cold CLI walls — plus a symbolised CPU profile of
-# this tree. Usage: gpurun -- 'bash tools/gpu_r6_ab.sh [bench|cold|prof]...' → gpurun_out/r6_ab/
+# this tree. Usage: gpurun -- 'bash tools/gpu_r6_ab.sh [bench|cold|prof|tests|preload|timeline]...' → gpurun_out/r6_ab/
 set -o pipefail
 O=gpurun_out/r6_ab
 mkdir -p $O
@@ -49,6 +49,15 @@ for s in $steps; do
       done
       cat $O/preload.txt
       rm -rf $C /dev/shm/pl_out
+      ;;
+    timeline)
+      # kernel + copy trace of the pipelined steady state (no counters): union-busy of kernels and H2D
+      timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d $O/tl -o bench -- \
+        python3 -u bench.py --keep-data --data-root $D --steps ${TL_STEPS:-1000} --warmup 5 --no-secondary --wipe-passes 0 \
+        --single-passes 0 --cli-runs 0 $TL_ARGS > $O/bench_tl.json 2> $O/bench_tl.err || exit 1
+      python3 tools/timeline.py --window $O/tl > $O/timeline.txt 2>&1 || exit 1
+      cat $O/timeline.txt
+      find $O/tl -name '*.csv' -size +20M -delete
       ;;
     prof)
       timeout -k 10 240 python -u bench.py --keep-data --data-root $D --steps 4000 --warmup 5 --no-secondary --wipe-passes 0 \

@@ -4,7 +4,8 @@
 Run (on the GPU box, no counters):
   NM03_ROCTX=1 rocprofv3 --kernel-trace --memory-copy-trace --marker-trace --output-format csv \
       -d gpurun_out/tl -o bench -- python3 bench.py --steps 3 --warmup 1
-then `python tools/timeline.py gpurun_out/tl`.
+then `python tools/timeline.py gpurun_out/tl` (per step, `--no-pipeline` runs), or
+`--window` for the pipelined default: utilisation over the whole `bench.steps` range.
 
 bench.py pushes a `bench.step` roctx range around every engine run when NM03_ROCTX is set; the
 engine pushes `nm03.load` (per slice), `nm03.gpu_batch` (per batch) and `nm03.export` (per slice).
@@ -72,9 +73,46 @@ def load(d):
     return ev
 
 
+def window(d):
+    """Pipelined bench (overlapping passes): utilisation over the whole `bench.steps` range — union-busy
+    fractions of kernels, H2D copies and either, mean kernel concurrency, per-kernel totals."""
+    ev = load(d)
+    rng = [(a, b) for a, b, m in ev["marker"] if "bench.steps" in m]
+    if rng:
+        lo, hi = rng[-1]
+    else:  # no roctx: the middle 80% of the kernels' span (leaves warm-up and tear-down out)
+        allv = [x for k in ("kernel", "h2d") for x in ev[k]]
+        lo, hi = min(a for a, _, _ in allv), max(b for _, b, _ in allv)
+        lo, hi = lo + (hi - lo) // 10, hi - (hi - lo) // 10
+    span = hi - lo
+    k = [(a, b) for a, b, _ in ev["kernel"]]
+    h = [(a, b) for a, b, _ in ev["h2d"]]
+    dh = [(a, b) for a, b, _ in ev["d2h"]]
+    ksum = sum(min(b, hi) - max(a, lo) for a, b in k if b > lo and a < hi)
+    print(f"window {span / 1e6:.2f} ms")
+    for name, iv in (("kernels", k), ("h2d", h), ("d2h", dh), ("kernels|h2d", k + h)):
+        u = union(iv, lo, hi)
+        print(f"  {name:12s} busy {u / 1e6:9.2f} ms  {100.0 * u / span:5.1f}% of the window")
+    ku = union(k, lo, hi)
+    if ku:
+        print(f"  mean kernels in flight while any runs: {ksum / ku:.2f}")
+    tot = {}
+    for a, b, n in ev["kernel"]:
+        if b > lo and a < hi:
+            t = tot.setdefault(n, [0, 0])
+            t[0] += min(b, hi) - max(a, lo)
+            t[1] += 1
+    for n, (t, c) in sorted(tot.items(), key=lambda x: -x[1][0]):
+        print(f"  {t / 1e6:9.2f} ms {100.0 * t / span:5.1f}%  n={c:6d}  mean {t / c / 1e3:7.1f} us  {n[:70]}")
+    if h:
+        durs = sorted((b - a) / 1e3 for a, b in h if b > lo and a < hi)
+        if durs:
+            print(f"  h2d copies: n={len(durs)} median={durs[len(durs) // 2]:.1f}us max={durs[-1]:.1f}us")
+
+
 def report(d):
     ev = load(d)
-    steps = sorted((a, b) for a, b, m in ev["marker"] if "bench.step" in m)
+    steps = sorted((a, b) for a, b, m in ev["marker"] if "bench.step" in m and "bench.steps" not in m)
     if not steps:  # fall back to the whole trace as one step
         allv = [x for k in ("kernel", "h2d") for x in ev[k]]
         steps = [(min(a for a, _, _ in allv), max(b for _, b, _ in allv))]
@@ -107,4 +145,5 @@ def report(d):
 
 
 if __name__ == "__main__":
-    report(sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/tl")
+    args = [a for a in sys.argv[1:] if not a.startswith("-")]
+    (window if "--window" in sys.argv else report)(args[0] if args else "gpurun_out/tl")
