@@ -499,14 +499,6 @@ struct Engine::Impl {
     return on;
   }
 
-  static bool event_timing() {
-    static const bool on = [] {
-      const char* e = std::getenv("NM03_EVENT_TIMING");
-      return !(e && *e == '0');
-    }();
-    return on;
-  }
-
   void make_templates() {
     golden::SliceInput in;
     in.w = in.h = 256;
@@ -616,13 +608,13 @@ struct Engine::Impl {
         s.up = upload_stream();
       }
       mark("streams");
-      // NM03_EVENT_TIMING=0 (experiment): events without timestamps and only the records the
-      // stream order needs; StageTimes then has no h2d / kernel split.
-      const unsigned ef = event_timing() ? hipEventDefault : hipEventDisableTiming;
-      check_hip(hipEventCreateWithFlags(&s.ev0, ef), "hipEventCreate");
-      check_hip(hipEventCreateWithFlags(&s.ev1, ef), "hipEventCreate");
-      // Batch completion is polled by the slot thread (wait_batch): no blocking-sync event.
-      check_hip(hipEventCreateWithFlags(&s.ev2, ef), "hipEventCreate");
+      // Timing events (the h2d / kernel split of StageTimes): events without timestamps and only the
+      // records the stream order needs measured no different (profiles/r6/ab_pool/spin_mutex_rejected/
+      // bench_new_noevt_*). Batch completion is polled by the slot thread (wait_batch): no
+      // blocking-sync event.
+      check_hip(hipEventCreateWithFlags(&s.ev0, hipEventDefault), "hipEventCreate");
+      check_hip(hipEventCreateWithFlags(&s.ev1, hipEventDefault), "hipEventCreate");
+      check_hip(hipEventCreateWithFlags(&s.ev2, hipEventDefault), "hipEventCreate");
       mark("events");
       if (arena_slot >= 0 && pin_arena_) {
         s.arena = true;
@@ -725,7 +717,7 @@ struct Engine::Impl {
       }
       if (chunk && (end - s.uploaded) * 2 >= chunk) {
         if (!s.upload_started) {
-          if (event_timing()) check_hip(hipEventRecord(s.ev0, s.up), "event");
+          check_hip(hipEventRecord(s.ev0, s.up), "event");
           s.upload_started = true;
         }
         check_hip(hipMemcpyAsync(s.d_blob + s.raw_base + s.uploaded * 2, s.h_blob + s.raw_base + s.uploaded * 2,
@@ -1080,7 +1072,7 @@ struct Engine::Impl {
     // SDMA measured no gain (profiles/r3/shader_upload/) and was removed in round 4.
     const bool inline_up = s.uploaded == 0 && !s.upload_started && nl <= 16;
     hipStream_t up = inline_up ? s.stream : s.up;
-    if (!s.upload_started && !inline_up && event_timing()) check_hip(hipEventRecord(s.ev0, up), "event");
+    if (!s.upload_started && !inline_up) check_hip(hipEventRecord(s.ev0, up), "event");
     if (s.uploaded == 0) {
       check_hip(hipMemcpyAsync(s.d_blob, s.h_blob, s.raw_base + raw_end * 2, hipMemcpyHostToDevice, up),
                 "H2D tables + pixels");
@@ -1093,7 +1085,7 @@ struct Engine::Impl {
     }
     s.uploaded = raw_end;
     // ev1: the kernels' wait on a separate upload stream, and the h2d/kernel time split.
-    if (!inline_up && (event_timing() || up != s.stream)) check_hip(hipEventRecord(s.ev1, up), "event");
+    if (!inline_up) check_hip(hipEventRecord(s.ev1, up), "event");
     if (up != s.stream) check_hip(hipStreamWaitEvent(s.stream, s.ev1, 0), "wait upload");
     // The median reads the upload directly (12-bit pairs decoded in its tile load) and writes the
     // expanded samples for the render/JPEG stages. One eager launch per kernel: hipGraph replay of
@@ -1127,7 +1119,7 @@ struct Engine::Impl {
     check_hip(hipEventRecord(s.ev2, s.stream), "event");
     if (mark) mark->enq = now_s();
     wait_batch(s, s.ev2, t_enq, nl);
-    if (acc && !inline_up && event_timing()) {  // an inline small upload records no split events
+    if (acc && !inline_up) {  // an inline small upload records no split events
       float a = 0, b = 0;
       (void)hipEventElapsedTime(&a, s.ev0, s.ev1);
       (void)hipEventElapsedTime(&b, s.ev1, s.ev2);
