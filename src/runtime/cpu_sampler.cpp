@@ -1,7 +1,7 @@
 // In-process CPU sampling profiler (nm03/cpu_sampler.h).
 //
 // Output (text, one record per line):
-//   # nm03 cpu samples v1
+//   # nm03 cpu samples v2
 //   period_us <p>
 //   samples <written> dropped <n>
 //   map <start> <end> <file offset> <path>          executable mappings (hex), from /proc/self/maps
@@ -54,8 +54,10 @@ bool g_have_timer = false;
 
 void on_sigprof(int, siginfo_t*, void* ctx) {
   const int saved = errno;
-  g_inside.fetch_add(1, std::memory_order_acquire);
-  if (g_on.load(std::memory_order_acquire)) {
+  // seq_cst with sampler_stop's store of g_on and load of g_inside (a Dekker pair): either stop
+  // sees this handler inside, or this handler sees the sampler off and records nothing.
+  g_inside.fetch_add(1, std::memory_order_seq_cst);
+  if (g_on.load(std::memory_order_seq_cst)) {
     const size_t i = g_next.fetch_add(1, std::memory_order_relaxed);
     if (i < g_cap) {
       uint64_t* r = g_buf.get() + i * g_stride;
@@ -165,13 +167,13 @@ size_t sampler_stop(const std::string& path) {
   for (timer_t t : g_timers) timer_delete(t);
   g_timers.clear();
   g_have_timer = false;
-  g_on.store(false, std::memory_order_release);
+  g_on.store(false, std::memory_order_seq_cst);
   // A SIGPROF already pending is discarded once ignored; handlers already running finish first.
   struct sigaction ign {};
   ign.sa_handler = SIG_IGN;
   sigemptyset(&ign.sa_mask);
   sigaction(SIGPROF, &ign, nullptr);
-  while (g_inside.load(std::memory_order_acquire) != 0) std::this_thread::sleep_for(std::chrono::microseconds(50));
+  while (g_inside.load(std::memory_order_seq_cst) != 0) std::this_thread::sleep_for(std::chrono::microseconds(50));
   const size_t n = std::min(g_next.load(), g_cap);
   // Distinct (thread, chain) with counts.
   std::map<std::vector<uint64_t>, uint64_t> stacks;
