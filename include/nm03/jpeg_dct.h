@@ -26,7 +26,9 @@ struct Info {
 // Decodes one sequential Huffman-coded DCT JPEG with a single component into rows × cols samples
 // (0 .. 2^P − 1). Throws SliceError on malformed input, on other processes (progressive,
 // lossless — see jpeg_lossless.h — hierarchical, arithmetic coding) and on several components.
-Info decode(const uint8_t* data, size_t len, std::vector<uint16_t>& out);
+// `expect_rows` / `expect_cols` > 0: the frame must have that size, checked at the SOF before any
+// allocation (a DICOM caller knows it: a corrupt SOF cannot make it allocate gigabytes).
+Info decode(const uint8_t* data, size_t len, std::vector<uint16_t>& out, int expect_rows = 0, int expect_cols = 0);
 
 // Encodes rows × cols samples of `precision` bits (8: baseline SOF0, 12: extended SOF1) at IJG
 // `quality` (the Annex K luminance table scaled like jcparam.c), floating-point forward DCT, optimal

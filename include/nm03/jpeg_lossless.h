@@ -28,7 +28,9 @@ struct Info {
 // the point transform). Throws SliceError on malformed input, other JPEG processes (baseline,
 // progressive, arithmetic coding, hierarchical), several components, restart intervals that do not
 // span whole rows, or a stream shorter than its image.
-Info decode(const uint8_t* data, size_t len, std::vector<uint16_t>& out);
+// `expect_rows` / `expect_cols` > 0: the frame must have that size (checked at the SOF, before any
+// allocation).
+Info decode(const uint8_t* data, size_t len, std::vector<uint16_t>& out, int expect_rows = 0, int expect_cols = 0);
 
 // Encodes rows × cols samples (only the low `precision` bits are used) with selection value
 // `predictor` (1..7), point transform `pt` and a restart marker every `restart_rows` rows (0: none);

@@ -268,10 +268,10 @@ void decode_jpeg_lossless_frames(Header& h, const uint8_t* d, const std::vector<
     }
     int rows = 0, cols = 0, precision = 0;
     if (h.syntax == Syntax::kJpegLossless) {
-      const jpegll::Info info = jpegll::decode(src, len, px);
+      const jpegll::Info info = jpegll::decode(src, len, px, h.rows, h.cols);
       rows = info.rows, cols = info.cols, precision = info.precision;
     } else {
-      const jpegdct::Info info = jpegdct::decode(src, len, px);
+      const jpegdct::Info info = jpegdct::decode(src, len, px, h.rows, h.cols);
       if (h.syntax == Syntax::kJpegBaseline && info.precision != 8)
         throw SliceError("JPEG Baseline transfer syntax with " + std::to_string(info.precision) + "-bit samples");
       rows = info.rows, cols = info.cols, precision = info.precision;

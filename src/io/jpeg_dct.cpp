@@ -154,7 +154,7 @@ inline int32_t extend(uint32_t v, int s) {
 
 }  // namespace
 
-Info decode(const uint8_t* d, size_t n, std::vector<uint16_t>& out) {
+Info decode(const uint8_t* d, size_t n, std::vector<uint16_t>& out, int expect_rows, int expect_cols) {
   if (n < 4 || d[0] != 0xFF || d[1] != 0xD8) throw SliceError("JPEG: missing SOI marker");
   size_t pos = 2;
   Info info;
@@ -187,6 +187,9 @@ Info decode(const uint8_t* d, size_t n, std::vector<uint16_t>& out) {
       if (m == 0xC0 && info.precision != 8) throw SliceError("JPEG: baseline with 12-bit samples");
       if (info.rows == 0 || info.cols == 0) throw SliceError("JPEG: zero image size (DNL not supported)");
       if (nf != 1) throw SliceError("JPEG with " + std::to_string(nf) + " components (monochrome supported)");
+      if ((expect_rows > 0 && info.rows != expect_rows) || (expect_cols > 0 && info.cols != expect_cols))
+        throw SliceError("JPEG frame is " + std::to_string(info.cols) + "x" + std::to_string(info.rows) + ", expected " +
+                         std::to_string(expect_cols) + "x" + std::to_string(expect_rows));
       if (sl < 9) throw SliceError("JPEG: short SOF");
       comp_id = s[6];
       tq = s[8];
@@ -257,7 +260,7 @@ Info decode(const uint8_t* d, size_t n, std::vector<uint16_t>& out) {
         std::memset(coef, 0, sizeof(coef));
         const int cs = decode_symbol(dc[td], br);
         if (cs > max_cat) throw SliceError("Corrupt JPEG: DC category out of range");
-        pred += extend(br.get(cs), cs);
+        pred = (int32_t)((uint32_t)pred + (uint32_t)extend(br.get(cs), cs));  // wraps on corrupt data (no UB)
         coef[0] = pred;
         for (int k = 1; k < 64; ++k) {
           const int rs = decode_symbol(ac[ta], br);

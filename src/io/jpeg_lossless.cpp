@@ -36,7 +36,7 @@ inline int32_t predict(int sv, bool first_line, int x, const uint16_t* cur, cons
 
 }  // namespace
 
-Info decode(const uint8_t* d, size_t n, std::vector<uint16_t>& out) {
+Info decode(const uint8_t* d, size_t n, std::vector<uint16_t>& out, int expect_rows, int expect_cols) {
   if (n < 4 || d[0] != 0xFF || d[1] != 0xD8) throw SliceError("Lossless JPEG: missing SOI marker");
   size_t pos = 2;
   Info info;
@@ -66,6 +66,9 @@ Info decode(const uint8_t* d, size_t n, std::vector<uint16_t>& out) {
       if (info.rows == 0) throw SliceError("Lossless JPEG: height given by DNL is not supported");
       if (info.cols == 0) throw SliceError("Lossless JPEG: zero width");
       if (nf != 1) throw SliceError("Lossless JPEG with " + std::to_string(nf) + " components (one is supported)");
+      if ((expect_rows > 0 && info.rows != expect_rows) || (expect_cols > 0 && info.cols != expect_cols))
+        throw SliceError("JPEG frame is " + std::to_string(info.cols) + "x" + std::to_string(info.rows) + ", expected " +
+                         std::to_string(expect_cols) + "x" + std::to_string(expect_rows));
       if (sl < 9) throw SliceError("Lossless JPEG: short SOF3");
       comp_id = s[6];
       if (s[7] != 0x11) throw SliceError("Lossless JPEG: subsampled component");

@@ -97,3 +97,16 @@ def test_dicom_lossy_jpeg_multiframe(native):
     for k in range(3):
         want = native.jpeg_dct_decode(native.jpeg_dct_encode(st[k], 12, 90, 2 * 6))["pixels"]
         assert np.array_equal(native.dicom_pixels(b, k), want)
+
+
+@pytest.mark.parametrize("syntax,sof", [("jpeg-extended", b"\xff\xc1"), ("jpeg-lossless", b"\xff\xc3")])
+def test_dicom_jpeg_frame_size_checked_before_decoding(native, syntax, sof):
+    """A SOF that disagrees with the dataset's Rows/Columns is rejected at the SOF, before the decoder
+    sizes its output from it (a corrupt 65535x65535 SOF must not allocate 8 GiB)."""
+    px = _smooth(np.random.default_rng(8), (40, 48), 4096)
+    b = bytearray(native.dicom_bytes(px, bits_stored=12, syntax=syntax))
+    i = b.find(sof)
+    assert i > 0
+    b[i + 5:i + 7] = b"\xff\xff"  # SOF rows
+    with pytest.raises(Exception, match="expected 48x40"):
+        native.dicom_pixels(bytes(b))
