@@ -90,7 +90,7 @@ def parse_args(argv=None):
     ap.add_argument("--no-secondary", action="store_true", help="skip the other scaling mode's measurement")
     # 150 wipe passes ≈ 0.3-0.7 s timed (20 passes were 43 ms: one 10 ms hiccup or the reaper's final
     # drain moved the figure by 25-40%).
-    ap.add_argument("--wipe-passes", type=int, default=150,
+    ap.add_argument("--wipe-passes", type=int, default=200,
                     help="also time this many passes that each first wipe their output directories (the "
                          "reference's per-run rm -rf; reported as config.wipe_each_pass; 0 = skip)")
     # 96 slices × 4 slots: 5 batches per 465-slice pass instead of 8 at 64 × 6; won 10 of 11
