@@ -122,7 +122,7 @@ def parse_args(argv=None):
     ap.add_argument("--keep-data", action="store_true", help="keep a generated dataset in tmpfs after the run")
     ap.add_argument("--keep-output", action="store_true")
     ap.add_argument("--pipeline-depth", type=int, default=0,
-                    help="passes in flight (each with its own output tree); 0 = auto: 2, or 4 when the rank's "
+                    help="passes in flight (each with its own output tree); 0 = auto: 2, or 6 when the rank's "
                          "shard is smaller than one batch per slot (strong scaling: a pass is then mostly "
                          "latency, and more passes in flight overlap it)")
     ap.add_argument("--no-pipeline", action="store_true",
@@ -320,7 +320,12 @@ def run_rank(args):
     def pipeline_depth(shard_len):
         if args.pipeline_depth > 0:
             return args.pipeline_depth
-        return 4 if shard_len < args.streams * args.batch_size else 2
+        # Small shards (strong scaling at N > 1): 6 passes in flight, so the slots still find queued
+        # batches while this thread wakes up to submit the next pass. At the driver's 20 steps the
+        # 58-slice shard of an 8-rank job measured the same median with 4 and 6 but no slow outliers
+        # with 6 (worst of 9 runs 304k vs 204k slices/s, profiles/r6/shard_depth/) — and the job's
+        # time is its slowest rank's.
+        return 6 if shard_len < args.streams * args.batch_size else 2
 
     def shard(scaling, out_root):
         """This rank's work list: weak = its own cohort replica, strong = its block of one cohort."""
