@@ -106,3 +106,14 @@ def test_bench_under_torchrun(tmp_path):
     assert rec["n_gpus"] == 2 and all(len(v) == 2 for v in rec["config"]["per_rank"].values())
     assert rec["config"]["comm"]["backend"] == "host"  # auto: no RCCL without a GPU, recorded
     assert "rccl_error" in rec["config"]["comm"]
+
+
+def test_bench_emulate_shard_of(tmp_path):
+    """--emulate-shard-of N: one rank processes rank 0's share of an N-rank strong-scaling step (465 // N
+    slices per pass), with the small-shard pipeline depth, and the record says it is an emulation."""
+    r = _bench(tmp_path, "--emulate-shard-of", "8", "--no-secondary", "--wipe-passes", "0")
+    assert r.returncode == 0, r.stderr
+    rec = _json_line(r.stdout)
+    assert rec["metric"].startswith("EMULATION") and rec["vs_baseline"] is None
+    assert rec["config"]["emulate_shard_of"] == 8 and rec["config"]["pipeline_depth"] == 6
+    assert rec["config"]["per_rank"]["slices"] == [2.0 * (465 // 8)]
