@@ -1336,13 +1336,24 @@ struct Engine::Impl {
     acc.batches += 1;
   }
 
-  // Batch schedule: full batches plus a remainder. Measured and removed in round 4: a tapered
-  // schedule (small first/last batches: 209k vs 220k slices/s, 234.7k vs 232.2k re-measured) and a
-  // spread schedule (equal-size batches, short lists split over the slots: slower on the headline,
-  // config 2 and strong-scaling shards, profiles/r2/spread/).
+  // Batch schedule: the fewest batches of at most B slices (⌈n / B⌉), of equal size (±1), larger
+  // ones first. Round 6: a strong-scaling shard of 116 slices ran as 96 + 20 — the short batch paid
+  // a whole batch's fixed costs for a fifth of the work — and measured 315k vs 350k slices/s per GPU
+  // at the driver's 20 steps as 58 + 58 (233 slices: 96 + 96 + 41 → 78 + 78 + 77, 362k vs 373k;
+  // profiles/r6/even_batches/). Measured and removed in round 4: a tapered schedule (small first /
+  // last batches: 209k vs 220k slices/s) and a spread schedule that split short lists over all the
+  // slots (more, smaller batches: slower on the headline, config 2 and strong-scaling shards,
+  // profiles/r2/spread/).
   static std::vector<std::pair<size_t, size_t>> plan_batches(size_t n, size_t B) {
     std::vector<std::pair<size_t, size_t>> out;
-    for (size_t first = 0; first < n; first += B) out.push_back({first, std::min(B, n - first)});
+    if (n == 0 || B == 0) return out;
+    const size_t k = (n + B - 1) / B, q = n / k, rem = n % k;
+    size_t first = 0;
+    for (size_t b = 0; b < k; ++b) {
+      const size_t len = q + (b < rem ? 1 : 0);
+      out.push_back({first, len});
+      first += len;
+    }
     return out;
   }
 

@@ -14,11 +14,14 @@ IFS=';' read -r -a VARS <<< "${VARIANTS:--}"
 for r in $(seq ${ROUNDS:-3}); do
   for i in "${!VARS[@]}"; do
     v=${VARS[$i]}
-    a=""; [ "$v" != "-" ] && a="$v"
+    a=(); e=()
+    if [ "$v" != "-" ]; then  # leading NAME=VAL words go to the environment (e.g. LD_LIBRARY_PATH=<older lib dir>)
+      for w in $v; do if [[ ${#a[@]} -eq 0 && "$w" == *=* && "$w" != --* ]]; then e+=("$w"); else a+=("$w"); fi; done
+    fi
     for n in ${SHARDS:-1 2 4 8}; do
       for st in ${STEPS:-20 200}; do
-        timeout -k 10 240 python -u bench.py --keep-data --data-root $D --steps $st --warmup 5 --no-secondary \
-          --wipe-passes 0 --single-passes 0 --cli-runs 0 --emulate-shard-of $n $a \
+        timeout -k 10 240 env "${e[@]}" python -u bench.py --keep-data --data-root $D --steps $st --warmup 5 --no-secondary \
+          --wipe-passes 0 --single-passes 0 --cli-runs 0 --emulate-shard-of $n "${a[@]}" \
           > "$O/shard${n}_steps${st}_v${i}_$r.json" 2>> $O/bench.err || exit 1
       done
     done
