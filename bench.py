@@ -122,9 +122,9 @@ def parse_args(argv=None):
     ap.add_argument("--keep-data", action="store_true", help="keep a generated dataset in tmpfs after the run")
     ap.add_argument("--keep-output", action="store_true")
     ap.add_argument("--pipeline-depth", type=int, default=0,
-                    help="passes in flight (each with its own output tree); 0 = auto: 2, or 6 when the rank's "
-                         "shard is smaller than one batch per slot (strong scaling: a pass is then mostly "
-                         "latency, and more passes in flight overlap it)")
+                    help="passes in flight (each with its own output tree); 0 = auto: 6 when the rank's pass is "
+                         "one or two batches (strong-scaling shards: a pass is then mostly latency, and more "
+                         "passes in flight overlap it), else 2")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="one blocking engine call per pass; by default pass k+1 is submitted before pass k "
                          "finished (Engine.submit/wait) so the slot ring never drains between passes")
@@ -327,12 +327,16 @@ def run_rank(args):
     def pipeline_depth(shard_len):
         if args.pipeline_depth > 0:
             return args.pipeline_depth
-        # Small shards (strong scaling at N > 1): 6 passes in flight, so the slots still find queued
-        # batches while this thread wakes up to submit the next pass. At the driver's 20 steps the
-        # 58-slice shard of an 8-rank job measured the same median with 4 and 6 but no slow outliers
-        # with 6 (worst of 9 runs 304k vs 204k slices/s, profiles/r6/shard_depth/) — and the job's
-        # time is its slowest rank's.
-        return 6 if shard_len < args.streams * args.batch_size else 2
+        # Passes in flight by batches per pass. One or two (the strong-scaling shards of 4- and 8-rank
+        # jobs): 6, so the slots still find queued batches while this thread wakes up to submit the
+        # next pass — at the driver's 20 steps the 58-slice shard measured the same median with 4 and
+        # 6 but no slow outliers with 6 (worst of 9 runs 304k vs 204k slices/s, profiles/r6/
+        # shard_depth/), and a job's time is its slowest rank's. Three or more (the whole cohort, the
+        # 2-rank shard): 2 — depths 2, 3 and 4 were within the box noise for the cohort over three
+        # interleaved experiments at 20 steps and equal at 3000 (412k vs 409k), while 6 trailed 2 and 3
+        # for the 2-rank shard in all three (profiles/r6/depth_full/).
+        batches = -(-shard_len // max(1, args.batch_size))
+        return 6 if batches <= 2 else 2
 
     def shard(scaling, out_root):
         """This rank's work list: weak = its own cohort replica, strong = its block of one cohort."""
