@@ -100,7 +100,10 @@ def parse_args(argv=None):
                     help="wipe passes: rename each output directory aside and delete it on 2 background "
                          "reaper threads (cohort.h OutputReaper; the final drain is inside the clock), or "
                          "unlink everything before the pass on 8 threads (round 3)")
-    ap.add_argument("--reaper-threads", type=int, default=4,
+    # 6 deletion threads: the wipe figure over 200 passes rose in three interleaved experiments on three
+    # boxes against 4 (179k -> 190k, 203k -> 239k with 2 creators, 196k -> 202k; 8 threads 220k in the
+    # third), profiles/r6/wipe_knobs/.
+    ap.add_argument("--reaper-threads", type=int, default=6,
                     help="background deletion threads of the wipe passes (--wipe-mode reaper)")
     ap.add_argument("--wipe-depth", type=int, default=3,
                     help="passes in flight (output trees) for the wipe passes")
