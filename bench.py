@@ -88,14 +88,11 @@ def parse_args(argv=None):
                     help="which figure is the headline value (default strong: BASELINE config 3, one cohort "
                          "sharded over the ranks); the other is reported next to it")
     ap.add_argument("--no-secondary", action="store_true", help="skip the other scaling mode's measurement")
-    # 150 wipe passes ≈ 0.3-0.7 s timed (20 passes were 43 ms: one 10 ms hiccup or the reaper's final
+    # 200 wipe passes ≈ 0.3-0.7 s timed (20 passes were 43 ms: one 10 ms hiccup or the reaper's final
     # drain moved the figure by 25-40%).
     ap.add_argument("--wipe-passes", type=int, default=200,
                     help="also time this many passes that each first wipe their output directories (the "
                          "reference's per-run rm -rf; reported as config.wipe_each_pass; 0 = skip)")
-    # 96 slices × 4 slots: 5 batches per 465-slice pass instead of 8 at 64 × 6; won 10 of 11
-    # interleaved pairs on two boxes (median 324k vs 297k and 354k vs 324k slices/s) with less host
-    # CPU per step (profiles/r2/batch_streams/).
     ap.add_argument("--wipe-mode", choices=("reaper", "inline"), default="reaper",
                     help="wipe passes: rename each output directory aside and delete it on 2 background "
                          "reaper threads (cohort.h OutputReaper; the final drain is inside the clock), or "
@@ -110,7 +107,11 @@ def parse_args(argv=None):
     ap.add_argument("--create-writers", type=int, default=-1,
                     help="EngineConfig.create_writers: pool workers writing a batch's JPEGs at once while "
                          "its directories are being filled (-1 = engine default, 0 = no limit)")
-    ap.add_argument("--batch-size", type=int, default=96)
+    # 4 slots (round 2: 96 slices × 4 won over 64 × 6, profiles/r2/batch_streams/; round 6: 4 slots over
+    # 5 and 6, profiles/r6/streams/). Batch size: see `batch` below.
+    ap.add_argument("--batch-size", type=int, default=0,
+                    help="slices per batch (engine capacity); 0 = auto: the rank's shard if at most 117 slices, "
+                         "else 117 (equal-size batches)")
     ap.add_argument("--streams", type=int, default=4)
     ap.add_argument("--threads", type=int, default=0,
                     help="host I/O threads per rank (0 = the rank's CPU partition and budget share, ≤16)")
@@ -318,15 +319,6 @@ def run_rank(args):
     if fail_rank != "" and int(fail_rank) == rank:
         print(f"bench: rank {rank}: injected failure", file=sys.stderr, flush=True)
         os._exit(5)
-    cfg = nm.PipelineConfig(batch_size=args.batch_size, streams=args.streams, threads=args.threads,
-                            device=device)
-    ecfg = cfg.engine_config()
-    ecfg.cpus = part["cpus"]
-    ecfg.host_only = args.host_only
-    if args.create_writers >= 0:
-        ecfg.create_writers = args.create_writers
-    engine = _DryEngine() if args.dry_run else n.Engine(ecfg)
-
     def pipeline_depth(shard_len):
         if args.pipeline_depth > 0:
             return args.pipeline_depth
@@ -338,7 +330,7 @@ def run_rank(args):
         # 2-rank shard): 2 — depths 2, 3 and 4 were within the box noise for the cohort over three
         # interleaved experiments at 20 steps and equal at 3000 (412k vs 409k), while 6 trailed 2 and 3
         # for the 2-rank shard in all three (profiles/r6/depth_full/).
-        batches = -(-shard_len // max(1, args.batch_size))
+        batches = -(-shard_len // max(1, batch))
         return 6 if batches <= 2 else 2
 
     def shard(scaling, out_root):
@@ -351,6 +343,26 @@ def run_rank(args):
         if world == 1 and args.emulate_shard_of > 1 and scaling == "strong":
             hi = len(items) // args.emulate_shard_of  # rank 0's share of an N-rank job
         return localize_items(items[lo:hi], roots[0], local_root), len(items)
+
+    # Slices per batch (the engine's capacity) from the rank's primary shard, unless --batch-size
+    # says: the whole shard when it is at most 117 slices (the 58- and 116-slice shards of 8- and
+    # 4-rank jobs run as one batch sized to fit), else batches of at most 117 (the 465-slice cohort as
+    # 4 × 116-117, the 233-slice shard of a 2-rank job as 117 + 116). Fixed 96-slice batches left a
+    # 116-slice shard as 58 + 58 and the cohort as 5 × 93; at the driver's 20 steps the fitted sizes
+    # measured 392k vs 346k (4 ranks) and 333k vs 329k (8 ranks) slices/s per GPU, and the cohort
+    # 428k vs 406k over 3000 steps (profiles/r6/batch_size/). Much larger batches (233, 465) gained
+    # more over long runs but spread widely over 20 steps, where a pass's fill and drain weigh more.
+    if args.batch_size > 0:
+        batch = args.batch_size
+    else:
+        batch = max(1, min(len(shard(args.scaling, args.out_root)[0]), 117))
+    cfg = nm.PipelineConfig(batch_size=batch, streams=args.streams, threads=args.threads, device=device)
+    ecfg = cfg.engine_config()
+    ecfg.cpus = part["cpus"]
+    ecfg.host_only = args.host_only
+    if args.create_writers >= 0:
+        ecfg.create_writers = args.create_writers
+    engine = _DryEngine() if args.dry_run else n.Engine(ecfg)
 
     def measure(scaling, out_root, steps, warmup, wipe=False, profile=""):
         mine, global_items = shard(scaling, out_root)
@@ -580,7 +592,7 @@ def run_rank(args):
                 "global_batch": primary["global_batch"],
                 "seq_len": 256,
                 "parallelism": f"dp{world}",
-                "batch_size": args.batch_size,
+                "batch_size": batch,
                 "streams": args.streams,
                 "threads": args.threads,
                 "create_writers": ecfg.create_writers,

@@ -45,9 +45,10 @@ def test_bench_self_launch_n_ranks(tmp_path, n):
     assert sum(pr["slices"]) == cohort * 2
     # weak: every rank processes one full cohort per step
     assert rec["config"]["weak"]["per_rank"]["slices"] == [float(cohort * 2)] * n
-    # passes in flight: 6 when a pass is one or two 96-slice batches (the 3-rank shard of 155), else 2
-    # (the 2-rank shard of 233, a full cohort per rank)
-    assert rec["config"]["pipeline_depth"] == (2 if n == 2 else 6) and rec["config"]["weak"]["pipeline_depth"] == 2
+    # auto batch size: at most 117 slices (233 → 117 + 116, 155 → 78 + 77); passes in flight: 6 when a
+    # pass is one or two batches, else 2 (a full cohort per rank: 4 batches)
+    assert rec["config"]["batch_size"] == 117
+    assert rec["config"]["pipeline_depth"] == 6 and rec["config"]["weak"]["pipeline_depth"] == 2
 
 
 def test_bench_auto_comm_records_rccl_failure(tmp_path):
@@ -116,4 +117,5 @@ def test_bench_emulate_shard_of(tmp_path):
     rec = _json_line(r.stdout)
     assert rec["metric"].startswith("EMULATION") and rec["vs_baseline"] is None
     assert rec["config"]["emulate_shard_of"] == 8 and rec["config"]["pipeline_depth"] == 6
+    assert rec["config"]["batch_size"] == 465 // 8  # the whole 58-slice shard as one batch
     assert rec["config"]["per_rank"]["slices"] == [2.0 * (465 // 8)]
