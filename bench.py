@@ -104,6 +104,9 @@ def parse_args(argv=None):
                     help="background deletion threads of the wipe passes (--wipe-mode reaper)")
     ap.add_argument("--wipe-depth", type=int, default=3,
                     help="passes in flight (output trees) for the wipe passes")
+    ap.add_argument("--upload-chunk-kb", type=int, default=-1,
+                    help="EngineConfig.upload_chunk_kb: smallest progressive upload copy (-1 = engine default, 2 MiB; "
+                         "a copy is also at least a quarter of the batch)")
     ap.add_argument("--create-writers", type=int, default=-1,
                     help="EngineConfig.create_writers: pool workers writing a batch's JPEGs at once while "
                          "its directories are being filled (-1 = engine default, 0 = no limit)")
@@ -362,6 +365,8 @@ def run_rank(args):
     ecfg.host_only = args.host_only
     if args.create_writers >= 0:
         ecfg.create_writers = args.create_writers
+    if args.upload_chunk_kb >= 0:
+        ecfg.upload_chunk_kb = args.upload_chunk_kb
     engine = _DryEngine() if args.dry_run else n.Engine(ecfg)
 
     def measure(scaling, out_root, steps, warmup, wipe=False, profile=""):
