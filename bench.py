@@ -104,7 +104,11 @@ def parse_args(argv=None):
                     help="background deletion threads of the wipe passes (--wipe-mode reaper)")
     ap.add_argument("--wipe-depth", type=int, default=3,
                     help="passes in flight (output trees) for the wipe passes")
-    ap.add_argument("--upload-chunk-kb", type=int, default=-1,
+    # 4 MiB progressive upload copies (the engine's default is 2 MiB, and a copy is at least a quarter of
+    # the batch): fewer, larger SDMA copies per 117-slice batch. Headline 440.7k vs 431.2k over 3000 steps;
+    # at the driver's 20 steps 434k vs 423k (1 GPU), 403k vs 388k (4-rank shard), 340k vs 333k (8-rank
+    # shard), equal for 2 ranks (profiles/r6/upload_chunk/).
+    ap.add_argument("--upload-chunk-kb", type=int, default=4096,
                     help="EngineConfig.upload_chunk_kb: smallest progressive upload copy (-1 = engine default, 2 MiB; "
                          "a copy is also at least a quarter of the batch)")
     ap.add_argument("--create-writers", type=int, default=-1,
