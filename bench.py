@@ -104,13 +104,15 @@ def parse_args(argv=None):
                     help="background deletion threads of the wipe passes (--wipe-mode reaper)")
     ap.add_argument("--wipe-depth", type=int, default=3,
                     help="passes in flight (output trees) for the wipe passes")
-    # 4 MiB progressive upload copies (the engine's default is 2 MiB, and a copy is at least a quarter of
-    # the batch): fewer, larger SDMA copies per 117-slice batch. Headline 440.7k vs 431.2k over 3000 steps;
-    # at the driver's 20 steps 434k vs 423k (1 GPU), 403k vs 388k (4-rank shard), 340k vs 333k (8-rank
-    # shard), equal for 2 ranks (profiles/r6/upload_chunk/).
-    ap.add_argument("--upload-chunk-kb", type=int, default=4096,
+    # One upload copy per batch, after its loads (progressive upload off): with batches fitted to the
+    # shard the engine's progressive copies (2 MiB, or a quarter of the batch) cost more in slot-thread
+    # wake-ups and copy set-up than their overlap with the loads saves. Minimum copy size 2 MiB → 4 →
+    # 6 → 64 MiB → off: headline 431k → 441k → 453k → 479k ≈ 460k (off), and at the driver's 20 steps
+    # the 8-rank shard 333k → 340k → 370k → 367k ≈ 357k, the 4-rank one 388k → 403k → 405k → 421k ≈
+    # 404k (interleaved, several boxes: profiles/r6/upload_chunk/).
+    ap.add_argument("--upload-chunk-kb", type=int, default=0,
                     help="EngineConfig.upload_chunk_kb: smallest progressive upload copy (-1 = engine default, 2 MiB; "
-                         "a copy is also at least a quarter of the batch)")
+                         "a copy is also at least a quarter of the batch); 0 = one copy per batch after its loads")
     ap.add_argument("--create-writers", type=int, default=-1,
                     help="EngineConfig.create_writers: pool workers writing a batch's JPEGs at once while "
                          "its directories are being filled (-1 = engine default, 0 = no limit)")
